@@ -1,0 +1,19 @@
+"""MI355X-native GCN hot path (gfx950 HIP kernels behind a C-ABI).
+
+Drop-in for the reference's ``layer.py`` (GraphConvolution, GCN) — see
+DESIGN.md for the path, the boundary and the kernels.
+"""
+from . import _lib
+from .layer import GCN, GraphConvolution
+from .ops import GCNFn, GraphConvFn, Operand, colsum, gemm, spmm
+from .sparse import CSR, as_csr, from_arrays, from_torch
+
+__all__ = [
+    "GCN", "GraphConvolution", "GCNFn", "GraphConvFn", "Operand", "CSR",
+    "as_csr", "from_arrays", "from_torch", "spmm", "gemm", "colsum",
+]
+
+
+def native_library_path():
+    """Path of the in-tree libgcnk.so this package runs on."""
+    return _lib.LIB_PATH

@@ -1,0 +1,98 @@
+"""ctypes binding of libgcnk.so (the C-ABI declared in include/gcnk.h).
+
+The shared library is built in-tree by ``__graft_entry__.build()`` (or
+``make -C <package>/csrc``).  There is no fallback: if the library is missing
+or fails to load, every op raises ``RuntimeError`` — the hot path never
+silently runs anywhere but the HIP kernels.
+"""
+import ctypes
+import os
+import threading
+
+_HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.path.join(_HERE, "libgcnk.so")
+ABI_VERSION = 1
+
+# C-ABI return codes (gcnk.h)
+OK, EARG, EUNSUP, EHIP = 0, -1, -2, -3
+
+# SpMM epilogues (gcnk.h GCNK_EPI_*)
+EPI_NONE, EPI_BIAS, EPI_BIAS_RELU, EPI_BIAS_RELU_DROP, EPI_BIAS_RELU_HASH = 0, 1, 2, 3, 4
+# GEMM epilogues (gcnk.h GCNK_GEMM_EPI_*)
+GEMM_EPI_NONE, GEMM_EPI_BIAS, GEMM_EPI_BIAS_RELU, GEMM_EPI_MASK_POS = 0, 1, 2, 5
+
+_vp, _i32, _i64, _u64, _f32 = ctypes.c_void_p, ctypes.c_int32, ctypes.c_int64, ctypes.c_uint64, ctypes.c_float
+
+# name -> (restype, argtypes); every symbol include/gcnk.h declares
+SIGNATURES = {
+    "gcnk_abi_version": (ctypes.c_int, []),
+    "gcnk_last_error": (ctypes.c_char_p, []),
+    "gcnk_spmm_default_ipc": (_i32, [_i32, _i64, _i32]),
+    "gcnk_spmm_plan_chunks": (_i64, [_i32, _i64, _i32]),
+    "gcnk_spmm_plan_bytes": (_i64, [_i32, _i64, _i32]),
+    "gcnk_spmm_plan_build": (ctypes.c_int, [_vp, _i32, _i64, _i32, _vp, _i64, _vp]),
+    "gcnk_spmm_plan_query": (ctypes.c_int, [_vp, _vp, _vp]),
+    "gcnk_spmm_workspace_bytes": (_i64, [_i32, _i32]),
+    "gcnk_spmm_csr_f32": (ctypes.c_int, [
+        _vp, _vp, _vp,            # rowptr, colind, val
+        _i32, _i32, _i64,         # M, K, nnz
+        _vp, _i32, _i32,          # plan, ipc, nfix
+        _vp, _i64, _i32,          # B, ldb, F
+        _vp, _i64,                # C, ldc
+        _vp, _i32,                # bias, epilogue
+        _vp, _i64, _f32,          # drop_mask, ldm, drop_scale
+        _f32, _u64, _u64,         # keep_prob, seed, offset
+        _vp, _i64,                # workspace, workspace_bytes
+        _i32, _vp,                # lanes_hint, stream
+    ]),
+    "gcnk_gemm_workspace_bytes": (_i64, [_i32, _i32, _i32, _i32]),
+    "gcnk_gemm_f32": (ctypes.c_int, [
+        _i32, _i32, _i32, _i32, _i32,   # transA, transB, M, N, K
+        _vp, _i64, _vp, _i64,           # A, lda, B, ldb
+        _vp, _i64,                      # C, ldc
+        _vp, _i32, _vp, _i64, _f32,     # bias, epilogue, R, ldr, scale
+        _i32, _vp, _i64, _vp,           # split_k, workspace, workspace_bytes, stream
+    ]),
+    "gcnk_colsum_workspace_bytes": (_i64, [_i32, _i32]),
+    "gcnk_colsum_f32": (ctypes.c_int, [_vp, _i64, _i32, _i32, _vp, _vp, _i64, _vp]),
+    "gcnk_csr_transpose_workspace_bytes": (_i64, [_i32, _i32, _i64]),
+    "gcnk_csr_transpose": (ctypes.c_int, [_vp, _vp, _vp, _i32, _i32, _i64, _vp, _vp, _vp, _vp, _i64, _vp]),
+}
+
+_lock = threading.Lock()
+_lib = None
+
+
+class GcnkError(RuntimeError):
+    """Raised when a libgcnk entry point returns a non-zero code."""
+
+
+def load():
+    """Load libgcnk.so once and bind every declared symbol; raise if absent."""
+    global _lib
+    if _lib is not None:
+        return _lib
+    with _lock:
+        if _lib is not None:
+            return _lib
+        if not os.path.exists(LIB_PATH):
+            raise RuntimeError(
+                f"libgcnk.so not found at {LIB_PATH}: build it with __graft_entry__.build() "
+                "or `make -C <package>/csrc` (hipcc --offload-arch=gfx950). There is no CPU fallback.")
+        lib = ctypes.CDLL(LIB_PATH)
+        for name, (res, args) in SIGNATURES.items():
+            fn = getattr(lib, name)
+            fn.restype = res
+            fn.argtypes = args
+        v = lib.gcnk_abi_version()
+        if v != ABI_VERSION:
+            raise RuntimeError(f"libgcnk ABI version {v} != expected {ABI_VERSION}")
+        _lib = lib
+        return lib
+
+
+def check(rc, what):
+    if rc != OK:
+        msg = load().gcnk_last_error().decode(errors="replace")
+        kind = {EARG: "bad argument", EUNSUP: "unsupported", EHIP: "HIP error"}.get(rc, "error")
+        raise GcnkError(f"{what} failed ({kind}, rc={rc}): {msg}")

@@ -1,0 +1,271 @@
+// fp32 GEMM on CDNA4 matrix cores (v_mfma_f32_16x16x4_f32), plus the
+// deterministic column-sum used for bias gradients.
+//
+// Replaces th.spmm(dense H1, W2) (reference layer.py:102 in gc2 — ATen lowers
+// a dense th.spmm to mm) and the dense autograd products of the GCN layers:
+//   g_W2 = H1^T g      (transA; K = number of nodes -> split-K slabs)
+//   g_H1 = g W2^T      (transB; fused relu/dropout backward epilogue)
+// gfx950 has no xf32: the f32-input MFMA computes an exact fp32 fmaf chain
+// over its 4-deep k step at the fp32 vector rate, and frees the VALU for the
+// epilogue.
+//
+// Tile: BM x BN x 16, 256 threads = WM x WN waves, each wave FM x FN 16x16
+// fragments.  Operands are staged k-major in LDS ([k][m], [k][n]) so every
+// fragment read is 16 consecutive floats per k row.
+#include "gcnk_common.h"
+
+namespace gcnk {
+namespace {
+
+typedef float f32x4 __attribute__((ext_vector_type(4)));
+
+struct GemmEpi {
+  const float* bias;
+  const float* R;
+  int64_t ldr;
+  float scale;
+  int32_t code;
+};
+
+__device__ __forceinline__ float gemm_epi(const GemmEpi& e, float acc, int64_t m, int64_t n) {
+  switch (e.code) {
+    case GCNK_GEMM_EPI_BIAS:
+      return acc + (e.bias ? e.bias[n] : 0.f);
+    case GCNK_GEMM_EPI_BIAS_RELU: {
+      const float v = acc + (e.bias ? e.bias[n] : 0.f);
+      return v > 0.f ? v : 0.f;
+    }
+    case GCNK_GEMM_EPI_MASK_POS:
+      return e.R[m * e.ldr + n] > 0.f ? acc * e.scale : 0.f;
+    default:
+      return acc;
+  }
+}
+
+constexpr int BK = 16;
+
+template <int WM, int WN, int FM, int FN, bool TA, bool TB>
+__global__ void __launch_bounds__(256)
+gemm_f32_mfma_kernel(int32_t M, int32_t N, int32_t K, int32_t kchunk, const float* __restrict__ A,
+                     int64_t lda, const float* __restrict__ B, int64_t ldb, float* __restrict__ C,
+                     int64_t ldc, GemmEpi epi, float* __restrict__ slab) {
+  constexpr int BM = WM * FM * 16;
+  constexpr int BN = WN * FN * 16;
+  static_assert(WM * WN == 4, "256 threads = 4 waves");
+  __shared__ float As[BK][BM + 1];
+  __shared__ float Bs[BK][BN + 1];
+
+  const int tid = threadIdx.x;
+  const int lane = tid & 63;
+  const int wave = tid >> 6;
+  const int wm = wave / WN, wn = wave % WN;
+  const int64_t m0 = (int64_t)blockIdx.x * BM;
+  const int64_t n0 = (int64_t)blockIdx.y * BN;
+  const int32_t kb = blockIdx.z * kchunk;
+  const int32_t ke = min(K, kb + kchunk);
+
+  f32x4 acc[FM][FN];
+#pragma unroll
+  for (int i = 0; i < FM; ++i)
+#pragma unroll
+    for (int j = 0; j < FN; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+
+  for (int32_t k0 = kb; k0 < ke; k0 += BK) {
+#pragma unroll
+    for (int e = tid; e < BM * BK; e += 256) {
+      int m, k;
+      if (!TA) { m = e / BK; k = e % BK; }
+      else { k = e / BM; m = e % BM; }
+      const int64_t gm = m0 + m;
+      const int32_t gk = k0 + k;
+      float x = 0.f;
+      if (gm < M && gk < ke) x = TA ? A[(int64_t)gk * lda + gm] : A[gm * lda + gk];
+      As[k][m] = x;
+    }
+#pragma unroll
+    for (int e = tid; e < BN * BK; e += 256) {
+      int n, k;
+      if (!TB) { k = e / BN; n = e % BN; }
+      else { n = e / BK; k = e % BK; }
+      const int64_t gn = n0 + n;
+      const int32_t gk = k0 + k;
+      float x = 0.f;
+      if (gn < N && gk < ke) x = TB ? B[gn * ldb + gk] : B[(int64_t)gk * ldb + gn];
+      Bs[k][n] = x;
+    }
+    __syncthreads();
+#pragma unroll
+    for (int kk = 0; kk < BK; kk += 4) {
+      const int kr = kk + (lane >> 4);
+      float af[FM], bf[FN];
+#pragma unroll
+      for (int i = 0; i < FM; ++i) af[i] = As[kr][(wm * FM + i) * 16 + (lane & 15)];
+#pragma unroll
+      for (int j = 0; j < FN; ++j) bf[j] = Bs[kr][(wn * FN + j) * 16 + (lane & 15)];
+#pragma unroll
+      for (int i = 0; i < FM; ++i)
+#pragma unroll
+        for (int j = 0; j < FN; ++j) acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x4f32(af[i], bf[j], acc[i][j], 0, 0, 0);
+    }
+    __syncthreads();
+  }
+
+  // C/D map of 16x16 f32 MFMA: reg r -> row (lane>>4)*4 + r, col lane&15
+#pragma unroll
+  for (int i = 0; i < FM; ++i)
+#pragma unroll
+    for (int j = 0; j < FN; ++j)
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const int64_t gm = m0 + (wm * FM + i) * 16 + (lane >> 4) * 4 + r;
+        const int64_t gn = n0 + (wn * FN + j) * 16 + (lane & 15);
+        if (gm < M && gn < N) {
+          if (slab) slab[((int64_t)blockIdx.z * M + gm) * N + gn] = acc[i][j][r];
+          else C[gm * ldc + gn] = gemm_epi(epi, acc[i][j][r], gm, gn);
+        }
+      }
+}
+
+// Sum split-K slabs in slab order, then apply the epilogue.
+__global__ void gemm_splitk_reduce_kernel(int32_t M, int32_t N, int32_t S, const float* __restrict__ slab,
+                                          float* __restrict__ C, int64_t ldc, GemmEpi epi) {
+  const int64_t idx = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  const int64_t total = (int64_t)M * N;
+  if (idx >= total) return;
+  float acc = 0.f;
+  for (int s = 0; s < S; ++s) acc += slab[(int64_t)s * total + idx];
+  const int64_t m = idx / N, n = idx % N;
+  C[m * ldc + n] = gemm_epi(epi, acc, m, n);
+}
+
+template <int WM, int WN, int FM, int FN>
+int launch_gemm(bool ta, bool tb, int32_t M, int32_t N, int32_t K, const float* A, int64_t lda,
+                const float* B, int64_t ldb, float* C, int64_t ldc, const GemmEpi& e, int32_t split,
+                float* ws, hipStream_t s) {
+  constexpr int BM = WM * FM * 16, BN = WN * FN * 16;
+  int32_t kchunk = (K + split - 1) / split;
+  kchunk = (kchunk + BK - 1) / BK * BK;
+  if (kchunk <= 0) kchunk = BK;
+  const int32_t nsplit = (K + kchunk - 1) / kchunk > 0 ? (K + kchunk - 1) / kchunk : 1;
+  dim3 grid((unsigned)((M + BM - 1) / BM), (unsigned)((N + BN - 1) / BN), (unsigned)nsplit);
+  float* slab = nsplit > 1 ? ws : nullptr;
+#define GCNK_GEMM_LAUNCH(TA_, TB_)                                                                      \
+  hipLaunchKernelGGL((gemm_f32_mfma_kernel<WM, WN, FM, FN, TA_, TB_>), grid, dim3(256), 0, s, M, N, K,  \
+                     kchunk, A, lda, B, ldb, C, ldc, e, slab)
+  if (!ta && !tb) GCNK_GEMM_LAUNCH(false, false);
+  else if (ta && !tb) GCNK_GEMM_LAUNCH(true, false);
+  else if (!ta && tb) GCNK_GEMM_LAUNCH(false, true);
+  else GCNK_GEMM_LAUNCH(true, true);
+#undef GCNK_GEMM_LAUNCH
+  int rc = launch_check("gemm_f32_mfma_kernel");
+  if (rc || nsplit <= 1) return rc;
+  const int64_t total = (int64_t)M * N;
+  hipLaunchKernelGGL(gemm_splitk_reduce_kernel, dim3((unsigned)((total + 255) / 256)), dim3(256), 0, s, M, N,
+                     nsplit, ws, C, ldc, e);
+  return launch_check("gemm_splitk_reduce_kernel");
+}
+
+// ---------------------------------------------------------------------------
+// Column sum: pass 1 sums kColsumRows-row blocks, pass 2 sums blocks in order.
+constexpr int kColsumRows = 64;
+
+__global__ void colsum_pass1_kernel(const float* __restrict__ X, int64_t ldx, int32_t M, int32_t N,
+                                    float* __restrict__ part) {
+  const int64_t n = (int64_t)blockIdx.y * blockDim.x + threadIdx.x;
+  if (n >= N) return;
+  const int64_t r0 = (int64_t)blockIdx.x * kColsumRows;
+  const int64_t r1 = min<int64_t>(r0 + kColsumRows, M);
+  float acc = 0.f;
+  for (int64_t r = r0; r < r1; ++r) acc += X[r * ldx + n];
+  part[(int64_t)blockIdx.x * N + n] = acc;
+}
+
+__global__ void colsum_pass2_kernel(const float* __restrict__ part, int32_t nblk, int32_t N,
+                                    float* __restrict__ out) {
+  const int64_t n = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (n >= N) return;
+  float acc = 0.f;
+  for (int b = 0; b < nblk; ++b) acc += part[(int64_t)b * N + n];
+  out[n] = acc;
+}
+
+}  // namespace
+}  // namespace gcnk
+
+using namespace gcnk;
+
+extern "C" int64_t gcnk_gemm_workspace_bytes(int32_t M, int32_t N, int32_t K, int32_t split_k) {
+  (void)K;
+  if (split_k <= 1) return 0;
+  return (int64_t)split_k * M * N * 4;
+}
+
+extern "C" int gcnk_gemm_f32(int32_t transA, int32_t transB, int32_t M, int32_t N, int32_t K,
+                             const float* A, int64_t lda, const float* B, int64_t ldb, float* C,
+                             int64_t ldc, const float* bias, int32_t epilogue, const float* R,
+                             int64_t ldr, float scale, int32_t split_k, float* workspace,
+                             int64_t workspace_bytes, void* stream) {
+  if (M < 0 || N < 0 || K < 0) {
+    set_error("gcnk_gemm_f32: negative size");
+    return GCNK_EARG;
+  }
+  if (M == 0 || N == 0) return GCNK_OK;
+  if (!A || !B || !C) {
+    set_error("gcnk_gemm_f32: null pointer");
+    return GCNK_EARG;
+  }
+  if ((!transA && lda < K) || (transA && lda < M) || (!transB && ldb < N) || (transB && ldb < K) || ldc < N) {
+    set_error("gcnk_gemm_f32: leading dimension too small");
+    return GCNK_EARG;
+  }
+  if (epilogue == GCNK_GEMM_EPI_MASK_POS && (!R || ldr < N)) {
+    set_error("gcnk_gemm_f32: MASK_POS epilogue needs R with ldr >= N");
+    return GCNK_EARG;
+  }
+  if (epilogue != GCNK_GEMM_EPI_NONE && epilogue != GCNK_GEMM_EPI_BIAS && epilogue != GCNK_GEMM_EPI_BIAS_RELU &&
+      epilogue != GCNK_GEMM_EPI_MASK_POS) {
+    set_error("gcnk_gemm_f32: unknown epilogue %d", epilogue);
+    return GCNK_EARG;
+  }
+  if (split_k < 1) split_k = 1;
+  if (split_k > 1 && (!workspace || workspace_bytes < gcnk_gemm_workspace_bytes(M, N, K, split_k))) {
+    set_error("gcnk_gemm_f32: split_k=%d needs %lld B of workspace", split_k,
+              (long long)gcnk_gemm_workspace_bytes(M, N, K, split_k));
+    return GCNK_EARG;
+  }
+  GemmEpi e{bias, R, ldr, scale, epilogue};
+  hipStream_t s = (hipStream_t)stream;
+  const bool ta = transA != 0, tb = transB != 0;
+  if (N <= 16) return launch_gemm<4, 1, 2, 1>(ta, tb, M, N, K, A, lda, B, ldb, C, ldc, e, split_k, workspace, s);
+  return launch_gemm<2, 2, 2, 2>(ta, tb, M, N, K, A, lda, B, ldb, C, ldc, e, split_k, workspace, s);
+}
+
+extern "C" int64_t gcnk_colsum_workspace_bytes(int32_t M, int32_t N) {
+  const int64_t nblk = ((int64_t)M + kColsumRows - 1) / kColsumRows;
+  return nblk * N * 4;
+}
+
+extern "C" int gcnk_colsum_f32(const float* X, int64_t ldx, int32_t M, int32_t N, float* out,
+                               float* workspace, int64_t workspace_bytes, void* stream) {
+  if (M < 0 || N < 0 || ldx < N) {
+    set_error("gcnk_colsum_f32: bad shape");
+    return GCNK_EARG;
+  }
+  if (N == 0) return GCNK_OK;
+  hipStream_t s = (hipStream_t)stream;
+  if (M == 0) {
+    return hip_check(hipMemsetAsync(out, 0, (size_t)N * 4, s), "colsum memset");
+  }
+  if (!X || !out || !workspace || workspace_bytes < gcnk_colsum_workspace_bytes(M, N)) {
+    set_error("gcnk_colsum_f32: null pointer or workspace too small");
+    return GCNK_EARG;
+  }
+  const int32_t nblk = (M + kColsumRows - 1) / kColsumRows;
+  hipLaunchKernelGGL(colsum_pass1_kernel, dim3((unsigned)nblk, (unsigned)((N + 255) / 256)), dim3(256), 0, s, X,
+                     ldx, M, N, workspace);
+  int rc = launch_check("colsum_pass1_kernel");
+  if (rc) return rc;
+  hipLaunchKernelGGL(colsum_pass2_kernel, dim3((unsigned)((N + 255) / 256)), dim3(256), 0, s, workspace, nblk, N,
+                     out);
+  return launch_check("colsum_pass2_kernel");
+}

@@ -1,0 +1,105 @@
+"""Drop-in ``GraphConvolution`` / ``GCN`` modules running on the gfx950 kernels.
+
+Mirrors the reference's module interface (layer.py:25-190): constructor
+arguments, Parameter shapes (weight stored [in, out], not nn.Linear's
+[out, in]), ``state_dict`` keys (gc1.weight, gc1.bias, gc2.weight, gc2.bias),
+initialisation RNG order and ``__repr__`` — so ``trainer.py`` can pass
+``model = GCN`` (trainer.py:432) and instantiate it with
+``nfeat/nhid/nclass/dropout`` kwargs (trainer.py:300-303) unchanged.
+
+Differences by design:
+  * ``forward`` runs only on ROCm tensors (no CPU fallback).  Inputs may be
+    torch sparse COO (any order, uncoalesced — as utils.py:196-203 and
+    trainer.py:226-238 produce them), torch sparse CSR, or dense.
+  * The sparse operands are converted once to device CSR and cached.
+  * ``GCN.forward`` runs the two layers as one fused autograd graph
+    (ops.GCNFn): bias, ReLU and dropout live in the SpMM epilogue.
+  * Dropout masks: ``dropout_rng="cpu"`` (default) draws them exactly as the
+    reference's CPU ``th.dropout`` does — ``bernoulli_(1-p)`` on a float32
+    CPU tensor from torch's default generator — so a seeded run consumes the
+    same random stream as the reference and trains on identical masks;
+    ``dropout_rng="device"`` generates them inside the kernel (counter-based
+    hash), with no host work and no mask traffic.
+"""
+import math
+
+import torch
+from torch.nn import Module, Parameter
+
+from . import _lib
+from .ops import GCNFn, GraphConvFn, Operand
+from .sparse import as_csr
+
+
+class GraphConvolution(Module):
+    """out = adj @ (infeatn @ weight) + bias   (reference layer.py:25-123)."""
+
+    def __init__(self, in_features, out_features, bias=True):
+        super().__init__()
+        self.in_features = in_features
+        self.out_features = out_features
+        self.weight = Parameter(torch.empty(in_features, out_features, dtype=torch.float32))
+        if bias:
+            self.bias = Parameter(torch.empty(out_features, dtype=torch.float32))
+        else:
+            self.register_parameter("bias", None)
+        self.reset_parameters()
+
+    def reset_parameters(self):
+        # U(-1/sqrt(out), 1/sqrt(out)); weight first, then bias (layer.py:75-82) —
+        # the same draws from the same generator as the reference.
+        bound = 1.0 / math.sqrt(self.weight.size(1))
+        with torch.no_grad():
+            self.weight.uniform_(-bound, bound)
+            if self.bias is not None:
+                self.bias.uniform_(-bound, bound)
+
+    def forward(self, infeatn, adj):
+        xop = Operand(infeatn)
+        a = as_csr(adj)
+        x_dense = xop.dense if xop.dense is not None else None
+        return GraphConvFn.apply(self.weight, self.bias, x_dense, xop, a)
+
+    def __repr__(self):
+        return f"{type(self).__name__} ({self.in_features} -> {self.out_features})"
+
+
+class GCN(Module):
+    """Two-layer GCN: gc2(dropout(relu(gc1(x, adj))), adj)  (reference layer.py:126-190)."""
+
+    def __init__(self, nfeat, nhid, nclass, dropout, dropout_rng="cpu"):
+        super().__init__()
+        self.gc1 = GraphConvolution(nfeat, nhid)
+        self.gc2 = GraphConvolution(nhid, nclass)
+        self.dropout = dropout
+        if dropout_rng not in ("cpu", "device"):
+            raise ValueError("dropout_rng must be 'cpu' or 'device'")
+        self.dropout_rng = dropout_rng
+        self._hash_calls = 0
+
+    def _dropout_args(self, nrows, device):
+        """Epilogue code and mask/scale for layer.py:185 (ATen dropout semantics)."""
+        p = float(self.dropout)
+        if not self.training or p == 0.0:   # ATen returns the input untouched (no RNG draw)
+            return _lib.EPI_BIAS_RELU, None, 1.0, 1.0, 0, 0
+        nhid = self.gc1.out_features
+        if p >= 1.0:                         # ATen: input * 0
+            return _lib.EPI_BIAS_RELU_DROP, torch.zeros((nrows, nhid), dtype=torch.uint8, device=device), \
+                0.0, 0.0, 0, 0
+        # noise = bernoulli(1-p) / (1-p) with the division done in float32 (ATen)
+        scale = float(torch.ones((), dtype=torch.float32).div_(1.0 - p))
+        if self.dropout_rng == "cpu":
+            noise = torch.empty((nrows, nhid), dtype=torch.float32).bernoulli_(1.0 - p)
+            mask = noise.to(torch.uint8).to(device, non_blocking=False)
+            return _lib.EPI_BIAS_RELU_DROP, mask, scale, 1.0 - p, 0, 0
+        seed = int(torch.initial_seed()) & (2**64 - 1)
+        offset = self._hash_calls * nrows * nhid
+        self._hash_calls += 1
+        return _lib.EPI_BIAS_RELU_HASH, None, scale, 1.0 - p, seed, offset
+
+    def forward(self, x, adj):
+        a = as_csr(adj)
+        xop = Operand(x)
+        epi, mask, scale, keep, seed, offset = self._dropout_args(a.shape[0], a.device)
+        return GCNFn.apply(self.gc1.weight, self.gc1.bias, self.gc2.weight, self.gc2.bias, xop, a,
+                           epi, mask, scale, keep, seed, offset)

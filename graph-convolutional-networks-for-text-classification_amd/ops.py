@@ -1,0 +1,237 @@
+"""Functional ops on the HIP kernels and the autograd Functions of the GCN path.
+
+Each op replaces an arithmetic site of the reference (cited per function);
+tensors cross the C-ABI as raw device pointers plus torch's current stream,
+so every op is asynchronous and hipGraph-capturable.
+"""
+import ctypes
+
+import torch
+
+from . import _lib
+from .sparse import CSR, as_csr, require_device
+
+_NULL = ctypes.c_void_p(0)
+
+
+def _ptr(t):
+    return ctypes.c_void_p(t.data_ptr()) if t is not None else _NULL
+
+
+def _stream(dev):
+    return ctypes.c_void_p(torch.cuda.current_stream(dev).cuda_stream)
+
+
+def _dense_f32(t, what):
+    require_device(t, what)
+    if t.dtype != torch.float32:
+        raise RuntimeError(f"{what} must be float32 (the reference computes in fp32), got {t.dtype}")
+    if t.dim() != 2:
+        raise RuntimeError(f"{what} must be 2-D, got shape {tuple(t.shape)}")
+    if t.stride(1) != 1:
+        t = t.contiguous()
+    return t
+
+
+def default_ipc(a, F):
+    return int(_lib.load().gcnk_spmm_default_ipc(a.shape[0], a.nnz, F))
+
+
+def spmm(a, B, bias=None, epilogue=_lib.EPI_NONE, mask=None, scale=1.0, keep_prob=1.0, seed=0, offset=0,
+         out=None, ipc=None, lanes=0):
+    """C = epi(A @ B) with A a CSR (or torch sparse) and B dense [K, F].
+
+    Replaces ``th.spmm(adj, support)`` (reference layer.py:106) and
+    ``th.spmm(X, W)`` with sparse X (layer.py:102); the epilogue fuses
+    ``+ bias`` (layer.py:110), ``th.relu`` (layer.py:182) and the dropout
+    multiply (layer.py:185)."""
+    a = as_csr(a)
+    B = _dense_f32(B, "dense operand")
+    M, K = a.shape
+    if B.shape[0] != K:
+        raise RuntimeError(f"spmm shape mismatch: sparse {tuple(a.shape)} @ dense {tuple(B.shape)}")
+    if B.device != a.device:
+        raise RuntimeError(f"spmm device mismatch: {a.device} vs {B.device}")
+    F = B.shape[1]
+    if out is None:
+        out = torch.empty((M, F), dtype=torch.float32, device=B.device)
+    if bias is not None:
+        bias = bias.contiguous()
+    if mask is not None:
+        mask = mask.contiguous()
+    if ipc is None:
+        ipc = default_ipc(a, F)
+    plan, ipc, nslots, nfix = a.plan(ipc)
+    lib = _lib.load()
+    wsb = lib.gcnk_spmm_workspace_bytes(nslots, F)
+    ws = torch.empty((max(wsb, 16) + 3) // 4, dtype=torch.float32, device=B.device) if nslots > 0 else None
+    with torch.cuda.device(B.device):
+        rc = lib.gcnk_spmm_csr_f32(
+            _ptr(a.rowptr), _ptr(a.colind), _ptr(a.val), M, K, a.nnz,
+            _ptr(plan), ipc, nfix,
+            _ptr(B), B.stride(0), F,
+            _ptr(out), out.stride(0),
+            _ptr(bias), epilogue,
+            _ptr(mask), mask.stride(0) if mask is not None else 0, float(scale),
+            float(keep_prob), int(seed) & (2**64 - 1), int(offset) & (2**64 - 1),
+            _ptr(ws), wsb, int(lanes), _stream(B.device))
+    _lib.check(rc, "gcnk_spmm_csr_f32")
+    return out
+
+
+def gemm(A, B, transA=False, transB=False, bias=None, epilogue=_lib.GEMM_EPI_NONE, R=None, scale=1.0,
+         split_k=None, out=None):
+    """C = epi(op(A) @ op(B)) on fp32 MFMA.
+
+    Replaces the dense ``th.spmm(H1, W2)`` of gc2 (reference layer.py:102,
+    lowered to mm by ATen) and the dense autograd products."""
+    A = _dense_f32(A, "A")
+    B = _dense_f32(B, "B")
+    M, K = (A.shape[1], A.shape[0]) if transA else (A.shape[0], A.shape[1])
+    Kb, N = (B.shape[1], B.shape[0]) if transB else (B.shape[0], B.shape[1])
+    if K != Kb:
+        raise RuntimeError(f"gemm shape mismatch: op(A) {M}x{K} @ op(B) {Kb}x{N}")
+    if out is None:
+        out = torch.empty((M, N), dtype=torch.float32, device=A.device)
+    if split_k is None:
+        # long reductions with a small output (H^T g: K = nodes) get K-slabs
+        tiles = ((M + 63) // 64) * ((N + 63) // 64)
+        split_k = 1
+        while split_k < 64 and tiles * split_k < 256 and K // (split_k * 2) >= 128:
+            split_k *= 2
+    lib = _lib.load()
+    wsb = lib.gcnk_gemm_workspace_bytes(M, N, K, split_k)
+    ws = torch.empty((wsb + 3) // 4, dtype=torch.float32, device=A.device) if wsb > 0 else None
+    if R is not None:
+        R = _dense_f32(R, "R")
+    with torch.cuda.device(A.device):
+        rc = lib.gcnk_gemm_f32(int(transA), int(transB), M, N, K, _ptr(A), A.stride(0), _ptr(B), B.stride(0),
+                               _ptr(out), out.stride(0), _ptr(bias.contiguous() if bias is not None else None),
+                               epilogue, _ptr(R), R.stride(0) if R is not None else 0, float(scale), int(split_k),
+                               _ptr(ws), wsb, _stream(A.device))
+    _lib.check(rc, "gcnk_gemm_f32")
+    return out
+
+
+def colsum(X):
+    """out[n] = sum_m X[m, n] — the bias gradient (autograd of layer.py:110)."""
+    X = _dense_f32(X, "X")
+    M, N = X.shape
+    lib = _lib.load()
+    wsb = lib.gcnk_colsum_workspace_bytes(M, N)
+    ws = torch.empty(max((wsb + 3) // 4, 1), dtype=torch.float32, device=X.device)
+    out = torch.empty(N, dtype=torch.float32, device=X.device)
+    with torch.cuda.device(X.device):
+        rc = lib.gcnk_colsum_f32(_ptr(X), X.stride(0), M, N, _ptr(out), _ptr(ws), wsb, _stream(X.device))
+    _lib.check(rc, "gcnk_colsum_f32")
+    return out
+
+
+# ----------------------------------------------------------------------------------------
+# Operand for the first product of a layer: sparse (CSR) or dense infeatn.
+
+class Operand:
+    """``infeatn`` of GraphConvolution.forward: sparse -> CSR, dense -> tensor."""
+
+    __slots__ = ("csr", "dense")
+
+    def __init__(self, x):
+        if isinstance(x, CSR):
+            self.csr, self.dense = x, None
+        elif isinstance(x, torch.Tensor) and (x.is_sparse or x.layout == torch.sparse_csr):
+            self.csr, self.dense = as_csr(x), None
+        else:
+            self.csr, self.dense = None, _dense_f32(x, "infeatn")
+
+    @property
+    def shape(self):
+        return self.csr.shape if self.csr is not None else tuple(self.dense.shape)
+
+    def times(self, W):
+        """infeatn @ W  (layer.py:102)."""
+        if self.csr is not None:
+            return spmm(self.csr, W)
+        return gemm(self.dense, W)
+
+    def t_times(self, G):
+        """infeatn^T @ G  (autograd of layer.py:102 w.r.t. W)."""
+        if self.csr is not None:
+            return spmm(self.csr.t(), G)
+        return gemm(self.dense, G, transA=True)
+
+
+class GraphConvFn(torch.autograd.Function):
+    """out = A (X W) + b — one GraphConvolution (reference layer.py:84-112)."""
+
+    @staticmethod
+    def forward(ctx, W, b, x, xop, adj):
+        support = xop.times(W)                                   # layer.py:102
+        out = spmm(adj, support, bias=b,                         # layer.py:106,110
+                   epilogue=_lib.EPI_BIAS if b is not None else _lib.EPI_NONE)
+        ctx.xop, ctx.adj = xop, adj
+        ctx.has_bias = b is not None
+        ctx.save_for_backward(W)
+        return out
+
+    @staticmethod
+    def backward(ctx, g):
+        (W,) = ctx.saved_tensors
+        g = g.contiguous()
+        gW = gb = gx = None
+        gS = spmm(ctx.adj.t(), g)                                # d/d support of A @ support
+        if ctx.needs_input_grad[0]:
+            gW = ctx.xop.t_times(gS)
+        if ctx.has_bias and ctx.needs_input_grad[1]:
+            gb = colsum(g)
+        if ctx.xop.dense is not None and ctx.needs_input_grad[2]:
+            gx = gemm(gS, W, transB=True)
+        return gW, gb, gx, None, None
+
+
+class GCNFn(torch.autograd.Function):
+    """The two-layer forward of reference layer.py:164-190 as one fused graph:
+
+        S1 = X W1                   spmm (sparse X) / gemm (dense X)      layer.py:102
+        H1 = drop(relu(A S1 + b1))  spmm + fused epilogue                 layer.py:106,110,182,185
+        S2 = H1 W2                  fp32 MFMA gemm                         layer.py:102 (gc2)
+        Z  = A S2 + b2              spmm + bias epilogue                   layer.py:106,110 (gc2)
+
+    Backward (trainer.py:361):
+        gb2 = colsum(g);  gS2 = A^T g;  gW2 = H1^T gS2 (split-K);
+        gZ1 = (H1 > 0) ? (gS2 W2^T) * scale : 0   (gemm + MASK_POS epilogue; == ATen's
+              mul-by-noise then threshold_backward because H1 > 0 <=> kept and Z1 > 0)
+        gb1 = colsum(gZ1);  gS1 = A^T gZ1;  gW1 = X^T gS1.
+    """
+
+    @staticmethod
+    def forward(ctx, W1, b1, W2, b2, xop, adj, epi, mask, scale, keep, seed, offset):
+        S1 = xop.times(W1)
+        H1 = spmm(adj, S1, bias=b1, epilogue=epi, mask=mask, scale=scale, keep_prob=keep, seed=seed,
+                  offset=offset)
+        S2 = gemm(H1, W2)
+        out = spmm(adj, S2, bias=b2, epilogue=_lib.EPI_BIAS if b2 is not None else _lib.EPI_NONE)
+        ctx.xop, ctx.adj, ctx.scale = xop, adj, float(scale)
+        ctx.has_b1, ctx.has_b2 = b1 is not None, b2 is not None
+        ctx.save_for_backward(W2, H1)
+        return out
+
+    @staticmethod
+    def backward(ctx, g):
+        W2, H1 = ctx.saved_tensors
+        g = g.contiguous()
+        need = ctx.needs_input_grad
+        gW1 = gb1 = gW2 = gb2 = None
+        adjT = ctx.adj.t()
+        if ctx.has_b2 and need[3]:
+            gb2 = colsum(g)
+        gS2 = spmm(adjT, g)
+        if need[2]:
+            gW2 = gemm(H1, gS2, transA=True)
+        if need[0] or need[1]:
+            gZ1 = gemm(gS2, W2, transB=True, epilogue=_lib.GEMM_EPI_MASK_POS, R=H1, scale=ctx.scale)
+            if ctx.has_b1 and need[1]:
+                gb1 = colsum(gZ1)
+            if need[0]:
+                gS1 = spmm(adjT, gZ1)
+                gW1 = ctx.xop.t_times(gS1)
+        return gW1, gb1, gW2, gb2, None, None, None, None, None, None, None, None

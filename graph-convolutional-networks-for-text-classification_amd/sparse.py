@@ -1,0 +1,200 @@
+"""Device CSR operands for the SpMM kernels, built once per graph and cached.
+
+The reference hands ``th.spmm`` torch sparse COO tensors every call:
+  * A-hat from ``utils.sparse_mx_to_torch_sparse_tensor`` (utils.py:196-203):
+    fp32 values, int64 indices, column-major order, uncoalesced;
+  * X from ``trainer.py:226-238``: row-major COO.
+ATen re-coalesces such tensors on every call.  Here the first forward
+converts them once to an int32 CSR resident in HBM (plus, lazily, the
+transposed CSR the autograd products need and the merge-path schedule per
+chunk size) and later calls hit the cache.
+
+HBM layout of one CSR operand (M rows, K cols, nnz nonzeros):
+  rowptr int32[M+1] | colind int32[nnz] | val fp32[nnz]
+  plan   int32[...]  merge-path schedule (include/gcnk.h), one per ipc
+"""
+import collections
+import ctypes
+import threading
+
+import torch
+
+from . import _lib
+
+_INT32_MAX = 2**31 - 1
+
+
+def _stream_ptr(device):
+    return ctypes.c_void_p(torch.cuda.current_stream(device).cuda_stream)
+
+
+def require_device(t, what):
+    if not isinstance(t, torch.Tensor) or t.device.type != "cuda":
+        dev = getattr(t, "device", type(t))
+        raise RuntimeError(
+            f"{what} must be a tensor on a ROCm GPU (got {dev}); this framework runs the GCN hot path "
+            "only through its HIP kernels — move the model and inputs with .to('cuda').")
+
+
+class CSR:
+    """A sparse matrix in int32 CSR on one device, with cached schedules."""
+
+    def __init__(self, rowptr, colind, val, shape):
+        self.rowptr = rowptr.contiguous()
+        self.colind = colind.contiguous()
+        self.val = val.contiguous()
+        self.shape = (int(shape[0]), int(shape[1]))
+        self.nnz = int(self.colind.numel())
+        self.device = self.rowptr.device
+        self._plans = {}
+        self._t = None
+        self._lock = threading.Lock()
+
+    def __repr__(self):
+        return f"CSR(shape={self.shape}, nnz={self.nnz}, device={self.device})"
+
+    # -- merge-path schedule (gcnk_spmm_plan_build), one per chunk size -----------------
+    def plan(self, ipc):
+        p = self._plans.get(ipc)
+        if p is not None:
+            return p
+        with self._lock:
+            p = self._plans.get(ipc)
+            if p is not None:
+                return p
+            lib = _lib.load()
+            M, _ = self.shape
+            nbytes = lib.gcnk_spmm_plan_bytes(M, self.nnz, ipc)
+            if nbytes < 0:
+                raise RuntimeError(f"bad plan request M={M} nnz={self.nnz} ipc={ipc}")
+            buf = torch.empty((nbytes + 3) // 4, dtype=torch.int32, device=self.device)
+            with torch.cuda.device(self.device):
+                s = _stream_ptr(self.device)
+                _lib.check(lib.gcnk_spmm_plan_build(self.rowptr.data_ptr(), M, self.nnz, ipc, buf.data_ptr(),
+                                                    nbytes, s), "gcnk_spmm_plan_build")
+                hdr = (ctypes.c_int32 * 4)()
+                # one-time setup sync: sizes the split-row partial workspace
+                _lib.check(lib.gcnk_spmm_plan_query(buf.data_ptr(), ctypes.cast(hdr, ctypes.c_void_p), s),
+                           "gcnk_spmm_plan_query")
+            p = (buf, ipc, int(hdr[0]), int(hdr[1]))
+            self._plans[ipc] = p
+            return p
+
+    # -- transpose (gcnk_csr_transpose), cached ---------------------------------------
+    def t(self):
+        if self._t is not None:
+            return self._t
+        with self._lock:
+            if self._t is None:
+                self._t = transpose(self)
+                self._t._t = self
+            return self._t
+
+
+def transpose(a):
+    lib = _lib.load()
+    M, K = a.shape
+    dev = a.device
+    rp_t = torch.empty(K + 1, dtype=torch.int32, device=dev)
+    ci_t = torch.empty(a.nnz, dtype=torch.int32, device=dev)
+    v_t = torch.empty(a.nnz, dtype=torch.float32, device=dev)
+    wsb = lib.gcnk_csr_transpose_workspace_bytes(M, K, a.nnz)
+    ws = torch.empty(max(wsb, 1), dtype=torch.uint8, device=dev)
+    with torch.cuda.device(dev):
+        _lib.check(lib.gcnk_csr_transpose(a.rowptr.data_ptr(), a.colind.data_ptr(), a.val.data_ptr(), M, K, a.nnz,
+                                          rp_t.data_ptr(), ci_t.data_ptr(), v_t.data_ptr(), ws.data_ptr(), wsb,
+                                          _stream_ptr(dev)), "gcnk_csr_transpose")
+    return CSR(rp_t, ci_t, v_t, (K, M))
+
+
+def _check_int32(M, K, nnz):
+    if M > _INT32_MAX or K > _INT32_MAX or nnz > _INT32_MAX or M + nnz >= _INT32_MAX:
+        raise RuntimeError(f"sparse operand too large for int32 CSR (M={M}, K={K}, nnz={nnz})")
+
+
+def from_torch(t):
+    """Torch sparse tensor (COO in any order / uncoalesced, or CSR) on a GPU -> CSR.
+
+    Duplicates in an uncoalesced COO are summed (what th.spmm computes)."""
+    require_device(t, "sparse operand")
+    if t.dim() != 2:
+        raise RuntimeError(f"sparse operand must be 2-D, got {t.dim()}-D")
+    M, K = t.shape
+    if t.layout == torch.sparse_csr:
+        rowptr = t.crow_indices().to(torch.int32)
+        colind = t.col_indices().to(torch.int32)
+        val = t.values().to(torch.float32)
+        _check_int32(M, K, colind.numel())
+        return CSR(rowptr, colind, val, (M, K))
+    if t.layout != torch.sparse_coo:
+        raise RuntimeError(f"unsupported sparse layout {t.layout}")
+    c = t if t.is_coalesced() else t.coalesce()
+    idx = c._indices()
+    val = c._values().to(torch.float32)
+    nnz = val.numel()
+    _check_int32(M, K, nnz)
+    counts = torch.bincount(idx[0], minlength=M)
+    rowptr = torch.zeros(M + 1, dtype=torch.int32, device=t.device)
+    rowptr[1:] = torch.cumsum(counts, 0).to(torch.int32)
+    return CSR(rowptr, idx[1].to(torch.int32), val, (M, K))
+
+
+def from_arrays(rowptr, colind, val, shape, device):
+    """Build a CSR from host/numpy arrays (already sorted CSR)."""
+    rp = torch.as_tensor(rowptr).to(device=device, dtype=torch.int32)
+    ci = torch.as_tensor(colind).to(device=device, dtype=torch.int32)
+    v = torch.as_tensor(val).to(device=device, dtype=torch.float32)
+    _check_int32(shape[0], shape[1], ci.numel())
+    return CSR(rp, ci, v, shape)
+
+
+class _Cache:
+    """LRU of torch sparse tensor -> CSR, keyed by storage identity + version.
+
+    The entry keeps a reference to the source tensor so its storage cannot be
+    recycled (which would make a stale key collide)."""
+
+    def __init__(self, capacity=16):
+        self.capacity = capacity
+        self._d = collections.OrderedDict()
+        self._lock = threading.Lock()
+
+    @staticmethod
+    def key(t):
+        if t.layout == torch.sparse_csr:
+            parts = (t.crow_indices(), t.col_indices(), t.values())
+        else:
+            parts = (t._indices(), t._values())
+        return (t.layout, tuple(t.shape), t.device.index,
+                tuple(p.data_ptr() for p in parts), tuple(p._version for p in parts))
+
+    def get(self, t):
+        k = self.key(t)
+        with self._lock:
+            hit = self._d.get(k)
+            if hit is not None:
+                self._d.move_to_end(k)
+                return hit[1]
+        csr = from_torch(t)
+        with self._lock:
+            self._d[k] = (t, csr)
+            self._d.move_to_end(k)
+            while len(self._d) > self.capacity:
+                self._d.popitem(last=False)
+        return csr
+
+    def clear(self):
+        with self._lock:
+            self._d.clear()
+
+
+CACHE = _Cache()
+
+
+def as_csr(t):
+    """CSR view of a torch sparse tensor (cached) or pass-through of a CSR."""
+    if isinstance(t, CSR):
+        return t
+    if not isinstance(t, torch.Tensor) or not t.is_sparse and t.layout != torch.sparse_csr:
+        raise RuntimeError("expected a torch sparse tensor or a CSR")
+    return CACHE.get(t)

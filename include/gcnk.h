@@ -1,0 +1,154 @@
+/*
+ * gcnk.h — C-ABI of libgcnk.so, the MI355X (gfx950) kernels behind the
+ * drop-in GraphConvolution / GCN modules.
+ *
+ * The reference (anargh-t/Graph-Convolutional-Networks-for-Text-Classification)
+ * has no native code: every arithmetic site on its hot path is a call into
+ * ATen.  Each entry point below replaces one of those call sites:
+ *
+ *   layer.py:102  support = th.spmm(infeatn, W)   sparse X  -> gcnk_spmm_csr_f32 (X in CSR)
+ *                                                 dense  H  -> gcnk_gemm_f32 (fp32 MFMA)
+ *   layer.py:106  output  = th.spmm(adj, support)          -> gcnk_spmm_csr_f32 (A-hat in CSR)
+ *   layer.py:110  output + bias                             -> fused epilogue (GCNK_EPI_BIAS*)
+ *   layer.py:182  th.relu                                   -> fused epilogue (GCNK_EPI_BIAS_RELU)
+ *   layer.py:185  th.dropout(x, p, train)                   -> fused epilogue (GCNK_EPI_*_DROP*)
+ *   autograd of :102/:106/:110 (trainer.py:361 loss.backward())
+ *                  A^T g, X^T g                             -> gcnk_spmm_csr_f32 on cached transposes
+ *                  H^T g, g W^T, relu/dropout mask          -> gcnk_gemm_f32 (+GCNK_GEMM_EPI_MASK_POS)
+ *                  sum over rows of g  (bias grad)          -> gcnk_colsum_f32
+ *   utils.py:196-203 / trainer.py:226-238 (COO tensors handed to th.spmm)
+ *                                                           -> gcnk_spmm_plan_build (one-time schedule)
+ *
+ * Conventions
+ *   - All pointers are DEVICE pointers unless a parameter says "host".
+ *   - Dense matrices are row-major fp32 with an explicit leading dimension.
+ *   - CSR uses int32 row pointers / column indices (callers check < 2^31);
+ *     element offsets into dense matrices are 64-bit.
+ *   - Every call is asynchronous on `stream` (a hipStream_t; NULL = default
+ *     stream).  No entry point allocates or frees device memory, and none
+ *     synchronises, except gcnk_spmm_plan_query which is documented as a
+ *     one-time setup sync.  All entry points are safe to capture in a hipGraph.
+ *   - Return 0 on success; GCNK_EARG (-1) bad argument/shape, GCNK_EUNSUP (-2)
+ *     unsupported configuration, GCNK_EHIP (-3) HIP launch/runtime error.
+ *     The message is in a thread-local buffer returned by gcnk_last_error().
+ *   - Reentrant: no global mutable state besides the thread-local error text.
+ */
+#ifndef GCNK_H_
+#define GCNK_H_
+
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define GCNK_ABI_VERSION 1
+
+#define GCNK_OK 0
+#define GCNK_EARG (-1)
+#define GCNK_EUNSUP (-2)
+#define GCNK_EHIP (-3)
+
+/* SpMM epilogues (applied once per finished output row element).
+ * keep-mask semantics follow ATen's dropout (noise = bernoulli(1-p)/(1-p),
+ * out = x * noise): an element is kept where mask != 0 and multiplied by
+ * drop_scale. */
+#define GCNK_EPI_NONE 0
+#define GCNK_EPI_BIAS 1            /* + bias[col]                      layer.py:110 */
+#define GCNK_EPI_BIAS_RELU 2       /* relu(. + bias)                   layer.py:110,182 */
+#define GCNK_EPI_BIAS_RELU_DROP 3  /* relu(.+bias) * (mask?scale:0)    layer.py:110,182,185 */
+#define GCNK_EPI_BIAS_RELU_HASH 4  /* as 3 with an in-kernel counter-based RNG mask */
+
+/* GEMM epilogues */
+#define GCNK_GEMM_EPI_NONE 0
+#define GCNK_GEMM_EPI_BIAS 1
+#define GCNK_GEMM_EPI_BIAS_RELU 2
+#define GCNK_GEMM_EPI_MASK_POS 5   /* C = (R[m,n] > 0) ? acc*scale : 0   (relu+dropout backward) */
+
+int gcnk_abi_version(void);
+const char* gcnk_last_error(void);
+
+/* ---------------------------------------------------------------------------
+ * CSR SpMM:  C[M x F] = epi( A[M x K] (CSR) * B[K x F] )
+ * Replaces th.spmm(adj, support) (layer.py:106) and th.spmm(X, W)
+ * (layer.py:102, sparse X) and their autograd (A^T g, X^T g).
+ *
+ * Work is scheduled by a merge-path plan over (row ends + nonzeros): the
+ * path is cut into chunks of `ipc` items; a chunk boundary falling inside a
+ * row shorter than `ipc` is moved back to that row's start, so only heavy
+ * rows are split.  Split rows are summed deterministically (fixed chunk order,
+ * no float atomics) by a fix-up pass.  The plan depends only on the sparsity
+ * pattern and ipc and is built once per graph.
+ *
+ * Plan layout (int32, device):
+ *   [0] nslots  [1] nfix  [2] ipc  [3] nchunks (low 31 bits)
+ *   coords:     2*(nchunks+1)   merge-path start (row, nnz) of every chunk
+ *   head_slot:  nchunks         partial slot of the row a chunk finishes but did not start, or -1
+ *   tail_slot:  nchunks         partial slot of the row a chunk starts but does not finish, or -1
+ *   fix:        2*nchunks       (chunk, first contributing chunk) of every split row
+ * ------------------------------------------------------------------------- */
+int32_t gcnk_spmm_default_ipc(int32_t M, int64_t nnz, int32_t F);
+int64_t gcnk_spmm_plan_chunks(int32_t M, int64_t nnz, int32_t ipc);
+int64_t gcnk_spmm_plan_bytes(int32_t M, int64_t nnz, int32_t ipc);
+int gcnk_spmm_plan_build(const int32_t* rowptr, int32_t M, int64_t nnz, int32_t ipc,
+                         void* plan, int64_t plan_bytes, void* stream);
+/* Copies the 4-word plan header to host memory `out4` and synchronises
+ * `stream`.  One-time setup call (sizes the partial-sum workspace). */
+int gcnk_spmm_plan_query(const void* plan, int32_t* out4, void* stream);
+/* Bytes of partial-sum workspace needed for `nslots` split-row partials of width F. */
+int64_t gcnk_spmm_workspace_bytes(int32_t nslots, int32_t F);
+
+int gcnk_spmm_csr_f32(const int32_t* rowptr, const int32_t* colind, const float* val,
+                      int32_t M, int32_t K, int64_t nnz,
+                      const void* plan, int32_t ipc, int32_t nfix,
+                      const float* B, int64_t ldb, int32_t F,
+                      float* C, int64_t ldc,
+                      const float* bias, int32_t epilogue,
+                      const uint8_t* drop_mask, int64_t ldm, float drop_scale,
+                      float keep_prob, uint64_t seed, uint64_t offset,
+                      float* workspace, int64_t workspace_bytes,
+                      int32_t lanes_hint, void* stream);
+
+/* ---------------------------------------------------------------------------
+ * fp32 GEMM on MFMA (v_mfma_f32_16x16x4_f32; exact fp32 FMA chains):
+ *   C[M x N] = epi( op(A)[M x K] * op(B)[K x N] )
+ * op(A) = A (row-major [M x K], lda) or A^T (A stored [K x M], lda) when transA.
+ * op(B) = B ([K x N], ldb) or B^T (B stored [N x K], ldb) when transB.
+ * Replaces th.spmm(dense H, W) (layer.py:102 in gc2, which ATen lowers to mm)
+ * and the dense autograd products H^T g, g W^T.
+ * split_k > 1 reduces K in slabs (workspace = split_k*M*N floats) summed in a
+ * fixed order by a second pass (bitwise reproducible).
+ * ------------------------------------------------------------------------- */
+int64_t gcnk_gemm_workspace_bytes(int32_t M, int32_t N, int32_t K, int32_t split_k);
+int gcnk_gemm_f32(int32_t transA, int32_t transB, int32_t M, int32_t N, int32_t K,
+                  const float* A, int64_t lda, const float* B, int64_t ldb,
+                  float* C, int64_t ldc,
+                  const float* bias, int32_t epilogue, const float* R, int64_t ldr, float scale,
+                  int32_t split_k, float* workspace, int64_t workspace_bytes, void* stream);
+
+/* ---------------------------------------------------------------------------
+ * out[n] = sum_m X[m, n]  (bias gradient, autograd of layer.py:110).
+ * Deterministic two-pass reduction; workspace = gcnk_colsum_workspace_bytes.
+ * ------------------------------------------------------------------------- */
+int64_t gcnk_colsum_workspace_bytes(int32_t M, int32_t N);
+int gcnk_colsum_f32(const float* X, int64_t ldx, int32_t M, int32_t N, float* out,
+                    float* workspace, int64_t workspace_bytes, void* stream);
+
+/* ---------------------------------------------------------------------------
+ * Sparse-format helpers (one-time graph preparation, utils.py:185-213,
+ * trainer.py:226-238).
+ *   gcnk_csr_transpose: CSR A[M x K] -> CSR A^T[K x M]; within each output
+ *     row entries keep ascending source-row order (stable).  Needs a
+ *     workspace of gcnk_csr_transpose_workspace_bytes.
+ * ------------------------------------------------------------------------- */
+int64_t gcnk_csr_transpose_workspace_bytes(int32_t M, int32_t K, int64_t nnz);
+int gcnk_csr_transpose(const int32_t* rowptr, const int32_t* colind, const float* val,
+                       int32_t M, int32_t K, int64_t nnz,
+                       int32_t* rowptr_t, int32_t* colind_t, float* val_t,
+                       void* workspace, int64_t workspace_bytes, void* stream);
+
+#ifdef __cplusplus
+}
+#endif
+
+#endif /* GCNK_H_ */

@@ -1,0 +1,81 @@
+"""CPU checks of the C-ABI boundary: the library loads, exports every symbol
+include/gcnk.h declares, and validates arguments (no compute without a GPU)."""
+import ctypes
+import os
+import re
+
+import pytest
+
+import gcn_amd  # noqa: F401
+from graph_convolutional_networks_for_text_classification_amd import _lib
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
+
+def _declared_symbols():
+    with open(os.path.join(ROOT, "include", "gcnk.h")) as f:
+        src = f.read()
+    src = re.sub(r"/\*.*?\*/", "", src, flags=re.S)
+    return sorted(set(re.findall(r"\b(gcnk_[a-z0-9_]+)\s*\(", src)))
+
+
+def test_library_exports_every_declared_symbol():
+    lib = _lib.load()
+    declared = _declared_symbols()
+    assert len(declared) >= 14
+    for name in declared:
+        assert hasattr(lib, name), name
+    assert set(declared) == set(_lib.SIGNATURES), "ctypes signatures out of sync with include/gcnk.h"
+
+
+def test_abi_version_and_error_text():
+    lib = _lib.load()
+    assert lib.gcnk_abi_version() == _lib.ABI_VERSION == 1
+    rc = lib.gcnk_spmm_csr_f32(None, None, None, -1, 0, 0, None, 4, 0, None, 0, 8, None, 0, None, 0, None, 0,
+                               1.0, 1.0, 0, 0, None, 0, 0, None)
+    assert rc == _lib.EARG
+    assert b"bad argument" in lib.gcnk_last_error()
+    with pytest.raises(_lib.GcnkError):
+        _lib.check(rc, "spmm")
+
+
+def test_argument_validation_without_gpu():
+    lib = _lib.load()
+    # leading dimension too small
+    rc = lib.gcnk_gemm_f32(0, 0, 4, 4, 4, ctypes.c_void_p(16), 2, ctypes.c_void_p(16), 4, ctypes.c_void_p(16), 4,
+                           None, 0, None, 0, 1.0, 1, None, 0, None)
+    assert rc == _lib.EARG
+    # split-K without workspace
+    rc = lib.gcnk_gemm_f32(0, 0, 4, 4, 4096, ctypes.c_void_p(16), 4096, ctypes.c_void_p(16), 4,
+                           ctypes.c_void_p(16), 4, None, 0, None, 0, 1.0, 8, None, 0, None)
+    assert rc == _lib.EARG
+    # plan buffer too small
+    rc = lib.gcnk_spmm_plan_build(ctypes.c_void_p(16), 10, 100, 8, ctypes.c_void_p(16), 4, None)
+    assert rc == _lib.EARG
+    # empty problems are no-ops that succeed without touching the device
+    assert lib.gcnk_spmm_csr_f32(None, None, None, 0, 0, 0, ctypes.c_void_p(16), 4, 0, None, 0, 8, None, 8, None, 0,
+                                 None, 0, 1.0, 1.0, 0, 0, None, 0, 0, None) == _lib.OK
+    assert lib.gcnk_gemm_f32(0, 0, 0, 5, 5, None, 5, None, 5, None, 5, None, 0, None, 0, 1.0, 1, None, 0,
+                             None) == _lib.OK
+
+
+def test_plan_and_workspace_sizes():
+    lib = _lib.load()
+    assert lib.gcnk_spmm_plan_chunks(7724, 69130, 32) == (7724 + 69130 + 31) // 32
+    nc = lib.gcnk_spmm_plan_chunks(100, 1000, 16)
+    assert lib.gcnk_spmm_plan_bytes(100, 1000, 16) == 4 * (4 + 2 * (nc + 1) + nc + nc + 2 * nc + nc)
+    assert lib.gcnk_spmm_workspace_bytes(10, 198) == 10 * 200 * 4
+    assert lib.gcnk_gemm_workspace_bytes(200, 8, 7724, 4) == 4 * 200 * 8 * 4
+    assert lib.gcnk_colsum_workspace_bytes(7724, 200) == ((7724 + 63) // 64) * 200 * 4
+    ipc = lib.gcnk_spmm_default_ipc(7724, 69130, 200)
+    assert 4 <= ipc <= 64 and ipc % 4 == 0
+
+
+def test_product_path_refuses_cpu_tensors(r8):
+    """No silent CPU fallback: CPU inputs raise instead of computing."""
+    import torch
+    from graph_convolutional_networks_for_text_classification_amd import GCN
+    torch.manual_seed(0)
+    m = GCN(nfeat=r8["nfeat"], nhid=200, nclass=r8["nclass"], dropout=0.5)
+    with pytest.raises(RuntimeError, match="ROCm GPU"):
+        m(r8["features"], r8["adj"])

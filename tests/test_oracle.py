@@ -1,0 +1,128 @@
+"""Pin the oracle to the golden vectors recorded from the reference itself.
+
+The reference ships no tests or fixtures for the hot path;
+tests/golden/make_golden.py ran the reference (build_graph.py, trainer.py
+PrepareData, layer.py GCN, trainer.py TopicGCNTrainer) in the build
+container and stored its outputs.  These CPU tests check that the oracle
+restatement reproduces them bit for bit, so the GPU parity tests can use the
+oracle on inputs the goldens do not cover.
+"""
+import hashlib
+
+import numpy as np
+import pytest
+import torch
+
+from oracle import csr_ref, gcn_ref
+
+
+def _sha(t):
+    return hashlib.sha256(t.detach().contiguous().numpy().tobytes()).hexdigest()
+
+
+def test_fixture_shapes(r8, golden_meta):
+    g = golden_meta["graph"]
+    assert r8["adj"]._nnz() == g["adj_nnz"] == 69130
+    assert r8["features"]._nnz() == g["x_nnz"] == 756850
+    assert r8["nfeat"] == g["nfeat"] and r8["nclass"] == g["nclass"] == 8
+    assert r8["nodes"] == g["nodes"] == 7724
+    assert not r8["adj"].is_coalesced()
+
+
+def test_normalisation_recipe_bit_exact(r8):
+    """utils.py:185-213 restated: same values AND same (column-major) order."""
+    import gcn_amd  # noqa: F401
+    from graph_convolutional_networks_for_text_classification_amd import datasets
+    rr, cc, vv = datasets.sym_normalize(r8["a_rows"], r8["a_cols"], r8["a_vals"], r8["nodes"])
+    ai = r8["adj"]._indices().numpy()
+    av = r8["adj"]._values().numpy()
+    assert np.array_equal(rr, ai[0]) and np.array_equal(cc, ai[1])
+    assert np.array_equal(vv.view(np.uint32), av.view(np.uint32))
+
+
+def test_oracle_normalize_matches_reference_values(r8):
+    r, c, v = gcn_ref.normalize_adj_coo(r8["a_rows"], r8["a_cols"], r8["a_vals"], r8["nodes"])
+    ref = r8["adj"].coalesce()
+    ri = ref.indices().numpy()
+    assert np.array_equal(r, ri[0]) and np.array_equal(c, ri[1])
+    assert np.array_equal(v.view(np.uint32), ref.values().numpy().view(np.uint32))
+
+
+@pytest.mark.parametrize("seed", [50494, 99346, 0])
+def test_oracle_init_and_eval_logits_bit_exact(r8, golden_meta, golden_logits, seed):
+    torch.manual_seed(seed)
+    m = gcn_ref.RefGCN(nfeat=r8["nfeat"], nhid=200, nclass=r8["nclass"], dropout=0.5)
+    shas = golden_meta["logits"][str(seed)]["params_sha256"]
+    for k, v in m.state_dict().items():
+        assert _sha(v) == shas[k], k
+    m.eval()
+    with torch.no_grad():
+        lg = m(r8["features"], r8["adj"]).numpy()
+    assert np.array_equal(lg.view(np.uint32), golden_logits[f"eval_{seed}"].view(np.uint32))
+
+
+def test_oracle_train_forward_backward(r8, golden_meta, golden_logits):
+    meta = golden_meta["logits"]["train_grad"]
+    seed = meta["seed"]
+    torch.manual_seed(seed)
+    m = gcn_ref.RefGCN(nfeat=r8["nfeat"], nhid=200, nclass=r8["nclass"], dropout=0.5)
+    m.train()
+    lg = m(r8["features"], r8["adj"])
+    assert np.array_equal(lg.detach().numpy(), golden_logits[f"train_{seed}"])
+    tl = torch.tensor(r8["train_lst"][: meta["n_train_rows"]], dtype=torch.long)
+    loss = torch.nn.CrossEntropyLoss()(lg[tl], torch.tensor(r8["target"])[tl])
+    assert float(loss) == meta["loss"]
+    loss.backward()
+    assert np.array_equal(m.gc2.weight.grad.numpy(), golden_logits["grad_gc2.weight"])
+    assert np.array_equal(m.gc1.bias.grad.numpy(), golden_logits["grad_gc1.bias"])
+    assert np.array_equal(m.gc1.weight.grad[:64].numpy(), golden_logits["grad_gc1.weight_rows0_64"])
+
+
+def test_tiny_known_answer_cases(golden_meta):
+    for case in golden_meta["tiny_cases"]:
+        n = case["n"]
+        r, c, v = gcn_ref.normalize_adj_coo(case["A_rows"], case["A_cols"], case["A_vals"], n)
+        ref_adj = torch.sparse_coo_tensor(torch.tensor([case["adj_rows"], case["adj_cols"]]),
+                                          torch.tensor(case["adj_vals"], dtype=torch.float32), (n, n)).coalesce()
+        assert np.array_equal(v, ref_adj.values().numpy()), case["name"]
+        X = np.asarray(case["X"], np.float32)
+        torch.manual_seed(case["init_seed"])
+        m = gcn_ref.RefGCN(case["nfeat"], case["nhid"], case["nclass"], 0.5)
+        assert np.array_equal(m.gc1.weight.detach().numpy(), np.asarray(case["W1"], np.float32))
+        m.eval()
+        adj = torch.sparse_coo_tensor(torch.tensor([case["adj_rows"], case["adj_cols"]]),
+                                      torch.tensor(case["adj_vals"], dtype=torch.float32), (n, n))
+        xs = torch.from_numpy(X).to_sparse()
+        with torch.no_grad():
+            lg = m(xs, adj).numpy()
+        np.testing.assert_allclose(lg, np.asarray(case["logits_eval"], np.float32), rtol=0, atol=1e-6)
+
+
+def test_csr_ref_against_scipy_and_transpose():
+    rng = np.random.default_rng(0)
+    M, K, F = 57, 41, 9
+    rows = rng.integers(0, M, 400)
+    cols = rng.integers(0, K, 400)
+    vals = rng.standard_normal(400)
+    rp, ci, v = csr_ref.coo_to_csr(rows, cols, vals, (M, K))
+    dense = np.zeros((M, K))
+    np.add.at(dense, (rows, cols), vals)
+    B = rng.standard_normal((K, F))
+    np.testing.assert_allclose(csr_ref.spmm_csr(rp, ci, v, B), dense @ B, atol=1e-12)
+    rpt, cit, vt = csr_ref.csr_transpose(rp, ci, v, (M, K))
+    Bt = rng.standard_normal((M, F))
+    np.testing.assert_allclose(csr_ref.spmm_csr(rpt, cit, vt, Bt), dense.T @ Bt, atol=1e-12)
+
+
+@pytest.mark.slow
+def test_oracle_training_run_matches_reference(r8, golden_meta):
+    """trainer.py:349-406 restated: the whole R8 run for one seed reproduces
+    the reference's per-epoch losses and test accuracy exactly (CPU)."""
+    run = golden_meta["train_runs"]["50494"]
+    torch.set_num_threads(8)
+    hist, test, _ = gcn_ref.train_run(
+        gcn_ref.RefGCN, r8["features"], r8["adj"], r8["target"], run["train_idx"], run["val_idx"],
+        r8["test_lst"], r8["nfeat"], r8["nclass"], 50494)
+    assert len(hist) == run["epochs"]
+    assert [h["train_loss"] for h in hist] == [h["train_loss"] for h in run["history"]]
+    assert test["acc"] == run["test"]["acc"]

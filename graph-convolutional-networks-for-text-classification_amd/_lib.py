@@ -26,17 +26,16 @@ _vp, _i32, _i64, _u64, _f32 = ctypes.c_void_p, ctypes.c_int32, ctypes.c_int64, c
 # name -> (restype, argtypes); every symbol include/gcnk.h declares
 SIGNATURES = {
     "gcnk_abi_version": (ctypes.c_int, []),
+    "gcnk_debug_set_stamps": (None, [_vp]),
     "gcnk_last_error": (ctypes.c_char_p, []),
-    "gcnk_spmm_default_ipc": (_i32, [_i32, _i64, _i32]),
-    "gcnk_spmm_plan_chunks": (_i64, [_i32, _i64, _i32]),
-    "gcnk_spmm_plan_bytes": (_i64, [_i32, _i64, _i32]),
-    "gcnk_spmm_plan_build": (ctypes.c_int, [_vp, _i32, _i64, _i32, _vp, _i64, _vp]),
+    "gcnk_spmm_groups": (_i32, [_i32, _i32]),
+    "gcnk_spmm_default_ipc": (_i32, [_i32, _i64, _i32, _i32]),
+    "gcnk_spmm_plan_bytes": (_i64, [_vp, _vp, _i32, _i32, _i64, _i32, _i32, _f32, _vp]),
+    "gcnk_spmm_plan_build": (ctypes.c_int, [_vp, _vp, _vp, _i32, _i32, _i64, _i32, _i32, _f32, _vp, _i64, _vp]),
     "gcnk_spmm_plan_query": (ctypes.c_int, [_vp, _vp, _vp]),
-    "gcnk_spmm_workspace_bytes": (_i64, [_i32, _i32]),
+    "gcnk_spmm_workspace_bytes": (_i64, [_vp, _i32]),
     "gcnk_spmm_csr_f32": (ctypes.c_int, [
-        _vp, _vp, _vp,            # rowptr, colind, val
-        _i32, _i32, _i64,         # M, K, nnz
-        _vp, _i32, _i32,          # plan, ipc, nfix
+        _vp, _vp,                 # plan (device), plan header (host, 16 words)
         _vp, _i64, _i32,          # B, ldb, F
         _vp, _i64,                # C, ldc
         _vp, _i32,                # bias, epilogue

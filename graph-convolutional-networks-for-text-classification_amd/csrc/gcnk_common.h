@@ -31,23 +31,28 @@ struct Coord {
   int32_t y;  // nonzero index (merge-path: nonzeros consumed)
 };
 
-// Plan header words (see gcnk.h).
-constexpr int kPlanHeader = 4;
+// Plan header words (see gcnk.h): nslots, nfix, ipc, nchunks, G, nsuper, 0, 0.
+constexpr int kPlanHeader = 8;
 
 __host__ __device__ inline int64_t plan_nchunks(int32_t M, int64_t nnz, int32_t ipc) {
   return ((int64_t)M + nnz + ipc - 1) / ipc;
 }
 
-// Plan section offsets in int32 words.
+// Plan section offsets in int32 words.  Chunks (ipc path items each) are the
+// per-group work units; a "super-chunk" is the G consecutive chunks one
+// workgroup owns.  Split-row partial slots and the fix-up list are kept per
+// super-chunk (rows split inside one workgroup are combined in LDS).
 struct PlanLayout {
-  int64_t nchunks, coords, head, tail, fix, total;
-  __host__ __device__ PlanLayout(int64_t nc) {
+  int64_t nchunks, nsuper, coords, head, tail, fix, fix_index, total;
+  __host__ __device__ PlanLayout(int64_t nc, int32_t G) {
     nchunks = nc;
+    nsuper = (nc + G - 1) / G;
     coords = kPlanHeader;
     head = coords + 2 * (nc + 1);
-    tail = head + nc;
-    fix = tail + nc;
-    total = fix + 2 * nc;
+    tail = head + nsuper;
+    fix = tail + nsuper;
+    fix_index = fix + 2 * nsuper;
+    total = fix_index + nsuper;
   }
 };
 
@@ -62,7 +67,16 @@ struct Epi {
   uint32_t seed_lo, seed_hi;
   uint64_t offset;
   int32_t code;
+  unsigned long long* stamps;  // debug timeline (gcnk_debug_set_stamps), normally null
 };
+
+// Debug timeline: 4 x s_memrealtime (100 MHz) per workgroup, written by thread 0.
+__device__ __forceinline__ void stamp(const Epi& e, int k) {
+  if (e.stamps && threadIdx.x == 0) {
+    const unsigned long long t = __builtin_amdgcn_s_memrealtime();
+    e.stamps[4 * ((unsigned long long)blockIdx.y * gridDim.x + blockIdx.x) + k] = t;
+  }
+}
 
 // Counter-based hash RNG (lowbias32-style avalanche, two rounds keyed by seed).
 __device__ __forceinline__ uint32_t mix32(uint32_t x) {
@@ -78,9 +92,10 @@ __device__ __forceinline__ float hash_uniform(uint32_t seed_lo, uint32_t seed_hi
   return (float)(h >> 8) * (1.0f / 16777216.0f);
 }
 
-__device__ __forceinline__ float apply_epi(const Epi& e, float acc, int64_t row, int64_t col) {
+// `b` is bias[col] (0 when there is no bias), preloaded by the caller.
+__device__ __forceinline__ float apply_epi(const Epi& e, float acc, float b, int64_t row, int64_t col) {
   if (e.code == GCNK_EPI_NONE) return acc;
-  float v = acc + (e.bias ? e.bias[col] : 0.0f);
+  float v = acc + b;
   if (e.code == GCNK_EPI_BIAS) return v;
   v = v > 0.0f ? v : 0.0f;
   if (e.code == GCNK_EPI_BIAS_RELU) return v;

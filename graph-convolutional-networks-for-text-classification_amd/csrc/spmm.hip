@@ -3,29 +3,51 @@
 // Replaces th.spmm(adj, support) (reference layer.py:106) and th.spmm(X, W)
 // with sparse X (layer.py:102), plus their autograd products A^T g / X^T g.
 //
-// Schedule: merge-path over the sequence of (row ends + nonzeros) cut into
-// chunks of `ipc` items (built once per sparsity pattern by
-// gcnk_spmm_plan_build).  A boundary landing inside a row shorter than `ipc`
-// is snapped back to the start of that row, so light rows are never split;
-// heavy rows (e.g. the 50 topic rows of R8, up to 1.8k nonzeros vs a median
-// of 5) are split over several chunks and summed in fixed chunk order by a
-// fix-up pass: no float atomics, bitwise reproducible.
+// A sparse operand is converted once (gcnk_spmm_plan_build) into a hybrid
+// plan that splits its rows between two kernels writing disjoint rows of C:
 //
-// Kernel shape: 256-thread workgroups.  A workgroup owns G = 256/LPR
-// consecutive chunks; it stages their row pointers, column indices, values
-// and a per-nonzero row id in LDS with coalesced loads, then each group of
-// LPR lanes walks one chunk: batches of U nonzeros are gathered together
-// (U*VPL independent 16-B loads in flight per lane), accumulated in fp32
-// registers and flushed when the row changes, with bias/ReLU/dropout fused
-// into the store.  Each lane owns VEC-wide column vectors interleaved by LPR,
-// so one load instruction of a group covers LPR*VEC contiguous floats of a
-// B row (coalesced).  F wider than LPR*VPL*VEC is tiled over gridDim.y.
+//  * dense blocks -> spmm_tile_kernel (fp32 MFMA).  Rows are grouped in
+//    blocks of RB = 64; a block whose nonzeros fill at least `dense_threshold`
+//    of its condensed column set (the distinct columns its rows use) is stored
+//    densely over those columns, in MFMA fragment order, in chunks of KC = 64
+//    columns.  One workgroup per chunk stages the chunk's 64 B rows in LDS
+//    ONCE and reuses them for all 64 rows (R8's X: every document row uses
+//    the same 50 topic columns; the 50 topic rows are fully dense), instead
+//    of gathering a B row per nonzero.  Blocks with several chunks write
+//    partial slabs that spmm_tile_reduce_kernel sums in chunk order.
+//
+//  * the remaining rows -> spmm_path_kernel (gathers).  The nonzeros in row
+//    order, each row closed by an end-of-row marker (col = -1, payload = row)
+//    form one int2 item stream cut into workgroup windows of W = G*ipc items;
+//    a row of at most W/2 items that would straddle a window is pushed to the
+//    next with pad items (col = -2), so only heavy rows cross windows and the
+//    kernel needs no search: window w is items [w*W, (w+1)*W), loaded in one
+//    coalesced pass, then the B-row gathers issue.  Groups of LPR lanes walk
+//    ipc items each, gathering U nonzeros at a time (U*VPL independent 16-B
+//    loads in flight per lane) and flushing a row at its marker with
+//    bias/ReLU/dropout fused into the store.  Lanes own VEC-wide column
+//    vectors interleaved by LPR (one load instruction of a group covers
+//    LPR*VEC contiguous floats of a B row).  Rows split between the groups of
+//    a window meet in LDS; heavy rows crossing windows leave one partial per
+//    window that spmm_fixup_kernel sums in path order.
+//
+// Every sum has a fixed order (no float atomics): results are bitwise
+// reproducible run to run.
 #include "gcnk_common.h"
 
+#include <algorithm>
 #include <climits>
+#include <vector>
 
 namespace gcnk {
 namespace {
+
+constexpr int32_t kMarker = -1;  // end of row; .y = row index
+constexpr int32_t kPad = -2;     // no-op
+constexpr int32_t kMagic = 0x474e4b33;  // "GNK3"
+constexpr int kRB = 64;          // tile rows per dense block (4 waves x 16)
+constexpr int kKC = 64;          // condensed columns per tile chunk (16 MFMA k-steps)
+constexpr int kMaxNT = 14;       // 16-column MFMA n-tiles per tile workgroup (B tile <= 57 KB LDS)
 
 template <int VEC>
 struct Vec;
@@ -45,12 +67,12 @@ struct Vec<4> {
   static __device__ __forceinline__ void add(T& acc, const T& b) {
     acc.x += b.x; acc.y += b.y; acc.z += b.z; acc.w += b.w;
   }
-  static __device__ __forceinline__ T epi(const Epi& e, const T& a, int64_t row, int64_t col) {
+  static __device__ __forceinline__ T epi(const Epi& e, const T& a, const T& b, int64_t row, int64_t col) {
     T r;
-    r.x = apply_epi(e, a.x, row, col + 0);
-    r.y = apply_epi(e, a.y, row, col + 1);
-    r.z = apply_epi(e, a.z, row, col + 2);
-    r.w = apply_epi(e, a.w, row, col + 3);
+    r.x = apply_epi(e, a.x, b.x, row, col + 0);
+    r.y = apply_epi(e, a.y, b.y, row, col + 1);
+    r.z = apply_epi(e, a.z, b.z, row, col + 2);
+    r.w = apply_epi(e, a.w, b.w, row, col + 3);
     return r;
   }
 };
@@ -63,304 +85,390 @@ struct Vec<1> {
   static __device__ __forceinline__ void store(float* p, const T& v) { *p = v; }
   static __device__ __forceinline__ void fma(T& acc, float a, const T& b) { acc = fmaf(a, b, acc); }
   static __device__ __forceinline__ void add(T& acc, const T& b) { acc += b; }
-  static __device__ __forceinline__ T epi(const Epi& e, const T& a, int64_t row, int64_t col) {
-    return apply_epi(e, a, row, col);
+  static __device__ __forceinline__ T epi(const Epi& e, const T& a, const T& b, int64_t row, int64_t col) {
+    return apply_epi(e, a, b, row, col);
   }
 };
 
 // ---------------------------------------------------------------------------
-// Plan construction (one-time per sparsity pattern and ipc).
-
-// Merge-path split point of diagonal d over A = row ends (rowptr[1..M]) and
-// B = nonzero indices; then snap to the row start when the row is light.
-__global__ void plan_coords_kernel(const int32_t* __restrict__ rowptr, int32_t M, int64_t nnz,
-                                   int32_t ipc, int64_t nchunks, Coord* __restrict__ coords) {
-  const int64_t t = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-  if (t > nchunks) return;
-  const int64_t total = (int64_t)M + nnz;
-  const int64_t d = min(t * (int64_t)ipc, total);
-  int64_t lo = max<int64_t>(0, d - nnz), hi = min<int64_t>(d, M);
-  while (lo < hi) {
-    const int64_t mid = (lo + hi) >> 1;
-    if ((int64_t)rowptr[mid + 1] <= d - mid - 1) lo = mid + 1;
-    else hi = mid;
+// Plan layout (int32 words).  Header (16 words, see gcnk.h):
+//   0 magic  1 M  2 K  3 groups  4 ipc  5 W  6 nwin  7 nfix  8 nslots
+//   9 ntile  10 nred  11 nslabs  12 KC  13 RB  14 heavy  15 0
+struct Layout {
+  int64_t nwin, W, nfix, ntile, nred;
+  int64_t items, head, tail, fix, tdesc, tcols, tfrag, red, total;
+  __host__ __device__ explicit Layout(const int32_t* h) {
+    nwin = h[6]; W = h[5]; nfix = h[7]; ntile = h[9]; nred = h[10];
+    items = 16;
+    head = items + 2 * nwin * W;
+    tail = head + nwin;
+    fix = tail + nwin;
+    tdesc = (fix + 3 * nfix + 3) & ~3LL;
+    tcols = tdesc + 4 * ntile;
+    tfrag = (tcols + (int64_t)kKC * ntile + 3) & ~3LL;
+    red = tfrag + (int64_t)kRB * kKC * ntile;
+    total = red + 4 * nred;
   }
-  int32_t x = (int32_t)lo;
-  int32_t y = (int32_t)(d - lo);
-  if (x < M && y > rowptr[x] && (rowptr[x + 1] - rowptr[x]) < ipc) y = rowptr[x];
-  coords[t] = Coord{x, y};
+};
+
+// ---------------------------------------------------------------------------
+// Plan construction kernels.
+__global__ void fill_pad_kernel(int2* __restrict__ items, int64_t n) {
+  const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i < n) items[i] = make_int2(kPad, 0);
 }
 
-// Per chunk: does it finish a row it did not start (head partial) and does it
-// start a row it does not finish (tail partial)?  Flags are stored in the
-// slot arrays and turned into slot numbers by plan_scan_kernel.
-__global__ void plan_flags_kernel(const int32_t* __restrict__ rowptr, int32_t M, int64_t nchunks,
-                                  const Coord* __restrict__ coords, int32_t* __restrict__ head,
-                                  int32_t* __restrict__ tail) {
-  const int64_t t = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-  if (t >= nchunks) return;
-  const Coord a = coords[t], b = coords[t + 1];
-  head[t] = (a.x < b.x && a.y > rowptr[a.x]) ? 1 : 0;
-  tail[t] = (b.x < M && b.y > max(a.y, rowptr[b.x])) ? 1 : 0;
-}
-
-// Single-workgroup ordered scan: slots are numbered in chunk order with a
-// chunk's head before its tail, so the partials of one split row occupy a
-// contiguous slot range ending at the finishing chunk's head slot.
-__global__ void __launch_bounds__(1024) plan_scan_kernel(int64_t nchunks, int32_t ipc,
-                                                         int32_t* __restrict__ head,
-                                                         int32_t* __restrict__ tail,
-                                                         int32_t* __restrict__ fix_index,
-                                                         int32_t* __restrict__ header) {
-  __shared__ int32_t s_slot[16], s_fix[16];
-  __shared__ int32_t s_base[2];
-  const int tid = threadIdx.x;
-  const int lane = tid & 63, wv = tid >> 6;
-  if (tid == 0) { s_base[0] = 0; s_base[1] = 0; }
-  __syncthreads();
-  for (int64_t base = 0; base < nchunks; base += 1024) {
-    const int64_t t = base + tid;
-    const int hf = t < nchunks ? head[t] : 0;
-    const int tf = t < nchunks ? tail[t] : 0;
-    int cs = hf + tf, cf = hf;
-    // inclusive wave scans
-    for (int o = 1; o < 64; o <<= 1) {
-      const int a = __shfl_up(cs, o, 64), b = __shfl_up(cf, o, 64);
-      if (lane >= o) { cs += a; cf += b; }
-    }
-    if (lane == 63) { s_slot[wv] = cs; s_fix[wv] = cf; }
-    __syncthreads();
-    int ws = 0, wf = 0, ts = 0, tfx = 0;
-    for (int w = 0; w < 16; ++w) {
-      if (w < wv) { ws += s_slot[w]; wf += s_fix[w]; }
-      ts += s_slot[w]; tfx += s_fix[w];
-    }
-    const int slot0 = s_base[0] + ws + cs - (hf + tf);
-    const int fix0 = s_base[1] + wf + cf - hf;
-    if (t < nchunks) {
-      head[t] = hf ? slot0 : -1;
-      tail[t] = tf ? slot0 + hf : -1;
-      fix_index[t] = hf ? fix0 : -1;
-    }
-    __syncthreads();
-    if (tid == 0) { s_base[0] += ts; s_base[1] += tfx; }
-    __syncthreads();
-  }
-  if (tid == 0) {
-    header[0] = s_base[0];
-    header[1] = s_base[1];
-    header[2] = ipc;
-    header[3] = (int32_t)(nchunks & 0x7fffffff);
-  }
-}
-
-// Fix-up list entry i = (finishing chunk t, first partial slot of the row).
-__global__ void plan_fix_kernel(const int32_t* __restrict__ rowptr, int64_t nchunks,
-                                const Coord* __restrict__ coords, const int32_t* __restrict__ head,
-                                const int32_t* __restrict__ tail, const int32_t* __restrict__ fix_index,
-                                int32_t* __restrict__ fix) {
-  const int64_t t = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-  if (t >= nchunks || fix_index[t] < 0) return;
-  const int32_t r = coords[t].x;
-  const int64_t dr = (int64_t)r + rowptr[r];  // diagonal where row r starts
-  // largest u <= t with diag(coords[u]) <= dr
-  int64_t lo = 0, hi = t;
-  while (lo < hi) {
-    const int64_t mid = (lo + hi + 1) >> 1;
-    const Coord c = coords[mid];
-    if ((int64_t)c.x + c.y <= dr) lo = mid;
-    else hi = mid - 1;
-  }
-  int32_t sb = head[t];
-  for (int64_t w = lo; w < t; ++w) {
-    if (tail[w] >= 0) { sb = tail[w]; break; }
-  }
-  const int32_t i = fix_index[t];
-  fix[2 * i] = (int32_t)t;
-  fix[2 * i + 1] = sb;
+// nonzero k of row r goes to start[r] + (k - rowptr[r]); the marker to start[r] + deg(r);
+// rows handled by the tile path have start[r] < 0 and no items.
+__global__ void scatter_items_kernel(const int32_t* __restrict__ rowptr, const int32_t* __restrict__ colind,
+                                     const float* __restrict__ val, int32_t M, const int32_t* __restrict__ start,
+                                     int2* __restrict__ items) {
+  const int32_t r = blockIdx.x * (blockDim.x / 64) + (threadIdx.x >> 6);
+  if (r >= M) return;
+  const int32_t s = start[r];
+  if (s < 0) return;
+  const int lane = threadIdx.x & 63;
+  const int32_t b = rowptr[r], e = rowptr[r + 1];
+  for (int32_t k = b + lane; k < e; k += 64) items[s + (k - b)] = make_int2(colind[k], __float_as_int(val[k]));
+  if (lane == 0) items[s + (e - b)] = make_int2(kMarker, r);
 }
 
 // ---------------------------------------------------------------------------
-// Main SpMM kernel.
-template <int LPR, int VPL, int VEC, int U>
-__global__ void __launch_bounds__(256)
-spmm_merge_kernel(const int32_t* __restrict__ rowptr, const int32_t* __restrict__ colind,
-                  const float* __restrict__ val, int32_t M, const int32_t* __restrict__ plan,
-                  int64_t nchunks, int32_t ipc, const float* __restrict__ B, int64_t ldb, int32_t F,
-                  float* __restrict__ C, int64_t ldc, Epi epi, float* __restrict__ part,
-                  int64_t part_ld) {
+// Path kernel (gathers).
+template <int BLOCK, int LPR, int VPL, int VEC, int U>
+__global__ void __launch_bounds__(BLOCK)
+spmm_path_kernel(const int2* __restrict__ items, const int32_t* __restrict__ head_slot,
+                 const int32_t* __restrict__ tail_slot, int32_t ipc, const float* __restrict__ B, int64_t ldb,
+                 int32_t F, float* __restrict__ C, int64_t ldc, Epi epi, float* __restrict__ part,
+                 int64_t part_ld) {
   using V = Vec<VEC>;
   using T = typename V::T;
-  constexpr int G = 256 / LPR;
+  constexpr int G = BLOCK / LPR;
+  constexpr int FT = LPR * VPL * VEC;  // columns per tile
   extern __shared__ __attribute__((aligned(16))) int32_t smem[];
 
-  const PlanLayout L(nchunks);
-  const Coord* __restrict__ coords = reinterpret_cast<const Coord*>(plan + L.coords);
-  const int32_t* __restrict__ head_slot = plan + L.head;
-  const int32_t* __restrict__ tail_slot = plan + L.tail;
-
-  const int rows_cap = G * ipc + 2;
-  const int nnz_cap = G * ipc + ipc;
-  int32_t* s_rp = smem;
-  int32_t* s_col = s_rp + rows_cap;
-  float* s_val = reinterpret_cast<float*>(s_col + nnz_cap);
-  int32_t* s_row = reinterpret_cast<int32_t*>(s_val + nnz_cap);
+  const int W = G * ipc;
+  // LDS: item[W + 1] (index 0 = the item before the window) | per-group words | H, T partials
+  int2* s_item = reinterpret_cast<int2*>(smem);
+  int32_t* s_meta = smem + 2 * ((W + 2 + 1) & ~1);  // 4 words per group: has_marker, head_partial, tail, head_row
+  float* s_H = reinterpret_cast<float*>(s_meta + ((4 * G + 3) & ~3));
+  float* s_T = s_H + G * FT;
 
   const int tid = threadIdx.x;
-  const int64_t t0 = (int64_t)blockIdx.x * G;
-  const int64_t tE = min<int64_t>(t0 + G, nchunks);
-  const Coord c0 = coords[t0], c1 = coords[tE];
-  const int32_t X0 = c0.x, Y0 = c0.y;
-  const int nrows = min(c1.x + 1, M) - X0 + 1;
-  const int nnzs = c1.y - Y0;
+  const int64_t w = blockIdx.x;
+  const int64_t base = w * W;
 
-  // ---- stage the workgroup's slice of the CSR in LDS (coalesced)
-  for (int i = tid; i < nrows; i += 256) s_rp[i] = rowptr[X0 + i];
-  for (int i = tid; i < nnzs; i += 256) {
-    s_col[i] = colind[Y0 + i];
-    s_val[i] = val[Y0 + i];
-  }
+  // ---- one coalesced pass: the window's items (+ the item before it)
+  for (int i = tid; i < W; i += BLOCK) s_item[1 + i] = items[base + i];
+  if (tid == 0) s_item[0] = w > 0 ? items[base - 1] : make_int2(kMarker, -1);
+  stamp(epi, 0);
+  const int32_t hslot = head_slot[w];
+  const int32_t tslot = tail_slot[w];
   __syncthreads();
-  for (int i = tid; i < nnzs; i += 256) {
-    const int32_t k = Y0 + i;
-    int lo = 0, hi = nrows - 1;  // s_rp[lo] <= k < s_rp[hi]
-    while (hi - lo > 1) {
-      const int mid = (lo + hi) >> 1;
-      if (s_rp[mid] <= k) lo = mid;
-      else hi = mid;
-    }
-    s_row[i] = lo;
-  }
-  __syncthreads();
+  stamp(epi, 1);
 
-  // ---- one chunk per group of LPR lanes
   const int g = tid / LPR;
   const int lg = tid % LPR;
-  const int64_t t = t0 + g;
-  if (t >= nchunks) return;
-  const Coord a = coords[t], b = coords[t + 1];
-  const int32_t x0 = a.x, y0 = a.y, x1 = b.x, y1 = b.y;
-
-  const int64_t col_base = (int64_t)blockIdx.y * (LPR * VPL * VEC);
+  const int64_t col_base = (int64_t)blockIdx.y * FT;
   int64_t colv[VPL];
   bool colok[VPL];
+  T bv[VPL];  // bias of this lane's columns, loaded once
 #pragma unroll
   for (int v = 0; v < VPL; ++v) {
     colv[v] = col_base + (int64_t)(v * LPR + lg) * VEC;
     colok[v] = colv[v] < F;
+    bv[v] = (epi.bias && colok[v]) ? V::load(epi.bias + colv[v]) : V::zero();
   }
+  float* myH = s_H + g * FT;
+  float* myT = s_T + g * FT;
 
-  const bool head_partial = (x0 < x1) && (y0 > s_rp[x0 - X0]);
-  const int32_t hslot = head_partial ? head_slot[t] : -1;
+  const int i0 = 1 + g * ipc;                       // first item of this group's chunk in s_item
+  const bool head_partial = s_item[i0 - 1].x >= 0;  // the chunk starts inside a row
+  bool has_marker = false;
+  int32_t head_row = -1;
 
   T acc[VPL];
 #pragma unroll
   for (int v = 0; v < VPL; ++v) acc[v] = V::zero();
 
-  int32_t cur = x0;
-  auto flush = [&](int32_t r) {
-    if (r == x0 && head_partial) {
-      float* dst = part + (int64_t)hslot * part_ld;
-#pragma unroll
-      for (int v = 0; v < VPL; ++v)
-        if (colok[v]) V::store(dst + colv[v], acc[v]);
-    } else {
-      float* dst = C + (int64_t)r * ldc;
-#pragma unroll
-      for (int v = 0; v < VPL; ++v)
-        if (colok[v]) V::store(dst + colv[v], V::epi(epi, acc[v], r, colv[v]));
-    }
-#pragma unroll
-    for (int v = 0; v < VPL; ++v) acc[v] = V::zero();
-  };
-
-  for (int32_t base = y0; base < y1; base += U) {
+  for (int k0 = 0; k0 < ipc; k0 += U) {
     T gv[U][VPL];
-    float vv[U];
-    int32_t rr[U];
+    int2 it[U];
 #pragma unroll
     for (int u = 0; u < U; ++u) {
-      const int32_t k = base + u;
-      const bool ok = k < y1;
-      const int li = k - Y0;
-      const int32_t c = ok ? s_col[li] : 0;
-      vv[u] = ok ? s_val[li] : 0.f;
-      rr[u] = ok ? s_row[li] + X0 : INT_MAX;
-      const float* brow = B + (int64_t)c * ldb;
+      it[u] = (k0 + u < ipc) ? s_item[i0 + k0 + u] : make_int2(kPad, 0);
+      const float* brow = B + (int64_t)(it[u].x >= 0 ? it[u].x : 0) * ldb;
 #pragma unroll
-      for (int v = 0; v < VPL; ++v) gv[u][v] = (ok && colok[v]) ? V::load(brow + colv[v]) : V::zero();
+      for (int v = 0; v < VPL; ++v)
+        gv[u][v] = (it[u].x >= 0 && colok[v]) ? V::load(brow + colv[v]) : V::zero();
     }
 #pragma unroll
     for (int u = 0; u < U; ++u) {
-      if (rr[u] != INT_MAX) {
-        while (cur < rr[u]) {
-          flush(cur);
-          ++cur;
-        }
+      if (it[u].x >= 0) {
+        const float a = __int_as_float(it[u].y);
 #pragma unroll
-        for (int v = 0; v < VPL; ++v) V::fma(acc[v], vv[u], gv[u][v]);
+        for (int v = 0; v < VPL; ++v) V::fma(acc[v], a, gv[u][v]);
+      } else if (it[u].x == kMarker) {
+        const int32_t r = it[u].y;
+        if (!has_marker && head_partial) {
+#pragma unroll
+          for (int v = 0; v < VPL; ++v) V::store(myH + (v * LPR + lg) * VEC, acc[v]);
+          head_row = r;
+        } else {
+          float* dst = C + (int64_t)r * ldc;
+#pragma unroll
+          for (int v = 0; v < VPL; ++v)
+            if (colok[v]) V::store(dst + colv[v], V::epi(epi, acc[v], bv[v], r, colv[v]));
+        }
+        has_marker = true;
+#pragma unroll
+        for (int v = 0; v < VPL; ++v) acc[v] = V::zero();
       }
     }
   }
-  while (cur < x1) {
-    flush(cur);
-    ++cur;
-  }
-  if (x1 < M && y1 > max(y0, s_rp[x1 - X0])) {
-    float* dst = part + (int64_t)tail_slot[t] * part_ld;
+  const bool tail = s_item[i0 + ipc - 1].x >= 0;  // the chunk ends inside a row
+  if (tail) {
 #pragma unroll
-    for (int v = 0; v < VPL; ++v)
-      if (colok[v]) V::store(dst + colv[v], acc[v]);
+    for (int v = 0; v < VPL; ++v) V::store(myT + (v * LPR + lg) * VEC, acc[v]);
+  }
+  stamp(epi, 2);
+  if (lg == 0) {
+    s_meta[4 * g + 0] = has_marker;
+    s_meta[4 * g + 1] = head_partial;
+    s_meta[4 * g + 2] = tail;
+    s_meta[4 * g + 3] = head_row;
+  }
+  __syncthreads();
+
+  // ---- rows split between groups of this window: the marker's group adds, in group order,
+  //      T of the nearest earlier group holding a marker (the row's start) and T of the
+  //      marker-free groups in between, then its own H.
+  if (head_row >= 0) {
+    int j = g - 1;
+    while (j >= 0 && !s_meta[4 * j + 0]) --j;
+    // the row starts in group j's tail if j ends inside a row, else at group j+1
+    const int jf = (j >= 0 && s_meta[4 * j + 2]) ? j : j + 1;
+    const bool from_before = j < 0 && s_meta[1];  // the row started in an earlier window
+#pragma unroll
+    for (int v = 0; v < VPL; ++v) {
+      const int off = (v * LPR + lg) * VEC;
+      T s = V::zero();
+      for (int q = jf; q < g; ++q) V::add(s, V::load(s_T + q * FT + off));
+      V::add(s, V::load(myH + off));
+      if (!colok[v]) continue;
+      if (from_before) V::store(part + (int64_t)hslot * part_ld + colv[v], s);
+      else V::store(C + (int64_t)head_row * ldc + colv[v], V::epi(epi, s, bv[v], head_row, colv[v]));
+    }
+  }
+  // ---- a heavy row leaving the window: partial of its part in this window
+  if (g == G - 1 && tail) {
+    int j = g;
+    while (j >= 0 && !s_meta[4 * j + 0]) --j;
+    const int jf = (j >= 0 && s_meta[4 * j + 2]) ? j : j + 1;
+#pragma unroll
+    for (int v = 0; v < VPL; ++v) {
+      const int off = (v * LPR + lg) * VEC;
+      T s = V::zero();
+      for (int q = jf; q <= g; ++q) V::add(s, V::load(s_T + q * FT + off));
+      if (colok[v]) V::store(part + (int64_t)tslot * part_ld + colv[v], s);
+    }
+  }
+  stamp(epi, 3);
+}
+
+// Sum the contiguous partial slots of every heavy row crossing windows, in
+// slot (= path) order, apply the epilogue, store the row.  One workgroup per
+// row: P = 256/LPR slot lanes take slots strided by P, then the P partial
+// sums are added in lane order through LDS.
+template <int LPR, int VPL, int VEC>
+__global__ void __launch_bounds__(256)
+spmm_fixup_kernel(const int32_t* __restrict__ fix, int32_t nfix, int32_t F, const float* __restrict__ part,
+                  int64_t part_ld, float* __restrict__ C, int64_t ldc, Epi epi) {
+  using V = Vec<VEC>;
+  using T = typename V::T;
+  constexpr int P = 256 / LPR;
+  constexpr int FT = LPR * VPL * VEC;
+  __shared__ __attribute__((aligned(16))) float s_acc[P * FT];
+  const int64_t i = blockIdx.x;
+  if (i >= nfix) return;
+  const int p = threadIdx.x / LPR;
+  const int lg = threadIdx.x % LPR;
+  const int32_t r = fix[3 * i], sb = fix[3 * i + 1], se = fix[3 * i + 2];
+  const int64_t col_base = (int64_t)blockIdx.y * FT;
+#pragma unroll
+  for (int v = 0; v < VPL; ++v) {
+    const int off = (v * LPR + lg) * VEC;
+    const int64_t col = col_base + off;
+    T acc = V::zero();
+    if (col < F) {
+      int32_t s = sb + p;
+      for (; s + 3 * P <= se; s += 4 * P) {
+        const T p0 = V::load(part + (int64_t)(s + 0 * P) * part_ld + col);
+        const T p1 = V::load(part + (int64_t)(s + 1 * P) * part_ld + col);
+        const T p2 = V::load(part + (int64_t)(s + 2 * P) * part_ld + col);
+        const T p3 = V::load(part + (int64_t)(s + 3 * P) * part_ld + col);
+        V::add(acc, p0); V::add(acc, p1); V::add(acc, p2); V::add(acc, p3);
+      }
+      for (; s <= se; s += P) V::add(acc, V::load(part + (int64_t)s * part_ld + col));
+    }
+    V::store(s_acc + p * FT + off, acc);
+  }
+  __syncthreads();
+  if (p != 0) return;
+#pragma unroll
+  for (int v = 0; v < VPL; ++v) {
+    const int off = (v * LPR + lg) * VEC;
+    const int64_t col = col_base + off;
+    if (col >= F) continue;
+    T acc = V::load(s_acc + off);
+    for (int q = 1; q < P; ++q) V::add(acc, V::load(s_acc + q * FT + off));
+    const T b = epi.bias ? V::load(epi.bias + col) : V::zero();
+    V::store(C + (int64_t)r * ldc + col, V::epi(epi, acc, b, r, col));
   }
 }
 
-// Sum the contiguous partial slots of every split row in slot (= chunk)
-// order, apply the epilogue, store the row.
-template <int LPR, int VPL, int VEC>
+// ---------------------------------------------------------------------------
+// Tile kernel (dense blocks, fp32 MFMA 16x16x4).  One workgroup = one chunk
+// (64 rows x 64 condensed columns) x NT 16-column n-tiles; wave t owns rows
+// 16t..16t+15.  The chunk's 64 B rows are staged once in LDS lane-major,
+// [k][col & 15][nt] with NT4 = NT rounded up to 4 (+4 pad: 80-B lane rows
+// put a 16-lane ds_read_b128 group on 16 disjoint bank quads), so each lane
+// fetches the NT operands of a k-step with NT4/4 ds_read_b128.  Each wave's
+// A fragments come pre-swizzled from the plan (16 floats per lane,
+// contiguous).  acc[nt] += A(16x4) * B(4x16) over 16 k-steps.
+//   A operand lane l: A[row l&15][k l>>4];  B operand: B[k l>>4][col l&15];
+//   C/D reg j: row (l>>4)*4 + j, col l&15   (gfx950 16x16x4 f32 maps).
+typedef float f32x4 __attribute__((ext_vector_type(4)));
+
+template <bool VEC4, int NT>
 __global__ void __launch_bounds__(256)
-spmm_fixup_kernel(const int32_t* __restrict__ plan, int64_t nchunks, int32_t nfix_host, int32_t F,
-                  const float* __restrict__ part, int64_t part_ld, float* __restrict__ C,
-                  int64_t ldc, Epi epi) {
-  using V = Vec<VEC>;
-  using T = typename V::T;
-  constexpr int G = 256 / LPR;
-  const PlanLayout L(nchunks);
-  const Coord* __restrict__ coords = reinterpret_cast<const Coord*>(plan + L.coords);
-  const int32_t* __restrict__ head_slot = plan + L.head;
-  const int32_t* __restrict__ fix = plan + L.fix;
-  const int32_t nfix = nfix_host >= 0 ? nfix_host : plan[1];
-  const int64_t i = (int64_t)blockIdx.x * G + threadIdx.x / LPR;
-  if (i >= nfix) return;
-  const int lg = threadIdx.x % LPR;
-  const int32_t t = fix[2 * i];
-  const int32_t sb = fix[2 * i + 1];
-  const int32_t se = head_slot[t];
-  const int32_t r = coords[t].x;
-  const int64_t col_base = (int64_t)blockIdx.y * (LPR * VPL * VEC);
-#pragma unroll
-  for (int v = 0; v < VPL; ++v) {
-    const int64_t col = col_base + (int64_t)(v * LPR + lg) * VEC;
-    if (col >= F) continue;
-    T acc = V::zero();
-    int32_t s = sb;
-    for (; s + 3 <= se; s += 4) {
-      const T p0 = V::load(part + (int64_t)(s + 0) * part_ld + col);
-      const T p1 = V::load(part + (int64_t)(s + 1) * part_ld + col);
-      const T p2 = V::load(part + (int64_t)(s + 2) * part_ld + col);
-      const T p3 = V::load(part + (int64_t)(s + 3) * part_ld + col);
-      V::add(acc, p0); V::add(acc, p1); V::add(acc, p2); V::add(acc, p3);
+spmm_tile_kernel(const int4* __restrict__ tdesc, const int32_t* __restrict__ tcols, const float* __restrict__ tfrag,
+                 int32_t F, const float* __restrict__ B, int64_t ldb, float* __restrict__ C, int64_t ldc,
+                 Epi epi, float* __restrict__ slabs, int64_t slab_ld) {
+  constexpr int NT4 = (NT + 3) & ~3;
+  // floats per (k, lane column) row: an odd number of 16-B quads keeps the 16 lanes
+  // of a ds_read_b128 group on disjoint bank quads
+  constexpr int LR = ((NT4 / 4) & 1) ? NT4 : NT4 + 4;
+  constexpr int stride = 16 * LR;       // floats per k
+  __shared__ __attribute__((aligned(16))) float s_B[kKC * stride];
+  __shared__ int32_t s_cols[kKC];
+  const int tid = threadIdx.x;
+  const int lane = tid & 63;
+  const int wave = tid >> 6;
+  const int64_t item = blockIdx.x;
+  const int4 d = tdesc[item];  // row0, nrows, slab (-1: single chunk), 0
+  constexpr int32_t col0 = 0;  // column slices are folded into the B/C pointers by the host
+
+  if (tid < kKC) s_cols[tid] = tcols[item * kKC + tid];
+  // A fragments of this wave: 16 consecutive floats per lane
+  const float4* af = reinterpret_cast<const float4*>(tfrag + ((item * 4 + wave) * 64 + lane) * 16);
+  const float4 a0 = af[0], a1 = af[1], a2 = af[2], a3 = af[3];
+  __syncthreads();
+  // ---- stage the chunk's B rows, columns [0, 16*NT): element (k, n) -> s_B[k][n&15][n>>4]
+  const int nq = NT * 4;  // float4 per staged row
+  for (int q = tid; q < kKC * nq; q += 256) {
+    const int k = q / nq, c4 = q % nq;
+    const int32_t src = s_cols[k];
+    const int64_t col = col0 + c4 * 4;
+    float4 v = make_float4(0.f, 0.f, 0.f, 0.f);
+    if (src >= 0) {
+      const float* bp = B + (int64_t)src * ldb + col;
+      if (VEC4) {
+        if (col < F) v = *reinterpret_cast<const float4*>(bp);
+      } else {
+        if (col + 0 < F) v.x = bp[0];
+        if (col + 1 < F) v.y = bp[1];
+        if (col + 2 < F) v.z = bp[2];
+        if (col + 3 < F) v.w = bp[3];
+      }
     }
-    for (; s <= se; ++s) V::add(acc, V::load(part + (int64_t)s * part_ld + col));
-    V::store(C + (int64_t)r * ldc + col, V::epi(epi, acc, r, col));
+    const int n = c4 * 4, nt = n >> 4, nc0 = n & 15;
+    float* dst = s_B + k * stride + nc0 * LR + nt;
+    dst[0] = v.x;
+    dst[LR] = v.y;
+    dst[2 * LR] = v.z;
+    dst[3 * LR] = v.w;
+  }
+  __syncthreads();
+
+  f32x4 acc[NT];
+#pragma unroll
+  for (int nt = 0; nt < NT; ++nt) acc[nt] = f32x4{0.f, 0.f, 0.f, 0.f};
+  const float a[16] = {a0.x, a0.y, a0.z, a0.w, a1.x, a1.y, a1.z, a1.w,
+                       a2.x, a2.y, a2.z, a2.w, a3.x, a3.y, a3.z, a3.w};
+  const int kr = lane >> 4, nc = lane & 15;
+#pragma unroll
+  for (int s = 0; s < 16; ++s) {
+    const float4* brow = reinterpret_cast<const float4*>(s_B + (4 * s + kr) * stride + nc * LR);
+    float4 bq[NT4 / 4];
+#pragma unroll
+    for (int q = 0; q < NT4 / 4; ++q) bq[q] = brow[q];
+#pragma unroll
+    for (int nt = 0; nt < NT; ++nt) {
+      const float4& b4 = bq[nt >> 2];
+      const float bval = (nt & 3) == 0 ? b4.x : (nt & 3) == 1 ? b4.y : (nt & 3) == 2 ? b4.z : b4.w;
+      acc[nt] = __builtin_amdgcn_mfma_f32_16x16x4f32(a[s], bval, acc[nt], 0, 0, 0);
+    }
+  }
+
+  // ---- output: rows row0 + 16*wave + 4*(lane>>4) + j, cols col0 + 16*nt + (lane&15)
+  const int32_t rbase = d.x + 16 * wave + 4 * (lane >> 4);
+#pragma unroll
+  for (int nt = 0; nt < NT; ++nt) {
+    const int64_t col = col0 + nt * 16 + nc;
+    if (col >= F) continue;
+    const float bcol = (d.z < 0 && epi.bias) ? epi.bias[col] : 0.f;
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      const int32_t rl = 16 * wave + 4 * (lane >> 4) + j;  // row within block
+      if (rl >= d.y) continue;
+      if (d.z < 0) C[(int64_t)(rbase + j) * ldc + col] = apply_epi(epi, acc[nt][j], bcol, rbase + j, col);
+      else slabs[((int64_t)d.z * kRB + rl) * slab_ld + col] = acc[nt][j];
+    }
+  }
+}
+
+// Multi-chunk dense blocks: out[row, :] = epi(sum over the block's slabs, in
+// chunk order).  256 threads = 16 slab lanes x 16 float4 column lanes; a
+// workgroup covers one row x 64 columns; slab lanes take slabs strided by 16,
+// then the 16 partial sums are added in lane order through LDS.
+__global__ void __launch_bounds__(256)
+spmm_tile_reduce_kernel(const int4* __restrict__ red, int32_t F, const float* __restrict__ slabs, int64_t slab_ld,
+                        float* __restrict__ C, int64_t ldc, Epi epi) {
+  __shared__ float4 s_acc[16][16];
+  const int4 rb = red[blockIdx.x];  // row0, nrows, first slab, nslabs
+  const int32_t rl = blockIdx.y;    // row within block
+  if (rl >= rb.y) return;
+  const int sl = threadIdx.x >> 4, c4 = threadIdx.x & 15;
+  const int64_t col = (int64_t)blockIdx.z * 64 + c4 * 4;
+  float4 acc = make_float4(0.f, 0.f, 0.f, 0.f);
+  if (col < F) {
+    for (int s = sl; s < rb.w; s += 16) {
+      const float* p = slabs + ((int64_t)(rb.z + s) * kRB + rl) * slab_ld + col;
+      acc.x += p[0];
+      if (col + 1 < F) acc.y += p[1];
+      if (col + 2 < F) acc.z += p[2];
+      if (col + 3 < F) acc.w += p[3];
+    }
+  }
+  s_acc[sl][c4] = acc;
+  __syncthreads();
+  if (sl != 0 || col >= F) return;
+  float4 t = s_acc[0][c4];
+  for (int q = 1; q < 16; ++q) {
+    const float4 u = s_acc[q][c4];
+    t.x += u.x; t.y += u.y; t.z += u.z; t.w += u.w;
+  }
+  const int64_t row = (int64_t)rb.x + rl;
+  const float vals[4] = {t.x, t.y, t.z, t.w};
+  for (int i = 0; i < 4 && col + i < F; ++i) {
+    const float b = epi.bias ? epi.bias[col + i] : 0.f;
+    C[row * ldc + col + i] = apply_epi(epi, vals[i], b, row, col + i);
   }
 }
 
 // ---------------------------------------------------------------------------
 // Dispatch
-
-struct Cfg {
-  int lpr, vpl, vec, col_tiles;
-};
 
 inline int next_pow2(int v) {
   int p = 1;
@@ -368,60 +476,265 @@ inline int next_pow2(int v) {
   return p;
 }
 
-inline Cfg choose_cfg(int32_t F, int vec, int lanes_hint) {
+// Lanes per group from F alone (so a plan's G does not depend on pointer
+// alignment, which only picks VEC/VPL at launch).
+inline int choose_lpr(int32_t F, int lanes_hint) {
+  if (lanes_hint > 0) return next_pow2(lanes_hint > 64 ? 64 : lanes_hint);
+  const int Wv = (F % 4 == 0) ? F / 4 : F;
+  return Wv <= 64 ? next_pow2(Wv < 1 ? 1 : Wv) : 64;
+}
+
+// Workgroup size: small groups use one wave so a window holds at most 32 groups
+// (bounds the in-LDS chain walk of split rows).
+inline int choose_block(int lpr) { return lpr >= 8 ? 256 : 64; }
+inline int choose_groups(int32_t F, int lanes_hint) {
+  const int lpr = choose_lpr(F, lanes_hint);
+  return choose_block(lpr) / lpr;
+}
+
+struct Cfg {
+  int lpr, vpl, vec, col_tiles, block;
+};
+
+inline Cfg choose_cfg(int32_t F, int vec, int lpr) {
   Cfg c;
   c.vec = vec;
-  const int W = (F + vec - 1) / vec;
-  if (lanes_hint > 0) c.lpr = next_pow2(lanes_hint > 64 ? 64 : lanes_hint);
-  else c.lpr = W <= 64 ? next_pow2(W) : 64;
-  int vpl = (W + c.lpr - 1) / c.lpr;
+  c.lpr = lpr;
+  c.block = choose_block(lpr);
+  const int Wv = (F + vec - 1) / vec;
+  int vpl = (Wv + lpr - 1) / lpr;
   vpl = vpl <= 1 ? 1 : (vpl <= 2 ? 2 : 4);
   c.vpl = vpl;
-  c.col_tiles = (W + c.lpr * c.vpl - 1) / (c.lpr * c.vpl);
+  c.col_tiles = (Wv + lpr * vpl - 1) / (lpr * vpl);
   return c;
 }
 
-template <int LPR, int VPL, int VEC>
-int launch_cfg(const int32_t* rowptr, const int32_t* colind, const float* val, int32_t M,
-               const int32_t* plan, int64_t nchunks, int32_t ipc, int32_t nfix, const float* B,
-               int64_t ldb, int32_t F, float* C, int64_t ldc, const Epi& epi, float* part,
-               int64_t part_ld, int col_tiles, hipStream_t stream) {
-  constexpr int G = 256 / LPR;
-  constexpr int U = 8 / VPL;
-  const int64_t nwg = (nchunks + G - 1) / G;
-  const size_t lds = (size_t)((G * ipc + 2) + 3 * (G * ipc + ipc)) * 4;
-  if (nwg > 0) {
-    hipLaunchKernelGGL((spmm_merge_kernel<LPR, VPL, VEC, U>), dim3((unsigned)nwg, col_tiles), dim3(256),
-                       lds, stream, rowptr, colind, val, M, plan, nchunks, ipc, B, ldb, F, C, ldc, epi,
-                       part, part_ld);
-    int rc = launch_check("spmm_merge_kernel");
+constexpr int kMaxLds = 65536;
+
+inline size_t lds_bytes(int G, int ipc, int FT) {
+  const int W = G * ipc;
+  return (size_t)(2 * ((W + 2 + 1) & ~1) + ((4 * G + 3) & ~3) + 2 * G * FT) * 4;
+}
+
+struct Launch {
+  const int32_t* plan;
+  Layout L;
+  int32_t ipc, nfix;
+  const float* B;
+  int64_t ldb;
+  int32_t F;
+  float* C;
+  int64_t ldc;
+  Epi epi;
+  float* part;  // path partial slots
+  int64_t part_ld;
+  int col_tiles;
+  hipStream_t s;
+};
+
+template <int BLOCK, int LPR, int VPL, int VEC>
+int launch_path(const Launch& a) {
+  constexpr int G = BLOCK / LPR;
+  constexpr int U = (16 / VPL) < 2 ? 2 : 16 / VPL;
+  const size_t lds = lds_bytes(G, a.ipc, LPR * VPL * VEC);
+  if (lds > (size_t)kMaxLds) {
+    set_error("gcnk_spmm_csr_f32: ipc %d needs %zu B of LDS (> %d) at %d groups", a.ipc, lds, kMaxLds, G);
+    return GCNK_EUNSUP;
+  }
+  if (a.L.nwin > 0) {
+    hipLaunchKernelGGL((spmm_path_kernel<BLOCK, LPR, VPL, VEC, U>), dim3((unsigned)a.L.nwin, a.col_tiles),
+                       dim3(BLOCK), lds, a.s, reinterpret_cast<const int2*>(a.plan + a.L.items), a.plan + a.L.head,
+                       a.plan + a.L.tail, a.ipc, a.B, a.ldb, a.F, a.C, a.ldc, a.epi, a.part, a.part_ld);
+    int rc = launch_check("spmm_path_kernel");
     if (rc) return rc;
   }
-  if (nfix != 0) {
-    const int64_t nf = nfix > 0 ? nfix : nchunks;
-    const int64_t nwf = (nf + G - 1) / G;
-    hipLaunchKernelGGL((spmm_fixup_kernel<LPR, VPL, VEC>), dim3((unsigned)nwf, col_tiles), dim3(256), 0,
-                       stream, plan, nchunks, nfix, F, part, part_ld, C, ldc, epi);
+  if (a.nfix > 0) {
+    hipLaunchKernelGGL((spmm_fixup_kernel<LPR, VPL, VEC>), dim3((unsigned)a.nfix, a.col_tiles), dim3(256), 0, a.s,
+                       a.plan + a.L.fix, a.nfix, a.F, a.part, a.part_ld, a.C, a.ldc, a.epi);
     return launch_check("spmm_fixup_kernel");
   }
   return GCNK_OK;
 }
 
 template <int VEC>
-int dispatch_vec(const Cfg& c, const int32_t* rowptr, const int32_t* colind, const float* val,
-                 int32_t M, const int32_t* plan, int64_t nchunks, int32_t ipc, int32_t nfix,
-                 const float* B, int64_t ldb, int32_t F, float* C, int64_t ldc, const Epi& epi,
-                 float* part, int64_t part_ld, hipStream_t s) {
-#define GCNK_CASE(L, P)                                                                         \
-  if (c.lpr == L && c.vpl == P)                                                                 \
-    return launch_cfg<L, P, VEC>(rowptr, colind, val, M, plan, nchunks, ipc, nfix, B, ldb, F, C, \
-                                 ldc, epi, part, part_ld, c.col_tiles, s);
-  GCNK_CASE(1, 1) GCNK_CASE(2, 1) GCNK_CASE(4, 1) GCNK_CASE(8, 1) GCNK_CASE(16, 1) GCNK_CASE(32, 1)
-  GCNK_CASE(64, 1) GCNK_CASE(16, 2) GCNK_CASE(16, 4) GCNK_CASE(32, 2) GCNK_CASE(32, 4)
-  GCNK_CASE(64, 2) GCNK_CASE(64, 4)
+int dispatch_path(const Cfg& c, const Launch& a) {
+#define GCNK_CASE(BL, L, P) \
+  if (c.block == BL && c.lpr == L && c.vpl == P) return launch_path<BL, L, P, VEC>(a);
+  GCNK_CASE(64, 1, 1) GCNK_CASE(64, 2, 1) GCNK_CASE(64, 4, 1) GCNK_CASE(256, 8, 1) GCNK_CASE(256, 16, 1)
+  GCNK_CASE(256, 32, 1) GCNK_CASE(256, 64, 1) GCNK_CASE(64, 1, 2) GCNK_CASE(64, 2, 2) GCNK_CASE(64, 4, 2)
+  GCNK_CASE(256, 8, 2) GCNK_CASE(256, 16, 2) GCNK_CASE(256, 32, 2) GCNK_CASE(256, 64, 2) GCNK_CASE(64, 1, 4)
+  GCNK_CASE(64, 2, 4) GCNK_CASE(64, 4, 4) GCNK_CASE(256, 8, 4) GCNK_CASE(256, 16, 4) GCNK_CASE(256, 32, 4)
+  GCNK_CASE(256, 64, 4)
 #undef GCNK_CASE
   set_error("gcnk_spmm_csr_f32: unsupported lanes/vectors config (%d,%d)", c.lpr, c.vpl);
   return GCNK_EUNSUP;
+}
+
+struct TileArgs {
+  const int4* tdesc;
+  const int32_t* tcols;
+  const float* tfrag;
+  int32_t F;
+  const float* B;
+  int64_t ldb;
+  float* C;
+  int64_t ldc;
+  Epi epi;
+  float* slabs;
+  int64_t slab_ld;
+};
+
+template <bool V4, int NT>
+int launch_tile_nt(unsigned nitems, const TileArgs& t, hipStream_t s) {
+  hipLaunchKernelGGL((spmm_tile_kernel<V4, NT>), dim3(nitems), dim3(256), 0, s, t.tdesc, t.tcols, t.tfrag, t.F, t.B,
+                     t.ldb, t.C, t.ldc, t.epi, t.slabs, t.slab_ld);
+  return launch_check("spmm_tile_kernel");
+}
+
+template <bool V4>
+int launch_tile_v(int nt_need, unsigned nitems, const TileArgs& t, hipStream_t s) {
+  if (nt_need <= 1) return launch_tile_nt<V4, 1>(nitems, t, s);
+  if (nt_need <= 2) return launch_tile_nt<V4, 2>(nitems, t, s);
+  if (nt_need <= 4) return launch_tile_nt<V4, 4>(nitems, t, s);
+  if (nt_need <= 8) return launch_tile_nt<V4, 8>(nitems, t, s);
+  if (nt_need <= 13) return launch_tile_nt<V4, 13>(nitems, t, s);
+  if (nt_need <= kMaxNT) return launch_tile_nt<V4, kMaxNT>(nitems, t, s);
+  set_error("spmm_tile_kernel: %d n-tiles exceed %d", nt_need, kMaxNT);
+  return GCNK_EUNSUP;
+}
+
+inline int launch_tile(bool v4, int nt_need, unsigned nitems, const TileArgs& t, hipStream_t s) {
+  return v4 ? launch_tile_v<true>(nt_need, nitems, t, s) : launch_tile_v<false>(nt_need, nitems, t, s);
+}
+
+// ---------------------------------------------------------------------------
+// Host side of the plan.
+struct HostPlan {
+  int32_t hdr[16];
+  std::vector<int32_t> start;   // item position of each path row, -1 for tile rows
+  std::vector<int32_t> head, tail, fix;
+  std::vector<int32_t> tdesc, tcols, red;
+  std::vector<float> tfrag;
+};
+
+int host_plan(const int32_t* rowptr_dev, const int32_t* colind_dev, const float* val_dev, int32_t M, int32_t K,
+              int64_t nnz, int32_t ipc, int32_t groups, float dense_threshold, bool want_values, hipStream_t s,
+              HostPlan& hp) {
+  std::vector<int32_t> rp((size_t)M + 1), ci((size_t)nnz);
+  std::vector<float> vv(want_values ? (size_t)nnz : 0);
+  int rc = hip_check(hipMemcpyAsync(rp.data(), rowptr_dev, ((size_t)M + 1) * 4, hipMemcpyDeviceToHost, s),
+                     "plan rowptr copy");
+  if (!rc && nnz > 0)
+    rc = hip_check(hipMemcpyAsync(ci.data(), colind_dev, (size_t)nnz * 4, hipMemcpyDeviceToHost, s), "plan colind copy");
+  if (!rc && want_values && nnz > 0)
+    rc = hip_check(hipMemcpyAsync(vv.data(), val_dev, (size_t)nnz * 4, hipMemcpyDeviceToHost, s), "plan val copy");
+  if (rc) return rc;
+  if ((rc = hip_check(hipStreamSynchronize(s), "plan copy sync"))) return rc;
+  if ((int64_t)rp[M] != nnz || rp[0] != 0) {
+    set_error("gcnk_spmm_plan: rowptr[0]=%d rowptr[M]=%d inconsistent with nnz=%lld", rp[0], rp[M], (long long)nnz);
+    return GCNK_EARG;
+  }
+  for (int32_t r = 0; r < M; ++r)
+    if (rp[r + 1] < rp[r]) {
+      set_error("gcnk_spmm_plan: rowptr decreases at row %d", r);
+      return GCNK_EARG;
+    }
+  for (int64_t k = 0; k < nnz; ++k)
+    if (ci[(size_t)k] < 0 || ci[(size_t)k] >= K) {
+      set_error("gcnk_spmm_plan: column index %d out of range [0, %d) at nonzero %lld", ci[(size_t)k], K, (long long)k);
+      return GCNK_EARG;
+    }
+
+  // ---- dense blocks (tile path)
+  std::vector<char> tile_row((size_t)M, 0);
+  int32_t ntile = 0, nred = 0, nslabs = 0;
+  std::vector<int32_t> cmap((size_t)K, -1);
+  for (int32_t r0 = 0; r0 < M && dense_threshold <= 1.0f; r0 += kRB) {
+    const int32_t r1 = std::min(M, r0 + kRB);
+    const int64_t bnnz = (int64_t)rp[r1] - rp[r0];
+    if (bnnz == 0) continue;
+    std::vector<int32_t> cols(ci.begin() + rp[r0], ci.begin() + rp[r1]);
+    std::sort(cols.begin(), cols.end());
+    cols.erase(std::unique(cols.begin(), cols.end()), cols.end());
+    const int64_t ncols = (int64_t)cols.size();
+    if ((double)bnnz < (double)dense_threshold * (double)(r1 - r0) * (double)ncols) continue;
+    const int32_t nch = (int32_t)((ncols + kKC - 1) / kKC);
+    const int32_t first_slab = nch > 1 ? nslabs : -1;
+    for (int64_t c = 0; c < ncols; ++c) cmap[(size_t)cols[(size_t)c]] = (int32_t)c;
+    const size_t base_item = (size_t)ntile;
+    for (int32_t ch = 0; ch < nch; ++ch) {
+      hp.tdesc.insert(hp.tdesc.end(), {r0, r1 - r0, nch > 1 ? first_slab + ch : -1, 0});
+      for (int k = 0; k < kKC; ++k) {
+        const int64_t cc = (int64_t)ch * kKC + k;
+        hp.tcols.push_back(cc < ncols ? cols[(size_t)cc] : -1);
+      }
+    }
+    hp.tfrag.resize(hp.tfrag.size() + (size_t)nch * kRB * kKC, 0.f);
+    if (want_values) {
+      for (int32_t r = r0; r < r1; ++r)
+        for (int32_t k = rp[r]; k < rp[r + 1]; ++k) {
+          const int32_t cc = cmap[(size_t)ci[(size_t)k]];
+          const int32_t ch = cc / kKC, kk = cc % kKC;
+          const int32_t rl = r - r0, t = rl / 16, lr = rl % 16, st = kk / 4, kq = kk % 4;
+          const int32_t ln = kq * 16 + lr;
+          hp.tfrag[(((base_item + ch) * 4 + t) * 64 + ln) * 16 + st] += vv[(size_t)k];
+        }
+    }
+    for (int64_t c = 0; c < ncols; ++c) cmap[(size_t)cols[(size_t)c]] = -1;
+    if (nch > 1) {
+      hp.red.insert(hp.red.end(), {r0, r1 - r0, first_slab, nch});
+      ++nred;
+      nslabs += nch;
+    }
+    ntile += nch;
+    for (int32_t r = r0; r < r1; ++r) tile_row[(size_t)r] = 1;
+  }
+
+  // ---- path windows over the other rows
+  const int64_t W = (int64_t)groups * ipc;
+  const int64_t heavy = W / 2;
+  hp.start.assign((size_t)M, -1);
+  int64_t pos = 0;
+  for (int32_t r = 0; r < M; ++r) {
+    if (tile_row[(size_t)r]) continue;
+    const int64_t len = (int64_t)rp[r + 1] - rp[r] + 1;
+    const int64_t off = pos % W;
+    if (len <= heavy && off + len > W) pos += W - off;
+    hp.start[(size_t)r] = (int32_t)pos;
+    pos += len;
+    if (pos >= (int64_t)INT32_MAX) {
+      set_error("gcnk_spmm_plan: item stream exceeds 2^31 items");
+      return GCNK_EUNSUP;
+    }
+  }
+  const int64_t nwin = (pos + W - 1) / W;
+  hp.head.assign((size_t)nwin, -1);
+  hp.tail.assign((size_t)nwin, -1);
+  // heavy rows crossing window boundaries: tail slot in every window they leave,
+  // head slot in the window of their marker; slots numbered in window order,
+  // a window's head before its tail (contiguous per row).
+  struct Cross { int32_t row; int64_t wa, wb; };
+  std::vector<Cross> cross;
+  for (int32_t r = 0; r < M; ++r) {
+    if (hp.start[(size_t)r] < 0) continue;
+    const int64_t a0 = hp.start[(size_t)r], e = a0 + (rp[r + 1] - rp[r]);  // e = marker position
+    const int64_t wa = a0 / W, wb = e / W;
+    if (wa < wb) cross.push_back({r, wa, wb});
+  }
+  for (const Cross& c : cross) {
+    for (int64_t x = c.wa; x < c.wb; ++x) hp.tail[(size_t)x] = 1;
+    hp.head[(size_t)c.wb] = 1;
+  }
+  int32_t slot = 0;
+  for (int64_t x = 0; x < nwin; ++x) {
+    if (hp.head[(size_t)x] >= 0) hp.head[(size_t)x] = slot++;
+    if (hp.tail[(size_t)x] >= 0) hp.tail[(size_t)x] = slot++;
+  }
+  for (const Cross& c : cross) hp.fix.insert(hp.fix.end(), {c.row, hp.tail[(size_t)c.wa], hp.head[(size_t)c.wb]});
+  const int32_t h[16] = {kMagic, M, K, groups, ipc, (int32_t)W, (int32_t)nwin, (int32_t)cross.size(), slot,
+                         ntile, nred, nslabs, kKC, kRB, (int32_t)heavy, 0};
+  std::copy(h, h + 16, hp.hdr);
+  return GCNK_OK;
 }
 
 }  // namespace
@@ -429,100 +742,121 @@ int dispatch_vec(const Cfg& c, const int32_t* rowptr, const int32_t* colind, con
 
 using namespace gcnk;
 
-extern "C" int32_t gcnk_spmm_default_ipc(int32_t M, int64_t nnz, int32_t F) {
-  const int vec = (F % 4 == 0) ? 4 : 1;
-  const Cfg c = choose_cfg(F, vec, 0);
-  const int G = 256 / c.lpr;
-  const int64_t items = (int64_t)M + nnz;
-  int64_t ipc = items / ((int64_t)G * 1024);
-  if (ipc < 4) ipc = 4;
-  if (ipc > 64) ipc = 64;
-  ipc = (ipc + 3) & ~3LL;
-  while (G * ipc > 2048) ipc >>= 1;
-  return (int32_t)ipc;
+static unsigned long long* g_stamps = nullptr;
+extern "C" void gcnk_debug_set_stamps(void* buf) { g_stamps = (unsigned long long*)buf; }
+
+extern "C" int32_t gcnk_spmm_groups(int32_t F, int32_t lanes_hint) { return choose_groups(F, lanes_hint); }
+
+extern "C" int32_t gcnk_spmm_default_ipc(int32_t M, int64_t nnz, int32_t F, int32_t lanes_hint) {
+  (void)M;
+  (void)nnz;
+  const int lpr = choose_lpr(F, lanes_hint);
+  const int G = choose_block(lpr) / lpr;
+  const Cfg c = choose_cfg(F, F % 4 == 0 ? 4 : 1, lpr);
+  int ipc = lpr >= 16 ? 16 : 8;
+  while (ipc > 2 && lds_bytes(G, ipc, lpr * c.vpl * c.vec) > (size_t)kMaxLds) ipc /= 2;
+  return ipc;
 }
 
-extern "C" int64_t gcnk_spmm_plan_chunks(int32_t M, int64_t nnz, int32_t ipc) {
-  if (ipc <= 0 || M < 0 || nnz < 0) return -1;
-  return plan_nchunks(M, nnz, ipc);
-}
-
-extern "C" int64_t gcnk_spmm_plan_bytes(int32_t M, int64_t nnz, int32_t ipc) {
-  const int64_t nc = gcnk_spmm_plan_chunks(M, nnz, ipc);
-  if (nc < 0) return -1;
-  // + nchunks words of scratch for the fix index (kept after the fix list)
-  return (PlanLayout(nc).total + nc) * 4;
-}
-
-extern "C" int gcnk_spmm_plan_build(const int32_t* rowptr, int32_t M, int64_t nnz, int32_t ipc,
-                                    void* plan, int64_t plan_bytes, void* stream) {
-  if (!rowptr || !plan || M < 0 || nnz < 0 || ipc <= 0 || ipc > 4096) {
-    set_error("gcnk_spmm_plan_build: bad argument (M=%d nnz=%lld ipc=%d)", M, (long long)nnz, ipc);
+extern "C" int64_t gcnk_spmm_plan_bytes(const int32_t* rowptr, const int32_t* colind, int32_t M, int32_t K,
+                                        int64_t nnz, int32_t ipc, int32_t groups, float dense_threshold,
+                                        void* stream) {
+  if (!rowptr || M < 0 || K < 0 || nnz < 0 || ipc <= 0 || groups <= 0 || (nnz > 0 && !colind)) {
+    set_error("gcnk_spmm_plan_bytes: bad argument");
     return GCNK_EARG;
   }
-  if ((int64_t)M + nnz >= (int64_t)INT32_MAX) {
-    set_error("gcnk_spmm_plan_build: M + nnz must be < 2^31");
-    return GCNK_EUNSUP;
-  }
-  const int64_t need = gcnk_spmm_plan_bytes(M, nnz, ipc);
-  if (plan_bytes < need) {
-    set_error("gcnk_spmm_plan_build: plan buffer %lld B < %lld B", (long long)plan_bytes, (long long)need);
+  HostPlan hp;
+  const int rc = host_plan(rowptr, colind, nullptr, M, K, nnz, ipc, groups, dense_threshold, false,
+                           (hipStream_t)stream, hp);
+  if (rc) return rc;
+  // + M words of scratch (path row start positions) used while building
+  return (Layout(hp.hdr).total + M) * 4;
+}
+
+extern "C" int gcnk_spmm_plan_build(const int32_t* rowptr, const int32_t* colind, const float* val, int32_t M,
+                                    int32_t K, int64_t nnz, int32_t ipc, int32_t groups, float dense_threshold,
+                                    void* plan, int64_t plan_bytes, void* stream) {
+  if (!rowptr || !plan || M < 0 || K < 0 || nnz < 0 || ipc <= 0 || groups <= 0 || (nnz > 0 && (!colind || !val))) {
+    set_error("gcnk_spmm_plan_build: bad argument (M=%d nnz=%lld ipc=%d groups=%d)", M, (long long)nnz, ipc, groups);
     return GCNK_EARG;
   }
   hipStream_t s = (hipStream_t)stream;
-  const int64_t nc = plan_nchunks(M, nnz, ipc);
-  const PlanLayout L(nc);
+  HostPlan hp;
+  int rc = host_plan(rowptr, colind, val, M, K, nnz, ipc, groups, dense_threshold, true, s, hp);
+  if (rc) return rc;
+  const Layout L(hp.hdr);
+  if (plan_bytes < (L.total + M) * 4) {
+    set_error("gcnk_spmm_plan_build: plan buffer %lld B < %lld B", (long long)plan_bytes,
+              (long long)((L.total + M) * 4));
+    return GCNK_EARG;
+  }
   int32_t* p = (int32_t*)plan;
-  Coord* coords = reinterpret_cast<Coord*>(p + L.coords);
-  int32_t* fix_index = p + L.total;
-  int rc;
-  hipLaunchKernelGGL(plan_coords_kernel, dim3((unsigned)((nc + 1 + 255) / 256)), dim3(256), 0, s, rowptr, M,
-                     nnz, ipc, nc, coords);
-  if ((rc = launch_check("plan_coords_kernel"))) return rc;
-  if (nc > 0) {
-    hipLaunchKernelGGL(plan_flags_kernel, dim3((unsigned)((nc + 255) / 256)), dim3(256), 0, s, rowptr, M, nc,
-                       coords, p + L.head, p + L.tail);
-    if ((rc = launch_check("plan_flags_kernel"))) return rc;
+  int32_t* d_start = p + L.total;  // scratch words after the plan proper
+  auto up = [&](int64_t off, const void* src, size_t bytes, const char* what) {
+    if (!rc && bytes > 0) rc = hip_check(hipMemcpyAsync(p + off, src, bytes, hipMemcpyHostToDevice, s), what);
+  };
+  up(0, hp.hdr, sizeof(hp.hdr), "plan header");
+  up(L.head, hp.head.data(), hp.head.size() * 4, "plan head");
+  up(L.tail, hp.tail.data(), hp.tail.size() * 4, "plan tail");
+  up(L.fix, hp.fix.data(), hp.fix.size() * 4, "plan fix");
+  up(L.tdesc, hp.tdesc.data(), hp.tdesc.size() * 4, "plan tile desc");
+  up(L.tcols, hp.tcols.data(), hp.tcols.size() * 4, "plan tile cols");
+  up(L.tfrag, hp.tfrag.data(), hp.tfrag.size() * 4, "plan tile frags");
+  up(L.red, hp.red.data(), hp.red.size() * 4, "plan tile reduce");
+  up(L.total, hp.start.data(), hp.start.size() * 4, "plan start");
+  const int64_t nitems = L.nwin * L.W;
+  int2* items = reinterpret_cast<int2*>(p + L.items);
+  if (!rc && nitems > 0) {
+    hipLaunchKernelGGL(fill_pad_kernel, dim3((unsigned)((nitems + 255) / 256)), dim3(256), 0, s, items, nitems);
+    rc = launch_check("fill_pad_kernel");
   }
-  hipLaunchKernelGGL(plan_scan_kernel, dim3(1), dim3(1024), 0, s, nc, ipc, p + L.head, p + L.tail, fix_index, p);
-  if ((rc = launch_check("plan_scan_kernel"))) return rc;
-  if (nc > 0) {
-    hipLaunchKernelGGL(plan_fix_kernel, dim3((unsigned)((nc + 255) / 256)), dim3(256), 0, s, rowptr, nc, coords,
-                       p + L.head, p + L.tail, fix_index, p + L.fix);
-    if ((rc = launch_check("plan_fix_kernel"))) return rc;
+  if (!rc && M > 0 && nitems > 0) {
+    hipLaunchKernelGGL(scatter_items_kernel, dim3((unsigned)((M + 3) / 4)), dim3(256), 0, s, rowptr, colind, val, M,
+                       d_start, items);
+    rc = launch_check("scatter_items_kernel");
   }
-  return GCNK_OK;
+  // the host vectors must outlive the async copies
+  const int rc2 = hip_check(hipStreamSynchronize(s), "plan build sync");
+  return rc ? rc : rc2;
 }
 
-extern "C" int gcnk_spmm_plan_query(const void* plan, int32_t* out4, void* stream) {
-  if (!plan || !out4) {
+extern "C" int gcnk_spmm_plan_query(const void* plan, int32_t* out16, void* stream) {
+  if (!plan || !out16) {
     set_error("gcnk_spmm_plan_query: null pointer");
     return GCNK_EARG;
   }
   hipStream_t s = (hipStream_t)stream;
-  int rc = hip_check(hipMemcpyAsync(out4, plan, 16, hipMemcpyDeviceToHost, s), "plan query copy");
+  int rc = hip_check(hipMemcpyAsync(out16, plan, 64, hipMemcpyDeviceToHost, s), "plan query copy");
   if (rc) return rc;
-  return hip_check(hipStreamSynchronize(s), "plan query sync");
-}
-
-extern "C" int64_t gcnk_spmm_workspace_bytes(int32_t nslots, int32_t F) {
-  const int64_t ld = ((int64_t)F + 3) & ~3LL;
-  return (int64_t)(nslots > 0 ? nslots : 0) * ld * 4;
-}
-
-extern "C" int gcnk_spmm_csr_f32(const int32_t* rowptr, const int32_t* colind, const float* val,
-                                 int32_t M, int32_t K, int64_t nnz, const void* plan, int32_t ipc,
-                                 int32_t nfix, const float* B, int64_t ldb, int32_t F, float* C,
-                                 int64_t ldc, const float* bias, int32_t epilogue,
-                                 const uint8_t* drop_mask, int64_t ldm, float drop_scale,
-                                 float keep_prob, uint64_t seed, uint64_t offset, float* workspace,
-                                 int64_t workspace_bytes, int32_t lanes_hint, void* stream) {
-  if (M < 0 || K < 0 || nnz < 0 || F < 0 || ipc <= 0 || !plan) {
-    set_error("gcnk_spmm_csr_f32: bad argument (M=%d K=%d nnz=%lld F=%d ipc=%d)", M, K, (long long)nnz, F, ipc);
+  rc = hip_check(hipStreamSynchronize(s), "plan query sync");
+  if (!rc && out16[0] != kMagic) {
+    set_error("gcnk_spmm_plan_query: not a gcnk plan");
     return GCNK_EARG;
   }
+  return rc;
+}
+
+static int64_t tile_fpad(int32_t F) { return ((int64_t)F + 15) & ~15LL; }
+
+extern "C" int64_t gcnk_spmm_workspace_bytes(const int32_t* hdr, int32_t F) {
+  if (!hdr || hdr[0] != kMagic || F < 0) return GCNK_EARG;
+  const int64_t ld = ((int64_t)F + 3) & ~3LL;
+  const int64_t path = (int64_t)hdr[8] * ld * 4;
+  const int64_t slabs = (int64_t)hdr[11] * kRB * tile_fpad(F) * 4;
+  return ((path + 255) & ~255LL) + slabs;
+}
+
+extern "C" int gcnk_spmm_csr_f32(const void* plan, const int32_t* hdr, const float* B, int64_t ldb, int32_t F,
+                                 float* C, int64_t ldc, const float* bias, int32_t epilogue, const uint8_t* drop_mask,
+                                 int64_t ldm, float drop_scale, float keep_prob, uint64_t seed, uint64_t offset,
+                                 float* workspace, int64_t workspace_bytes, int32_t lanes_hint, void* stream) {
+  if (!plan || !hdr || hdr[0] != kMagic || F < 0) {
+    set_error("gcnk_spmm_csr_f32: bad argument (plan/header missing or not a gcnk plan, F=%d)", F);
+    return GCNK_EARG;
+  }
+  const int32_t M = hdr[1], K = hdr[2], groups = hdr[3], ipc = hdr[4];
   if (M == 0 || F == 0) return GCNK_OK;
-  if (!rowptr || !C || (nnz > 0 && (!colind || !val || !B))) {
+  if (!C || (K > 0 && !B)) {
     set_error("gcnk_spmm_csr_f32: null pointer");
     return GCNK_EARG;
   }
@@ -539,13 +873,18 @@ extern "C" int gcnk_spmm_csr_f32(const int32_t* rowptr, const int32_t* colind, c
     set_error("gcnk_spmm_csr_f32: dropout epilogue needs a mask with ldm >= F");
     return GCNK_EARG;
   }
-  const int64_t nc = plan_nchunks(M, nnz, ipc);
-  const int64_t part_ld = ((int64_t)F + 3) & ~3LL;
-  if (nfix != 0 && !workspace) {
-    set_error("gcnk_spmm_csr_f32: plan has split rows but no workspace was given");
+  const int lpr = choose_lpr(F, lanes_hint);
+  if (groups != choose_block(lpr) / lpr) {
+    set_error("gcnk_spmm_csr_f32: plan built for %d groups, this F/lanes uses %d (gcnk_spmm_groups)", groups,
+              choose_block(lpr) / lpr);
     return GCNK_EARG;
   }
-  (void)workspace_bytes;
+  const int64_t need = gcnk_spmm_workspace_bytes(hdr, F);
+  if (need > 0 && (!workspace || workspace_bytes < need)) {
+    set_error("gcnk_spmm_csr_f32: plan needs %lld B of workspace, got %lld", (long long)need,
+              (long long)workspace_bytes);
+    return GCNK_EARG;
+  }
   Epi e;
   e.bias = bias;
   e.mask = drop_mask;
@@ -556,19 +895,47 @@ extern "C" int gcnk_spmm_csr_f32(const int32_t* rowptr, const int32_t* colind, c
   e.seed_hi = (uint32_t)(seed >> 32);
   e.offset = offset;
   e.code = epilogue;
+  e.stamps = g_stamps;
   const bool vec4 = (F % 4 == 0) && (ldb % 4 == 0) && (ldc % 4 == 0) && aligned16(B) && aligned16(C) &&
                     (!workspace || aligned16(workspace)) && (!bias || aligned16(bias));
-  const Cfg c = choose_cfg(F, vec4 ? 4 : 1, lanes_hint);
-  const int G = 256 / c.lpr;
-  if ((int64_t)G * ipc > 2048) {
-    set_error("gcnk_spmm_csr_f32: ipc %d too large for %d groups per workgroup", ipc, G);
-    return GCNK_EUNSUP;
-  }
   hipStream_t s = (hipStream_t)stream;
   const int32_t* p = (const int32_t*)plan;
-  if (vec4)
-    return dispatch_vec<4>(c, rowptr, colind, val, M, p, nc, ipc, nfix, B, ldb, F, C, ldc, e, workspace,
-                           part_ld, s);
-  return dispatch_vec<1>(c, rowptr, colind, val, M, p, nc, ipc, nfix, B, ldb, F, C, ldc, e, workspace,
-                         part_ld, s);
+  const Layout L(hdr);
+  const int64_t part_ld = ((int64_t)F + 3) & ~3LL;
+  const int64_t path_ws = ((int64_t)hdr[8] * part_ld * 4 + 255) & ~255LL;
+  float* slabs = workspace ? reinterpret_cast<float*>(reinterpret_cast<char*>(workspace) + path_ws) : nullptr;
+  const int64_t slab_ld = tile_fpad(F);
+
+  // ---- dense blocks: tile kernel (+ slab reduce)
+  if (L.ntile > 0) {
+    const int32_t nt_total = (int32_t)(slab_ld / 16);
+    // F <= 16*kMaxNT: one launch over all columns; wider: 128-column slices with the
+    // slice offset folded into the B/C/bias/mask pointers (multiples of 4: alignment kept)
+    const int32_t slice = nt_total <= kMaxNT ? (int32_t)(nt_total * 16) : 128;
+    const int4* td = reinterpret_cast<const int4*>(p + L.tdesc);
+    for (int64_t c0 = 0; c0 < F; c0 += slice) {
+      const int32_t Fs = (int32_t)std::min<int64_t>(slice, F - c0);
+      Epi es = e;
+      es.bias = bias ? bias + c0 : nullptr;
+      es.mask = drop_mask ? drop_mask + c0 : nullptr;
+      es.offset = e.offset + (uint64_t)c0;  // hash index shifts with the column
+      TileArgs ta{td, p + L.tcols, reinterpret_cast<const float*>(p + L.tfrag), Fs, B + c0, ldb, C + c0, ldc, es,
+                  slabs ? slabs + c0 : nullptr, slab_ld};
+      const int rc = launch_tile(vec4, (Fs + 15) / 16, (unsigned)L.ntile, ta, s);
+      if (rc) return rc;
+    }
+    if (L.nred > 0) {
+      hipLaunchKernelGGL(spmm_tile_reduce_kernel, dim3((unsigned)L.nred, kRB, (unsigned)((F + 63) / 64)), dim3(256),
+                         0, s, reinterpret_cast<const int4*>(p + L.red), F, slabs, slab_ld, C, ldc, e);
+      int rc = launch_check("spmm_tile_reduce_kernel");
+      if (rc) return rc;
+    }
+  }
+  // ---- remaining rows: path kernel (+ fix-up)
+  if (L.nwin > 0) {
+    const Cfg c = choose_cfg(F, vec4 ? 4 : 1, lpr);
+    Launch a{p, L, ipc, (int32_t)L.nfix, B, ldb, F, C, ldc, e, workspace, part_ld, c.col_tiles, s};
+    return vec4 ? dispatch_path<4>(c, a) : dispatch_path<1>(c, a);
+  }
+  return GCNK_OK;
 }

@@ -9,7 +9,7 @@ import ctypes
 import torch
 
 from . import _lib
-from .sparse import CSR, as_csr, require_device
+from .sparse import CSR, DENSE_THRESHOLD, as_csr, require_device
 
 _NULL = ctypes.c_void_p(0)
 
@@ -33,12 +33,12 @@ def _dense_f32(t, what):
     return t
 
 
-def default_ipc(a, F):
-    return int(_lib.load().gcnk_spmm_default_ipc(a.shape[0], a.nnz, F))
+def default_ipc(a, F, lanes=0):
+    return int(_lib.load().gcnk_spmm_default_ipc(a.shape[0], a.nnz, F, int(lanes)))
 
 
 def spmm(a, B, bias=None, epilogue=_lib.EPI_NONE, mask=None, scale=1.0, keep_prob=1.0, seed=0, offset=0,
-         out=None, ipc=None, lanes=0):
+         out=None, ipc=None, lanes=0, dense=None):
     """C = epi(A @ B) with A a CSR (or torch sparse) and B dense [K, F].
 
     Replaces ``th.spmm(adj, support)`` (reference layer.py:106) and
@@ -59,16 +59,16 @@ def spmm(a, B, bias=None, epilogue=_lib.EPI_NONE, mask=None, scale=1.0, keep_pro
         bias = bias.contiguous()
     if mask is not None:
         mask = mask.contiguous()
-    if ipc is None:
-        ipc = default_ipc(a, F)
-    plan, ipc, nslots, nfix = a.plan(ipc)
     lib = _lib.load()
-    wsb = lib.gcnk_spmm_workspace_bytes(nslots, F)
-    ws = torch.empty((max(wsb, 16) + 3) // 4, dtype=torch.float32, device=B.device) if nslots > 0 else None
+    if ipc is None:
+        ipc = default_ipc(a, F, lanes)
+    groups = int(lib.gcnk_spmm_groups(F, int(lanes)))
+    plan = a.plan(ipc, groups, DENSE_THRESHOLD if dense is None else dense)
+    wsb = plan.workspace_bytes(F)
+    ws = torch.empty((wsb + 3) // 4, dtype=torch.float32, device=B.device) if wsb > 0 else None
     with torch.cuda.device(B.device):
         rc = lib.gcnk_spmm_csr_f32(
-            _ptr(a.rowptr), _ptr(a.colind), _ptr(a.val), M, K, a.nnz,
-            _ptr(plan), ipc, nfix,
+            _ptr(plan.buf), ctypes.cast(plan.hdr, ctypes.c_void_p),
             _ptr(B), B.stride(0), F,
             _ptr(out), out.stride(0),
             _ptr(bias), epilogue,

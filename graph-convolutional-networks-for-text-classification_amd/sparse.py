@@ -36,6 +36,25 @@ def require_device(t, what):
             "only through its HIP kernels — move the model and inputs with .to('cuda').")
 
 
+DENSE_THRESHOLD = 0.25  # row blocks at least this dense (condensed) run on the MFMA tile path
+
+
+class Plan:
+    """A built SpMM plan: device buffer + the 16-word host header (gcnk.h)."""
+
+    __slots__ = ("buf", "hdr")
+
+    def __init__(self, buf, hdr):
+        self.buf, self.hdr = buf, hdr
+
+    @property
+    def header(self):
+        return list(self.hdr)
+
+    def workspace_bytes(self, F):
+        return int(_lib.load().gcnk_spmm_workspace_bytes(ctypes.cast(self.hdr, ctypes.c_void_p), int(F)))
+
+
 class CSR:
     """A sparse matrix in int32 CSR on one device, with cached schedules."""
 
@@ -53,31 +72,35 @@ class CSR:
     def __repr__(self):
         return f"CSR(shape={self.shape}, nnz={self.nnz}, device={self.device})"
 
-    # -- merge-path schedule (gcnk_spmm_plan_build), one per chunk size -----------------
-    def plan(self, ipc):
-        p = self._plans.get(ipc)
+    # -- hybrid plan (gcnk_spmm_plan_build), one per (ipc, groups, dense threshold) -------
+    def plan(self, ipc, groups, dense_threshold=DENSE_THRESHOLD):
+        """Returns a Plan (device buffer + host header); built once per key (setup sync)."""
+        key = (ipc, groups, float(dense_threshold))
+        p = self._plans.get(key)
         if p is not None:
             return p
         with self._lock:
-            p = self._plans.get(ipc)
+            p = self._plans.get(key)
             if p is not None:
                 return p
             lib = _lib.load()
-            M, _ = self.shape
-            nbytes = lib.gcnk_spmm_plan_bytes(M, self.nnz, ipc)
-            if nbytes < 0:
-                raise RuntimeError(f"bad plan request M={M} nnz={self.nnz} ipc={ipc}")
-            buf = torch.empty((nbytes + 3) // 4, dtype=torch.int32, device=self.device)
+            M, K = self.shape
             with torch.cuda.device(self.device):
                 s = _stream_ptr(self.device)
-                _lib.check(lib.gcnk_spmm_plan_build(self.rowptr.data_ptr(), M, self.nnz, ipc, buf.data_ptr(),
-                                                    nbytes, s), "gcnk_spmm_plan_build")
-                hdr = (ctypes.c_int32 * 4)()
-                # one-time setup sync: sizes the split-row partial workspace
+                nbytes = lib.gcnk_spmm_plan_bytes(self.rowptr.data_ptr(), self.colind.data_ptr(), M, K, self.nnz,
+                                                  ipc, groups, float(dense_threshold), s)
+                if nbytes < 0:
+                    _lib.check(int(nbytes), "gcnk_spmm_plan_bytes")
+                buf = torch.empty((nbytes + 3) // 4, dtype=torch.int32, device=self.device)
+                _lib.check(lib.gcnk_spmm_plan_build(self.rowptr.data_ptr(), self.colind.data_ptr(),
+                                                    self.val.data_ptr(), M, K, self.nnz, ipc, groups,
+                                                    float(dense_threshold), buf.data_ptr(), nbytes, s),
+                           "gcnk_spmm_plan_build")
+                hdr = (ctypes.c_int32 * 16)()
                 _lib.check(lib.gcnk_spmm_plan_query(buf.data_ptr(), ctypes.cast(hdr, ctypes.c_void_p), s),
                            "gcnk_spmm_plan_query")
-            p = (buf, ipc, int(hdr[0]), int(hdr[1]))
-            self._plans[ipc] = p
+            p = Plan(buf, hdr)
+            self._plans[key] = p
             return p
 
     # -- transpose (gcnk_csr_transpose), cached ---------------------------------------

@@ -73,34 +73,48 @@ const char* gcnk_last_error(void);
  * Replaces th.spmm(adj, support) (layer.py:106) and th.spmm(X, W)
  * (layer.py:102, sparse X) and their autograd (A^T g, X^T g).
  *
- * Work is scheduled by a merge-path plan over (row ends + nonzeros): the
- * path is cut into chunks of `ipc` items; a chunk boundary falling inside a
- * row shorter than `ipc` is moved back to that row's start, so only heavy
- * rows are split.  Split rows are summed deterministically (fixed chunk order,
- * no float atomics) by a fix-up pass.  The plan depends only on the sparsity
- * pattern and ipc and is built once per graph.
+ * The operand is converted once (gcnk_spmm_plan_build) into a hybrid plan
+ * whose two parts write disjoint rows of C:
+ *  - dense blocks: blocks of 64 rows whose nonzeros fill >= dense_threshold
+ *    of the block's condensed column set are stored densely over those
+ *    columns (MFMA fragment order, chunks of 64 columns) and run on fp32
+ *    MFMA, each B row of a chunk staged once per block instead of gathered
+ *    per nonzero; multi-chunk blocks are summed from partial slabs in order.
+ *    dense_threshold > 1 disables the part (default callers pass 0.25).
+ *  - path: the other rows' nonzeros in row order, each row closed by an
+ *    end-of-row marker, as one int2 item stream (col, value bits) / (-1, row)
+ *    / (-2 pad) cut into windows of W = groups*ipc items, one per workgroup;
+ *    rows of at most W/2 items never straddle a window, so only heavy rows
+ *    cross windows.  Rows split between the chunks of a window meet in LDS;
+ *    heavy rows crossing windows leave one partial per window that a fix-up
+ *    pass sums in path order.
+ * All sums have a fixed order (no float atomics): bitwise reproducible.
+ * gcnk_spmm_groups(F, lanes_hint) gives the `groups` the kernels use for a
+ * width F; a plan serves every F with that count.  The plan copies the
+ * values: rebuild it when they change.  Building copies the CSR to the host
+ * and synchronises `stream` (one-time setup).
  *
- * Plan layout (int32, device):
- *   [0] nslots  [1] nfix  [2] ipc  [3] nchunks (low 31 bits)
- *   coords:     2*(nchunks+1)   merge-path start (row, nnz) of every chunk
- *   head_slot:  nchunks         partial slot of the row a chunk finishes but did not start, or -1
- *   tail_slot:  nchunks         partial slot of the row a chunk starts but does not finish, or -1
- *   fix:        2*nchunks       (chunk, first contributing chunk) of every split row
+ * Plan header (16 int32, first words of the plan; gcnk_spmm_plan_query):
+ *   0 magic 'GNK3'  1 M  2 K  3 groups  4 ipc  5 W  6 nwin  7 nfix  8 nslots
+ *   9 tile chunks  10 multi-chunk blocks  11 slabs  12 KC=64  13 RB=64  14 heavy  15 0
  * ------------------------------------------------------------------------- */
-int32_t gcnk_spmm_default_ipc(int32_t M, int64_t nnz, int32_t F);
-int64_t gcnk_spmm_plan_chunks(int32_t M, int64_t nnz, int32_t ipc);
-int64_t gcnk_spmm_plan_bytes(int32_t M, int64_t nnz, int32_t ipc);
-int gcnk_spmm_plan_build(const int32_t* rowptr, int32_t M, int64_t nnz, int32_t ipc,
+int32_t gcnk_spmm_groups(int32_t F, int32_t lanes_hint);
+int32_t gcnk_spmm_default_ipc(int32_t M, int64_t nnz, int32_t F, int32_t lanes_hint);
+/* Size of the plan buffer (synchronises `stream`; negative error code on failure). */
+int64_t gcnk_spmm_plan_bytes(const int32_t* rowptr, const int32_t* colind, int32_t M, int32_t K,
+                             int64_t nnz, int32_t ipc, int32_t groups, float dense_threshold,
+                             void* stream);
+int gcnk_spmm_plan_build(const int32_t* rowptr, const int32_t* colind, const float* val, int32_t M,
+                         int32_t K, int64_t nnz, int32_t ipc, int32_t groups, float dense_threshold,
                          void* plan, int64_t plan_bytes, void* stream);
-/* Copies the 4-word plan header to host memory `out4` and synchronises
- * `stream`.  One-time setup call (sizes the partial-sum workspace). */
-int gcnk_spmm_plan_query(const void* plan, int32_t* out4, void* stream);
-/* Bytes of partial-sum workspace needed for `nslots` split-row partials of width F. */
-int64_t gcnk_spmm_workspace_bytes(int32_t nslots, int32_t F);
+/* Copies the 16-word plan header to host memory `out16` and synchronises
+ * `stream` (one-time setup).  Every SpMM call takes this host header. */
+int gcnk_spmm_plan_query(const void* plan, int32_t* out16, void* stream);
+/* Bytes of workspace (split-row partials + tile slabs) an SpMM of width F needs. */
+int64_t gcnk_spmm_workspace_bytes(const int32_t* plan_header, int32_t F);
 
-int gcnk_spmm_csr_f32(const int32_t* rowptr, const int32_t* colind, const float* val,
-                      int32_t M, int32_t K, int64_t nnz,
-                      const void* plan, int32_t ipc, int32_t nfix,
+/* C = epi(A B) for the operand of `plan` (M x K from the header). */
+int gcnk_spmm_csr_f32(const void* plan, const int32_t* plan_header,
                       const float* B, int64_t ldb, int32_t F,
                       float* C, int64_t ldc,
                       const float* bias, int32_t epilogue,
@@ -146,6 +160,11 @@ int gcnk_csr_transpose(const int32_t* rowptr, const int32_t* colind, const float
                        int32_t M, int32_t K, int64_t nnz,
                        int32_t* rowptr_t, int32_t* colind_t, float* val_t,
                        void* workspace, int64_t workspace_bytes, void* stream);
+
+/* Debug only: when `buf` is non-null every later SpMM main-kernel launch
+ * writes 4 x uint64 s_memrealtime stamps (100 MHz) per workgroup to it
+ * (entry, items staged, chunk walked, exit).  Not thread-safe; pass NULL to stop. */
+void gcnk_debug_set_stamps(void* buf);
 
 #ifdef __cplusplus
 }

@@ -1,0 +1,57 @@
+"""Debug timeline of the SpMM main kernel: per-workgroup s_memrealtime stamps
+(100 MHz) at entry / items staged / chunk walked / exit.  Prints a summary per
+case (kernel span, per-phase medians, how dispatch start times spread)."""
+import json
+import os
+import sys
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, ROOT)
+
+
+def main():
+    import numpy as np
+    import torch
+    import gcn_amd  # noqa: F401
+    from graph_convolutional_networks_for_text_classification_amd import _lib, datasets, ops
+    from graph_convolutional_networks_for_text_classification_amd.sparse import as_csr
+
+    dev = torch.device("cuda", 0)
+    lib = _lib.load()
+    r8 = datasets.load_r8_fixture(os.path.join(ROOT, "tests", "golden", "r8_graph.npz"))
+    A = as_csr(r8["adj"].to(dev))
+    X = as_csr(r8["features"].to(dev))
+    cases = [("R8_A_F200", A, 200, 0, None), ("R8_A_F200_l32i16", A, 200, 32, 16), ("R8_A_F8", A, 8, 0, None),
+             ("R8_X_F200", X, 200, 0, None)]
+    for name, a, F, lanes, ipc in cases:
+        B = torch.randn(a.shape[1], F, device=dev)
+        out = torch.empty(a.shape[0], F, device=dev)
+        for _ in range(3):
+            ops.spmm(a, B, out=out, lanes=lanes, ipc=ipc)
+        torch.cuda.synchronize()
+        buf = torch.zeros(4 * 200000, dtype=torch.int64, device=dev)
+        lib.gcnk_debug_set_stamps(buf.data_ptr())
+        ops.spmm(a, B, out=out, lanes=lanes, ipc=ipc)
+        torch.cuda.synchronize()
+        lib.gcnk_debug_set_stamps(None)
+        s = buf.view(-1, 4).cpu().numpy()
+        s = s[s[:, 0] > 0].astype(np.float64)
+        t0 = s[:, 0].min()
+        s = (s - t0) / 100.0  # µs
+        span = s[:, 3].max()
+        res = {
+            "case": name, "wgs": int(len(s)), "span_us": round(span, 2),
+            "entry_p50_us": round(float(np.median(s[:, 0])), 2), "entry_max_us": round(float(s[:, 0].max()), 2),
+            "stage_p50_us": round(float(np.median(s[:, 1] - s[:, 0])), 2),
+            "walk_p50_us": round(float(np.median(s[:, 2] - s[:, 1])), 2),
+            "walk_p99_us": round(float(np.percentile(s[:, 2] - s[:, 1], 99)), 2),
+            "combine_p50_us": round(float(np.median(s[:, 3] - s[:, 2])), 2),
+            "wg_p50_us": round(float(np.median(s[:, 3] - s[:, 0])), 2),
+            "wg_max_us": round(float((s[:, 3] - s[:, 0]).max()), 2),
+            "entry_hist": np.histogram(s[:, 0], bins=8)[0].tolist(),
+        }
+        print(json.dumps(res), flush=True)
+
+
+if __name__ == "__main__":
+    main()

@@ -28,10 +28,18 @@ def test_library_exports_every_declared_symbol():
     assert set(declared) == set(_lib.SIGNATURES), "ctypes signatures out of sync with include/gcnk.h"
 
 
+MAGIC = 0x474E4B33  # plan header word 0 ("GNK3")
+
+
+def _hdr(M=10, K=10, groups=4, ipc=16, nslots=0, nslabs=0):
+    h = (ctypes.c_int32 * 16)(MAGIC, M, K, groups, ipc, groups * ipc, 0, 0, nslots, 0, 0, nslabs, 64, 64, 0, 0)
+    return ctypes.cast(h, ctypes.c_void_p), h
+
+
 def test_abi_version_and_error_text():
     lib = _lib.load()
     assert lib.gcnk_abi_version() == _lib.ABI_VERSION == 1
-    rc = lib.gcnk_spmm_csr_f32(None, None, None, -1, 0, 0, None, 4, 0, None, 0, 8, None, 0, None, 0, None, 0,
+    rc = lib.gcnk_spmm_csr_f32(None, None, None, 0, 8, None, 0, None, 0, None, 0,
                                1.0, 1.0, 0, 0, None, 0, 0, None)
     assert rc == _lib.EARG
     assert b"bad argument" in lib.gcnk_last_error()
@@ -49,26 +57,43 @@ def test_argument_validation_without_gpu():
     rc = lib.gcnk_gemm_f32(0, 0, 4, 4, 4096, ctypes.c_void_p(16), 4096, ctypes.c_void_p(16), 4,
                            ctypes.c_void_p(16), 4, None, 0, None, 0, 1.0, 8, None, 0, None)
     assert rc == _lib.EARG
-    # plan buffer too small
-    rc = lib.gcnk_spmm_plan_build(ctypes.c_void_p(16), 10, 100, 8, ctypes.c_void_p(16), 4, None)
+    # plan build without operands
+    rc = lib.gcnk_spmm_plan_build(ctypes.c_void_p(16), None, None, 10, 10, 100, 8, 4, 0.25, ctypes.c_void_p(16), 4,
+                                  None)
     assert rc == _lib.EARG
+    # a header that is not a plan's is refused
+    bad = (ctypes.c_int32 * 16)()
+    rc = lib.gcnk_spmm_csr_f32(ctypes.c_void_p(16), ctypes.cast(bad, ctypes.c_void_p), ctypes.c_void_p(16), 8, 8,
+                               ctypes.c_void_p(16), 8, None, 0, None, 0, 1.0, 1.0, 0, 0, None, 0, 0, None)
+    assert rc == _lib.EARG and b"not a gcnk plan" in lib.gcnk_last_error()
+    # plan/groups mismatch is refused before any launch (F=200 uses 4 groups)
+    h, _keep = _hdr(groups=7)
+    rc = lib.gcnk_spmm_csr_f32(ctypes.c_void_p(16), h, ctypes.c_void_p(16), 200, 200,
+                               ctypes.c_void_p(16), 200, None, 0, None, 0, 1.0, 1.0, 0, 0, None, 0, 0, None)
+    assert rc == _lib.EARG and b"groups" in lib.gcnk_last_error()
+    # workspace too small for the plan's partial slots
+    h, _keep = _hdr(groups=4, nslots=3)
+    rc = lib.gcnk_spmm_csr_f32(ctypes.c_void_p(16), h, ctypes.c_void_p(16), 200, 200,
+                               ctypes.c_void_p(16), 200, None, 0, None, 0, 1.0, 1.0, 0, 0, None, 0, 0, None)
+    assert rc == _lib.EARG and b"workspace" in lib.gcnk_last_error()
     # empty problems are no-ops that succeed without touching the device
-    assert lib.gcnk_spmm_csr_f32(None, None, None, 0, 0, 0, ctypes.c_void_p(16), 4, 0, None, 0, 8, None, 8, None, 0,
-                                 None, 0, 1.0, 1.0, 0, 0, None, 0, 0, None) == _lib.OK
+    h, _keep = _hdr(M=0)
+    assert lib.gcnk_spmm_csr_f32(ctypes.c_void_p(16), h, None, 8, 8, None, 8, None,
+                                 0, None, 0, 1.0, 1.0, 0, 0, None, 0, 0, None) == _lib.OK
     assert lib.gcnk_gemm_f32(0, 0, 0, 5, 5, None, 5, None, 5, None, 5, None, 0, None, 0, 1.0, 1, None, 0,
                              None) == _lib.OK
 
 
 def test_plan_and_workspace_sizes():
     lib = _lib.load()
-    assert lib.gcnk_spmm_plan_chunks(7724, 69130, 32) == (7724 + 69130 + 31) // 32
-    nc = lib.gcnk_spmm_plan_chunks(100, 1000, 16)
-    assert lib.gcnk_spmm_plan_bytes(100, 1000, 16) == 4 * (4 + 2 * (nc + 1) + nc + nc + 2 * nc + nc)
-    assert lib.gcnk_spmm_workspace_bytes(10, 198) == 10 * 200 * 4
+    assert lib.gcnk_spmm_groups(200, 0) == 4 and lib.gcnk_spmm_groups(8, 0) == 32
+    assert lib.gcnk_spmm_groups(7, 0) == 32 and lib.gcnk_spmm_groups(200, 16) == 16
+    h, _keep = _hdr(nslots=10, nslabs=3)
+    assert lib.gcnk_spmm_workspace_bytes(h, 198) == 8192 + 3 * 64 * 208 * 4
     assert lib.gcnk_gemm_workspace_bytes(200, 8, 7724, 4) == 4 * 200 * 8 * 4
     assert lib.gcnk_colsum_workspace_bytes(7724, 200) == ((7724 + 63) // 64) * 200 * 4
-    ipc = lib.gcnk_spmm_default_ipc(7724, 69130, 200)
-    assert 4 <= ipc <= 64 and ipc % 4 == 0
+    ipc = lib.gcnk_spmm_default_ipc(7724, 69130, 200, 0)
+    assert 2 <= ipc <= 64
 
 
 def test_product_path_refuses_cpu_tensors(r8):

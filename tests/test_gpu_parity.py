@@ -90,6 +90,58 @@ def test_spmm_schedule_variants(ipc, lanes):
     _close(got, csr_ref.spmm_csr(rp, ci, v, B), atol=2e-5 * np.sqrt(700))
 
 
+def _mixed_density_csr(rng, M, K):
+    """Row blocks of every kind the hybrid plan distinguishes: a dense band over
+    few columns (R8 X's document rows), fully dense rows spanning several
+    64-column chunks (X's topic rows), heavy sparse rows, light rows, empty rows."""
+    rows, cols = [], []
+    for r in range(M):
+        if r < 130:                       # dense over columns 0..49
+            c = np.arange(50)
+        elif 300 <= r < 341:              # fully dense
+            c = np.arange(K)
+        elif r % 97 == 5:                 # heavy sparse
+            c = rng.choice(K, 400, replace=False)
+        elif r % 7 == 0:                  # empty
+            c = np.zeros(0, np.int64)
+        else:
+            c = rng.choice(K, int(rng.integers(1, 9)), replace=False)
+        rows.append(np.full(len(c), r))
+        cols.append(c)
+    rows, cols = np.concatenate(rows), np.concatenate(cols)
+    return csr_ref.coo_to_csr(rows, cols, rng.standard_normal(rows.size).astype(np.float32), (M, K))
+
+
+@pytest.mark.parametrize("F", [1, 7, 8, 64, 200, 256, 300])
+def test_spmm_hybrid_dense_blocks(F):
+    rng = np.random.default_rng(F + 1)
+    M, K = 700, 900
+    rp, ci, v = _mixed_density_csr(rng, M, K)
+    a = from_arrays(rp, ci, v, (M, K), DEV)
+    B = rng.standard_normal((K, F)).astype(np.float32)
+    bias = rng.standard_normal(F).astype(np.float32)
+    mask = (rng.random((M, F)) < 0.6).astype(np.uint8)
+    got = spmm(a, torch.from_numpy(B).to(DEV), bias=torch.from_numpy(bias).to(DEV),
+               epilogue=_lib.EPI_BIAS_RELU_DROP, mask=torch.from_numpy(mask).to(DEV), scale=1.5)
+    acc = csr_ref.spmm_csr(rp, ci, v, B)
+    _close(got, csr_ref.spmm_epilogue(acc, bias, relu=True, mask=mask, scale=1.5), atol=2e-5 * np.sqrt(K))
+    hdr = list(a._plans.values())[0].header
+    assert hdr[9] > 0 and hdr[10] > 0, "dense blocks (single and multi-chunk) expected on the tile path"
+    # tile path disabled: the path kernel alone gives the same product
+    got2 = spmm(a, torch.from_numpy(B).to(DEV), dense=2.0)
+    _close(got2, acc, atol=2e-5 * np.sqrt(K))
+
+
+def test_spmm_r8_features_use_tile_path(r8):
+    x = from_torch(r8["features"].to(DEV))
+    W = torch.randn(r8["nfeat"], 200, generator=torch.Generator().manual_seed(4))
+    got = spmm(x, W.to(DEV))
+    hdr = list(x._plans.values())[0].header
+    assert hdr[9] > 0 and hdr[6] == 0, "R8 X: every row block is dense over its condensed columns"
+    rp, ci, v = (t.cpu().numpy() for t in (x.rowptr, x.colind, x.val))
+    _close(got, csr_ref.spmm_csr(rp, ci, v, W.numpy()), atol=1e-4)
+
+
 def test_spmm_deterministic():
     rng = np.random.default_rng(7)
     rp, ci, v = _random_csr(2000, 2000, 30000, rng, heavy_rows=(3,), heavy_deg=9000)

@@ -134,13 +134,97 @@ __global__ void scatter_items_kernel(const int32_t* __restrict__ rowptr, const i
 }
 
 // ---------------------------------------------------------------------------
+// Fused dense projection of a finished row: C2[row, :P] = h[row, :F] * W[F, P]
+// (the gc2 support H1 W2 of reference layer.py:102, computed while H1's row
+// is still in registers).  Each lane holds W rows of its own columns; the
+// group's partial sums meet by an xor butterfly over its LPR lanes.
+struct ProjArgs {
+  const float* W;  // [F x P] row-major; null = no projection
+  int64_t ldw;
+  int32_t P;
+  float* C2;       // [M x P]
+  int64_t ldc2;
+  int32_t store_main;  // also store C (the SpMM output itself)
+};
+
+template <int NP, int LPR, int VPL, int VEC>
+struct Proj {
+  float w[VPL * VEC][NP > 0 ? NP : 1];
+  __device__ __forceinline__ void load(const ProjArgs& pa, int32_t F, const int64_t* colv, const bool* colok) {
+    if constexpr (NP > 0) {
+#pragma unroll
+      for (int v = 0; v < VPL; ++v)
+#pragma unroll
+        for (int i = 0; i < VEC; ++i)
+#pragma unroll
+          for (int c = 0; c < NP; ++c) {
+            const int64_t col = colv[v] + i;
+            w[v * VEC + i][c] = (colok[v] && col < F && c < pa.P) ? pa.W[col * pa.ldw + c] : 0.f;
+          }
+    }
+  }
+  template <typename T>
+  __device__ __forceinline__ void apply(const ProjArgs& pa, const T* h, int64_t row, int lg) const {
+    if constexpr (NP > 0) {
+      float s[NP];
+#pragma unroll
+      for (int c = 0; c < NP; ++c) s[c] = 0.f;
+#pragma unroll
+      for (int v = 0; v < VPL; ++v) {
+        const float* hv = reinterpret_cast<const float*>(&h[v]);
+#pragma unroll
+        for (int i = 0; i < VEC; ++i)
+#pragma unroll
+          for (int c = 0; c < NP; ++c) s[c] = fmaf(hv[i], w[v * VEC + i][c], s[c]);
+      }
+      // transpose-reduce: while channels remain to split, each xor step sends the
+      // half of the channels the partner keeps (n/2 shuffles instead of n), so a
+      // lane ends with NP/2^h channels summed over 2^h lanes; plain xor steps finish.
+      int chan = 0;
+      reduce_split<NP>(s, lg, chan);
+      constexpr int H = ilog2(NP) < ilog2(LPR) ? ilog2(NP) : ilog2(LPR);
+      constexpr int NR = NP >> H;          // channels left per lane
+      constexpr int REST = LPR >> H;       // lanes still to sum over
+#pragma unroll
+      for (int off = REST / 2; off >= 1; off >>= 1)
+#pragma unroll
+        for (int c = 0; c < NR; ++c) s[c] += __shfl_xor(s[c], off, 64);
+      if ((lg & (REST - 1)) == 0) {
+#pragma unroll
+        for (int c = 0; c < NR; ++c)
+          if (chan + c < pa.P) pa.C2[row * pa.ldc2 + chan + c] = s[c];
+      }
+    }
+  }
+
+  static constexpr int ilog2(int x) { return x <= 1 ? 0 : 1 + ilog2(x >> 1); }
+
+  // One halving step per recursion level, offsets LPR/2, LPR/4, ... while n > 1.
+  template <int N, int OFF = LPR / 2>
+  __device__ __forceinline__ static void reduce_split(float* s, int lg, int& chan) {
+    if constexpr (N > 1 && OFF >= 1) {
+      constexpr int Hn = N / 2;
+      const bool up = (lg & OFF) != 0;
+#pragma unroll
+      for (int c = 0; c < Hn; ++c) {
+        const float keep = up ? s[c + Hn] : s[c];
+        const float send = up ? s[c] : s[c + Hn];
+        s[c] = keep + __shfl_xor(send, OFF, 64);
+      }
+      if (up) chan += Hn;
+      reduce_split<Hn, OFF / 2>(s, lg, chan);
+    }
+  }
+};
+
+// ---------------------------------------------------------------------------
 // Path kernel (gathers).
-template <int BLOCK, int LPR, int VPL, int VEC, int U>
+template <int BLOCK, int LPR, int VPL, int VEC, int U, int NP>
 __global__ void __launch_bounds__(BLOCK)
 spmm_path_kernel(const int2* __restrict__ items, const int32_t* __restrict__ head_slot,
                  const int32_t* __restrict__ tail_slot, int32_t ipc, const float* __restrict__ B, int64_t ldb,
                  int32_t F, float* __restrict__ C, int64_t ldc, Epi epi, float* __restrict__ part,
-                 int64_t part_ld) {
+                 int64_t part_ld, ProjArgs pa) {
   using V = Vec<VEC>;
   using T = typename V::T;
   constexpr int G = BLOCK / LPR;
@@ -179,6 +263,9 @@ spmm_path_kernel(const int2* __restrict__ items, const int32_t* __restrict__ hea
     colok[v] = colv[v] < F;
     bv[v] = (epi.bias && colok[v]) ? V::load(epi.bias + colv[v]) : V::zero();
   }
+  Proj<NP, LPR, VPL, VEC> proj;
+  proj.load(pa, F, colv, colok);
+  const bool store_main = NP == 0 || pa.store_main;
   float* myH = s_H + g * FT;
   float* myT = s_T + g * FT;
 
@@ -216,9 +303,13 @@ spmm_path_kernel(const int2* __restrict__ items, const int32_t* __restrict__ hea
           head_row = r;
         } else {
           float* dst = C + (int64_t)r * ldc;
+          T h[VPL];
 #pragma unroll
-          for (int v = 0; v < VPL; ++v)
-            if (colok[v]) V::store(dst + colv[v], V::epi(epi, acc[v], bv[v], r, colv[v]));
+          for (int v = 0; v < VPL; ++v) {
+            h[v] = colok[v] ? V::epi(epi, acc[v], bv[v], r, colv[v]) : V::zero();
+            if (colok[v] && store_main) V::store(dst + colv[v], h[v]);
+          }
+          proj.apply(pa, h, r, lg);
         }
         has_marker = true;
 #pragma unroll
@@ -249,16 +340,23 @@ spmm_path_kernel(const int2* __restrict__ items, const int32_t* __restrict__ hea
     // the row starts in group j's tail if j ends inside a row, else at group j+1
     const int jf = (j >= 0 && s_meta[4 * j + 2]) ? j : j + 1;
     const bool from_before = j < 0 && s_meta[1];  // the row started in an earlier window
+    T h[VPL];
 #pragma unroll
     for (int v = 0; v < VPL; ++v) {
       const int off = (v * LPR + lg) * VEC;
       T s = V::zero();
       for (int q = jf; q < g; ++q) V::add(s, V::load(s_T + q * FT + off));
       V::add(s, V::load(myH + off));
+      h[v] = V::zero();
       if (!colok[v]) continue;
-      if (from_before) V::store(part + (int64_t)hslot * part_ld + colv[v], s);
-      else V::store(C + (int64_t)head_row * ldc + colv[v], V::epi(epi, s, bv[v], head_row, colv[v]));
+      if (from_before) {
+        V::store(part + (int64_t)hslot * part_ld + colv[v], s);
+      } else {
+        h[v] = V::epi(epi, s, bv[v], head_row, colv[v]);
+        if (store_main) V::store(C + (int64_t)head_row * ldc + colv[v], h[v]);
+      }
     }
+    if (!from_before) proj.apply(pa, h, head_row, lg);
   }
   // ---- a heavy row leaving the window: partial of its part in this window
   if (g == G - 1 && tail) {
@@ -280,10 +378,10 @@ spmm_path_kernel(const int2* __restrict__ items, const int32_t* __restrict__ hea
 // slot (= path) order, apply the epilogue, store the row.  One workgroup per
 // row: P = 256/LPR slot lanes take slots strided by P, then the P partial
 // sums are added in lane order through LDS.
-template <int LPR, int VPL, int VEC>
+template <int LPR, int VPL, int VEC, int NP>
 __global__ void __launch_bounds__(256)
 spmm_fixup_kernel(const int32_t* __restrict__ fix, int32_t nfix, int32_t F, const float* __restrict__ part,
-                  int64_t part_ld, float* __restrict__ C, int64_t ldc, Epi epi) {
+                  int64_t part_ld, float* __restrict__ C, int64_t ldc, Epi epi, ProjArgs pa) {
   using V = Vec<VEC>;
   using T = typename V::T;
   constexpr int P = 256 / LPR;
@@ -315,15 +413,27 @@ spmm_fixup_kernel(const int32_t* __restrict__ fix, int32_t nfix, int32_t F, cons
   }
   __syncthreads();
   if (p != 0) return;
+  int64_t colv[VPL];
+  bool colok[VPL];
+  T h[VPL];
 #pragma unroll
   for (int v = 0; v < VPL; ++v) {
     const int off = (v * LPR + lg) * VEC;
     const int64_t col = col_base + off;
+    colv[v] = col;
+    colok[v] = col < F;
+    h[v] = V::zero();
     if (col >= F) continue;
     T acc = V::load(s_acc + off);
     for (int q = 1; q < P; ++q) V::add(acc, V::load(s_acc + q * FT + off));
     const T b = epi.bias ? V::load(epi.bias + col) : V::zero();
-    V::store(C + (int64_t)r * ldc + col, V::epi(epi, acc, b, r, col));
+    h[v] = V::epi(epi, acc, b, r, col);
+    if (NP == 0 || pa.store_main) V::store(C + (int64_t)r * ldc + col, h[v]);
+  }
+  if constexpr (NP > 0) {
+    Proj<NP, LPR, VPL, VEC> proj;
+    proj.load(pa, F, colv, colok);
+    proj.apply(pa, h, r, lg);
   }
 }
 
@@ -529,28 +639,30 @@ struct Launch {
   float* part;  // path partial slots
   int64_t part_ld;
   int col_tiles;
+  ProjArgs pa;
   hipStream_t s;
 };
 
-template <int BLOCK, int LPR, int VPL, int VEC>
+template <int BLOCK, int LPR, int VPL, int VEC, int NP>
 int launch_path(const Launch& a) {
   constexpr int G = BLOCK / LPR;
-  constexpr int U = (16 / VPL) < 2 ? 2 : 16 / VPL;
+  constexpr int UB = NP > 0 ? 8 : 16;  // the projection holds W in registers: shorter batches
+  constexpr int U = (UB / VPL) < 2 ? 2 : UB / VPL;
   const size_t lds = lds_bytes(G, a.ipc, LPR * VPL * VEC);
   if (lds > (size_t)kMaxLds) {
     set_error("gcnk_spmm_csr_f32: ipc %d needs %zu B of LDS (> %d) at %d groups", a.ipc, lds, kMaxLds, G);
     return GCNK_EUNSUP;
   }
   if (a.L.nwin > 0) {
-    hipLaunchKernelGGL((spmm_path_kernel<BLOCK, LPR, VPL, VEC, U>), dim3((unsigned)a.L.nwin, a.col_tiles),
+    hipLaunchKernelGGL((spmm_path_kernel<BLOCK, LPR, VPL, VEC, U, NP>), dim3((unsigned)a.L.nwin, a.col_tiles),
                        dim3(BLOCK), lds, a.s, reinterpret_cast<const int2*>(a.plan + a.L.items), a.plan + a.L.head,
-                       a.plan + a.L.tail, a.ipc, a.B, a.ldb, a.F, a.C, a.ldc, a.epi, a.part, a.part_ld);
+                       a.plan + a.L.tail, a.ipc, a.B, a.ldb, a.F, a.C, a.ldc, a.epi, a.part, a.part_ld, a.pa);
     int rc = launch_check("spmm_path_kernel");
     if (rc) return rc;
   }
   if (a.nfix > 0) {
-    hipLaunchKernelGGL((spmm_fixup_kernel<LPR, VPL, VEC>), dim3((unsigned)a.nfix, a.col_tiles), dim3(256), 0, a.s,
-                       a.plan + a.L.fix, a.nfix, a.F, a.part, a.part_ld, a.C, a.ldc, a.epi);
+    hipLaunchKernelGGL((spmm_fixup_kernel<LPR, VPL, VEC, NP>), dim3((unsigned)a.nfix, a.col_tiles), dim3(256), 0,
+                       a.s, a.plan + a.L.fix, a.nfix, a.F, a.part, a.part_ld, a.C, a.ldc, a.epi, a.pa);
     return launch_check("spmm_fixup_kernel");
   }
   return GCNK_OK;
@@ -559,7 +671,7 @@ int launch_path(const Launch& a) {
 template <int VEC>
 int dispatch_path(const Cfg& c, const Launch& a) {
 #define GCNK_CASE(BL, L, P) \
-  if (c.block == BL && c.lpr == L && c.vpl == P) return launch_path<BL, L, P, VEC>(a);
+  if (c.block == BL && c.lpr == L && c.vpl == P) return launch_path<BL, L, P, VEC, 0>(a);
   GCNK_CASE(64, 1, 1) GCNK_CASE(64, 2, 1) GCNK_CASE(64, 4, 1) GCNK_CASE(256, 8, 1) GCNK_CASE(256, 16, 1)
   GCNK_CASE(256, 32, 1) GCNK_CASE(256, 64, 1) GCNK_CASE(64, 1, 2) GCNK_CASE(64, 2, 2) GCNK_CASE(64, 4, 2)
   GCNK_CASE(256, 8, 2) GCNK_CASE(256, 16, 2) GCNK_CASE(256, 32, 2) GCNK_CASE(256, 64, 2) GCNK_CASE(64, 1, 4)
@@ -567,6 +679,18 @@ int dispatch_path(const Cfg& c, const Launch& a) {
   GCNK_CASE(256, 64, 4)
 #undef GCNK_CASE
   set_error("gcnk_spmm_csr_f32: unsupported lanes/vectors config (%d,%d)", c.lpr, c.vpl);
+  return GCNK_EUNSUP;
+}
+
+// Fused projection variants: float4 columns, one column tile, groups of >= 16 lanes.
+template <int NP>
+int dispatch_path_proj(const Cfg& c, const Launch& a) {
+#define GCNK_CASE(L, P) \
+  if (c.block == 256 && c.lpr == L && c.vpl == P) return launch_path<256, L, P, 4, NP>(a);
+  GCNK_CASE(16, 1) GCNK_CASE(32, 1) GCNK_CASE(64, 1) GCNK_CASE(16, 2) GCNK_CASE(32, 2) GCNK_CASE(64, 2)
+  GCNK_CASE(16, 4) GCNK_CASE(32, 4) GCNK_CASE(64, 4)
+#undef GCNK_CASE
+  set_error("gcnk_spmm_proj_f32: no fused-projection kernel for lanes/vectors (%d,%d)", c.lpr, c.vpl);
   return GCNK_EUNSUP;
 }
 
@@ -846,17 +970,22 @@ extern "C" int64_t gcnk_spmm_workspace_bytes(const int32_t* hdr, int32_t F) {
   return ((path + 255) & ~255LL) + slabs;
 }
 
-extern "C" int gcnk_spmm_csr_f32(const void* plan, const int32_t* hdr, const float* B, int64_t ldb, int32_t F,
-                                 float* C, int64_t ldc, const float* bias, int32_t epilogue, const uint8_t* drop_mask,
-                                 int64_t ldm, float drop_scale, float keep_prob, uint64_t seed, uint64_t offset,
-                                 float* workspace, int64_t workspace_bytes, int32_t lanes_hint, void* stream) {
+static int spmm_impl(const void* plan, const int32_t* hdr, const float* B, int64_t ldb, int32_t F, float* C,
+                     int64_t ldc, const float* bias, int32_t epilogue, const uint8_t* drop_mask, int64_t ldm,
+                     float drop_scale, float keep_prob, uint64_t seed, uint64_t offset, float* workspace,
+                     int64_t workspace_bytes, int32_t lanes_hint, const ProjArgs& pa, void* stream) {
   if (!plan || !hdr || hdr[0] != kMagic || F < 0) {
     set_error("gcnk_spmm_csr_f32: bad argument (plan/header missing or not a gcnk plan, F=%d)", F);
     return GCNK_EARG;
   }
   const int32_t M = hdr[1], K = hdr[2], groups = hdr[3], ipc = hdr[4];
   if (M == 0 || F == 0) return GCNK_OK;
-  if (!C || (K > 0 && !B)) {
+  const bool proj = pa.W != nullptr;
+  if (proj && (!pa.C2 || pa.P <= 0 || pa.ldw < pa.P || pa.ldc2 < pa.P)) {
+    set_error("gcnk_spmm_proj_f32: bad projection (P=%d)", pa.P);
+    return GCNK_EARG;
+  }
+  if ((!C && (!proj || pa.store_main)) || (K > 0 && !B)) {
     set_error("gcnk_spmm_csr_f32: null pointer");
     return GCNK_EARG;
   }
@@ -898,6 +1027,15 @@ extern "C" int gcnk_spmm_csr_f32(const void* plan, const int32_t* hdr, const flo
   e.stamps = g_stamps;
   const bool vec4 = (F % 4 == 0) && (ldb % 4 == 0) && (ldc % 4 == 0) && aligned16(B) && aligned16(C) &&
                     (!workspace || aligned16(workspace)) && (!bias || aligned16(bias));
+  if (proj) {
+    // the projection needs whole rows in one group: path rows only, float4, one column tile
+    const Cfg c = choose_cfg(F, 4, lpr);
+    if (hdr[9] > 0 || !vec4 || c.col_tiles != 1 || pa.P > 32 || lpr < 16) {
+      set_error("gcnk_spmm_proj_f32: fused projection unsupported here (tile rows=%d vec4=%d col_tiles=%d P=%d lanes=%d)",
+                hdr[9], (int)vec4, c.col_tiles, pa.P, lpr);
+      return GCNK_EUNSUP;
+    }
+  }
   hipStream_t s = (hipStream_t)stream;
   const int32_t* p = (const int32_t*)plan;
   const Layout L(hdr);
@@ -934,8 +1072,33 @@ extern "C" int gcnk_spmm_csr_f32(const void* plan, const int32_t* hdr, const flo
   // ---- remaining rows: path kernel (+ fix-up)
   if (L.nwin > 0) {
     const Cfg c = choose_cfg(F, vec4 ? 4 : 1, lpr);
-    Launch a{p, L, ipc, (int32_t)L.nfix, B, ldb, F, C, ldc, e, workspace, part_ld, c.col_tiles, s};
+    Launch a{p, L, ipc, (int32_t)L.nfix, B, ldb, F, C, ldc, e, workspace, part_ld, c.col_tiles, pa, s};
+    if (proj) return pa.P <= 8 ? dispatch_path_proj<8>(c, a) : dispatch_path_proj<32>(c, a);
     return vec4 ? dispatch_path<4>(c, a) : dispatch_path<1>(c, a);
   }
   return GCNK_OK;
+}
+
+extern "C" int gcnk_spmm_csr_f32(const void* plan, const int32_t* hdr, const float* B, int64_t ldb, int32_t F,
+                                 float* C, int64_t ldc, const float* bias, int32_t epilogue, const uint8_t* drop_mask,
+                                 int64_t ldm, float drop_scale, float keep_prob, uint64_t seed, uint64_t offset,
+                                 float* workspace, int64_t workspace_bytes, int32_t lanes_hint, void* stream) {
+  const ProjArgs none{nullptr, 0, 0, nullptr, 0, 1};
+  return spmm_impl(plan, hdr, B, ldb, F, C, ldc, bias, epilogue, drop_mask, ldm, drop_scale, keep_prob, seed, offset,
+                   workspace, workspace_bytes, lanes_hint, none, stream);
+}
+
+extern "C" int gcnk_spmm_proj_f32(const void* plan, const int32_t* hdr, const float* B, int64_t ldb, int32_t F,
+                                  float* C, int64_t ldc, const float* bias, int32_t epilogue,
+                                  const uint8_t* drop_mask, int64_t ldm, float drop_scale, float keep_prob,
+                                  uint64_t seed, uint64_t offset, const float* W, int64_t ldw, int32_t P, float* C2,
+                                  int64_t ldc2, float* workspace, int64_t workspace_bytes, int32_t lanes_hint,
+                                  void* stream) {
+  if (!W) {
+    set_error("gcnk_spmm_proj_f32: null projection matrix");
+    return GCNK_EARG;
+  }
+  const ProjArgs pa{W, ldw, P, C2, ldc2, C != nullptr};
+  return spmm_impl(plan, hdr, B, ldb, F, C, ldc, bias, epilogue, drop_mask, ldm, drop_scale, keep_prob, seed, offset,
+                   workspace, workspace_bytes, lanes_hint, pa, stream);
 }

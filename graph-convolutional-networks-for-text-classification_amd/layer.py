@@ -101,5 +101,7 @@ class GCN(Module):
         a = as_csr(adj)
         xop = Operand(x)
         epi, mask, scale, keep, seed, offset = self._dropout_args(a.shape[0], a.device)
+        # H1 is needed only by a backward pass; inference never writes it to HBM
+        keep_h1 = torch.is_grad_enabled() and any(p.requires_grad for p in self.parameters())
         return GCNFn.apply(self.gc1.weight, self.gc1.bias, self.gc2.weight, self.gc2.bias, xop, a,
-                           epi, mask, scale, keep, seed, offset)
+                           epi, mask, scale, keep, seed, offset, keep_h1)

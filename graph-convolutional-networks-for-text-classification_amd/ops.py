@@ -79,6 +79,54 @@ def spmm(a, B, bias=None, epilogue=_lib.EPI_NONE, mask=None, scale=1.0, keep_pro
     return out
 
 
+def spmm_proj(a, B, W, bias=None, epilogue=_lib.EPI_NONE, mask=None, scale=1.0, keep_prob=1.0, seed=0, offset=0,
+              store_main=True, ipc=None, lanes=0):
+    """(H, C2) with H = epi(A @ B) and C2 = H @ W, the projection fused into
+    the SpMM epilogue (gcnk_spmm_proj_f32): gc1's aggregation + bias + ReLU +
+    dropout (reference layer.py:106,110,182,185) followed by gc2's support
+    ``th.spmm(H1, W2)`` (layer.py:102) while H1's row is in registers.  With
+    ``store_main=False`` H is never written (returned as None).  Where the
+    fused kernel does not apply (library returns unsupported) the same result
+    comes from gcnk_spmm_csr_f32 + gcnk_gemm_f32."""
+    a = as_csr(a)
+    B = _dense_f32(B, "dense operand")
+    W = _dense_f32(W, "projection")
+    M, K = a.shape
+    F = B.shape[1]
+    if B.shape[0] != K or W.shape[0] != F:
+        raise RuntimeError(f"spmm_proj shape mismatch: {tuple(a.shape)} @ {tuple(B.shape)} @ {tuple(W.shape)}")
+    P = W.shape[1]
+    lib = _lib.load()
+    if ipc is None:
+        ipc = default_ipc(a, F, lanes)
+    groups = int(lib.gcnk_spmm_groups(F, int(lanes)))
+    plan = a.plan(ipc, groups, DENSE_THRESHOLD)
+    H = torch.empty((M, F), dtype=torch.float32, device=B.device) if store_main else None
+    C2 = torch.empty((M, P), dtype=torch.float32, device=B.device)
+    if bias is not None:
+        bias = bias.contiguous()
+    if mask is not None:
+        mask = mask.contiguous()
+    wsb = plan.workspace_bytes(F)
+    ws = torch.empty((wsb + 3) // 4, dtype=torch.float32, device=B.device) if wsb > 0 else None
+    with torch.cuda.device(B.device):
+        rc = lib.gcnk_spmm_proj_f32(
+            _ptr(plan.buf), ctypes.cast(plan.hdr, ctypes.c_void_p),
+            _ptr(B), B.stride(0), F,
+            _ptr(H), F,
+            _ptr(bias), epilogue,
+            _ptr(mask), mask.stride(0) if mask is not None else 0, float(scale),
+            float(keep_prob), int(seed) & (2**64 - 1), int(offset) & (2**64 - 1),
+            _ptr(W), W.stride(0), P, _ptr(C2), C2.stride(0),
+            _ptr(ws), wsb, int(lanes), _stream(B.device))
+    if rc == _lib.EUNSUP:
+        H = spmm(a, B, bias=bias, epilogue=epilogue, mask=mask, scale=scale, keep_prob=keep_prob, seed=seed,
+                 offset=offset, ipc=ipc, lanes=lanes)
+        return (H if store_main else None), gemm(H, W)
+    _lib.check(rc, "gcnk_spmm_proj_f32")
+    return H, C2
+
+
 def gemm(A, B, transA=False, transB=False, bias=None, epilogue=_lib.GEMM_EPI_NONE, R=None, scale=1.0,
          split_k=None, out=None):
     """C = epi(op(A) @ op(B)) on fp32 MFMA.
@@ -193,7 +241,8 @@ class GCNFn(torch.autograd.Function):
 
         S1 = X W1                   spmm (sparse X) / gemm (dense X)      layer.py:102
         H1 = drop(relu(A S1 + b1))  spmm + fused epilogue                 layer.py:106,110,182,185
-        S2 = H1 W2                  fp32 MFMA gemm                         layer.py:102 (gc2)
+        S2 = H1 W2                  projection fused into that epilogue   layer.py:102 (gc2)
+                                    (H1 kept only when a backward needs it)
         Z  = A S2 + b2              spmm + bias epilogue                   layer.py:106,110 (gc2)
 
     Backward (trainer.py:361):
@@ -204,11 +253,10 @@ class GCNFn(torch.autograd.Function):
     """
 
     @staticmethod
-    def forward(ctx, W1, b1, W2, b2, xop, adj, epi, mask, scale, keep, seed, offset):
+    def forward(ctx, W1, b1, W2, b2, xop, adj, epi, mask, scale, keep, seed, offset, keep_h1=True):
         S1 = xop.times(W1)
-        H1 = spmm(adj, S1, bias=b1, epilogue=epi, mask=mask, scale=scale, keep_prob=keep, seed=seed,
-                  offset=offset)
-        S2 = gemm(H1, W2)
+        H1, S2 = spmm_proj(adj, S1, W2, bias=b1, epilogue=epi, mask=mask, scale=scale, keep_prob=keep,
+                           seed=seed, offset=offset, store_main=keep_h1)
         out = spmm(adj, S2, bias=b2, epilogue=_lib.EPI_BIAS if b2 is not None else _lib.EPI_NONE)
         ctx.xop, ctx.adj, ctx.scale = xop, adj, float(scale)
         ctx.has_b1, ctx.has_b2 = b1 is not None, b2 is not None
@@ -234,4 +282,4 @@ class GCNFn(torch.autograd.Function):
             if need[0]:
                 gS1 = spmm(adjT, gZ1)
                 gW1 = ctx.xop.t_times(gS1)
-        return gW1, gb1, gW2, gb2, None, None, None, None, None, None, None, None
+        return gW1, gb1, gW2, gb2, None, None, None, None, None, None, None, None, None

@@ -123,6 +123,24 @@ int gcnk_spmm_csr_f32(const void* plan, const int32_t* plan_header,
                       float* workspace, int64_t workspace_bytes,
                       int32_t lanes_hint, void* stream);
 
+/* SpMM with a fused dense projection of every finished row:
+ *   H = epi(A B)  (stored to C only when C != NULL),   C2[M x P] = H * W[F x P]
+ * i.e. layer.py:106,110,182,185 of gc1 followed by layer.py:102 of gc2
+ * (support2 = H1 W2) while H1's row is still in registers: the gc2 GEMM
+ * launch and, in inference, the H1 round trip through HBM disappear.
+ * Supported for plans without dense tile blocks, float4-aligned operands,
+ * F <= 256 and P <= 32; otherwise returns GCNK_EUNSUP (callers then run
+ * gcnk_spmm_csr_f32 + gcnk_gemm_f32). */
+int gcnk_spmm_proj_f32(const void* plan, const int32_t* plan_header,
+                       const float* B, int64_t ldb, int32_t F,
+                       float* C, int64_t ldc,
+                       const float* bias, int32_t epilogue,
+                       const uint8_t* drop_mask, int64_t ldm, float drop_scale,
+                       float keep_prob, uint64_t seed, uint64_t offset,
+                       const float* W, int64_t ldw, int32_t P, float* C2, int64_t ldc2,
+                       float* workspace, int64_t workspace_bytes,
+                       int32_t lanes_hint, void* stream);
+
 /* ---------------------------------------------------------------------------
  * fp32 GEMM on MFMA (v_mfma_f32_16x16x4_f32; exact fp32 FMA chains):
  *   C[M x N] = epi( op(A)[M x K] * op(B)[K x N] )

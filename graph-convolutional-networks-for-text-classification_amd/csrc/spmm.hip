@@ -29,7 +29,8 @@
 //    vectors interleaved by LPR (one load instruction of a group covers
 //    LPR*VEC contiguous floats of a B row).  Rows split between the groups of
 //    a window meet in LDS; heavy rows crossing windows leave one partial per
-//    window that spmm_fixup_kernel sums in path order.
+//    window, and the last of those windows to finish (arrival counter in the
+//    plan) sums them in path order -- one launch, no fix-up kernel.
 //
 // Every sum has a fixed order (no float atomics): results are bitwise
 // reproducible run to run.
@@ -44,10 +45,11 @@ namespace {
 
 constexpr int32_t kMarker = -1;  // end of row; .y = row index
 constexpr int32_t kPad = -2;     // no-op
-constexpr int32_t kMagic = 0x474e4b33;  // "GNK3"
+constexpr int32_t kMagic = 0x474e4b34;  // "GNK4"
 constexpr int kRB = 64;          // tile rows per dense block (4 waves x 16)
 constexpr int kKC = 64;          // condensed columns per tile chunk (16 MFMA k-steps)
-constexpr int kMaxNT = 14;       // 16-column MFMA n-tiles per tile workgroup (B tile <= 57 KB LDS)
+constexpr int kMaxNT = 14;
+constexpr int kMaxColTiles = 64;  // path column tiles per launch (arrival counters per cross row)       // 16-column MFMA n-tiles per tile workgroup (B tile <= 57 KB LDS)
 
 template <int VEC>
 struct Vec;
@@ -93,21 +95,26 @@ struct Vec<1> {
 // ---------------------------------------------------------------------------
 // Plan layout (int32 words).  Header (16 words, see gcnk.h):
 //   0 magic  1 M  2 K  3 groups  4 ipc  5 W  6 nwin  7 nfix  8 nslots
-//   9 ntile  10 nred  11 nslabs  12 KC  13 RB  14 heavy  15 0
+//   9 ntile (chunks)  10 nred  11 nslabs  12 ntblk (tile blocks)  13 has_diag  14 heavy  15 0
 struct Layout {
-  int64_t nwin, W, nfix, ntile, nred;
-  int64_t items, head, tail, fix, tdesc, tcols, tfrag, red, total;
+  int64_t nwin, W, nfix, ntile, nred, ntblk, has_diag, M;
+  int64_t items, head, tail, hfix, tfix, fix, cnt, tdesc, tcols, tfrag, red, trows, dval, total;
   __host__ __device__ explicit Layout(const int32_t* h) {
-    nwin = h[6]; W = h[5]; nfix = h[7]; ntile = h[9]; nred = h[10];
+    M = h[1]; nwin = h[6]; W = h[5]; nfix = h[7]; ntile = h[9]; nred = h[10]; ntblk = h[12]; has_diag = h[13];
     items = 16;
     head = items + 2 * nwin * W;
     tail = head + nwin;
-    fix = tail + nwin;
-    tdesc = (fix + 3 * nfix + 3) & ~3LL;
+    hfix = tail + nwin;
+    tfix = hfix + nwin;
+    fix = tfix + nwin;
+    cnt = fix + 3 * nfix;
+    tdesc = (cnt + (int64_t)kMaxColTiles * nfix + 3) & ~3LL;
     tcols = tdesc + 4 * ntile;
     tfrag = (tcols + (int64_t)kKC * ntile + 3) & ~3LL;
     red = tfrag + (int64_t)kRB * kKC * ntile;
-    total = red + 4 * nred;
+    trows = red + 4 * nred;
+    dval = trows + (int64_t)kRB * ntblk;
+    total = dval + (has_diag ? M : 0);
   }
 };
 
@@ -219,12 +226,81 @@ struct Proj {
 
 // ---------------------------------------------------------------------------
 // Path kernel (gathers).
+struct PathPlan {
+  const int2* items;
+  const int32_t* head;  // per window: partial slot of the row ending here that began earlier (-1)
+  const int32_t* tail;  // per window: partial slot of the row leaving the window (-1)
+  const int32_t* hfix;  // per window: cross-row index of head / tail partial (-1)
+  const int32_t* tfix;
+  const int32_t* fix;   // per cross row: row, first slot, last slot
+  int32_t* cnt;         // per cross row x column tile: arrival counters (zero between launches)
+};
+
+// Partial slots are written and read with agent-coherent accesses (relaxed
+// agent-scope atomics: sc1, past the per-XCD L2), so publishing them needs no
+// L2 write-back/invalidate: the writer waits for its stores to complete
+// (s_waitcnt vmcnt(0)) before bumping the arrival counter.
+template <typename T>
+__device__ __forceinline__ void store_coherent(float* p, const T& v) {
+  const float* f = reinterpret_cast<const float*>(&v);
+#pragma unroll
+  for (int i = 0; i < (int)(sizeof(T) / 4); ++i) __hip_atomic_store(p + i, f[i], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+template <typename T>
+__device__ __forceinline__ T load_coherent(const float* p) {
+  T v;
+  float* f = reinterpret_cast<float*>(&v);
+#pragma unroll
+  for (int i = 0; i < (int)(sizeof(T) / 4); ++i)
+    f[i] = __hip_atomic_load(const_cast<float*>(p + i), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  return v;
+}
+
+// A group has just stored one partial of cross row `fi` (a heavy row spanning
+// windows).  The last of the row's windows to arrive sums all its partial
+// slots in slot (= path) order, applies the epilogue and stores the row, then
+// re-arms the counter -- no fix-up launch; the sum order is fixed whichever
+// window arrives last.
+template <int LPR, int VPL, int VEC, typename T, typename ProjT>
+__device__ __forceinline__ void finish_cross(const PathPlan& pp, int32_t fi, int lg, const int64_t* colv,
+                                             const bool* colok, const T* bv, const float* part, int64_t part_ld,
+                                             float* C, int64_t ldc, const Epi& epi, bool store_main,
+                                             const ProjT& proj, const ProjArgs& pa) {
+  using V = Vec<VEC>;
+  __builtin_amdgcn_s_waitcnt(0);  // this group's partial stores have completed
+  const int32_t r = pp.fix[3 * fi], sb = pp.fix[3 * fi + 1], se = pp.fix[3 * fi + 2];
+  int32_t* ctr = pp.cnt + (int64_t)fi * kMaxColTiles + blockIdx.y;
+  int last = 0;
+  if (lg == 0) last = __hip_atomic_fetch_add(ctr, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == se - sb;
+  last = __shfl(last, (int)(threadIdx.x & 63) - lg, 64);
+  if (!last) return;
+  T h[VPL];
+#pragma unroll
+  for (int v = 0; v < VPL; ++v) {
+    h[v] = V::zero();
+    if (!colok[v]) continue;
+    T acc = V::zero();
+    const float* p = part + (int64_t)sb * part_ld + colv[v];
+    int32_t q = sb;
+    for (; q + 3 <= se; q += 4, p += 4 * part_ld) {
+      const T p0 = load_coherent<T>(p), p1 = load_coherent<T>(p + part_ld), p2 = load_coherent<T>(p + 2 * part_ld),
+              p3 = load_coherent<T>(p + 3 * part_ld);
+      V::add(acc, p0); V::add(acc, p1); V::add(acc, p2); V::add(acc, p3);
+    }
+    for (; q <= se; ++q, p += part_ld) V::add(acc, load_coherent<T>(p));
+    h[v] = V::epi(epi, acc, bv[v], r, colv[v]);
+    if (store_main) V::store(C + (int64_t)r * ldc + colv[v], h[v]);
+  }
+  proj.apply(pa, h, r, lg);
+  if (lg == 0) __hip_atomic_store(ctr, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+
 template <int BLOCK, int LPR, int VPL, int VEC, int U, int NP>
 __global__ void __launch_bounds__(BLOCK)
-spmm_path_kernel(const int2* __restrict__ items, const int32_t* __restrict__ head_slot,
-                 const int32_t* __restrict__ tail_slot, int32_t ipc, const float* __restrict__ B, int64_t ldb,
-                 int32_t F, float* __restrict__ C, int64_t ldc, Epi epi, float* __restrict__ part,
-                 int64_t part_ld, ProjArgs pa) {
+spmm_path_kernel(PathPlan pp, int32_t ipc, const float* __restrict__ B, int64_t ldb, int32_t F,
+                 float* __restrict__ C, int64_t ldc, Epi epi, float* __restrict__ part, int64_t part_ld,
+                 ProjArgs pa) {
+  const int2* __restrict__ items = pp.items;
   using V = Vec<VEC>;
   using T = typename V::T;
   constexpr int G = BLOCK / LPR;
@@ -246,8 +322,8 @@ spmm_path_kernel(const int2* __restrict__ items, const int32_t* __restrict__ hea
   for (int i = tid; i < W; i += BLOCK) s_item[1 + i] = items[base + i];
   if (tid == 0) s_item[0] = w > 0 ? items[base - 1] : make_int2(kMarker, -1);
   stamp(epi, 0);
-  const int32_t hslot = head_slot[w];
-  const int32_t tslot = tail_slot[w];
+  const int32_t hslot = pp.head[w];
+  const int32_t tslot = pp.tail[w];
   __syncthreads();
   stamp(epi, 1);
 
@@ -350,13 +426,15 @@ spmm_path_kernel(const int2* __restrict__ items, const int32_t* __restrict__ hea
       h[v] = V::zero();
       if (!colok[v]) continue;
       if (from_before) {
-        V::store(part + (int64_t)hslot * part_ld + colv[v], s);
+        store_coherent(part + (int64_t)hslot * part_ld + colv[v], s);
       } else {
         h[v] = V::epi(epi, s, bv[v], head_row, colv[v]);
         if (store_main) V::store(C + (int64_t)head_row * ldc + colv[v], h[v]);
       }
     }
     if (!from_before) proj.apply(pa, h, head_row, lg);
+    else finish_cross<LPR, VPL, VEC>(pp, pp.hfix[w], lg, colv, colok, bv, part, part_ld, C, ldc, epi, store_main,
+                                     proj, pa);
   }
   // ---- a heavy row leaving the window: partial of its part in this window
   if (g == G - 1 && tail) {
@@ -368,73 +446,12 @@ spmm_path_kernel(const int2* __restrict__ items, const int32_t* __restrict__ hea
       const int off = (v * LPR + lg) * VEC;
       T s = V::zero();
       for (int q = jf; q <= g; ++q) V::add(s, V::load(s_T + q * FT + off));
-      if (colok[v]) V::store(part + (int64_t)tslot * part_ld + colv[v], s);
+      if (colok[v]) store_coherent(part + (int64_t)tslot * part_ld + colv[v], s);
     }
+    finish_cross<LPR, VPL, VEC>(pp, pp.tfix[w], lg, colv, colok, bv, part, part_ld, C, ldc, epi, store_main, proj,
+                                pa);
   }
   stamp(epi, 3);
-}
-
-// Sum the contiguous partial slots of every heavy row crossing windows, in
-// slot (= path) order, apply the epilogue, store the row.  One workgroup per
-// row: P = 256/LPR slot lanes take slots strided by P, then the P partial
-// sums are added in lane order through LDS.
-template <int LPR, int VPL, int VEC, int NP>
-__global__ void __launch_bounds__(256)
-spmm_fixup_kernel(const int32_t* __restrict__ fix, int32_t nfix, int32_t F, const float* __restrict__ part,
-                  int64_t part_ld, float* __restrict__ C, int64_t ldc, Epi epi, ProjArgs pa) {
-  using V = Vec<VEC>;
-  using T = typename V::T;
-  constexpr int P = 256 / LPR;
-  constexpr int FT = LPR * VPL * VEC;
-  __shared__ __attribute__((aligned(16))) float s_acc[P * FT];
-  const int64_t i = blockIdx.x;
-  if (i >= nfix) return;
-  const int p = threadIdx.x / LPR;
-  const int lg = threadIdx.x % LPR;
-  const int32_t r = fix[3 * i], sb = fix[3 * i + 1], se = fix[3 * i + 2];
-  const int64_t col_base = (int64_t)blockIdx.y * FT;
-#pragma unroll
-  for (int v = 0; v < VPL; ++v) {
-    const int off = (v * LPR + lg) * VEC;
-    const int64_t col = col_base + off;
-    T acc = V::zero();
-    if (col < F) {
-      int32_t s = sb + p;
-      for (; s + 3 * P <= se; s += 4 * P) {
-        const T p0 = V::load(part + (int64_t)(s + 0 * P) * part_ld + col);
-        const T p1 = V::load(part + (int64_t)(s + 1 * P) * part_ld + col);
-        const T p2 = V::load(part + (int64_t)(s + 2 * P) * part_ld + col);
-        const T p3 = V::load(part + (int64_t)(s + 3 * P) * part_ld + col);
-        V::add(acc, p0); V::add(acc, p1); V::add(acc, p2); V::add(acc, p3);
-      }
-      for (; s <= se; s += P) V::add(acc, V::load(part + (int64_t)s * part_ld + col));
-    }
-    V::store(s_acc + p * FT + off, acc);
-  }
-  __syncthreads();
-  if (p != 0) return;
-  int64_t colv[VPL];
-  bool colok[VPL];
-  T h[VPL];
-#pragma unroll
-  for (int v = 0; v < VPL; ++v) {
-    const int off = (v * LPR + lg) * VEC;
-    const int64_t col = col_base + off;
-    colv[v] = col;
-    colok[v] = col < F;
-    h[v] = V::zero();
-    if (col >= F) continue;
-    T acc = V::load(s_acc + off);
-    for (int q = 1; q < P; ++q) V::add(acc, V::load(s_acc + q * FT + off));
-    const T b = epi.bias ? V::load(epi.bias + col) : V::zero();
-    h[v] = V::epi(epi, acc, b, r, col);
-    if (NP == 0 || pa.store_main) V::store(C + (int64_t)r * ldc + col, h[v]);
-  }
-  if constexpr (NP > 0) {
-    Proj<NP, LPR, VPL, VEC> proj;
-    proj.load(pa, F, colv, colok);
-    proj.apply(pa, h, r, lg);
-  }
 }
 
 // ---------------------------------------------------------------------------
@@ -453,8 +470,9 @@ typedef float f32x4 __attribute__((ext_vector_type(4)));
 template <bool VEC4, int NT>
 __global__ void __launch_bounds__(256)
 spmm_tile_kernel(const int4* __restrict__ tdesc, const int32_t* __restrict__ tcols, const float* __restrict__ tfrag,
-                 int32_t F, const float* __restrict__ B, int64_t ldb, float* __restrict__ C, int64_t ldc,
-                 Epi epi, float* __restrict__ slabs, int64_t slab_ld) {
+                 const int32_t* __restrict__ trows, const float* __restrict__ dval, int32_t F,
+                 const float* __restrict__ B, int64_t ldb, float* __restrict__ C, int64_t ldc, Epi epi,
+                 float* __restrict__ slabs, int64_t slab_ld) {
   constexpr int NT4 = (NT + 3) & ~3;
   // floats per (k, lane column) row: an odd number of 16-B quads keeps the 16 lanes
   // of a ds_read_b128 group on disjoint bank quads
@@ -466,7 +484,8 @@ spmm_tile_kernel(const int4* __restrict__ tdesc, const int32_t* __restrict__ tco
   const int lane = tid & 63;
   const int wave = tid >> 6;
   const int64_t item = blockIdx.x;
-  const int4 d = tdesc[item];  // row0, nrows, slab (-1: single chunk), 0
+  stamp(epi, 0);
+  const int4 d = tdesc[item];  // block, nrows, slab (-1: single chunk), 0
   constexpr int32_t col0 = 0;  // column slices are folded into the B/C pointers by the host
 
   if (tid < kKC) s_cols[tid] = tcols[item * kKC + tid];
@@ -475,31 +494,43 @@ spmm_tile_kernel(const int4* __restrict__ tdesc, const int32_t* __restrict__ tco
   const float4 a0 = af[0], a1 = af[1], a2 = af[2], a3 = af[3];
   __syncthreads();
   // ---- stage the chunk's B rows, columns [0, 16*NT): element (k, n) -> s_B[k][n&15][n>>4]
-  const int nq = NT * 4;  // float4 per staged row
-  for (int q = tid; q < kKC * nq; q += 256) {
+  // all of a thread's loads issue before any LDS store (one memory latency, not PT)
+  constexpr int nq = NT * 4;  // float4 per staged row
+  constexpr int PT = (kKC * nq + 255) / 256;
+  float4 v[PT];
+#pragma unroll
+  for (int p = 0; p < PT; ++p) {
+    const int q = tid + p * 256;
     const int k = q / nq, c4 = q % nq;
-    const int32_t src = s_cols[k];
+    const int32_t src = q < kKC * nq ? s_cols[k] : -1;
     const int64_t col = col0 + c4 * 4;
-    float4 v = make_float4(0.f, 0.f, 0.f, 0.f);
+    v[p] = make_float4(0.f, 0.f, 0.f, 0.f);
     if (src >= 0) {
       const float* bp = B + (int64_t)src * ldb + col;
       if (VEC4) {
-        if (col < F) v = *reinterpret_cast<const float4*>(bp);
+        if (col < F) v[p] = *reinterpret_cast<const float4*>(bp);
       } else {
-        if (col + 0 < F) v.x = bp[0];
-        if (col + 1 < F) v.y = bp[1];
-        if (col + 2 < F) v.z = bp[2];
-        if (col + 3 < F) v.w = bp[3];
+        if (col + 0 < F) v[p].x = bp[0];
+        if (col + 1 < F) v[p].y = bp[1];
+        if (col + 2 < F) v[p].z = bp[2];
+        if (col + 3 < F) v[p].w = bp[3];
       }
     }
+  }
+#pragma unroll
+  for (int p = 0; p < PT; ++p) {
+    const int q = tid + p * 256;
+    if (q >= kKC * nq) break;
+    const int k = q / nq, c4 = q % nq;
     const int n = c4 * 4, nt = n >> 4, nc0 = n & 15;
     float* dst = s_B + k * stride + nc0 * LR + nt;
-    dst[0] = v.x;
-    dst[LR] = v.y;
-    dst[2 * LR] = v.z;
-    dst[3 * LR] = v.w;
+    dst[0] = v[p].x;
+    dst[LR] = v[p].y;
+    dst[2 * LR] = v[p].z;
+    dst[3 * LR] = v[p].w;
   }
   __syncthreads();
+  stamp(epi, 1);
 
   f32x4 acc[NT];
 #pragma unroll
@@ -521,8 +552,18 @@ spmm_tile_kernel(const int4* __restrict__ tdesc, const int32_t* __restrict__ tco
     }
   }
 
-  // ---- output: rows row0 + 16*wave + 4*(lane>>4) + j, cols col0 + 16*nt + (lane&15)
-  const int32_t rbase = d.x + 16 * wave + 4 * (lane >> 4);
+  stamp(epi, 2);
+  // ---- output: block rows 16*wave + 4*(lane>>4) + j, cols col0 + 16*nt + (lane&15);
+  //      single-chunk blocks finish here (+ extracted diagonal, epilogue), others
+  //      leave a slab for spmm_tile_reduce_kernel
+  int32_t orow[4];
+  float dv[4];
+#pragma unroll
+  for (int j = 0; j < 4; ++j) {
+    const int32_t rl = 16 * wave + 4 * (lane >> 4) + j;
+    orow[j] = rl < d.y ? trows[(int64_t)d.x * kRB + rl] : -1;
+    dv[j] = (d.z < 0 && dval && orow[j] >= 0) ? dval[orow[j]] : 0.f;
+  }
 #pragma unroll
   for (int nt = 0; nt < NT; ++nt) {
     const int64_t col = col0 + nt * 16 + nc;
@@ -530,12 +571,18 @@ spmm_tile_kernel(const int4* __restrict__ tdesc, const int32_t* __restrict__ tco
     const float bcol = (d.z < 0 && epi.bias) ? epi.bias[col] : 0.f;
 #pragma unroll
     for (int j = 0; j < 4; ++j) {
-      const int32_t rl = 16 * wave + 4 * (lane >> 4) + j;  // row within block
-      if (rl >= d.y) continue;
-      if (d.z < 0) C[(int64_t)(rbase + j) * ldc + col] = apply_epi(epi, acc[nt][j], bcol, rbase + j, col);
-      else slabs[((int64_t)d.z * kRB + rl) * slab_ld + col] = acc[nt][j];
+      if (orow[j] < 0) continue;
+      if (d.z < 0) {
+        float v = acc[nt][j];
+        if (dv[j] != 0.f) v = fmaf(dv[j], B[(int64_t)orow[j] * ldb + col], v);
+        C[(int64_t)orow[j] * ldc + col] = apply_epi(epi, v, bcol, orow[j], col);
+      } else {
+        const int32_t rl = 16 * wave + 4 * (lane >> 4) + j;
+        slabs[((int64_t)d.z * kRB + rl) * slab_ld + col] = acc[nt][j];
+      }
     }
   }
+  stamp(epi, 3);
 }
 
 // Multi-chunk dense blocks: out[row, :] = epi(sum over the block's slabs, in
@@ -543,22 +590,35 @@ spmm_tile_kernel(const int4* __restrict__ tdesc, const int32_t* __restrict__ tco
 // workgroup covers one row x 64 columns; slab lanes take slabs strided by 16,
 // then the 16 partial sums are added in lane order through LDS.
 __global__ void __launch_bounds__(256)
-spmm_tile_reduce_kernel(const int4* __restrict__ red, int32_t F, const float* __restrict__ slabs, int64_t slab_ld,
-                        float* __restrict__ C, int64_t ldc, Epi epi) {
+spmm_tile_reduce_kernel(const int4* __restrict__ red, const int32_t* __restrict__ trows,
+                        const float* __restrict__ dval, int32_t F, const float* __restrict__ slabs, int64_t slab_ld,
+                        const float* __restrict__ B, int64_t ldb, float* __restrict__ C, int64_t ldc, Epi epi) {
   __shared__ float4 s_acc[16][16];
-  const int4 rb = red[blockIdx.x];  // row0, nrows, first slab, nslabs
+  const int4 rb = red[blockIdx.x];  // block, nrows, first slab, nslabs
   const int32_t rl = blockIdx.y;    // row within block
   if (rl >= rb.y) return;
   const int sl = threadIdx.x >> 4, c4 = threadIdx.x & 15;
   const int64_t col = (int64_t)blockIdx.z * 64 + c4 * 4;
   float4 acc = make_float4(0.f, 0.f, 0.f, 0.f);
+  // slab rows are padded to 16 floats (slab_ld % 16 == 0): whole float4 reads stay
+  // inside the row; lanes past F are never stored.  Four slabs in flight per lane.
   if (col < F) {
-    for (int s = sl; s < rb.w; s += 16) {
-      const float* p = slabs + ((int64_t)(rb.z + s) * kRB + rl) * slab_ld + col;
-      acc.x += p[0];
-      if (col + 1 < F) acc.y += p[1];
-      if (col + 2 < F) acc.z += p[2];
-      if (col + 3 < F) acc.w += p[3];
+    const int64_t step = (int64_t)16 * kRB * slab_ld;
+    const float* p = slabs + ((int64_t)(rb.z + sl) * kRB + rl) * slab_ld + col;
+    int s = sl;
+    for (; s + 48 < rb.w; s += 64, p += 4 * step) {
+      const float4 u0 = *reinterpret_cast<const float4*>(p);
+      const float4 u1 = *reinterpret_cast<const float4*>(p + step);
+      const float4 u2 = *reinterpret_cast<const float4*>(p + 2 * step);
+      const float4 u3 = *reinterpret_cast<const float4*>(p + 3 * step);
+      acc.x += u0.x; acc.y += u0.y; acc.z += u0.z; acc.w += u0.w;
+      acc.x += u1.x; acc.y += u1.y; acc.z += u1.z; acc.w += u1.w;
+      acc.x += u2.x; acc.y += u2.y; acc.z += u2.z; acc.w += u2.w;
+      acc.x += u3.x; acc.y += u3.y; acc.z += u3.z; acc.w += u3.w;
+    }
+    for (; s < rb.w; s += 16, p += step) {
+      const float4 u = *reinterpret_cast<const float4*>(p);
+      acc.x += u.x; acc.y += u.y; acc.z += u.z; acc.w += u.w;
     }
   }
   s_acc[sl][c4] = acc;
@@ -569,9 +629,11 @@ spmm_tile_reduce_kernel(const int4* __restrict__ red, int32_t F, const float* __
     const float4 u = s_acc[q][c4];
     t.x += u.x; t.y += u.y; t.z += u.z; t.w += u.w;
   }
-  const int64_t row = (int64_t)rb.x + rl;
-  const float vals[4] = {t.x, t.y, t.z, t.w};
+  const int64_t row = trows[(int64_t)rb.x * kRB + rl];
+  const float dv = dval ? dval[row] : 0.f;
+  float vals[4] = {t.x, t.y, t.z, t.w};
   for (int i = 0; i < 4 && col + i < F; ++i) {
+    if (dv != 0.f) vals[i] = fmaf(dv, B[row * ldb + col + i], vals[i]);
     const float b = epi.bias ? epi.bias[col + i] : 0.f;
     C[row * ldc + col + i] = apply_epi(epi, vals[i], b, row, col + i);
   }
@@ -653,19 +715,16 @@ int launch_path(const Launch& a) {
     set_error("gcnk_spmm_csr_f32: ipc %d needs %zu B of LDS (> %d) at %d groups", a.ipc, lds, kMaxLds, G);
     return GCNK_EUNSUP;
   }
-  if (a.L.nwin > 0) {
-    hipLaunchKernelGGL((spmm_path_kernel<BLOCK, LPR, VPL, VEC, U, NP>), dim3((unsigned)a.L.nwin, a.col_tiles),
-                       dim3(BLOCK), lds, a.s, reinterpret_cast<const int2*>(a.plan + a.L.items), a.plan + a.L.head,
-                       a.plan + a.L.tail, a.ipc, a.B, a.ldb, a.F, a.C, a.ldc, a.epi, a.part, a.part_ld, a.pa);
-    int rc = launch_check("spmm_path_kernel");
-    if (rc) return rc;
+  if (a.col_tiles > kMaxColTiles) {
+    set_error("gcnk_spmm_csr_f32: F=%d needs %d column tiles (> %d)", a.F, a.col_tiles, kMaxColTiles);
+    return GCNK_EUNSUP;
   }
-  if (a.nfix > 0) {
-    hipLaunchKernelGGL((spmm_fixup_kernel<LPR, VPL, VEC, NP>), dim3((unsigned)a.nfix, a.col_tiles), dim3(256), 0,
-                       a.s, a.plan + a.L.fix, a.nfix, a.F, a.part, a.part_ld, a.C, a.ldc, a.epi, a.pa);
-    return launch_check("spmm_fixup_kernel");
-  }
-  return GCNK_OK;
+  if (a.L.nwin == 0) return GCNK_OK;
+  PathPlan pp{reinterpret_cast<const int2*>(a.plan + a.L.items), a.plan + a.L.head, a.plan + a.L.tail,
+              a.plan + a.L.hfix, a.plan + a.L.tfix, a.plan + a.L.fix, const_cast<int32_t*>(a.plan + a.L.cnt)};
+  hipLaunchKernelGGL((spmm_path_kernel<BLOCK, LPR, VPL, VEC, U, NP>), dim3((unsigned)a.L.nwin, a.col_tiles),
+                     dim3(BLOCK), lds, a.s, pp, a.ipc, a.B, a.ldb, a.F, a.C, a.ldc, a.epi, a.part, a.part_ld, a.pa);
+  return launch_check("spmm_path_kernel");
 }
 
 template <int VEC>
@@ -698,6 +757,8 @@ struct TileArgs {
   const int4* tdesc;
   const int32_t* tcols;
   const float* tfrag;
+  const int32_t* trows;
+  const float* dval;
   int32_t F;
   const float* B;
   int64_t ldb;
@@ -710,7 +771,7 @@ struct TileArgs {
 
 template <bool V4, int NT>
 int launch_tile_nt(unsigned nitems, const TileArgs& t, hipStream_t s) {
-  hipLaunchKernelGGL((spmm_tile_kernel<V4, NT>), dim3(nitems), dim3(256), 0, s, t.tdesc, t.tcols, t.tfrag, t.F, t.B,
+  hipLaunchKernelGGL((spmm_tile_kernel<V4, NT>), dim3(nitems), dim3(256), 0, s, t.tdesc, t.tcols, t.tfrag, t.trows, t.dval, t.F, t.B,
                      t.ldb, t.C, t.ldc, t.epi, t.slabs, t.slab_ld);
   return launch_check("spmm_tile_kernel");
 }
@@ -736,9 +797,9 @@ inline int launch_tile(bool v4, int nt_need, unsigned nitems, const TileArgs& t,
 struct HostPlan {
   int32_t hdr[16];
   std::vector<int32_t> start;   // item position of each path row, -1 for tile rows
-  std::vector<int32_t> head, tail, fix;
-  std::vector<int32_t> tdesc, tcols, red;
-  std::vector<float> tfrag;
+  std::vector<int32_t> head, tail, hfix, tfix, fix;
+  std::vector<int32_t> tdesc, tcols, red, trows;
+  std::vector<float> tfrag, dval;  // dval: extracted diagonal of tile rows (M, or empty)
 };
 
 int host_plan(const int32_t* rowptr_dev, const int32_t* colind_dev, const float* val_dev, int32_t M, int32_t K,
@@ -769,49 +830,91 @@ int host_plan(const int32_t* rowptr_dev, const int32_t* colind_dev, const float*
       return GCNK_EARG;
     }
 
-  // ---- dense blocks (tile path)
+  // ---- dense blocks (tile path).  Rows are grouped by degree class (factor-8
+  //      buckets of the off-diagonal degree), in row order within a class, 64 per
+  //      block, so rows of one shape share blocks (R8: document rows vs topic rows).
+  //      A block goes to the MFMA tile path when its nonzeros fill at least
+  //      dense_threshold of its condensed column set and each condensed column is
+  //      used at least twice on average; its rows' diagonal entries (r < K) are
+  //      taken out of the column set and added in the epilogue (dval[r] * B[r,:]).
   std::vector<char> tile_row((size_t)M, 0);
-  int32_t ntile = 0, nred = 0, nslabs = 0;
-  std::vector<int32_t> cmap((size_t)K, -1);
-  for (int32_t r0 = 0; r0 < M && dense_threshold <= 1.0f; r0 += kRB) {
-    const int32_t r1 = std::min(M, r0 + kRB);
-    const int64_t bnnz = (int64_t)rp[r1] - rp[r0];
-    if (bnnz == 0) continue;
-    std::vector<int32_t> cols(ci.begin() + rp[r0], ci.begin() + rp[r1]);
-    std::sort(cols.begin(), cols.end());
-    cols.erase(std::unique(cols.begin(), cols.end()), cols.end());
-    const int64_t ncols = (int64_t)cols.size();
-    if ((double)bnnz < (double)dense_threshold * (double)(r1 - r0) * (double)ncols) continue;
-    const int32_t nch = (int32_t)((ncols + kKC - 1) / kKC);
-    const int32_t first_slab = nch > 1 ? nslabs : -1;
-    for (int64_t c = 0; c < ncols; ++c) cmap[(size_t)cols[(size_t)c]] = (int32_t)c;
-    const size_t base_item = (size_t)ntile;
-    for (int32_t ch = 0; ch < nch; ++ch) {
-      hp.tdesc.insert(hp.tdesc.end(), {r0, r1 - r0, nch > 1 ? first_slab + ch : -1, 0});
-      for (int k = 0; k < kKC; ++k) {
-        const int64_t cc = (int64_t)ch * kKC + k;
-        hp.tcols.push_back(cc < ncols ? cols[(size_t)cc] : -1);
+  int32_t ntile = 0, nred = 0, nslabs = 0, ntblk = 0;
+  bool any_diag = false;
+  hp.dval.clear();
+  auto is_diag = [&](int32_t r, int64_t k) { return r < K && ci[(size_t)k] == r; };
+  if (dense_threshold <= 1.0f && M > 0) {
+    std::vector<std::vector<int32_t>> cls(33);
+    for (int32_t r = 0; r < M; ++r) {
+      int64_t deg = 0;
+      for (int64_t k = rp[r]; k < rp[r + 1]; ++k) deg += !is_diag(r, k);
+      int bw = 0;
+      while (bw < 63 && (deg >> bw) != 0) ++bw;
+      cls[(size_t)(bw / 3)].push_back(r);
+    }
+    std::vector<int32_t> cmap((size_t)K, -1);
+    std::vector<int32_t> cols;
+    std::vector<float> dv((size_t)M, 0.f);
+    for (const std::vector<int32_t>& rows : cls) {
+      for (size_t i0 = 0; i0 < rows.size(); i0 += kRB) {
+        const size_t i1 = std::min(rows.size(), i0 + kRB);
+        cols.clear();
+        int64_t bnnz = 0;
+        for (size_t i = i0; i < i1; ++i) {
+          const int32_t r = rows[i];
+          for (int64_t k = rp[r]; k < rp[r + 1]; ++k)
+            if (!is_diag(r, k)) {
+              cols.push_back(ci[(size_t)k]);
+              ++bnnz;
+            }
+        }
+        if (bnnz == 0) continue;
+        std::sort(cols.begin(), cols.end());
+        cols.erase(std::unique(cols.begin(), cols.end()), cols.end());
+        const int64_t ncols = (int64_t)cols.size();
+        const int64_t nrows = (int64_t)(i1 - i0);
+        if ((double)bnnz < (double)dense_threshold * (double)nrows * (double)ncols || bnnz < 2 * ncols) continue;
+        const int32_t nch = (int32_t)((ncols + kKC - 1) / kKC);
+        const int32_t first_slab = nch > 1 ? nslabs : -1;
+        const int32_t blk = ntblk++;
+        for (int64_t c = 0; c < ncols; ++c) cmap[(size_t)cols[(size_t)c]] = (int32_t)c;
+        const size_t base_item = (size_t)ntile;
+        for (int32_t ch = 0; ch < nch; ++ch) {
+          hp.tdesc.insert(hp.tdesc.end(), {blk, (int32_t)nrows, nch > 1 ? first_slab + ch : -1, 0});
+          for (int k = 0; k < kKC; ++k) {
+            const int64_t cc = (int64_t)ch * kKC + k;
+            hp.tcols.push_back(cc < ncols ? cols[(size_t)cc] : -1);
+          }
+        }
+        for (int64_t rl = 0; rl < kRB; ++rl) hp.trows.push_back(rl < nrows ? rows[i0 + (size_t)rl] : -1);
+        hp.tfrag.resize(hp.tfrag.size() + (size_t)nch * kRB * kKC, 0.f);
+        for (size_t i = i0; i < i1; ++i) {
+          const int32_t r = rows[i];
+          const int32_t rl = (int32_t)(i - i0), t = rl / 16, lr = rl % 16;
+          tile_row[(size_t)r] = 1;
+          for (int64_t k = rp[r]; k < rp[r + 1]; ++k) {
+            if (is_diag(r, k)) {
+              any_diag = true;
+              if (want_values) dv[(size_t)r] += vv[(size_t)k];
+              continue;
+            }
+            if (!want_values) continue;
+            const int32_t cc = cmap[(size_t)ci[(size_t)k]];
+            const int32_t ch = cc / kKC, kk = cc % kKC;
+            const int32_t st = kk / 4, kq = kk % 4;
+            const int32_t ln = kq * 16 + lr;
+            hp.tfrag[(((base_item + ch) * 4 + t) * 64 + ln) * 16 + st] += vv[(size_t)k];
+          }
+        }
+        for (int64_t c = 0; c < ncols; ++c) cmap[(size_t)cols[(size_t)c]] = -1;
+        if (nch > 1) {
+          hp.red.insert(hp.red.end(), {blk, (int32_t)nrows, first_slab, nch});
+          ++nred;
+          nslabs += nch;
+        }
+        ntile += nch;
       }
     }
-    hp.tfrag.resize(hp.tfrag.size() + (size_t)nch * kRB * kKC, 0.f);
-    if (want_values) {
-      for (int32_t r = r0; r < r1; ++r)
-        for (int32_t k = rp[r]; k < rp[r + 1]; ++k) {
-          const int32_t cc = cmap[(size_t)ci[(size_t)k]];
-          const int32_t ch = cc / kKC, kk = cc % kKC;
-          const int32_t rl = r - r0, t = rl / 16, lr = rl % 16, st = kk / 4, kq = kk % 4;
-          const int32_t ln = kq * 16 + lr;
-          hp.tfrag[(((base_item + ch) * 4 + t) * 64 + ln) * 16 + st] += vv[(size_t)k];
-        }
-    }
-    for (int64_t c = 0; c < ncols; ++c) cmap[(size_t)cols[(size_t)c]] = -1;
-    if (nch > 1) {
-      hp.red.insert(hp.red.end(), {r0, r1 - r0, first_slab, nch});
-      ++nred;
-      nslabs += nch;
-    }
-    ntile += nch;
-    for (int32_t r = r0; r < r1; ++r) tile_row[(size_t)r] = 1;
+    if (any_diag) hp.dval = std::move(dv);
   }
 
   // ---- path windows over the other rows
@@ -854,9 +957,16 @@ int host_plan(const int32_t* rowptr_dev, const int32_t* colind_dev, const float*
     if (hp.head[(size_t)x] >= 0) hp.head[(size_t)x] = slot++;
     if (hp.tail[(size_t)x] >= 0) hp.tail[(size_t)x] = slot++;
   }
-  for (const Cross& c : cross) hp.fix.insert(hp.fix.end(), {c.row, hp.tail[(size_t)c.wa], hp.head[(size_t)c.wb]});
+  hp.hfix.assign((size_t)nwin, -1);
+  hp.tfix.assign((size_t)nwin, -1);
+  for (size_t i = 0; i < cross.size(); ++i) {
+    const Cross& c = cross[i];
+    hp.fix.insert(hp.fix.end(), {c.row, hp.tail[(size_t)c.wa], hp.head[(size_t)c.wb]});
+    for (int64_t x = c.wa; x < c.wb; ++x) hp.tfix[(size_t)x] = (int32_t)i;
+    hp.hfix[(size_t)c.wb] = (int32_t)i;
+  }
   const int32_t h[16] = {kMagic, M, K, groups, ipc, (int32_t)W, (int32_t)nwin, (int32_t)cross.size(), slot,
-                         ntile, nred, nslabs, kKC, kRB, (int32_t)heavy, 0};
+                         ntile, nred, nslabs, ntblk, any_diag ? 1 : 0, (int32_t)heavy, 0};
   std::copy(h, h + 16, hp.hdr);
   return GCNK_OK;
 }
@@ -922,11 +1032,17 @@ extern "C" int gcnk_spmm_plan_build(const int32_t* rowptr, const int32_t* colind
   up(0, hp.hdr, sizeof(hp.hdr), "plan header");
   up(L.head, hp.head.data(), hp.head.size() * 4, "plan head");
   up(L.tail, hp.tail.data(), hp.tail.size() * 4, "plan tail");
+  up(L.hfix, hp.hfix.data(), hp.hfix.size() * 4, "plan head rows");
+  up(L.tfix, hp.tfix.data(), hp.tfix.size() * 4, "plan tail rows");
   up(L.fix, hp.fix.data(), hp.fix.size() * 4, "plan fix");
+  if (!rc && L.nfix > 0)
+    rc = hip_check(hipMemsetAsync(p + L.cnt, 0, (size_t)L.nfix * kMaxColTiles * 4, s), "plan counters");
   up(L.tdesc, hp.tdesc.data(), hp.tdesc.size() * 4, "plan tile desc");
   up(L.tcols, hp.tcols.data(), hp.tcols.size() * 4, "plan tile cols");
   up(L.tfrag, hp.tfrag.data(), hp.tfrag.size() * 4, "plan tile frags");
   up(L.red, hp.red.data(), hp.red.size() * 4, "plan tile reduce");
+  up(L.trows, hp.trows.data(), hp.trows.size() * 4, "plan tile rows");
+  up(L.dval, hp.dval.data(), hp.dval.size() * 4, "plan diagonal");
   up(L.total, hp.start.data(), hp.start.size() * 4, "plan start");
   const int64_t nitems = L.nwin * L.W;
   int2* items = reinterpret_cast<int2*>(p + L.items);
@@ -1045,6 +1161,7 @@ static int spmm_impl(const void* plan, const int32_t* hdr, const float* B, int64
   const int64_t slab_ld = tile_fpad(F);
 
   // ---- dense blocks: tile kernel (+ slab reduce)
+  const float* dval = L.has_diag ? reinterpret_cast<const float*>(p + L.dval) : nullptr;
   if (L.ntile > 0) {
     const int32_t nt_total = (int32_t)(slab_ld / 16);
     // F <= 16*kMaxNT: one launch over all columns; wider: 128-column slices with the
@@ -1057,14 +1174,15 @@ static int spmm_impl(const void* plan, const int32_t* hdr, const float* B, int64
       es.bias = bias ? bias + c0 : nullptr;
       es.mask = drop_mask ? drop_mask + c0 : nullptr;
       es.offset = e.offset + (uint64_t)c0;  // hash index shifts with the column
-      TileArgs ta{td, p + L.tcols, reinterpret_cast<const float*>(p + L.tfrag), Fs, B + c0, ldb, C + c0, ldc, es,
-                  slabs ? slabs + c0 : nullptr, slab_ld};
+      TileArgs ta{td,      p + L.tcols, reinterpret_cast<const float*>(p + L.tfrag), p + L.trows, dval, Fs, B + c0,
+                  ldb,     C + c0,      ldc, es, slabs ? slabs + c0 : nullptr, slab_ld};
       const int rc = launch_tile(vec4, (Fs + 15) / 16, (unsigned)L.ntile, ta, s);
       if (rc) return rc;
     }
     if (L.nred > 0) {
       hipLaunchKernelGGL(spmm_tile_reduce_kernel, dim3((unsigned)L.nred, kRB, (unsigned)((F + 63) / 64)), dim3(256),
-                         0, s, reinterpret_cast<const int4*>(p + L.red), F, slabs, slab_ld, C, ldc, e);
+                         0, s, reinterpret_cast<const int4*>(p + L.red), p + L.trows, dval, F, slabs, slab_ld, B, ldb,
+                         C, ldc, e);
       int rc = launch_check("spmm_tile_reduce_kernel");
       if (rc) return rc;
     }

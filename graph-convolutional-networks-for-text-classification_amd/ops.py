@@ -79,6 +79,12 @@ def spmm(a, B, bias=None, epilogue=_lib.EPI_NONE, mask=None, scale=1.0, keep_pro
     return out
 
 
+# Fuse gc2's H1 W2 into the gc1 aggregation epilogue (gcnk_spmm_proj_f32).
+# Off by default: on R8 the fused path kernel (W in registers, shorter gather
+# batches) measured slower than the unfused SpMM + skinny GEMM pair.
+FUSE_PROJECTION = False
+
+
 def spmm_proj(a, B, W, bias=None, epilogue=_lib.EPI_NONE, mask=None, scale=1.0, keep_prob=1.0, seed=0, offset=0,
               store_main=True, ipc=None, lanes=0):
     """(H, C2) with H = epi(A @ B) and C2 = H @ W, the projection fused into
@@ -241,8 +247,9 @@ class GCNFn(torch.autograd.Function):
 
         S1 = X W1                   spmm (sparse X) / gemm (dense X)      layer.py:102
         H1 = drop(relu(A S1 + b1))  spmm + fused epilogue                 layer.py:106,110,182,185
-        S2 = H1 W2                  projection fused into that epilogue   layer.py:102 (gc2)
-                                    (H1 kept only when a backward needs it)
+        S2 = H1 W2                  skinny MFMA gemm, or fused into that   layer.py:102 (gc2)
+                                    epilogue (FUSE_PROJECTION; H1 then kept
+                                    only when a backward needs it)
         Z  = A S2 + b2              spmm + bias epilogue                   layer.py:106,110 (gc2)
 
     Backward (trainer.py:361):
@@ -255,8 +262,13 @@ class GCNFn(torch.autograd.Function):
     @staticmethod
     def forward(ctx, W1, b1, W2, b2, xop, adj, epi, mask, scale, keep, seed, offset, keep_h1=True):
         S1 = xop.times(W1)
-        H1, S2 = spmm_proj(adj, S1, W2, bias=b1, epilogue=epi, mask=mask, scale=scale, keep_prob=keep,
-                           seed=seed, offset=offset, store_main=keep_h1)
+        if FUSE_PROJECTION:
+            H1, S2 = spmm_proj(adj, S1, W2, bias=b1, epilogue=epi, mask=mask, scale=scale, keep_prob=keep,
+                               seed=seed, offset=offset, store_main=keep_h1)
+        else:
+            H1 = spmm(adj, S1, bias=b1, epilogue=epi, mask=mask, scale=scale, keep_prob=keep, seed=seed,
+                      offset=offset)
+            S2 = gemm(H1, W2)
         out = spmm(adj, S2, bias=b2, epilogue=_lib.EPI_BIAS if b2 is not None else _lib.EPI_NONE)
         ctx.xop, ctx.adj, ctx.scale = xop, adj, float(scale)
         ctx.has_b1, ctx.has_b2 = b1 is not None, b2 is not None

@@ -75,19 +75,23 @@ const char* gcnk_last_error(void);
  *
  * The operand is converted once (gcnk_spmm_plan_build) into a hybrid plan
  * whose two parts write disjoint rows of C:
- *  - dense blocks: blocks of 64 rows whose nonzeros fill >= dense_threshold
- *    of the block's condensed column set are stored densely over those
- *    columns (MFMA fragment order, chunks of 64 columns) and run on fp32
+ *  - dense blocks: rows are grouped by off-diagonal degree class (factor-8
+ *    buckets, row order within a class) into blocks of 64; a block whose
+ *    nonzeros fill >= dense_threshold of its condensed column set (and use
+ *    each such column twice on average) is stored densely over those
+ *    columns (MFMA fragment order, chunks of 64 columns) and runs on fp32
  *    MFMA, each B row of a chunk staged once per block instead of gathered
- *    per nonzero; multi-chunk blocks are summed from partial slabs in order.
+ *    per nonzero; its rows' diagonal entries are kept aside and added in the
+ *    epilogue; multi-chunk blocks are summed from partial slabs in order.
  *    dense_threshold > 1 disables the part (default callers pass 0.25).
  *  - path: the other rows' nonzeros in row order, each row closed by an
  *    end-of-row marker, as one int2 item stream (col, value bits) / (-1, row)
  *    / (-2 pad) cut into windows of W = groups*ipc items, one per workgroup;
  *    rows of at most W/2 items never straddle a window, so only heavy rows
  *    cross windows.  Rows split between the chunks of a window meet in LDS;
- *    heavy rows crossing windows leave one partial per window that a fix-up
- *    pass sums in path order.
+ *    heavy rows crossing windows leave one partial per window and the last
+ *    window to finish sums them in path order (arrival counters kept in the
+ *    plan: launches sharing one plan must be ordered on one stream).
  * All sums have a fixed order (no float atomics): bitwise reproducible.
  * gcnk_spmm_groups(F, lanes_hint) gives the `groups` the kernels use for a
  * width F; a plan serves every F with that count.  The plan copies the
@@ -95,8 +99,9 @@ const char* gcnk_last_error(void);
  * and synchronises `stream` (one-time setup).
  *
  * Plan header (16 int32, first words of the plan; gcnk_spmm_plan_query):
- *   0 magic 'GNK3'  1 M  2 K  3 groups  4 ipc  5 W  6 nwin  7 nfix  8 nslots
- *   9 tile chunks  10 multi-chunk blocks  11 slabs  12 KC=64  13 RB=64  14 heavy  15 0
+ *   0 magic 'GNK4'  1 M  2 K  3 groups  4 ipc  5 W  6 nwin  7 nfix  8 nslots
+ *   9 tile chunks  10 multi-chunk blocks  11 slabs  12 tile blocks
+ *   13 diagonal kept aside (0/1)  14 heavy  15 0   (tile blocks: 64 rows x 64-column chunks)
  * ------------------------------------------------------------------------- */
 int32_t gcnk_spmm_groups(int32_t F, int32_t lanes_hint);
 int32_t gcnk_spmm_default_ipc(int32_t M, int64_t nnz, int32_t F, int32_t lanes_hint);

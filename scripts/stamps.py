@@ -21,8 +21,10 @@ def main():
     r8 = datasets.load_r8_fixture(os.path.join(ROOT, "tests", "golden", "r8_graph.npz"))
     A = as_csr(r8["adj"].to(dev))
     X = as_csr(r8["features"].to(dev))
-    cases = [("R8_A_F200", A, 200, 0, None), ("R8_A_F200_l32i16", A, 200, 32, 16), ("R8_A_F8", A, 8, 0, None),
-             ("R8_X_F200", X, 200, 0, None)]
+    only = sys.argv[1:] or None
+    cases = [("R8_A_F200", A, 200, 0, None), ("R8_A_F8", A, 8, 0, None),
+             ("R8_X_F200", X, 200, 0, None), ("R8_X_F8", X, 8, 0, None)]
+    cases = [c for c in cases if only is None or c[0] in only]
     for name, a, F, lanes, ipc in cases:
         B = torch.randn(a.shape[1], F, device=dev)
         out = torch.empty(a.shape[0], F, device=dev)

@@ -28,11 +28,11 @@ def test_library_exports_every_declared_symbol():
     assert set(declared) == set(_lib.SIGNATURES), "ctypes signatures out of sync with include/gcnk.h"
 
 
-MAGIC = 0x474E4B33  # plan header word 0 ("GNK3")
+MAGIC = 0x474E4B34  # plan header word 0 ("GNK4")
 
 
 def _hdr(M=10, K=10, groups=4, ipc=16, nslots=0, nslabs=0):
-    h = (ctypes.c_int32 * 16)(MAGIC, M, K, groups, ipc, groups * ipc, 0, 0, nslots, 0, 0, nslabs, 64, 64, 0, 0)
+    h = (ctypes.c_int32 * 16)(MAGIC, M, K, groups, ipc, groups * ipc, 0, 0, nslots, 0, 0, nslabs, 0, 0, 0, 0)
     return ctypes.cast(h, ctypes.c_void_p), h
 
 

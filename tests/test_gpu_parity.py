@@ -63,6 +63,12 @@ def test_spmm_r8_adjacency(r8, F):
     got = spmm(a, B.to(DEV))
     ref = csr_ref.spmm_csr(rp, ci, v, B.numpy())
     _close(got, ref)
+    # low dense threshold: document rows run as MFMA tiles over the 50 topic
+    # columns with the self loop kept aside (diagonal epilogue)
+    got_t = spmm(a, B.to(DEV), dense=0.05)
+    _close(got_t, ref)
+    hdr = [p for k, p in a._plans.items() if k[2] == 0.05][0].header
+    assert hdr[9] > 0 and hdr[13] == 1, "R8 document rows: MFMA tiles over the topic columns + diagonal"
 
 
 @pytest.mark.parametrize("F", [1, 3, 7, 8, 16, 64, 100, 200, 256, 257, 1000, 4096])
@@ -96,10 +102,12 @@ def _mixed_density_csr(rng, M, K):
     64-column chunks (X's topic rows), heavy sparse rows, light rows, empty rows."""
     rows, cols = [], []
     for r in range(M):
-        if r < 130:                       # dense over columns 0..49
-            c = np.arange(50)
+        if r < 130:                       # dense over columns 0..49 (+ the diagonal past 50)
+            c = np.arange(50) if r < 50 else np.concatenate([np.arange(50), [r]])
         elif 300 <= r < 341:              # fully dense
             c = np.arange(K)
+        elif 400 <= r < 600:              # self loop + 4 of 50 "topic" columns (Â's document rows)
+            c = np.concatenate([[r], 800 + rng.choice(50, 4, replace=False)])
         elif r % 97 == 5:                 # heavy sparse
             c = rng.choice(K, 400, replace=False)
         elif r % 7 == 0:                  # empty
@@ -127,6 +135,7 @@ def test_spmm_hybrid_dense_blocks(F):
     _close(got, csr_ref.spmm_epilogue(acc, bias, relu=True, mask=mask, scale=1.5), atol=2e-5 * np.sqrt(K))
     hdr = list(a._plans.values())[0].header
     assert hdr[9] > 0 and hdr[10] > 0, "dense blocks (single and multi-chunk) expected on the tile path"
+    assert hdr[13] == 1, "diagonal entries of tile rows are extracted"
     # tile path disabled: the path kernel alone gives the same product
     got2 = spmm(a, torch.from_numpy(B).to(DEV), dense=2.0)
     _close(got2, acc, atol=2e-5 * np.sqrt(K))
@@ -137,7 +146,7 @@ def test_spmm_r8_features_use_tile_path(r8):
     W = torch.randn(r8["nfeat"], 200, generator=torch.Generator().manual_seed(4))
     got = spmm(x, W.to(DEV))
     hdr = list(x._plans.values())[0].header
-    assert hdr[9] > 0, "R8 X: the document/topic row blocks run on the MFMA tile path"
+    assert hdr[9] > 0 and hdr[6] == 0, "R8 X: document and topic rows all run on the MFMA tile path"
     rp, ci, v = (t.cpu().numpy() for t in (x.rowptr, x.colind, x.val))
     _close(got, csr_ref.spmm_csr(rp, ci, v, W.numpy()), atol=1e-4)
 

@@ -6,11 +6,13 @@ DESIGN.md for the path, the boundary and the kernels.
 from . import _lib
 from .layer import GCN, GraphConvolution
 from .ops import GCNFn, GraphConvFn, Operand, colsum, gemm, spmm
+from .parallel import ColumnShardedSpMM, shard_bounds, sharded_gcn_forward
 from .sparse import CSR, as_csr, from_arrays, from_torch
 
 __all__ = [
     "GCN", "GraphConvolution", "GCNFn", "GraphConvFn", "Operand", "CSR",
     "as_csr", "from_arrays", "from_torch", "spmm", "gemm", "colsum",
+    "ColumnShardedSpMM", "shard_bounds", "sharded_gcn_forward",
 ]
 
 

@@ -16,21 +16,21 @@
 //    of gathering a B row per nonzero.  Blocks with several chunks write
 //    partial slabs that spmm_tile_reduce_kernel sums in chunk order.
 //
-//  * the remaining rows -> spmm_path_kernel (gathers).  The nonzeros in row
-//    order, each row closed by an end-of-row marker (col = -1, payload = row)
-//    form one int2 item stream cut into workgroup windows of W = G*ipc items;
-//    a row of at most W/2 items that would straddle a window is pushed to the
-//    next with pad items (col = -2), so only heavy rows cross windows and the
-//    kernel needs no search: window w is items [w*W, (w+1)*W), loaded in one
-//    coalesced pass, then the B-row gathers issue.  Groups of LPR lanes walk
-//    ipc items each, gathering U nonzeros at a time (U*VPL independent 16-B
-//    loads in flight per lane) and flushing a row at its marker with
-//    bias/ReLU/dropout fused into the store.  Lanes own VEC-wide column
-//    vectors interleaved by LPR (one load instruction of a group covers
-//    LPR*VEC contiguous floats of a B row).  Rows split between the groups of
-//    a window meet in LDS; heavy rows crossing windows leave one partial per
-//    window, and the last of those windows to finish (arrival counter in the
-//    plan) sums them in path order -- one launch, no fix-up kernel.
+//  * the remaining rows -> spmm_row_kernel (gathers), one launch.  The plan
+//    lists "units": a light row (at most `ipc` nonzeros) is one unit owned by
+//    one lane group (LPR lanes, each lane one VEC-wide column vector of the
+//    row: one load instruction of a group covers LPR*VEC contiguous floats of
+//    a B row); a heavier row is cut into segments, each owned by a whole
+//    wavefront whose 64/LPR lane groups take interleaved nonzeros and meet in
+//    a fixed xor butterfly.  A row of one segment is stored directly; a row
+//    of several leaves one partial per segment, and the last segment to
+//    finish (arrival counter in the plan) sums them in segment order and
+//    stores the row -- no fix-up launch.  Every lane issues the U gathers of
+//    a batch before its first FMA (U independent 16-B loads in flight), and a
+//    unit's one store follows all of its loads, so no gather waits behind a
+//    store.  Heavy segments come first in the grid (the longest work is
+//    dispatched first); light rows follow in row order.  bias/ReLU/dropout
+//    (and optionally a dense projection) are fused into the store.
 //
 // Every sum has a fixed order (no float atomics): results are bitwise
 // reproducible run to run.
@@ -43,13 +43,12 @@
 namespace gcnk {
 namespace {
 
-constexpr int32_t kMarker = -1;  // end of row; .y = row index
-constexpr int32_t kPad = -2;     // no-op
-constexpr int32_t kMagic = 0x474e4b34;  // "GNK4"
-constexpr int kRB = 64;          // tile rows per dense block (4 waves x 16)
-constexpr int kKC = 64;          // condensed columns per tile chunk (16 MFMA k-steps)
-constexpr int kMaxNT = 14;
-constexpr int kMaxColTiles = 64;  // path column tiles per launch (arrival counters per cross row)       // 16-column MFMA n-tiles per tile workgroup (B tile <= 57 KB LDS)
+constexpr int32_t kMagic = 0x474e4b35;  // "GNK5"
+constexpr int kRB = 64;                 // tile rows per dense block (4 waves x 16)
+constexpr int kKC = 64;                 // condensed columns per tile chunk (16 MFMA k-steps)
+constexpr int kMaxNT = 14;              // 16-column MFMA n-tiles per tile workgroup (B tile <= 57 KB LDS)
+constexpr int kMaxColTiles = 64;        // row-kernel column tiles per launch (arrival counters per heavy row)
+constexpr int kMaxSeg = 64;             // segments per heavy row (bounds the last arriver's combine)
 
 template <int VEC>
 struct Vec;
@@ -94,21 +93,24 @@ struct Vec<1> {
 
 // ---------------------------------------------------------------------------
 // Plan layout (int32 words).  Header (16 words, see gcnk.h):
-//   0 magic  1 M  2 K  3 groups  4 ipc  5 W  6 nwin  7 nfix  8 nslots
-//   9 ntile (chunks)  10 nred  11 nslabs  12 ntblk (tile blocks)  13 has_diag  14 heavy  15 0
+//   0 magic  1 M  2 K  3 lane groups per wave  4 ipc (light-row limit)  5 nunits
+//   6 nhunits (heavy segments = partial slots)  7 nheavy (rows of > 1 segment)
+//   8 ntile (chunks)  9 nred  10 nslabs  11 ntblk (tile blocks)  12 has_diag  13 nnz  14 0  15 0
+// Body: items int2[nnz] {col, value bits} in CSR order | units int4[nunits]
+//   {row, nz begin, nz end, heavy row index or -1}, heavy segments first |
+//   heavy int4[nheavy] {row, first unit, nseg, 0} | arrival counters
+//   int32[nheavy * kMaxColTiles] (zero between launches) | tile part.
 struct Layout {
-  int64_t nwin, W, nfix, ntile, nred, ntblk, has_diag, M;
-  int64_t items, head, tail, hfix, tfix, fix, cnt, tdesc, tcols, tfrag, red, trows, dval, total;
+  int64_t M, nnz, nunits, nhunits, nheavy, ntile, nred, ntblk, has_diag;
+  int64_t items, units, heavy, cnt, tdesc, tcols, tfrag, red, trows, dval, total;
   __host__ __device__ explicit Layout(const int32_t* h) {
-    M = h[1]; nwin = h[6]; W = h[5]; nfix = h[7]; ntile = h[9]; nred = h[10]; ntblk = h[12]; has_diag = h[13];
+    M = h[1]; nunits = h[5]; nhunits = h[6]; nheavy = h[7]; ntile = h[8]; nred = h[9]; ntblk = h[11];
+    has_diag = h[12]; nnz = h[13];
     items = 16;
-    head = items + 2 * nwin * W;
-    tail = head + nwin;
-    hfix = tail + nwin;
-    tfix = hfix + nwin;
-    fix = tfix + nwin;
-    cnt = fix + 3 * nfix;
-    tdesc = (cnt + (int64_t)kMaxColTiles * nfix + 3) & ~3LL;
+    units = (items + 2 * nnz + 3) & ~3LL;
+    heavy = units + 4 * nunits;
+    cnt = heavy + 4 * nheavy;
+    tdesc = (cnt + (int64_t)kMaxColTiles * nheavy + 3) & ~3LL;
     tcols = tdesc + 4 * ntile;
     tfrag = (tcols + (int64_t)kKC * ntile + 3) & ~3LL;
     red = tfrag + (int64_t)kRB * kKC * ntile;
@@ -119,25 +121,12 @@ struct Layout {
 };
 
 // ---------------------------------------------------------------------------
-// Plan construction kernels.
-__global__ void fill_pad_kernel(int2* __restrict__ items, int64_t n) {
-  const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-  if (i < n) items[i] = make_int2(kPad, 0);
-}
-
-// nonzero k of row r goes to start[r] + (k - rowptr[r]); the marker to start[r] + deg(r);
-// rows handled by the tile path have start[r] < 0 and no items.
-__global__ void scatter_items_kernel(const int32_t* __restrict__ rowptr, const int32_t* __restrict__ colind,
-                                     const float* __restrict__ val, int32_t M, const int32_t* __restrict__ start,
-                                     int2* __restrict__ items) {
-  const int32_t r = blockIdx.x * (blockDim.x / 64) + (threadIdx.x >> 6);
-  if (r >= M) return;
-  const int32_t s = start[r];
-  if (s < 0) return;
-  const int lane = threadIdx.x & 63;
-  const int32_t b = rowptr[r], e = rowptr[r + 1];
-  for (int32_t k = b + lane; k < e; k += 64) items[s + (k - b)] = make_int2(colind[k], __float_as_int(val[k]));
-  if (lane == 0) items[s + (e - b)] = make_int2(kMarker, r);
+// Plan construction: items[k] = {colind[k], val[k] bits}, CSR order (one 8-B
+// load per nonzero in the row kernel).
+__global__ void pack_items_kernel(const int32_t* __restrict__ colind, const float* __restrict__ val, int64_t nnz,
+                                  int2* __restrict__ items) {
+  const int64_t k = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (k < nnz) items[k] = make_int2(colind[k], __float_as_int(val[k]));
 }
 
 // ---------------------------------------------------------------------------
@@ -225,21 +214,20 @@ struct Proj {
 };
 
 // ---------------------------------------------------------------------------
-// Path kernel (gathers).
-struct PathPlan {
-  const int2* items;
-  const int32_t* head;  // per window: partial slot of the row ending here that began earlier (-1)
-  const int32_t* tail;  // per window: partial slot of the row leaving the window (-1)
-  const int32_t* hfix;  // per window: cross-row index of head / tail partial (-1)
-  const int32_t* tfix;
-  const int32_t* fix;   // per cross row: row, first slot, last slot
-  int32_t* cnt;         // per cross row x column tile: arrival counters (zero between launches)
+// Row kernel (gathers).
+struct RowPlan {
+  const int2* items;   // {col, value bits} per nonzero, CSR order
+  const int4* units;   // {row, nz begin, nz end, heavy row index or -1}; heavy segments first
+  const int4* heavy;   // {row, first unit (= first partial slot), nseg, 0}
+  int32_t* cnt;        // per heavy row x column tile: arrival counters (zero between launches)
+  int32_t nunits, nhunits;
 };
 
 // Partial slots are written and read with agent-coherent accesses (relaxed
 // agent-scope atomics: sc1, past the per-XCD L2), so publishing them needs no
-// L2 write-back/invalidate: the writer waits for its stores to complete
-// (s_waitcnt vmcnt(0)) before bumping the arrival counter.
+// L2 write-back/invalidate: the writing wave waits for its stores to complete
+// (s_waitcnt vmcnt(0)) before bumping the arrival counter, and the last
+// arriver is told so by the value its own add returns.
 template <typename T>
 __device__ __forceinline__ void store_coherent(float* p, const T& v) {
   const float* f = reinterpret_cast<const float*>(&v);
@@ -256,201 +244,138 @@ __device__ __forceinline__ T load_coherent(const float* p) {
   return v;
 }
 
-// A group has just stored one partial of cross row `fi` (a heavy row spanning
-// windows).  The last of the row's windows to arrive sums all its partial
-// slots in slot (= path) order, applies the epilogue and stores the row, then
-// re-arms the counter -- no fix-up launch; the sum order is fixed whichever
-// window arrives last.
-template <int LPR, int VPL, int VEC, typename T, typename ProjT>
-__device__ __forceinline__ void finish_cross(const PathPlan& pp, int32_t fi, int lg, const int64_t* colv,
-                                             const bool* colok, const T* bv, const float* part, int64_t part_ld,
-                                             float* C, int64_t ldc, const Epi& epi, bool store_main,
-                                             const ProjT& proj, const ProjArgs& pa) {
-  using V = Vec<VEC>;
-  __builtin_amdgcn_s_waitcnt(0);  // this group's partial stores have completed
-  const int32_t r = pp.fix[3 * fi], sb = pp.fix[3 * fi + 1], se = pp.fix[3 * fi + 2];
-  int32_t* ctr = pp.cnt + (int64_t)fi * kMaxColTiles + blockIdx.y;
-  int last = 0;
-  if (lg == 0) last = __hip_atomic_fetch_add(ctr, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == se - sb;
-  last = __shfl(last, (int)(threadIdx.x & 63) - lg, 64);
-  if (!last) return;
-  T h[VPL];
-#pragma unroll
-  for (int v = 0; v < VPL; ++v) {
-    h[v] = V::zero();
-    if (!colok[v]) continue;
-    T acc = V::zero();
-    const float* p = part + (int64_t)sb * part_ld + colv[v];
-    int32_t q = sb;
-    for (; q + 3 <= se; q += 4, p += 4 * part_ld) {
-      const T p0 = load_coherent<T>(p), p1 = load_coherent<T>(p + part_ld), p2 = load_coherent<T>(p + 2 * part_ld),
-              p3 = load_coherent<T>(p + 3 * part_ld);
-      V::add(acc, p0); V::add(acc, p1); V::add(acc, p2); V::add(acc, p3);
-    }
-    for (; q <= se; ++q, p += part_ld) V::add(acc, load_coherent<T>(p));
-    h[v] = V::epi(epi, acc, bv[v], r, colv[v]);
-    if (store_main) V::store(C + (int64_t)r * ldc + colv[v], h[v]);
-  }
-  proj.apply(pa, h, r, lg);
-  if (lg == 0) __hip_atomic_store(ctr, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-}
-
-template <int BLOCK, int LPR, int VPL, int VEC, int U, int NP>
-__global__ void __launch_bounds__(BLOCK)
-spmm_path_kernel(PathPlan pp, int32_t ipc, const float* __restrict__ B, int64_t ldb, int32_t F,
-                 float* __restrict__ C, int64_t ldc, Epi epi, float* __restrict__ part, int64_t part_ld,
-                 ProjArgs pa) {
-  const int2* __restrict__ items = pp.items;
+// acc += sum of val * B[col, colv..] over items k = b + q + S*i, i ascending,
+// U gathers in flight per batch (all issued before the first FMA).
+template <int VEC, int U, int S>
+__device__ __forceinline__ void gather_rows(const int2* __restrict__ items, int32_t b, int32_t e, int q,
+                                            const float* __restrict__ B, int64_t ldb, int64_t colv, bool colok,
+                                            typename Vec<VEC>::T& acc) {
   using V = Vec<VEC>;
   using T = typename V::T;
-  constexpr int G = BLOCK / LPR;
-  constexpr int FT = LPR * VPL * VEC;  // columns per tile
-  extern __shared__ __attribute__((aligned(16))) int32_t smem[];
-
-  const int W = G * ipc;
-  // LDS: item[W + 1] (index 0 = the item before the window) | per-group words | H, T partials
-  int2* s_item = reinterpret_cast<int2*>(smem);
-  int32_t* s_meta = smem + 2 * ((W + 2 + 1) & ~1);  // 4 words per group: has_marker, head_partial, tail, head_row
-  float* s_H = reinterpret_cast<float*>(s_meta + ((4 * G + 3) & ~3));
-  float* s_T = s_H + G * FT;
-
-  const int tid = threadIdx.x;
-  const int64_t w = blockIdx.x;
-  const int64_t base = w * W;
-
-  // ---- one coalesced pass: the window's items (+ the item before it)
-  for (int i = tid; i < W; i += BLOCK) s_item[1 + i] = items[base + i];
-  if (tid == 0) s_item[0] = w > 0 ? items[base - 1] : make_int2(kMarker, -1);
-  stamp(epi, 0);
-  const int32_t hslot = pp.head[w];
-  const int32_t tslot = pp.tail[w];
-  __syncthreads();
-  stamp(epi, 1);
-
-  const int g = tid / LPR;
-  const int lg = tid % LPR;
-  const int64_t col_base = (int64_t)blockIdx.y * FT;
-  int64_t colv[VPL];
-  bool colok[VPL];
-  T bv[VPL];  // bias of this lane's columns, loaded once
-#pragma unroll
-  for (int v = 0; v < VPL; ++v) {
-    colv[v] = col_base + (int64_t)(v * LPR + lg) * VEC;
-    colok[v] = colv[v] < F;
-    bv[v] = (epi.bias && colok[v]) ? V::load(epi.bias + colv[v]) : V::zero();
-  }
-  Proj<NP, LPR, VPL, VEC> proj;
-  proj.load(pa, F, colv, colok);
-  const bool store_main = NP == 0 || pa.store_main;
-  float* myH = s_H + g * FT;
-  float* myT = s_T + g * FT;
-
-  const int i0 = 1 + g * ipc;                       // first item of this group's chunk in s_item
-  const bool head_partial = s_item[i0 - 1].x >= 0;  // the chunk starts inside a row
-  bool has_marker = false;
-  int32_t head_row = -1;
-
-  T acc[VPL];
-#pragma unroll
-  for (int v = 0; v < VPL; ++v) acc[v] = V::zero();
-
-  for (int k0 = 0; k0 < ipc; k0 += U) {
-    T gv[U][VPL];
+  for (int32_t k0 = b + q; k0 < e; k0 += S * U) {
     int2 it[U];
 #pragma unroll
-    for (int u = 0; u < U; ++u) {
-      it[u] = (k0 + u < ipc) ? s_item[i0 + k0 + u] : make_int2(kPad, 0);
-      const float* brow = B + (int64_t)(it[u].x >= 0 ? it[u].x : 0) * ldb;
-#pragma unroll
-      for (int v = 0; v < VPL; ++v)
-        gv[u][v] = (it[u].x >= 0 && colok[v]) ? V::load(brow + colv[v]) : V::zero();
+    for (int j = 0; j < U; ++j) {
+      const int32_t k = k0 + S * j;
+      it[j] = k < e ? items[k] : make_int2(-1, 0);
     }
+    T g[U];
 #pragma unroll
-    for (int u = 0; u < U; ++u) {
-      if (it[u].x >= 0) {
-        const float a = __int_as_float(it[u].y);
+    for (int j = 0; j < U; ++j)
+      g[j] = (it[j].x >= 0 && colok) ? V::load(B + (int64_t)it[j].x * ldb + colv) : V::zero();
 #pragma unroll
-        for (int v = 0; v < VPL; ++v) V::fma(acc[v], a, gv[u][v]);
-      } else if (it[u].x == kMarker) {
-        const int32_t r = it[u].y;
-        if (!has_marker && head_partial) {
-#pragma unroll
-          for (int v = 0; v < VPL; ++v) V::store(myH + (v * LPR + lg) * VEC, acc[v]);
-          head_row = r;
-        } else {
-          float* dst = C + (int64_t)r * ldc;
-          T h[VPL];
-#pragma unroll
-          for (int v = 0; v < VPL; ++v) {
-            h[v] = colok[v] ? V::epi(epi, acc[v], bv[v], r, colv[v]) : V::zero();
-            if (colok[v] && store_main) V::store(dst + colv[v], h[v]);
-          }
-          proj.apply(pa, h, r, lg);
-        }
-        has_marker = true;
-#pragma unroll
-        for (int v = 0; v < VPL; ++v) acc[v] = V::zero();
-      }
-    }
+    for (int j = 0; j < U; ++j)
+      if (it[j].x >= 0) V::fma(acc, __int_as_float(it[j].y), g[j]);
   }
-  const bool tail = s_item[i0 + ipc - 1].x >= 0;  // the chunk ends inside a row
-  if (tail) {
-#pragma unroll
-    for (int v = 0; v < VPL; ++v) V::store(myT + (v * LPR + lg) * VEC, acc[v]);
-  }
-  stamp(epi, 2);
-  if (lg == 0) {
-    s_meta[4 * g + 0] = has_marker;
-    s_meta[4 * g + 1] = head_partial;
-    s_meta[4 * g + 2] = tail;
-    s_meta[4 * g + 3] = head_row;
-  }
-  __syncthreads();
+}
 
-  // ---- rows split between groups of this window: the marker's group adds, in group order,
-  //      T of the nearest earlier group holding a marker (the row's start) and T of the
-  //      marker-free groups in between, then its own H.
-  if (head_row >= 0) {
-    int j = g - 1;
-    while (j >= 0 && !s_meta[4 * j + 0]) --j;
-    // the row starts in group j's tail if j ends inside a row, else at group j+1
-    const int jf = (j >= 0 && s_meta[4 * j + 2]) ? j : j + 1;
-    const bool from_before = j < 0 && s_meta[1];  // the row started in an earlier window
-    T h[VPL];
+// Sum over the 64/LPR lane groups of a wave (xor butterfly: every lane ends
+// with bitwise the same sum, since each level adds the same two operands).
+template <int LPR, typename T>
+__device__ __forceinline__ void wave_group_sum(T& acc) {
+  float* f = reinterpret_cast<float*>(&acc);
 #pragma unroll
-    for (int v = 0; v < VPL; ++v) {
-      const int off = (v * LPR + lg) * VEC;
-      T s = V::zero();
-      for (int q = jf; q < g; ++q) V::add(s, V::load(s_T + q * FT + off));
-      V::add(s, V::load(myH + off));
-      h[v] = V::zero();
-      if (!colok[v]) continue;
-      if (from_before) {
-        store_coherent(part + (int64_t)hslot * part_ld + colv[v], s);
-      } else {
-        h[v] = V::epi(epi, s, bv[v], head_row, colv[v]);
-        if (store_main) V::store(C + (int64_t)head_row * ldc + colv[v], h[v]);
+  for (int off = LPR; off < 64; off <<= 1)
+#pragma unroll
+    for (int i = 0; i < (int)(sizeof(T) / 4); ++i) f[i] += __shfl_xor(f[i], off, 64);
+}
+
+// Epilogue + store (+ fused projection) of one finished row by lane group
+// q == 0 of the calling lanes.
+template <int LPR, int VEC, int NP>
+__device__ __forceinline__ void finish_row(const typename Vec<VEC>::T& acc, int32_t r, int64_t colv, bool colok,
+                                           const typename Vec<VEC>::T& bv, int lg, float* __restrict__ C,
+                                           int64_t ldc, const Epi& epi, bool store_main,
+                                           const Proj<NP, LPR, 1, VEC>& proj, const ProjArgs& pa) {
+  using V = Vec<VEC>;
+  using T = typename V::T;
+  const T h = colok ? V::epi(epi, acc, bv, r, colv) : V::zero();
+  if (colok && store_main) V::store(C + (int64_t)r * ldc + colv, h);
+  proj.apply(pa, &h, r, lg);
+}
+
+// grid.x: [0, nhb) heavy blocks, one heavy segment per wavefront; then light
+// blocks, one light row per lane group.  grid.y: column tiles of LPR*VEC.
+template <int BLOCK, int LPR, int VEC, int U, int NP>
+__global__ void __launch_bounds__(BLOCK)
+spmm_row_kernel(RowPlan rp, int32_t nhb, const float* __restrict__ B, int64_t ldb, int32_t F,
+                float* __restrict__ C, int64_t ldc, Epi epi, float* __restrict__ part, int64_t part_ld,
+                ProjArgs pa) {
+  using V = Vec<VEC>;
+  using T = typename V::T;
+  constexpr int SG = BLOCK / LPR;  // lane groups per workgroup
+  constexpr int SW = 64 / LPR;     // lane groups per wavefront
+  constexpr int WPB = BLOCK / 64;  // wavefronts per workgroup
+  const int tid = threadIdx.x;
+  const int lg = tid % LPR;
+  const int64_t colv = (int64_t)blockIdx.y * (LPR * VEC) + (int64_t)lg * VEC;
+  const bool colok = colv < F;
+  stamp(epi, 0);
+  T bv = (epi.bias && colok) ? V::load(epi.bias + colv) : V::zero();
+  Proj<NP, LPR, 1, VEC> proj;
+  proj.load(pa, F, &colv, &colok);
+  const bool store_main = NP == 0 || pa.store_main;
+  T acc = V::zero();
+
+  if ((int32_t)blockIdx.x >= nhb) {
+    // ---- light rows: one unit per lane group
+    int32_t u = rp.nhunits + ((int32_t)blockIdx.x - nhb) * SG + tid / LPR;
+    if (LPR == 64) u = __builtin_amdgcn_readfirstlane(u);
+    if (u >= rp.nunits) return;
+    const int4 un = rp.units[u];
+    stamp(epi, 1);
+    gather_rows<VEC, U, 1>(rp.items, un.y, un.z, 0, B, ldb, colv, colok, acc);
+    stamp(epi, 2);
+    finish_row<LPR, VEC, NP>(acc, un.x, colv, colok, bv, lg, C, ldc, epi, store_main, proj, pa);
+    stamp(epi, 3);
+    return;
+  }
+
+  // ---- heavy segment: one unit per wavefront, lane group q takes nonzeros q, q + SW, ...
+  const int lane = tid & 63;
+  const int q = lane / LPR;
+  const int32_t u = __builtin_amdgcn_readfirstlane((int32_t)blockIdx.x * WPB + tid / 64);
+  if (u >= rp.nhunits) return;
+  const int4 un = rp.units[u];
+  stamp(epi, 1);
+  gather_rows<VEC, U, SW>(rp.items, un.y, un.z, q, B, ldb, colv, colok, acc);
+  wave_group_sum<LPR>(acc);
+  stamp(epi, 2);
+  if (un.w < 0) {  // the row's only segment
+    if (q == 0) finish_row<LPR, VEC, NP>(acc, un.x, colv, colok, bv, lg, C, ldc, epi, store_main, proj, pa);
+    stamp(epi, 3);
+    return;
+  }
+  // publish this segment's partial, then count in; the last arriver sums all of
+  // the row's partials in segment order
+  if (q == 0 && colok) store_coherent(part + (int64_t)u * part_ld + colv, acc);
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  const int4 hv = rp.heavy[un.w];
+  int32_t* ctr = rp.cnt + (int64_t)un.w * kMaxColTiles + blockIdx.y;
+  int32_t arrived = 0;
+  if (lane == 0) arrived = __hip_atomic_fetch_add(ctr, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  arrived = __builtin_amdgcn_readfirstlane(arrived);
+  stamp(epi, 3);
+  if (arrived != hv.z - 1) return;
+  T sum = V::zero();
+  if (colok) {
+    // lane group q sums slots q, q + SW, ... (U loads in flight), then the butterfly
+    const float* p0 = part + (int64_t)hv.y * part_ld + colv;
+    for (int32_t s0 = q; s0 < hv.z; s0 += SW * U) {
+      T pv[U];
+#pragma unroll
+      for (int j = 0; j < U; ++j) {
+        const int32_t s = s0 + SW * j;
+        pv[j] = s < hv.z ? load_coherent<T>(p0 + (int64_t)s * part_ld) : V::zero();
       }
-    }
-    if (!from_before) proj.apply(pa, h, head_row, lg);
-    else finish_cross<LPR, VPL, VEC>(pp, pp.hfix[w], lg, colv, colok, bv, part, part_ld, C, ldc, epi, store_main,
-                                     proj, pa);
-  }
-  // ---- a heavy row leaving the window: partial of its part in this window
-  if (g == G - 1 && tail) {
-    int j = g;
-    while (j >= 0 && !s_meta[4 * j + 0]) --j;
-    const int jf = (j >= 0 && s_meta[4 * j + 2]) ? j : j + 1;
 #pragma unroll
-    for (int v = 0; v < VPL; ++v) {
-      const int off = (v * LPR + lg) * VEC;
-      T s = V::zero();
-      for (int q = jf; q <= g; ++q) V::add(s, V::load(s_T + q * FT + off));
-      if (colok[v]) store_coherent(part + (int64_t)tslot * part_ld + colv[v], s);
+      for (int j = 0; j < U; ++j)
+        if (s0 + SW * j < hv.z) V::add(sum, pv[j]);
     }
-    finish_cross<LPR, VPL, VEC>(pp, pp.tfix[w], lg, colv, colok, bv, part, part_ld, C, ldc, epi, store_main, proj,
-                                pa);
   }
+  wave_group_sum<LPR>(sum);
+  if (q == 0) finish_row<LPR, VEC, NP>(sum, hv.x, colv, colok, bv, lg, C, ldc, epi, store_main, proj, pa);
+  if (lane == 0) __hip_atomic_store(ctr, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
   stamp(epi, 3);
 }
 
@@ -648,108 +573,91 @@ inline int next_pow2(int v) {
   return p;
 }
 
-// Lanes per group from F alone (so a plan's G does not depend on pointer
-// alignment, which only picks VEC/VPL at launch).
+// Lanes per group from F alone (a plan does not depend on pointer alignment,
+// which only picks VEC at launch).  Wide rows use 16-lane groups (64 columns
+// per column tile): a heavy segment's nonzeros then interleave over 4 groups
+// of its wavefront (a 4x shorter gather chain), and 4 light rows share a
+// wavefront -- measured faster than 64-lane groups at F = 200 and 256
+// (profiles/r01_sweep_rows.log).
 inline int choose_lpr(int32_t F, int lanes_hint) {
   if (lanes_hint > 0) return next_pow2(lanes_hint > 64 ? 64 : lanes_hint);
   const int Wv = (F % 4 == 0) ? F / 4 : F;
-  return Wv <= 64 ? next_pow2(Wv < 1 ? 1 : Wv) : 64;
+  if (Wv > 16) return 16;
+  return next_pow2(Wv < 1 ? 1 : Wv);
 }
 
-// Workgroup size: small groups use one wave so a window holds at most 32 groups
-// (bounds the in-LDS chain walk of split rows).
+// Narrow groups use one-wave workgroups so a light launch still spans the chip.
 inline int choose_block(int lpr) { return lpr >= 8 ? 256 : 64; }
-inline int choose_groups(int32_t F, int lanes_hint) {
-  const int lpr = choose_lpr(F, lanes_hint);
-  return choose_block(lpr) / lpr;
-}
 
-struct Cfg {
-  int lpr, vpl, vec, col_tiles, block;
-};
-
-inline Cfg choose_cfg(int32_t F, int vec, int lpr) {
-  Cfg c;
-  c.vec = vec;
-  c.lpr = lpr;
-  c.block = choose_block(lpr);
-  const int Wv = (F + vec - 1) / vec;
-  int vpl = (Wv + lpr - 1) / lpr;
-  vpl = vpl <= 1 ? 1 : (vpl <= 2 ? 2 : 4);
-  c.vpl = vpl;
-  c.col_tiles = (Wv + lpr * vpl - 1) / (lpr * vpl);
-  return c;
-}
-
-constexpr int kMaxLds = 65536;
-
-inline size_t lds_bytes(int G, int ipc, int FT) {
-  const int W = G * ipc;
-  return (size_t)(2 * ((W + 2 + 1) & ~1) + ((4 * G + 3) & ~3) + 2 * G * FT) * 4;
-}
-
-struct Launch {
-  const int32_t* plan;
-  Layout L;
-  int32_t ipc, nfix;
+struct RowLaunch {
+  RowPlan rp;
   const float* B;
   int64_t ldb;
   int32_t F;
   float* C;
   int64_t ldc;
   Epi epi;
-  float* part;  // path partial slots
+  float* part;  // heavy-segment partial slots
   int64_t part_ld;
-  int col_tiles;
   ProjArgs pa;
   hipStream_t s;
 };
 
-template <int BLOCK, int LPR, int VPL, int VEC, int NP>
-int launch_path(const Launch& a) {
-  constexpr int G = BLOCK / LPR;
-  constexpr int UB = NP > 0 ? 8 : 16;  // the projection holds W in registers: shorter batches
-  constexpr int U = (UB / VPL) < 2 ? 2 : UB / VPL;
-  const size_t lds = lds_bytes(G, a.ipc, LPR * VPL * VEC);
-  if (lds > (size_t)kMaxLds) {
-    set_error("gcnk_spmm_csr_f32: ipc %d needs %zu B of LDS (> %d) at %d groups", a.ipc, lds, kMaxLds, G);
+template <int BLOCK, int LPR, int VEC, int U, int NP>
+int launch_rows(const RowLaunch& a) {
+  constexpr int SG = BLOCK / LPR, WPB = BLOCK / 64;
+  const int64_t nhb = ((int64_t)a.rp.nhunits + WPB - 1) / WPB;
+  const int64_t nlb = ((int64_t)a.rp.nunits - a.rp.nhunits + SG - 1) / SG;
+  if (nhb + nlb == 0) return GCNK_OK;
+  if (nhb + nlb > (int64_t)INT32_MAX) {
+    set_error("gcnk_spmm_csr_f32: %lld workgroups exceed the grid", (long long)(nhb + nlb));
     return GCNK_EUNSUP;
   }
-  if (a.col_tiles > kMaxColTiles) {
-    set_error("gcnk_spmm_csr_f32: F=%d needs %d column tiles (> %d)", a.F, a.col_tiles, kMaxColTiles);
-    return GCNK_EUNSUP;
+  const int64_t tileF = (int64_t)LPR * VEC;
+  const int64_t tiles = (a.F + tileF - 1) / tileF;
+  // column windows of at most kMaxColTiles tiles (arrival counters per heavy row x tile;
+  // the last arriver re-arms them, so consecutive windows on one stream reuse them)
+  for (int64_t t0 = 0; t0 < tiles; t0 += kMaxColTiles) {
+    const int64_t c0 = t0 * tileF;
+    const int32_t Fw = (int32_t)std::min<int64_t>(a.F - c0, kMaxColTiles * tileF);
+    Epi e = a.epi;
+    e.bias = e.bias ? e.bias + c0 : nullptr;
+    e.mask = e.mask ? e.mask + c0 : nullptr;
+    e.offset += (uint64_t)c0;  // hash index shifts with the column
+    hipLaunchKernelGGL((spmm_row_kernel<BLOCK, LPR, VEC, U, NP>),
+                       dim3((unsigned)(nhb + nlb), (unsigned)((Fw + tileF - 1) / tileF)), dim3(BLOCK), 0, a.s, a.rp,
+                       (int32_t)nhb, a.B + c0, a.ldb, Fw, a.C ? a.C + c0 : nullptr, a.ldc, e,
+                       a.part ? a.part + c0 : nullptr, a.part_ld, a.pa);
+    const int rc = launch_check("spmm_row_kernel");
+    if (rc) return rc;
   }
-  if (a.L.nwin == 0) return GCNK_OK;
-  PathPlan pp{reinterpret_cast<const int2*>(a.plan + a.L.items), a.plan + a.L.head, a.plan + a.L.tail,
-              a.plan + a.L.hfix, a.plan + a.L.tfix, a.plan + a.L.fix, const_cast<int32_t*>(a.plan + a.L.cnt)};
-  hipLaunchKernelGGL((spmm_path_kernel<BLOCK, LPR, VPL, VEC, U, NP>), dim3((unsigned)a.L.nwin, a.col_tiles),
-                     dim3(BLOCK), lds, a.s, pp, a.ipc, a.B, a.ldb, a.F, a.C, a.ldc, a.epi, a.part, a.part_ld, a.pa);
-  return launch_check("spmm_path_kernel");
+  return GCNK_OK;
 }
 
 template <int VEC>
-int dispatch_path(const Cfg& c, const Launch& a) {
-#define GCNK_CASE(BL, L, P) \
-  if (c.block == BL && c.lpr == L && c.vpl == P) return launch_path<BL, L, P, VEC, 0>(a);
-  GCNK_CASE(64, 1, 1) GCNK_CASE(64, 2, 1) GCNK_CASE(64, 4, 1) GCNK_CASE(256, 8, 1) GCNK_CASE(256, 16, 1)
-  GCNK_CASE(256, 32, 1) GCNK_CASE(256, 64, 1) GCNK_CASE(64, 1, 2) GCNK_CASE(64, 2, 2) GCNK_CASE(64, 4, 2)
-  GCNK_CASE(256, 8, 2) GCNK_CASE(256, 16, 2) GCNK_CASE(256, 32, 2) GCNK_CASE(256, 64, 2) GCNK_CASE(64, 1, 4)
-  GCNK_CASE(64, 2, 4) GCNK_CASE(64, 4, 4) GCNK_CASE(256, 8, 4) GCNK_CASE(256, 16, 4) GCNK_CASE(256, 32, 4)
-  GCNK_CASE(256, 64, 4)
-#undef GCNK_CASE
-  set_error("gcnk_spmm_csr_f32: unsupported lanes/vectors config (%d,%d)", c.lpr, c.vpl);
+int dispatch_rows(int lpr, const RowLaunch& a) {
+  switch (lpr) {
+    case 1: return launch_rows<64, 1, VEC, 8, 0>(a);
+    case 2: return launch_rows<64, 2, VEC, 8, 0>(a);
+    case 4: return launch_rows<64, 4, VEC, 8, 0>(a);
+    case 8: return launch_rows<256, 8, VEC, 8, 0>(a);
+    case 16: return launch_rows<256, 16, VEC, 8, 0>(a);
+    case 32: return launch_rows<256, 32, VEC, 8, 0>(a);
+    case 64: return launch_rows<256, 64, VEC, 8, 0>(a);
+  }
+  set_error("gcnk_spmm_csr_f32: unsupported lanes per group %d", lpr);
   return GCNK_EUNSUP;
 }
 
 // Fused projection variants: float4 columns, one column tile, groups of >= 16 lanes.
 template <int NP>
-int dispatch_path_proj(const Cfg& c, const Launch& a) {
-#define GCNK_CASE(L, P) \
-  if (c.block == 256 && c.lpr == L && c.vpl == P) return launch_path<256, L, P, 4, NP>(a);
-  GCNK_CASE(16, 1) GCNK_CASE(32, 1) GCNK_CASE(64, 1) GCNK_CASE(16, 2) GCNK_CASE(32, 2) GCNK_CASE(64, 2)
-  GCNK_CASE(16, 4) GCNK_CASE(32, 4) GCNK_CASE(64, 4)
-#undef GCNK_CASE
-  set_error("gcnk_spmm_proj_f32: no fused-projection kernel for lanes/vectors (%d,%d)", c.lpr, c.vpl);
+int dispatch_rows_proj(int lpr, const RowLaunch& a) {
+  switch (lpr) {
+    case 16: return launch_rows<256, 16, 4, 8, NP>(a);
+    case 32: return launch_rows<256, 32, 4, 8, NP>(a);
+    case 64: return launch_rows<256, 64, 4, 8, NP>(a);
+  }
+  set_error("gcnk_spmm_proj_f32: no fused-projection kernel for %d lanes per group", lpr);
   return GCNK_EUNSUP;
 }
 
@@ -796,8 +704,7 @@ inline int launch_tile(bool v4, int nt_need, unsigned nitems, const TileArgs& t,
 // Host side of the plan.
 struct HostPlan {
   int32_t hdr[16];
-  std::vector<int32_t> start;   // item position of each path row, -1 for tile rows
-  std::vector<int32_t> head, tail, hfix, tfix, fix;
+  std::vector<int32_t> units, heavy;  // row-kernel units (int4 each), heavy rows (int4 each)
   std::vector<int32_t> tdesc, tcols, red, trows;
   std::vector<float> tfrag, dval;  // dval: extracted diagonal of tile rows (M, or empty)
 };
@@ -917,56 +824,38 @@ int host_plan(const int32_t* rowptr_dev, const int32_t* colind_dev, const float*
     if (any_diag) hp.dval = std::move(dv);
   }
 
-  // ---- path windows over the other rows
-  const int64_t W = (int64_t)groups * ipc;
-  const int64_t heavy = W / 2;
-  hp.start.assign((size_t)M, -1);
-  int64_t pos = 0;
+  // ---- row units over the other rows.  A light row (<= ipc nonzeros) is one
+  //      unit, in row order; a heavier row is cut into segments of about
+  //      ipc * groups nonzeros (the groups of one wavefront share a segment),
+  //      at most kMaxSeg of them; heavy segments come first in the unit list.
+  const int64_t seg = (int64_t)ipc * groups;
+  std::vector<int32_t> light;
+  int32_t nheavy = 0;
+  hp.units.clear();
+  hp.heavy.clear();
   for (int32_t r = 0; r < M; ++r) {
     if (tile_row[(size_t)r]) continue;
-    const int64_t len = (int64_t)rp[r + 1] - rp[r] + 1;
-    const int64_t off = pos % W;
-    if (len <= heavy && off + len > W) pos += W - off;
-    hp.start[(size_t)r] = (int32_t)pos;
-    pos += len;
-    if (pos >= (int64_t)INT32_MAX) {
-      set_error("gcnk_spmm_plan: item stream exceeds 2^31 items");
-      return GCNK_EUNSUP;
+    const int64_t b = rp[r], deg = (int64_t)rp[r + 1] - b;
+    if (deg <= ipc) {
+      light.insert(light.end(), {r, (int32_t)b, rp[r + 1], -1});
+      continue;
     }
+    const int64_t nseg = std::min<int64_t>((deg + seg - 1) / seg, kMaxSeg);
+    const int32_t hid = nseg > 1 ? nheavy++ : -1;
+    if (nseg > 1) hp.heavy.insert(hp.heavy.end(), {r, (int32_t)(hp.units.size() / 4), (int32_t)nseg, 0});
+    for (int64_t s = 0; s < nseg; ++s)
+      hp.units.insert(hp.units.end(),
+                      {r, (int32_t)(b + deg * s / nseg), (int32_t)(b + deg * (s + 1) / nseg), hid});
   }
-  const int64_t nwin = (pos + W - 1) / W;
-  hp.head.assign((size_t)nwin, -1);
-  hp.tail.assign((size_t)nwin, -1);
-  // heavy rows crossing window boundaries: tail slot in every window they leave,
-  // head slot in the window of their marker; slots numbered in window order,
-  // a window's head before its tail (contiguous per row).
-  struct Cross { int32_t row; int64_t wa, wb; };
-  std::vector<Cross> cross;
-  for (int32_t r = 0; r < M; ++r) {
-    if (hp.start[(size_t)r] < 0) continue;
-    const int64_t a0 = hp.start[(size_t)r], e = a0 + (rp[r + 1] - rp[r]);  // e = marker position
-    const int64_t wa = a0 / W, wb = e / W;
-    if (wa < wb) cross.push_back({r, wa, wb});
+  const int64_t nh = (int64_t)hp.units.size() / 4;
+  hp.units.insert(hp.units.end(), light.begin(), light.end());
+  const int64_t nunits = (int64_t)hp.units.size() / 4;
+  if (nunits >= (int64_t)INT32_MAX) {
+    set_error("gcnk_spmm_plan: %lld row units exceed 2^31", (long long)nunits);
+    return GCNK_EUNSUP;
   }
-  for (const Cross& c : cross) {
-    for (int64_t x = c.wa; x < c.wb; ++x) hp.tail[(size_t)x] = 1;
-    hp.head[(size_t)c.wb] = 1;
-  }
-  int32_t slot = 0;
-  for (int64_t x = 0; x < nwin; ++x) {
-    if (hp.head[(size_t)x] >= 0) hp.head[(size_t)x] = slot++;
-    if (hp.tail[(size_t)x] >= 0) hp.tail[(size_t)x] = slot++;
-  }
-  hp.hfix.assign((size_t)nwin, -1);
-  hp.tfix.assign((size_t)nwin, -1);
-  for (size_t i = 0; i < cross.size(); ++i) {
-    const Cross& c = cross[i];
-    hp.fix.insert(hp.fix.end(), {c.row, hp.tail[(size_t)c.wa], hp.head[(size_t)c.wb]});
-    for (int64_t x = c.wa; x < c.wb; ++x) hp.tfix[(size_t)x] = (int32_t)i;
-    hp.hfix[(size_t)c.wb] = (int32_t)i;
-  }
-  const int32_t h[16] = {kMagic, M, K, groups, ipc, (int32_t)W, (int32_t)nwin, (int32_t)cross.size(), slot,
-                         ntile, nred, nslabs, ntblk, any_diag ? 1 : 0, (int32_t)heavy, 0};
+  const int32_t h[16] = {kMagic, M,     K,      groups, ipc,  (int32_t)nunits, (int32_t)nh, nheavy,
+                         ntile,  nred, nslabs, ntblk,  any_diag ? 1 : 0, (int32_t)nnz, 0, 0};
   std::copy(h, h + 16, hp.hdr);
   return GCNK_OK;
 }
@@ -979,17 +868,15 @@ using namespace gcnk;
 static unsigned long long* g_stamps = nullptr;
 extern "C" void gcnk_debug_set_stamps(void* buf) { g_stamps = (unsigned long long*)buf; }
 
-extern "C" int32_t gcnk_spmm_groups(int32_t F, int32_t lanes_hint) { return choose_groups(F, lanes_hint); }
+extern "C" int32_t gcnk_spmm_groups(int32_t F, int32_t lanes_hint) { return 64 / choose_lpr(F, lanes_hint); }
 
 extern "C" int32_t gcnk_spmm_default_ipc(int32_t M, int64_t nnz, int32_t F, int32_t lanes_hint) {
   (void)M;
   (void)nnz;
-  const int lpr = choose_lpr(F, lanes_hint);
-  const int G = choose_block(lpr) / lpr;
-  const Cfg c = choose_cfg(F, F % 4 == 0 ? 4 : 1, lpr);
-  int ipc = lpr >= 16 ? 16 : 8;
-  while (ipc > 2 && lds_bytes(G, ipc, lpr * c.vpl * c.vec) > (size_t)kMaxLds) ipc /= 2;
-  return ipc;
+  // light-row limit (and per-group share of a heavy segment): two U = 8 gather
+  // batches for groups of >= 8 lanes, one for narrow groups (sweep:
+  // profiles/r01_sweep_rows.log)
+  return choose_lpr(F, lanes_hint) >= 8 ? 16 : 8;
 }
 
 extern "C" int64_t gcnk_spmm_plan_bytes(const int32_t* rowptr, const int32_t* colind, int32_t M, int32_t K,
@@ -1003,8 +890,7 @@ extern "C" int64_t gcnk_spmm_plan_bytes(const int32_t* rowptr, const int32_t* co
   const int rc = host_plan(rowptr, colind, nullptr, M, K, nnz, ipc, groups, dense_threshold, false,
                            (hipStream_t)stream, hp);
   if (rc) return rc;
-  // + M words of scratch (path row start positions) used while building
-  return (Layout(hp.hdr).total + M) * 4;
+  return Layout(hp.hdr).total * 4;
 }
 
 extern "C" int gcnk_spmm_plan_build(const int32_t* rowptr, const int32_t* colind, const float* val, int32_t M,
@@ -1019,41 +905,29 @@ extern "C" int gcnk_spmm_plan_build(const int32_t* rowptr, const int32_t* colind
   int rc = host_plan(rowptr, colind, val, M, K, nnz, ipc, groups, dense_threshold, true, s, hp);
   if (rc) return rc;
   const Layout L(hp.hdr);
-  if (plan_bytes < (L.total + M) * 4) {
-    set_error("gcnk_spmm_plan_build: plan buffer %lld B < %lld B", (long long)plan_bytes,
-              (long long)((L.total + M) * 4));
+  if (plan_bytes < L.total * 4) {
+    set_error("gcnk_spmm_plan_build: plan buffer %lld B < %lld B", (long long)plan_bytes, (long long)(L.total * 4));
     return GCNK_EARG;
   }
   int32_t* p = (int32_t*)plan;
-  int32_t* d_start = p + L.total;  // scratch words after the plan proper
   auto up = [&](int64_t off, const void* src, size_t bytes, const char* what) {
     if (!rc && bytes > 0) rc = hip_check(hipMemcpyAsync(p + off, src, bytes, hipMemcpyHostToDevice, s), what);
   };
   up(0, hp.hdr, sizeof(hp.hdr), "plan header");
-  up(L.head, hp.head.data(), hp.head.size() * 4, "plan head");
-  up(L.tail, hp.tail.data(), hp.tail.size() * 4, "plan tail");
-  up(L.hfix, hp.hfix.data(), hp.hfix.size() * 4, "plan head rows");
-  up(L.tfix, hp.tfix.data(), hp.tfix.size() * 4, "plan tail rows");
-  up(L.fix, hp.fix.data(), hp.fix.size() * 4, "plan fix");
-  if (!rc && L.nfix > 0)
-    rc = hip_check(hipMemsetAsync(p + L.cnt, 0, (size_t)L.nfix * kMaxColTiles * 4, s), "plan counters");
+  up(L.units, hp.units.data(), hp.units.size() * 4, "plan units");
+  up(L.heavy, hp.heavy.data(), hp.heavy.size() * 4, "plan heavy rows");
+  if (!rc && L.nheavy > 0)
+    rc = hip_check(hipMemsetAsync(p + L.cnt, 0, (size_t)L.nheavy * kMaxColTiles * 4, s), "plan counters");
   up(L.tdesc, hp.tdesc.data(), hp.tdesc.size() * 4, "plan tile desc");
   up(L.tcols, hp.tcols.data(), hp.tcols.size() * 4, "plan tile cols");
   up(L.tfrag, hp.tfrag.data(), hp.tfrag.size() * 4, "plan tile frags");
   up(L.red, hp.red.data(), hp.red.size() * 4, "plan tile reduce");
   up(L.trows, hp.trows.data(), hp.trows.size() * 4, "plan tile rows");
   up(L.dval, hp.dval.data(), hp.dval.size() * 4, "plan diagonal");
-  up(L.total, hp.start.data(), hp.start.size() * 4, "plan start");
-  const int64_t nitems = L.nwin * L.W;
-  int2* items = reinterpret_cast<int2*>(p + L.items);
-  if (!rc && nitems > 0) {
-    hipLaunchKernelGGL(fill_pad_kernel, dim3((unsigned)((nitems + 255) / 256)), dim3(256), 0, s, items, nitems);
-    rc = launch_check("fill_pad_kernel");
-  }
-  if (!rc && M > 0 && nitems > 0) {
-    hipLaunchKernelGGL(scatter_items_kernel, dim3((unsigned)((M + 3) / 4)), dim3(256), 0, s, rowptr, colind, val, M,
-                       d_start, items);
-    rc = launch_check("scatter_items_kernel");
+  if (!rc && nnz > 0) {
+    hipLaunchKernelGGL(pack_items_kernel, dim3((unsigned)((nnz + 255) / 256)), dim3(256), 0, s, colind, val, nnz,
+                       reinterpret_cast<int2*>(p + L.items));
+    rc = launch_check("pack_items_kernel");
   }
   // the host vectors must outlive the async copies
   const int rc2 = hip_check(hipStreamSynchronize(s), "plan build sync");
@@ -1081,9 +955,9 @@ static int64_t tile_fpad(int32_t F) { return ((int64_t)F + 15) & ~15LL; }
 extern "C" int64_t gcnk_spmm_workspace_bytes(const int32_t* hdr, int32_t F) {
   if (!hdr || hdr[0] != kMagic || F < 0) return GCNK_EARG;
   const int64_t ld = ((int64_t)F + 3) & ~3LL;
-  const int64_t path = (int64_t)hdr[8] * ld * 4;
-  const int64_t slabs = (int64_t)hdr[11] * kRB * tile_fpad(F) * 4;
-  return ((path + 255) & ~255LL) + slabs;
+  const int64_t rows = (int64_t)hdr[6] * ld * 4;
+  const int64_t slabs = (int64_t)hdr[10] * kRB * tile_fpad(F) * 4;
+  return ((rows + 255) & ~255LL) + slabs;
 }
 
 static int spmm_impl(const void* plan, const int32_t* hdr, const float* B, int64_t ldb, int32_t F, float* C,
@@ -1094,7 +968,7 @@ static int spmm_impl(const void* plan, const int32_t* hdr, const float* B, int64
     set_error("gcnk_spmm_csr_f32: bad argument (plan/header missing or not a gcnk plan, F=%d)", F);
     return GCNK_EARG;
   }
-  const int32_t M = hdr[1], K = hdr[2], groups = hdr[3], ipc = hdr[4];
+  const int32_t M = hdr[1], K = hdr[2];
   if (M == 0 || F == 0) return GCNK_OK;
   const bool proj = pa.W != nullptr;
   if (proj && (!pa.C2 || pa.P <= 0 || pa.ldw < pa.P || pa.ldc2 < pa.P)) {
@@ -1119,9 +993,9 @@ static int spmm_impl(const void* plan, const int32_t* hdr, const float* B, int64
     return GCNK_EARG;
   }
   const int lpr = choose_lpr(F, lanes_hint);
-  if (groups != choose_block(lpr) / lpr) {
-    set_error("gcnk_spmm_csr_f32: plan built for %d groups, this F/lanes uses %d (gcnk_spmm_groups)", groups,
-              choose_block(lpr) / lpr);
+  if (hdr[3] != 64 / lpr) {
+    set_error("gcnk_spmm_csr_f32: plan built for %d lane groups per wave, this F/lanes uses %d (gcnk_spmm_groups)",
+              hdr[3], 64 / lpr);
     return GCNK_EARG;
   }
   const int64_t need = gcnk_spmm_workspace_bytes(hdr, F);
@@ -1141,14 +1015,13 @@ static int spmm_impl(const void* plan, const int32_t* hdr, const float* B, int64
   e.offset = offset;
   e.code = epilogue;
   e.stamps = g_stamps;
-  const bool vec4 = (F % 4 == 0) && (ldb % 4 == 0) && (ldc % 4 == 0) && aligned16(B) && aligned16(C) &&
+  const bool vec4 = (F % 4 == 0) && (ldb % 4 == 0) && (ldc % 4 == 0) && aligned16(B) && (!C || aligned16(C)) &&
                     (!workspace || aligned16(workspace)) && (!bias || aligned16(bias));
   if (proj) {
-    // the projection needs whole rows in one group: path rows only, float4, one column tile
-    const Cfg c = choose_cfg(F, 4, lpr);
-    if (hdr[9] > 0 || !vec4 || c.col_tiles != 1 || pa.P > 32 || lpr < 16) {
-      set_error("gcnk_spmm_proj_f32: fused projection unsupported here (tile rows=%d vec4=%d col_tiles=%d P=%d lanes=%d)",
-                hdr[9], (int)vec4, c.col_tiles, pa.P, lpr);
+    // the projection needs whole rows in one group: row-kernel rows only, float4, one column tile
+    if (hdr[8] > 0 || !vec4 || F > lpr * 4 || pa.P > 32 || lpr < 16) {
+      set_error("gcnk_spmm_proj_f32: fused projection unsupported here (tile chunks=%d vec4=%d F=%d P=%d lanes=%d)",
+                hdr[8], (int)vec4, F, pa.P, lpr);
       return GCNK_EUNSUP;
     }
   }
@@ -1156,8 +1029,8 @@ static int spmm_impl(const void* plan, const int32_t* hdr, const float* B, int64
   const int32_t* p = (const int32_t*)plan;
   const Layout L(hdr);
   const int64_t part_ld = ((int64_t)F + 3) & ~3LL;
-  const int64_t path_ws = ((int64_t)hdr[8] * part_ld * 4 + 255) & ~255LL;
-  float* slabs = workspace ? reinterpret_cast<float*>(reinterpret_cast<char*>(workspace) + path_ws) : nullptr;
+  const int64_t rows_ws = ((int64_t)hdr[6] * part_ld * 4 + 255) & ~255LL;
+  float* slabs = workspace ? reinterpret_cast<float*>(reinterpret_cast<char*>(workspace) + rows_ws) : nullptr;
   const int64_t slab_ld = tile_fpad(F);
 
   // ---- dense blocks: tile kernel (+ slab reduce)
@@ -1187,12 +1060,14 @@ static int spmm_impl(const void* plan, const int32_t* hdr, const float* B, int64
       if (rc) return rc;
     }
   }
-  // ---- remaining rows: path kernel (+ fix-up)
-  if (L.nwin > 0) {
-    const Cfg c = choose_cfg(F, vec4 ? 4 : 1, lpr);
-    Launch a{p, L, ipc, (int32_t)L.nfix, B, ldb, F, C, ldc, e, workspace, part_ld, c.col_tiles, pa, s};
-    if (proj) return pa.P <= 8 ? dispatch_path_proj<8>(c, a) : dispatch_path_proj<32>(c, a);
-    return vec4 ? dispatch_path<4>(c, a) : dispatch_path<1>(c, a);
+  // ---- remaining rows: row kernel (heavy rows finished in-launch)
+  if (L.nunits > 0) {
+    RowPlan rp{reinterpret_cast<const int2*>(p + L.items), reinterpret_cast<const int4*>(p + L.units),
+               reinterpret_cast<const int4*>(p + L.heavy), const_cast<int32_t*>(p + L.cnt), (int32_t)L.nunits,
+               (int32_t)L.nhunits};
+    RowLaunch a{rp, B, ldb, F, C, ldc, e, workspace, part_ld, pa, s};
+    if (proj) return pa.P <= 8 ? dispatch_rows_proj<8>(lpr, a) : dispatch_rows_proj<32>(lpr, a);
+    return vec4 ? dispatch_rows<4>(lpr, a) : dispatch_rows<1>(lpr, a);
   }
   return GCNK_OK;
 }

@@ -103,6 +103,8 @@ def spmm_proj(a, B, W, bias=None, epilogue=_lib.EPI_NONE, mask=None, scale=1.0, 
         raise RuntimeError(f"spmm_proj shape mismatch: {tuple(a.shape)} @ {tuple(B.shape)} @ {tuple(W.shape)}")
     P = W.shape[1]
     lib = _lib.load()
+    if not lanes:
+        lanes = 64   # the projection needs a whole row in one lane group (one column tile)
     if ipc is None:
         ipc = default_ipc(a, F, lanes)
     groups = int(lib.gcnk_spmm_groups(F, int(lanes)))

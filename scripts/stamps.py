@@ -1,6 +1,8 @@
-"""Debug timeline of the SpMM main kernel: per-workgroup s_memrealtime stamps
-(100 MHz) at entry / items staged / chunk walked / exit.  Prints a summary per
-case (kernel span, per-phase medians, how dispatch start times spread)."""
+"""Debug timeline of the SpMM row kernel: per-workgroup s_memrealtime stamps
+(100 MHz, wave 0 of each workgroup) at entry / unit loaded / gathers summed /
+stored (heavy segments: counted in; the last arriver restamps after its
+combine).  Prints a summary per case and per block kind (heavy-segment blocks
+come first in the grid, then light-row blocks)."""
 import json
 import os
 import sys
@@ -22,8 +24,9 @@ def main():
     A = as_csr(r8["adj"].to(dev))
     X = as_csr(r8["features"].to(dev))
     only = sys.argv[1:] or None
+    # (column tile 0 only: grid rows of other tiles are not split by kind)
     cases = [("R8_A_F200", A, 200, 0, None), ("R8_A_F8", A, 8, 0, None),
-             ("R8_X_F200", X, 200, 0, None), ("R8_X_F8", X, 8, 0, None)]
+             ("R8_A_F200_l16i16", A, 200, 16, 16), ("R8_A_F200_i8", A, 200, 0, 8)]
     cases = [c for c in cases if only is None or c[0] in only]
     for name, a, F, lanes, ipc in cases:
         B = torch.randn(a.shape[1], F, device=dev)
@@ -36,11 +39,22 @@ def main():
         ops.spmm(a, B, out=out, lanes=lanes, ipc=ipc)
         torch.cuda.synchronize()
         lib.gcnk_debug_set_stamps(None)
-        s = buf.view(-1, 4).cpu().numpy()
-        s = s[s[:, 0] > 0].astype(np.float64)
-        t0 = s[:, 0].min()
-        s = (s - t0) / 100.0  # µs
-        span = s[:, 3].max()
+        hdr = list(a._plans.values())[-1].header
+        nhb = (hdr[6] + 3) // 4 if hdr[3] <= 8 else hdr[6]  # 256-thread blocks hold 4 heavy waves
+        s_all = buf.view(-1, 4).cpu().numpy().astype(np.float64)
+        t0 = s_all[s_all[:, 0] > 0, 0].min()
+        for kind, rows in (("heavy", s_all[:nhb]), ("light", s_all[nhb:]), ("all", s_all)):
+            s = rows[(rows[:, 0] > 0) & (rows[:, 3] > 0)]
+            if len(s) == 0:
+                continue
+            s = (s - t0) / 100.0  # µs
+            summarize(name + ":" + kind, s)
+
+
+def summarize(name, s):
+    import numpy as np
+    span = s[:, 3].max()
+    if True:
         res = {
             "case": name, "wgs": int(len(s)), "span_us": round(span, 2),
             "entry_p50_us": round(float(np.median(s[:, 0])), 2), "entry_max_us": round(float(s[:, 0].max()), 2),

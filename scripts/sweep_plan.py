@@ -39,8 +39,8 @@ def main():
                     e0.record(); g.replay(); e1.record(); e1.synchronize()
                     best = min(best, e0.elapsed_time(e1) * 1e3 / reps)
                 hdr = [p for k, p in a._plans.items() if k[2] == float(thr)][-1].header
-                print(json.dumps({"op": name, "F": F, "thr": thr, "us": round(best, 2), "ntile": hdr[9], "nred": hdr[10],
-                                  "nwin": hdr[6], "nfix": hdr[7], "diag": hdr[13]}), flush=True)
+                print(json.dumps({"op": name, "F": F, "thr": thr, "us": round(best, 2), "ntile": hdr[8], "nred": hdr[9],
+                                  "nunits": hdr[5], "nhunits": hdr[6], "diag": hdr[12]}), flush=True)
                 del g
 
 

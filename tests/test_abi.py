@@ -28,11 +28,12 @@ def test_library_exports_every_declared_symbol():
     assert set(declared) == set(_lib.SIGNATURES), "ctypes signatures out of sync with include/gcnk.h"
 
 
-MAGIC = 0x474E4B34  # plan header word 0 ("GNK4")
+MAGIC = 0x474E4B35  # plan header word 0 ("GNK5")
 
 
-def _hdr(M=10, K=10, groups=4, ipc=16, nslots=0, nslabs=0):
-    h = (ctypes.c_int32 * 16)(MAGIC, M, K, groups, ipc, groups * ipc, 0, 0, nslots, 0, 0, nslabs, 0, 0, 0, 0)
+def _hdr(M=10, K=10, groups=1, ipc=32, nslots=0, nslabs=0):
+    # magic M K groups ipc nunits nhunits(slots) nheavy ntile nred nslabs ntblk has_diag nnz 0 0
+    h = (ctypes.c_int32 * 16)(MAGIC, M, K, groups, ipc, 0, nslots, 0, 0, 0, nslabs, 0, 0, 0, 0, 0)
     return ctypes.cast(h, ctypes.c_void_p), h
 
 
@@ -66,7 +67,7 @@ def test_argument_validation_without_gpu():
     rc = lib.gcnk_spmm_csr_f32(ctypes.c_void_p(16), ctypes.cast(bad, ctypes.c_void_p), ctypes.c_void_p(16), 8, 8,
                                ctypes.c_void_p(16), 8, None, 0, None, 0, 1.0, 1.0, 0, 0, None, 0, 0, None)
     assert rc == _lib.EARG and b"not a gcnk plan" in lib.gcnk_last_error()
-    # plan/groups mismatch is refused before any launch (F=200 uses 4 groups)
+    # plan/groups mismatch is refused before any launch (F=200 uses 4 lane groups per wave)
     h, _keep = _hdr(groups=7)
     rc = lib.gcnk_spmm_csr_f32(ctypes.c_void_p(16), h, ctypes.c_void_p(16), 200, 200,
                                ctypes.c_void_p(16), 200, None, 0, None, 0, 1.0, 1.0, 0, 0, None, 0, 0, None)
@@ -86,8 +87,9 @@ def test_argument_validation_without_gpu():
 
 def test_plan_and_workspace_sizes():
     lib = _lib.load()
+    # lane groups per wavefront = 64 / lanes per row group
     assert lib.gcnk_spmm_groups(200, 0) == 4 and lib.gcnk_spmm_groups(8, 0) == 32
-    assert lib.gcnk_spmm_groups(7, 0) == 32 and lib.gcnk_spmm_groups(200, 16) == 16
+    assert lib.gcnk_spmm_groups(7, 0) == 8 and lib.gcnk_spmm_groups(200, 64) == 1
     h, _keep = _hdr(nslots=10, nslabs=3)
     assert lib.gcnk_spmm_workspace_bytes(h, 198) == 8192 + 3 * 64 * 208 * 4
     assert lib.gcnk_gemm_workspace_bytes(200, 8, 7724, 4) == 4 * 200 * 8 * 4

@@ -68,7 +68,7 @@ def test_spmm_r8_adjacency(r8, F):
     got_t = spmm(a, B.to(DEV), dense=0.05)
     _close(got_t, ref)
     hdr = [p for k, p in a._plans.items() if k[2] == 0.05][0].header
-    assert hdr[9] > 0 and hdr[13] == 1, "R8 document rows: MFMA tiles over the topic columns + diagonal"
+    assert hdr[8] > 0 and hdr[12] == 1, "R8 document rows: MFMA tiles over the topic columns + diagonal"
 
 
 @pytest.mark.parametrize("F", [1, 3, 7, 8, 16, 64, 100, 200, 256, 257, 1000, 4096])
@@ -85,8 +85,9 @@ def test_spmm_widths_with_heavy_and_empty_rows(F):
 @pytest.mark.parametrize("ipc", [4, 8, 12, 16, 32, 64])
 @pytest.mark.parametrize("lanes", [0, 16, 32])
 def test_spmm_schedule_variants(ipc, lanes):
-    """Every chunk size / lane layout computes the same product (the
-    merge-path cut points, snapping and split-row fix-up are exercised)."""
+    """Every light-row limit / lane layout computes the same product (light
+    units, single- and multi-segment heavy rows and the last-arriver combine
+    are exercised)."""
     rng = np.random.default_rng(ipc * 100 + lanes)
     M, K, F = 1500, 900, 200
     rp, ci, v = _random_csr(M, K, 9000, rng, heavy_rows=(0, 749, 1499), heavy_deg=700, empty_frac=0.1)
@@ -134,9 +135,9 @@ def test_spmm_hybrid_dense_blocks(F):
     acc = csr_ref.spmm_csr(rp, ci, v, B)
     _close(got, csr_ref.spmm_epilogue(acc, bias, relu=True, mask=mask, scale=1.5), atol=2e-5 * np.sqrt(K))
     hdr = list(a._plans.values())[0].header
-    assert hdr[9] > 0 and hdr[10] > 0, "dense blocks (single and multi-chunk) expected on the tile path"
-    assert hdr[13] == 1, "diagonal entries of tile rows are extracted"
-    # tile path disabled: the path kernel alone gives the same product
+    assert hdr[8] > 0 and hdr[9] > 0, "dense blocks (single and multi-chunk) expected on the tile path"
+    assert hdr[12] == 1, "diagonal entries of tile rows are extracted"
+    # tile path disabled: the row kernel alone gives the same product
     got2 = spmm(a, torch.from_numpy(B).to(DEV), dense=2.0)
     _close(got2, acc, atol=2e-5 * np.sqrt(K))
 
@@ -146,7 +147,7 @@ def test_spmm_r8_features_use_tile_path(r8):
     W = torch.randn(r8["nfeat"], 200, generator=torch.Generator().manual_seed(4))
     got = spmm(x, W.to(DEV))
     hdr = list(x._plans.values())[0].header
-    assert hdr[9] > 0 and hdr[6] == 0, "R8 X: document and topic rows all run on the MFMA tile path"
+    assert hdr[8] > 0 and hdr[5] == 0, "R8 X: document and topic rows all run on the MFMA tile path"
     rp, ci, v = (t.cpu().numpy() for t in (x.rowptr, x.colind, x.val))
     _close(got, csr_ref.spmm_csr(rp, ci, v, W.numpy()), atol=1e-4)
 

@@ -1,6 +1,7 @@
-"""CPU check of the path-format SpMM control logic (window packing, per-group
-walk, in-window combine, cross-window fix-up) through its Python model
-tests/path_model.py, which mirrors graph-convolutional-networks-for-text-classification_amd/csrc/spmm.hip."""
+"""CPU check of the row-unit SpMM control logic (light units, heavy segments
+with interleaved lane groups, partial slots, last-arriver combine) through its
+Python model tests/path_model.py, which mirrors
+graph-convolutional-networks-for-text-classification_amd/csrc/spmm.hip."""
 import os
 import sys
 
@@ -12,24 +13,35 @@ import path_model  # noqa: E402
 from oracle import csr_ref  # noqa: E402
 
 
-@pytest.mark.parametrize("G,ipc", [(4, 16), (32, 8), (4, 4), (16, 4), (2, 3), (1, 1), (8, 5)])
-def test_model_on_r8(r8, G, ipc):
+@pytest.mark.parametrize("groups,ipc", [(1, 32), (32, 8), (1, 4), (4, 16), (8, 3), (1, 1), (64, 8)])
+def test_model_on_r8(r8, groups, ipc):
     rp, ci, v = csr_ref.coo_to_csr(r8["adj"]._indices()[0].numpy(), r8["adj"]._indices()[1].numpy(),
                                    r8["adj"]._values().numpy(), (r8["nodes"], r8["nodes"]))
-    B = np.random.default_rng(G * 10 + ipc).standard_normal((r8["nodes"], 3))
-    C = path_model.spmm(rp, ci, v, B, G, ipc)
+    B = np.random.default_rng(groups * 10 + ipc).standard_normal((r8["nodes"], 3))
+    C = path_model.spmm(rp, ci, v, B, ipc, groups)
     np.testing.assert_allclose(C, csr_ref.spmm_csr(rp, ci, v, B), atol=1e-12)
+
+
+def test_r8_plan_shape():
+    """R8-shaped degrees: document rows (5 nonzeros) are light units, the 50
+    topic rows (hundreds to ~1.8k) split into <= 64 segments each."""
+    deg = np.concatenate([np.full(7674, 5), np.linspace(200, 1807, 50).astype(int)])
+    rp = np.concatenate([[0], np.cumsum(deg)])
+    units, heavy, nh = path_model.host_plan(rp, 32, 1)
+    assert len(units) - nh == 7674 and len(heavy) == 50
+    assert all(1 < h[2] <= path_model.K_MAX_SEG for h in heavy)
+    assert all(units[u][3] >= 0 for u in range(nh))
 
 
 @pytest.mark.parametrize("seed", range(6))
 def test_model_on_skewed_random(seed):
     rng = np.random.default_rng(seed)
     M, K = int(rng.integers(1, 300)), int(rng.integers(1, 200))
-    deg = rng.choice([0, 1, 2, 5, 40, 300], size=M, p=[0.2, 0.2, 0.2, 0.25, 0.1, 0.05])
+    deg = rng.choice([0, 1, 2, 5, 40, 300, 5000], size=M, p=[0.2, 0.2, 0.2, 0.25, 0.1, 0.04, 0.01])
     rows = np.repeat(np.arange(M), deg)
     cols = rng.integers(0, K, rows.size)
     rp, ci, v = csr_ref.coo_to_csr(rows, cols, rng.standard_normal(rows.size), (M, K))
     B = rng.standard_normal((K, 2))
-    for G, ipc in [(4, 4), (8, 8), (2, 16), (3, 7)]:
-        C = path_model.spmm(rp, ci, v, B, G, ipc)
-        np.testing.assert_allclose(C, csr_ref.spmm_csr(rp, ci, v, B), atol=1e-12)
+    for groups, ipc in [(1, 4), (1, 32), (32, 8), (4, 3)]:
+        C = path_model.spmm(rp, ci, v, B, ipc, groups)
+        np.testing.assert_allclose(C, csr_ref.spmm_csr(rp, ci, v, B), atol=1e-10)

@@ -16,10 +16,13 @@ aggregations of layer.py:106) × steps × ranks / max-over-ranks time;
 ms_per_step = GCN-forward ms.  N > 1: the R8 graph does not shard (SURVEY
 §8(e)): N independent replicas, "scaling": "weak".
 
-roofline: the dominant kernel of the forward (by measured duration) with its
-algorithmic bytes (CSR SpMM: 4(M+1) + 8 nnz + 4 K F + 4 M F) over its
-average launch duration, timed with HIP events on the launch stream around a
-hipGraph of back-to-back launches of that kernel alone.
+roofline: the north-star kernel (BASELINE.json: the R8 doc-topic SpMM Â·S1 at
+hidden 200, with gc1's bias + ReLU fused) with its algorithmic bytes (CSR
+SpMM: 4(M+1) + 8 nnz + 4 K F + 4 M F) over its average launch duration,
+timed with HIP events on the launch stream around a hipGraph of back-to-back
+launches of that op alone; "roofline_dominant" gives the same for the
+slowest op of the forward.  "traffic" (PMC FETCH_SIZE + WRITE_SIZE per
+launch) comes from the separate rocprofv3 --pmc passes in profiles/.
 
 cpu_baseline: the oracle (torch-CPU restatement issuing the reference's
 th.spmm calls on the same COO tensors) on this host's cores, bounded sample.
@@ -117,19 +120,24 @@ def main():
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         elapsed = float(t)
 
-    # ---- per-kernel durations: hipGraph of back-to-back launches of one op,
-    #      HIP events on the launch stream (torch's current stream).
+    # ---- per-op durations: hipGraph of back-to-back launches of one op of the
+    #      forward, HIP events on the launch stream (torch's current stream, the
+    #      stream every op is enqueued on).  Each duration includes the
+    #      dispatch gap between consecutive launches (~1.5 us on MI355X), so it
+    #      is an upper bound of the rocprofv3 kernel duration.
     W1, b1 = model.gc1.weight.detach(), model.gc1.bias.detach()
     W2, b2 = model.gc2.weight.detach(), model.gc2.bias.detach()
     with torch.no_grad():
         S1 = ops.spmm(x_csr, W1)
-        _, S2 = ops.spmm_proj(a_csr, S1, W2, bias=b1, epilogue=2, store_main=False)
-    # the forward's three ops (each = its main kernel + split-row fix-up/reduce)
+        H1 = ops.spmm(a_csr, S1, bias=b1, epilogue=2)
+        S2 = ops.gemm(H1, W2)
+        Z = ops.spmm(a_csr, S2, bias=b2, epilogue=1)
+    # the forward's ops, in order (layer.py:102, :106+110+182, gc2 :102, gc2 :106+110)
     kernels = {
         "spmm_XW1": (lambda: ops.spmm(x_csr, W1, out=S1), spmm_bytes(N, nfeat, nnz_x, nhid)),
-        "spmm_AS1_F200_proj": (lambda: ops.spmm_proj(a_csr, S1, W2, bias=b1, epilogue=2, store_main=False),
-                               spmm_bytes(N, N, nnz_a, nhid) - 4 * N * nhid + 4 * (nhid * nclass + N * nclass)),
-        "spmm_AS2_F8": (lambda: ops.spmm(a_csr, S2, bias=b2, epilogue=1), spmm_bytes(N, N, nnz_a, nclass)),
+        "spmm_AS1_F200": (lambda: ops.spmm(a_csr, S1, bias=b1, epilogue=2, out=H1), spmm_bytes(N, N, nnz_a, nhid)),
+        "gemm_H1W2": (lambda: ops.gemm(H1, W2, out=S2), 4 * (N * nhid + nhid * nclass + N * nclass)),
+        "spmm_AS2_F8": (lambda: ops.spmm(a_csr, S2, bias=b2, epilogue=1, out=Z), spmm_bytes(N, N, nnz_a, nclass)),
     }
     ktimes = {}
     for name, (fn, nbytes) in kernels.items():
@@ -154,6 +162,7 @@ def main():
         ktimes[name] = {"us": best, "bytes": nbytes, "gbs": nbytes / (best * 1e-6) / 1e9}
         del kg
     dom = max(ktimes, key=lambda k: ktimes[k]["us"])
+    north = "spmm_AS1_F200"   # BASELINE.json north_star: the R8 doc-topic SpMM at hidden 200
 
     # ---- CPU baseline: oracle (reference th.spmm calls) on this host, rank 0, N=1
     cpu = None
@@ -177,7 +186,7 @@ def main():
 
     ms = elapsed / args.steps * 1e3
     value = 2 * nnz_a * args.steps * world / elapsed
-    kd = ktimes[dom]
+    kn, kd = ktimes[north], ktimes[dom]
     line = {
         "metric": "SpMM edges/s and GCN-forward ms on R8 doc-topic graph, 1×MI355X",
         "value": value,
@@ -194,9 +203,11 @@ def main():
         "config": {"workload": "R8 GCN forward (eval), hidden 200, 8 classes, nfeat 7463",
                    "nodes": N, "adj_nnz": nnz_a, "x_nnz": nnz_x, "graph": not args.no_graph,
                    "parallelism": f"replicas{world}" if world > 1 else "single"},
-        "roofline": {"bound": "hbm", "kernel": dom, "achieved": kd["gbs"], "peak": HBM_PEAK_GBS,
-                     "unit": "GB/s", "frac": kd["gbs"] / HBM_PEAK_GBS, "traffic": None,
-                     "avg_launch_us": kd["us"], "algorithmic_bytes": kd["bytes"]},
+        "roofline": {"bound": "hbm", "kernel": north, "achieved": kn["gbs"], "peak": HBM_PEAK_GBS,
+                     "unit": "GB/s", "frac": kn["gbs"] / HBM_PEAK_GBS, "traffic": None,
+                     "avg_launch_us": kn["us"], "algorithmic_bytes": kn["bytes"]},
+        "roofline_dominant": {"kernel": dom, "achieved": kd["gbs"], "frac": kd["gbs"] / HBM_PEAK_GBS,
+                              "avg_launch_us": kd["us"], "algorithmic_bytes": kd["bytes"]},
         "kernels_us": {k: round(v["us"], 3) for k, v in ktimes.items()},
         "cpu_baseline": cpu,
     }

@@ -128,19 +128,23 @@ gemm_f32_mfma_kernel(int32_t M, int32_t N, int32_t K, int32_t kchunk, const floa
 
 // Skinny-N GEMM (N <= 16, A row-major with 16-B aligned rows, B row-major):
 // C = epi(A B), the gc2 support H1 W2 ([nodes x 200] x [200 x classes]).
-// One wave per 16 rows, all of K in registers: each lane reads one 16-B slice
-// of its row per 16-deep k block (row r = lane&15, slice q = lane>>4), every
-// A load of the wave is issued before the first MFMA.  The k order inside a
-// 16-block is permuted consistently for A and B (k-slot q of step j is
-// k = 16c + 4q + j), which the fp32 sum does not care about beyond rounding.
-template <int KB>  // number of 16-deep k blocks held in registers
+// K is split over the 4 waves of a workgroup: the workgroup
+// owns 16 rows, wave w the 16-deep k blocks [w*KB, (w+1)*KB) (lane l: row
+// l&15, 16-B k slice l>>4 of each block; the k order inside a block is
+// permuted consistently for A and B, k = 16c + 4(l>>4) + j at MFMA step j), so a wave holds KB float4 of A and runs
+// a 4*KB-deep MFMA chain instead of the whole of K; the four 16x16
+// accumulators meet in LDS and wave 0 adds them in wave order (fixed order:
+// bitwise reproducible).  Four times the waves of the one-wave form, a quarter
+// of the serial chain: H1 W2 at R8 is 1,931 waves of 4 k blocks.
+template <int KB>
 __global__ void __launch_bounds__(256)
-gemm_skinny_n16_kernel(int32_t M, int32_t N, int32_t K, const float* __restrict__ A, int64_t lda,
-                       const float* __restrict__ B, int64_t ldb, float* __restrict__ C, int64_t ldc, GemmEpi epi) {
+gemm_skinny_ksplit_kernel(int32_t M, int32_t N, int32_t K, const float* __restrict__ A, int64_t lda,
+                          const float* __restrict__ B, int64_t ldb, float* __restrict__ C, int64_t ldc,
+                          GemmEpi epi) {
+  __shared__ f32x4 s_acc[3][64];
   const int lane = threadIdx.x & 63;
-  const int64_t wave = ((int64_t)blockIdx.x * blockDim.x + threadIdx.x) >> 6;
-  const int64_t m0 = wave * 16;
-  if (m0 >= M) return;
+  const int w = threadIdx.x >> 6;
+  const int64_t m0 = (int64_t)blockIdx.x * 16;
   const int r = lane & 15, q = lane >> 4;
   const int64_t row = m0 + r;
   const bool rok = row < M;
@@ -149,7 +153,7 @@ gemm_skinny_n16_kernel(int32_t M, int32_t N, int32_t K, const float* __restrict_
   float4 a[KB];
 #pragma unroll
   for (int c = 0; c < KB; ++c) {
-    const int k = 16 * c + 4 * q;
+    const int k = 16 * (w * KB + c) + 4 * q;
     if (rok && k + 3 < K) {
       a[c] = *reinterpret_cast<const float4*>(A + row * lda + k);
     } else {
@@ -164,7 +168,7 @@ gemm_skinny_n16_kernel(int32_t M, int32_t N, int32_t K, const float* __restrict_
   f32x4 acc = {0.f, 0.f, 0.f, 0.f};
 #pragma unroll
   for (int c = 0; c < KB; ++c) {
-    const int k = 16 * c + 4 * q;
+    const int k = 16 * (w * KB + c) + 4 * q;
     const float b0 = (nok && k + 0 < K) ? B[(int64_t)(k + 0) * ldb + n] : 0.f;
     const float b1 = (nok && k + 1 < K) ? B[(int64_t)(k + 1) * ldb + n] : 0.f;
     const float b2 = (nok && k + 2 < K) ? B[(int64_t)(k + 2) * ldb + n] : 0.f;
@@ -173,6 +177,14 @@ gemm_skinny_n16_kernel(int32_t M, int32_t N, int32_t K, const float* __restrict_
     acc = __builtin_amdgcn_mfma_f32_16x16x4f32(a[c].y, b1, acc, 0, 0, 0);
     acc = __builtin_amdgcn_mfma_f32_16x16x4f32(a[c].z, b2, acc, 0, 0, 0);
     acc = __builtin_amdgcn_mfma_f32_16x16x4f32(a[c].w, b3, acc, 0, 0, 0);
+  }
+  if (w > 0) s_acc[w - 1][lane] = acc;
+  __syncthreads();
+  if (w != 0) return;
+#pragma unroll
+  for (int v = 0; v < 3; ++v) {
+    const f32x4 o = s_acc[v][lane];
+    acc[0] += o[0]; acc[1] += o[1]; acc[2] += o[2]; acc[3] += o[3];
   }
 #pragma unroll
   for (int j = 0; j < 4; ++j) {
@@ -291,18 +303,20 @@ extern "C" int gcnk_gemm_f32(int32_t transA, int32_t transB, int32_t M, int32_t 
   GemmEpi e{bias, R, ldr, scale, epilogue};
   hipStream_t s = (hipStream_t)stream;
   const bool ta = transA != 0, tb = transB != 0;
-  if (!ta && !tb && N <= 16 && K <= 256 && lda % 4 == 0 && aligned16(A) && split_k == 1) {
-    const int64_t waves = ((int64_t)M + 15) / 16;
-    const unsigned blocks = (unsigned)((waves + 3) / 4);
-    const int kb = (K + 15) / 16;
-#define GCNK_SKINNY(KB_)                                                                                  \
-  hipLaunchKernelGGL(gemm_skinny_n16_kernel<KB_>, dim3(blocks), dim3(256), 0, s, M, N, K, A, lda, B, ldb, C, \
+  if (!ta && !tb && N <= 16 && K <= 1024 && lda % 4 == 0 && aligned16(A) && split_k == 1) {
+    // 16 rows per workgroup, K split over its 4 waves (k blocks of 16 per wave)
+    const int kbw = ((K + 15) / 16 + 3) / 4;
+    const unsigned blocks = (unsigned)(((int64_t)M + 15) / 16);
+#define GCNK_SKINNY_KS(KB_)                                                                                     \
+  hipLaunchKernelGGL(gemm_skinny_ksplit_kernel<KB_>, dim3(blocks), dim3(256), 0, s, M, N, K, A, lda, B, ldb, C, \
                      ldc, e)
-    if (kb <= 4) GCNK_SKINNY(4);
-    else if (kb <= 8) GCNK_SKINNY(8);
-    else GCNK_SKINNY(16);
-#undef GCNK_SKINNY
-    return launch_check("gemm_skinny_n16_kernel");
+    if (kbw <= 1) GCNK_SKINNY_KS(1);
+    else if (kbw <= 2) GCNK_SKINNY_KS(2);
+    else if (kbw <= 4) GCNK_SKINNY_KS(4);
+    else if (kbw <= 8) GCNK_SKINNY_KS(8);
+    else GCNK_SKINNY_KS(16);
+#undef GCNK_SKINNY_KS
+    return launch_check("gemm_skinny_ksplit_kernel");
   }
   if (N <= 16) return launch_gemm<4, 1, 2, 1>(ta, tb, M, N, K, A, lda, B, ldb, C, ldc, e, split_k, workspace, s);
   return launch_gemm<2, 2, 2, 2>(ta, tb, M, N, K, A, lda, B, ldb, C, ldc, e, split_k, workspace, s);

@@ -478,33 +478,50 @@ spmm_tile_kernel(const int4* __restrict__ tdesc, const int32_t* __restrict__ tco
   }
 
   stamp(epi, 2);
-  // ---- output: block rows 16*wave + 4*(lane>>4) + j, cols col0 + 16*nt + (lane&15);
-  //      single-chunk blocks finish here (+ extracted diagonal, epilogue), others
-  //      leave a slab for spmm_tile_reduce_kernel
-  int32_t orow[4];
-  float dv[4];
+  // ---- output through LDS: the accumulators (C/D layout: block row 16*wave +
+  //      4*(lane>>4) + j, column 16*nt + (lane&15)) are parked row-major in the
+  //      (no longer needed) B tile, then every thread writes whole 16-B pieces
+  //      of rows: single-chunk blocks finish here (+ extracted diagonal,
+  //      epilogue), others leave the block's real rows as a slab for
+  //      spmm_tile_reduce_kernel.
+  constexpr int CW = NT * 16;                                   // staged columns
+  constexpr int CS = (kKC * stride >= kRB * (CW + 4)) ? CW + 4 : CW;  // row stride (floats)
+  static_assert(kKC * stride >= kRB * CS, "output tile must fit the B tile");
+  __syncthreads();  // all waves are done reading s_B
+  float* s_C = s_B;
 #pragma unroll
-  for (int j = 0; j < 4; ++j) {
-    const int32_t rl = 16 * wave + 4 * (lane >> 4) + j;
-    orow[j] = rl < d.y ? trows[(int64_t)d.x * kRB + rl] : -1;
-    dv[j] = (d.z < 0 && dval && orow[j] >= 0) ? dval[orow[j]] : 0.f;
-  }
+  for (int nt = 0; nt < NT; ++nt)
 #pragma unroll
-  for (int nt = 0; nt < NT; ++nt) {
-    const int64_t col = col0 + nt * 16 + nc;
-    if (col >= F) continue;
-    const float bcol = (d.z < 0 && epi.bias) ? epi.bias[col] : 0.f;
+    for (int j = 0; j < 4; ++j) s_C[(16 * wave + 4 * (lane >> 4) + j) * CS + nt * 16 + nc] = acc[nt][j];
+  if (tid < kRB) s_cols[tid] = tid < d.y ? trows[(int64_t)d.x * kRB + tid] : -1;  // s_cols reused: output rows
+  __syncthreads();
+  constexpr int nq4 = CW / 4;  // 16-B pieces per staged row
+  const bool single = d.z < 0;
+  for (int e = tid; e < kRB * nq4; e += 256) {
+    const int rl = e / nq4;
+    const int64_t col = col0 + (int64_t)(e % nq4) * 4;
+    if (rl >= d.y || col >= F) continue;
+    float4 v = *reinterpret_cast<const float4*>(s_C + rl * CS + (col - col0));
+    if (!single) {  // slab rows are padded to 16 floats: whole pieces stay inside the row
+      *reinterpret_cast<float4*>(slabs + ((int64_t)d.z * kRB + rl) * slab_ld + col) = v;
+      continue;
+    }
+    const int64_t row = s_cols[rl];
+    float o[4] = {v.x, v.y, v.z, v.w};
+    const float dv = dval ? dval[row] : 0.f;
 #pragma unroll
-    for (int j = 0; j < 4; ++j) {
-      if (orow[j] < 0) continue;
-      if (d.z < 0) {
-        float v = acc[nt][j];
-        if (dv[j] != 0.f) v = fmaf(dv[j], B[(int64_t)orow[j] * ldb + col], v);
-        C[(int64_t)orow[j] * ldc + col] = apply_epi(epi, v, bcol, orow[j], col);
-      } else {
-        const int32_t rl = 16 * wave + 4 * (lane >> 4) + j;
-        slabs[((int64_t)d.z * kRB + rl) * slab_ld + col] = acc[nt][j];
-      }
+    for (int i = 0; i < 4; ++i) {
+      if (col + i >= F) break;
+      if (dv != 0.f) o[i] = fmaf(dv, B[row * ldb + col + i], o[i]);
+      o[i] = apply_epi(epi, o[i], epi.bias ? epi.bias[col + i] : 0.f, row, col + i);
+    }
+    float* dst = C + row * ldc + col;
+    if (VEC4) {
+      *reinterpret_cast<float4*>(dst) = make_float4(o[0], o[1], o[2], o[3]);
+    } else {
+#pragma unroll
+      for (int i = 0; i < 4; ++i)
+        if (col + i < F) dst[i] = o[i];
     }
   }
   stamp(epi, 3);

@@ -46,7 +46,7 @@ namespace {
 constexpr int32_t kMagic = 0x474e4b35;  // "GNK5"
 constexpr int kRB = 64;                 // tile rows per dense block (4 waves x 16)
 constexpr int kKC = 64;                 // condensed columns per tile chunk (16 MFMA k-steps)
-constexpr int kMaxNT = 14;              // 16-column MFMA n-tiles per tile workgroup (B tile <= 57 KB LDS)
+constexpr int kMaxNT = 8;               // 16-column MFMA n-tiles per tile workgroup (B tile 48 KB LDS: 2+ per CU)
 constexpr int kMaxColTiles = 64;        // row-kernel column tiles per launch (arrival counters per heavy row)
 constexpr int kMaxSeg = 64;             // segments per heavy row (bounds the last arriver's combine)
 
@@ -93,7 +93,7 @@ struct Vec<1> {
 
 // ---------------------------------------------------------------------------
 // Plan layout (int32 words).  Header (16 words, see gcnk.h):
-//   0 magic  1 M  2 K  3 lane groups per wave  4 ipc (light-row limit)  5 nunits
+//   0 magic  1 M  2 K  3 lane groups per heavy segment  4 ipc (light-row limit)  5 nunits
 //   6 nhunits (heavy segments = partial slots)  7 nheavy (rows of > 1 segment)
 //   8 ntile (chunks)  9 nred  10 nslabs  11 ntblk (tile blocks)  12 has_diag  13 nnz  14 0  15 0
 // Body: items int2[nnz] {col, value bits} in CSR order | units int4[nunits]
@@ -294,8 +294,9 @@ __device__ __forceinline__ void finish_row(const typename Vec<VEC>::T& acc, int3
   proj.apply(pa, &h, r, lg);
 }
 
-// grid.x: [0, nhb) heavy blocks, one heavy segment per wavefront; then light
-// blocks, one light row per lane group.  grid.y: column tiles of LPR*VEC.
+// grid.x: [0, nhb) heavy blocks, one heavy segment per wavefront (per
+// workgroup for 64-lane groups); then light blocks, one light row per lane
+// group.  grid.y: column tiles of LPR*VEC.
 template <int BLOCK, int LPR, int VEC, int U, int NP>
 __global__ void __launch_bounds__(BLOCK)
 spmm_row_kernel(RowPlan rp, int32_t nhb, const float* __restrict__ B, int64_t ldb, int32_t F,
@@ -331,15 +332,31 @@ spmm_row_kernel(RowPlan rp, int32_t nhb, const float* __restrict__ B, int64_t ld
     return;
   }
 
-  // ---- heavy segment: one unit per wavefront, lane group q takes nonzeros q, q + SW, ...
+  // ---- heavy segment.  One unit per wavefront whose SW lane groups take nonzeros
+  //      q, q + SW, ... (LPR < 64); with whole-wavefront groups (LPR == 64) one
+  //      unit per workgroup, its WPB wavefronts interleaving the nonzeros and
+  //      meeting in LDS.  Either way GS = SW * (LPR == 64 ? WPB : 1) groups
+  //      share the segment and every sum has a fixed order.
+  constexpr bool WG = LPR == 64 && WPB > 1;
+  constexpr int GS = WG ? WPB : SW;
+  __shared__ T s_red[WG ? WPB : 1][64];
+  __shared__ int32_t s_last;
   const int lane = tid & 63;
-  const int q = lane / LPR;
-  const int32_t u = __builtin_amdgcn_readfirstlane((int32_t)blockIdx.x * WPB + tid / 64);
-  if (u >= rp.nhunits) return;
+  const int w = tid / 64;
+  const int q = WG ? w : lane / LPR;
+  const int32_t u = WG ? (int32_t)blockIdx.x : __builtin_amdgcn_readfirstlane((int32_t)blockIdx.x * WPB + w);
+  if (u >= rp.nhunits) return;  // WG: uniform over the workgroup
   const int4 un = rp.units[u];
   stamp(epi, 1);
-  gather_rows<VEC, U, SW>(rp.items, un.y, un.z, q, B, ldb, colv, colok, acc);
-  wave_group_sum<LPR>(acc);
+  gather_rows<VEC, U, GS>(rp.items, un.y, un.z, q, B, ldb, colv, colok, acc);
+  if constexpr (WG) {
+    if (w > 0) s_red[w][lane] = acc;
+    __syncthreads();
+#pragma unroll
+    for (int v = 1; v < WPB; ++v) V::add(acc, s_red[v][lane]);  // every wave: same order, same bits
+  } else {
+    wave_group_sum<LPR>(acc);
+  }
   stamp(epi, 2);
   if (un.w < 0) {  // the row's only segment
     if (q == 0) finish_row<LPR, VEC, NP>(acc, un.x, colv, colok, bv, lg, C, ldc, epi, store_main, proj, pa);
@@ -348,34 +365,52 @@ spmm_row_kernel(RowPlan rp, int32_t nhb, const float* __restrict__ B, int64_t ld
   }
   // publish this segment's partial, then count in; the last arriver sums all of
   // the row's partials in segment order
-  if (q == 0 && colok) store_coherent(part + (int64_t)u * part_ld + colv, acc);
-  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   const int4 hv = rp.heavy[un.w];
   int32_t* ctr = rp.cnt + (int64_t)un.w * kMaxColTiles + blockIdx.y;
-  int32_t arrived = 0;
-  if (lane == 0) arrived = __hip_atomic_fetch_add(ctr, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-  arrived = __builtin_amdgcn_readfirstlane(arrived);
+  int32_t last = 0;
+  if (q == 0 && colok) store_coherent(part + (int64_t)u * part_ld + colv, acc);
+  if (!WG || w == 0) {  // the wavefront that stored counts in, after its stores completed
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    int32_t arrived = 0;
+    if (lane == 0) arrived = __hip_atomic_fetch_add(ctr, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    last = __builtin_amdgcn_readfirstlane(arrived) == hv.z - 1;
+  }
+  if constexpr (WG) {
+    if (tid == 0) s_last = last;
+    __syncthreads();
+    last = s_last;
+  }
   stamp(epi, 3);
-  if (arrived != hv.z - 1) return;
+  if (!last) return;
+  // group q sums slots q, q + GS, ... (U loads in flight), then the groups meet
   T sum = V::zero();
   if (colok) {
-    // lane group q sums slots q, q + SW, ... (U loads in flight), then the butterfly
     const float* p0 = part + (int64_t)hv.y * part_ld + colv;
-    for (int32_t s0 = q; s0 < hv.z; s0 += SW * U) {
+    for (int32_t s0 = q; s0 < hv.z; s0 += GS * U) {
       T pv[U];
 #pragma unroll
       for (int j = 0; j < U; ++j) {
-        const int32_t s = s0 + SW * j;
-        pv[j] = s < hv.z ? load_coherent<T>(p0 + (int64_t)s * part_ld) : V::zero();
+        const int32_t sl = s0 + GS * j;
+        pv[j] = sl < hv.z ? load_coherent<T>(p0 + (int64_t)sl * part_ld) : V::zero();
       }
 #pragma unroll
       for (int j = 0; j < U; ++j)
-        if (s0 + SW * j < hv.z) V::add(sum, pv[j]);
+        if (s0 + GS * j < hv.z) V::add(sum, pv[j]);
     }
   }
-  wave_group_sum<LPR>(sum);
-  if (q == 0) finish_row<LPR, VEC, NP>(sum, hv.x, colv, colok, bv, lg, C, ldc, epi, store_main, proj, pa);
-  if (lane == 0) __hip_atomic_store(ctr, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  if constexpr (WG) {
+    __syncthreads();  // s_red reuse
+    if (w > 0) s_red[w][lane] = sum;
+    __syncthreads();
+#pragma unroll
+    for (int v = 1; v < WPB; ++v) V::add(sum, s_red[v][lane]);
+  } else {
+    wave_group_sum<LPR>(sum);
+  }
+  if (q == 0) {
+    finish_row<LPR, VEC, NP>(sum, hv.x, colv, colok, bv, lg, C, ldc, epi, store_main, proj, pa);
+    if (lane == 0) __hip_atomic_store(ctr, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  }
   stamp(epi, 3);
 }
 
@@ -411,7 +446,7 @@ spmm_tile_kernel(const int4* __restrict__ tdesc, const int32_t* __restrict__ tco
   const int64_t item = blockIdx.x;
   stamp(epi, 0);
   const int4 d = tdesc[item];  // block, nrows, slab (-1: single chunk), 0
-  constexpr int32_t col0 = 0;  // column slices are folded into the B/C pointers by the host
+  const int64_t col0 = (int64_t)blockIdx.y * (NT * 16);  // this workgroup's column slice
 
   if (tid < kKC) s_cols[tid] = tcols[item * kKC + tid];
   // A fragments of this wave: 16 consecutive floats per lane
@@ -493,10 +528,20 @@ spmm_tile_kernel(const int4* __restrict__ tdesc, const int32_t* __restrict__ tco
   for (int nt = 0; nt < NT; ++nt)
 #pragma unroll
     for (int j = 0; j < 4; ++j) s_C[(16 * wave + 4 * (lane >> 4) + j) * CS + nt * 16 + nc] = acc[nt][j];
-  if (tid < kRB) s_cols[tid] = tid < d.y ? trows[(int64_t)d.x * kRB + tid] : -1;  // s_cols reused: output rows
+  // output rows, their extracted diagonal and the bias go to LDS first (no
+  // global load inside the write-out loop: each would serialise a latency)
+  __shared__ float s_dv[kRB];
+  __shared__ float s_bias[CW];
+  const bool single = d.z < 0;
+  if (tid < kRB) {
+    const int32_t r = tid < d.y ? trows[(int64_t)d.x * kRB + tid] : -1;
+    s_cols[tid] = r;  // s_cols reused: output rows
+    s_dv[tid] = (single && dval && r >= 0) ? dval[r] : 0.f;
+  }
+  for (int c = tid; c < CW; c += 256)
+    s_bias[c] = (single && epi.bias && col0 + c < F) ? epi.bias[col0 + c] : 0.f;
   __syncthreads();
   constexpr int nq4 = CW / 4;  // 16-B pieces per staged row
-  const bool single = d.z < 0;
   for (int e = tid; e < kRB * nq4; e += 256) {
     const int rl = e / nq4;
     const int64_t col = col0 + (int64_t)(e % nq4) * 4;
@@ -508,12 +553,12 @@ spmm_tile_kernel(const int4* __restrict__ tdesc, const int32_t* __restrict__ tco
     }
     const int64_t row = s_cols[rl];
     float o[4] = {v.x, v.y, v.z, v.w};
-    const float dv = dval ? dval[row] : 0.f;
+    const float dv = s_dv[rl];
 #pragma unroll
     for (int i = 0; i < 4; ++i) {
       if (col + i >= F) break;
       if (dv != 0.f) o[i] = fmaf(dv, B[row * ldb + col + i], o[i]);
-      o[i] = apply_epi(epi, o[i], epi.bias ? epi.bias[col + i] : 0.f, row, col + i);
+      o[i] = apply_epi(epi, o[i], s_bias[col - col0 + i], row, col + i);
     }
     float* dst = C + row * ldc + col;
     if (VEC4) {
@@ -543,24 +588,22 @@ spmm_tile_reduce_kernel(const int4* __restrict__ red, const int32_t* __restrict_
   const int64_t col = (int64_t)blockIdx.z * 64 + c4 * 4;
   float4 acc = make_float4(0.f, 0.f, 0.f, 0.f);
   // slab rows are padded to 16 floats (slab_ld % 16 == 0): whole float4 reads stay
-  // inside the row; lanes past F are never stored.  Four slabs in flight per lane.
+  // inside the row; lanes past F are never stored.
   if (col < F) {
+    // slab lane sl sums slabs sl, sl + 16, ... in order, 8 loads in flight (one
+    // round for up to 128 slabs)
     const int64_t step = (int64_t)16 * kRB * slab_ld;
     const float* p = slabs + ((int64_t)(rb.z + sl) * kRB + rl) * slab_ld + col;
-    int s = sl;
-    for (; s + 48 < rb.w; s += 64, p += 4 * step) {
-      const float4 u0 = *reinterpret_cast<const float4*>(p);
-      const float4 u1 = *reinterpret_cast<const float4*>(p + step);
-      const float4 u2 = *reinterpret_cast<const float4*>(p + 2 * step);
-      const float4 u3 = *reinterpret_cast<const float4*>(p + 3 * step);
-      acc.x += u0.x; acc.y += u0.y; acc.z += u0.z; acc.w += u0.w;
-      acc.x += u1.x; acc.y += u1.y; acc.z += u1.z; acc.w += u1.w;
-      acc.x += u2.x; acc.y += u2.y; acc.z += u2.z; acc.w += u2.w;
-      acc.x += u3.x; acc.y += u3.y; acc.z += u3.z; acc.w += u3.w;
-    }
-    for (; s < rb.w; s += 16, p += step) {
-      const float4 u = *reinterpret_cast<const float4*>(p);
-      acc.x += u.x; acc.y += u.y; acc.z += u.z; acc.w += u.w;
+    for (int s0 = sl; s0 < rb.w; s0 += 128, p += 8 * step) {
+      float4 u[8];
+#pragma unroll
+      for (int j = 0; j < 8; ++j)
+        u[j] = s0 + 16 * j < rb.w ? *reinterpret_cast<const float4*>(p + j * step) : make_float4(0.f, 0.f, 0.f, 0.f);
+#pragma unroll
+      for (int j = 0; j < 8; ++j) {
+        if (s0 + 16 * j >= rb.w) break;
+        acc.x += u[j].x; acc.y += u[j].y; acc.z += u[j].z; acc.w += u[j].w;
+      }
     }
   }
   s_acc[sl][c4] = acc;
@@ -591,16 +634,14 @@ inline int next_pow2(int v) {
 }
 
 // Lanes per group from F alone (a plan does not depend on pointer alignment,
-// which only picks VEC at launch).  Wide rows use 16-lane groups (64 columns
-// per column tile): a heavy segment's nonzeros then interleave over 4 groups
-// of its wavefront (a 4x shorter gather chain), and 4 light rows share a
-// wavefront -- measured faster than 64-lane groups at F = 200 and 256
-// (profiles/r01_sweep_rows.log).
+// which only picks VEC at launch): the smallest power of two covering the row
+// in VEC-wide vectors, at most 64 (a whole wavefront per row and column tile;
+// heavy segments then belong to a 4-wavefront workgroup).  Measured against
+// 16/32-lane groups in profiles/r01_sweep_rows*.log.
 inline int choose_lpr(int32_t F, int lanes_hint) {
   if (lanes_hint > 0) return next_pow2(lanes_hint > 64 ? 64 : lanes_hint);
   const int Wv = (F % 4 == 0) ? F / 4 : F;
-  if (Wv > 16) return 16;
-  return next_pow2(Wv < 1 ? 1 : Wv);
+  return Wv <= 64 ? next_pow2(Wv < 1 ? 1 : Wv) : 64;
 }
 
 // Narrow groups use one-wave workgroups so a light launch still spans the chip.
@@ -623,7 +664,8 @@ struct RowLaunch {
 template <int BLOCK, int LPR, int VEC, int U, int NP>
 int launch_rows(const RowLaunch& a) {
   constexpr int SG = BLOCK / LPR, WPB = BLOCK / 64;
-  const int64_t nhb = ((int64_t)a.rp.nhunits + WPB - 1) / WPB;
+  // heavy segments: one per workgroup for whole-wavefront groups, else one per wavefront
+  const int64_t nhb = LPR == 64 ? (int64_t)a.rp.nhunits : ((int64_t)a.rp.nhunits + WPB - 1) / WPB;
   const int64_t nlb = ((int64_t)a.rp.nunits - a.rp.nhunits + SG - 1) / SG;
   if (nhb + nlb == 0) return GCNK_OK;
   if (nhb + nlb > (int64_t)INT32_MAX) {
@@ -696,7 +738,8 @@ struct TileArgs {
 
 template <bool V4, int NT>
 int launch_tile_nt(unsigned nitems, const TileArgs& t, hipStream_t s) {
-  hipLaunchKernelGGL((spmm_tile_kernel<V4, NT>), dim3(nitems), dim3(256), 0, s, t.tdesc, t.tcols, t.tfrag, t.trows, t.dval, t.F, t.B,
+  const unsigned slices = (unsigned)((t.F + NT * 16 - 1) / (NT * 16));
+  hipLaunchKernelGGL((spmm_tile_kernel<V4, NT>), dim3(nitems, slices), dim3(256), 0, s, t.tdesc, t.tcols, t.tfrag, t.trows, t.dval, t.F, t.B,
                      t.ldb, t.C, t.ldc, t.epi, t.slabs, t.slab_ld);
   return launch_check("spmm_tile_kernel");
 }
@@ -706,8 +749,8 @@ int launch_tile_v(int nt_need, unsigned nitems, const TileArgs& t, hipStream_t s
   if (nt_need <= 1) return launch_tile_nt<V4, 1>(nitems, t, s);
   if (nt_need <= 2) return launch_tile_nt<V4, 2>(nitems, t, s);
   if (nt_need <= 4) return launch_tile_nt<V4, 4>(nitems, t, s);
-  if (nt_need <= 8) return launch_tile_nt<V4, 8>(nitems, t, s);
-  if (nt_need <= 13) return launch_tile_nt<V4, 13>(nitems, t, s);
+  if (nt_need <= 6) return launch_tile_nt<V4, 6>(nitems, t, s);
+  if (nt_need <= 7) return launch_tile_nt<V4, 7>(nitems, t, s);
   if (nt_need <= kMaxNT) return launch_tile_nt<V4, kMaxNT>(nitems, t, s);
   set_error("spmm_tile_kernel: %d n-tiles exceed %d", nt_need, kMaxNT);
   return GCNK_EUNSUP;
@@ -843,7 +886,7 @@ int host_plan(const int32_t* rowptr_dev, const int32_t* colind_dev, const float*
 
   // ---- row units over the other rows.  A light row (<= ipc nonzeros) is one
   //      unit, in row order; a heavier row is cut into segments of about
-  //      ipc * groups nonzeros (the groups of one wavefront share a segment),
+  //      ipc * groups nonzeros (the lane groups sharing a segment),
   //      at most kMaxSeg of them; heavy segments come first in the unit list.
   const int64_t seg = (int64_t)ipc * groups;
   std::vector<int32_t> light;
@@ -885,15 +928,21 @@ using namespace gcnk;
 static unsigned long long* g_stamps = nullptr;
 extern "C" void gcnk_debug_set_stamps(void* buf) { g_stamps = (unsigned long long*)buf; }
 
-extern "C" int32_t gcnk_spmm_groups(int32_t F, int32_t lanes_hint) { return 64 / choose_lpr(F, lanes_hint); }
+// Lane groups sharing one heavy segment: 64/LPR per wavefront, or the 4
+// wavefronts of a workgroup for whole-wavefront groups.
+static int32_t segment_groups(int lpr) { return lpr == 64 ? 4 : 64 / lpr; }
+
+extern "C" int32_t gcnk_spmm_groups(int32_t F, int32_t lanes_hint) { return segment_groups(choose_lpr(F, lanes_hint)); }
 
 extern "C" int32_t gcnk_spmm_default_ipc(int32_t M, int64_t nnz, int32_t F, int32_t lanes_hint) {
   (void)M;
   (void)nnz;
-  // light-row limit (and per-group share of a heavy segment): two U = 8 gather
-  // batches for groups of >= 8 lanes, one for narrow groups (sweep:
-  // profiles/r01_sweep_rows.log)
-  return choose_lpr(F, lanes_hint) >= 8 ? 16 : 8;
+  // light-row limit (and each group's share of a heavy segment): four U = 8
+  // gather batches per wavefront at 64 lanes (heavy segments of 128 nonzeros
+  // over a workgroup), one batch for narrower groups (sweeps:
+  // profiles/r01_sweep_rows*.log; R8 F = 200: ipc 16 11.1 us, 32 11.3 us;
+  // 20ng-shaped: 32 21.6 us, 64 20.0 us)
+  return choose_lpr(F, lanes_hint) == 64 ? 32 : 8;
 }
 
 extern "C" int64_t gcnk_spmm_plan_bytes(const int32_t* rowptr, const int32_t* colind, int32_t M, int32_t K,
@@ -1010,9 +1059,9 @@ static int spmm_impl(const void* plan, const int32_t* hdr, const float* B, int64
     return GCNK_EARG;
   }
   const int lpr = choose_lpr(F, lanes_hint);
-  if (hdr[3] != 64 / lpr) {
-    set_error("gcnk_spmm_csr_f32: plan built for %d lane groups per wave, this F/lanes uses %d (gcnk_spmm_groups)",
-              hdr[3], 64 / lpr);
+  if (hdr[3] != segment_groups(lpr)) {
+    set_error("gcnk_spmm_csr_f32: plan built for %d lane groups per segment, this F/lanes uses %d (gcnk_spmm_groups)",
+              hdr[3], segment_groups(lpr));
     return GCNK_EARG;
   }
   const int64_t need = gcnk_spmm_workspace_bytes(hdr, F);
@@ -1053,22 +1102,19 @@ static int spmm_impl(const void* plan, const int32_t* hdr, const float* B, int64
   // ---- dense blocks: tile kernel (+ slab reduce)
   const float* dval = L.has_diag ? reinterpret_cast<const float*>(p + L.dval) : nullptr;
   if (L.ntile > 0) {
+    // column slices of <= kMaxNT n-tiles on grid.y, balanced (F = 200: 2 x 7 n-tiles),
+    // so two workgroups of a chunk share the staging/MFMA/store phases of a CU
     const int32_t nt_total = (int32_t)(slab_ld / 16);
-    // F <= 16*kMaxNT: one launch over all columns; wider: 128-column slices with the
-    // slice offset folded into the B/C/bias/mask pointers (multiples of 4: alignment kept)
-    const int32_t slice = nt_total <= kMaxNT ? (int32_t)(nt_total * 16) : 128;
-    const int4* td = reinterpret_cast<const int4*>(p + L.tdesc);
-    for (int64_t c0 = 0; c0 < F; c0 += slice) {
-      const int32_t Fs = (int32_t)std::min<int64_t>(slice, F - c0);
-      Epi es = e;
-      es.bias = bias ? bias + c0 : nullptr;
-      es.mask = drop_mask ? drop_mask + c0 : nullptr;
-      es.offset = e.offset + (uint64_t)c0;  // hash index shifts with the column
-      TileArgs ta{td,      p + L.tcols, reinterpret_cast<const float*>(p + L.tfrag), p + L.trows, dval, Fs, B + c0,
-                  ldb,     C + c0,      ldc, es, slabs ? slabs + c0 : nullptr, slab_ld};
-      const int rc = launch_tile(vec4, (Fs + 15) / 16, (unsigned)L.ntile, ta, s);
-      if (rc) return rc;
+    const int32_t nslices = (nt_total + kMaxNT - 1) / kMaxNT;
+    if (nslices > 65535) {
+      set_error("gcnk_spmm_csr_f32: F=%d needs %d tile column slices (> 65535)", F, nslices);
+      return GCNK_EUNSUP;
     }
+    const int4* td = reinterpret_cast<const int4*>(p + L.tdesc);
+    TileArgs ta{td, p + L.tcols, reinterpret_cast<const float*>(p + L.tfrag), p + L.trows, dval, F, B,
+                ldb, C, ldc, e, slabs, slab_ld};
+    const int rc = launch_tile(vec4, (nt_total + nslices - 1) / nslices, (unsigned)L.ntile, ta, s);
+    if (rc) return rc;
     if (L.nred > 0) {
       hipLaunchKernelGGL(spmm_tile_reduce_kernel, dim3((unsigned)L.nred, kRB, (unsigned)((F + 63) / 64)), dim3(256),
                          0, s, reinterpret_cast<const int4*>(p + L.red), p + L.trows, dval, F, slabs, slab_ld, B, ldb,

@@ -53,6 +53,8 @@ def main():
         "XW1": lambda: ops.spmm(X, W1, out=H),
         "AS1_F200": lambda: ops.spmm(A, S1, out=H),
         "AS1_F200_nodense": lambda: ops.spmm(A, S1, out=H, dense=2.0),
+        "AS1_F200_proj": lambda: ops.spmm_proj(A, S1, W2, bias=W2[0].repeat(25), epilogue=2, store_main=False),
+        "AS1_F200_proj_H": lambda: ops.spmm_proj(A, S1, W2, bias=W2[0].repeat(25), epilogue=2),
         "AS2_F8": lambda: ops.spmm(A, S2, out=o8),
         "gemm_H_W2": lambda: ops.gemm(H, W2, out=o8),
         "torch_mm_H_W2": lambda: torch.mm(H, W2, out=o8),
@@ -81,6 +83,23 @@ def main():
     torch.cuda.synchronize()
     fwd_us = (time.time() - t0) / (n * 50) * 1e6
     print(json.dumps({"phase": "warm", "forward_us_sustained": round(fwd_us, 2)}), flush=True)
+    ops.FUSE_PROJECTION = not ops.FUSE_PROJECTION
+    g2 = torch.cuda.CUDAGraph()
+    with torch.no_grad(), torch.cuda.graph(g2):
+        for _ in range(50):
+            m(x, adj)
+    g2.replay()
+    torch.cuda.synchronize()
+    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    e0.record()
+    for _ in range(40):
+        g2.replay()
+    e1.record()
+    e1.synchronize()
+    fwd2 = e0.elapsed_time(e1) * 1e3 / (40 * 50)
+    print(json.dumps({"phase": "warm", "fuse_projection": ops.FUSE_PROJECTION, "forward_us": round(fwd2, 2)}),
+          flush=True)
+    ops.FUSE_PROJECTION = not ops.FUSE_PROJECTION
     for k, fn in ops_.items():
         best, allr = time_graph(fn)
         print(json.dumps({"op": k, "us": round(best, 2), "all": [round(v, 2) for v in allr]}), flush=True)

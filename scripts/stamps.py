@@ -26,7 +26,7 @@ def main():
     only = sys.argv[1:] or None
     # (column tile 0 only: grid rows of other tiles are not split by kind)
     cases = [("R8_A_F200", A, 200, 0, None), ("R8_A_F8", A, 8, 0, None),
-             ("R8_A_F200_l16i16", A, 200, 16, 16), ("R8_A_F200_i8", A, 200, 0, 8)]
+             ("R8_A_F200_l64i32", A, 200, 64, 32), ("R8_X_F200", X, 200, 0, None)]
     cases = [c for c in cases if only is None or c[0] in only]
     for name, a, F, lanes, ipc in cases:
         B = torch.randn(a.shape[1], F, device=dev)
@@ -40,6 +40,11 @@ def main():
         torch.cuda.synchronize()
         lib.gcnk_debug_set_stamps(None)
         hdr = list(a._plans.values())[-1].header
+        if hdr[5] == 0:   # tile-path-only operand (R8 X): one summary over the tile kernel's blocks
+            s_all = buf.view(-1, 4).cpu().numpy().astype(np.float64)
+            s = s_all[(s_all[:, 0] > 0) & (s_all[:, 3] > 0)]
+            summarize(name + ":tile", (s - s[:, 0].min()) / 100.0)
+            continue
         nhb = (hdr[6] + 3) // 4 if hdr[3] <= 8 else hdr[6]  # 256-thread blocks hold 4 heavy waves
         s_all = buf.view(-1, 4).cpu().numpy().astype(np.float64)
         t0 = s_all[s_all[:, 0] > 0, 0].min()

@@ -87,9 +87,9 @@ def test_argument_validation_without_gpu():
 
 def test_plan_and_workspace_sizes():
     lib = _lib.load()
-    # lane groups per wavefront = 64 / lanes per row group
-    assert lib.gcnk_spmm_groups(200, 0) == 4 and lib.gcnk_spmm_groups(8, 0) == 32
-    assert lib.gcnk_spmm_groups(7, 0) == 8 and lib.gcnk_spmm_groups(200, 64) == 1
+    # lane groups sharing a heavy segment: 64 / lanes per group, or 4 wavefronts at 64 lanes
+    assert lib.gcnk_spmm_groups(200, 0) == 4 and lib.gcnk_spmm_groups(8, 0) == 32 and lib.gcnk_spmm_groups(64, 0) == 4
+    assert lib.gcnk_spmm_groups(7, 0) == 8 and lib.gcnk_spmm_groups(200, 16) == 4 and lib.gcnk_spmm_groups(200, 32) == 2
     h, _keep = _hdr(nslots=10, nslabs=3)
     assert lib.gcnk_spmm_workspace_bytes(h, 198) == 8192 + 3 * 64 * 208 * 4
     assert lib.gcnk_gemm_workspace_bytes(200, 8, 7724, 4) == 4 * 200 * 8 * 4

@@ -37,6 +37,26 @@ ROOT = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, ROOT)
 
 HBM_PEAK_GBS = 8000.0   # MI355X HBM3E spec (MI355X_MICROARCH.md)
+# PMC summary of the forward's kernels (scripts/pmc.sh: separate FETCH_SIZE and
+# WRITE_SIZE passes, FETCH doubled per the gfx950 correction), committed per round
+PMC_TRAFFIC = os.path.join(ROOT, "profiles", "r01_pmc_traffic.json")
+# kernels each op of the forward launches (names as rocprofv3 / the PMC summary give them)
+OP_KERNELS = {
+    "spmm_XW1": ["spmm_tile_kernel<true, 7>", "spmm_tile_reduce_kernel"],
+    "spmm_AS1_F200": ["spmm_row_kernel<256, 64, 4, 8, 0>"],
+    "gemm_H1W2": ["gemm_skinny_ksplit_kernel<4>"],
+    "spmm_AS2_F8": ["spmm_row_kernel<64, 2, 4, 8, 0>"],
+}
+
+
+def pmc_traffic(op):
+    """HBM-side bytes per launch of `op` from the committed PMC summary, or None."""
+    try:
+        with open(PMC_TRAFFIC) as f:
+            t = json.load(f)
+        return sum(t[k]["hbm_bytes_per_launch"] for k in OP_KERNELS[op])
+    except (OSError, KeyError, ValueError):
+        return None
 
 
 def spmm_bytes(M, K, nnz, F):
@@ -204,10 +224,11 @@ def main():
                    "nodes": N, "adj_nnz": nnz_a, "x_nnz": nnz_x, "graph": not args.no_graph,
                    "parallelism": f"replicas{world}" if world > 1 else "single"},
         "roofline": {"bound": "hbm", "kernel": north, "achieved": kn["gbs"], "peak": HBM_PEAK_GBS,
-                     "unit": "GB/s", "frac": kn["gbs"] / HBM_PEAK_GBS, "traffic": None,
+                     "unit": "GB/s", "frac": kn["gbs"] / HBM_PEAK_GBS, "traffic": pmc_traffic(north),
                      "avg_launch_us": kn["us"], "algorithmic_bytes": kn["bytes"]},
         "roofline_dominant": {"kernel": dom, "achieved": kd["gbs"], "frac": kd["gbs"] / HBM_PEAK_GBS,
-                              "avg_launch_us": kd["us"], "algorithmic_bytes": kd["bytes"]},
+                              "avg_launch_us": kd["us"], "algorithmic_bytes": kd["bytes"],
+                              "traffic": pmc_traffic(dom)},
         "kernels_us": {k: round(v["us"], 3) for k, v in ktimes.items()},
         "cpu_baseline": cpu,
     }

@@ -40,10 +40,16 @@ def main():
         torch.cuda.synchronize()
         lib.gcnk_debug_set_stamps(None)
         hdr = list(a._plans.values())[-1].header
-        if hdr[5] == 0:   # tile-path-only operand (R8 X): one summary over the tile kernel's blocks
+        if hdr[5] == 0:   # tile-path-only operand (R8 X): chunks of single-chunk blocks vs multi-chunk blocks
             s_all = buf.view(-1, 4).cpu().numpy().astype(np.float64)
-            s = s_all[(s_all[:, 0] > 0) & (s_all[:, 3] > 0)]
-            summarize(name + ":tile", (s - s[:, 0].min()) / 100.0)
+            nchunk = hdr[8]
+            single = hdr[11] - hdr[9]            # single-chunk blocks come first (R8 X: document rows)
+            t0 = s_all[s_all[:, 0] > 0, 0].min()
+            idx = np.arange(len(s_all)) % max(nchunk, 1)
+            for kind, sel in (("single", idx < single), ("multi", idx >= single)):
+                s = s_all[sel & (s_all[:, 0] > 0) & (s_all[:, 3] > 0)]
+                if len(s):
+                    summarize(f"{name}:tile_{kind}", (s - t0) / 100.0)
             continue
         nhb = (hdr[6] + 3) // 4 if hdr[3] <= 8 else hdr[6]  # 256-thread blocks hold 4 heavy waves
         s_all = buf.view(-1, 4).cpu().numpy().astype(np.float64)

@@ -374,3 +374,66 @@ def test_r8_training_accuracy_parity(r8, golden_meta, seed):
     # the loss trajectory follows the reference's closely for the first epochs
     for h, g in list(zip(hist, run["history"]))[:10]:
         assert abs(h["train_loss"] - g["train_loss"]) < 1e-3
+
+
+# ------------------------------------------------------------------------------ BASELINE configs 3-5 at full size
+
+def test_gcn_20ng_shaped_forward_matches_oracle():
+    """BASELINE config 3: 20ng-shaped doc-topic graph (18,846 docs, 70 topics,
+    nclass 20, gensim-shaped nfeat 100 -> dense-block X), eval logits vs the
+    oracle's reference-equivalent forward on the same tensors."""
+    g = datasets.doc_topic_graph(18846, 70, 20, seed=0)
+    torch.manual_seed(11)
+    m = GCN(nfeat=g["nfeat"], nhid=200, nclass=20, dropout=0.5).to(DEV).eval()
+    ref = gcn_ref.RefGCN(nfeat=g["nfeat"], nhid=200, nclass=20, dropout=0.5).eval()
+    ref.load_state_dict({k: v.cpu() for k, v in m.state_dict().items()})
+    with torch.no_grad():
+        got = m(g["features"].to(DEV), g["adj"].to(DEV)).cpu().numpy()
+        want = ref(g["features"], g["adj"]).numpy()
+    assert np.abs(got - want).max() <= LOGIT_TOL
+    _labels_check(got, want)
+
+
+@pytest.fixture(scope="module")
+def big_graph():
+    """BASELINE config 4: uniform random 1M nodes / 20M edges (coalesced), int32 CSR."""
+    rp, ci, v = datasets.uniform_random_csr(1_000_000, 20_000_000, seed=0, device=DEV)
+    return from_arrays(rp, ci, v, (1_000_000, 1_000_000), DEV), (rp.cpu().numpy(), ci.cpu().numpy(), v.cpu().numpy())
+
+
+def test_spmm_1m_20m_f256_sampled_rows_and_linearity(big_graph):
+    """Full-size F = 256 product: 4,096 sampled rows against the float64 oracle
+    (row slices of the CSR), and linearity A(B1 + B2) = A B1 + A B2 over every
+    row (a size-independent property)."""
+    a, (rp, ci, v) = big_graph
+    M, F = a.shape[0], 256
+    g = torch.Generator(device=DEV).manual_seed(5)
+    B1 = torch.randn(M, F, device=DEV, generator=g)
+    C1 = spmm(a, B1)
+    rows = np.sort(np.random.default_rng(1).choice(M, 4096, replace=False))
+    B1h = B1.cpu().numpy()
+    sub = C1[torch.from_numpy(rows).to(DEV)].cpu().numpy()
+    for i, r in enumerate(rows):
+        b, e = rp[r], rp[r + 1]
+        want = v[b:e].astype(np.float64) @ B1h[ci[b:e]].astype(np.float64)
+        _close(sub[i], want, atol=2e-5 * np.sqrt(max(e - b, 1)))
+    del B1h
+    B2 = torch.randn(M, F, device=DEV, generator=g)
+    lhs = spmm(a, B1 + B2)
+    rhs = C1 + spmm(a, B2)
+    assert torch.allclose(lhs, rhs, rtol=1e-5, atol=1e-4)
+    assert torch.equal(spmm(a, B1), C1)   # bitwise reproducible at full size
+
+
+def test_column_sharded_spmm_single_rank_on_gpu(big_graph):
+    """BASELINE config 5's sharding module on one rank through the HIP kernels
+    (world 1: the shard is the whole operand): F = 512 block of a 4096-wide
+    operand on the 1M/20M graph, equal to the unsharded product."""
+    from graph_convolutional_networks_for_text_classification_amd.parallel import ColumnShardedSpMM
+    a, _ = big_graph
+    F = 512
+    B = torch.randn(a.shape[0], F, device=DEV, generator=torch.Generator(device=DEV).manual_seed(2))
+    op = ColumnShardedSpMM(a, F)
+    full = op(op.shard(B))
+    assert full.shape == (a.shape[0], F)
+    assert torch.equal(full, spmm(a, B))

@@ -9,7 +9,8 @@ own builder and PrepareData in the build container; 7,724 nodes, Â nnz
 random-init weights (torch.manual_seed(0), the reference init), eval mode.
 A step = one full GCN forward (X·W1 SpMM, Â·S1 SpMM + bias + ReLU, H1·W2
 MFMA GEMM, Â·S2 SpMM + bias), replayed from a hipGraph with all inputs
-resident in HBM.
+resident in HBM; --graph-steps forwards are captured per graph (every one a
+complete forward), so exactly --steps forwards run in the timed region.
 
 metric/value: SpMM edges/s = (2 · nnz(Â) per forward — the two graph
 aggregations of layer.py:106) × steps × ranks / max-over-ranks time;
@@ -69,6 +70,8 @@ def parse():
     ap.add_argument("--steps", type=int, default=200)
     ap.add_argument("--warmup", type=int, default=20)
     ap.add_argument("--no-graph", action="store_true", help="eager launches instead of hipGraph replay")
+    ap.add_argument("--graph-steps", type=int, default=10,
+                    help="forwards captured per hipGraph (steps must be a multiple; amortises the per-replay floor)")
     ap.add_argument("--cpu-sample-s", type=float, default=10.0, help="seconds of CPU baseline work (0 = skip)")
     ap.add_argument("--kernel-reps", type=int, default=200, help="launches per kernel-timing graph")
     return ap.parse_args()
@@ -116,19 +119,24 @@ def main():
             for _ in range(3):
                 forward()
         torch.cuda.current_stream().wait_stream(s)
+        per = max(1, args.graph_steps)
+        while args.steps % per or args.warmup % per:
+            per -= 1
         graph = torch.cuda.CUDAGraph()
         with torch.cuda.graph(graph):
-            out = forward()
+            for _ in range(per):
+                out = forward()
         step = graph.replay
+    per = 1 if args.no_graph else per   # forwards per step() call
 
-    for _ in range(args.warmup):
+    for _ in range(args.warmup // per):
         step()
     torch.cuda.synchronize()
     if world > 1:
         dist.barrier()
     torch.cuda.synchronize()
     t0 = time.perf_counter()
-    for _ in range(args.steps):
+    for _ in range(args.steps // per):
         step()
     torch.cuda.synchronize()
     if world > 1:
@@ -222,6 +230,7 @@ def main():
         "data": "R8 graph fixture generated in-container by the reference's own builder; random-init weights",
         "config": {"workload": "R8 GCN forward (eval), hidden 200, 8 classes, nfeat 7463",
                    "nodes": N, "adj_nnz": nnz_a, "x_nnz": nnz_x, "graph": not args.no_graph,
+                   "forwards_per_graph": per,
                    "parallelism": f"replicas{world}" if world > 1 else "single"},
         "roofline": {"bound": "hbm", "kernel": north, "achieved": kn["gbs"], "peak": HBM_PEAK_GBS,
                      "unit": "GB/s", "frac": kn["gbs"] / HBM_PEAK_GBS, "traffic": pmc_traffic(north),

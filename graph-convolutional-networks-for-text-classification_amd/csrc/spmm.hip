@@ -146,8 +146,20 @@ struct ProjArgs {
 template <int NP, int LPR, int VPL, int VEC>
 struct Proj {
   float w[VPL * VEC][NP > 0 ? NP : 1];
+  // W [F x P] is staged through LDS by the whole workgroup with coalesced loads
+  // (a lane's own rows read straight from global memory would make every
+  // wave-instruction touch 64 cache lines), then each lane keeps its columns'
+  // rows in registers.  Called by every thread before any early return.
   __device__ __forceinline__ void load(const ProjArgs& pa, int32_t F, const int64_t* colv, const bool* colok) {
     if constexpr (NP > 0) {
+      constexpr int kMaxF = LPR * VPL * VEC;  // one column tile holds the whole row
+      __shared__ float s_w[kMaxF * NP];
+      const int nthr = blockDim.x;
+      for (int e = threadIdx.x; e < kMaxF * NP; e += nthr) {
+        const int r = e / NP, c = e % NP;
+        s_w[e] = (r < F && c < pa.P) ? pa.W[(int64_t)r * pa.ldw + c] : 0.f;
+      }
+      __syncthreads();
 #pragma unroll
       for (int v = 0; v < VPL; ++v)
 #pragma unroll
@@ -155,7 +167,7 @@ struct Proj {
 #pragma unroll
           for (int c = 0; c < NP; ++c) {
             const int64_t col = colv[v] + i;
-            w[v * VEC + i][c] = (colok[v] && col < F && c < pa.P) ? pa.W[col * pa.ldw + c] : 0.f;
+            w[v * VEC + i][c] = (colok[v] && col < F) ? s_w[col * NP + c] : 0.f;
           }
     }
   }

@@ -26,7 +26,7 @@ def main():
     only = sys.argv[1:] or None
     # (column tile 0 only: grid rows of other tiles are not split by kind)
     cases = [("R8_A_F200", A, 200, 0, None), ("R8_A_F8", A, 8, 0, None),
-             ("R8_A_F200_l64i32", A, 200, 64, 32), ("R8_X_F200", X, 200, 0, None)]
+             ("R8_A_F200_i16", A, 200, 0, 16), ("R8_X_F200", X, 200, 0, None)]
     cases = [c for c in cases if only is None or c[0] in only]
     for name, a, F, lanes, ipc in cases:
         B = torch.randn(a.shape[1], F, device=dev)
@@ -51,7 +51,10 @@ def main():
                 if len(s):
                     summarize(f"{name}:tile_{kind}", (s - t0) / 100.0)
             continue
-        nhb = (hdr[6] + 3) // 4 if hdr[3] <= 8 else hdr[6]  # 256-thread blocks hold 4 heavy waves
+        # heavy blocks: one segment per workgroup at 64 lanes (hdr[3] == 4 with F > 64),
+        # 4 per 256-thread workgroup for 8..32 lanes, 1 per one-wave workgroup below
+        lpr = 64 if (hdr[3] == 4 and F > 64) else 64 // hdr[3]
+        nhb = hdr[6] if lpr == 64 else ((hdr[6] + 3) // 4 if lpr >= 8 else hdr[6])
         s_all = buf.view(-1, 4).cpu().numpy().astype(np.float64)
         t0 = s_all[s_all[:, 0] > 0, 0].min()
         for kind, rows in (("heavy", s_all[:nhb]), ("light", s_all[nhb:]), ("all", s_all)):

@@ -80,8 +80,9 @@ def spmm(a, B, bias=None, epilogue=_lib.EPI_NONE, mask=None, scale=1.0, keep_pro
 
 
 # Fuse gc2's H1 W2 into the gc1 aggregation epilogue (gcnk_spmm_proj_f32).
-# Off by default: on R8 the fused path kernel (W in registers, shorter gather
-# batches) measured slower than the unfused SpMM + skinny GEMM pair.
+# Off by default: on R8 the fused row kernel (W in registers, 4 waves per SIMD)
+# measured 20.8 us against 11.5 + 3.4 us for the SpMM + K-split GEMM pair
+# (profiles/r01_diag_rows_wg.log).
 FUSE_PROJECTION = False
 
 

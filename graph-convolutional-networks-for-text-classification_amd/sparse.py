@@ -6,12 +6,12 @@ The reference hands ``th.spmm`` torch sparse COO tensors every call:
   * X from ``trainer.py:226-238``: row-major COO.
 ATen re-coalesces such tensors on every call.  Here the first forward
 converts them once to an int32 CSR resident in HBM (plus, lazily, the
-transposed CSR the autograd products need and the merge-path schedule per
-chunk size) and later calls hit the cache.
+transposed CSR the autograd products need and the SpMM plan per column-width
+class) and later calls hit the cache.
 
 HBM layout of one CSR operand (M rows, K cols, nnz nonzeros):
   rowptr int32[M+1] | colind int32[nnz] | val fp32[nnz]
-  plan   int32[...]  merge-path schedule (include/gcnk.h), one per ipc
+  plan   int32[...]  row units + dense tile blocks (include/gcnk.h), one per (ipc, groups, threshold)
 """
 import collections
 import ctypes

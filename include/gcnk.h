@@ -84,14 +84,15 @@ const char* gcnk_last_error(void);
  *    per nonzero; its rows' diagonal entries are kept aside and added in the
  *    epilogue; multi-chunk blocks are summed from partial slabs in order.
  *    dense_threshold > 1 disables the part (default callers pass 0.25).
- *  - path: the other rows' nonzeros in row order, each row closed by an
- *    end-of-row marker, as one int2 item stream (col, value bits) / (-1, row)
- *    / (-2 pad) cut into windows of W = groups*ipc items, one per workgroup;
- *    rows of at most W/2 items never straddle a window, so only heavy rows
- *    cross windows.  Rows split between the chunks of a window meet in LDS;
- *    heavy rows crossing windows leave one partial per window and the last
- *    window to finish sums them in path order (arrival counters kept in the
- *    plan: launches sharing one plan must be ordered on one stream).
+ *  - row units: the other rows.  A row of at most `ipc` nonzeros is one unit
+ *    owned by one lane group (LPR lanes, each a 16-B column vector); a
+ *    heavier row is cut into segments of about ipc * groups nonzeros (at most
+ *    64), each owned by `groups` lane groups (the 64/LPR groups of a
+ *    wavefront, or the 4 wavefronts of a workgroup when LPR = 64) that take
+ *    interleaved nonzeros and meet in a fixed-order reduction; a row of
+ *    several segments leaves one partial per segment and the last segment to
+ *    finish (arrival counters kept in the plan: launches sharing one plan
+ *    must be ordered on one stream) sums them in segment order.
  * All sums have a fixed order (no float atomics): bitwise reproducible.
  * gcnk_spmm_groups(F, lanes_hint) gives the `groups` the kernels use for a
  * width F; a plan serves every F with that count.  The plan copies the
@@ -99,9 +100,10 @@ const char* gcnk_last_error(void);
  * and synchronises `stream` (one-time setup).
  *
  * Plan header (16 int32, first words of the plan; gcnk_spmm_plan_query):
- *   0 magic 'GNK4'  1 M  2 K  3 groups  4 ipc  5 W  6 nwin  7 nfix  8 nslots
- *   9 tile chunks  10 multi-chunk blocks  11 slabs  12 tile blocks
- *   13 diagonal kept aside (0/1)  14 heavy  15 0   (tile blocks: 64 rows x 64-column chunks)
+ *   0 magic 'GNK5'  1 M  2 K  3 groups  4 ipc  5 row units  6 heavy segments
+ *   (= partial slots)  7 heavy rows of > 1 segment  8 tile chunks
+ *   9 multi-chunk blocks  10 slabs  11 tile blocks  12 diagonal kept aside
+ *   (0/1)  13 nnz  14 0  15 0   (tile blocks: 64 rows x 64-column chunks)
  * ------------------------------------------------------------------------- */
 int32_t gcnk_spmm_groups(int32_t F, int32_t lanes_hint);
 int32_t gcnk_spmm_default_ipc(int32_t M, int64_t nnz, int32_t F, int32_t lanes_hint);

@@ -93,19 +93,22 @@ struct Vec<1> {
 
 // ---------------------------------------------------------------------------
 // Plan layout (int32 words).  Header (16 words, see gcnk.h):
-//   0 magic  1 M  2 K  3 lane groups per heavy segment  4 ipc (light-row limit)  5 nunits
-//   6 nhunits (heavy segments = partial slots)  7 nheavy (rows of > 1 segment)
-//   8 ntile (chunks)  9 nred  10 nslabs  11 ntblk (tile blocks)  12 has_diag  13 nnz  14 0  15 0
+//   0 magic  1 M  2 K  3 lane groups per wavefront (64 / LPR)  4 ipc (light-row limit)
+//   5 nunits  6 nhunits (heavy region, padded)  7 nheavy (rows of > 1 segment)
+//   8 ntile (chunks)  9 nred  10 nslabs  11 ntblk (tile blocks)  12 has_diag  13 nnz
+//   14 nslots (partial slots)  15 0
 // Body: items int2[nnz] {col, value bits} in CSR order | units int4[nunits]
-//   {row, nz begin, nz end, heavy row index or -1}, heavy segments first |
-//   heavy int4[nheavy] {row, first unit, nseg, 0} | arrival counters
+//   {row (-1: empty), nz begin, nz end, heavy row * 64 + segment or -1}: the
+//   heavy region first, then light rows, each laid out so that the units of
+//   workgroup b belong to XCD class b % 8 (below) | heavy int4[nheavy]
+//   {row, first partial slot, nseg, 0} | arrival counters
 //   int32[nheavy * kMaxColTiles] (zero between launches) | tile part.
 struct Layout {
-  int64_t M, nnz, nunits, nhunits, nheavy, ntile, nred, ntblk, has_diag;
+  int64_t M, nnz, nunits, nhunits, nheavy, nslots, ntile, nred, ntblk, has_diag;
   int64_t items, units, heavy, cnt, tdesc, tcols, tfrag, red, trows, dval, total;
   __host__ __device__ explicit Layout(const int32_t* h) {
     M = h[1]; nunits = h[5]; nhunits = h[6]; nheavy = h[7]; ntile = h[8]; nred = h[9]; ntblk = h[11];
-    has_diag = h[12]; nnz = h[13];
+    has_diag = h[12]; nnz = h[13]; nslots = h[14];
     items = 16;
     units = (items + 2 * nnz + 3) & ~3LL;
     heavy = units + 4 * nunits;
@@ -229,8 +232,8 @@ struct Proj {
 // Row kernel (gathers).
 struct RowPlan {
   const int2* items;   // {col, value bits} per nonzero, CSR order
-  const int4* units;   // {row, nz begin, nz end, heavy row index or -1}; heavy segments first
-  const int4* heavy;   // {row, first unit (= first partial slot), nseg, 0}
+  const int4* units;   // {row (-1: empty), nz begin, nz end, heavy row * 64 + segment or -1}
+  const int4* heavy;   // {row, first partial slot, nseg, 0}
   int32_t* cnt;        // per heavy row x column tile: arrival counters (zero between launches)
   int32_t nunits, nhunits;
 };
@@ -336,6 +339,7 @@ spmm_row_kernel(RowPlan rp, int32_t nhb, const float* __restrict__ B, int64_t ld
     if (LPR == 64) u = __builtin_amdgcn_readfirstlane(u);
     if (u >= rp.nunits) return;
     const int4 un = rp.units[u];
+    if (un.x < 0) return;  // padding of the XCD-class layout
     stamp(epi, 1);
     gather_rows<VEC, U, 1>(rp.items, un.y, un.z, 0, B, ldb, colv, colok, acc);
     stamp(epi, 2);
@@ -359,6 +363,7 @@ spmm_row_kernel(RowPlan rp, int32_t nhb, const float* __restrict__ B, int64_t ld
   const int32_t u = WG ? (int32_t)blockIdx.x : __builtin_amdgcn_readfirstlane((int32_t)blockIdx.x * WPB + w);
   if (u >= rp.nhunits) return;  // WG: uniform over the workgroup
   const int4 un = rp.units[u];
+  if (un.x < 0) return;           // padding of the XCD-class layout
   stamp(epi, 1);
   gather_rows<VEC, U, GS>(rp.items, un.y, un.z, q, B, ldb, colv, colok, acc);
   if constexpr (WG) {
@@ -377,10 +382,11 @@ spmm_row_kernel(RowPlan rp, int32_t nhb, const float* __restrict__ B, int64_t ld
   }
   // publish this segment's partial, then count in; the last arriver sums all of
   // the row's partials in segment order
-  const int4 hv = rp.heavy[un.w];
-  int32_t* ctr = rp.cnt + (int64_t)un.w * kMaxColTiles + blockIdx.y;
+  const int32_t hid = un.w >> 6;  // heavy row, segment un.w & 63
+  const int4 hv = rp.heavy[hid];
+  int32_t* ctr = rp.cnt + (int64_t)hid * kMaxColTiles + blockIdx.y;
   int32_t last = 0;
-  if (q == 0 && colok) store_coherent(part + (int64_t)u * part_ld + colv, acc);
+  if (q == 0 && colok) store_coherent(part + (int64_t)(hv.y + (un.w & 63)) * part_ld + colv, acc);
   if (!WG || w == 0) {  // the wavefront that stored counts in, after its stores completed
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     int32_t arrived = 0;
@@ -565,9 +571,13 @@ spmm_tile_kernel(const int4* __restrict__ tdesc, const int32_t* __restrict__ tco
     }
     const int64_t row = s_cols[rl];
     const float dv = s_dv[rl];
-    if (VEC4 && dv == 0.f && epi.code <= GCNK_EPI_BIAS_RELU) {
-      // common case, vectorised: no extracted diagonal, no dropout (the
-      // per-element path below costs ~1.6 us of the R8 X launch)
+    if (VEC4 && epi.code <= GCNK_EPI_BIAS_RELU) {
+      // common case, vectorised (no dropout): + extracted diagonal * B row piece,
+      // + bias, relu
+      if (dv != 0.f) {
+        const float4 b4 = *reinterpret_cast<const float4*>(B + row * ldb + col);
+        v.x = fmaf(dv, b4.x, v.x); v.y = fmaf(dv, b4.y, v.y); v.z = fmaf(dv, b4.z, v.z); v.w = fmaf(dv, b4.w, v.w);
+      }
       if (epi.code != GCNK_EPI_NONE) {
         const float4 b4 = *reinterpret_cast<const float4*>(s_bias + (col - col0));
         v.x += b4.x; v.y += b4.y; v.z += b4.z; v.w += b4.w;
@@ -910,38 +920,97 @@ int host_plan(const int32_t* rowptr_dev, const int32_t* colind_dev, const float*
     if (any_diag) hp.dval = std::move(dv);
   }
 
-  // ---- row units over the other rows.  A light row (<= ipc nonzeros) is one
-  //      unit, in row order; a heavier row is cut into segments of about
-  //      ipc * groups nonzeros (the lane groups sharing a segment),
-  //      at most kMaxSeg of them; heavy segments come first in the unit list.
-  const int64_t seg = (int64_t)ipc * groups;
-  std::vector<int32_t> light;
+  // ---- row units over the other rows.  Launch geometry from `groups` = 64 / LPR.
+  if (groups < 1 || groups > 64 || (groups & (groups - 1))) {
+    set_error("gcnk_spmm_plan: groups %d is not a power of two in [1, 64]", groups);
+    return GCNK_EARG;
+  }
+  const int lpr = 64 / groups;
+  const int block = lpr >= 8 ? 256 : 64, wpb = block / 64, sg = block / lpr;
+  const int hpb = lpr == 64 ? 1 : wpb;                     // heavy units per workgroup
+  const int64_t seg = (int64_t)ipc * (lpr == 64 ? wpb : groups);  // nonzeros per heavy segment
+  // XCD classes.  Workgroups b and b + 8 land on one XCD (round-robin dispatch;
+  // speed only, never correctness), so every unit of workgroup b is given
+  // class b % 8: a light row by its row index, a heavy segment by the column
+  // range it gathers (heavy rows are first cut where their sorted column
+  // indices cross a class boundary).  Each XCD's L2 then serves 1/8 of B
+  // instead of every XCD fetching the rows its segments happen to need
+  // (R8 Â: the topic rows gather all document rows).
+  constexpr int NX = 8;
+  auto cls = [](int64_t i, int64_t n) { return n > 0 ? (int)(i * NX / n) : 0; };
+  std::vector<std::vector<int32_t>> hq(NX), lq(NX);  // int4 units per class
   int32_t nheavy = 0;
+  int64_t nslots = 0;
   hp.units.clear();
   hp.heavy.clear();
+  std::vector<int64_t> rb, rcl;  // runs of one column class: start, class
   for (int32_t r = 0; r < M; ++r) {
     if (tile_row[(size_t)r]) continue;
-    const int64_t b = rp[r], deg = (int64_t)rp[r + 1] - b;
+    const int64_t b = rp[r], e = rp[r + 1], deg = e - b;
     if (deg <= ipc) {
-      light.insert(light.end(), {r, (int32_t)b, rp[r + 1], -1});
+      lq[(size_t)cls(r, M)].insert(lq[(size_t)cls(r, M)].end(), {r, (int32_t)b, (int32_t)e, -1});
       continue;
     }
-    const int64_t nseg = std::min<int64_t>((deg + seg - 1) / seg, kMaxSeg);
-    const int32_t hid = nseg > 1 ? nheavy++ : -1;
-    if (nseg > 1) hp.heavy.insert(hp.heavy.end(), {r, (int32_t)(hp.units.size() / 4), (int32_t)nseg, 0});
-    for (int64_t s = 0; s < nseg; ++s)
-      hp.units.insert(hp.units.end(),
-                      {r, (int32_t)(b + deg * s / nseg), (int32_t)(b + deg * (s + 1) / nseg), hid});
+    rb.clear();
+    rcl.clear();
+    for (int64_t k = b; k < e; ++k) {
+      const int c = cls(ci[(size_t)k], K);
+      if (rcl.empty() || rcl.back() != c) { rb.push_back(k); rcl.push_back(c); }
+    }
+    if ((int64_t)rb.size() > NX) {  // columns not sorted: one run
+      rb.assign(1, b);
+      rcl.assign(1, cls(r, M));
+    }
+    rb.push_back(e);
+    const int64_t nruns = (int64_t)rcl.size();
+    int64_t sr = seg, nseg = 0;
+    for (;;) {
+      nseg = 0;
+      for (int64_t i = 0; i < nruns; ++i) nseg += (rb[(size_t)i + 1] - rb[(size_t)i] + sr - 1) / sr;
+      if (nseg <= kMaxSeg) break;
+      sr *= 2;
+    }
+    if (nseg == 1) {
+      hq[(size_t)rcl[0]].insert(hq[(size_t)rcl[0]].end(), {r, (int32_t)b, (int32_t)e, -1});
+      continue;
+    }
+    const int32_t hid = nheavy++;
+    hp.heavy.insert(hp.heavy.end(), {r, (int32_t)nslots, (int32_t)nseg, 0});
+    int32_t sgi = 0;
+    for (int64_t i = 0; i < nruns; ++i) {
+      const int64_t pb = rb[(size_t)i], len = rb[(size_t)i + 1] - pb, np = (len + sr - 1) / sr;
+      std::vector<int32_t>& q = hq[(size_t)rcl[(size_t)i]];
+      for (int64_t s = 0; s < np; ++s, ++sgi)
+        q.insert(q.end(), {r, (int32_t)(pb + len * s / np), (int32_t)(pb + len * (s + 1) / np), hid * 64 + sgi});
+    }
+    nslots += nseg;
   }
+  // lay out rounds of NX workgroups, workgroup 8k + c taking `per` units of class c
+  // (empty units pad short classes)
+  auto layout = [&](std::vector<std::vector<int32_t>>& qs, int per) {
+    size_t rounds = 0;
+    for (const auto& q : qs) rounds = std::max(rounds, (q.size() / 4 + per - 1) / per);
+    for (size_t k = 0; k < rounds; ++k)
+      for (int c = 0; c < NX; ++c)
+        for (int j = 0; j < per; ++j) {
+          const size_t i = (k * per + j) * 4;
+          if (i < qs[(size_t)c].size())
+            hp.units.insert(hp.units.end(), qs[(size_t)c].begin() + i, qs[(size_t)c].begin() + i + 4);
+          else
+            hp.units.insert(hp.units.end(), {-1, 0, 0, -1});
+        }
+  };
+  layout(hq, hpb);
   const int64_t nh = (int64_t)hp.units.size() / 4;
-  hp.units.insert(hp.units.end(), light.begin(), light.end());
+  layout(lq, sg);
   const int64_t nunits = (int64_t)hp.units.size() / 4;
-  if (nunits >= (int64_t)INT32_MAX) {
-    set_error("gcnk_spmm_plan: %lld row units exceed 2^31", (long long)nunits);
+  if (nunits >= (int64_t)INT32_MAX || nslots >= (int64_t)INT32_MAX || nheavy >= (1 << 25)) {
+    set_error("gcnk_spmm_plan: %lld row units / %lld partial slots exceed the plan's int32 fields",
+              (long long)nunits, (long long)nslots);
     return GCNK_EUNSUP;
   }
   const int32_t h[16] = {kMagic, M,     K,      groups, ipc,  (int32_t)nunits, (int32_t)nh, nheavy,
-                         ntile,  nred, nslabs, ntblk,  any_diag ? 1 : 0, (int32_t)nnz, 0, 0};
+                         ntile,  nred, nslabs, ntblk,  any_diag ? 1 : 0, (int32_t)nnz, (int32_t)nslots, 0};
   std::copy(h, h + 16, hp.hdr);
   return GCNK_OK;
 }
@@ -954,21 +1023,20 @@ using namespace gcnk;
 static unsigned long long* g_stamps = nullptr;
 extern "C" void gcnk_debug_set_stamps(void* buf) { g_stamps = (unsigned long long*)buf; }
 
-// Lane groups sharing one heavy segment: 64/LPR per wavefront, or the 4
-// wavefronts of a workgroup for whole-wavefront groups.
-static int32_t segment_groups(int lpr) { return lpr == 64 ? 4 : 64 / lpr; }
-
-extern "C" int32_t gcnk_spmm_groups(int32_t F, int32_t lanes_hint) { return segment_groups(choose_lpr(F, lanes_hint)); }
+// Lane groups per wavefront (64 / LPR): identifies the launch geometry a plan
+// is laid out for (heavy segments are shared by these groups, or by the 4
+// wavefronts of a workgroup when a group is a whole wavefront).
+extern "C" int32_t gcnk_spmm_groups(int32_t F, int32_t lanes_hint) { return 64 / choose_lpr(F, lanes_hint); }
 
 extern "C" int32_t gcnk_spmm_default_ipc(int32_t M, int64_t nnz, int32_t F, int32_t lanes_hint) {
   (void)M;
   (void)nnz;
   // light-row limit (and each group's share of a heavy segment): four U = 8
   // gather batches per wavefront at 64 lanes (heavy segments of 128 nonzeros
-  // over a workgroup), one batch for narrower groups (sweeps:
-  // profiles/r01_sweep_rows*.log; R8 F = 200: ipc 16 11.1 us, 32 11.3 us;
-  // 20ng-shaped: 32 21.6 us, 64 20.0 us)
-  return choose_lpr(F, lanes_hint) == 64 ? 32 : 8;
+  // over a workgroup), two for narrower groups (sweeps with the XCD-class
+  // layout, profiles/r01_sweep_xcd.log: R8 F = 200 ipc 32 11.2 us, 16 11.3;
+  // 20ng-shaped 32 19.1 us, 64 18.4; R8 F = 8 ipc 16 5.4 us, 8 6.9)
+  return choose_lpr(F, lanes_hint) == 64 ? 32 : 16;
 }
 
 extern "C" int64_t gcnk_spmm_plan_bytes(const int32_t* rowptr, const int32_t* colind, int32_t M, int32_t K,
@@ -1047,7 +1115,7 @@ static int64_t tile_fpad(int32_t F) { return ((int64_t)F + 15) & ~15LL; }
 extern "C" int64_t gcnk_spmm_workspace_bytes(const int32_t* hdr, int32_t F) {
   if (!hdr || hdr[0] != kMagic || F < 0) return GCNK_EARG;
   const int64_t ld = ((int64_t)F + 3) & ~3LL;
-  const int64_t rows = (int64_t)hdr[6] * ld * 4;
+  const int64_t rows = (int64_t)hdr[14] * ld * 4;
   const int64_t slabs = (int64_t)hdr[10] * kRB * tile_fpad(F) * 4;
   return ((rows + 255) & ~255LL) + slabs;
 }
@@ -1085,9 +1153,9 @@ static int spmm_impl(const void* plan, const int32_t* hdr, const float* B, int64
     return GCNK_EARG;
   }
   const int lpr = choose_lpr(F, lanes_hint);
-  if (hdr[3] != segment_groups(lpr)) {
-    set_error("gcnk_spmm_csr_f32: plan built for %d lane groups per segment, this F/lanes uses %d (gcnk_spmm_groups)",
-              hdr[3], segment_groups(lpr));
+  if (hdr[3] != 64 / lpr) {
+    set_error("gcnk_spmm_csr_f32: plan built for %d lane groups per wavefront, this F/lanes uses %d (gcnk_spmm_groups)",
+              hdr[3], 64 / lpr);
     return GCNK_EARG;
   }
   const int64_t need = gcnk_spmm_workspace_bytes(hdr, F);
@@ -1121,7 +1189,7 @@ static int spmm_impl(const void* plan, const int32_t* hdr, const float* B, int64
   const int32_t* p = (const int32_t*)plan;
   const Layout L(hdr);
   const int64_t part_ld = ((int64_t)F + 3) & ~3LL;
-  const int64_t rows_ws = ((int64_t)hdr[6] * part_ld * 4 + 255) & ~255LL;
+  const int64_t rows_ws = ((int64_t)hdr[14] * part_ld * 4 + 255) & ~255LL;
   float* slabs = workspace ? reinterpret_cast<float*>(reinterpret_cast<char*>(workspace) + rows_ws) : nullptr;
   const int64_t slab_ld = tile_fpad(F);
 

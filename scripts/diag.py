@@ -53,6 +53,7 @@ def main():
         "XW1": lambda: ops.spmm(X, W1, out=H),
         "AS1_F200": lambda: ops.spmm(A, S1, out=H),
         "AS1_F200_nodense": lambda: ops.spmm(A, S1, out=H, dense=2.0),
+        "AS1_F200_dense05": lambda: ops.spmm(A, S1, out=H, dense=0.05),
         "AS1_F200_proj": lambda: ops.spmm_proj(A, S1, W2, bias=W2[0].repeat(25), epilogue=2, store_main=False),
         "AS1_F200_proj_H": lambda: ops.spmm_proj(A, S1, W2, bias=W2[0].repeat(25), epilogue=2),
         "AS2_F8": lambda: ops.spmm(A, S2, out=o8),

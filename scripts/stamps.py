@@ -51,10 +51,10 @@ def main():
                 if len(s):
                     summarize(f"{name}:tile_{kind}", (s - t0) / 100.0)
             continue
-        # heavy blocks: one segment per workgroup at 64 lanes (hdr[3] == 4 with F > 64),
-        # 4 per 256-thread workgroup for 8..32 lanes, 1 per one-wave workgroup below
-        lpr = 64 if (hdr[3] == 4 and F > 64) else 64 // hdr[3]
-        nhb = hdr[6] if lpr == 64 else ((hdr[6] + 3) // 4 if lpr >= 8 else hdr[6])
+        # heavy blocks: one unit per workgroup at 64 lanes, 4 per 256-thread workgroup
+        # for 8..32 lanes, 1 per one-wave workgroup below (hdr[3] = 64 / lanes)
+        lpr = 64 // hdr[3]
+        nhb = hdr[6] if lpr == 64 else (hdr[6] // 4 if lpr >= 8 else hdr[6])
         s_all = buf.view(-1, 4).cpu().numpy().astype(np.float64)
         t0 = s_all[s_all[:, 0] > 0, 0].min()
         for kind, rows in (("heavy", s_all[:nhb]), ("light", s_all[nhb:]), ("all", s_all)):

@@ -1,42 +1,95 @@
 """Pure-Python model of the row-unit SpMM schedule (test infrastructure).
 
-Mirrors, step by step, the host unit planning (spmm.hip host_plan, row part)
-and the row kernel's control flow (light units per lane group, heavy segments
-per wavefront with lane groups on interleaved nonzeros, partial slots and the
-last-arriver combine in segment order), so the control logic can be checked on
-CPU against a dense product."""
+Mirrors, step by step, the host unit planning (spmm.hip host_plan, row part:
+light rows, heavy rows cut at XCD column-class boundaries and into segments,
+the class-by-workgroup layout with empty padding units) and the row kernel's
+control flow (light units per lane group, heavy segments shared by lane
+groups, partial slots and the last-arriver combine in segment order), so the
+control logic can be checked on CPU against a dense product."""
 import numpy as np
 
 K_MAX_SEG = 64
+NX = 8
 
 
-def host_plan(rowptr, ipc, groups, tile_rows=()):
-    """-> (units [(row, b, e, hid)], heavy [(row, first unit, nseg)], nh)."""
-    seg = ipc * groups
-    tile = set(tile_rows)
-    heavy_units, light, heavy = [], [], []
-    for r in range(len(rowptr) - 1):
-        if r in tile:
-            continue
-        b, deg = int(rowptr[r]), int(rowptr[r + 1] - rowptr[r])
+def _cls(i, n):
+    return i * NX // n if n > 0 else 0
+
+
+def geometry(groups):
+    lpr = 64 // groups
+    block = 256 if lpr >= 8 else 64
+    wpb, sg = block // 64, block // lpr
+    hpb = 1 if lpr == 64 else wpb
+    seg_groups = wpb if lpr == 64 else groups
+    return hpb, sg, seg_groups
+
+
+def host_plan(rowptr, colind, K, ipc, groups):
+    """-> (units [(row, b, e, w)], heavy [(row, first slot, nseg)], nh, nslots)."""
+    hpb, sg, seg_groups = geometry(groups)
+    seg = ipc * seg_groups
+    M = len(rowptr) - 1
+    hq, lq, heavy = [[] for _ in range(NX)], [[] for _ in range(NX)], []
+    nslots = 0
+    for r in range(M):
+        b, e = int(rowptr[r]), int(rowptr[r + 1])
+        deg = e - b
         if deg <= ipc:
-            light.append((r, b, b + deg, -1))
+            lq[_cls(r, M)].append((r, b, e, -1))
             continue
-        nseg = min((deg + seg - 1) // seg, K_MAX_SEG)
-        hid = len(heavy) if nseg > 1 else -1
-        if nseg > 1:
-            heavy.append((r, len(heavy_units), nseg))
-        for s in range(nseg):
-            heavy_units.append((r, b + deg * s // nseg, b + deg * (s + 1) // nseg, hid))
-    return heavy_units + light, heavy, len(heavy_units)
+        runs = []
+        for k in range(b, e):
+            c = _cls(int(colind[k]), K)
+            if not runs or runs[-1][1] != c:
+                runs.append([k, c])
+        if len(runs) > NX:
+            runs = [[b, _cls(r, M)]]
+        bounds = [x[0] for x in runs] + [e]
+        sr = seg
+        while True:
+            nseg = sum((bounds[i + 1] - bounds[i] + sr - 1) // sr for i in range(len(runs)))
+            if nseg <= K_MAX_SEG:
+                break
+            sr *= 2
+        if nseg == 1:
+            hq[runs[0][1]].append((r, b, e, -1))
+            continue
+        hid = len(heavy)
+        heavy.append((r, nslots, nseg))
+        sgi = 0
+        for i, (pb, c) in enumerate(runs):
+            ln = bounds[i + 1] - pb
+            npc = (ln + sr - 1) // sr
+            for s in range(npc):
+                hq[c].append((r, pb + ln * s // npc, pb + ln * (s + 1) // npc, hid * 64 + sgi))
+                sgi += 1
+        nslots += nseg
+
+    def layout(qs, per):
+        out = []
+        rounds = max((len(q) + per - 1) // per for q in qs)
+        for k in range(rounds):
+            for c in range(NX):
+                for j in range(per):
+                    i = k * per + j
+                    out.append(qs[c][i] if i < len(qs[c]) else (-1, 0, 0, -1))
+        return out
+
+    units = layout(hq, hpb)
+    nh = len(units)
+    units += layout(lq, sg)
+    return units, heavy, nh, nslots
 
 
 def spmm(rowptr, colind, val, B, ipc, groups):
-    """C = A @ B computed the way the row kernel schedules it (float64)."""
-    M = len(rowptr) - 1
-    units, heavy, nh = host_plan(rowptr, ipc, groups)
+    """C = A @ B computed the way the row kernel schedules it (float64), with
+    the per-workgroup XCD class of every unit checked."""
+    M, K = len(rowptr) - 1, B.shape[0]
+    hpb, sg, seg_groups = geometry(groups)
+    units, heavy, nh, nslots = host_plan(rowptr, colind, K, ipc, groups)
     C = np.full((M, B.shape[1]), np.nan)
-    part = np.zeros((nh, B.shape[1]))
+    part = np.zeros((nslots, B.shape[1]))
     arrivals = [0] * len(heavy)
     written = np.zeros(M, np.int64)
 
@@ -46,23 +99,30 @@ def spmm(rowptr, colind, val, B, ipc, groups):
             acc += val[k] * B[colind[k]]
         return acc
 
-    # heavy segments first (grid order), each wavefront's lane groups interleave
-    # nonzeros; arrivals in an arbitrary (here reversed) order
+    # heavy region (workgroup u // hpb); arrivals in an arbitrary (reversed) order
     for u in reversed(range(nh)):
-        r, b, e, hid = units[u]
-        acc = sum(gather(b, e, q, groups) for q in range(groups))
-        if hid < 0:
+        r, b, e, w = units[u]
+        if r < 0:
+            continue
+        c = (u // hpb) % NX
+        assert all(_cls(int(colind[k]), K) == c for k in range(b, e)) or w < 0 or _cls(r, M) == c
+        acc = sum(gather(b, e, q, seg_groups) for q in range(seg_groups))
+        if w < 0:
             C[r] = acc
             written[r] += 1
             continue
-        part[u] = acc
-        arrivals[hid] += 1
+        hid, sgi = w >> 6, w & 63
         hr, first, nseg = heavy[hid]
+        part[first + sgi] = acc
+        arrivals[hid] += 1
         if arrivals[hid] == nseg:       # last arriver: slots in segment order
             C[hr] = sum(part[first + s] for s in range(nseg))
             written[hr] += 1
     for u in range(nh, len(units)):
         r, b, e, _ = units[u]
+        if r < 0:
+            continue
+        assert ((nh // hpb + (u - nh) // sg) % NX) == _cls(r, M), "light unit in its XCD class"
         C[r] = gather(b, e, 0, 1)
         written[r] += 1
     assert np.all(written == 1), "every row is stored exactly once"

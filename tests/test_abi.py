@@ -32,8 +32,8 @@ MAGIC = 0x474E4B35  # plan header word 0 ("GNK5")
 
 
 def _hdr(M=10, K=10, groups=1, ipc=32, nslots=0, nslabs=0):
-    # magic M K groups ipc nunits nhunits(slots) nheavy ntile nred nslabs ntblk has_diag nnz 0 0
-    h = (ctypes.c_int32 * 16)(MAGIC, M, K, groups, ipc, 0, nslots, 0, 0, 0, nslabs, 0, 0, 0, 0, 0)
+    # magic M K groups ipc nunits nhunits nheavy ntile nred nslabs ntblk has_diag nnz nslots 0
+    h = (ctypes.c_int32 * 16)(MAGIC, M, K, groups, ipc, 0, 0, 0, 0, 0, nslabs, 0, 0, 0, nslots, 0)
     return ctypes.cast(h, ctypes.c_void_p), h
 
 
@@ -67,13 +67,13 @@ def test_argument_validation_without_gpu():
     rc = lib.gcnk_spmm_csr_f32(ctypes.c_void_p(16), ctypes.cast(bad, ctypes.c_void_p), ctypes.c_void_p(16), 8, 8,
                                ctypes.c_void_p(16), 8, None, 0, None, 0, 1.0, 1.0, 0, 0, None, 0, 0, None)
     assert rc == _lib.EARG and b"not a gcnk plan" in lib.gcnk_last_error()
-    # plan/groups mismatch is refused before any launch (F=200 uses 4 lane groups per wave)
+    # plan/groups mismatch is refused before any launch (F=200 uses 1 lane group per wave)
     h, _keep = _hdr(groups=7)
     rc = lib.gcnk_spmm_csr_f32(ctypes.c_void_p(16), h, ctypes.c_void_p(16), 200, 200,
                                ctypes.c_void_p(16), 200, None, 0, None, 0, 1.0, 1.0, 0, 0, None, 0, 0, None)
     assert rc == _lib.EARG and b"groups" in lib.gcnk_last_error()
     # workspace too small for the plan's partial slots
-    h, _keep = _hdr(groups=4, nslots=3)
+    h, _keep = _hdr(groups=1, nslots=3)
     rc = lib.gcnk_spmm_csr_f32(ctypes.c_void_p(16), h, ctypes.c_void_p(16), 200, 200,
                                ctypes.c_void_p(16), 200, None, 0, None, 0, 1.0, 1.0, 0, 0, None, 0, 0, None)
     assert rc == _lib.EARG and b"workspace" in lib.gcnk_last_error()
@@ -87,8 +87,8 @@ def test_argument_validation_without_gpu():
 
 def test_plan_and_workspace_sizes():
     lib = _lib.load()
-    # lane groups sharing a heavy segment: 64 / lanes per group, or 4 wavefronts at 64 lanes
-    assert lib.gcnk_spmm_groups(200, 0) == 4 and lib.gcnk_spmm_groups(8, 0) == 32 and lib.gcnk_spmm_groups(64, 0) == 4
+    # lane groups per wavefront = 64 / lanes per row group
+    assert lib.gcnk_spmm_groups(200, 0) == 1 and lib.gcnk_spmm_groups(8, 0) == 32 and lib.gcnk_spmm_groups(64, 0) == 4
     assert lib.gcnk_spmm_groups(7, 0) == 8 and lib.gcnk_spmm_groups(200, 16) == 4 and lib.gcnk_spmm_groups(200, 32) == 2
     h, _keep = _hdr(nslots=10, nslabs=3)
     assert lib.gcnk_spmm_workspace_bytes(h, 198) == 8192 + 3 * 64 * 208 * 4

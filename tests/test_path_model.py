@@ -22,15 +22,18 @@ def test_model_on_r8(r8, groups, ipc):
     np.testing.assert_allclose(C, csr_ref.spmm_csr(rp, ci, v, B), atol=1e-12)
 
 
-def test_r8_plan_shape():
-    """R8-shaped degrees: document rows (5 nonzeros) are light units, the 50
-    topic rows (hundreds to ~1.8k) split into <= 64 segments each."""
-    deg = np.concatenate([np.full(7674, 5), np.linspace(200, 1807, 50).astype(int)])
-    rp = np.concatenate([[0], np.cumsum(deg)])
-    units, heavy, nh = path_model.host_plan(rp, 32, 1)
-    assert len(units) - nh == 7674 and len(heavy) == 50
+def test_r8_plan_shape(r8):
+    """R8: document rows (5 nonzeros) are light units, the 50 topic rows (up to
+    ~1.8k nonzeros over all document columns) split at the 8 column classes
+    into <= 64 segments each; padding stays small."""
+    rp, ci, v = csr_ref.coo_to_csr(r8["adj"]._indices()[0].numpy(), r8["adj"]._indices()[1].numpy(),
+                                   r8["adj"]._values().numpy(), (r8["nodes"], r8["nodes"]))
+    units, heavy, nh, nslots = path_model.host_plan(rp, ci, r8["nodes"], 32, 1)
+    light = [x for x in units[nh:] if x[0] >= 0]
+    assert len(light) == 7674 and len(heavy) == 50
     assert all(1 < h[2] <= path_model.K_MAX_SEG for h in heavy)
-    assert all(units[u][3] >= 0 for u in range(nh))
+    assert nslots == sum(h[2] for h in heavy)
+    assert sum(1 for x in units if x[0] < 0) < 0.05 * len(units)
 
 
 @pytest.mark.parametrize("seed", range(6))

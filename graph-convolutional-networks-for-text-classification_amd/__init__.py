@@ -7,11 +7,11 @@ from . import _lib
 from .layer import GCN, GraphConvolution
 from .ops import GCNFn, GraphConvFn, Operand, colsum, gemm, spmm
 from .parallel import ColumnShardedSpMM, shard_bounds, sharded_gcn_forward
-from .sparse import CSR, as_csr, from_arrays, from_torch
+from .sparse import CSR, as_csr, from_arrays, from_torch, preprocess_adj
 
 __all__ = [
     "GCN", "GraphConvolution", "GCNFn", "GraphConvFn", "Operand", "CSR",
-    "as_csr", "from_arrays", "from_torch", "spmm", "gemm", "colsum",
+    "as_csr", "from_arrays", "from_torch", "preprocess_adj", "spmm", "gemm", "colsum",
     "ColumnShardedSpMM", "shard_bounds", "sharded_gcn_forward",
 ]
 

@@ -171,6 +171,35 @@ def from_arrays(rowptr, colind, val, shape, device):
     return CSR(rp, ci, v, shape)
 
 
+def preprocess_adj(adj):
+    """Â = D^-1/2 (A + I) D^-1/2 on the device (gcnk_sym_normalize): the
+    reference's ``utils.preprocess_adj(adj, is_sparse=True)`` (utils.py:185-213)
+    for an adjacency that is already a GPU tensor, with the reference's
+    float64 arithmetic and one rounding to fp32, so the values are bit-for-bit
+    what the host path produces.  ``adj``: symmetric A as a torch sparse
+    tensor (any COO order, duplicates summed) or a CSR on the GPU.  Returns the
+    CSR of Â (usable directly as ``adj`` of GCN.forward)."""
+    a = adj if isinstance(adj, CSR) else from_torch(adj)
+    n, k = a.shape
+    if n != k:
+        raise RuntimeError(f"preprocess_adj: adjacency must be square, got {a.shape}")
+    lib = _lib.load()
+    dev = a.device
+    rp = torch.empty(n + 1, dtype=torch.int32, device=dev)
+    ci = torch.empty(a.nnz + n, dtype=torch.int32, device=dev)
+    v = torch.empty(a.nnz + n, dtype=torch.float32, device=dev)
+    wsb = int(lib.gcnk_sym_normalize_workspace_bytes(n, a.nnz))
+    if wsb < 0:
+        _lib.check(wsb, "gcnk_sym_normalize_workspace_bytes")
+    ws = torch.empty(max(wsb, 1), dtype=torch.uint8, device=dev)
+    with torch.cuda.device(dev):
+        _lib.check(lib.gcnk_sym_normalize(a.rowptr.data_ptr(), a.colind.data_ptr(), a.val.data_ptr(), n, a.nnz,
+                                          rp.data_ptr(), ci.data_ptr(), v.data_ptr(), ws.data_ptr(), wsb,
+                                          _stream_ptr(dev)), "gcnk_sym_normalize")
+    nnz = int(rp[n])   # one-time setup sync
+    return CSR(rp, ci[:nnz], v[:nnz], (n, n))
+
+
 class _Cache:
     """LRU of torch sparse tensor -> CSR, keyed by storage identity + version.
 

@@ -18,6 +18,7 @@
  *                  sum over rows of g  (bias grad)          -> gcnk_colsum_f32
  *   utils.py:196-203 / trainer.py:226-238 (COO tensors handed to th.spmm)
  *                                                           -> gcnk_spmm_plan_build (one-time schedule)
+ *   utils.py:185-213 preprocess_adj / normalize_adj          -> gcnk_sym_normalize (device, bit-exact)
  *
  * Conventions
  *   - All pointers are DEVICE pointers unless a parameter says "host".
@@ -184,6 +185,22 @@ int64_t gcnk_csr_transpose_workspace_bytes(int32_t M, int32_t K, int64_t nnz);
 int gcnk_csr_transpose(const int32_t* rowptr, const int32_t* colind, const float* val,
                        int32_t M, int32_t K, int64_t nnz,
                        int32_t* rowptr_t, int32_t* colind_t, float* val_t,
+                       void* workspace, int64_t workspace_bytes, void* stream);
+
+/* ---------------------------------------------------------------------------
+ * Device-side adjacency preparation (utils.py:185-213, preprocess_adj /
+ * normalize_adj, which the reference runs on the host with scipy):
+ *   A_hat = D^-1/2 (A + I) D^-1/2,  D = rowsum(A + I)
+ * with the reference's arithmetic (A + I and D in float64, d = rowsum^-0.5,
+ * inf -> 0, value = (d[r] * a) * d[c] rounded once to fp32), so the values are
+ * bit-for-bit the reference's.  Input: n x n CSR with sorted, duplicate-free
+ * columns per row (a symmetric A, as trainer.py:148 makes it).  Output CSR
+ * arrays have capacity nnz + n; rowptr_out[n] is the output nnz (read it
+ * after the stream completes).  Workspace: gcnk_sym_normalize_workspace_bytes.
+ * ------------------------------------------------------------------------- */
+int64_t gcnk_sym_normalize_workspace_bytes(int32_t n, int64_t nnz);
+int gcnk_sym_normalize(const int32_t* rowptr, const int32_t* colind, const float* val, int32_t n, int64_t nnz,
+                       int32_t* rowptr_out, int32_t* colind_out, float* val_out,
                        void* workspace, int64_t workspace_bytes, void* stream);
 
 /* Debug only: when `buf` is non-null every later SpMM main-kernel launch

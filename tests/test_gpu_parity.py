@@ -437,3 +437,53 @@ def test_column_sharded_spmm_single_rank_on_gpu(big_graph):
     full = op(op.shard(B))
     assert full.shape == (a.shape[0], F)
     assert torch.equal(full, spmm(a, B))
+
+
+# ------------------------------------------------------------------------------ device adjacency preparation
+
+def test_preprocess_adj_on_device_bit_exact_r8(r8):
+    """gcnk_sym_normalize on R8's raw symmetric A (the adjacency trainer.py:148
+    hands to utils.preprocess_adj) reproduces the reference's normalised
+    values bit for bit, in CSR order."""
+    from graph_convolutional_networks_for_text_classification_amd import preprocess_adj
+    n = r8["nodes"]
+    A = torch.sparse_coo_tensor(torch.from_numpy(np.vstack([r8["a_rows"], r8["a_cols"]]).astype(np.int64)),
+                                torch.from_numpy(np.asarray(r8["a_vals"], np.float32)), (n, n)).to(DEV)
+    ah = preprocess_adj(A)
+    ref = r8["adj"].coalesce()
+    assert np.array_equal(ah.rowptr.cpu().numpy(), np.concatenate([[0], np.cumsum(np.bincount(
+        ref.indices()[0].numpy(), minlength=n))]))
+    assert np.array_equal(ah.colind.cpu().numpy(), ref.indices()[1].numpy())
+    assert np.array_equal(ah.val.cpu().numpy().view(np.uint32), ref.values().numpy().view(np.uint32))
+    # and it drives the forward directly
+    torch.manual_seed(0)
+    m = GCN(nfeat=r8["nfeat"], nhid=200, nclass=r8["nclass"], dropout=0.5).to(DEV).eval()
+    with torch.no_grad():
+        a = m(r8["features"].to(DEV), ah)
+        b = m(r8["features"].to(DEV), r8["adj"].to(DEV))
+    assert torch.equal(a, b)
+
+
+def test_preprocess_adj_known_answers(golden_meta):
+    """The reference's own preprocess_adj outputs on tiny graphs with isolated
+    nodes and explicit diagonal entries (tests/golden known-answer cases)."""
+    from graph_convolutional_networks_for_text_classification_amd import preprocess_adj
+    for case in golden_meta["tiny_cases"]:
+        n = case["n"]
+        A = torch.sparse_coo_tensor(torch.tensor([case["A_rows"], case["A_cols"]], dtype=torch.int64),
+                                    torch.tensor(case["A_vals"], dtype=torch.float32), (n, n)).to(DEV)
+        ah = preprocess_adj(A)
+        rows = np.repeat(np.arange(n), np.diff(ah.rowptr.cpu().numpy()))
+        got = {(int(r), int(c)): v for r, c, v in zip(rows, ah.colind.cpu().numpy(), ah.val.cpu().numpy())}
+        want = {(int(r), int(c)): np.float32(v) for r, c, v in zip(case["adj_rows"], case["adj_cols"],
+                                                                   case["adj_vals"])}
+        assert got.keys() == want.keys(), case["name"]
+        assert all(got[k].view(np.uint32) == want[k].view(np.uint32) for k in want), case["name"]
+    # an explicit self loop gets + 1 (A + I) and stays one entry
+    A = torch.sparse_coo_tensor(torch.tensor([[0, 0, 1], [0, 1, 0]]), torch.tensor([2.0, 1.0, 1.0]), (3, 3)).to(DEV)
+    ah = preprocess_adj(A)
+    assert ah.nnz == 5 and ah.rowptr.cpu().tolist() == [0, 2, 4, 5]
+    assert ah.colind.cpu().tolist() == [0, 1, 0, 1, 2]
+    d = np.array([4.0, 2.0, 1.0]) ** -0.5
+    want = np.float32([(d[0] * 3.0) * d[0], (d[0] * 1.0) * d[1], (d[1] * 1.0) * d[0], (d[1] * 1.0) * d[1], 1.0])
+    assert np.array_equal(ah.val.cpu().numpy(), want)

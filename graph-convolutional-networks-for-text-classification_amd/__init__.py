@@ -3,7 +3,7 @@
 Drop-in for the reference's ``layer.py`` (GraphConvolution, GCN) — see
 DESIGN.md for the path, the boundary and the kernels.
 """
-from . import _lib
+from . import _lib, metrics
 from .layer import GCN, GraphConvolution
 from .ops import GCNFn, GraphConvFn, Operand, colsum, gemm, spmm
 from .parallel import ColumnShardedSpMM, shard_bounds, sharded_gcn_forward

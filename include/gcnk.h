@@ -19,6 +19,7 @@
  *   utils.py:196-203 / trainer.py:226-238 (COO tensors handed to th.spmm)
  *                                                           -> gcnk_spmm_plan_build (one-time schedule)
  *   utils.py:185-213 preprocess_adj / normalize_adj          -> gcnk_sym_normalize (device, bit-exact)
+ *   utils.py:25-109  accuracy / macro_f1 counts              -> gcnk_class_stats (one launch, no per-class syncs)
  *
  * Conventions
  *   - All pointers are DEVICE pointers unless a parameter says "host".
@@ -202,6 +203,18 @@ int64_t gcnk_sym_normalize_workspace_bytes(int32_t n, int64_t nnz);
 int gcnk_sym_normalize(const int32_t* rowptr, const int32_t* colind, const float* val, int32_t n, int64_t nnz,
                        int32_t* rowptr_out, int32_t* colind_out, float* val_out,
                        void* workspace, int64_t workspace_bytes, void* stream);
+
+/* ---------------------------------------------------------------------------
+ * Evaluation counts in one launch (utils.py:25-109 accuracy / macro_f1 issue
+ * 3 * nclass + 1 .item() syncs): for the n scored rows (row = idx[i], or i
+ * when idx is NULL) of logits [rows x nclass] (leading dimension ld) with
+ * int64 labels `target` (indexed by row), predicted class = first maximal
+ * logit (NaN counts as maximal: th.max semantics); counts[3 * nclass + 1]
+ * (zeroed by the call) = TP[nclass] | FP[nclass] | FN[nclass] | correct.
+ * nclass <= 1024.  Integer atomics: exact.
+ * ------------------------------------------------------------------------- */
+int gcnk_class_stats(const float* logits, int64_t ld, const int64_t* target, const int64_t* idx, int64_t n,
+                     int32_t nclass, int32_t* counts, void* stream);
 
 /* Debug only: when `buf` is non-null every later SpMM main-kernel launch
  * writes 4 x uint64 s_memrealtime stamps (100 MHz) per workgroup to it

@@ -487,3 +487,47 @@ def test_preprocess_adj_known_answers(golden_meta):
     d = np.array([4.0, 2.0, 1.0]) ** -0.5
     want = np.float32([(d[0] * 3.0) * d[0], (d[0] * 1.0) * d[1], (d[1] * 1.0) * d[0], (d[1] * 1.0) * d[1], 1.0])
     assert np.array_equal(ah.val.cpu().numpy(), want)
+
+
+# ------------------------------------------------------------------------------ evaluation metrics
+
+@pytest.mark.parametrize("nclass", [8, 20])
+def test_metrics_match_reference_restatement(nclass):
+    """metrics.evaluate / accuracy / macro_f1 (one launch, one copy) equal the
+    reference's utils.py:25-109 arithmetic (oracle restatement) on logits with
+    exact ties and NaNs, with and without a row subset, with num_classes given
+    and inferred from the targets."""
+    from graph_convolutional_networks_for_text_classification_amd import metrics
+    g = torch.Generator().manual_seed(nclass)
+    rows = 5000
+    logits = torch.randn(rows, nclass, generator=g)
+    logits[::97, 3] = logits[::97, 1]                  # ties: first maximum wins
+    logits[::97, 1] = logits[::97].max(1).values + 1
+    logits[::97, 3] = logits[::97, 1]
+    logits[5::503, 2] = float("nan")                   # NaN is maximal (th.max)
+    targ = torch.randint(0, nclass - 1, (rows,), generator=g)   # the last class never a target
+    idx = torch.randperm(rows, generator=g)[:1700]
+    for sub in (None, idx):
+        p_c = logits if sub is None else logits[sub]
+        t_c = targ if sub is None else targ[sub]
+        want_acc = gcn_ref.accuracy(p_c, t_c)
+        want = gcn_ref.macro_f1(p_c, t_c, nclass)
+        acc, f1, p, r = metrics.evaluate(logits.to(DEV), targ.to(DEV), None if sub is None else sub.to(DEV),
+                                         num_classes=nclass)
+        assert acc == want_acc
+        assert (f1, p, r) == pytest.approx(want, rel=0, abs=0)
+    # num_classes=None: only the classes present in the targets (utils.py:53-54)
+    pred = logits.argmax(1)
+    present = sorted(set(targ.tolist()))
+    tp = np.array([((pred == i) & (targ == i)).sum().item() for i in present])
+    fp = np.array([((pred == i) & (targ != i)).sum().item() for i in present])
+    fn = np.array([((pred != i) & (targ == i)).sum().item() for i in present])
+    with np.errstate(divide="ignore", invalid="ignore"):
+        pr = tp / (tp + fp)
+        pr[np.isnan(pr)] = 0
+        rc = tp / (tp + fn)
+        rc[np.isnan(rc)] = 0
+    pm, rm = np.mean(pr), np.mean(rc)
+    f1, p, r = metrics.macro_f1(logits.to(DEV), targ.to(DEV))
+    assert (f1, p, r) == (2 * pm * rm / (pm + rm), pm, rm)
+    assert metrics.accuracy(logits.to(DEV), targ.to(DEV)) == gcn_ref.accuracy(logits, targ)

@@ -118,3 +118,28 @@ def uniform_random_csr(n, nnz, seed=0, device="cpu"):
     rowptr = torch.zeros(n + 1, dtype=torch.int64)
     rowptr[1:] = torch.cumsum(torch.bincount(idx[0], minlength=n), 0)
     return rowptr.to(torch.int32).to(device), idx[1].to(torch.int32).to(device), t.values().to(device)
+
+
+def load_edgelist(path, device=None):
+    """The graph file the reference's builder writes (build_graph.py:199,
+    "u v weight" lines) -> the symmetric float32 adjacency A that
+    trainer.py:98-148 builds from it, as int32 CSR arrays (native loader,
+    gcnk_edgelist_*; no networkx).  Returns (rowptr, colind, val) numpy arrays,
+    or a device CSR when ``device`` is given (feed it to
+    sparse.preprocess_adj for Â)."""
+    import ctypes
+
+    from . import _lib
+    lib = _lib.load()
+    n, nnz = ctypes.c_int64(), ctypes.c_int64()
+    bpath = str(path).encode()
+    _lib.check(lib.gcnk_edgelist_size(bpath, ctypes.byref(n), ctypes.byref(nnz)), "gcnk_edgelist_size")
+    rp = np.empty(n.value + 1, np.int32)
+    ci = np.empty(nnz.value, np.int32)
+    v = np.empty(nnz.value, np.float32)
+    _lib.check(lib.gcnk_edgelist_csr(bpath, n.value, nnz.value, rp.ctypes.data, ci.ctypes.data, v.ctypes.data),
+               "gcnk_edgelist_csr")
+    if device is None:
+        return rp, ci, v
+    from .sparse import from_arrays
+    return from_arrays(rp, ci, v, (n.value, n.value), device)

@@ -20,6 +20,7 @@
  *                                                           -> gcnk_spmm_plan_build (one-time schedule)
  *   utils.py:185-213 preprocess_adj / normalize_adj          -> gcnk_sym_normalize (device, bit-exact)
  *   utils.py:25-109  accuracy / macro_f1 counts              -> gcnk_class_stats (one launch, no per-class syncs)
+ *   trainer.py:98-148 edge list -> symmetric adjacency        -> gcnk_edgelist_size / _csr (host, no networkx)
  *
  * Conventions
  *   - All pointers are DEVICE pointers unless a parameter says "host".
@@ -215,6 +216,18 @@ int gcnk_sym_normalize(const int32_t* rowptr, const int32_t* colind, const float
  * ------------------------------------------------------------------------- */
 int gcnk_class_stats(const float* logits, int64_t ld, const int64_t* target, const int64_t* idx, int64_t n,
                      int32_t nclass, int32_t* counts, void* stream);
+
+/* ---------------------------------------------------------------------------
+ * Weighted edge-list loader (HOST pointers; no device work): the graph file
+ * build_graph.py:199 writes (nx.write_weighted_edgelist: "u v weight" lines,
+ * integer node ids) -> the symmetric float32 adjacency trainer.py:98-148
+ * builds from it, as an int32 CSR with sorted, duplicate-free columns
+ * (a repeated edge keeps its last weight; ids must be 0..n-1).
+ * gcnk_edgelist_size gives n and nnz; gcnk_edgelist_csr fills host buffers
+ * rowptr[n + 1], colind[nnz], val[nnz].
+ * ------------------------------------------------------------------------- */
+int gcnk_edgelist_size(const char* path, int64_t* n_nodes, int64_t* nnz);
+int gcnk_edgelist_csr(const char* path, int64_t n_nodes, int64_t nnz, int32_t* rowptr, int32_t* colind, float* val);
 
 /* Debug only: when `buf` is non-null every later SpMM main-kernel launch
  * writes 4 x uint64 s_memrealtime stamps (100 MHz) per workgroup to it

@@ -284,6 +284,42 @@ __device__ __forceinline__ void gather_rows(const int2* __restrict__ items, int3
   }
 }
 
+// Whole-wavefront groups (LPR == 64; b, e, q wave-uniform): the same sum, but
+// the items come in with ONE vector load per 64 of them (lane l holds item
+// b + q + S*l) and are broadcast with v_readlane, so a batch of U gathers
+// waits for one latency instead of an item load and then the gathers (a heavy
+// segment's 4 batches: 5 latencies instead of 8).
+template <int VEC, int U, int S>
+__device__ __forceinline__ void gather_rows_wave(const int2* __restrict__ items, int32_t b, int32_t e, int q,
+                                                 const float* __restrict__ B, int64_t ldb, int64_t colv, bool colok,
+                                                 typename Vec<VEC>::T& acc) {
+  using V = Vec<VEC>;
+  using T = typename V::T;
+  const int lane = threadIdx.x & 63;
+  for (int32_t base = b + q; base < e; base += 64 * S) {
+    const int32_t k = base + S * lane;
+    const int2 mine = k < e ? items[k] : make_int2(-1, 0);
+    const int32_t cnt = min(64, (e - base + S - 1) / S);  // wave-uniform
+    for (int32_t j0 = 0; j0 < cnt; j0 += U) {
+      T g[U];
+      float a[U];
+#pragma unroll
+      for (int j = 0; j < U; ++j) {
+        g[j] = V::zero();
+        a[j] = 0.f;
+        if (j0 + j < cnt) {
+          const int32_t c = __builtin_amdgcn_readlane(mine.x, j0 + j);
+          a[j] = __int_as_float(__builtin_amdgcn_readlane(mine.y, j0 + j));
+          if (colok) g[j] = V::load(B + (int64_t)c * ldb + colv);
+        }
+      }
+#pragma unroll
+      for (int j = 0; j < U; ++j)
+        if (j0 + j < cnt) V::fma(acc, a[j], g[j]);
+    }
+  }
+}
+
 // Sum over the 64/LPR lane groups of a wave (xor butterfly: every lane ends
 // with bitwise the same sum, since each level adds the same two operands).
 template <int LPR, typename T>
@@ -341,7 +377,8 @@ spmm_row_kernel(RowPlan rp, int32_t nhb, const float* __restrict__ B, int64_t ld
     const int4 un = rp.units[u];
     if (un.x < 0) return;  // padding of the XCD-class layout
     stamp(epi, 1);
-    gather_rows<VEC, U, 1>(rp.items, un.y, un.z, 0, B, ldb, colv, colok, acc);
+    if constexpr (LPR == 64) gather_rows_wave<VEC, U, 1>(rp.items, un.y, un.z, 0, B, ldb, colv, colok, acc);
+    else gather_rows<VEC, U, 1>(rp.items, un.y, un.z, 0, B, ldb, colv, colok, acc);
     stamp(epi, 2);
     finish_row<LPR, VEC, NP>(acc, un.x, colv, colok, bv, lg, C, ldc, epi, store_main, proj, pa);
     stamp(epi, 3);
@@ -365,7 +402,8 @@ spmm_row_kernel(RowPlan rp, int32_t nhb, const float* __restrict__ B, int64_t ld
   const int4 un = rp.units[u];
   if (un.x < 0) return;           // padding of the XCD-class layout
   stamp(epi, 1);
-  gather_rows<VEC, U, GS>(rp.items, un.y, un.z, q, B, ldb, colv, colok, acc);
+  if constexpr (LPR == 64) gather_rows_wave<VEC, U, GS>(rp.items, un.y, un.z, q, B, ldb, colv, colok, acc);
+  else gather_rows<VEC, U, GS>(rp.items, un.y, un.z, q, B, ldb, colv, colok, acc);
   if constexpr (WG) {
     if (w > 0) s_red[w][lane] = acc;
     __syncthreads();
@@ -929,6 +967,9 @@ int host_plan(const int32_t* rowptr_dev, const int32_t* colind_dev, const float*
   const int block = lpr >= 8 ? 256 : 64, wpb = block / 64, sg = block / lpr;
   const int hpb = lpr == 64 ? 1 : wpb;                     // heavy units per workgroup
   const int64_t seg = (int64_t)ipc * (lpr == 64 ? wpb : groups);  // nonzeros per heavy segment
+  // light-row limit: 2 * ipc for whole-wavefront groups (a light row is walked by
+  // one wavefront; a heavy one by a 4-wavefront workgroup), ipc otherwise
+  const int64_t light_max = lpr == 64 ? 2 * (int64_t)ipc : ipc;
   // XCD classes.  Workgroups b and b + 8 land on one XCD (round-robin dispatch;
   // speed only, never correctness), so every unit of workgroup b is given
   // class b % 8: a light row by its row index, a heavy segment by the column
@@ -944,22 +985,26 @@ int host_plan(const int32_t* rowptr_dev, const int32_t* colind_dev, const float*
   hp.units.clear();
   hp.heavy.clear();
   std::vector<int64_t> rb, rcl;  // runs of one column class: start, class
+  int64_t rr_class = 0;
   for (int32_t r = 0; r < M; ++r) {
     if (tile_row[(size_t)r]) continue;
     const int64_t b = rp[r], e = rp[r + 1], deg = e - b;
-    if (deg <= ipc) {
+    if (deg <= light_max) {
       lq[(size_t)cls(r, M)].insert(lq[(size_t)cls(r, M)].end(), {r, (int32_t)b, (int32_t)e, -1});
       continue;
     }
     rb.clear();
     rcl.clear();
-    for (int64_t k = b; k < e; ++k) {
-      const int c = cls(ci[(size_t)k], K);
-      if (rcl.empty() || rcl.back() != c) { rb.push_back(k); rcl.push_back(c); }
-    }
-    if ((int64_t)rb.size() > NX) {  // columns not sorted: one run
-      rb.assign(1, b);
-      rcl.assign(1, cls(r, M));
+    // cut at column-class boundaries only when the runs average half a segment or
+    // more (a 20-nonzero row must not become 8 tiny segments)
+    if (deg * 2 >= seg * NX)
+      for (int64_t k = b; k < e; ++k) {
+        const int c = cls(ci[(size_t)k], K);
+        if (rcl.empty() || rcl.back() != c) { rb.push_back(k); rcl.push_back(c); }
+      }
+    if (rb.empty() || (int64_t)rb.size() > NX) {  // short row, or columns not sorted: one run,
+      rb.assign(1, b);                              // classes dealt round-robin (balance)
+      rcl.assign(1, (int64_t)(rr_class++ % NX));
     }
     rb.push_back(e);
     const int64_t nruns = (int64_t)rcl.size();
@@ -1031,12 +1076,13 @@ extern "C" int32_t gcnk_spmm_groups(int32_t F, int32_t lanes_hint) { return 64 /
 extern "C" int32_t gcnk_spmm_default_ipc(int32_t M, int64_t nnz, int32_t F, int32_t lanes_hint) {
   (void)M;
   (void)nnz;
-  // light-row limit (and each group's share of a heavy segment): four U = 8
-  // gather batches per wavefront at 64 lanes (heavy segments of 128 nonzeros
-  // over a workgroup), two for narrower groups (sweeps with the XCD-class
-  // layout, profiles/r01_sweep_xcd.log: R8 F = 200 ipc 32 11.2 us, 16 11.3;
-  // 20ng-shaped 32 19.1 us, 64 18.4; R8 F = 8 ipc 16 5.4 us, 8 6.9)
-  return choose_lpr(F, lanes_hint) == 64 ? 32 : 16;
+  // each lane group's share of a heavy segment (the light-row limit is 2 * ipc
+  // at 64 lanes, ipc below): two U = 8 gather batches per wavefront at 64 lanes
+  // (heavy segments of 64 nonzeros over a 4-wavefront workgroup), one for
+  // narrow groups.  Sweeps (profiles/r01_sweep_final.log): R8 F = 200 ipc 16
+  // 10.4 us, 32 11.7, 8 14.4; 20ng-shaped 16 18.8, 32 17.2; 1M/20M F = 256
+  // 16 3.33 ms; R8 F = 8 ipc 8 5.1 us, 16 5.7.
+  return choose_lpr(F, lanes_hint) == 64 ? 16 : 8;
 }
 
 extern "C" int64_t gcnk_spmm_plan_bytes(const int32_t* rowptr, const int32_t* colind, int32_t M, int32_t K,

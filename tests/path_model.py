@@ -29,22 +29,26 @@ def host_plan(rowptr, colind, K, ipc, groups):
     """-> (units [(row, b, e, w)], heavy [(row, first slot, nseg)], nh, nslots)."""
     hpb, sg, seg_groups = geometry(groups)
     seg = ipc * seg_groups
+    light_max = 2 * ipc if hpb == 1 else ipc
     M = len(rowptr) - 1
     hq, lq, heavy = [[] for _ in range(NX)], [[] for _ in range(NX)], []
     nslots = 0
+    rr_class = 0
     for r in range(M):
         b, e = int(rowptr[r]), int(rowptr[r + 1])
         deg = e - b
-        if deg <= ipc:
+        if deg <= light_max:
             lq[_cls(r, M)].append((r, b, e, -1))
             continue
         runs = []
-        for k in range(b, e):
-            c = _cls(int(colind[k]), K)
-            if not runs or runs[-1][1] != c:
-                runs.append([k, c])
-        if len(runs) > NX:
-            runs = [[b, _cls(r, M)]]
+        if deg * 2 >= seg * NX:
+            for k in range(b, e):
+                c = _cls(int(colind[k]), K)
+                if not runs or runs[-1][1] != c:
+                    runs.append([k, c])
+        if not runs or len(runs) > NX:
+            runs = [[b, rr_class % NX]]
+            rr_class += 1
         bounds = [x[0] for x in runs] + [e]
         sr = seg
         while True:
@@ -104,8 +108,6 @@ def spmm(rowptr, colind, val, B, ipc, groups):
         r, b, e, w = units[u]
         if r < 0:
             continue
-        c = (u // hpb) % NX
-        assert all(_cls(int(colind[k]), K) == c for k in range(b, e)) or w < 0 or _cls(r, M) == c
         acc = sum(gather(b, e, q, seg_groups) for q in range(seg_groups))
         if w < 0:
             C[r] = acc

@@ -505,6 +505,22 @@ spmm_tile_kernel(const int4* __restrict__ tdesc, const int32_t* __restrict__ tco
   const int64_t col0 = (int64_t)blockIdx.y * (NT * 16);  // this workgroup's column slice
 
   if (tid < kKC) s_cols[tid] = tcols[item * kKC + tid];
+  // output rows, their extracted diagonal and the bias: fetched now (their
+  // latency hides behind the staging) and parked in LDS for the write-out
+  constexpr int CWP = NT * 16;
+  __shared__ int32_t s_rows[kRB];
+  __shared__ float s_dv[kRB];
+  __shared__ __attribute__((aligned(16))) float s_bias[CWP];
+  const bool single = d.z < 0;
+  if (tid < kRB) {
+    const int32_t r = tid < d.y ? trows[(int64_t)d.x * kRB + tid] : -1;
+    s_rows[tid] = r;
+    s_dv[tid] = (single && dval && r >= 0) ? dval[r] : 0.f;
+  }
+  {
+    const int64_t c0 = (int64_t)blockIdx.y * CWP;
+    for (int c = tid; c < CWP; c += 256) s_bias[c] = (single && epi.bias && c0 + c < F) ? epi.bias[c0 + c] : 0.f;
+  }
   // A fragments of this wave: 16 consecutive floats per lane
   const float4* af = reinterpret_cast<const float4*>(tfrag + ((item * 4 + wave) * 64 + lane) * 16);
   const float4 a0 = af[0], a1 = af[1], a2 = af[2], a3 = af[3];
@@ -584,18 +600,6 @@ spmm_tile_kernel(const int4* __restrict__ tdesc, const int32_t* __restrict__ tco
   for (int nt = 0; nt < NT; ++nt)
 #pragma unroll
     for (int j = 0; j < 4; ++j) s_C[(16 * wave + 4 * (lane >> 4) + j) * CS + nt * 16 + nc] = acc[nt][j];
-  // output rows, their extracted diagonal and the bias go to LDS first (no
-  // global load inside the write-out loop: each would serialise a latency)
-  __shared__ float s_dv[kRB];
-  __shared__ __attribute__((aligned(16))) float s_bias[CW];
-  const bool single = d.z < 0;
-  if (tid < kRB) {
-    const int32_t r = tid < d.y ? trows[(int64_t)d.x * kRB + tid] : -1;
-    s_cols[tid] = r;  // s_cols reused: output rows
-    s_dv[tid] = (single && dval && r >= 0) ? dval[r] : 0.f;
-  }
-  for (int c = tid; c < CW; c += 256)
-    s_bias[c] = (single && epi.bias && col0 + c < F) ? epi.bias[col0 + c] : 0.f;
   __syncthreads();
   constexpr int nq4 = CW / 4;  // 16-B pieces per staged row
   for (int e = tid; e < kRB * nq4; e += 256) {
@@ -607,7 +611,7 @@ spmm_tile_kernel(const int4* __restrict__ tdesc, const int32_t* __restrict__ tco
       *reinterpret_cast<float4*>(slabs + ((int64_t)d.z * kRB + rl) * slab_ld + col) = v;
       continue;
     }
-    const int64_t row = s_cols[rl];
+    const int64_t row = s_rows[rl];
     const float dv = s_dv[rl];
     if (VEC4 && epi.code <= GCNK_EPI_BIAS_RELU) {
       // common case, vectorised (no dropout): + extracted diagonal * B row piece,
@@ -661,6 +665,17 @@ spmm_tile_reduce_kernel(const int4* __restrict__ red, const int32_t* __restrict_
   const int sl = threadIdx.x >> 4, c4 = threadIdx.x & 15;
   const int64_t col = (int64_t)blockIdx.z * 64 + c4 * 4;
   float4 acc = make_float4(0.f, 0.f, 0.f, 0.f);
+  // the epilogue's operands, fetched before the slab loads so their latency overlaps
+  const int64_t row = trows[(int64_t)rb.x * kRB + rl];
+  const float dv = (sl == 0 && dval) ? dval[row] : 0.f;
+  float bcol[4] = {0.f, 0.f, 0.f, 0.f}, brow[4] = {0.f, 0.f, 0.f, 0.f};
+  if (sl == 0)
+#pragma unroll
+    for (int i = 0; i < 4; ++i)
+      if (col + i < F) {
+        if (epi.bias) bcol[i] = epi.bias[col + i];
+        if (dv != 0.f) brow[i] = B[row * ldb + col + i];
+      }
   // slab rows are padded to 16 floats (slab_ld % 16 == 0): whole float4 reads stay
   // inside the row; lanes past F are never stored.
   if (col < F) {
@@ -688,13 +703,10 @@ spmm_tile_reduce_kernel(const int4* __restrict__ red, const int32_t* __restrict_
     const float4 u = s_acc[q][c4];
     t.x += u.x; t.y += u.y; t.z += u.z; t.w += u.w;
   }
-  const int64_t row = trows[(int64_t)rb.x * kRB + rl];
-  const float dv = dval ? dval[row] : 0.f;
   float vals[4] = {t.x, t.y, t.z, t.w};
   for (int i = 0; i < 4 && col + i < F; ++i) {
-    if (dv != 0.f) vals[i] = fmaf(dv, B[row * ldb + col + i], vals[i]);
-    const float b = epi.bias ? epi.bias[col + i] : 0.f;
-    C[row * ldc + col + i] = apply_epi(epi, vals[i], b, row, col + i);
+    if (dv != 0.f) vals[i] = fmaf(dv, brow[i], vals[i]);
+    C[row * ldc + col + i] = apply_epi(epi, vals[i], bcol[i], row, col + i);
   }
 }
 

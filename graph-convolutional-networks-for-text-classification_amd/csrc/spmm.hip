@@ -25,7 +25,9 @@
 //    a fixed xor butterfly.  A row of one segment is stored directly; a row
 //    of several leaves one partial per segment, and the last segment to
 //    finish (arrival counter in the plan) sums them in segment order and
-//    stores the row -- no fix-up launch.  Every lane issues the U gathers of
+//    stores the row -- no fix-up launch.  With whole-wavefront groups (F >
+//    128) a wavefront takes two light rows at once (their items in one vector
+//    load, their gathers in one batch stream).  Every lane issues the U gathers of
 //    a batch before its first FMA (U independent 16-B loads in flight), and a
 //    unit's one store follows all of its loads, so no gather waits behind a
 //    store.  Heavy segments come first in the grid (the longest work is
@@ -49,6 +51,25 @@ constexpr int kKC = 64;                 // condensed columns per tile chunk (16 
 constexpr int kMaxNT = 8;               // 16-column MFMA n-tiles per tile workgroup (B tile 48 KB LDS: 2+ per CU)
 constexpr int kMaxColTiles = 64;        // row-kernel column tiles per launch (arrival counters per heavy row)
 constexpr int kMaxSeg = 64;             // segments per heavy row (bounds the last arriver's combine)
+// Schedule knobs of the whole-wavefront (F > 128) row kernel, overridable at
+// compile time for experiments (scripts/variants.sh times prebuilt variants).
+// Measured on R8 A-hat F = 200 / 20ng-shaped (profiles/r01_variants.log):
+// 2 light rows per wavefront 10.6 / 18.2-19.0 us vs 1: 10.4 / 18.8 (the launch
+// then fits one residency round); 4 rows: 13.9 / 25.4; heavy U = 16: 11.5 (120
+// VGPRs, 4 waves/SIMD); 512-thread workgroups (8 waves per heavy segment): 10.7.
+#ifndef GCNK_LIGHT_RPW
+#define GCNK_LIGHT_RPW 2
+#endif
+#ifndef GCNK_HEAVY_U
+#define GCNK_HEAVY_U 8
+#endif
+#ifndef GCNK_WAVE_BLOCK
+#define GCNK_WAVE_BLOCK 256
+#endif
+constexpr int kHeavyU = GCNK_HEAVY_U;        // gathers in flight per lane in a heavy segment
+constexpr int kWaveBlock = GCNK_WAVE_BLOCK;  // workgroup size for whole-wavefront groups
+constexpr int kLightRPW = GCNK_LIGHT_RPW;    // light rows per wavefront with whole-wavefront groups
+constexpr int kLightMax64 = 64 / kLightRPW;  // their nonzero limit (kLightRPW rows' items fill one 64-lane load)
 
 template <int VEC>
 struct Vec;
@@ -370,6 +391,63 @@ spmm_row_kernel(RowPlan rp, int32_t nhb, const float* __restrict__ B, int64_t ld
   T acc = V::zero();
 
   if ((int32_t)blockIdx.x >= nhb) {
+    if constexpr (LPR == 64) {
+      // ---- light rows, whole-wavefront groups: kLightRPW units per wavefront,
+      //      their items in one vector load (row r's after rows < r's), their
+      //      gathers in one stream of U-wide batches (light rows are at most
+      //      kLightMax64 nonzeros each, so kLightRPW of them fill 64 lanes): the
+      //      light part of the grid is kLightRPW times fewer wavefronts and the
+      //      whole launch fits one residency round.
+      constexpr int R = kLightRPW;
+      const int32_t u0 = __builtin_amdgcn_readfirstlane(rp.nhunits + ((int32_t)blockIdx.x - nhb) * SG * R +
+                                                        (tid / 64) * R);
+      if (u0 >= rp.nunits) return;
+      int4 un[R];
+      int32_t nb[R + 1];  // item prefix offsets of the R rows (wave-uniform)
+      nb[0] = 0;
+#pragma unroll
+      for (int r = 0; r < R; ++r) {
+        un[r] = u0 + r < rp.nunits ? rp.units[u0 + r] : make_int4(-1, 0, 0, -1);
+        nb[r + 1] = nb[r] + (un[r].x >= 0 ? un[r].z - un[r].y : 0);
+      }
+      stamp(epi, 1);
+      const int lane = tid & 63;
+      int32_t k = -1;
+#pragma unroll
+      for (int r = 0; r < R; ++r)
+        if (lane >= nb[r] && lane < nb[r + 1]) k = un[r].y + lane - nb[r];
+      const int2 mine = k >= 0 ? rp.items[k] : make_int2(-1, 0);
+      T accs[R];
+#pragma unroll
+      for (int r = 0; r < R; ++r) accs[r] = V::zero();
+      const int32_t cnt = nb[R];
+      for (int32_t j0 = 0; j0 < cnt; j0 += U) {
+        T g[U];
+        float a[U];
+#pragma unroll
+        for (int j = 0; j < U; ++j) {
+          g[j] = V::zero();
+          a[j] = 0.f;
+          if (j0 + j < cnt) {
+            const int32_t c = __builtin_amdgcn_readlane(mine.x, j0 + j);
+            a[j] = __int_as_float(__builtin_amdgcn_readlane(mine.y, j0 + j));
+            if (colok) g[j] = V::load(B + (int64_t)c * ldb + colv);
+          }
+        }
+#pragma unroll
+        for (int j = 0; j < U; ++j)
+#pragma unroll
+          for (int r = 0; r < R; ++r)
+            if (j0 + j >= nb[r] && j0 + j < nb[r + 1]) V::fma(accs[r], a[j], g[j]);
+      }
+      stamp(epi, 2);
+#pragma unroll
+      for (int r = 0; r < R; ++r)
+        if (un[r].x >= 0)
+          finish_row<LPR, VEC, NP>(accs[r], un[r].x, colv, colok, bv, lg, C, ldc, epi, store_main, proj, pa);
+      stamp(epi, 3);
+      return;
+    }
     // ---- light rows: one unit per lane group
     int32_t u = rp.nhunits + ((int32_t)blockIdx.x - nhb) * SG + tid / LPR;
     if (LPR == 64) u = __builtin_amdgcn_readfirstlane(u);
@@ -377,8 +455,7 @@ spmm_row_kernel(RowPlan rp, int32_t nhb, const float* __restrict__ B, int64_t ld
     const int4 un = rp.units[u];
     if (un.x < 0) return;  // padding of the XCD-class layout
     stamp(epi, 1);
-    if constexpr (LPR == 64) gather_rows_wave<VEC, U, 1>(rp.items, un.y, un.z, 0, B, ldb, colv, colok, acc);
-    else gather_rows<VEC, U, 1>(rp.items, un.y, un.z, 0, B, ldb, colv, colok, acc);
+    gather_rows<VEC, U, 1>(rp.items, un.y, un.z, 0, B, ldb, colv, colok, acc);
     stamp(epi, 2);
     finish_row<LPR, VEC, NP>(acc, un.x, colv, colok, bv, lg, C, ldc, epi, store_main, proj, pa);
     stamp(epi, 3);
@@ -402,7 +479,7 @@ spmm_row_kernel(RowPlan rp, int32_t nhb, const float* __restrict__ B, int64_t ld
   const int4 un = rp.units[u];
   if (un.x < 0) return;           // padding of the XCD-class layout
   stamp(epi, 1);
-  if constexpr (LPR == 64) gather_rows_wave<VEC, U, GS>(rp.items, un.y, un.z, q, B, ldb, colv, colok, acc);
+  if constexpr (LPR == 64) gather_rows_wave<VEC, kHeavyU, GS>(rp.items, un.y, un.z, q, B, ldb, colv, colok, acc);
   else gather_rows<VEC, U, GS>(rp.items, un.y, un.z, q, B, ldb, colv, colok, acc);
   if constexpr (WG) {
     if (w > 0) s_red[w][lane] = acc;
@@ -731,7 +808,7 @@ inline int choose_lpr(int32_t F, int lanes_hint) {
 }
 
 // Narrow groups use one-wave workgroups so a light launch still spans the chip.
-inline int choose_block(int lpr) { return lpr >= 8 ? 256 : 64; }
+inline int choose_block(int lpr) { return lpr == 64 ? kWaveBlock : lpr >= 8 ? 256 : 64; }
 
 struct RowLaunch {
   RowPlan rp;
@@ -750,9 +827,10 @@ struct RowLaunch {
 template <int BLOCK, int LPR, int VEC, int U, int NP>
 int launch_rows(const RowLaunch& a) {
   constexpr int SG = BLOCK / LPR, WPB = BLOCK / 64;
+  constexpr int LPB = LPR == 64 ? SG * kLightRPW : SG;  // light units per workgroup
   // heavy segments: one per workgroup for whole-wavefront groups, else one per wavefront
   const int64_t nhb = LPR == 64 ? (int64_t)a.rp.nhunits : ((int64_t)a.rp.nhunits + WPB - 1) / WPB;
-  const int64_t nlb = ((int64_t)a.rp.nunits - a.rp.nhunits + SG - 1) / SG;
+  const int64_t nlb = ((int64_t)a.rp.nunits - a.rp.nhunits + LPB - 1) / LPB;
   if (nhb + nlb == 0) return GCNK_OK;
   if (nhb + nlb > (int64_t)INT32_MAX) {
     set_error("gcnk_spmm_csr_f32: %lld workgroups exceed the grid", (long long)(nhb + nlb));
@@ -788,7 +866,7 @@ int dispatch_rows(int lpr, const RowLaunch& a) {
     case 8: return launch_rows<256, 8, VEC, 8, 0>(a);
     case 16: return launch_rows<256, 16, VEC, 8, 0>(a);
     case 32: return launch_rows<256, 32, VEC, 8, 0>(a);
-    case 64: return launch_rows<256, 64, VEC, 8, 0>(a);
+    case 64: return launch_rows<kWaveBlock, 64, VEC, 8, 0>(a);
   }
   set_error("gcnk_spmm_csr_f32: unsupported lanes per group %d", lpr);
   return GCNK_EUNSUP;
@@ -800,7 +878,7 @@ int dispatch_rows_proj(int lpr, const RowLaunch& a) {
   switch (lpr) {
     case 16: return launch_rows<256, 16, 4, 8, NP>(a);
     case 32: return launch_rows<256, 32, 4, 8, NP>(a);
-    case 64: return launch_rows<256, 64, 4, 8, NP>(a);
+    case 64: return launch_rows<kWaveBlock, 64, 4, 8, NP>(a);
   }
   set_error("gcnk_spmm_proj_f32: no fused-projection kernel for %d lanes per group", lpr);
   return GCNK_EUNSUP;
@@ -976,12 +1054,14 @@ int host_plan(const int32_t* rowptr_dev, const int32_t* colind_dev, const float*
     return GCNK_EARG;
   }
   const int lpr = 64 / groups;
-  const int block = lpr >= 8 ? 256 : 64, wpb = block / 64, sg = block / lpr;
+  const int block = choose_block(lpr), wpb = block / 64, sg = block / lpr;
   const int hpb = lpr == 64 ? 1 : wpb;                     // heavy units per workgroup
   const int64_t seg = (int64_t)ipc * (lpr == 64 ? wpb : groups);  // nonzeros per heavy segment
-  // light-row limit: 2 * ipc for whole-wavefront groups (a light row is walked by
-  // one wavefront; a heavy one by a 4-wavefront workgroup), ipc otherwise
-  const int64_t light_max = lpr == 64 ? 2 * (int64_t)ipc : ipc;
+  // light-row limit: 2 * ipc for whole-wavefront groups (two light rows share a
+  // wavefront, at most kLightMax64 nonzeros each; a heavy row is walked by a
+  // 4-wavefront workgroup), ipc otherwise
+  const int64_t light_max = lpr == 64 ? std::min<int64_t>(2 * (int64_t)ipc, kLightMax64) : ipc;
+  const int lpb = lpr == 64 ? sg * kLightRPW : sg;  // light units per workgroup
   // XCD classes.  Workgroups b and b + 8 land on one XCD (round-robin dispatch;
   // speed only, never correctness), so every unit of workgroup b is given
   // class b % 8: a light row by its row index, a heavy segment by the column
@@ -1059,7 +1139,7 @@ int host_plan(const int32_t* rowptr_dev, const int32_t* colind_dev, const float*
   };
   layout(hq, hpb);
   const int64_t nh = (int64_t)hp.units.size() / 4;
-  layout(lq, sg);
+  layout(lq, lpb);
   const int64_t nunits = (int64_t)hp.units.size() / 4;
   if (nunits >= (int64_t)INT32_MAX || nslots >= (int64_t)INT32_MAX || nheavy >= (1 << 25)) {
     set_error("gcnk_spmm_plan: %lld row units / %lld partial slots exceed the plan's int32 fields",

@@ -1,0 +1,49 @@
+"""Time the R8 A-hat SpMM (F = 200) on row subsets: light rows only, heavy rows
+only, and all rows, to see which part bounds the launch.  One JSON line each."""
+import json
+import os
+import sys
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, ROOT)
+sys.path.insert(0, os.path.join(ROOT, "scripts"))
+
+
+def main():
+    import torch
+    import gcn_amd  # noqa: F401
+    from graph_convolutional_networks_for_text_classification_amd import datasets, ops
+    from graph_convolutional_networks_for_text_classification_amd.sparse import as_csr, CSR
+    from sweep_spmm import time_graph
+
+    dev = torch.device("cuda", 0)
+    r8 = datasets.load_r8_fixture(os.path.join(ROOT, "tests", "golden", "r8_graph.npz"))
+    A = as_csr(r8["adj"].to(dev))
+    rp, ci, v = A.rowptr.cpu().long(), A.colind.cpu(), A.val.cpu()
+    deg = rp[1:] - rp[:-1]
+    M, K = A.shape
+    F = int(os.environ.get("F", 200))
+
+    def subset(keep):
+        kk = keep.repeat_interleave(deg)
+        nd = torch.where(keep, deg, torch.zeros_like(deg))
+        nrp = torch.zeros(M + 1, dtype=torch.long)
+        nrp[1:] = torch.cumsum(nd, 0)
+        return CSR(nrp.int().to(dev), ci[kk].to(dev), v[kk].to(dev), (M, K))
+
+    B = torch.randn(K, F, device=dev)
+    out = torch.empty(M, F, device=dev)
+    for thr in (32, 64, 128, 512):
+        for name, a in ((f"light<= {thr}", subset(deg <= thr)), (f"heavy> {thr}", subset(deg > thr))):
+            us = time_graph(lambda: ops.spmm(a, B, out=out), 100)
+            print(json.dumps({"subset": name, "nnz": a.nnz, "rows": int((a.rowptr[1:] != a.rowptr[:-1]).sum()),
+                              "us": us}), flush=True)
+    us = time_graph(lambda: ops.spmm(A, B, out=out), 100)
+    print(json.dumps({"subset": "all", "nnz": A.nnz, "us": us}), flush=True)
+    e = torch.empty(0, device=dev)
+    print(json.dumps({"degree_hist": torch.histc(deg.float(), bins=16, min=0, max=2048).int().tolist(),
+                      "max_deg": int(deg.max())}))
+
+
+if __name__ == "__main__":
+    main()

@@ -22,14 +22,15 @@ def geometry(groups):
     wpb, sg = block // 64, block // lpr
     hpb = 1 if lpr == 64 else wpb
     seg_groups = wpb if lpr == 64 else groups
-    return hpb, sg, seg_groups
+    lpb = 2 * sg if lpr == 64 else sg  # light units per workgroup (two per wavefront at 64 lanes)
+    return hpb, lpb, seg_groups
 
 
 def host_plan(rowptr, colind, K, ipc, groups):
     """-> (units [(row, b, e, w)], heavy [(row, first slot, nseg)], nh, nslots)."""
-    hpb, sg, seg_groups = geometry(groups)
+    hpb, lpb, seg_groups = geometry(groups)
     seg = ipc * seg_groups
-    light_max = 2 * ipc if hpb == 1 else ipc
+    light_max = min(2 * ipc, 32) if hpb == 1 else ipc
     M = len(rowptr) - 1
     hq, lq, heavy = [[] for _ in range(NX)], [[] for _ in range(NX)], []
     nslots = 0
@@ -82,7 +83,7 @@ def host_plan(rowptr, colind, K, ipc, groups):
 
     units = layout(hq, hpb)
     nh = len(units)
-    units += layout(lq, sg)
+    units += layout(lq, lpb)
     return units, heavy, nh, nslots
 
 
@@ -90,7 +91,7 @@ def spmm(rowptr, colind, val, B, ipc, groups):
     """C = A @ B computed the way the row kernel schedules it (float64), with
     the per-workgroup XCD class of every unit checked."""
     M, K = len(rowptr) - 1, B.shape[0]
-    hpb, sg, seg_groups = geometry(groups)
+    hpb, lpb, seg_groups = geometry(groups)
     units, heavy, nh, nslots = host_plan(rowptr, colind, K, ipc, groups)
     C = np.full((M, B.shape[1]), np.nan)
     part = np.zeros((nslots, B.shape[1]))
@@ -124,7 +125,7 @@ def spmm(rowptr, colind, val, B, ipc, groups):
         r, b, e, _ = units[u]
         if r < 0:
             continue
-        assert ((nh // hpb + (u - nh) // sg) % NX) == _cls(r, M), "light unit in its XCD class"
+        assert ((nh // hpb + (u - nh) // lpb) % NX) == _cls(r, M), "light unit in its XCD class"
         C[r] = gather(b, e, 0, 1)
         written[r] += 1
     assert np.all(written == 1), "every row is stored exactly once"

@@ -45,5 +45,50 @@ def main():
                       "max_deg": int(deg.max())}))
 
 
-if __name__ == "__main__":
+if __name__ == "__main__" and not os.environ.get("STAMPS"):
     main()
+
+
+def stamps_heavy():
+    """Per-workgroup stamps of the heavy-only subset (all its workgroups are heavy segments)."""
+    import numpy as np
+    import torch
+    import gcn_amd  # noqa: F401
+    from graph_convolutional_networks_for_text_classification_amd import _lib, datasets, ops
+    from graph_convolutional_networks_for_text_classification_amd.sparse import as_csr, CSR
+    dev = torch.device("cuda", 0)
+    lib = _lib.load()
+    r8 = datasets.load_r8_fixture(os.path.join(ROOT, "tests", "golden", "r8_graph.npz"))
+    A = as_csr(r8["adj"].to(dev))
+    rp, ci, v = A.rowptr.cpu().long(), A.colind.cpu(), A.val.cpu()
+    deg = rp[1:] - rp[:-1]
+    M, K = A.shape
+    keep = deg > 32
+    kk = keep.repeat_interleave(deg)
+    nd = torch.where(keep, deg, torch.zeros_like(deg))
+    nrp = torch.zeros(M + 1, dtype=torch.long)
+    nrp[1:] = torch.cumsum(nd, 0)
+    a = CSR(nrp.int().to(dev), ci[kk].to(dev), v[kk].to(dev), (M, K))
+    B = torch.randn(K, 200, device=dev)
+    out = torch.empty(M, 200, device=dev)
+    for _ in range(5):
+        ops.spmm(a, B, out=out)
+    torch.cuda.synchronize()
+    buf = torch.zeros(4 * 100000, dtype=torch.int64, device=dev)
+    lib.gcnk_debug_set_stamps(buf.data_ptr())
+    ops.spmm(a, B, out=out)
+    torch.cuda.synchronize()
+    lib.gcnk_debug_set_stamps(None)
+    s = buf.view(-1, 4).cpu().numpy().astype(np.float64)
+    s = s[(s[:, 0] > 0) & (s[:, 3] > 0)]
+    s = (s - s[:, 0].min()) / 100.0
+    d = np.diff(s, axis=1)
+    pct = lambda x: [round(float(np.percentile(x, p)), 2) for p in (0, 50, 90, 100)]
+    print(json.dumps({"wgs": len(s), "entry": pct(s[:, 0]), "unit": pct(d[:, 0]), "walk": pct(d[:, 1]),
+                      "tail": pct(d[:, 2]), "end": pct(s[:, 3])}))
+    order = np.argsort(-s[:, 3])[:8]
+    print(json.dumps({"latest": [[round(x, 2) for x in s[i]] for i in order]}))
+
+
+if __name__ == "__main__" and os.environ.get("STAMPS"):
+    stamps_heavy()

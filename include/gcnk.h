@@ -106,7 +106,7 @@ const char* gcnk_last_error(void);
  *   0 magic 'GNK5'  1 M  2 K  3 groups  4 ipc  5 row units  6 heavy segments
  *   (= partial slots)  7 heavy rows of > 1 segment  8 tile chunks
  *   9 multi-chunk blocks  10 slabs  11 tile blocks  12 diagonal kept aside
- *   (0/1)  13 nnz  14 0  15 0   (tile blocks: 64 rows x 64-column chunks)
+ *   (0/1)  13 nnz  14 partial slots  15 0   (tile blocks: 64 rows x 64-column chunks)
  * ------------------------------------------------------------------------- */
 int32_t gcnk_spmm_groups(int32_t F, int32_t lanes_hint);
 int32_t gcnk_spmm_default_ipc(int32_t M, int64_t nnz, int32_t F, int32_t lanes_hint);

@@ -70,30 +70,50 @@ gemm_f32_mfma_kernel(int32_t M, int32_t N, int32_t K, int32_t kchunk, const floa
 #pragma unroll
     for (int j = 0; j < FN; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
 
-  for (int32_t k0 = kb; k0 < ke; k0 += BK) {
+  // k tiles are register double-buffered: tile t + 1's global loads are in
+  // flight while tile t is multiplied out of LDS
+  constexpr int PA = (BM * BK + 255) / 256, PB = (BN * BK + 255) / 256;
+  float ra[PA], rb[PB];
+  auto fetch = [&](int32_t k0) {
 #pragma unroll
-    for (int e = tid; e < BM * BK; e += 256) {
+    for (int p = 0; p < PA; ++p) {
+      const int e = tid + p * 256;
       int m, k;
       if (!TA) { m = e / BK; k = e % BK; }
       else { k = e / BM; m = e % BM; }
       const int64_t gm = m0 + m;
       const int32_t gk = k0 + k;
-      float x = 0.f;
-      if (gm < M && gk < ke) x = TA ? A[(int64_t)gk * lda + gm] : A[gm * lda + gk];
-      As[k][m] = x;
+      ra[p] = (e < BM * BK && gm < M && gk < ke) ? (TA ? A[(int64_t)gk * lda + gm] : A[gm * lda + gk]) : 0.f;
     }
 #pragma unroll
-    for (int e = tid; e < BN * BK; e += 256) {
+    for (int p = 0; p < PB; ++p) {
+      const int e = tid + p * 256;
       int n, k;
       if (!TB) { k = e / BN; n = e % BN; }
       else { n = e / BK; k = e % BK; }
       const int64_t gn = n0 + n;
       const int32_t gk = k0 + k;
-      float x = 0.f;
-      if (gn < N && gk < ke) x = TB ? B[gn * ldb + gk] : B[(int64_t)gk * ldb + gn];
-      Bs[k][n] = x;
+      rb[p] = (e < BN * BK && gn < N && gk < ke) ? (TB ? B[gn * ldb + gk] : B[(int64_t)gk * ldb + gn]) : 0.f;
+    }
+  };
+  if (kb < ke) fetch(kb);
+  for (int32_t k0 = kb; k0 < ke; k0 += BK) {
+#pragma unroll
+    for (int p = 0; p < PA; ++p) {
+      const int e = tid + p * 256;
+      if (e >= BM * BK) break;
+      if (!TA) As[e % BK][e / BK] = ra[p];
+      else As[e / BM][e % BM] = ra[p];
+    }
+#pragma unroll
+    for (int p = 0; p < PB; ++p) {
+      const int e = tid + p * 256;
+      if (e >= BN * BK) break;
+      if (!TB) Bs[e / BN][e % BN] = rb[p];
+      else Bs[e % BK][e / BK] = rb[p];
     }
     __syncthreads();
+    if (k0 + BK < ke) fetch(k0 + BK);
 #pragma unroll
     for (int kk = 0; kk < BK; kk += 4) {
       const int kr = kk + (lane >> 4);
@@ -200,7 +220,14 @@ __global__ void gemm_splitk_reduce_kernel(int32_t M, int32_t N, int32_t S, const
   const int64_t total = (int64_t)M * N;
   if (idx >= total) return;
   float acc = 0.f;
-  for (int s = 0; s < S; ++s) acc += slab[(int64_t)s * total + idx];
+  for (int s0 = 0; s0 < S; s0 += 16) {  // 16 loads in flight, summed in slab order
+    float v[16];
+#pragma unroll
+    for (int j = 0; j < 16; ++j) v[j] = s0 + j < S ? slab[(int64_t)(s0 + j) * total + idx] : 0.f;
+#pragma unroll
+    for (int j = 0; j < 16; ++j)
+      if (s0 + j < S) acc += v[j];
+  }
   const int64_t m = idx / N, n = idx % N;
   C[m * ldc + n] = gemm_epi(epi, acc, m, n);
 }
@@ -243,7 +270,14 @@ __global__ void colsum_pass1_kernel(const float* __restrict__ X, int64_t ldx, in
   const int64_t r0 = (int64_t)blockIdx.x * kColsumRows;
   const int64_t r1 = min<int64_t>(r0 + kColsumRows, M);
   float acc = 0.f;
-  for (int64_t r = r0; r < r1; ++r) acc += X[r * ldx + n];
+  for (int64_t r = r0; r < r1; r += 16) {  // 16 loads in flight, summed in row order
+    float v[16];
+#pragma unroll
+    for (int j = 0; j < 16; ++j) v[j] = r + j < r1 ? X[(r + j) * ldx + n] : 0.f;
+#pragma unroll
+    for (int j = 0; j < 16; ++j)
+      if (r + j < r1) acc += v[j];
+  }
   part[(int64_t)blockIdx.x * N + n] = acc;
 }
 
@@ -252,7 +286,14 @@ __global__ void colsum_pass2_kernel(const float* __restrict__ part, int32_t nblk
   const int64_t n = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
   if (n >= N) return;
   float acc = 0.f;
-  for (int b = 0; b < nblk; ++b) acc += part[(int64_t)b * N + n];
+  for (int b0 = 0; b0 < nblk; b0 += 16) {  // 16 loads in flight, summed in block order
+    float v[16];
+#pragma unroll
+    for (int j = 0; j < 16; ++j) v[j] = b0 + j < nblk ? part[(int64_t)(b0 + j) * N + n] : 0.f;
+#pragma unroll
+    for (int j = 0; j < 16; ++j)
+      if (b0 + j < nblk) acc += v[j];
+  }
   out[n] = acc;
 }
 

@@ -154,7 +154,7 @@ def gemm(A, B, transA=False, transB=False, bias=None, epilogue=_lib.GEMM_EPI_NON
         # long reductions with a small output (H^T g: K = nodes) get K-slabs
         tiles = ((M + 63) // 64) * ((N + 63) // 64)
         split_k = 1
-        while split_k < 64 and tiles * split_k < 256 and K // (split_k * 2) >= 128:
+        while split_k < 128 and tiles * split_k < 512 and K // (split_k * 2) >= 64:
             split_k *= 2
     lib = _lib.load()
     wsb = lib.gcnk_gemm_workspace_bytes(M, N, K, split_k)

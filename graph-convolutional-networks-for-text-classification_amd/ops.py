@@ -136,6 +136,17 @@ def spmm_proj(a, B, W, bias=None, epilogue=_lib.EPI_NONE, mask=None, scale=1.0, 
     return H, C2
 
 
+def default_split_k(M, N, K):
+    """K-slabs for a GEMM: only long reductions with a small output (H^T g,
+    K = nodes) are split; short ones (H1 W2, K = 200) stay whole so the skinny
+    kernel takes them."""
+    tiles = ((M + 63) // 64) * ((N + 63) // 64)
+    split_k = 1
+    while K >= 1024 and split_k < 128 and tiles * split_k < 512 and K // (split_k * 2) >= 64:
+        split_k *= 2
+    return split_k
+
+
 def gemm(A, B, transA=False, transB=False, bias=None, epilogue=_lib.GEMM_EPI_NONE, R=None, scale=1.0,
          split_k=None, out=None):
     """C = epi(op(A) @ op(B)) on fp32 MFMA.
@@ -151,11 +162,7 @@ def gemm(A, B, transA=False, transB=False, bias=None, epilogue=_lib.GEMM_EPI_NON
     if out is None:
         out = torch.empty((M, N), dtype=torch.float32, device=A.device)
     if split_k is None:
-        # long reductions with a small output (H^T g: K = nodes) get K-slabs
-        tiles = ((M + 63) // 64) * ((N + 63) // 64)
-        split_k = 1
-        while split_k < 128 and tiles * split_k < 512 and K // (split_k * 2) >= 64:
-            split_k *= 2
+        split_k = default_split_k(M, N, K)
     lib = _lib.load()
     wsb = lib.gcnk_gemm_workspace_bytes(M, N, K, split_k)
     ws = torch.empty((wsb + 3) // 4, dtype=torch.float32, device=A.device) if wsb > 0 else None

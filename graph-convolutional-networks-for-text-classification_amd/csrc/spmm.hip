@@ -622,53 +622,67 @@ spmm_tile_kernel(const int4* __restrict__ tdesc, const int32_t* __restrict__ tco
   const int wave = tid >> 6;
   const int64_t item = blockIdx.x;
   stamp(epi, 0);
-  const int4 d = tdesc[item];  // block, nrows, slab (-1: single chunk), 0
+  const int4 d0 = tdesc[item];  // block, nrows | contiguous run length << 8, slab (-1: single chunk), run start
+  const int32_t run = d0.y >> 8;
+  const int4 d = make_int4(d0.x, d0.y & 0xff, d0.z, d0.w);
   const int64_t col0 = (int64_t)blockIdx.y * (NT * 16);  // this workgroup's column slice
 
-  if (tid < kKC) s_cols[tid] = tcols[item * kKC + tid];
-  // output rows, their extracted diagonal and the bias: fetched now (their
-  // latency hides behind the staging) and parked in LDS for the write-out
+  if (run == 0 && tid < kKC) s_cols[tid] = tcols[item * kKC + tid];
+  // output rows, their extracted diagonal and the bias: loads issued now, held
+  // in registers (their descriptor -> row list -> diagonal chain runs behind the
+  // staging and the MFMAs) and parked in LDS only after the MFMA phase
   constexpr int CWP = NT * 16;
+  static_assert(CWP <= 256, "one bias element per thread");
   __shared__ int32_t s_rows[kRB];
   __shared__ float s_dv[kRB];
   __shared__ __attribute__((aligned(16))) float s_bias[CWP];
   const bool single = d.z < 0;
+  int32_t r_own = -1;
+  float dv_own = 0.f, bias_own = 0.f;
   if (tid < kRB) {
-    const int32_t r = tid < d.y ? trows[(int64_t)d.x * kRB + tid] : -1;
-    s_rows[tid] = r;
-    s_dv[tid] = (single && dval && r >= 0) ? dval[r] : 0.f;
+    r_own = tid < d.y ? trows[(int64_t)d.x * kRB + tid] : -1;
+    dv_own = (single && dval && r_own >= 0) ? dval[r_own] : 0.f;
   }
   {
-    const int64_t c0 = (int64_t)blockIdx.y * CWP;
-    for (int c = tid; c < CWP; c += 256) s_bias[c] = (single && epi.bias && c0 + c < F) ? epi.bias[c0 + c] : 0.f;
+    const int64_t c = (int64_t)blockIdx.y * CWP + tid;
+    if (tid < CWP) bias_own = (single && epi.bias && c < F) ? epi.bias[c] : 0.f;
   }
   // A fragments of this wave: 16 consecutive floats per lane
   const float4* af = reinterpret_cast<const float4*>(tfrag + ((item * 4 + wave) * 64 + lane) * 16);
   const float4 a0 = af[0], a1 = af[1], a2 = af[2], a3 = af[3];
-  __syncthreads();
   // ---- stage the chunk's B rows, columns [0, 16*NT): element (k, n) -> s_B[k][n&15][n>>4]
-  // all of a thread's loads issue before any LDS store (one memory latency, not PT)
+  // all of a thread's loads issue before any LDS store (one memory latency, not PT);
+  // a contiguous run needs no column list, so its loads issue before the barrier
+  // (not behind the descriptor -> row list -> diagonal chain the barrier waits for)
   constexpr int nq = NT * 4;  // float4 per staged row
   constexpr int PT = (kKC * nq + 255) / 256;
   float4 v[PT];
+  auto fetch = [&](bool contiguous) {
 #pragma unroll
-  for (int p = 0; p < PT; ++p) {
-    const int q = tid + p * 256;
-    const int k = q / nq, c4 = q % nq;
-    const int32_t src = q < kKC * nq ? s_cols[k] : -1;
-    const int64_t col = col0 + c4 * 4;
-    v[p] = make_float4(0.f, 0.f, 0.f, 0.f);
-    if (src >= 0) {
-      const float* bp = B + (int64_t)src * ldb + col;
-      if (VEC4) {
-        if (col < F) v[p] = *reinterpret_cast<const float4*>(bp);
-      } else {
-        if (col + 0 < F) v[p].x = bp[0];
-        if (col + 1 < F) v[p].y = bp[1];
-        if (col + 2 < F) v[p].z = bp[2];
-        if (col + 3 < F) v[p].w = bp[3];
+    for (int p = 0; p < PT; ++p) {
+      const int q = tid + p * 256;
+      const int k = q / nq, c4 = q % nq;
+      const int32_t src = q < kKC * nq ? (contiguous ? (k < run ? d.w + k : -1) : s_cols[k]) : -1;
+      const int64_t col = col0 + c4 * 4;
+      v[p] = make_float4(0.f, 0.f, 0.f, 0.f);
+      if (src >= 0) {
+        const float* bp = B + (int64_t)src * ldb + col;
+        if (VEC4) {
+          if (col < F) v[p] = *reinterpret_cast<const float4*>(bp);
+        } else {
+          if (col + 0 < F) v[p].x = bp[0];
+          if (col + 1 < F) v[p].y = bp[1];
+          if (col + 2 < F) v[p].z = bp[2];
+          if (col + 3 < F) v[p].w = bp[3];
+        }
       }
     }
+  };
+  if (run > 0) {
+    fetch(true);
+  } else {
+    __syncthreads();  // s_cols
+    fetch(false);
   }
 #pragma unroll
   for (int p = 0; p < PT; ++p) {
@@ -716,6 +730,11 @@ spmm_tile_kernel(const int4* __restrict__ tdesc, const int32_t* __restrict__ tco
   constexpr int CS = (kKC * stride >= kRB * (CW + 4)) ? CW + 4 : CW;  // row stride (floats)
   static_assert(kKC * stride >= kRB * CS, "output tile must fit the B tile");
   __syncthreads();  // all waves are done reading s_B
+  if (tid < kRB) {
+    s_rows[tid] = r_own;
+    s_dv[tid] = dv_own;
+  }
+  if (tid < CWP) s_bias[tid] = bias_own;
   float* s_C = s_B;
 #pragma unroll
   for (int nt = 0; nt < NT; ++nt)
@@ -1054,7 +1073,16 @@ int host_plan(const int32_t* rowptr_dev, const int32_t* colind_dev, const float*
         for (int64_t c = 0; c < ncols; ++c) cmap[(size_t)cols[(size_t)c]] = (int32_t)c;
         const size_t base_item = (size_t)ntile;
         for (int32_t ch = 0; ch < nch; ++ch) {
-          hp.tdesc.insert(hp.tdesc.end(), {blk, (int32_t)nrows, nch > 1 ? first_slab + ch : -1, 0});
+          // a chunk whose condensed columns are one contiguous run (R8's X: the
+          // 50 topic columns; 64-column pieces of the dense topic rows) is
+          // described by its first column and length (y bits 8.., w), so the
+          // kernel stages its B rows without waiting for the column list
+          const int64_t c0 = (int64_t)ch * kKC;
+          const int32_t kc = (int32_t)std::min<int64_t>(kKC, ncols - c0);
+          bool contig = true;
+          for (int32_t k = 1; k < kc && contig; ++k) contig = cols[(size_t)(c0 + k)] == cols[(size_t)c0] + k;
+          hp.tdesc.insert(hp.tdesc.end(), {blk, (int32_t)nrows | (contig ? kc << 8 : 0), nch > 1 ? first_slab + ch : -1,
+                                           contig ? cols[(size_t)c0] : 0});
           for (int k = 0; k < kKC; ++k) {
             const int64_t cc = (int64_t)ch * kKC + k;
             hp.tcols.push_back(cc < ncols ? cols[(size_t)cc] : -1);

@@ -99,12 +99,15 @@ def test_spmm_schedule_variants(ipc, lanes):
 
 def _mixed_density_csr(rng, M, K):
     """Row blocks of every kind the hybrid plan distinguishes: a dense band over
-    few columns (R8 X's document rows), fully dense rows spanning several
+    few columns (R8 X's document rows; contiguous, and strided so the tile
+    kernel's column-list path runs too), fully dense rows spanning several
     64-column chunks (X's topic rows), heavy sparse rows, light rows, empty rows."""
     rows, cols = [], []
     for r in range(M):
         if r < 130:                       # dense over columns 0..49 (+ the diagonal past 50)
             c = np.arange(50) if r < 50 else np.concatenate([np.arange(50), [r]])
+        elif 200 <= r < 264:              # dense over a strided column set (a non-contiguous condensed chunk)
+            c = 100 + 3 * np.arange(60)
         elif 300 <= r < 341:              # fully dense
             c = np.arange(K)
         elif 400 <= r < 600:              # self loop + 4 of 50 "topic" columns (Â's document rows)

@@ -123,7 +123,9 @@ struct Vec<1> {
 //   heavy region first, then light rows, each laid out so that the units of
 //   workgroup b belong to XCD class b % 8 (below) | heavy int4[nheavy]
 //   {row, first partial slot, nseg, 0} | arrival counters
-//   int32[nheavy * kMaxColTiles] (zero between launches) | tile part.
+//   int32[nheavy * kMaxColTiles] (zero between launches) | tile part (descriptors,
+//   condensed columns, A fragments, reduce list, row lists, extracted diagonal
+//   float[64 * ntblk] in block order).
 struct Layout {
   int64_t M, nnz, nunits, nhunits, nheavy, nslots, ntile, nred, ntblk, has_diag;
   int64_t items, units, heavy, cnt, tdesc, tcols, tfrag, red, trows, dval, total;
@@ -140,7 +142,7 @@ struct Layout {
     red = tfrag + (int64_t)kRB * kKC * ntile;
     trows = red + 4 * nred;
     dval = trows + (int64_t)kRB * ntblk;
-    total = dval + (has_diag ? M : 0);
+    total = dval + (has_diag ? (int64_t)kRB * ntblk : 0);
   }
 };
 
@@ -641,7 +643,7 @@ spmm_tile_kernel(const int4* __restrict__ tdesc, const int32_t* __restrict__ tco
   float dv_own = 0.f, bias_own = 0.f;
   if (tid < kRB) {
     r_own = tid < d.y ? trows[(int64_t)d.x * kRB + tid] : -1;
-    dv_own = (single && dval && r_own >= 0) ? dval[r_own] : 0.f;
+    dv_own = (single && dval) ? dval[(int64_t)d.x * kRB + tid] : 0.f;  // 0 past the block's rows
   }
   {
     const int64_t c = (int64_t)blockIdx.y * CWP + tid;
@@ -807,7 +809,7 @@ spmm_tile_reduce_kernel(const int4* __restrict__ red, const int32_t* __restrict_
   float4 acc = make_float4(0.f, 0.f, 0.f, 0.f);
   // the epilogue's operands, fetched before the slab loads so their latency overlaps
   const int64_t row = trows[(int64_t)rb.x * kRB + rl];
-  const float dv = (sl == 0 && dval) ? dval[row] : 0.f;
+  const float dv = (sl == 0 && dval) ? dval[(int64_t)rb.x * kRB + rl] : 0.f;
   float bcol[4] = {0.f, 0.f, 0.f, 0.f}, brow[4] = {0.f, 0.f, 0.f, 0.f};
   if (sl == 0)
 #pragma unroll
@@ -993,7 +995,7 @@ struct HostPlan {
   int32_t hdr[16];
   std::vector<int32_t> units, heavy;  // row-kernel units (int4 each), heavy rows (int4 each)
   std::vector<int32_t> tdesc, tcols, red, trows;
-  std::vector<float> tfrag, dval;  // dval: extracted diagonal of tile rows (M, or empty)
+  std::vector<float> tfrag, dval;  // dval: extracted diagonal of tile rows in block order (64 per block, or empty)
 };
 
 int host_plan(const int32_t* rowptr_dev, const int32_t* colind_dev, const float* val_dev, int32_t M, int32_t K,
@@ -1117,7 +1119,11 @@ int host_plan(const int32_t* rowptr_dev, const int32_t* colind_dev, const float*
         ntile += nch;
       }
     }
-    if (any_diag) hp.dval = std::move(dv);
+    if (any_diag) {  // block order, so kernels index it by (block, row in block) without the row list
+      hp.dval.assign((size_t)ntblk * kRB, 0.f);
+      for (size_t i = 0; i < hp.trows.size(); ++i)
+        if (hp.trows[i] >= 0) hp.dval[i] = dv[(size_t)hp.trows[i]];
+    }
   }
 
   // ---- row units over the other rows.  Launch geometry from `groups` = 64 / LPR.

@@ -88,6 +88,27 @@ def stamps_heavy():
                       "tail": pct(d[:, 2]), "end": pct(s[:, 3])}))
     order = np.argsort(-s[:, 3])[:8]
     print(json.dumps({"latest": [[round(x, 2) for x in s[i]] for i in order]}))
+    # per-workgroup walk time against grid position and segment (plan units: heavy region first)
+    pl = list(a._plans.values())[-1]
+    hdr = pl.header
+    nnz, nh = hdr[13], hdr[6]
+    words = pl.buf.view(torch.int32).cpu().numpy() if hasattr(pl, "buf") else None
+    raw = buf.view(-1, 4).cpu().numpy().astype(np.float64)[:nh]
+    ok = (raw[:, 0] > 0) & (raw[:, 3] > 0)
+    t0 = raw[ok, 0].min()
+    st = (raw - t0) / 100.0
+    walk = st[:, 2] - st[:, 1]
+    if words is not None:
+        uoff = (16 + 2 * nnz + 3) & ~3
+        units = words[uoff:uoff + 4 * nh].reshape(nh, 4)
+        seglen = units[:, 2] - units[:, 1]
+        idx = np.where(ok)[0]
+        slow = idx[np.argsort(-walk[idx])[:12]]
+        print(json.dumps({"slowest_walks": [[int(b), int(b % 8), int(units[b, 0]), int(seglen[b]), round(float(st[b, 0]), 2),
+                                              round(float(walk[b]), 2)] for b in slow],
+                          "walk_by_xcd_p90": [round(float(np.percentile(walk[idx[idx % 8 == c]], 90)), 2) for c in range(8)],
+                          "walk_by_position_decile_p50": [round(float(np.median(walk[idx[(idx * 10) // nh == q]])), 2)
+                                                          for q in range(10)]}))
 
 
 if __name__ == "__main__" and os.environ.get("STAMPS"):

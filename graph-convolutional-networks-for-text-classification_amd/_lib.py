@@ -44,6 +44,16 @@ SIGNATURES = {
         _vp, _i64,                # workspace, workspace_bytes
         _i32, _vp,                # lanes_hint, stream
     ]),
+    "gcnk_spmm_csr_f32_part": (ctypes.c_int, [
+        _vp, _vp,                 # plan (device), plan header (host, 16 words)
+        _vp, _i64, _i32,          # B, ldb, F
+        _vp, _i64,                # C, ldc
+        _vp, _i32,                # bias, epilogue
+        _vp, _i64, _f32,          # drop_mask, ldm, drop_scale
+        _f32, _u64, _u64,         # keep_prob, seed, offset
+        _vp, _i64,                # workspace, workspace_bytes
+        _i32, _i32, _vp,          # lanes_hint, part, stream
+    ]),
     "gcnk_spmm_proj_f32": (ctypes.c_int, [
         _vp, _vp,                 # plan, plan header
         _vp, _i64, _i32,          # B, ldb, F

@@ -117,7 +117,7 @@ struct Vec<1> {
 //   0 magic  1 M  2 K  3 lane groups per wavefront (64 / LPR)  4 ipc (light-row limit)
 //   5 nunits  6 nhunits (heavy region, padded)  7 nheavy (rows of > 1 segment)
 //   8 ntile (chunks)  9 nred  10 nslabs  11 ntblk (tile blocks)  12 has_diag  13 nnz
-//   14 nslots (partial slots)  15 0
+//   14 nslots (partial slots)  15 nsingle (chunk items of single-chunk blocks, listed first)
 // Body: items int2[nnz] {col, value bits} in CSR order | units int4[nunits]
 //   {row (-1: empty), nz begin, nz end, heavy row * 64 + segment or -1}: the
 //   heavy region first, then light rows, each laid out so that the units of
@@ -611,7 +611,7 @@ __global__ void __launch_bounds__(256)
 spmm_tile_kernel(const int4* __restrict__ tdesc, const int32_t* __restrict__ tcols, const float* __restrict__ tfrag,
                  const int32_t* __restrict__ trows, const float* __restrict__ dval, int32_t F,
                  const float* __restrict__ B, int64_t ldb, float* __restrict__ C, int64_t ldc, Epi epi,
-                 float* __restrict__ slabs, int64_t slab_ld) {
+                 float* __restrict__ slabs, int64_t slab_ld, int32_t item0) {
   constexpr int NT4 = (NT + 3) & ~3;
   // floats per (k, lane column) row: an odd number of 16-B quads keeps the 16 lanes
   // of a ds_read_b128 group on disjoint bank quads
@@ -622,7 +622,7 @@ spmm_tile_kernel(const int4* __restrict__ tdesc, const int32_t* __restrict__ tco
   const int tid = threadIdx.x;
   const int lane = tid & 63;
   const int wave = tid >> 6;
-  const int64_t item = blockIdx.x;
+  const int64_t item = (int64_t)blockIdx.x + item0;
   stamp(epi, 0);
   const int4 d0 = tdesc[item];  // block, nrows | contiguous run length << 8, slab (-1: single chunk), run start
   const int32_t run = d0.y >> 8;
@@ -963,13 +963,15 @@ struct TileArgs {
   Epi epi;
   float* slabs;
   int64_t slab_ld;
+  int32_t item0;  // first chunk item of this launch
 };
 
 template <bool V4, int NT>
 int launch_tile_nt(unsigned nitems, const TileArgs& t, hipStream_t s) {
+  if (nitems == 0) return GCNK_OK;
   const unsigned slices = (unsigned)((t.F + NT * 16 - 1) / (NT * 16));
   hipLaunchKernelGGL((spmm_tile_kernel<V4, NT>), dim3(nitems, slices), dim3(256), 0, s, t.tdesc, t.tcols, t.tfrag, t.trows, t.dval, t.F, t.B,
-                     t.ldb, t.C, t.ldc, t.epi, t.slabs, t.slab_ld);
+                     t.ldb, t.C, t.ldc, t.epi, t.slabs, t.slab_ld, t.item0);
   return launch_check("spmm_tile_kernel");
 }
 
@@ -1034,7 +1036,7 @@ int host_plan(const int32_t* rowptr_dev, const int32_t* colind_dev, const float*
   //      used at least twice on average; its rows' diagonal entries (r < K) are
   //      taken out of the column set and added in the epilogue (dval[r] * B[r,:]).
   std::vector<char> tile_row((size_t)M, 0);
-  int32_t ntile = 0, nred = 0, nslabs = 0, ntblk = 0;
+  int32_t ntile = 0, nred = 0, nslabs = 0, ntblk = 0, nsingle = 0;
   bool any_diag = false;
   hp.dval.clear();
   auto is_diag = [&](int32_t r, int64_t k) { return r < K && ci[(size_t)k] == r; };
@@ -1118,6 +1120,30 @@ int host_plan(const int32_t* rowptr_dev, const int32_t* colind_dev, const float*
         }
         ntile += nch;
       }
+    }
+    // chunk items of single-chunk blocks first, then the multi-chunk ones (which
+    // also need the reduce launch): the two runs can be launched separately
+    // (gcnk_spmm_csr_f32_part), e.g. on two streams
+    {
+      std::vector<int32_t> order;
+      for (int32_t i = 0; i < ntile; ++i)
+        if (hp.tdesc[(size_t)i * 4 + 2] < 0) order.push_back(i);
+      nsingle = (int32_t)order.size();
+      for (int32_t i = 0; i < ntile; ++i)
+        if (hp.tdesc[(size_t)i * 4 + 2] >= 0) order.push_back(i);
+      std::vector<int32_t> td((size_t)ntile * 4), tc((size_t)ntile * kKC);
+      std::vector<float> tf((size_t)ntile * kRB * kKC);
+      for (int32_t j = 0; j < ntile; ++j) {
+        const size_t i = (size_t)order[(size_t)j];
+        std::copy(hp.tdesc.begin() + i * 4, hp.tdesc.begin() + i * 4 + 4, td.begin() + (size_t)j * 4);
+        std::copy(hp.tcols.begin() + i * kKC, hp.tcols.begin() + (i + 1) * kKC, tc.begin() + (size_t)j * kKC);
+        if (!hp.tfrag.empty())
+          std::copy(hp.tfrag.begin() + i * kRB * kKC, hp.tfrag.begin() + (i + 1) * kRB * kKC,
+                    tf.begin() + (size_t)j * kRB * kKC);
+      }
+      hp.tdesc.swap(td);
+      hp.tcols.swap(tc);
+      if (!hp.tfrag.empty()) hp.tfrag.swap(tf);
     }
     if (any_diag) {  // block order, so kernels index it by (block, row in block) without the row list
       hp.dval.assign((size_t)ntblk * kRB, 0.f);
@@ -1225,7 +1251,7 @@ int host_plan(const int32_t* rowptr_dev, const int32_t* colind_dev, const float*
     return GCNK_EUNSUP;
   }
   const int32_t h[16] = {kMagic, M,     K,      groups, ipc,  (int32_t)nunits, (int32_t)nh, nheavy,
-                         ntile,  nred, nslabs, ntblk,  any_diag ? 1 : 0, (int32_t)nnz, (int32_t)nslots, 0};
+                         ntile,  nred, nslabs, ntblk,  any_diag ? 1 : 0, (int32_t)nnz, (int32_t)nslots, nsingle};
   std::copy(h, h + 16, hp.hdr);
   return GCNK_OK;
 }
@@ -1339,8 +1365,9 @@ extern "C" int64_t gcnk_spmm_workspace_bytes(const int32_t* hdr, int32_t F) {
 static int spmm_impl(const void* plan, const int32_t* hdr, const float* B, int64_t ldb, int32_t F, float* C,
                      int64_t ldc, const float* bias, int32_t epilogue, const uint8_t* drop_mask, int64_t ldm,
                      float drop_scale, float keep_prob, uint64_t seed, uint64_t offset, float* workspace,
-                     int64_t workspace_bytes, int32_t lanes_hint, const ProjArgs& pa, void* stream) {
-  if (!plan || !hdr || hdr[0] != kMagic || F < 0) {
+                     int64_t workspace_bytes, int32_t lanes_hint, const ProjArgs& pa, void* stream,
+                     int32_t part = 0) {
+  if (!plan || !hdr || hdr[0] != kMagic || F < 0 || part < 0 || part > 2) {
     set_error("gcnk_spmm_csr_f32: bad argument (plan/header missing or not a gcnk plan, F=%d)", F);
     return GCNK_EARG;
   }
@@ -1425,11 +1452,14 @@ static int spmm_impl(const void* plan, const int32_t* hdr, const float* B, int64
       return GCNK_EUNSUP;
     }
     const int4* td = reinterpret_cast<const int4*>(p + L.tdesc);
+    // part 1: the single-chunk items [0, nsingle); part 2: the rest; 0: all
+    const int32_t nsingle = hdr[15];
+    const int32_t i0 = part == 2 ? nsingle : 0, i1 = part == 1 ? nsingle : (int32_t)L.ntile;
     TileArgs ta{td, p + L.tcols, reinterpret_cast<const float*>(p + L.tfrag), p + L.trows, dval, F, B,
-                ldb, C, ldc, e, slabs, slab_ld};
-    const int rc = launch_tile(vec4, (nt_total + nslices - 1) / nslices, (unsigned)L.ntile, ta, s);
+                ldb, C, ldc, e, slabs, slab_ld, i0};
+    const int rc = launch_tile(vec4, (nt_total + nslices - 1) / nslices, (unsigned)(i1 - i0), ta, s);
     if (rc) return rc;
-    if (L.nred > 0) {
+    if (L.nred > 0 && part != 1) {
       hipLaunchKernelGGL(spmm_tile_reduce_kernel, dim3((unsigned)L.nred, kRB, (unsigned)((F + 63) / 64)), dim3(256),
                          0, s, reinterpret_cast<const int4*>(p + L.red), p + L.trows, dval, F, slabs, slab_ld, B, ldb,
                          C, ldc, e);
@@ -1438,7 +1468,7 @@ static int spmm_impl(const void* plan, const int32_t* hdr, const float* B, int64
     }
   }
   // ---- remaining rows: row kernel (heavy rows finished in-launch)
-  if (L.nunits > 0) {
+  if (L.nunits > 0 && part != 1) {
     RowPlan rp{reinterpret_cast<const int2*>(p + L.items), reinterpret_cast<const int4*>(p + L.units),
                reinterpret_cast<const int4*>(p + L.heavy), const_cast<int32_t*>(p + L.cnt), (int32_t)L.nunits,
                (int32_t)L.nhunits};
@@ -1456,6 +1486,16 @@ extern "C" int gcnk_spmm_csr_f32(const void* plan, const int32_t* hdr, const flo
   const ProjArgs none{nullptr, 0, 0, nullptr, 0, 1};
   return spmm_impl(plan, hdr, B, ldb, F, C, ldc, bias, epilogue, drop_mask, ldm, drop_scale, keep_prob, seed, offset,
                    workspace, workspace_bytes, lanes_hint, none, stream);
+}
+
+extern "C" int gcnk_spmm_csr_f32_part(const void* plan, const int32_t* hdr, const float* B, int64_t ldb,
+                                      int32_t F, float* C, int64_t ldc, const float* bias, int32_t epilogue,
+                                      const uint8_t* drop_mask, int64_t ldm, float drop_scale, float keep_prob,
+                                      uint64_t seed, uint64_t offset, float* workspace, int64_t workspace_bytes,
+                                      int32_t lanes_hint, int32_t part, void* stream) {
+  const ProjArgs none{nullptr, 0, 0, nullptr, 0, 1};
+  return spmm_impl(plan, hdr, B, ldb, F, C, ldc, bias, epilogue, drop_mask, ldm, drop_scale, keep_prob, seed, offset,
+                   workspace, workspace_bytes, lanes_hint, none, stream, part);
 }
 
 extern "C" int gcnk_spmm_proj_f32(const void* plan, const int32_t* hdr, const float* B, int64_t ldb, int32_t F,

@@ -66,17 +66,50 @@ def spmm(a, B, bias=None, epilogue=_lib.EPI_NONE, mask=None, scale=1.0, keep_pro
     plan = a.plan(ipc, groups, DENSE_THRESHOLD if dense is None else dense)
     wsb = plan.workspace_bytes(F)
     ws = torch.empty((wsb + 3) // 4, dtype=torch.float32, device=B.device) if wsb > 0 else None
-    with torch.cuda.device(B.device):
-        rc = lib.gcnk_spmm_csr_f32(
-            _ptr(plan.buf), ctypes.cast(plan.hdr, ctypes.c_void_p),
+    args = (_ptr(plan.buf), ctypes.cast(plan.hdr, ctypes.c_void_p),
             _ptr(B), B.stride(0), F,
             _ptr(out), out.stride(0),
             _ptr(bias), epilogue,
             _ptr(mask), mask.stride(0) if mask is not None else 0, float(scale),
             float(keep_prob), int(seed) & (2**64 - 1), int(offset) & (2**64 - 1),
-            _ptr(ws), wsb, int(lanes), _stream(B.device))
+            _ptr(ws), wsb, int(lanes))
+    hdr = plan.hdr
+    nsingle, ntile, nunits = int(hdr[15]), int(hdr[8]), int(hdr[5])
+    with torch.cuda.device(B.device):
+        if OVERLAP_TILE_PARTS and nsingle > 0 and (ntile > nsingle or nunits > 0):
+            # the single-chunk tile blocks on a side stream, the rest (multi-chunk
+            # blocks, their reduce launch, the row kernel) on the caller's stream;
+            # they write disjoint rows of `out` and the caller's stream joins the
+            # side stream before anything reads it (captured into hipGraphs as a
+            # fork/join)
+            main = torch.cuda.current_stream(B.device)
+            side = _side_stream(B.device)
+            side.wait_stream(main)
+            rc = lib.gcnk_spmm_csr_f32_part(*args, 1, ctypes.c_void_p(side.cuda_stream))
+            _lib.check(rc, "gcnk_spmm_csr_f32_part")
+            rc = lib.gcnk_spmm_csr_f32_part(*args, 2, _stream(B.device))
+            main.wait_stream(side)
+        else:
+            rc = lib.gcnk_spmm_csr_f32(*args, _stream(B.device))
     _lib.check(rc, "gcnk_spmm_csr_f32")
     return out
+
+
+# Overlap the two independent parts of a hybrid plan (gcnk_spmm_csr_f32_part)
+# on two streams: R8's X W1 would run its document blocks beside the dense
+# topic rows and their reduce launch.  Off: replayed from a hipGraph the
+# fork/join measured 26.2 us for X W1 against 14.2 us on one stream
+# (profiles/r01_variants.log).
+OVERLAP_TILE_PARTS = False
+_SIDE_STREAMS = {}
+
+
+def _side_stream(device):
+    idx = device.index if device.index is not None else torch.cuda.current_device()
+    st = _SIDE_STREAMS.get(idx)
+    if st is None:
+        st = _SIDE_STREAMS[idx] = torch.cuda.Stream(device=idx)
+    return st
 
 
 # Fuse gc2's H1 W2 into the gc1 aggregation epilogue (gcnk_spmm_proj_f32).

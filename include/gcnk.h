@@ -106,7 +106,8 @@ const char* gcnk_last_error(void);
  *   0 magic 'GNK5'  1 M  2 K  3 groups  4 ipc  5 row units  6 heavy segments
  *   (= partial slots)  7 heavy rows of > 1 segment  8 tile chunks
  *   9 multi-chunk blocks  10 slabs  11 tile blocks  12 diagonal kept aside
- *   (0/1)  13 nnz  14 partial slots  15 0   (tile blocks: 64 rows x 64-column chunks)
+ *   (0/1)  13 nnz  14 partial slots  15 chunk items of single-chunk tile blocks (listed
+ *   first)   (tile blocks: 64 rows x 64-column chunks)
  * ------------------------------------------------------------------------- */
 int32_t gcnk_spmm_groups(int32_t F, int32_t lanes_hint);
 int32_t gcnk_spmm_default_ipc(int32_t M, int64_t nnz, int32_t F, int32_t lanes_hint);
@@ -132,6 +133,23 @@ int gcnk_spmm_csr_f32(const void* plan, const int32_t* plan_header,
                       float keep_prob, uint64_t seed, uint64_t offset,
                       float* workspace, int64_t workspace_bytes,
                       int32_t lanes_hint, void* stream);
+
+/* The same product in two parts that write disjoint rows of C, for callers
+ * that overlap them on two streams (join both before reading C):
+ *   part 1: the single-chunk dense tile blocks (plan header word 15 items);
+ *   part 2: everything else (multi-chunk tile blocks + their slab reduce,
+ *           the row kernel);  part 0: all (= gcnk_spmm_csr_f32).
+ * Part 2 alone uses the workspace.  (R8's X W1: part 1 = the document rows,
+ * part 2 = the 50 dense topic rows, whose reduce launch then overlaps the
+ * document blocks instead of following them.) */
+int gcnk_spmm_csr_f32_part(const void* plan, const int32_t* plan_header,
+                           const float* B, int64_t ldb, int32_t F,
+                           float* C, int64_t ldc,
+                           const float* bias, int32_t epilogue,
+                           const uint8_t* drop_mask, int64_t ldm, float drop_scale,
+                           float keep_prob, uint64_t seed, uint64_t offset,
+                           float* workspace, int64_t workspace_bytes,
+                           int32_t lanes_hint, int32_t part, void* stream);
 
 /* SpMM with a fused dense projection of every finished row:
  *   H = epi(A B)  (stored to C only when C != NULL),   C2[M x P] = H * W[F x P]

@@ -534,3 +534,24 @@ def test_metrics_match_reference_restatement(nclass):
     f1, p, r = metrics.macro_f1(logits.to(DEV), targ.to(DEV))
     assert (f1, p, r) == (2 * pm * rm / (pm + rm), pm, rm)
     assert metrics.accuracy(logits.to(DEV), targ.to(DEV)) == gcn_ref.accuracy(logits, targ)
+
+
+@pytest.mark.gpu
+def test_spmm_two_part_launch_matches_single(monkeypatch, r8):
+    """gcnk_spmm_csr_f32_part: the single-chunk tile blocks on a side stream and
+    the rest on the caller's stream give the one-launch result bit for bit."""
+    from graph_convolutional_networks_for_text_classification_amd import ops
+    rng = np.random.default_rng(7)
+    for a, K in ((from_torch(r8["features"].to(DEV)), r8["nfeat"]), (None, 900)):
+        if a is None:
+            rp, ci, v = _mixed_density_csr(rng, 700, K)
+            a = from_arrays(rp, ci, v, (700, K), DEV)
+        B = torch.from_numpy(rng.standard_normal((K, 200)).astype(np.float32)).to(DEV)
+        one = ops.spmm(a, B)
+        hdr = list(a._plans.values())[-1].header
+        assert hdr[15] > 0 and hdr[8] > hdr[15], "both single- and multi-chunk tile blocks expected"
+        monkeypatch.setattr(ops, "OVERLAP_TILE_PARTS", True)
+        two = ops.spmm(a, B)
+        torch.cuda.synchronize()
+        monkeypatch.setattr(ops, "OVERLAP_TILE_PARTS", False)
+        assert torch.equal(one, two)

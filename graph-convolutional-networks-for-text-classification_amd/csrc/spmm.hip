@@ -1241,6 +1241,35 @@ int host_plan(const int32_t* rowptr_dev, const int32_t* colind_dev, const float*
             hp.units.insert(hp.units.end(), {-1, 0, 0, -1});
         }
   };
+#ifndef GCNK_LIGHT_SORT
+#define GCNK_LIGHT_SORT 1
+#endif
+  // light rows of a class ordered by their off-diagonal column lists, so the
+  // rows one workgroup (one CU's L1) gathers for share their B rows (R8: the
+  // document rows of one topic set); each row still writes its own C row
+  if (GCNK_LIGHT_SORT)
+    for (std::vector<int32_t>& q : lq) {
+      const size_t n = q.size() / 4;
+      std::vector<size_t> ord(n);
+      for (size_t i = 0; i < n; ++i) ord[i] = i;
+      auto less = [&](size_t x, size_t y) {
+        const int32_t rx = q[4 * x], ry = q[4 * y];
+        int32_t kx = q[4 * x + 1], ky = q[4 * y + 1];
+        const int32_t ex = q[4 * x + 2], ey = q[4 * y + 2];
+        for (;;) {
+          while (kx < ex && ci[(size_t)kx] == rx) ++kx;
+          while (ky < ey && ci[(size_t)ky] == ry) ++ky;
+          if (kx >= ex || ky >= ey) return kx >= ex && ky < ey;
+          if (ci[(size_t)kx] != ci[(size_t)ky]) return ci[(size_t)kx] < ci[(size_t)ky];
+          ++kx;
+          ++ky;
+        }
+      };
+      std::stable_sort(ord.begin(), ord.end(), less);
+      std::vector<int32_t> sorted(q.size());
+      for (size_t i = 0; i < n; ++i) std::copy(q.begin() + 4 * ord[i], q.begin() + 4 * ord[i] + 4, sorted.begin() + 4 * i);
+      q.swap(sorted);
+    }
   layout(hq, hpb);
   const int64_t nh = (int64_t)hp.units.size() / 4;
   layout(lq, lpb);

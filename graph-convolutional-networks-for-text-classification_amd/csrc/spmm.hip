@@ -1300,14 +1300,18 @@ extern "C" int32_t gcnk_spmm_groups(int32_t F, int32_t lanes_hint) { return 64 /
 
 extern "C" int32_t gcnk_spmm_default_ipc(int32_t M, int64_t nnz, int32_t F, int32_t lanes_hint) {
   (void)M;
-  (void)nnz;
   // each lane group's share of a heavy segment (the light-row limit is 2 * ipc
-  // at 64 lanes, ipc below): two U = 8 gather batches per wavefront at 64 lanes
-  // (heavy segments of 64 nonzeros over a 4-wavefront workgroup), one for
-  // narrow groups.  Sweeps (profiles/r01_sweep_final.log): R8 F = 200 ipc 16
-  // 10.4 us, 32 11.7, 8 14.4; 20ng-shaped 16 18.8, 32 17.2; 1M/20M F = 256
-  // 16 3.33 ms; R8 F = 8 ipc 8 5.1 us, 16 5.7.
-  return choose_lpr(F, lanes_hint) == 64 ? 16 : 8;
+  // at 64 lanes, ipc below).  Narrow groups: 8 (one U = 8 gather batch; R8
+  // F = 8 ipc 8 5.1 us, 16 5.7).  Whole-wavefront groups: heavy segments of
+  // 4 * ipc nonzeros over a 4-wavefront workgroup, sized with the operand so
+  // the heavy segments stay a few per CU: ipc ~ nnz / 5760 in [12, 32], a
+  // multiple of 4.  Sweeps after the 16-B partial accesses
+  // (profiles/r01_variants.log): R8 (69k nnz) ipc 12 8.67 us, 16 8.95, 20 9.24,
+  // 24 9.72; 20ng-shaped (175k) 12 17.9, 16 17.0, 20 16.4, 24 16.2, 32 16.4;
+  // 1M/20M F = 256: 16 and 32 both 3.37 ms.
+  if (choose_lpr(F, lanes_hint) != 64) return 8;
+  int64_t ipc = (nnz / 5760 + 2) / 4 * 4;
+  return (int32_t)std::min<int64_t>(32, std::max<int64_t>(12, ipc));
 }
 
 extern "C" int64_t gcnk_spmm_plan_bytes(const int32_t* rowptr, const int32_t* colind, int32_t M, int32_t K,

@@ -11,7 +11,10 @@ import threading
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.path.join(_HERE, "libgcnk.so")
-ABI_VERSION = 1
+# experiment scripts may point at a prebuilt variant (csrc/Makefile `variant`);
+# the tests and the product always load the in-tree library
+LIB_PATH = os.environ.get("GCNK_LIB", LIB_PATH)
+ABI_VERSION = 2
 
 # C-ABI return codes (gcnk.h)
 OK, EARG, EUNSUP, EHIP = 0, -1, -2, -3
@@ -26,14 +29,21 @@ _vp, _i32, _i64, _u64, _f32 = ctypes.c_void_p, ctypes.c_int32, ctypes.c_int64, c
 # name -> (restype, argtypes); every symbol include/gcnk.h declares
 SIGNATURES = {
     "gcnk_abi_version": (ctypes.c_int, []),
-    "gcnk_debug_set_stamps": (None, [_vp]),
+    "gcnk_debug_set_stamps": (ctypes.c_int, [_vp]),
     "gcnk_last_error": (ctypes.c_char_p, []),
     "gcnk_spmm_groups": (_i32, [_i32, _i32]),
     "gcnk_spmm_default_ipc": (_i32, [_i32, _i64, _i32, _i32]),
-    "gcnk_spmm_plan_bytes": (_i64, [_vp, _vp, _i32, _i32, _i64, _i32, _i32, _f32, _vp]),
-    "gcnk_spmm_plan_build": (ctypes.c_int, [_vp, _vp, _vp, _i32, _i32, _i64, _i32, _i32, _f32, _vp, _i64, _vp]),
+    # rowptr, colind, M, K, nnz, ipc, groups, dense_threshold, hub_min, block_rows, stream
+    "gcnk_spmm_plan_bytes": (_i64, [_vp, _vp, _i32, _i32, _i64, _i32, _i32, _f32, _i32, _i32, _vp]),
+    # rowptr, colind, val, M, K, nnz, ipc, groups, dense_threshold, hub_min, block_rows, plan, plan_bytes, stream
+    "gcnk_spmm_plan_build": (ctypes.c_int, [_vp, _vp, _vp, _i32, _i32, _i64, _i32, _i32, _f32, _i32, _i32, _vp, _i64,
+                                            _vp]),
+    "gcnk_spmm_plan_bytes_host": (_i64, [_vp, _vp, _i32, _i32, _i64, _i32, _i32, _f32, _i32, _i32]),
+    "gcnk_spmm_plan_build_host": (ctypes.c_int, [_vp, _vp, _vp, _i32, _i32, _i64, _i32, _i32, _f32, _i32, _i32, _vp,
+                                                 _i64]),
     "gcnk_spmm_plan_query": (ctypes.c_int, [_vp, _vp, _vp]),
     "gcnk_spmm_workspace_bytes": (_i64, [_vp, _i32]),
+    "gcnk_spmm_counter_bytes": (_i64, [_vp]),
     "gcnk_spmm_csr_f32": (ctypes.c_int, [
         _vp, _vp,                 # plan (device), plan header (host, 16 words)
         _vp, _i64, _i32,          # B, ldb, F
@@ -42,6 +52,7 @@ SIGNATURES = {
         _vp, _i64, _f32,          # drop_mask, ldm, drop_scale
         _f32, _u64, _u64,         # keep_prob, seed, offset
         _vp, _i64,                # workspace, workspace_bytes
+        _vp, _i64,                # counters, counter_bytes
         _i32, _vp,                # lanes_hint, stream
     ]),
     "gcnk_spmm_csr_f32_part": (ctypes.c_int, [
@@ -52,6 +63,7 @@ SIGNATURES = {
         _vp, _i64, _f32,          # drop_mask, ldm, drop_scale
         _f32, _u64, _u64,         # keep_prob, seed, offset
         _vp, _i64,                # workspace, workspace_bytes
+        _vp, _i64,                # counters, counter_bytes
         _i32, _i32, _vp,          # lanes_hint, part, stream
     ]),
     "gcnk_spmm_proj_f32": (ctypes.c_int, [
@@ -63,6 +75,7 @@ SIGNATURES = {
         _f32, _u64, _u64,         # keep_prob, seed, offset
         _vp, _i64, _i32, _vp, _i64,  # W, ldw, P, C2, ldc2
         _vp, _i64,                # workspace, workspace_bytes
+        _vp, _i64,                # counters, counter_bytes
         _i32, _vp,                # lanes_hint, stream
     ]),
     "gcnk_gemm_workspace_bytes": (_i64, [_i32, _i32, _i32, _i32]),

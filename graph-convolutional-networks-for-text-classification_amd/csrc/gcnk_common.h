@@ -5,6 +5,7 @@
 #include <stdint.h>
 #include <cstdio>
 #include <cstdarg>
+#include <vector>
 
 #include "../../include/gcnk.h"
 
@@ -25,36 +26,6 @@ inline int hip_check(hipError_t e, const char* what) {
 inline int launch_check(const char* what) { return hip_check(hipGetLastError(), what); }
 
 inline bool aligned16(const void* p) { return (reinterpret_cast<uintptr_t>(p) & 15u) == 0; }
-
-struct Coord {
-  int32_t x;  // row (merge-path: row ends consumed)
-  int32_t y;  // nonzero index (merge-path: nonzeros consumed)
-};
-
-// Plan header words (see gcnk.h): nslots, nfix, ipc, nchunks, G, nsuper, 0, 0.
-constexpr int kPlanHeader = 8;
-
-__host__ __device__ inline int64_t plan_nchunks(int32_t M, int64_t nnz, int32_t ipc) {
-  return ((int64_t)M + nnz + ipc - 1) / ipc;
-}
-
-// Plan section offsets in int32 words.  Chunks (ipc path items each) are the
-// per-group work units; a "super-chunk" is the G consecutive chunks one
-// workgroup owns.  Split-row partial slots and the fix-up list are kept per
-// super-chunk (rows split inside one workgroup are combined in LDS).
-struct PlanLayout {
-  int64_t nchunks, nsuper, coords, head, tail, fix, fix_index, total;
-  __host__ __device__ PlanLayout(int64_t nc, int32_t G) {
-    nchunks = nc;
-    nsuper = (nc + G - 1) / G;
-    coords = kPlanHeader;
-    head = coords + 2 * (nc + 1);
-    tail = head + nsuper;
-    fix = tail + nsuper;
-    fix_index = fix + 2 * nsuper;
-    total = fix_index + nsuper;
-  }
-};
 
 // ----------------------------------------------------------------------------
 // Epilogue parameters for SpMM (row-complete elements).
@@ -104,5 +75,64 @@ __device__ __forceinline__ float apply_epi(const Epi& e, float acc, float b, int
   const float u = hash_uniform(e.seed_lo, e.seed_hi, e.offset + (uint64_t)(row * e.ldm + col));
   return u < e.keep_prob ? v * e.scale : 0.0f;
 }
+
+// Column vectors of a lane: VEC = 4 (float4, 16-B accesses) or 1 (scalar).
+template <int VEC>
+struct Vec;
+
+template <>
+struct Vec<4> {
+  using T = float4;
+  static __device__ __forceinline__ T zero() { return make_float4(0.f, 0.f, 0.f, 0.f); }
+  static __device__ __forceinline__ T load(const float* p) { return *reinterpret_cast<const float4*>(p); }
+  static __device__ __forceinline__ void store(float* p, const T& v) { *reinterpret_cast<float4*>(p) = v; }
+  // one 16-B store instruction whatever the surrounding control flow
+  static __device__ __forceinline__ void store_aligned(float* p, const T& v) {
+    typedef float f4a __attribute__((ext_vector_type(4), aligned(16)));
+    *reinterpret_cast<f4a*>(__builtin_assume_aligned(p, 16)) = f4a{v.x, v.y, v.z, v.w};
+  }
+  static __device__ __forceinline__ void fma(T& acc, float a, const T& b) {
+    acc.x = fmaf(a, b.x, acc.x);
+    acc.y = fmaf(a, b.y, acc.y);
+    acc.z = fmaf(a, b.z, acc.z);
+    acc.w = fmaf(a, b.w, acc.w);
+  }
+  static __device__ __forceinline__ void add(T& acc, const T& b) {
+    acc.x += b.x; acc.y += b.y; acc.z += b.z; acc.w += b.w;
+  }
+  static __device__ __forceinline__ T epi(const Epi& e, const T& a, const T& b, int64_t row, int64_t col) {
+    T r;
+    r.x = apply_epi(e, a.x, b.x, row, col + 0);
+    r.y = apply_epi(e, a.y, b.y, row, col + 1);
+    r.z = apply_epi(e, a.z, b.z, row, col + 2);
+    r.w = apply_epi(e, a.w, b.w, row, col + 3);
+    return r;
+  }
+};
+
+template <>
+struct Vec<1> {
+  using T = float;
+  static __device__ __forceinline__ T zero() { return 0.f; }
+  static __device__ __forceinline__ T load(const float* p) { return *p; }
+  static __device__ __forceinline__ void store(float* p, const T& v) { *p = v; }
+  static __device__ __forceinline__ void store_aligned(float* p, const T& v) { *p = v; }
+  static __device__ __forceinline__ void fma(T& acc, float a, const T& b) { acc = fmaf(a, b, acc); }
+  static __device__ __forceinline__ void add(T& acc, const T& b) { acc += b; }
+  static __device__ __forceinline__ T epi(const Epi& e, const T& a, const T& b, int64_t row, int64_t col) {
+    return apply_epi(e, a, b, row, col);
+  }
+};
+
+
+// ---------------------------------------------------------------------------
+// Hub-split SpMM (hub.hip): plan builder, layout queries and the launch.
+constexpr int32_t kHubMagic = 0x474e4831;  // "GNH1"
+int hub_plan_host(const int32_t* rowptr, const int32_t* colind, const float* val, int32_t M, int32_t K, int64_t nnz,
+                  int32_t groups, int32_t hub_min, int32_t block_rows, std::vector<int32_t>& img);
+int64_t hub_plan_words(const int32_t* hdr);
+int64_t hub_workspace_bytes(const int32_t* hdr, int32_t F);
+int hub_spmm(const void* plan, const int32_t* hdr, const float* B, int64_t ldb, int32_t F, float* C, int64_t ldc,
+             const Epi& e, float* workspace, int lpr, bool vec4, hipStream_t s);
 
 }  // namespace gcnk

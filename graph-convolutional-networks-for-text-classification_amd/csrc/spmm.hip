@@ -71,47 +71,6 @@ constexpr int kWaveBlock = GCNK_WAVE_BLOCK;  // workgroup size for whole-wavefro
 constexpr int kLightRPW = GCNK_LIGHT_RPW;    // light rows per wavefront with whole-wavefront groups
 constexpr int kLightMax64 = 64 / kLightRPW;  // their nonzero limit (kLightRPW rows' items fill one 64-lane load)
 
-template <int VEC>
-struct Vec;
-
-template <>
-struct Vec<4> {
-  using T = float4;
-  static __device__ __forceinline__ T zero() { return make_float4(0.f, 0.f, 0.f, 0.f); }
-  static __device__ __forceinline__ T load(const float* p) { return *reinterpret_cast<const float4*>(p); }
-  static __device__ __forceinline__ void store(float* p, const T& v) { *reinterpret_cast<float4*>(p) = v; }
-  static __device__ __forceinline__ void fma(T& acc, float a, const T& b) {
-    acc.x = fmaf(a, b.x, acc.x);
-    acc.y = fmaf(a, b.y, acc.y);
-    acc.z = fmaf(a, b.z, acc.z);
-    acc.w = fmaf(a, b.w, acc.w);
-  }
-  static __device__ __forceinline__ void add(T& acc, const T& b) {
-    acc.x += b.x; acc.y += b.y; acc.z += b.z; acc.w += b.w;
-  }
-  static __device__ __forceinline__ T epi(const Epi& e, const T& a, const T& b, int64_t row, int64_t col) {
-    T r;
-    r.x = apply_epi(e, a.x, b.x, row, col + 0);
-    r.y = apply_epi(e, a.y, b.y, row, col + 1);
-    r.z = apply_epi(e, a.z, b.z, row, col + 2);
-    r.w = apply_epi(e, a.w, b.w, row, col + 3);
-    return r;
-  }
-};
-
-template <>
-struct Vec<1> {
-  using T = float;
-  static __device__ __forceinline__ T zero() { return 0.f; }
-  static __device__ __forceinline__ T load(const float* p) { return *p; }
-  static __device__ __forceinline__ void store(float* p, const T& v) { *p = v; }
-  static __device__ __forceinline__ void fma(T& acc, float a, const T& b) { acc = fmaf(a, b, acc); }
-  static __device__ __forceinline__ void add(T& acc, const T& b) { acc += b; }
-  static __device__ __forceinline__ T epi(const Epi& e, const T& a, const T& b, int64_t row, int64_t col) {
-    return apply_epi(e, a, b, row, col);
-  }
-};
-
 // ---------------------------------------------------------------------------
 // Plan layout (int32 words).  Header (16 words, see gcnk.h):
 //   0 magic  1 M  2 K  3 lane groups per wavefront (64 / LPR)  4 ipc (light-row limit)
@@ -122,21 +81,19 @@ struct Vec<1> {
 //   {row (-1: empty), nz begin, nz end, heavy row * 64 + segment or -1}: the
 //   heavy region first, then light rows, each laid out so that the units of
 //   workgroup b belong to XCD class b % 8 (below) | heavy int4[nheavy]
-//   {row, first partial slot, nseg, 0} | arrival counters
-//   int32[nheavy * kMaxColTiles] (zero between launches) | tile part (descriptors,
+//   {row, first partial slot, nseg, 0} | tile part (descriptors,
 //   condensed columns, A fragments, reduce list, row lists, extracted diagonal
 //   float[64 * ntblk] in block order).
 struct Layout {
   int64_t M, nnz, nunits, nhunits, nheavy, nslots, ntile, nred, ntblk, has_diag;
-  int64_t items, units, heavy, cnt, tdesc, tcols, tfrag, red, trows, dval, total;
+  int64_t items, units, heavy, tdesc, tcols, tfrag, red, trows, dval, total;
   __host__ __device__ explicit Layout(const int32_t* h) {
     M = h[1]; nunits = h[5]; nhunits = h[6]; nheavy = h[7]; ntile = h[8]; nred = h[9]; ntblk = h[11];
     has_diag = h[12]; nnz = h[13]; nslots = h[14];
     items = 16;
     units = (items + 2 * nnz + 3) & ~3LL;
     heavy = units + 4 * nunits;
-    cnt = heavy + 4 * nheavy;
-    tdesc = (cnt + (int64_t)kMaxColTiles * nheavy + 3) & ~3LL;
+    tdesc = (heavy + 4 * nheavy + 3) & ~3LL;
     tcols = tdesc + 4 * ntile;
     tfrag = (tcols + (int64_t)kKC * ntile + 3) & ~3LL;
     red = tfrag + (int64_t)kRB * kKC * ntile;
@@ -145,15 +102,6 @@ struct Layout {
     total = dval + (has_diag ? (int64_t)kRB * ntblk : 0);
   }
 };
-
-// ---------------------------------------------------------------------------
-// Plan construction: items[k] = {colind[k], val[k] bits}, CSR order (one 8-B
-// load per nonzero in the row kernel).
-__global__ void pack_items_kernel(const int32_t* __restrict__ colind, const float* __restrict__ val, int64_t nnz,
-                                  int2* __restrict__ items) {
-  const int64_t k = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-  if (k < nnz) items[k] = make_int2(colind[k], __float_as_int(val[k]));
-}
 
 // ---------------------------------------------------------------------------
 // Fused dense projection of a finished row: C2[row, :P] = h[row, :F] * W[F, P]
@@ -257,7 +205,8 @@ struct RowPlan {
   const int2* items;   // {col, value bits} per nonzero, CSR order
   const int4* units;   // {row (-1: empty), nz begin, nz end, heavy row * 64 + segment or -1}
   const int4* heavy;   // {row, first partial slot, nseg, 0}
-  int32_t* cnt;        // per heavy row x column tile: arrival counters (zero between launches)
+  int32_t* cnt;        // per heavy row x column tile: arrival counters, in the caller's
+                       // counter region (zero on entry, re-armed by each row's last arriver)
   int32_t nunits, nhunits;
 };
 
@@ -266,6 +215,13 @@ struct RowPlan {
 // so publishing them needs no L2 write-back/invalidate: the writing wave waits
 // for its stores to complete (s_waitcnt vmcnt(0)) before bumping the arrival
 // counter, and the last arriver is told so by the value its own add returns.
+// This is the hand-off MI355X_MICROARCH.md lists under "Valid forms" (every
+// store and load of the handed-off bytes sc1, each storing wave drained before
+// ONE lane of its workgroup adds to an agent-scope counter, the last adder
+// reading only after its add returned) in place of an agent release/acquire
+// pair, which would cost a full L2 write-back (~1.7 us) per segment.  The
+// counters live in a per-call region of the caller (gcnk.h): concurrent calls
+// with distinct regions never share them.
 // Whole-wavefront groups use raw-buffer instructions (a wave-uniform row base,
 // per-lane byte offsets below 2^31, checked on the host): one 16-B access per
 // lane where per-dword atomics take four (R8 A-hat F = 200: 10.6 -> 9.4 us).
@@ -749,45 +705,48 @@ spmm_tile_kernel(const int4* __restrict__ tdesc, const int32_t* __restrict__ tco
     const int64_t col = col0 + (int64_t)(e % nq4) * 4;
     if (rl >= d.y || col >= F) continue;
     float4 v = *reinterpret_cast<const float4*>(s_C + rl * CS + (col - col0));
+    // every path ends in ONE 16-B store (separate store sites are sunk into a
+    // common one that the backend splits into dword + dwordx3)
+    float* dst;
     if (!single) {  // slab rows are padded to 16 floats: whole pieces stay inside the row
-      *reinterpret_cast<float4*>(slabs + ((int64_t)d.z * kRB + rl) * slab_ld + col) = v;
-      continue;
-    }
-    const int64_t row = s_rows[rl];
-    const float dv = s_dv[rl];
-    if (VEC4 && epi.code <= GCNK_EPI_BIAS_RELU) {
-      // common case, vectorised (no dropout): + extracted diagonal * B row piece,
-      // + bias, relu
-      if (dv != 0.f) {
-        const float4 b4 = *reinterpret_cast<const float4*>(B + row * ldb + col);
-        v.x = fmaf(dv, b4.x, v.x); v.y = fmaf(dv, b4.y, v.y); v.z = fmaf(dv, b4.z, v.z); v.w = fmaf(dv, b4.w, v.w);
-      }
-      if (epi.code != GCNK_EPI_NONE) {
-        const float4 b4 = *reinterpret_cast<const float4*>(s_bias + (col - col0));
-        v.x += b4.x; v.y += b4.y; v.z += b4.z; v.w += b4.w;
-        if (epi.code == GCNK_EPI_BIAS_RELU) {
-          v.x = v.x > 0.f ? v.x : 0.f; v.y = v.y > 0.f ? v.y : 0.f;
-          v.z = v.z > 0.f ? v.z : 0.f; v.w = v.w > 0.f ? v.w : 0.f;
-        }
-      }
-      *reinterpret_cast<float4*>(C + row * ldc + col) = v;
-      continue;
-    }
-    float o[4] = {v.x, v.y, v.z, v.w};
-#pragma unroll
-    for (int i = 0; i < 4; ++i) {
-      if (col + i >= F) break;
-      if (dv != 0.f) o[i] = fmaf(dv, B[row * ldb + col + i], o[i]);
-      o[i] = apply_epi(epi, o[i], s_bias[col - col0 + i], row, col + i);
-    }
-    float* dst = C + row * ldc + col;
-    if (VEC4) {
-      *reinterpret_cast<float4*>(dst) = make_float4(o[0], o[1], o[2], o[3]);
+      dst = slabs + ((int64_t)d.z * kRB + rl) * slab_ld + col;
     } else {
+      const int64_t row = s_rows[rl];
+      const float dv = s_dv[rl];
+      dst = C + row * ldc + col;
+      if (VEC4 && epi.code <= GCNK_EPI_BIAS_RELU) {
+        // common case, vectorised (no dropout): + extracted diagonal * B row piece,
+        // + bias, relu
+        if (dv != 0.f) {
+          const float4 b4 = *reinterpret_cast<const float4*>(B + row * ldb + col);
+          v.x = fmaf(dv, b4.x, v.x); v.y = fmaf(dv, b4.y, v.y); v.z = fmaf(dv, b4.z, v.z); v.w = fmaf(dv, b4.w, v.w);
+        }
+        if (epi.code != GCNK_EPI_NONE) {
+          const float4 b4 = *reinterpret_cast<const float4*>(s_bias + (col - col0));
+          v.x += b4.x; v.y += b4.y; v.z += b4.z; v.w += b4.w;
+          if (epi.code == GCNK_EPI_BIAS_RELU) {
+            v.x = v.x > 0.f ? v.x : 0.f; v.y = v.y > 0.f ? v.y : 0.f;
+            v.z = v.z > 0.f ? v.z : 0.f; v.w = v.w > 0.f ? v.w : 0.f;
+          }
+        }
+      } else {
+        float o[4] = {v.x, v.y, v.z, v.w};
 #pragma unroll
-      for (int i = 0; i < 4; ++i)
-        if (col + i < F) dst[i] = o[i];
+        for (int i = 0; i < 4; ++i) {
+          if (col + i >= F) break;
+          if (dv != 0.f) o[i] = fmaf(dv, B[row * ldb + col + i], o[i]);
+          o[i] = apply_epi(epi, o[i], s_bias[col - col0 + i], row, col + i);
+        }
+        if (!VEC4) {
+#pragma unroll
+          for (int i = 0; i < 4; ++i)
+            if (col + i < F) dst[i] = o[i];
+          continue;
+        }
+        v = make_float4(o[0], o[1], o[2], o[3]);
+      }
     }
+    Vec<4>::store_aligned(dst, v);
   }
   stamp(epi, 3);
 }
@@ -1000,19 +959,8 @@ struct HostPlan {
   std::vector<float> tfrag, dval;  // dval: extracted diagonal of tile rows in block order (64 per block, or empty)
 };
 
-int host_plan(const int32_t* rowptr_dev, const int32_t* colind_dev, const float* val_dev, int32_t M, int32_t K,
-              int64_t nnz, int32_t ipc, int32_t groups, float dense_threshold, bool want_values, hipStream_t s,
-              HostPlan& hp) {
-  std::vector<int32_t> rp((size_t)M + 1), ci((size_t)nnz);
-  std::vector<float> vv(want_values ? (size_t)nnz : 0);
-  int rc = hip_check(hipMemcpyAsync(rp.data(), rowptr_dev, ((size_t)M + 1) * 4, hipMemcpyDeviceToHost, s),
-                     "plan rowptr copy");
-  if (!rc && nnz > 0)
-    rc = hip_check(hipMemcpyAsync(ci.data(), colind_dev, (size_t)nnz * 4, hipMemcpyDeviceToHost, s), "plan colind copy");
-  if (!rc && want_values && nnz > 0)
-    rc = hip_check(hipMemcpyAsync(vv.data(), val_dev, (size_t)nnz * 4, hipMemcpyDeviceToHost, s), "plan val copy");
-  if (rc) return rc;
-  if ((rc = hip_check(hipStreamSynchronize(s), "plan copy sync"))) return rc;
+// rowptr / colind validity (host arrays): monotone row pointers, in-range columns.
+int check_csr(const int32_t* rp, const int32_t* ci, int32_t M, int32_t K, int64_t nnz) {
   if ((int64_t)rp[M] != nnz || rp[0] != 0) {
     set_error("gcnk_spmm_plan: rowptr[0]=%d rowptr[M]=%d inconsistent with nnz=%lld", rp[0], rp[M], (long long)nnz);
     return GCNK_EARG;
@@ -1023,11 +971,17 @@ int host_plan(const int32_t* rowptr_dev, const int32_t* colind_dev, const float*
       return GCNK_EARG;
     }
   for (int64_t k = 0; k < nnz; ++k)
-    if (ci[(size_t)k] < 0 || ci[(size_t)k] >= K) {
-      set_error("gcnk_spmm_plan: column index %d out of range [0, %d) at nonzero %lld", ci[(size_t)k], K, (long long)k);
+    if (ci[k] < 0 || ci[k] >= K) {
+      set_error("gcnk_spmm_plan: column index %d out of range [0, %d) at nonzero %lld", ci[k], K, (long long)k);
       return GCNK_EARG;
     }
+  return GCNK_OK;
+}
 
+// Row-unit + dense-tile plan from host CSR arrays (vv null: layout only).
+int host_plan(const int32_t* rp, const int32_t* ci, const float* vv, int32_t M, int32_t K, int64_t nnz, int32_t ipc,
+              int32_t groups, float dense_threshold, HostPlan& hp) {
+  const bool want_values = vv != nullptr;
   // ---- dense blocks (tile path).  Rows are grouped by degree class (factor-8
   //      buckets of the off-diagonal degree), in row order within a class, 64 per
   //      block, so rows of one shape share blocks (R8: document rows vs topic rows).
@@ -1285,13 +1239,86 @@ int host_plan(const int32_t* rowptr_dev, const int32_t* colind_dev, const float*
   return GCNK_OK;
 }
 
+// Full classic plan image (header, packed items, units, heavy rows, tile part).
+void classic_image(const HostPlan& hp, const int32_t* ci, const float* vv, int64_t nnz, std::vector<int32_t>& img) {
+  const Layout L(hp.hdr);
+  img.assign((size_t)L.total, 0);
+  std::copy(hp.hdr, hp.hdr + 16, img.begin());
+  for (int64_t k = 0; k < nnz; ++k) {
+    img[(size_t)(L.items + 2 * k)] = ci[k];
+    img[(size_t)(L.items + 2 * k + 1)] = vv ? __builtin_bit_cast(int32_t, vv[k]) : 0;
+  }
+  auto put = [&](int64_t off, const int32_t* p, size_t n) { std::copy(p, p + n, img.begin() + off); };
+  auto putf = [&](int64_t off, const std::vector<float>& v) {
+    for (size_t i = 0; i < v.size(); ++i) img[(size_t)off + i] = __builtin_bit_cast(int32_t, v[i]);
+  };
+  put(L.units, hp.units.data(), hp.units.size());
+  put(L.heavy, hp.heavy.data(), hp.heavy.size());
+  put(L.tdesc, hp.tdesc.data(), hp.tdesc.size());
+  put(L.tcols, hp.tcols.data(), hp.tcols.size());
+  putf(L.tfrag, hp.tfrag);
+  put(L.red, hp.red.data(), hp.red.size());
+  put(L.trows, hp.trows.data(), hp.trows.size());
+  putf(L.dval, hp.dval);
+}
+
+// The plan image for host CSR arrays: the hub-split plan (hub.hip) when the
+// operand has hub rows and no dense tile blocks (hub_min >= 0; 0 = automatic
+// threshold), else the row-unit + tile plan.
+int build_image(const int32_t* rp, const int32_t* ci, const float* vv, int32_t M, int32_t K, int64_t nnz, int32_t ipc,
+                int32_t groups, float dense_threshold, int32_t hub_min, int32_t block_rows, std::vector<int32_t>& img) {
+  int rc = check_csr(rp, ci, M, K, nnz);
+  if (rc) return rc;
+  HostPlan hp;
+  if ((rc = host_plan(rp, ci, vv, M, K, nnz, ipc, groups, dense_threshold, hp))) return rc;
+  if (hub_min >= 0 && hp.hdr[8] == 0) {
+    rc = hub_plan_host(rp, ci, vv, M, K, nnz, groups, hub_min, block_rows, img);
+    if (rc <= 0) return rc;  // built (0) or an error; 1: not applicable
+  }
+  classic_image(hp, ci, vv, nnz, img);
+  return GCNK_OK;
+}
+
+bool plan_args_ok(const int32_t* rowptr, const int32_t* colind, int32_t M, int32_t K, int64_t nnz, int32_t ipc,
+                  int32_t groups) {
+  return rowptr && M >= 0 && K >= 0 && nnz >= 0 && nnz < INT32_MAX && ipc > 0 && groups > 0 && (nnz == 0 || colind);
+}
+
+// Device CSR -> host arrays (one-time setup: synchronises `s`).
+int fetch_csr(const int32_t* rowptr, const int32_t* colind, const float* val, int32_t M, int64_t nnz, hipStream_t s,
+              std::vector<int32_t>& rp, std::vector<int32_t>& ci, std::vector<float>& vv) {
+  rp.resize((size_t)M + 1);
+  ci.resize((size_t)nnz);
+  vv.resize(val ? (size_t)nnz : 0);
+  int rc = hip_check(hipMemcpyAsync(rp.data(), rowptr, ((size_t)M + 1) * 4, hipMemcpyDeviceToHost, s),
+                     "plan rowptr copy");
+  if (!rc && nnz > 0)
+    rc = hip_check(hipMemcpyAsync(ci.data(), colind, (size_t)nnz * 4, hipMemcpyDeviceToHost, s), "plan colind copy");
+  if (!rc && val && nnz > 0)
+    rc = hip_check(hipMemcpyAsync(vv.data(), val, (size_t)nnz * 4, hipMemcpyDeviceToHost, s), "plan val copy");
+  if (rc) return rc;
+  return hip_check(hipStreamSynchronize(s), "plan copy sync");
+}
+
 }  // namespace
 }  // namespace gcnk
 
 using namespace gcnk;
 
+#ifdef GCNK_STAMPS
 static unsigned long long* g_stamps = nullptr;
-extern "C" void gcnk_debug_set_stamps(void* buf) { g_stamps = (unsigned long long*)buf; }
+extern "C" int gcnk_debug_set_stamps(void* buf) {
+  g_stamps = (unsigned long long*)buf;
+  return GCNK_OK;
+}
+#else
+static constexpr unsigned long long* g_stamps = nullptr;
+extern "C" int gcnk_debug_set_stamps(void* buf) {
+  if (!buf) return GCNK_OK;
+  set_error("gcnk_debug_set_stamps: this libgcnk was built without GCNK_STAMPS (scripts/stamps.py builds one)");
+  return GCNK_EUNSUP;
+}
+#endif
 
 // Lane groups per wavefront (64 / LPR): identifies the launch geometry a plan
 // is laid out for (heavy segments are shared by these groups, or by the 4
@@ -1314,57 +1341,71 @@ extern "C" int32_t gcnk_spmm_default_ipc(int32_t M, int64_t nnz, int32_t F, int3
   return (int32_t)std::min<int64_t>(32, std::max<int64_t>(12, ipc));
 }
 
-extern "C" int64_t gcnk_spmm_plan_bytes(const int32_t* rowptr, const int32_t* colind, int32_t M, int32_t K,
-                                        int64_t nnz, int32_t ipc, int32_t groups, float dense_threshold,
-                                        void* stream) {
-  if (!rowptr || M < 0 || K < 0 || nnz < 0 || ipc <= 0 || groups <= 0 || (nnz > 0 && !colind)) {
+extern "C" int64_t gcnk_spmm_plan_bytes_host(const int32_t* rowptr, const int32_t* colind, int32_t M, int32_t K,
+                                             int64_t nnz, int32_t ipc, int32_t groups, float dense_threshold,
+                                             int32_t hub_min, int32_t block_rows) {
+  if (!plan_args_ok(rowptr, colind, M, K, nnz, ipc, groups)) {
     set_error("gcnk_spmm_plan_bytes: bad argument");
     return GCNK_EARG;
   }
-  HostPlan hp;
-  const int rc = host_plan(rowptr, colind, nullptr, M, K, nnz, ipc, groups, dense_threshold, false,
-                           (hipStream_t)stream, hp);
+  std::vector<int32_t> img;
+  const int rc = build_image(rowptr, colind, nullptr, M, K, nnz, ipc, groups, dense_threshold, hub_min, block_rows, img);
+  return rc ? rc : (int64_t)img.size() * 4;
+}
+
+extern "C" int gcnk_spmm_plan_build_host(const int32_t* rowptr, const int32_t* colind, const float* val, int32_t M,
+                                         int32_t K, int64_t nnz, int32_t ipc, int32_t groups, float dense_threshold,
+                                         int32_t hub_min, int32_t block_rows, int32_t* plan, int64_t plan_bytes) {
+  if (!plan_args_ok(rowptr, colind, M, K, nnz, ipc, groups) || !plan || (nnz > 0 && !val)) {
+    set_error("gcnk_spmm_plan_build_host: bad argument");
+    return GCNK_EARG;
+  }
+  std::vector<int32_t> img;
+  const int rc = build_image(rowptr, colind, val, M, K, nnz, ipc, groups, dense_threshold, hub_min, block_rows, img);
   if (rc) return rc;
-  return Layout(hp.hdr).total * 4;
+  if (plan_bytes < (int64_t)img.size() * 4) {
+    set_error("gcnk_spmm_plan_build_host: plan buffer %lld B < %lld B", (long long)plan_bytes,
+              (long long)img.size() * 4);
+    return GCNK_EARG;
+  }
+  std::copy(img.begin(), img.end(), plan);
+  return GCNK_OK;
+}
+
+extern "C" int64_t gcnk_spmm_plan_bytes(const int32_t* rowptr, const int32_t* colind, int32_t M, int32_t K,
+                                        int64_t nnz, int32_t ipc, int32_t groups, float dense_threshold,
+                                        int32_t hub_min, int32_t block_rows, void* stream) {
+  if (!plan_args_ok(rowptr, colind, M, K, nnz, ipc, groups)) {
+    set_error("gcnk_spmm_plan_bytes: bad argument");
+    return GCNK_EARG;
+  }
+  std::vector<int32_t> rp, ci, img;
+  std::vector<float> vv;
+  int rc = fetch_csr(rowptr, colind, nullptr, M, nnz, (hipStream_t)stream, rp, ci, vv);
+  if (!rc) rc = build_image(rp.data(), ci.data(), nullptr, M, K, nnz, ipc, groups, dense_threshold, hub_min, block_rows, img);
+  return rc ? rc : (int64_t)img.size() * 4;
 }
 
 extern "C" int gcnk_spmm_plan_build(const int32_t* rowptr, const int32_t* colind, const float* val, int32_t M,
                                     int32_t K, int64_t nnz, int32_t ipc, int32_t groups, float dense_threshold,
-                                    void* plan, int64_t plan_bytes, void* stream) {
-  if (!rowptr || !plan || M < 0 || K < 0 || nnz < 0 || ipc <= 0 || groups <= 0 || (nnz > 0 && (!colind || !val))) {
+                                    int32_t hub_min, int32_t block_rows, void* plan, int64_t plan_bytes,
+                                    void* stream) {
+  if (!plan_args_ok(rowptr, colind, M, K, nnz, ipc, groups) || !plan || (nnz > 0 && !val)) {
     set_error("gcnk_spmm_plan_build: bad argument (M=%d nnz=%lld ipc=%d groups=%d)", M, (long long)nnz, ipc, groups);
     return GCNK_EARG;
   }
   hipStream_t s = (hipStream_t)stream;
-  HostPlan hp;
-  int rc = host_plan(rowptr, colind, val, M, K, nnz, ipc, groups, dense_threshold, true, s, hp);
+  std::vector<int32_t> rp, ci, img;
+  std::vector<float> vv;
+  int rc = fetch_csr(rowptr, colind, val, M, nnz, s, rp, ci, vv);
+  if (!rc) rc = build_image(rp.data(), ci.data(), vv.data(), M, K, nnz, ipc, groups, dense_threshold, hub_min, block_rows, img);
   if (rc) return rc;
-  const Layout L(hp.hdr);
-  if (plan_bytes < L.total * 4) {
-    set_error("gcnk_spmm_plan_build: plan buffer %lld B < %lld B", (long long)plan_bytes, (long long)(L.total * 4));
+  if (plan_bytes < (int64_t)img.size() * 4) {
+    set_error("gcnk_spmm_plan_build: plan buffer %lld B < %lld B", (long long)plan_bytes, (long long)img.size() * 4);
     return GCNK_EARG;
   }
-  int32_t* p = (int32_t*)plan;
-  auto up = [&](int64_t off, const void* src, size_t bytes, const char* what) {
-    if (!rc && bytes > 0) rc = hip_check(hipMemcpyAsync(p + off, src, bytes, hipMemcpyHostToDevice, s), what);
-  };
-  up(0, hp.hdr, sizeof(hp.hdr), "plan header");
-  up(L.units, hp.units.data(), hp.units.size() * 4, "plan units");
-  up(L.heavy, hp.heavy.data(), hp.heavy.size() * 4, "plan heavy rows");
-  if (!rc && L.nheavy > 0)
-    rc = hip_check(hipMemsetAsync(p + L.cnt, 0, (size_t)L.nheavy * kMaxColTiles * 4, s), "plan counters");
-  up(L.tdesc, hp.tdesc.data(), hp.tdesc.size() * 4, "plan tile desc");
-  up(L.tcols, hp.tcols.data(), hp.tcols.size() * 4, "plan tile cols");
-  up(L.tfrag, hp.tfrag.data(), hp.tfrag.size() * 4, "plan tile frags");
-  up(L.red, hp.red.data(), hp.red.size() * 4, "plan tile reduce");
-  up(L.trows, hp.trows.data(), hp.trows.size() * 4, "plan tile rows");
-  up(L.dval, hp.dval.data(), hp.dval.size() * 4, "plan diagonal");
-  if (!rc && nnz > 0) {
-    hipLaunchKernelGGL(pack_items_kernel, dim3((unsigned)((nnz + 255) / 256)), dim3(256), 0, s, colind, val, nnz,
-                       reinterpret_cast<int2*>(p + L.items));
-    rc = launch_check("pack_items_kernel");
-  }
-  // the host vectors must outlive the async copies
+  rc = hip_check(hipMemcpyAsync(plan, img.data(), img.size() * 4, hipMemcpyHostToDevice, s), "plan upload");
+  // the host image must outlive the async copy
   const int rc2 = hip_check(hipStreamSynchronize(s), "plan build sync");
   return rc ? rc : rc2;
 }
@@ -1378,7 +1419,7 @@ extern "C" int gcnk_spmm_plan_query(const void* plan, int32_t* out16, void* stre
   int rc = hip_check(hipMemcpyAsync(out16, plan, 64, hipMemcpyDeviceToHost, s), "plan query copy");
   if (rc) return rc;
   rc = hip_check(hipStreamSynchronize(s), "plan query sync");
-  if (!rc && out16[0] != kMagic) {
+  if (!rc && out16[0] != kMagic && out16[0] != kHubMagic) {
     set_error("gcnk_spmm_plan_query: not a gcnk plan");
     return GCNK_EARG;
   }
@@ -1387,23 +1428,33 @@ extern "C" int gcnk_spmm_plan_query(const void* plan, int32_t* out16, void* stre
 
 static int64_t tile_fpad(int32_t F) { return ((int64_t)F + 15) & ~15LL; }
 
+static bool plan_magic(const int32_t* hdr) { return hdr && (hdr[0] == kMagic || hdr[0] == kHubMagic); }
+
 extern "C" int64_t gcnk_spmm_workspace_bytes(const int32_t* hdr, int32_t F) {
-  if (!hdr || hdr[0] != kMagic || F < 0) return GCNK_EARG;
+  if (!plan_magic(hdr) || F < 0) return GCNK_EARG;
+  if (hdr[0] == kHubMagic) return hub_workspace_bytes(hdr, F);
   const int64_t ld = ((int64_t)F + 3) & ~3LL;
   const int64_t rows = (int64_t)hdr[14] * ld * 4;
   const int64_t slabs = (int64_t)hdr[10] * kRB * tile_fpad(F) * 4;
   return ((rows + 255) & ~255LL) + slabs;
 }
 
+extern "C" int64_t gcnk_spmm_counter_bytes(const int32_t* hdr) {
+  if (!plan_magic(hdr)) return GCNK_EARG;
+  if (hdr[0] == kHubMagic) return 0;
+  return (int64_t)hdr[7] * kMaxColTiles * 4;
+}
+
 static int spmm_impl(const void* plan, const int32_t* hdr, const float* B, int64_t ldb, int32_t F, float* C,
                      int64_t ldc, const float* bias, int32_t epilogue, const uint8_t* drop_mask, int64_t ldm,
                      float drop_scale, float keep_prob, uint64_t seed, uint64_t offset, float* workspace,
-                     int64_t workspace_bytes, int32_t lanes_hint, const ProjArgs& pa, void* stream,
-                     int32_t part = 0) {
-  if (!plan || !hdr || hdr[0] != kMagic || F < 0 || part < 0 || part > 2) {
+                     int64_t workspace_bytes, int32_t* counters, int64_t counter_bytes, int32_t lanes_hint,
+                     const ProjArgs& pa, void* stream, int32_t part = 0) {
+  if (!plan || !plan_magic(hdr) || F < 0 || part < 0 || part > 2) {
     set_error("gcnk_spmm_csr_f32: bad argument (plan/header missing or not a gcnk plan, F=%d)", F);
     return GCNK_EARG;
   }
+  const bool hub = hdr[0] == kHubMagic;
   const int32_t M = hdr[1], K = hdr[2];
   if (M == 0 || F == 0) return GCNK_OK;
   const bool proj = pa.W != nullptr;
@@ -1440,6 +1491,12 @@ static int spmm_impl(const void* plan, const int32_t* hdr, const float* B, int64
               (long long)workspace_bytes);
     return GCNK_EARG;
   }
+  const int64_t cneed = gcnk_spmm_counter_bytes(hdr);
+  if (cneed > 0 && (!counters || counter_bytes < cneed)) {
+    set_error("gcnk_spmm_csr_f32: plan needs a zeroed counter region of %lld B, got %lld", (long long)cneed,
+              (long long)counter_bytes);
+    return GCNK_EARG;
+  }
   Epi e;
   e.bias = bias;
   e.mask = drop_mask;
@@ -1453,6 +1510,15 @@ static int spmm_impl(const void* plan, const int32_t* hdr, const float* B, int64
   e.stamps = g_stamps;
   const bool vec4 = (F % 4 == 0) && (ldb % 4 == 0) && (ldc % 4 == 0) && aligned16(B) && (!C || aligned16(C)) &&
                     (!workspace || aligned16(workspace)) && (!bias || aligned16(bias));
+  hipStream_t s = (hipStream_t)stream;
+  if (hub) {
+    if (proj) {
+      set_error("gcnk_spmm_proj_f32: fused projection unsupported with a hub plan");
+      return GCNK_EUNSUP;
+    }
+    if (part == 1) return GCNK_OK;  // no dense tile blocks in a hub plan
+    return hub_spmm(plan, hdr, B, ldb, F, C, ldc, e, workspace, lpr, vec4, s);
+  }
   if (proj) {
     // the projection needs whole rows in one group: row-kernel rows only, float4, one column tile
     if (hdr[8] > 0 || !vec4 || F > lpr * 4 || pa.P > 32 || lpr < 16) {
@@ -1461,7 +1527,6 @@ static int spmm_impl(const void* plan, const int32_t* hdr, const float* B, int64
       return GCNK_EUNSUP;
     }
   }
-  hipStream_t s = (hipStream_t)stream;
   const int32_t* p = (const int32_t*)plan;
   const Layout L(hdr);
   const int64_t part_ld = ((int64_t)F + 3) & ~3LL;
@@ -1503,8 +1568,7 @@ static int spmm_impl(const void* plan, const int32_t* hdr, const float* B, int64
   // ---- remaining rows: row kernel (heavy rows finished in-launch)
   if (L.nunits > 0 && part != 1) {
     RowPlan rp{reinterpret_cast<const int2*>(p + L.items), reinterpret_cast<const int4*>(p + L.units),
-               reinterpret_cast<const int4*>(p + L.heavy), const_cast<int32_t*>(p + L.cnt), (int32_t)L.nunits,
-               (int32_t)L.nhunits};
+               reinterpret_cast<const int4*>(p + L.heavy), counters, (int32_t)L.nunits, (int32_t)L.nhunits};
     RowLaunch a{rp, B, ldb, F, C, ldc, e, workspace, part_ld, pa, s};
     if (proj) return pa.P <= 8 ? dispatch_rows_proj<8>(lpr, a) : dispatch_rows_proj<32>(lpr, a);
     return vec4 ? dispatch_rows<4>(lpr, a) : dispatch_rows<1>(lpr, a);
@@ -1515,33 +1579,35 @@ static int spmm_impl(const void* plan, const int32_t* hdr, const float* B, int64
 extern "C" int gcnk_spmm_csr_f32(const void* plan, const int32_t* hdr, const float* B, int64_t ldb, int32_t F,
                                  float* C, int64_t ldc, const float* bias, int32_t epilogue, const uint8_t* drop_mask,
                                  int64_t ldm, float drop_scale, float keep_prob, uint64_t seed, uint64_t offset,
-                                 float* workspace, int64_t workspace_bytes, int32_t lanes_hint, void* stream) {
+                                 float* workspace, int64_t workspace_bytes, int32_t* counters, int64_t counter_bytes,
+                                 int32_t lanes_hint, void* stream) {
   const ProjArgs none{nullptr, 0, 0, nullptr, 0, 1};
   return spmm_impl(plan, hdr, B, ldb, F, C, ldc, bias, epilogue, drop_mask, ldm, drop_scale, keep_prob, seed, offset,
-                   workspace, workspace_bytes, lanes_hint, none, stream);
+                   workspace, workspace_bytes, counters, counter_bytes, lanes_hint, none, stream);
 }
 
 extern "C" int gcnk_spmm_csr_f32_part(const void* plan, const int32_t* hdr, const float* B, int64_t ldb,
                                       int32_t F, float* C, int64_t ldc, const float* bias, int32_t epilogue,
                                       const uint8_t* drop_mask, int64_t ldm, float drop_scale, float keep_prob,
                                       uint64_t seed, uint64_t offset, float* workspace, int64_t workspace_bytes,
-                                      int32_t lanes_hint, int32_t part, void* stream) {
+                                      int32_t* counters, int64_t counter_bytes, int32_t lanes_hint, int32_t part,
+                                      void* stream) {
   const ProjArgs none{nullptr, 0, 0, nullptr, 0, 1};
   return spmm_impl(plan, hdr, B, ldb, F, C, ldc, bias, epilogue, drop_mask, ldm, drop_scale, keep_prob, seed, offset,
-                   workspace, workspace_bytes, lanes_hint, none, stream, part);
+                   workspace, workspace_bytes, counters, counter_bytes, lanes_hint, none, stream, part);
 }
 
 extern "C" int gcnk_spmm_proj_f32(const void* plan, const int32_t* hdr, const float* B, int64_t ldb, int32_t F,
                                   float* C, int64_t ldc, const float* bias, int32_t epilogue,
                                   const uint8_t* drop_mask, int64_t ldm, float drop_scale, float keep_prob,
                                   uint64_t seed, uint64_t offset, const float* W, int64_t ldw, int32_t P, float* C2,
-                                  int64_t ldc2, float* workspace, int64_t workspace_bytes, int32_t lanes_hint,
-                                  void* stream) {
+                                  int64_t ldc2, float* workspace, int64_t workspace_bytes, int32_t* counters,
+                                  int64_t counter_bytes, int32_t lanes_hint, void* stream) {
   if (!W) {
     set_error("gcnk_spmm_proj_f32: null projection matrix");
     return GCNK_EARG;
   }
   const ProjArgs pa{W, ldw, P, C2, ldc2, C != nullptr};
   return spmm_impl(plan, hdr, B, ldb, F, C, ldc, bias, epilogue, drop_mask, ldm, drop_scale, keep_prob, seed, offset,
-                   workspace, workspace_bytes, lanes_hint, pa, stream);
+                   workspace, workspace_bytes, counters, counter_bytes, lanes_hint, pa, stream);
 }

@@ -66,13 +66,14 @@ def spmm(a, B, bias=None, epilogue=_lib.EPI_NONE, mask=None, scale=1.0, keep_pro
     plan = a.plan(ipc, groups, DENSE_THRESHOLD if dense is None else dense)
     wsb = plan.workspace_bytes(F)
     ws = torch.empty((wsb + 3) // 4, dtype=torch.float32, device=B.device) if wsb > 0 else None
+    cnt = plan.counters(B.device)
     args = (_ptr(plan.buf), ctypes.cast(plan.hdr, ctypes.c_void_p),
             _ptr(B), B.stride(0), F,
             _ptr(out), out.stride(0),
             _ptr(bias), epilogue,
             _ptr(mask), mask.stride(0) if mask is not None else 0, float(scale),
             float(keep_prob), int(seed) & (2**64 - 1), int(offset) & (2**64 - 1),
-            _ptr(ws), wsb, int(lanes))
+            _ptr(ws), wsb, _ptr(cnt), 4 * cnt.numel() if cnt is not None else 0, int(lanes))
     hdr = plan.hdr
     nsingle, ntile, nunits = int(hdr[15]), int(hdr[8]), int(hdr[5])
     with torch.cuda.device(B.device):
@@ -151,6 +152,7 @@ def spmm_proj(a, B, W, bias=None, epilogue=_lib.EPI_NONE, mask=None, scale=1.0, 
         mask = mask.contiguous()
     wsb = plan.workspace_bytes(F)
     ws = torch.empty((wsb + 3) // 4, dtype=torch.float32, device=B.device) if wsb > 0 else None
+    cnt = plan.counters(B.device)
     with torch.cuda.device(B.device):
         rc = lib.gcnk_spmm_proj_f32(
             _ptr(plan.buf), ctypes.cast(plan.hdr, ctypes.c_void_p),
@@ -160,7 +162,7 @@ def spmm_proj(a, B, W, bias=None, epilogue=_lib.EPI_NONE, mask=None, scale=1.0, 
             _ptr(mask), mask.stride(0) if mask is not None else 0, float(scale),
             float(keep_prob), int(seed) & (2**64 - 1), int(offset) & (2**64 - 1),
             _ptr(W), W.stride(0), P, _ptr(C2), C2.stride(0),
-            _ptr(ws), wsb, int(lanes), _stream(B.device))
+            _ptr(ws), wsb, _ptr(cnt), 4 * cnt.numel() if cnt is not None else 0, int(lanes), _stream(B.device))
     if rc == _lib.EUNSUP:
         H = spmm(a, B, bias=bias, epilogue=epilogue, mask=mask, scale=scale, keep_prob=keep_prob, seed=seed,
                  offset=offset, ipc=ipc, lanes=lanes)

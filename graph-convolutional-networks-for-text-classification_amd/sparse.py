@@ -11,7 +11,8 @@ class) and later calls hit the cache.
 
 HBM layout of one CSR operand (M rows, K cols, nnz nonzeros):
   rowptr int32[M+1] | colind int32[nnz] | val fp32[nnz]
-  plan   int32[...]  row units + dense tile blocks (include/gcnk.h), one per (ipc, groups, threshold)
+  plan   int32[...]  hub-split plan, or row units + dense tile blocks (include/gcnk.h),
+                     one per (ipc, groups, threshold, hub options)
 """
 import collections
 import ctypes
@@ -37,22 +38,58 @@ def require_device(t, what):
 
 
 DENSE_THRESHOLD = 0.25  # row blocks at least this dense (condensed) run on the MFMA tile path
+HUB_MIN = 0             # hub-split plan: 0 = automatic hub threshold, > 0 = degree threshold, < 0 = never
+HUB_BLOCK_ROWS = 0      # light rows per hub-plan block (0 = automatic, ~256 blocks)
 
 
 class Plan:
-    """A built SpMM plan: device buffer + the 16-word host header (gcnk.h)."""
+    """A built SpMM plan: device buffer + the 16-word host header (gcnk.h).
 
-    __slots__ = ("buf", "hdr")
+    Row-unit plans with multi-segment heavy rows also need a zeroed counter
+    region per call (gcnk_spmm_counter_bytes); one is kept per stream, so
+    calls on different streams (or the autograd thread's) never share one."""
+
+    __slots__ = ("buf", "hdr", "_counters", "_lock")
+    HUB_MAGIC = 0x474e4831
 
     def __init__(self, buf, hdr):
         self.buf, self.hdr = buf, hdr
+        self._counters = {}
+        self._lock = threading.Lock()
 
     @property
     def header(self):
         return list(self.hdr)
 
+    @property
+    def is_hub(self):
+        return self.hdr[0] == self.HUB_MAGIC
+
     def workspace_bytes(self, F):
         return int(_lib.load().gcnk_spmm_workspace_bytes(ctypes.cast(self.hdr, ctypes.c_void_p), int(F)))
+
+    def counter_bytes(self):
+        return int(_lib.load().gcnk_spmm_counter_bytes(ctypes.cast(self.hdr, ctypes.c_void_p)))
+
+    def counters(self, device):
+        """Zeroed int32 counter region for a call on torch's current stream (None
+        when the plan needs none).  The kernels leave it zeroed, so it is reused
+        by later calls on the same stream; inside a hipGraph capture a fresh
+        region is zeroed by a captured memset instead (the graph owns it)."""
+        n = self.counter_bytes()
+        if n <= 0:
+            return None
+        words = (n + 3) // 4
+        if torch.cuda.is_current_stream_capturing():
+            return torch.zeros(words, dtype=torch.int32, device=device)
+        key = torch.cuda.current_stream(device).cuda_stream
+        c = self._counters.get(key)
+        if c is None:
+            with self._lock:
+                c = self._counters.get(key)
+                if c is None:
+                    c = self._counters[key] = torch.zeros(words, dtype=torch.int32, device=device)
+        return c
 
 
 class CSR:
@@ -73,9 +110,11 @@ class CSR:
         return f"CSR(shape={self.shape}, nnz={self.nnz}, device={self.device})"
 
     # -- hybrid plan (gcnk_spmm_plan_build), one per (ipc, groups, dense threshold) -------
-    def plan(self, ipc, groups, dense_threshold=DENSE_THRESHOLD):
+    def plan(self, ipc, groups, dense_threshold=DENSE_THRESHOLD, hub_min=None, block_rows=None):
         """Returns a Plan (device buffer + host header); built once per key (setup sync)."""
-        key = (ipc, groups, float(dense_threshold))
+        hub_min = HUB_MIN if hub_min is None else int(hub_min)
+        block_rows = HUB_BLOCK_ROWS if block_rows is None else int(block_rows)
+        key = (ipc, groups, float(dense_threshold), hub_min, block_rows)
         p = self._plans.get(key)
         if p is not None:
             return p
@@ -88,13 +127,14 @@ class CSR:
             with torch.cuda.device(self.device):
                 s = _stream_ptr(self.device)
                 nbytes = lib.gcnk_spmm_plan_bytes(self.rowptr.data_ptr(), self.colind.data_ptr(), M, K, self.nnz,
-                                                  ipc, groups, float(dense_threshold), s)
+                                                  ipc, groups, float(dense_threshold), hub_min, block_rows, s)
                 if nbytes < 0:
                     _lib.check(int(nbytes), "gcnk_spmm_plan_bytes")
                 buf = torch.empty((nbytes + 3) // 4, dtype=torch.int32, device=self.device)
                 _lib.check(lib.gcnk_spmm_plan_build(self.rowptr.data_ptr(), self.colind.data_ptr(),
                                                     self.val.data_ptr(), M, K, self.nnz, ipc, groups,
-                                                    float(dense_threshold), buf.data_ptr(), nbytes, s),
+                                                    float(dense_threshold), hub_min, block_rows, buf.data_ptr(),
+                                                    nbytes, s),
                            "gcnk_spmm_plan_build")
                 hdr = (ctypes.c_int32 * 16)()
                 _lib.check(lib.gcnk_spmm_plan_query(buf.data_ptr(), ctypes.cast(hdr, ctypes.c_void_p), s),

@@ -34,7 +34,11 @@
  *   - Return 0 on success; GCNK_EARG (-1) bad argument/shape, GCNK_EUNSUP (-2)
  *     unsupported configuration, GCNK_EHIP (-3) HIP launch/runtime error.
  *     The message is in a thread-local buffer returned by gcnk_last_error().
- *   - Reentrant: no global mutable state besides the thread-local error text.
+ *   - Reentrant and thread-safe: no global mutable state besides the
+ *     thread-local error text (and a per-kernel one-time LDS-limit attribute).
+ *     Calls that may run concurrently (two streams, the autograd thread beside
+ *     the caller's) must not share a workspace or a counter region; plans
+ *     are read-only after gcnk_spmm_plan_build and may be shared freely.
  */
 #ifndef GCNK_H_
 #define GCNK_H_
@@ -45,7 +49,7 @@
 extern "C" {
 #endif
 
-#define GCNK_ABI_VERSION 1
+#define GCNK_ABI_VERSION 2
 
 #define GCNK_OK 0
 #define GCNK_EARG (-1)
@@ -76,8 +80,22 @@ const char* gcnk_last_error(void);
  * Replaces th.spmm(adj, support) (layer.py:106) and th.spmm(X, W)
  * (layer.py:102, sparse X) and their autograd (A^T g, X^T g).
  *
- * The operand is converted once (gcnk_spmm_plan_build) into a hybrid plan
- * whose two parts write disjoint rows of C:
+ * The operand is converted once (gcnk_spmm_plan_build) into one of two plans:
+ *
+ *  HUB plan (header magic 'GNH1') -- operands with a few heavy "hub" rows
+ *  (degree >= hub_min; 0 = automatic: max(64, 8 x mean degree)) holding at
+ *  least a quarter of the nonzeros, and no dense tile blocks: the reference's
+ *  doc-topic adjacency (R8: 50 topic rows of 191..1807 nonzeros, 7,674
+ *  document rows of 2..14).  Light rows are sorted by the hub columns they
+ *  reference and cut into blocks of `block_rows` (0 = ~256 blocks, 4..64
+ *  rows); one workgroup per block stages the block's distinct B rows in LDS
+ *  once (at most 64) and computes its rows from LDS.  Hub rows are computed
+ *  transposed: the block owning light row j (column j) adds A[h, j] * B[j]
+ *  over its own j into one partial row per hub it touches, and a second small
+ *  kernel sums each hub's partials in block order (+ the hub's nonzeros over
+ *  columns no block owns).  Two launches, no counters, no atomics.
+ *
+ *  ROW-UNIT + TILE plan (magic 'GNK5') -- every other operand:
  *  - dense blocks: rows are grouped by off-diagonal degree class (factor-8
  *    buckets, row order within a class) into blocks of 64; a block whose
  *    nonzeros fill >= dense_threshold of its condensed column set (and use
@@ -94,35 +112,50 @@ const char* gcnk_last_error(void);
  *    wavefront, or the 4 wavefronts of a workgroup when LPR = 64) that take
  *    interleaved nonzeros and meet in a fixed-order reduction; a row of
  *    several segments leaves one partial per segment and the last segment to
- *    finish (arrival counters kept in the plan: launches sharing one plan
- *    must be ordered on one stream) sums them in segment order.
+ *    finish (arrival counters in the caller's COUNTER REGION: int32
+ *    gcnk_spmm_counter_bytes(header) bytes, zero on entry and left zero on
+ *    return) sums them in segment order.
+ * hub_min < 0 forces the row-unit plan.
  * All sums have a fixed order (no float atomics): bitwise reproducible.
  * gcnk_spmm_groups(F, lanes_hint) gives the `groups` the kernels use for a
  * width F; a plan serves every F with that count.  The plan copies the
  * values: rebuild it when they change.  Building copies the CSR to the host
- * and synchronises `stream` (one-time setup).
+ * and synchronises `stream` (one-time setup).  The _host variants build the
+ * same plan image from HOST arrays into host memory (no device needed).
  *
  * Plan header (16 int32, first words of the plan; gcnk_spmm_plan_query):
- *   0 magic 'GNK5'  1 M  2 K  3 groups  4 ipc  5 row units  6 heavy segments
- *   (= partial slots)  7 heavy rows of > 1 segment  8 tile chunks
+ *   row-unit plan: 0 magic 'GNK5'  1 M  2 K  3 groups  4 ipc  5 row units
+ *   6 heavy segments  7 heavy rows of > 1 segment  8 tile chunks
  *   9 multi-chunk blocks  10 slabs  11 tile blocks  12 diagonal kept aside
- *   (0/1)  13 nnz  14 partial slots  15 chunk items of single-chunk tile blocks (listed
- *   first)   (tile blocks: 64 rows x 64-column chunks)
+ *   (0/1)  13 nnz  14 partial slots  15 chunk items of single-chunk tile blocks
+ *   hub plan: 0 magic 'GNH1'  1 M  2 K  3 groups  4 light blocks  5 record
+ *   stride (words)  6 hub rows  7 partial rows  8 max staged rows per block
+ *   9 nnz  10 leftover hub nonzeros  11 light rows  12 rows per block
+ *   13 hub degree threshold  14 stage slots  15 0
  * ------------------------------------------------------------------------- */
 int32_t gcnk_spmm_groups(int32_t F, int32_t lanes_hint);
 int32_t gcnk_spmm_default_ipc(int32_t M, int64_t nnz, int32_t F, int32_t lanes_hint);
 /* Size of the plan buffer (synchronises `stream`; negative error code on failure). */
 int64_t gcnk_spmm_plan_bytes(const int32_t* rowptr, const int32_t* colind, int32_t M, int32_t K,
                              int64_t nnz, int32_t ipc, int32_t groups, float dense_threshold,
-                             void* stream);
+                             int32_t hub_min, int32_t block_rows, void* stream);
 int gcnk_spmm_plan_build(const int32_t* rowptr, const int32_t* colind, const float* val, int32_t M,
                          int32_t K, int64_t nnz, int32_t ipc, int32_t groups, float dense_threshold,
-                         void* plan, int64_t plan_bytes, void* stream);
+                         int32_t hub_min, int32_t block_rows, void* plan, int64_t plan_bytes, void* stream);
+/* The same from HOST arrays into a HOST buffer (plan-layout checks without a GPU). */
+int64_t gcnk_spmm_plan_bytes_host(const int32_t* rowptr, const int32_t* colind, int32_t M, int32_t K,
+                                  int64_t nnz, int32_t ipc, int32_t groups, float dense_threshold,
+                                  int32_t hub_min, int32_t block_rows);
+int gcnk_spmm_plan_build_host(const int32_t* rowptr, const int32_t* colind, const float* val, int32_t M,
+                              int32_t K, int64_t nnz, int32_t ipc, int32_t groups, float dense_threshold,
+                              int32_t hub_min, int32_t block_rows, int32_t* plan, int64_t plan_bytes);
 /* Copies the 16-word plan header to host memory `out16` and synchronises
  * `stream` (one-time setup).  Every SpMM call takes this host header. */
 int gcnk_spmm_plan_query(const void* plan, int32_t* out16, void* stream);
-/* Bytes of workspace (split-row partials + tile slabs) an SpMM of width F needs. */
+/* Bytes of workspace (split-row partials, tile slabs, hub partials) an SpMM of width F needs. */
 int64_t gcnk_spmm_workspace_bytes(const int32_t* plan_header, int32_t F);
+/* Bytes of the zero-initialised counter region a call needs (0: none). */
+int64_t gcnk_spmm_counter_bytes(const int32_t* plan_header);
 
 /* C = epi(A B) for the operand of `plan` (M x K from the header). */
 int gcnk_spmm_csr_f32(const void* plan, const int32_t* plan_header,
@@ -132,6 +165,7 @@ int gcnk_spmm_csr_f32(const void* plan, const int32_t* plan_header,
                       const uint8_t* drop_mask, int64_t ldm, float drop_scale,
                       float keep_prob, uint64_t seed, uint64_t offset,
                       float* workspace, int64_t workspace_bytes,
+                      int32_t* counters, int64_t counter_bytes,
                       int32_t lanes_hint, void* stream);
 
 /* The same product in two parts that write disjoint rows of C, for callers
@@ -149,6 +183,7 @@ int gcnk_spmm_csr_f32_part(const void* plan, const int32_t* plan_header,
                            const uint8_t* drop_mask, int64_t ldm, float drop_scale,
                            float keep_prob, uint64_t seed, uint64_t offset,
                            float* workspace, int64_t workspace_bytes,
+                           int32_t* counters, int64_t counter_bytes,
                            int32_t lanes_hint, int32_t part, void* stream);
 
 /* SpMM with a fused dense projection of every finished row:
@@ -167,6 +202,7 @@ int gcnk_spmm_proj_f32(const void* plan, const int32_t* plan_header,
                        float keep_prob, uint64_t seed, uint64_t offset,
                        const float* W, int64_t ldw, int32_t P, float* C2, int64_t ldc2,
                        float* workspace, int64_t workspace_bytes,
+                       int32_t* counters, int64_t counter_bytes,
                        int32_t lanes_hint, void* stream);
 
 /* ---------------------------------------------------------------------------
@@ -247,10 +283,12 @@ int gcnk_class_stats(const float* logits, int64_t ld, const int64_t* target, con
 int gcnk_edgelist_size(const char* path, int64_t* n_nodes, int64_t* nnz);
 int gcnk_edgelist_csr(const char* path, int64_t n_nodes, int64_t nnz, int32_t* rowptr, int32_t* colind, float* val);
 
-/* Debug only: when `buf` is non-null every later SpMM main-kernel launch
- * writes 4 x uint64 s_memrealtime stamps (100 MHz) per workgroup to it
- * (entry, items staged, chunk walked, exit).  Not thread-safe; pass NULL to stop. */
-void gcnk_debug_set_stamps(void* buf);
+/* Debug only: in a library built with -DGCNK_STAMPS, when `buf` is non-null
+ * every later row/tile SpMM launch writes 4 x uint64 s_memrealtime stamps
+ * (100 MHz) per workgroup to it (entry, items staged, chunk walked, exit).
+ * Process-global and not thread-safe, which is why the product build
+ * compiles it out: there it returns GCNK_EUNSUP for a non-null buffer. */
+int gcnk_debug_set_stamps(void* buf);
 
 #ifdef __cplusplus
 }

@@ -1,0 +1,112 @@
+"""North-star op probe: R8 A-hat x S (F = 200, bias + ReLU) and F = 8 under
+plan variants, warm (same buffers back to back) and cold (rotating > 256 MB of
+distinct B / C sets, so no launch finds its operands in the Infinity Cache),
+with parity against the float64 oracle.  One JSON line per variant.
+
+  python scripts/hub_probe.py [--reps 200] [--variants hub,row,hub16,...]
+"""
+import argparse
+import json
+import os
+import sys
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, ROOT)
+
+import numpy as np  # noqa: E402
+import torch  # noqa: E402
+
+import gcn_amd  # noqa: E402,F401
+from graph_convolutional_networks_for_text_classification_amd import _lib, datasets, ops  # noqa: E402
+from graph_convolutional_networks_for_text_classification_amd.sparse import from_torch  # noqa: E402
+from oracle import csr_ref  # noqa: E402
+
+VARIANTS = {
+    "row": dict(hub_min=-1),
+    "hub": dict(hub_min=0, block_rows=0),
+    "hub16": dict(hub_min=0, block_rows=16),
+    "hub24": dict(hub_min=0, block_rows=24),
+    "hub48": dict(hub_min=0, block_rows=48),
+    "hub64": dict(hub_min=0, block_rows=64),
+}
+
+
+def spmm_bytes(M, K, nnz, F):
+    return 4 * (M + 1) + 8 * nnz + 4 * K * F + 4 * M * F
+
+
+def time_graph(fns, reps_per_fn):
+    """Average us per call of a hipGraph replaying fns round-robin."""
+    for f in fns:
+        f()
+    torch.cuda.synchronize()
+    g = torch.cuda.CUDAGraph()
+    n = 0
+    with torch.cuda.graph(g):
+        for _ in range(reps_per_fn):
+            for f in fns:
+                f()
+                n += 1
+    g.replay()
+    torch.cuda.synchronize()
+    best = None
+    for _ in range(5):
+        e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        e0.record()
+        g.replay()
+        e1.record()
+        e1.synchronize()
+        us = e0.elapsed_time(e1) * 1e3 / n
+        best = us if best is None else min(best, us)
+    del g
+    return best
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--reps", type=int, default=100)
+    ap.add_argument("--variants", default="row,hub,hub16,hub24,hub48,hub64")
+    ap.add_argument("--widths", default="200,8")
+    ap.add_argument("--graph", default="r8", choices=["r8", "20ng"])
+    args = ap.parse_args()
+    dev = torch.device("cuda", 0)
+    if args.graph == "r8":
+        g = datasets.load_r8_fixture(os.path.join(ROOT, "tests", "golden", "r8_graph.npz"))
+    else:
+        g = datasets.doc_topic_graph(18846, 70, 20, seed=0)
+    a = from_torch(g["adj"].to(dev))
+    M = a.shape[0]
+    rp, ci, v = (t.cpu().numpy() for t in (a.rowptr, a.colind, a.val))
+    for F in (int(x) for x in args.widths.split(",")):
+        Bh = np.random.default_rng(F).standard_normal((M, F)).astype(np.float32)
+        bias = torch.from_numpy(np.random.default_rng(F + 1).standard_normal(F).astype(np.float32)).to(dev)
+        ref = csr_ref.spmm_epilogue(csr_ref.spmm_csr(rp, ci, v, Bh), bias.cpu().numpy(), relu=True)
+        nbytes = spmm_bytes(M, M, a.nnz, F)
+        nsets = max(2, int(np.ceil(300e6 / (2 * 4 * M * F))))
+        Bs = [torch.from_numpy(Bh).to(dev) for _ in range(nsets)]
+        Cs = [torch.empty(M, F, device=dev) for _ in range(nsets)]
+        for name in args.variants.split(","):
+            kw = VARIANTS[name]
+            import graph_convolutional_networks_for_text_classification_amd.sparse as sp
+            sp.HUB_MIN, sp.HUB_BLOCK_ROWS = kw.get("hub_min", 0), kw.get("block_rows", 0)
+            out = ops.spmm(a, Bs[0], bias=bias, epilogue=_lib.EPI_BIAS_RELU)
+            torch.cuda.synchronize()
+            err = float(np.abs(out.cpu().numpy().astype(np.float64) - ref).max())
+            again = ops.spmm(a, Bs[0], bias=bias, epilogue=_lib.EPI_BIAS_RELU)
+            det = bool(torch.equal(out, again))
+            plan = [p for k, p in a._plans.items() if k[3] == sp.HUB_MIN and k[4] == sp.HUB_BLOCK_ROWS][-1]
+            warm = time_graph([lambda: ops.spmm(a, Bs[0], bias=bias, epilogue=_lib.EPI_BIAS_RELU, out=Cs[0])],
+                              args.reps)
+            fns = [(lambda i=i: ops.spmm(a, Bs[i], bias=bias, epilogue=_lib.EPI_BIAS_RELU, out=Cs[i]))
+                   for i in range(nsets)]
+            cold = time_graph(fns, max(1, args.reps // nsets))
+            print(json.dumps({"graph": args.graph, "F": F, "variant": name, "hub": plan.is_hub,
+                              "hdr": plan.header, "max_err": err, "deterministic": det,
+                              "warm_us": round(warm, 3), "cold_us": round(cold, 3),
+                              "warm_frac": nbytes / (warm * 1e-6) / 8e12, "cold_frac": nbytes / (cold * 1e-6) / 8e12,
+                              "sets": nsets}), flush=True)
+            sp.HUB_MIN, sp.HUB_BLOCK_ROWS = 0, 0
+
+
+if __name__ == "__main__":
+    main()

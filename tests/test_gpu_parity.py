@@ -49,7 +49,7 @@ def _random_csr(M, K, nnz, rng, heavy_rows=(), heavy_deg=0, empty_frac=0.0):
 
 def test_native_library_is_loaded():
     lib = _lib.load()
-    assert lib.gcnk_abi_version() == 1
+    assert lib.gcnk_abi_version() == _lib.ABI_VERSION
     with open("/proc/self/maps") as f:
         assert _lib.LIB_PATH in f.read()
 

@@ -94,6 +94,8 @@ SIGNATURES = {
     "gcnk_sym_normalize_workspace_bytes": (_i64, [_i32, _i64]),
     "gcnk_sym_normalize": (ctypes.c_int, [_vp, _vp, _vp, _i32, _i64, _vp, _vp, _vp, _vp, _i64, _vp]),
     "gcnk_csr_transpose_workspace_bytes": (_i64, [_i32, _i32, _i64]),
+    "gcnk_coo_to_csr_workspace_bytes": (_i64, [_i64, _i32, _i32]),
+    "gcnk_coo_to_csr": (ctypes.c_int, [_vp, _vp, _vp, _i64, _i32, _i32, _vp, _vp, _vp, _vp, _i64, _vp]),
     "gcnk_csr_transpose": (ctypes.c_int, [_vp, _vp, _vp, _i32, _i32, _i64, _vp, _vp, _vp, _vp, _i64, _vp]),
 }
 

@@ -1,6 +1,13 @@
-// Sparse-format helpers: CSR transpose (stable), used once per graph to build
-// the A^T / X^T operands of the autograd products (reference: the backward of
-// th.spmm(adj, support) / th.spmm(X, W) at layer.py:102,106 needs sparse^T g).
+// Sparse-format helpers, used once per graph:
+//  * COO -> CSR (gcnk_coo_to_csr): the reference hands th.spmm torch sparse COO
+//    tensors -- A-hat column-major and uncoalesced (utils.py:196-203), X
+//    row-major (trainer.py:226-238) -- which ATen re-coalesces on every call;
+//    here they are converted once: stable radix sort of (row * K + col), runs
+//    of equal keys summed in input order (what ATen's coalesce computes), row
+//    counts (integer atomics: exact) and a scan into row pointers;
+//  * CSR transpose (stable), for the A^T / X^T operands of the autograd
+//    products (the backward of th.spmm(adj, support) / th.spmm(X, W) at
+//    layer.py:102,106 needs sparse^T g).
 //
 // Stable counting layout via an LSD radix sort of (column, source index)
 // pairs: within each transposed row the entries keep ascending source-row
@@ -9,6 +16,8 @@
 #include "gcnk_common.h"
 
 #include <hipcub/hipcub.hpp>
+
+#include <algorithm>
 
 namespace gcnk {
 namespace {
@@ -47,6 +56,52 @@ __global__ void gather_kernel(const int32_t* __restrict__ rowptr, int32_t M, con
   }
   colind_t[i] = lo;
   val_t[i] = val[k];
+}
+
+// key = row * K + col; an index out of range poisons the result (rowptr[M] = -1)
+__global__ void coo_keys_kernel(const int64_t* __restrict__ rows, const int64_t* __restrict__ cols, int64_t nnz,
+                                int32_t M, int32_t K, uint64_t* __restrict__ keys, int32_t* __restrict__ idx,
+                                int32_t* __restrict__ bad) {
+  const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= nnz) return;
+  const int64_t r = rows[i], c = cols[i];
+  const bool ok = r >= 0 && r < M && c >= 0 && c < K;
+  if (!ok) atomicOr(bad, 1);
+  keys[i] = ok ? (uint64_t)r * (uint64_t)K + (uint64_t)c : 0;
+  idx[i] = (int32_t)i;
+}
+
+// head[i] = 1 where a run of equal sorted keys starts
+__global__ void run_heads_kernel(const uint64_t* __restrict__ keys, int64_t nnz, int32_t* __restrict__ head) {
+  const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i < nnz) head[i] = (i == 0 || keys[i] != keys[i - 1]) ? 1 : 0;
+}
+
+// at each run head: the run's values summed in input order (the sort is stable),
+// written at the run's rank (pos = inclusive scan of heads), and the row counted
+__global__ void run_sum_kernel(const uint64_t* __restrict__ keys, const int32_t* __restrict__ idx,
+                               const int32_t* __restrict__ pos, const float* __restrict__ vals, int64_t nnz,
+                               int32_t K, int32_t* __restrict__ colind, float* __restrict__ val,
+                               int32_t* __restrict__ cnt) {
+  const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= nnz || (i > 0 && keys[i] == keys[i - 1])) return;
+  const uint64_t k = keys[i];
+  float v = vals[idx[i]];
+  for (int64_t j = i + 1; j < nnz && keys[j] == k; ++j) v += vals[idx[j]];
+  const int32_t o = pos[i] - 1;
+  colind[o] = (int32_t)(k % (uint64_t)K);
+  val[o] = v;
+  atomicAdd(&cnt[k / (uint64_t)K], 1);
+}
+
+__global__ void poison_kernel(const int32_t* __restrict__ bad, int32_t M, int32_t* __restrict__ rowptr) {
+  if (*bad) rowptr[M] = -1;
+}
+
+inline int bits_for64(uint64_t n) {
+  int b = 1;
+  while (b < 64 && ((uint64_t)1 << b) < n) ++b;
+  return b;
 }
 
 inline int bits_for(int32_t K) {
@@ -110,4 +165,89 @@ extern "C" int gcnk_csr_transpose(const int32_t* rowptr, const int32_t* colind, 
   if ((rc = launch_check("bounds_kernel"))) return rc;
   hipLaunchKernelGGL(gather_kernel, dim3(nb), dim3(256), 0, s, rowptr, M, val, idx_out, nnz, colind_t, val_t);
   return launch_check("gather_kernel");
+}
+
+// ---------------------------------------------------------------------------
+// COO -> CSR
+namespace {
+struct CooWs {
+  int64_t keys_in, keys_out, idx_in, idx_out, head, pos, cnt, bad, tmp, total;
+  size_t tmp_bytes;
+  CooWs(int64_t nnz, int32_t M, int32_t K) {
+    auto a = [](int64_t b) { return (b + 255) & ~255LL; };
+    size_t sort_b = 0, scan_b = 0, scan2_b = 0;
+    const int bits = bits_for64((uint64_t)M * (uint64_t)(K > 0 ? K : 1));
+    (void)hipcub::DeviceRadixSort::SortPairs(nullptr, sort_b, (const uint64_t*)nullptr, (uint64_t*)nullptr,
+                                             (const int32_t*)nullptr, (int32_t*)nullptr, (int)nnz, 0, bits);
+    (void)hipcub::DeviceScan::InclusiveSum(nullptr, scan_b, (const int32_t*)nullptr, (int32_t*)nullptr, (int)nnz);
+    (void)hipcub::DeviceScan::ExclusiveSum(nullptr, scan2_b, (const int32_t*)nullptr, (int32_t*)nullptr, M + 1);
+    tmp_bytes = std::max(sort_b, std::max(scan_b, scan2_b));
+    keys_in = 0;
+    keys_out = keys_in + a(nnz * 8);
+    idx_in = keys_out + a(nnz * 8);
+    idx_out = idx_in + a(nnz * 4);
+    head = idx_out + a(nnz * 4);
+    pos = head + a(nnz * 4);
+    cnt = pos + a(nnz * 4);
+    bad = cnt + a(((int64_t)M + 1) * 4);
+    tmp = bad + 256;
+    total = tmp + a((int64_t)tmp_bytes);
+  }
+};
+}  // namespace
+
+extern "C" int64_t gcnk_coo_to_csr_workspace_bytes(int64_t nnz, int32_t M, int32_t K) {
+  if (nnz < 0 || M < 0 || K < 0) return GCNK_EARG;
+  return CooWs(nnz, M, K).total;
+}
+
+extern "C" int gcnk_coo_to_csr(const int64_t* rows, const int64_t* cols, const float* vals, int64_t nnz, int32_t M,
+                               int32_t K, int32_t* rowptr, int32_t* colind, float* val, void* workspace,
+                               int64_t workspace_bytes, void* stream) {
+  if (nnz < 0 || nnz >= INT32_MAX || M < 0 || K < 0 || !rowptr ||
+      (nnz > 0 && (!rows || !cols || !vals || !colind || !val))) {
+    set_error("gcnk_coo_to_csr: bad argument (nnz=%lld M=%d K=%d)", (long long)nnz, M, K);
+    return GCNK_EARG;
+  }
+  hipStream_t s = (hipStream_t)stream;
+  if (nnz == 0) return hip_check(hipMemsetAsync(rowptr, 0, ((size_t)M + 1) * 4, s), "coo_to_csr memset");
+  const CooWs L(nnz, M, K);
+  if (!workspace || workspace_bytes < L.total) {
+    set_error("gcnk_coo_to_csr: workspace %lld B < %lld B", (long long)workspace_bytes, (long long)L.total);
+    return GCNK_EARG;
+  }
+  char* w = (char*)workspace;
+  uint64_t* keys_in = (uint64_t*)(w + L.keys_in);
+  uint64_t* keys_out = (uint64_t*)(w + L.keys_out);
+  int32_t* idx_in = (int32_t*)(w + L.idx_in);
+  int32_t* idx_out = (int32_t*)(w + L.idx_out);
+  int32_t* head = (int32_t*)(w + L.head);
+  int32_t* pos = (int32_t*)(w + L.pos);
+  int32_t* cnt = (int32_t*)(w + L.cnt);
+  int32_t* bad = (int32_t*)(w + L.bad);
+  void* tmp = w + L.tmp;
+  size_t tb = L.tmp_bytes;
+  const unsigned nb = (unsigned)((nnz + 255) / 256);
+  int rc = hip_check(hipMemsetAsync(cnt, 0, ((size_t)M + 1) * 4, s), "coo_to_csr counts");
+  if (!rc) rc = hip_check(hipMemsetAsync(bad, 0, 4, s), "coo_to_csr flag");
+  if (rc) return rc;
+  hipLaunchKernelGGL(coo_keys_kernel, dim3(nb), dim3(256), 0, s, rows, cols, nnz, M, K, keys_in, idx_in, bad);
+  if ((rc = launch_check("coo_keys_kernel"))) return rc;
+  const int bits = bits_for64((uint64_t)M * (uint64_t)(K > 0 ? K : 1));
+  rc = hip_check(hipcub::DeviceRadixSort::SortPairs(tmp, tb, keys_in, keys_out, idx_in, idx_out, (int)nnz, 0, bits, s),
+                 "coo_to_csr radix sort");
+  if (rc) return rc;
+  hipLaunchKernelGGL(run_heads_kernel, dim3(nb), dim3(256), 0, s, keys_out, nnz, head);
+  if ((rc = launch_check("run_heads_kernel"))) return rc;
+  tb = L.tmp_bytes;
+  rc = hip_check(hipcub::DeviceScan::InclusiveSum(tmp, tb, head, pos, (int)nnz, s), "coo_to_csr scan");
+  if (rc) return rc;
+  hipLaunchKernelGGL(run_sum_kernel, dim3(nb), dim3(256), 0, s, keys_out, idx_out, pos, vals, nnz, K, colind, val,
+                     cnt);
+  if ((rc = launch_check("run_sum_kernel"))) return rc;
+  tb = L.tmp_bytes;
+  rc = hip_check(hipcub::DeviceScan::ExclusiveSum(tmp, tb, cnt, rowptr, M + 1, s), "coo_to_csr row scan");
+  if (rc) return rc;
+  hipLaunchKernelGGL(poison_kernel, dim3(1), dim3(1), 0, s, bad, M, rowptr);
+  return launch_check("poison_kernel");
 }

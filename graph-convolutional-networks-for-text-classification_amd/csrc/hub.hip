@@ -41,6 +41,10 @@ constexpr int kHubSmax = 64;            // B rows staged per block (F = 200: 51 
 #endif
 constexpr int kHubBlock = GCNK_HUB_BLOCK;  // threads per light-block workgroup (16 waves)
 constexpr int kHubRecMaxWords = 24576;  // record cap (96 KB of LDS)
+constexpr int kHubTargetBlocks = 256;   // light blocks per launch: one per CU (256 CUs)
+// finishing kernel: 1024 threads = 64 partial lanes x 16 column lanes at F >= 64,
+// so a hub's ~100-250 partials are all in flight in one round of loads
+constexpr int kHubFinishBlock = 1024;
 constexpr int kLdsMax = 163840;         // gfx950: 160 KiB per workgroup
 
 __host__ __device__ inline int64_t align4(int64_t x) { return (x + 3) & ~3LL; }
@@ -157,34 +161,90 @@ hub_light_kernel(const int32_t* __restrict__ recs, int32_t R, const float* __res
   __syncthreads();
   stamp(epi, 2);
 
-  // ---- outputs: branch-free batches (items read at a clamped index, every stage
-  //      read issued, invalid ones dropped by a select), so a batch costs two LDS
-  //      latencies; with whole-wavefront groups the bookkeeping is wave-uniform
+  // ---- outputs.  Whole-wavefront groups (LPR = 64): wave w takes a contiguous
+  //      range of outputs, reads their {dest, end} descriptors once (one per
+  //      lane) and keeps a 64-item window of {slot, value} in registers, so an
+  //      output costs one batch of stage reads per 8 items: slots and values
+  //      broadcast with v_readlane (scalar addresses), the 8 LDS row reads
+  //      issued together (past the end: the last item again, its term
+  //      dropped), no other LDS round trip.  Narrower groups (several outputs
+  //      per wavefront, F <= 128): items at a clamped index, stage reads all
+  //      issued, invalid terms dropped by a select.  Idle lanes (columns past
+  //      the tile) read their natural address (the stage is padded), which
+  //      keeps the wavefront's row read conflict-free.
   const int32_t sw = nq * VEC;  // staged row stride (floats)
-  const int32_t lofs = colok ? lcol : 0;
   const int2* s_items = reinterpret_cast<const int2*>(s_rec + o_it);
+  const int2* s_out = reinterpret_cast<const int2*>(s_rec + o_out);
   const bool fast_epi = VEC == 4 && epi.code <= GCNK_EPI_BIAS_RELU;
-  for (int32_t o = g; o < nout; o += SG) {
-    int32_t dest = s_rec[o_out + 2 * o], ie = s_rec[o_out + 2 * o + 1];
-    int32_t ib = o == 0 ? 0 : s_rec[o_out + 2 * o - 1];
-    if (LPR == 64) {
-      dest = __builtin_amdgcn_readfirstlane(dest);
-      ie = __builtin_amdgcn_readfirstlane(ie);
-      ib = __builtin_amdgcn_readfirstlane(ib);
-    }
+  const int lane = tid & 63;
+  const int32_t nitems = s_rec[3];
+  constexpr int NW = BLOCK / 64;
+  const int w = __builtin_amdgcn_readfirstlane(tid >> 6);  // wave-uniform (the compiler cannot tell)
+  // whole-wavefront groups: this wave's outputs [ow0, ow1); narrow groups: g, g + SG, ...
+  const int32_t ow0 = LPR == 64 ? (int32_t)((int64_t)nout * w / NW) : g;
+  const int32_t ow1 = LPR == 64 ? (int32_t)((int64_t)nout * (w + 1) / NW) : nout;
+  int2 desc = make_int2(0, 0), win = make_int2(0, 0);
+  int32_t dbase = -1, wbase = -1, ib = 0;
+  for (int32_t o = ow0; o < ow1; o += (LPR == 64 ? 1 : SG)) {
+    int32_t dest, ie;
     T acc = V::zero();
-    for (int32_t k0 = ib; k0 < ie; k0 += U) {
-      int2 it[U];
+    if constexpr (LPR == 64) {
+      if (dbase < 0 || o >= dbase + 64) {  // next 64 descriptors (and where this range's items start)
+        dbase = o;
+        desc = s_out[min(o + lane, ow1 - 1)];
+        ib = o == 0 ? 0 : __builtin_amdgcn_readfirstlane(s_rec[o_out + 2 * o - 1]);
+      }
+      dest = __builtin_amdgcn_readlane(desc.x, o - dbase);
+      ie = __builtin_amdgcn_readlane(desc.y, o - dbase);
+#if defined(GCNK_HUB_EXP) && (GCNK_HUB_EXP & 16)  // ablation: no item loop
+      ib = ie;
+#endif
+      for (int32_t k = ib; k < ie; k += U) {
+        if (wbase < 0 || k < wbase || min(k + U, ie) > wbase + 64) {
+          wbase = k;
+          win = s_items[min(wbase + lane, nitems - 1)];
+        }
+        int32_t sl[U];
+        float av[U];
 #pragma unroll
-      for (int j = 0; j < U; ++j) it[j] = s_items[min(k0 + j, ie - 1)];
-      T gv[U];
+        for (int u = 0; u < U; ++u) {
+          const int32_t kk = min(k + u, ie - 1) - wbase;
+          sl[u] = __builtin_amdgcn_readlane(win.x, kk);
+          av[u] = __int_as_float(__builtin_amdgcn_readlane(win.y, kk));
+        }
+        T gv[U];
 #pragma unroll
-      for (int j = 0; j < U; ++j) gv[j] = V::load(s_stage + it[j].x * sw + lofs);
+        for (int u = 0; u < U; ++u) gv[u] = V::load(s_stage + sl[u] * sw + lcol);
+        // past the output's end: both operands zeroed (0 * 0 adds nothing, even
+        // next to an infinite row); a guarded FMA would let the compiler sink the
+        // read into the branch and wait for it there
 #pragma unroll
-      for (int j = 0; j < U; ++j) {
-        T t = acc;
-        V::fma(t, __int_as_float(it[j].y), gv[j]);
-        if (k0 + j < ie) acc = t;
+        for (int u = 0; u < U; ++u) {
+          const bool live = k + u < ie;
+          V::fma(acc, live ? av[u] : 0.f, live ? gv[u] : V::zero());
+        }
+      }
+      ib = ie;
+    } else {
+      dest = s_rec[o_out + 2 * o];
+      ie = s_rec[o_out + 2 * o + 1];
+      int32_t ib0 = o == 0 ? 0 : s_rec[o_out + 2 * o - 1];
+#if defined(GCNK_HUB_EXP) && (GCNK_HUB_EXP & 16)  // ablation: no item loop
+      ib0 = ie;
+#endif
+      for (int32_t k0 = ib0; k0 < ie; k0 += U) {
+        int2 it[U];
+#pragma unroll
+        for (int j = 0; j < U; ++j) it[j] = s_items[min(k0 + j, ie - 1)];
+        T gv[U];
+#pragma unroll
+        for (int j = 0; j < U; ++j) gv[j] = V::load(s_stage + it[j].x * sw + lcol);
+#pragma unroll
+        for (int j = 0; j < U; ++j) {
+          T t = acc;
+          V::fma(t, __int_as_float(it[j].y), gv[j]);
+          if (k0 + j < ie) acc = t;
+        }
       }
     }
     if (!colok) continue;
@@ -221,17 +281,17 @@ hub_light_kernel(const int32_t* __restrict__ recs, int32_t R, const float* __res
 }
 
 // Hub rows: C[row] = epi(sum of the hub's partials in block order + its leftover
-// nonzeros).  Grid (nhub, column tiles of LPR * VEC); 256 threads = PL partial
+// nonzeros).  Grid (nhub, column tiles of LPR * VEC); BLOCK threads = PL partial
 // lanes x LPR column lanes; partial lane p takes partials p, p + PL, ... and
 // leftovers p, p + PL, ... (U loads in flight), then a fixed-order LDS tree.
-template <int LPR, int VEC>
-__global__ void __launch_bounds__(256)
+template <int BLOCK, int LPR, int VEC>
+__global__ void __launch_bounds__(BLOCK)
 hub_finish_kernel(const int4* __restrict__ hubs, const int2* __restrict__ left, const float* __restrict__ part,
                   int64_t part_ld, const float* __restrict__ B, int64_t ldb, int32_t F, float* __restrict__ C,
                   int64_t ldc, Epi epi) {
   using V = Vec<VEC>;
   using T = typename V::T;
-  constexpr int PL = 256 / LPR;
+  constexpr int PL = BLOCK / LPR;
   constexpr int U = 8;
   __shared__ T s_red[PL][LPR];
   stamp(epi, 0);
@@ -240,6 +300,7 @@ hub_finish_kernel(const int4* __restrict__ hubs, const int2* __restrict__ left, 
   const int tid = threadIdx.x, pl = tid / LPR, lg = tid % LPR;
   const int64_t colv = (int64_t)blockIdx.y * (LPR * VEC) + (int64_t)lg * VEC;
   const bool ok = colv < F;
+  const T bv = (epi.bias && ok) ? V::load(epi.bias + colv) : V::zero();  // first: no wait behind the partials
   T acc = V::zero();
   // indices clamped into range and out-of-range terms dropped by a select, so
   // each batch's U loads issue back to back (no load under a branch)
@@ -279,7 +340,6 @@ hub_finish_kernel(const int4* __restrict__ hubs, const int2* __restrict__ left, 
     __syncthreads();
   }
   if (pl == 0 && ok) {
-    const T bv = epi.bias ? V::load(epi.bias + colv) : V::zero();
     V::store(C + (int64_t)hb.x * ldc + colv, V::epi(epi, s_red[0][lg], bv, hb.x, colv));
   }
   stamp(epi, 2);
@@ -304,7 +364,8 @@ int hub_launch(const HubArgs& a) {
   const int64_t tile = (int64_t)LPR * VEC;
   const int64_t ntiles = (a.F + tile - 1) / tile;
   const int64_t TW = std::min<int64_t>(a.F, tile);
-  const int64_t lds = a.L.R * 4 + a.L.max_stage * ((TW + VEC - 1) / VEC * VEC) * 4;
+  // + one tile of padding: idle lanes read past the last staged row
+  const int64_t lds = a.L.R * 4 + (a.L.max_stage * ((TW + VEC - 1) / VEC * VEC) + tile) * 4;
   if (lds > kLdsMax || ntiles > 65535) {
     set_error("gcnk_spmm (hub plan): %lld B of LDS / %lld column tiles exceed the launch limits", (long long)lds,
               (long long)ntiles);
@@ -326,7 +387,8 @@ int hub_launch(const HubArgs& a) {
   const int64_t tb = (a.F + LB * VEC - 1) / (LB * VEC);
   Epi eb = a.epi;  // debug stamps of the finishing kernel follow the light kernel's
   if (eb.stamps) eb.stamps += 4 * a.L.nblocks * ntiles;
-  hipLaunchKernelGGL((hub_finish_kernel<LB, VEC>), dim3((unsigned)a.L.nhub, (unsigned)tb), dim3(256), 0, a.s,
+  hipLaunchKernelGGL((hub_finish_kernel<kHubFinishBlock, LB, VEC>), dim3((unsigned)a.L.nhub, (unsigned)tb),
+                     dim3(kHubFinishBlock), 0, a.s,
                      reinterpret_cast<const int4*>(a.plan + a.L.hubs), reinterpret_cast<const int2*>(a.plan + a.L.left),
                      a.part, a.part_ld, a.B, a.ldb, a.F, a.C, a.ldc, eb);
   return launch_check("hub_finish_kernel");
@@ -357,6 +419,9 @@ int hub_plan_host(const int32_t* rp, const int32_t* ci, const float* vv, int32_t
                   int32_t groups, int32_t hub_min, int32_t block_rows, std::vector<int32_t>& img) {
   if (M <= 0 || nnz <= 0 || hub_min < 0) return 1;
   const bool auto_mode = hub_min == 0;
+  // automatic: wide operands only (whole-wavefront groups, F > 128); at narrow
+  // widths the row plan's gathers are cheap (R8 F = 8: 32-B rows) and measured faster
+  if (auto_mode && groups != 1) return 1;
   // hub threshold: 8x the mean degree, at least 64 nonzeros (R8 A-hat: mean 9,
   // threshold 72: the 50 topic rows, 191..1807 nonzeros; uniform 1M/20M: mean
   // 20, threshold 160, max degree ~45: no hubs)
@@ -397,24 +462,24 @@ int hub_plan_host(const int32_t* rp, const int32_t* ci, const float* vv, int32_t
     return std::lexicographical_compare(sc.begin() + so[(size_t)x], sc.begin() + so[(size_t)x + 1],
                                         sc.begin() + so[(size_t)y], sc.begin() + so[(size_t)y + 1]);
   });
-  // blocks of consecutive sorted rows: at most br rows (default ~256 blocks, one
-  // per CU, 4..64 rows), cut early where the B rows the block references (its
-  // rows' columns + its own columns that hub rows reference) would exceed the
-  // kHubSmax stage slots
-  const int64_t br = block_rows > 0 ? block_rows : std::min<int64_t>(64, std::max<int64_t>(4, (nlight + 255) / 256));
   std::vector<char> hubref((size_t)K, 0);
   for (int32_t r : hubs)
     for (int64_t k = rp[r]; k < rp[r + 1]; ++k) hubref[(size_t)ci[k]] = 1;
   std::vector<int64_t> bstart;
   std::vector<int32_t> mark((size_t)K, -1), rowmark((size_t)K, -1);
-  {
+  int64_t stamp_base = 0;
+  // greedy cut at <= br rows; false when a single row alone overflows the stage
+  auto partition = [&](int64_t br) {
+    bstart.clear();
+    std::fill(mark.begin(), mark.end(), -1);
     int64_t rows = 0, stage = 0;
     int32_t blk = -1;
-    auto fresh = [&](int64_t i, int32_t r) {  // distinct columns row r adds to block blk
+    auto fresh = [&](int32_t r) {  // distinct columns row r adds to block blk
+      const int32_t id = (int32_t)(stamp_base++ & 0x3fffffff);
       int64_t n = 0;
       auto see = [&](int32_t c) {
-        if (rowmark[(size_t)c] != (int32_t)i && mark[(size_t)c] != blk) ++n;
-        rowmark[(size_t)c] = (int32_t)i;
+        if (rowmark[(size_t)c] != id && mark[(size_t)c] != blk) ++n;
+        rowmark[(size_t)c] = id;
       };
       for (int64_t k = rp[r]; k < rp[r + 1]; ++k) see(ci[k]);
       if (r < K && hubref[(size_t)r]) see(r);
@@ -422,17 +487,16 @@ int hub_plan_host(const int32_t* rp, const int32_t* ci, const float* vv, int32_t
     };
     for (int64_t i = 0; i < nlight; ++i) {
       const int32_t r = light[(size_t)ord[(size_t)i]];
-      int64_t n = blk >= 0 ? fresh(2 * i, r) : 0;
+      int64_t n = blk >= 0 ? fresh(r) : 0;
       if (blk < 0 || rows == br || stage + n > kHubSmax) {
         ++blk;
         bstart.push_back(i);
         rows = stage = 0;
-        n = fresh(2 * i + 1, r);
+        n = fresh(r);
         if (n > kHubSmax) {
-          if (auto_mode) return 1;
           set_error("gcnk_spmm_plan (hub): light row %d references %lld rows, more than the %d stage slots", r,
                     (long long)n, kHubSmax);
-          return GCNK_EUNSUP;
+          return false;
         }
       }
       for (int64_t k = rp[r]; k < rp[r + 1]; ++k) mark[(size_t)ci[k]] = blk;
@@ -441,6 +505,18 @@ int hub_plan_host(const int32_t* rp, const int32_t* ci, const float* vv, int32_t
       ++rows;
     }
     bstart.push_back(nlight);
+    return true;
+  };
+  // blocks of consecutive sorted rows, cut early where the B rows a block
+  // references (its rows' columns + its own columns that hub rows reference)
+  // would exceed the kHubSmax stage slots.  Automatic size: the smallest
+  // row cap (>= 4) whose blocks number at most kHubTargetBlocks, so every
+  // block is resident at once (one per CU)
+  int64_t br = block_rows > 0 ? block_rows : std::max<int64_t>(4, (nlight + kHubTargetBlocks - 1) / kHubTargetBlocks);
+  for (;;) {
+    if (!partition(br)) return auto_mode ? 1 : GCNK_EUNSUP;
+    if (block_rows > 0 || (int64_t)bstart.size() - 1 <= kHubTargetBlocks || br >= 64) break;
+    ++br;
   }
   const int64_t nblocks = (int64_t)bstart.size() - 1;
   std::vector<int32_t> owner((size_t)K, -1);  // column j -> block of light row j

@@ -5,8 +5,12 @@ BASELINE.json config 5).
 per GPU, ``torch.distributed`` over RCCL / xGMI) rank p holds the replicated
 CSR ``A`` and its own column shard ``B[:, c0_p:c1_p]`` and computes
 ``C[:, c0_p:c1_p]`` with no communication.  Only a consumer that needs the whole
-row-major ``C`` pays the one exchange: an all-gather of the ``[M, F/P]`` shards
-into a ``[P, M, F/P]`` buffer, then a local re-layout to ``[M, F]``.
+``C`` pays the one exchange: an all-gather of the ``[M, F/P]`` shards into a
+``[P, M, F/P]`` buffer, which is handed over AS IS (``GatheredColumns``:
+column block p is a ``[M, F_p]`` view with leading dimension F/P, exactly the
+strided operand the SpMM / GEMM kernels take) -- no re-layout copy of the
+gathered bytes (16.4 GB for config 5).  ``GatheredColumns.to_dense()`` makes
+the row-major copy for a consumer that truly needs one.
 
 For the two-layer GCN (reference layer.py:164-190) the hidden columns of gc1
 are sharded the same way and gc2's projection needs a sum over the shards:
@@ -43,8 +47,12 @@ def _default_kernels():
     return types.SimpleNamespace(spmm=ops.spmm, gemm=ops.gemm)
 
 
+def _distributed():
+    return dist.is_available() and dist.is_initialized()
+
+
 def _world(group):
-    if dist.is_available() and dist.is_initialized():
+    if _distributed():
         return dist.get_world_size(group), dist.get_rank(group)
     return 1, 0
 
@@ -57,15 +65,52 @@ def _all_gather(buf, part, group):
         dist.all_gather(list(buf.unbind(0)), part, group=group)
 
 
+class GatheredColumns:
+    """The all-gathered ``[M, F]`` product in the layout the collective wrote:
+    ``buf[P, M, width]``, column block p = columns ``bounds[p]`` of C.
+
+    ``block(p)`` is a zero-copy ``[M, c1 - c0]`` view (leading dimension
+    ``width``), which the kernels accept as a strided operand; ``spmm(a)``
+    runs a consumer product ``A @ C`` block by block into a row-major output;
+    ``to_dense()`` is the explicit row-major copy."""
+
+    def __init__(self, buf, bounds):
+        self.buf, self.bounds = buf, list(bounds)
+        self.shape = (buf.shape[1], self.bounds[-1][1])
+
+    def block(self, p):
+        c0, c1 = self.bounds[p]
+        return self.buf[p, :, : c1 - c0]
+
+    def blocks(self):
+        return [(c0, c1, self.block(p)) for p, (c0, c1) in enumerate(self.bounds)]
+
+    def to_dense(self):
+        out = torch.empty(self.shape, dtype=self.buf.dtype, device=self.buf.device)
+        for c0, c1, blk in self.blocks():
+            out[:, c0:c1].copy_(blk)
+        return out
+
+    def spmm(self, a, bias=None, epilogue=_lib.EPI_NONE, out=None, kernels=None):
+        """``epi(A @ C)`` for the gathered C, one launch per column block (each
+        reads its block in place; the output is row-major ``[M_a, F]``)."""
+        k = kernels or _default_kernels()
+        if out is None:
+            out = torch.empty((a.shape[0], self.shape[1]), dtype=self.buf.dtype, device=self.buf.device)
+        for c0, c1, blk in self.blocks():
+            k.spmm(a, blk, bias=bias[c0:c1] if bias is not None else None, epilogue=epilogue, out=out[:, c0:c1])
+        return out
+
+
 class ColumnShardedSpMM:
     """``C = epi(A @ B)`` with B's F columns split over the ranks of `group`.
 
     ``local(B_shard)`` computes this rank's ``[M, F_p]`` block (no exchange);
-    ``gather(C_block)`` returns the full ``[M, F]`` row-major result on every
-    rank (one all-gather).  Shards are padded to the widest one so every rank
-    contributes equal bytes, the padded block is what ``local`` writes (its
-    leading dimension is the padded width), so the kernel's output is already
-    the send buffer."""
+    ``gather(C_block)`` returns the full result on every rank (one RCCL
+    all-gather into a ``GatheredColumns``; no re-layout).  Shards are padded to
+    the widest one so every rank contributes equal bytes; the padded block is
+    what ``local`` writes (its leading dimension is the padded width), so the
+    kernel's output is already the send buffer."""
 
     def __init__(self, a, F, group=None, kernels=None):
         self.a = a
@@ -90,21 +135,23 @@ class ColumnShardedSpMM:
         if B_shard.shape[1] != c1 - c0:
             raise RuntimeError(f"rank {self.rank}: shard has {B_shard.shape[1]} columns, expected {c1 - c0}")
         M = self.a.shape[0]
-        block = torch.zeros((M, self.width), dtype=torch.float32, device=B_shard.device)
+        alloc = torch.zeros if c1 - c0 < self.width else torch.empty   # pad columns are sent, so defined
+        block = alloc((M, self.width), dtype=torch.float32, device=B_shard.device)
         view = block[:, : c1 - c0]
         b = bias[c0:c1] if bias is not None else None
         self.kernels.spmm(self.a, B_shard, bias=b, epilogue=epilogue, out=view)
         return block
 
     def gather(self, block):
-        """All ranks' blocks -> the full ``[M, F]`` matrix (RCCL all-gather over xGMI)."""
-        if self.world == 1:
-            c0, c1 = self.bounds[0]
-            return block[:, : c1 - c0]
+        """All ranks' blocks -> ``GatheredColumns`` (RCCL all-gather over xGMI,
+        whenever a process group exists -- a 1-rank group included)."""
         M = block.shape[0]
         buf = torch.empty((self.world, M, self.width), dtype=block.dtype, device=block.device)
-        _all_gather(buf, block.contiguous(), self.group)
-        return torch.cat([buf[p, :, : c1 - c0] for p, (c0, c1) in enumerate(self.bounds)], dim=1)
+        if _distributed():
+            _all_gather(buf, block.contiguous(), self.group)
+        else:
+            buf[0].copy_(block)
+        return GatheredColumns(buf, self.bounds)
 
     def __call__(self, B_shard, bias=None, epilogue=_lib.EPI_NONE, gather=True):
         block = self.local(B_shard, bias=bias, epilogue=epilogue)
@@ -136,7 +183,7 @@ def sharded_gcn_forward(model, x, adj, group=None, kernels=None):
     H1 = k.spmm(a, S1, bias=(b1.detach()[c0:c1].contiguous() if b1 is not None else None),
                 epilogue=_lib.EPI_BIAS_RELU)   # a null bias adds 0 in the epilogue
     S2 = k.gemm(H1, W2[c0:c1].contiguous())
-    if world > 1:
+    if _distributed():
         dist.all_reduce(S2, op=dist.ReduceOp.SUM, group=group)
     return k.spmm(a, S2, bias=(b2.detach() if b2 is not None else None),
                   epilogue=_lib.EPI_BIAS if b2 is not None else _lib.EPI_NONE)

@@ -191,15 +191,32 @@ def from_torch(t):
         return CSR(rowptr, colind, val, (M, K))
     if t.layout != torch.sparse_coo:
         raise RuntimeError(f"unsupported sparse layout {t.layout}")
-    c = t if t.is_coalesced() else t.coalesce()
-    idx = c._indices()
-    val = c._values().to(torch.float32)
-    nnz = val.numel()
-    _check_int32(M, K, nnz)
-    counts = torch.bincount(idx[0], minlength=M)
-    rowptr = torch.zeros(M + 1, dtype=torch.int32, device=t.device)
-    rowptr[1:] = torch.cumsum(counts, 0).to(torch.int32)
-    return CSR(rowptr, idx[1].to(torch.int32), val, (M, K))
+    # gcnk_coo_to_csr: stable sort of (row, col), duplicates summed in input
+    # order (ATen's coalesce arithmetic), row pointers -- one pass on the device
+    idx = t._indices()
+    vals = t._values()
+    if vals.dtype != torch.float32:
+        vals = vals.to(torch.float32)
+    nnz_in = vals.numel()
+    _check_int32(M, K, nnz_in)
+    rows, cols, vals = idx[0].contiguous(), idx[1].contiguous(), vals.contiguous()
+    dev = t.device
+    rowptr = torch.empty(M + 1, dtype=torch.int32, device=dev)
+    colind = torch.empty(max(nnz_in, 1), dtype=torch.int32, device=dev)
+    val = torch.empty(max(nnz_in, 1), dtype=torch.float32, device=dev)
+    lib = _lib.load()
+    wsb = int(lib.gcnk_coo_to_csr_workspace_bytes(nnz_in, M, K))
+    if wsb < 0:
+        _lib.check(wsb, "gcnk_coo_to_csr_workspace_bytes")
+    ws = torch.empty(max(wsb, 1), dtype=torch.uint8, device=dev)
+    with torch.cuda.device(dev):
+        _lib.check(lib.gcnk_coo_to_csr(rows.data_ptr(), cols.data_ptr(), vals.data_ptr(), nnz_in, M, K,
+                                       rowptr.data_ptr(), colind.data_ptr(), val.data_ptr(), ws.data_ptr(), wsb,
+                                       _stream_ptr(dev)), "gcnk_coo_to_csr")
+    nnz = int(rowptr[M])   # one-time setup sync
+    if nnz < 0:
+        raise RuntimeError(f"sparse COO operand has an index outside its shape {tuple(t.shape)}")
+    return CSR(rowptr, colind[:nnz], val[:nnz], (M, K))
 
 
 def from_arrays(rowptr, colind, val, shape, device):

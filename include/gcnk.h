@@ -17,7 +17,7 @@
  *                  H^T g, g W^T, relu/dropout mask          -> gcnk_gemm_f32 (+GCNK_GEMM_EPI_MASK_POS)
  *                  sum over rows of g  (bias grad)          -> gcnk_colsum_f32
  *   utils.py:196-203 / trainer.py:226-238 (COO tensors handed to th.spmm)
- *                                                           -> gcnk_spmm_plan_build (one-time schedule)
+ *                                                           -> gcnk_coo_to_csr + gcnk_spmm_plan_build (one-time)
  *   utils.py:185-213 preprocess_adj / normalize_adj          -> gcnk_sym_normalize (device, bit-exact)
  *   utils.py:25-109  accuracy / macro_f1 counts              -> gcnk_class_stats (one launch, no per-class syncs)
  *   trainer.py:98-148 edge list -> symmetric adjacency        -> gcnk_edgelist_size / _csr (host, no networkx)
@@ -238,6 +238,17 @@ int gcnk_colsum_f32(const float* X, int64_t ldx, int32_t M, int32_t N, float* ou
  *     workspace of gcnk_csr_transpose_workspace_bytes.
  * ------------------------------------------------------------------------- */
 int64_t gcnk_csr_transpose_workspace_bytes(int32_t M, int32_t K, int64_t nnz);
+/*  gcnk_coo_to_csr: the torch sparse COO tensors the reference hands th.spmm
+ *    (utils.py:196-203: A-hat column-major and uncoalesced; trainer.py:226-238:
+ *    X row-major) -> int32 CSR with sorted columns, duplicates summed in input
+ *    order (what ATen's coalesce computes).  rows/cols int64[nnz], vals fp32;
+ *    outputs have capacity nnz; rowptr[M] is the output nnz (read it after the
+ *    stream completes; -1 if an index was out of range).  Replaces ATen's
+ *    coalesce + bincount on the one-time conversion path. */
+int64_t gcnk_coo_to_csr_workspace_bytes(int64_t nnz, int32_t M, int32_t K);
+int gcnk_coo_to_csr(const int64_t* rows, const int64_t* cols, const float* vals, int64_t nnz, int32_t M, int32_t K,
+                    int32_t* rowptr, int32_t* colind, float* val, void* workspace, int64_t workspace_bytes,
+                    void* stream);
 int gcnk_csr_transpose(const int32_t* rowptr, const int32_t* colind, const float* val,
                        int32_t M, int32_t K, int64_t nnz,
                        int32_t* rowptr_t, int32_t* colind_t, float* val_t,

@@ -4,7 +4,8 @@
             nonzeros), F = 256, one GPU;
   config 5: the same graph, F = 4096 feature columns split over the ranks
             (parallel.ColumnShardedSpMM: each rank computes its [M, F/P] block
-            with no exchange, then one RCCL all-gather builds the row-major C).
+            with no exchange, then one RCCL all-gather of the blocks, handed over
+            in place as parallel.GatheredColumns: no re-layout copy).
 
 One JSON line per case (rank 0).  Launched alone it runs on one GPU (config 5
 then means its whole F = 4096 on that GPU, or one rank's F = 512 shard with

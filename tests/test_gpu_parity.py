@@ -189,6 +189,45 @@ def test_spmm_deterministic():
     assert torch.equal(o1, o2)
 
 
+@pytest.mark.parametrize("kind", ["hub", "row"])
+def test_spmm_two_streams_share_one_plan_concurrently(r8, kind, monkeypatch):
+    """Reentrancy (gcnk.h threading contract): two streams run SpMMs on the same
+    cached operand at the same time, with different inputs and outputs.  The
+    hub plan has no cross-call state; the row-unit plan's heavy-row arrival
+    counters live in a per-stream region (sparse.Plan.counters), so neither can
+    corrupt the other: every output equals the single-stream result bit for bit."""
+    rng = np.random.default_rng(17)
+    if kind == "hub":
+        a, K = from_torch(r8["adj"].to(DEV)), r8["nodes"]
+    else:   # row-unit plan with multi-segment heavy rows (hub plan and tile path off)
+        from graph_convolutional_networks_for_text_classification_amd import sparse as sp
+        monkeypatch.setattr(sp, "HUB_MIN", -1)
+        M, K = 3001, 20003
+        rp, ci, v = _random_csr(M, K, 20000, rng, heavy_rows=(5, 1700, 3000), heavy_deg=2500)
+        a = from_arrays(rp, ci, v, (M, K), DEV)
+    F = 200
+    Bs = [torch.from_numpy(rng.standard_normal((K, F)).astype(np.float32)).to(DEV) for _ in range(2)]
+    dense = 2.0 if kind == "row" else None
+    ref = [spmm(a, B, dense=dense) for B in Bs]
+    plan = list(a._plans.values())[-1]
+    assert plan.is_hub == (kind == "hub")
+    if kind == "row":
+        assert plan.counter_bytes() > 0, "multi-segment heavy rows use arrival counters"
+    streams = [torch.cuda.Stream(), torch.cuda.Stream()]
+    outs = [[torch.empty_like(ref[i]) for _ in range(24)] for i in range(2)]
+    torch.cuda.synchronize()
+    for it in range(24):
+        for i in range(2):
+            with torch.cuda.stream(streams[i]):
+                spmm(a, Bs[i], out=outs[i][it], dense=dense)
+    torch.cuda.synchronize()
+    for i in range(2):
+        for o in outs[i]:
+            assert torch.equal(o, ref[i])
+    if kind == "row":
+        assert len(plan._counters) >= 3, "one counter region per stream"
+
+
 def test_spmm_epilogues_and_strided_operands():
     rng = np.random.default_rng(11)
     M, K, F = 700, 500, 64
@@ -230,6 +269,39 @@ def test_spmm_coo_input_with_duplicates_and_shuffled_order():
     B = rng.standard_normal((K, F)).astype(np.float32)
     rp, ci, v = csr_ref.coo_to_csr(rows, cols, vals, (M, K))
     _close(spmm(t, torch.from_numpy(B).to(DEV)), csr_ref.spmm_csr(rp, ci, v, B))
+
+
+def test_coo_to_csr_matches_aten_coalesce(r8):
+    """gcnk_coo_to_csr (sparse.from_torch) against ATen's own coalesce -- what
+    th.spmm does to the reference's uncoalesced COO on every call -- bit for
+    bit: R8's column-major A-hat (utils.py:196-203), R8's row-major X
+    (trainer.py:226-238), and a shuffled COO with duplicates; an out-of-range
+    index raises."""
+    rng = np.random.default_rng(21)
+    M, K = 900, 700
+    rows = rng.integers(0, M, 9000)
+    cols = rng.integers(0, K, 9000)
+    rows = np.concatenate([rows, rows[:3000], rows[:100]])
+    cols = np.concatenate([cols, cols[:3000], cols[:100]])
+    vals = rng.standard_normal(rows.size).astype(np.float32)
+    perm = rng.permutation(rows.size)
+    dup = torch.sparse_coo_tensor(torch.from_numpy(np.vstack([rows[perm], cols[perm]])),
+                                  torch.from_numpy(vals[perm]), (M, K))
+    for t in (r8["adj"], r8["features"], dup):
+        c = t.coalesce()
+        a = from_torch(t.to(DEV))
+        want_rp = np.concatenate([[0], np.cumsum(np.bincount(c.indices()[0].numpy(), minlength=t.shape[0]))])
+        assert np.array_equal(a.rowptr.cpu().numpy(), want_rp)
+        assert np.array_equal(a.colind.cpu().numpy(), c.indices()[1].numpy())
+        if t is dup:
+            # >= 3 duplicates: we sum in input order; ATen's CPU coalesce sorts
+            # unstably, so its fp32 order (hence the last bit) is not defined
+            np.testing.assert_allclose(a.val.cpu().numpy(), c.values().numpy(), rtol=1e-6, atol=1e-6)
+        else:   # the reference's own tensors (no duplicates): bit for bit
+            assert np.array_equal(a.val.cpu().numpy().view(np.uint32), c.values().numpy().view(np.uint32))
+    bad = torch.sparse_coo_tensor(torch.tensor([[0, 5], [1, 2]]), torch.tensor([1.0, 2.0]), (4, 4))
+    with pytest.raises(RuntimeError, match="outside its shape"):
+        from_torch(bad.to(DEV))
 
 
 def test_empty_graph_and_empty_rows_only():
@@ -296,6 +368,11 @@ def _labels_check(got, golden):
     return int(np.sum(~decided))
 
 
+# rows whose golden top-2 gap is <= 2e-4 (2x the logit tolerance): random-init
+# logits have near-ties no fp32 reordering can label bit-exactly; pinned per seed
+NEAR_TIES = {0: 11, 50494: 0, 99346: 29}
+
+
 @pytest.mark.parametrize("seed", [50494, 99346, 0])
 def test_gcn_eval_logits_match_reference(r8, golden_logits, seed):
     torch.manual_seed(seed)
@@ -305,7 +382,84 @@ def test_gcn_eval_logits_match_reference(r8, golden_logits, seed):
         lg = m(r8["features"].to(DEV), r8["adj"].to(DEV)).cpu().numpy()
     gold = golden_logits[f"eval_{seed}"]
     assert np.abs(lg - gold).max() <= LOGIT_TOL
-    _labels_check(lg, gold)
+    undecided = _labels_check(lg, gold)
+    print(f"seed {seed}: labels bit-exact on {len(gold) - undecided} rows, {undecided} near-tie rows excluded, "
+          f"{int(np.sum(lg.argmax(1) != gold.argmax(1)))} labels differ overall")
+    assert undecided == NEAR_TIES[seed]
+    # even among the near ties, at most a handful may flip
+    assert int(np.sum(lg.argmax(1) != gold.argmax(1))) <= undecided
+
+
+def test_graph_convolution_without_bias_forward_backward(r8):
+    """GraphConvolution(bias=False) (layer.py:62 registers bias=None and :111-112
+    returns the product alone) through the HIP path: forward and the gradients
+    of W and of a dense input against the oracle's reference module."""
+    from graph_convolutional_networks_for_text_classification_amd import GraphConvolution
+    torch.manual_seed(4)
+    gc = GraphConvolution(200, 16, bias=False).to(DEV)
+    assert gc.bias is None and "bias" not in dict(gc.named_parameters())
+    ref = gcn_ref.RefGraphConvolution(200, 16, bias=False)
+    ref.load_state_dict({k: v.cpu() for k, v in gc.state_dict().items()})
+    H = torch.randn(r8["nodes"], 200, generator=torch.Generator().manual_seed(5))
+    Hd = H.clone().to(DEV).requires_grad_(True)
+    Hc = H.clone().requires_grad_(True)
+    out = gc(Hd, r8["adj"].to(DEV))
+    out_ref = ref(Hc, r8["adj"])
+    assert (out.detach().cpu() - out_ref.detach()).abs().max() < 1e-4
+    w = torch.randn_like(out_ref)
+    (out * w.to(DEV)).sum().backward()
+    (out_ref * w).sum().backward()
+    np.testing.assert_allclose(gc.weight.grad.cpu().numpy(), ref.weight.grad.numpy(), rtol=1e-4, atol=1e-4)
+    np.testing.assert_allclose(Hd.grad.cpu().numpy(), Hc.grad.numpy(), rtol=1e-4, atol=1e-4)
+    # sparse input too (X of the reference, layer.py:102 with sparse infeatn)
+    gc1 = GraphConvolution(r8["nfeat"], 8, bias=False).to(DEV)
+    ref1 = gcn_ref.RefGraphConvolution(r8["nfeat"], 8, bias=False)
+    ref1.load_state_dict({k: v.cpu() for k, v in gc1.state_dict().items()})
+    o = gc1(r8["features"].to(DEV), r8["adj"].to(DEV))
+    o_ref = ref1(r8["features"], r8["adj"])
+    assert (o.detach().cpu() - o_ref.detach()).abs().max() < 1e-4
+    o.sum().backward()
+    o_ref.sum().backward()
+    np.testing.assert_allclose(gc1.weight.grad.cpu().numpy(), ref1.weight.grad.numpy(), rtol=1e-4, atol=1e-5)
+
+
+def test_gcn_gensim_shaped_r8_forward_backward(r8):
+    """SURVEY §8(d) config 1's feature shape: R8 with the 100-d gensim-style X
+    the README's 94.11 % run used (documents: the reference's LDA theta in
+    columns 0-49; topics: N(0,1) 100-d rows, L2-normalised; default_rng(0);
+    nnz 388,700) -- X is then two dense blocks on the MFMA tile path.  Eval
+    logits and one train-mode step's gradients against the oracle."""
+    ndoc, ntopic = r8["ndoc"], r8["ntopic"]
+    X = np.zeros((r8["nodes"], 100), np.float32)
+    X[:ndoc, :ntopic] = r8["x_doc"] if "x_doc" in r8 else r8["features_dense"][:ndoc, :ntopic]
+    X[ndoc:] = np.random.default_rng(0).standard_normal((ntopic, 100))
+    X /= np.maximum(np.linalg.norm(X, axis=1, keepdims=True), 1e-12)
+    Xs = datasets.dense_to_coo(X)
+    assert Xs._nnz() == 388_700
+    torch.manual_seed(50494)
+    m = GCN(nfeat=100, nhid=200, nclass=r8["nclass"], dropout=0.5).to(DEV)
+    ref = gcn_ref.RefGCN(nfeat=100, nhid=200, nclass=r8["nclass"], dropout=0.5)
+    ref.load_state_dict({k: v.cpu() for k, v in m.state_dict().items()})
+    m.eval()
+    ref.eval()
+    with torch.no_grad():
+        lg = m(Xs.to(DEV), r8["adj"].to(DEV)).cpu().numpy()
+        want = ref(Xs, r8["adj"]).numpy()
+    assert np.abs(lg - want).max() <= LOGIT_TOL
+    _labels_check(lg, want)
+    m.train()
+    ref.train()
+    torch.manual_seed(7)
+    out = m(Xs.to(DEV), r8["adj"].to(DEV))
+    torch.manual_seed(7)
+    out_ref = ref(Xs, r8["adj"])                    # same CPU dropout stream (dropout_rng="cpu")
+    assert (out.detach().cpu() - out_ref.detach()).abs().max() <= LOGIT_TOL
+    tgt = torch.from_numpy(np.concatenate([r8["target"], np.zeros(ntopic, np.int64)]))
+    torch.nn.functional.cross_entropy(out, tgt.to(DEV)).backward()
+    torch.nn.functional.cross_entropy(out_ref, tgt).backward()
+    for (k, p), (_, q) in zip(m.named_parameters(), ref.named_parameters()):
+        np.testing.assert_allclose(p.grad.cpu().numpy(), q.grad.numpy(), rtol=1e-4,
+                                   atol=1e-4 * max(1.0, float(q.grad.abs().max())), err_msg=k)
 
 
 def test_gcn_dense_features_path(r8, golden_logits):
@@ -430,8 +584,8 @@ def test_spmm_1m_20m_f256_sampled_rows_and_linearity(big_graph):
 
 def test_column_sharded_spmm_single_rank_on_gpu(big_graph):
     """BASELINE config 5's sharding module on one rank through the HIP kernels
-    (world 1: the shard is the whole operand): F = 512 block of a 4096-wide
-    operand on the 1M/20M graph, equal to the unsharded product."""
+    (no process group: the shard is the whole operand): F = 512 block of a
+    4096-wide operand on the 1M/20M graph, equal to the unsharded product."""
     from graph_convolutional_networks_for_text_classification_amd.parallel import ColumnShardedSpMM
     a, _ = big_graph
     F = 512
@@ -439,7 +593,48 @@ def test_column_sharded_spmm_single_rank_on_gpu(big_graph):
     op = ColumnShardedSpMM(a, F)
     full = op(op.shard(B))
     assert full.shape == (a.shape[0], F)
-    assert torch.equal(full, spmm(a, B))
+    assert torch.equal(full.block(0), spmm(a, B))
+
+
+def test_rccl_process_group_collectives_on_gpu(r8):
+    """The sharded path over a real RCCL (torch "nccl") process group of one
+    rank on this GPU: ColumnShardedSpMM's all_gather_into_tensor and
+    sharded_gcn_forward's all_reduce run through RCCL; results equal the
+    unsharded HIP products bit for bit and the oracle within tolerance.  (N > 1
+    is covered by the gloo world-2 tests; the driver's 8-GPU runs use RCCL.)"""
+    import socket
+    import torch.distributed as dist
+    from graph_convolutional_networks_for_text_classification_amd.parallel import (
+        ColumnShardedSpMM, sharded_gcn_forward)
+    with socket.socket() as sk:
+        sk.bind(("127.0.0.1", 0))
+        port = sk.getsockname()[1]
+    dist.init_process_group("nccl", init_method=f"tcp://127.0.0.1:{port}", rank=0, world_size=1,
+                            device_id=torch.device(DEV, 0))
+    try:
+        assert dist.get_backend() == "nccl"
+        a = from_torch(r8["adj"].to(DEV))
+        rp, ci, v = (t.cpu().numpy() for t in (a.rowptr, a.colind, a.val))
+        F = 256
+        B = torch.randn(r8["nodes"], F, device=DEV, generator=torch.Generator(device=DEV).manual_seed(9))
+        bias = torch.randn(F, device=DEV, generator=torch.Generator(device=DEV).manual_seed(10))
+        op = ColumnShardedSpMM(a, F)
+        gathered = op(op.shard(B), bias=bias, epilogue=_lib.EPI_BIAS_RELU)      # RCCL all-gather
+        want = spmm(a, B, bias=bias, epilogue=_lib.EPI_BIAS_RELU)
+        assert torch.equal(gathered.to_dense(), want)
+        _close(gathered.block(0), csr_ref.spmm_epilogue(csr_ref.spmm_csr(rp, ci, v, B.cpu().numpy()),
+                                                        bias.cpu().numpy(), relu=True))
+        # a consumer product reading the gathered blocks in place
+        assert torch.equal(gathered.spmm(a), spmm(a, want))
+        torch.manual_seed(0)
+        m = GCN(nfeat=r8["nfeat"], nhid=200, nclass=r8["nclass"], dropout=0.5).to(DEV).eval()
+        with torch.no_grad():
+            got = sharded_gcn_forward(m, r8["features"].to(DEV), r8["adj"].to(DEV))   # RCCL all-reduce
+            ref = m(r8["features"].to(DEV), r8["adj"].to(DEV))
+        assert (got - ref).abs().max().item() <= 1e-5
+        torch.cuda.synchronize()
+    finally:
+        dist.destroy_process_group()
 
 
 # ------------------------------------------------------------------------------ device adjacency preparation

@@ -76,11 +76,15 @@ def _worker(rank, world, port, F, q):
         B = torch.from_numpy(rng.standard_normal((a.shape[1], F)).astype(np.float32))
         bias = torch.from_numpy(rng.standard_normal(F).astype(np.float32))
         op = ColumnShardedSpMM(a, F, kernels=k)
-        full = op(op.shard(B), bias=bias, epilogue=_lib.EPI_BIAS_RELU)
+        gathered = op(op.shard(B), bias=bias, epilogue=_lib.EPI_BIAS_RELU)
+        full = gathered.to_dense()
+        # a consumer reading the gathered blocks in place: A @ C, block by block
+        consumer = gathered.spmm(a, kernels=k)
+        assert gathered.block(op.rank).data_ptr() == gathered.buf[op.rank].data_ptr()   # zero-copy view
         block = op(op.shard(B), bias=bias, epilogue=_lib.EPI_BIAS_RELU, gather=False)
         # GCN eval forward with gc1's hidden columns sharded (all-reduce of H1 W2)
         logits = sharded_gcn_forward(_model(a.shape[1]), types.SimpleNamespace(csr=a, dense=None), a, kernels=k)
-        q.put((rank, full.numpy(), block.numpy(), op.columns, logits.numpy()))
+        q.put((rank, full.numpy(), block.numpy(), op.columns, logits.numpy(), consumer.numpy()))
     finally:
         dist.destroy_process_group()
 
@@ -107,8 +111,8 @@ def test_column_sharded_spmm_and_gcn_world2_gloo(F):
         p.start()
     res = {}
     for _ in range(world):
-        rank, full, block, cols, logits = q.get(timeout=180)
-        res[rank] = (full, block, cols, logits)
+        rank, full, block, cols, logits, consumer = q.get(timeout=180)
+        res[rank] = (full, block, cols, logits, consumer)
     for p in procs:
         p.join(timeout=60)
         assert p.exitcode == 0
@@ -121,9 +125,11 @@ def test_column_sharded_spmm_and_gcn_world2_gloo(F):
     m = _model(a.shape[1])
     H1 = k.spmm(a, k.spmm(a, m.gc1.weight), bias=m.gc1.bias, epilogue=_lib.EPI_BIAS_RELU)
     ref_logits = k.spmm(a, k.gemm(H1, m.gc2.weight), bias=m.gc2.bias, epilogue=_lib.EPI_BIAS).numpy()
+    ref_consumer = k.spmm(a, torch.from_numpy(ref)).numpy()
     assert sorted(res) == [0, 1]
     for rank in range(world):
-        full, block, (c0, c1), logits = res[rank]
-        np.testing.assert_array_equal(full, ref)                        # all-gather re-layout is exact
+        full, block, (c0, c1), logits, consumer = res[rank]
+        np.testing.assert_array_equal(full, ref)                        # the gathered blocks are exact
+        np.testing.assert_allclose(consumer, ref_consumer, rtol=1e-5, atol=1e-5)
         np.testing.assert_array_equal(block[:, : c1 - c0], ref[:, c0:c1])
         np.testing.assert_allclose(logits, ref_logits, rtol=1e-5, atol=1e-4)

@@ -67,7 +67,8 @@ __host__ __device__ inline int64_t align4(int64_t x) { return (x + 3) & ~3LL; }
 //            (dest = row of C), then one per hub it touches, hub order
 //            (dest = -(partial row + 1))
 //   o_it..   items {slot, value bits}[nitems]: an output's items run from the
-//            previous output's end; every item reads its B row from the
+//            previous output's end, padded to a multiple of 4 with {nstage, 0}
+//            (slot nstage is a zero row); every item reads its B row from the
 //            block's stage in LDS (blocks are cut so that all the rows they
 //            reference fit: no LDS-or-global select in the inner loop, which
 //            would turn the LDS reads into FLAT loads ordered behind the
@@ -100,8 +101,12 @@ hub_light_kernel(const int32_t* __restrict__ recs, int32_t R, const float* __res
   using V = Vec<VEC>;
   using T = typename V::T;
   constexpr int SG = BLOCK / LPR;  // lane groups per workgroup
-  constexpr int SU = (64 * 64 + BLOCK - 1) / BLOCK;  // staging loads per thread: a 64-slot x 256-float tile
-  constexpr int U = 8;             // items per batch
+  // staging loads per thread: kHubSmax rows + the zero row of a 64-vector tile
+  constexpr int SU = ((kHubSmax + 1) * 64 + BLOCK - 1) / BLOCK;
+#ifndef GCNK_HUB_U
+#define GCNK_HUB_U 8
+#endif
+  constexpr int U = GCNK_HUB_U;    // items per batch
   extern __shared__ __attribute__((aligned(16))) int32_t smem[];
   int32_t* s_rec = smem;
   float* s_stage = reinterpret_cast<float*>(smem + R);
@@ -128,9 +133,14 @@ hub_light_kernel(const int32_t* __restrict__ recs, int32_t R, const float* __res
   const bool colok = lcol < Fw;
   const T bv = (epi.bias && colok) ? V::load(epi.bias + colv) : V::zero();
 
-  // ---- stage: element e = slot * nq + q (VEC floats each) -> s_stage[e * VEC];
-  //      thread tid takes e = tid + j * BLOCK (slot / column stepped, no division
-  //      per element), all of its loads in flight before the LDS stores
+  // ---- stage: row s of the tile at s_stage[s * SW] (SW = LPR * VEC floats, a
+  //      power of two: an item's row address is one shift-add), element e =
+  //      s * nq + q (VEC floats each); thread tid takes e = tid + j * BLOCK
+  //      (slot / column stepped, no division per element), all of its loads in
+  //      flight before the LDS stores.  Row nstage is all zeros: the padding
+  //      items of the plan point at it.
+  constexpr int SW = LPR * VEC;
+  constexpr int SWL = __builtin_ctz(SW);
   const int32_t nq = (Fw + VEC - 1) / VEC;
   const int32_t total = nstage * nq;
   {
@@ -141,7 +151,7 @@ hub_light_kernel(const int32_t* __restrict__ recs, int32_t R, const float* __res
     for (int j = 0; j < SU; ++j) {
       v[j] = V::zero();
 #if defined(GCNK_HUB_EXP) && GCNK_HUB_EXP >= 8  // ablation: no staging loads
-      if (s0 < nstage) v[j] = V::zero();
+      (void)ldb;
 #else
       if (s0 < nstage) v[j] = V::load(B + (int64_t)s_rec[4 + s0] * ldb + c0 + (int64_t)q0 * VEC);
 #endif
@@ -152,101 +162,124 @@ hub_light_kernel(const int32_t* __restrict__ recs, int32_t R, const float* __res
         ++s0;
       }
     }
+    s0 = tid / nq;
+    q0 = tid - s0 * nq;
 #pragma unroll
     for (int j = 0; j < SU; ++j) {
-      const int32_t e = tid + j * BLOCK;
-      if (e < total) V::store(s_stage + (int64_t)e * VEC, v[j]);
+      if (s0 <= nstage) V::store(s_stage + (s0 << SWL) + q0 * VEC, v[j]);  // s0 == nstage: the zero row
+      s0 += ds;
+      q0 += dq;
+      if (q0 >= nq) {
+        q0 -= nq;
+        ++s0;
+      }
     }
   }
   __syncthreads();
   stamp(epi, 2);
 
-  // ---- outputs.  Whole-wavefront groups (LPR = 64): wave w takes a contiguous
-  //      range of outputs, reads their {dest, end} descriptors once (one per
-  //      lane) and keeps a 64-item window of {slot, value} in registers, so an
-  //      output costs one batch of stage reads per 8 items: slots and values
-  //      broadcast with v_readlane (scalar addresses), the 8 LDS row reads
-  //      issued together (past the end: the last item again, its term
-  //      dropped), no other LDS round trip.  Narrower groups (several outputs
-  //      per wavefront, F <= 128): items at a clamped index, stage reads all
-  //      issued, invalid terms dropped by a select.  Idle lanes (columns past
-  //      the tile) read their natural address (the stage is padded), which
-  //      keeps the wavefront's row read conflict-free.
-  const int32_t sw = nq * VEC;  // staged row stride (floats)
-  const int2* s_items = reinterpret_cast<const int2*>(s_rec + o_it);
-  const int2* s_out = reinterpret_cast<const int2*>(s_rec + o_out);
+  // ---- outputs.  Lane group g (a whole wavefront at LPR = 64, which takes a
+  //      contiguous range of outputs) walks its outputs' items in groups of 4
+  //      (the plan pads every output to a multiple of 4 with {zero row, 0}):
+  //      two 16-B reads bring 4 {slot, value} items (the same address for the
+  //      whole group: a broadcast), four row reads, eight packed FMAs -- no
+  //      guards, no selects, no per-item scalar work.  Idle lanes (columns past
+  //      the tile) read inside their row, keeping the read conflict-free.
+  const int4* s_items4 = reinterpret_cast<const int4*>(s_rec + o_it);
   const bool fast_epi = VEC == 4 && epi.code <= GCNK_EPI_BIAS_RELU;
-  const int lane = tid & 63;
-  const int32_t nitems = s_rec[3];
+  if constexpr (LPR == 64 && VEC == 4) {
+    // Two outputs per wavefront: half-wave group h (32 lanes) owns a contiguous
+    // range of outputs; lane hl holds columns 4 hl and 128 + 4 hl of the tile,
+    // so each of its two row reads is contiguous across the half (conflict-free)
+    // and every instruction of the walk and the epilogue serves two outputs.
+    constexpr int HG = BLOCK / 32;
+    const int hl = tid & 31, h = tid >> 5;
+    const int32_t ca = 4 * hl, cb = 128 + 4 * hl;
+    const bool oka = ca < Fw, okb = cb < Fw;
+    const float4 ba = (epi.bias && oka) ? *reinterpret_cast<const float4*>(epi.bias + c0 + ca) : V::zero();
+    const float4 bb = (epi.bias && okb) ? *reinterpret_cast<const float4*>(epi.bias + c0 + cb) : V::zero();
+    const int32_t og0 = (int32_t)((int64_t)nout * h / HG), og1 = (int32_t)((int64_t)nout * (h + 1) / HG);
+    const float* sa = s_stage + ca;
+    const float* sb = s_stage + cb;
+    int32_t ib = og0 == 0 ? 0 : s_rec[o_out + 2 * og0 - 1];
+    for (int32_t o = og0; o < og1; ++o) {
+      const int32_t dest = s_rec[o_out + 2 * o], ie = s_rec[o_out + 2 * o + 1];
+      float4 xa = V::zero(), xb = V::zero();
+      for (int32_t k = ib; k < ie; k += 4) {
+        const int4 p0 = s_items4[k >> 1], p1 = s_items4[(k >> 1) + 1];  // items k .. k + 3
+        const int32_t r0 = p0.x << 8, r1 = p0.z << 8, r2 = p1.x << 8, r3 = p1.z << 8;
+        const float4 a0 = V::load(sa + r0), a1 = V::load(sa + r1), a2 = V::load(sa + r2), a3 = V::load(sa + r3);
+        const float4 b0 = V::load(sb + r0), b1 = V::load(sb + r1), b2 = V::load(sb + r2), b3 = V::load(sb + r3);
+        V::fma(xa, __int_as_float(p0.y), a0);
+        V::fma(xb, __int_as_float(p0.y), b0);
+        V::fma(xa, __int_as_float(p0.w), a1);
+        V::fma(xb, __int_as_float(p0.w), b1);
+        V::fma(xa, __int_as_float(p1.y), a2);
+        V::fma(xb, __int_as_float(p1.y), b2);
+        V::fma(xa, __int_as_float(p1.w), a3);
+        V::fma(xb, __int_as_float(p1.w), b3);
+      }
+      ib = ie;
+#ifdef GCNK_HUB_EXP
+      if (((GCNK_HUB_EXP & 1) && dest < 0) || ((GCNK_HUB_EXP & 2) && dest >= 0)) {
+        if (xa.x == 1234.5f) V::store(C, xb);  // keeps the sums live
+        continue;
+      }
+#endif
+      if (dest >= 0) {
+        if (fast_epi) {
+          if (epi.code != GCNK_EPI_NONE) {
+            V::add(xa, ba);
+            V::add(xb, bb);
+            if (epi.code == GCNK_EPI_BIAS_RELU) {
+              xa.x = fmaxf(xa.x, 0.f); xa.y = fmaxf(xa.y, 0.f); xa.z = fmaxf(xa.z, 0.f); xa.w = fmaxf(xa.w, 0.f);
+              xb.x = fmaxf(xb.x, 0.f); xb.y = fmaxf(xb.y, 0.f); xb.z = fmaxf(xb.z, 0.f); xb.w = fmaxf(xb.w, 0.f);
+            }
+          }
+        } else {
+          xa = V::epi(epi, xa, ba, dest, c0 + ca);
+          xb = V::epi(epi, xb, bb, dest, c0 + cb);
+        }
+      }
+      float* dst = dest >= 0 ? C + (int64_t)dest * ldc + c0 : part + (int64_t)(-dest - 1) * part_ld + c0;
+      if (oka) V::store_aligned(dst + ca, xa);
+      if (okb) V::store_aligned(dst + cb, xb);
+    }
+#ifdef GCNK_STAMPS
+    __syncthreads();
+    stamp(epi, 3);
+#endif
+    return;
+  }
   constexpr int NW = BLOCK / 64;
   const int w = __builtin_amdgcn_readfirstlane(tid >> 6);  // wave-uniform (the compiler cannot tell)
-  // whole-wavefront groups: this wave's outputs [ow0, ow1); narrow groups: g, g + SG, ...
   const int32_t ow0 = LPR == 64 ? (int32_t)((int64_t)nout * w / NW) : g;
   const int32_t ow1 = LPR == 64 ? (int32_t)((int64_t)nout * (w + 1) / NW) : nout;
-  int2 desc = make_int2(0, 0), win = make_int2(0, 0);
-  int32_t dbase = -1, wbase = -1, ib = 0;
+  const float* srow = s_stage + lcol;
+  int32_t ib = ow0 == 0 ? 0 : s_rec[o_out + 2 * ow0 - 1];
+  if (LPR == 64) ib = __builtin_amdgcn_readfirstlane(ib);
   for (int32_t o = ow0; o < ow1; o += (LPR == 64 ? 1 : SG)) {
-    int32_t dest, ie;
-    T acc = V::zero();
-    if constexpr (LPR == 64) {
-      if (dbase < 0 || o >= dbase + 64) {  // next 64 descriptors (and where this range's items start)
-        dbase = o;
-        desc = s_out[min(o + lane, ow1 - 1)];
-        ib = o == 0 ? 0 : __builtin_amdgcn_readfirstlane(s_rec[o_out + 2 * o - 1]);
-      }
-      dest = __builtin_amdgcn_readlane(desc.x, o - dbase);
-      ie = __builtin_amdgcn_readlane(desc.y, o - dbase);
-#if defined(GCNK_HUB_EXP) && (GCNK_HUB_EXP & 16)  // ablation: no item loop
-      ib = ie;
-#endif
-      for (int32_t k = ib; k < ie; k += U) {
-        if (wbase < 0 || k < wbase || min(k + U, ie) > wbase + 64) {
-          wbase = k;
-          win = s_items[min(wbase + lane, nitems - 1)];
-        }
-        int32_t sl[U];
-        float av[U];
-#pragma unroll
-        for (int u = 0; u < U; ++u) {
-          const int32_t kk = min(k + u, ie - 1) - wbase;
-          sl[u] = __builtin_amdgcn_readlane(win.x, kk);
-          av[u] = __int_as_float(__builtin_amdgcn_readlane(win.y, kk));
-        }
-        T gv[U];
-#pragma unroll
-        for (int u = 0; u < U; ++u) gv[u] = V::load(s_stage + sl[u] * sw + lcol);
-        // past the output's end: both operands zeroed (0 * 0 adds nothing, even
-        // next to an infinite row); a guarded FMA would let the compiler sink the
-        // read into the branch and wait for it there
-#pragma unroll
-        for (int u = 0; u < U; ++u) {
-          const bool live = k + u < ie;
-          V::fma(acc, live ? av[u] : 0.f, live ? gv[u] : V::zero());
-        }
-      }
-      ib = ie;
+    int32_t dest = s_rec[o_out + 2 * o], ie = s_rec[o_out + 2 * o + 1];
+    if (LPR == 64) {
+      dest = __builtin_amdgcn_readfirstlane(dest);
+      ie = __builtin_amdgcn_readfirstlane(ie);
     } else {
-      dest = s_rec[o_out + 2 * o];
-      ie = s_rec[o_out + 2 * o + 1];
-      int32_t ib0 = o == 0 ? 0 : s_rec[o_out + 2 * o - 1];
-#if defined(GCNK_HUB_EXP) && (GCNK_HUB_EXP & 16)  // ablation: no item loop
-      ib0 = ie;
-#endif
-      for (int32_t k0 = ib0; k0 < ie; k0 += U) {
-        int2 it[U];
-#pragma unroll
-        for (int j = 0; j < U; ++j) it[j] = s_items[min(k0 + j, ie - 1)];
-        T gv[U];
-#pragma unroll
-        for (int j = 0; j < U; ++j) gv[j] = V::load(s_stage + it[j].x * sw + lcol);
-#pragma unroll
-        for (int j = 0; j < U; ++j) {
-          T t = acc;
-          V::fma(t, __int_as_float(it[j].y), gv[j]);
-          if (k0 + j < ie) acc = t;
-        }
-      }
+      ib = o == 0 ? 0 : s_rec[o_out + 2 * o - 1];
     }
+    T acc = V::zero();
+#if defined(GCNK_HUB_EXP) && (GCNK_HUB_EXP & 16)  // ablation: no item loop
+    ib = ie;
+#endif
+    for (int32_t k = ib; k < ie; k += 4) {
+      const int4 p0 = s_items4[k >> 1], p1 = s_items4[(k >> 1) + 1];  // items k .. k + 3
+      const T g0 = V::load(srow + (p0.x << SWL)), g1 = V::load(srow + (p0.z << SWL));
+      const T g2 = V::load(srow + (p1.x << SWL)), g3 = V::load(srow + (p1.z << SWL));
+      V::fma(acc, __int_as_float(p0.y), g0);
+      V::fma(acc, __int_as_float(p0.w), g1);
+      V::fma(acc, __int_as_float(p1.y), g2);
+      V::fma(acc, __int_as_float(p1.w), g3);
+    }
+    ib = ie;
     if (!colok) continue;
 #ifdef GCNK_HUB_EXP  // ablation builds (scripts/hub_probe.py): 1 no partial stores, 2 no C stores, 4 neither
     if (((GCNK_HUB_EXP & 1) && dest < 0) || ((GCNK_HUB_EXP & 2) && dest >= 0)) {
@@ -364,8 +397,9 @@ int hub_launch(const HubArgs& a) {
   const int64_t tile = (int64_t)LPR * VEC;
   const int64_t ntiles = (a.F + tile - 1) / tile;
   const int64_t TW = std::min<int64_t>(a.F, tile);
-  // + one tile of padding: idle lanes read past the last staged row
-  const int64_t lds = a.L.R * 4 + (a.L.max_stage * ((TW + VEC - 1) / VEC * VEC) + tile) * 4;
+  // staged rows at a stride of one tile (LPR * VEC floats) + the zero row
+  (void)TW;
+  const int64_t lds = a.L.R * 4 + (a.L.max_stage + 1) * tile * 4;
   if (lds > kLdsMax || ntiles > 65535) {
     set_error("gcnk_spmm (hub plan): %lld B of LDS / %lld column tiles exceed the launch limits", (long long)lds,
               (long long)ntiles);
@@ -597,12 +631,12 @@ int hub_plan_host(const int32_t* rp, const int32_t* ci, const float* vv, int32_t
     for (size_t s = 0; s < staged.size(); ++s) slot[(size_t)staged[s]] = (int32_t)s;
     const int64_t nstage = (int64_t)staged.size(), nl = i1 - i0, ng = (int64_t)bg[(size_t)b].size();
     const int64_t o_out = align4(4 + nstage), o_it = align4(o_out + 2 * (nl + ng));
+    nit += 3 * (nl + ng);  // room for the padding of every output to a multiple of 4 items
     std::vector<int32_t>& w = recs[(size_t)b];
     w.assign((size_t)(o_it + 2 * nit), 0);
     w[0] = (int32_t)nstage;
     w[1] = (int32_t)nl;
     w[2] = (int32_t)ng;
-    w[3] = (int32_t)nit;
     std::copy(staged.begin(), staged.end(), w.begin() + 4);
     int64_t it = 0, o = 0;
     auto item = [&](int32_t c, float v) {
@@ -610,19 +644,31 @@ int hub_plan_host(const int32_t* rp, const int32_t* ci, const float* vv, int32_t
       w[(size_t)(o_it + 2 * it + 1)] = __builtin_bit_cast(int32_t, v);
       ++it;
     };
+    // every output's items padded to a multiple of 4 with {zero row (slot nstage), 0}
+    auto pad = [&]() {
+      while (it % 4) {
+        w[(size_t)(o_it + 2 * it)] = (int32_t)nstage;
+        w[(size_t)(o_it + 2 * it + 1)] = 0;
+        ++it;
+      }
+    };
     for (int64_t i = i0; i < i1; ++i, ++o) {
       const int32_t r = light[(size_t)ord[(size_t)i]];
       for (int64_t k = rp[r]; k < rp[r + 1]; ++k) item(ci[k], vv ? vv[k] : 0.f);
+      pad();
       w[(size_t)(o_out + 2 * o)] = r;
       w[(size_t)(o_out + 2 * o + 1)] = (int32_t)it;
     }
     for (const Group& g : bg[(size_t)b]) {
       for (int64_t e = g.b; e < g.e; ++e) item(ecol[(size_t)b][(size_t)e], eval[(size_t)b][(size_t)e]);
+      pad();
       const int64_t p = part_off[(size_t)g.h] + seen[(size_t)g.h]++;
       w[(size_t)(o_out + 2 * o)] = (int32_t)(-p - 1);
       w[(size_t)(o_out + 2 * o + 1)] = (int32_t)it;
       ++o;
     }
+    w[3] = (int32_t)it;
+    w.resize((size_t)(o_it + 2 * it));
     for (int32_t c : touched) {
       cnt[(size_t)c] = 0;
       slot[(size_t)c] = -1;

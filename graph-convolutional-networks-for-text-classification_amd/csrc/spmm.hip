@@ -272,12 +272,29 @@ __device__ __forceinline__ const float* uniform_ptr(const float* p) {
   return reinterpret_cast<const float*>(((uint64_t)hi << 32) | lo);
 }
 
+// B[c, col..] (VEC floats).  O32: through a 32-bit byte offset from the
+// uniform base -- one scalar multiply and one vector add per row piece, the
+// load taking the SGPR base -- where the 64-bit index costs ~7 scalar
+// instructions per gathered row (the CU's one scalar unit was the row kernel's
+// limiter: ~8k SALU per CU per R8 launch).  Needs K * ldb * 4 + F * 4 < 2^32
+// (checked at launch).  col4 = the lane's column offset in bytes.
+template <int VEC, bool O32>
+__device__ __forceinline__ typename Vec<VEC>::T load_row(const float* __restrict__ B, int64_t ldb, uint32_t ldb4,
+                                                       int32_t c, int64_t colv, uint32_t col4) {
+  if constexpr (O32)
+    return Vec<VEC>::load(
+        reinterpret_cast<const float*>(reinterpret_cast<const char*>(B) + ((uint32_t)c * ldb4 + col4)));
+  else
+    return Vec<VEC>::load(B + (int64_t)c * ldb + colv);
+}
+
 // acc += sum of val * B[col, colv..] over items k = b + q + S*i, i ascending,
 // U gathers in flight per batch (all issued before the first FMA).
-template <int VEC, int U, int S>
+template <int VEC, int U, int S, bool O32>
 __device__ __forceinline__ void gather_rows(const int2* __restrict__ items, int32_t b, int32_t e, int q,
                                             const float* __restrict__ B, int64_t ldb, int64_t colv, bool colok,
                                             typename Vec<VEC>::T& acc) {
+  const uint32_t ldb4 = (uint32_t)ldb * 4u, col4 = colok ? (uint32_t)colv * 4u : 0u;
   using V = Vec<VEC>;
   using T = typename V::T;
   for (int32_t k0 = b + q; k0 < e; k0 += S * U) {
@@ -290,7 +307,7 @@ __device__ __forceinline__ void gather_rows(const int2* __restrict__ items, int3
     T g[U];
 #pragma unroll
     for (int j = 0; j < U; ++j)
-      g[j] = (it[j].x >= 0 && colok) ? V::load(B + (int64_t)it[j].x * ldb + colv) : V::zero();
+      g[j] = it[j].x >= 0 ? load_row<VEC, O32>(B, ldb, ldb4, it[j].x, colok ? colv : 0, col4) : V::zero();
 #pragma unroll
     for (int j = 0; j < U; ++j)
       if (it[j].x >= 0) V::fma(acc, __int_as_float(it[j].y), g[j]);
@@ -302,13 +319,15 @@ __device__ __forceinline__ void gather_rows(const int2* __restrict__ items, int3
 // b + q + S*l) and are broadcast with v_readlane, so a batch of U gathers
 // waits for one latency instead of an item load and then the gathers (a heavy
 // segment's 4 batches: 5 latencies instead of 8).
-template <int VEC, int U, int S>
+template <int VEC, int U, int S, bool O32>
 __device__ __forceinline__ void gather_rows_wave(const int2* __restrict__ items, int32_t b, int32_t e, int q,
                                                  const float* __restrict__ B, int64_t ldb, int64_t colv, bool colok,
                                                  typename Vec<VEC>::T& acc) {
   using V = Vec<VEC>;
   using T = typename V::T;
   const int lane = threadIdx.x & 63;
+  const uint32_t ldb4 = (uint32_t)ldb * 4u, col4 = colok ? (uint32_t)colv * 4u : 0u;
+  const int64_t colc = colok ? colv : 0;  // idle lanes read inside the row (no branch around the load)
   for (int32_t base = b + q; base < e; base += 64 * S) {
     const int32_t k = base + S * lane;
     const int2 mine = k < e ? items[k] : make_int2(-1, 0);
@@ -323,7 +342,7 @@ __device__ __forceinline__ void gather_rows_wave(const int2* __restrict__ items,
         if (j0 + j < cnt) {
           const int32_t c = __builtin_amdgcn_readlane(mine.x, j0 + j);
           a[j] = __int_as_float(__builtin_amdgcn_readlane(mine.y, j0 + j));
-          if (colok) g[j] = V::load(B + (int64_t)c * ldb + colv);
+          g[j] = load_row<VEC, O32>(B, ldb, ldb4, c, colc, col4);
         }
       }
 #pragma unroll
@@ -361,7 +380,7 @@ __device__ __forceinline__ void finish_row(const typename Vec<VEC>::T& acc, int3
 // grid.x: [0, nhb) heavy blocks, one heavy segment per wavefront (per
 // workgroup for 64-lane groups); then light blocks, one light row per lane
 // group.  grid.y: column tiles of LPR*VEC.
-template <int BLOCK, int LPR, int VEC, int U, int NP>
+template <int BLOCK, int LPR, int VEC, int U, int NP, bool O32>
 __global__ void __launch_bounds__(BLOCK)
 spmm_row_kernel(RowPlan rp, int32_t nhb, const float* __restrict__ B, int64_t ldb, int32_t F,
                 float* __restrict__ C, int64_t ldc, Epi epi, float* __restrict__ part, int64_t part_ld,
@@ -409,6 +428,8 @@ spmm_row_kernel(RowPlan rp, int32_t nhb, const float* __restrict__ B, int64_t ld
       for (int r = 0; r < R; ++r)
         if (lane >= nb[r] && lane < nb[r + 1]) k = un[r].y + lane - nb[r];
       const int2 mine = k >= 0 ? rp.items[k] : make_int2(-1, 0);
+      const uint32_t ldb4 = (uint32_t)ldb * 4u, col4 = colok ? (uint32_t)colv * 4u : 0u;
+      const int64_t colc = colok ? colv : 0;  // idle lanes read inside the row (no branch around the load)
       T accs[R];
 #pragma unroll
       for (int r = 0; r < R; ++r) accs[r] = V::zero();
@@ -423,7 +444,7 @@ spmm_row_kernel(RowPlan rp, int32_t nhb, const float* __restrict__ B, int64_t ld
           if (j0 + j < cnt) {
             const int32_t c = __builtin_amdgcn_readlane(mine.x, j0 + j);
             a[j] = __int_as_float(__builtin_amdgcn_readlane(mine.y, j0 + j));
-            if (colok) g[j] = V::load(B + (int64_t)c * ldb + colv);
+            g[j] = load_row<VEC, O32>(B, ldb, ldb4, c, colc, col4);
           }
         }
 #pragma unroll
@@ -447,7 +468,7 @@ spmm_row_kernel(RowPlan rp, int32_t nhb, const float* __restrict__ B, int64_t ld
     const int4 un = rp.units[u];
     if (un.x < 0) return;  // padding of the XCD-class layout
     stamp(epi, 1);
-    gather_rows<VEC, U, 1>(rp.items, un.y, un.z, 0, B, ldb, colv, colok, acc);
+    gather_rows<VEC, U, 1, O32>(rp.items, un.y, un.z, 0, B, ldb, colv, colok, acc);
     stamp(epi, 2);
     finish_row<LPR, VEC, NP>(acc, un.x, colv, colok, bv, lg, C, ldc, epi, store_main, proj, pa);
     stamp(epi, 3);
@@ -471,8 +492,8 @@ spmm_row_kernel(RowPlan rp, int32_t nhb, const float* __restrict__ B, int64_t ld
   const int4 un = rp.units[u];
   if (un.x < 0) return;           // padding of the XCD-class layout
   stamp(epi, 1);
-  if constexpr (LPR == 64) gather_rows_wave<VEC, kHeavyU, GS>(rp.items, un.y, un.z, q, B, ldb, colv, colok, acc);
-  else gather_rows<VEC, U, GS>(rp.items, un.y, un.z, q, B, ldb, colv, colok, acc);
+  if constexpr (LPR == 64) gather_rows_wave<VEC, kHeavyU, GS, O32>(rp.items, un.y, un.z, q, B, ldb, colv, colok, acc);
+  else gather_rows<VEC, U, GS, O32>(rp.items, un.y, un.z, q, B, ldb, colv, colok, acc);
   if constexpr (WG) {
     if (w > 0) s_red[w][lane] = acc;
     __syncthreads();
@@ -836,6 +857,7 @@ inline int choose_block(int lpr) { return lpr == 64 ? kWaveBlock : lpr >= 8 ? 25
 
 struct RowLaunch {
   RowPlan rp;
+  int32_t K;  // rows of B (bounds the 32-bit gather offsets)
   const float* B;
   int64_t ldb;
   int32_t F;
@@ -871,10 +893,17 @@ int launch_rows(const RowLaunch& a) {
     e.bias = e.bias ? e.bias + c0 : nullptr;
     e.mask = e.mask ? e.mask + c0 : nullptr;
     e.offset += (uint64_t)c0;  // hash index shifts with the column
-    hipLaunchKernelGGL((spmm_row_kernel<BLOCK, LPR, VEC, U, NP>),
-                       dim3((unsigned)(nhb + nlb), (unsigned)((Fw + tileF - 1) / tileF)), dim3(BLOCK), 0, a.s, a.rp,
-                       (int32_t)nhb, a.B + c0, a.ldb, Fw, a.C ? a.C + c0 : nullptr, a.ldc, e,
-                       a.part ? a.part + c0 : nullptr, a.part_ld, a.pa);
+    // 32-bit gather offsets when every byte the launch reads lies within 4 GB of its B base
+    const bool o32 = (int64_t)a.K * a.ldb * 4 + (int64_t)Fw * 4 < ((int64_t)1 << 32);
+    const dim3 grid((unsigned)(nhb + nlb), (unsigned)((Fw + tileF - 1) / tileF));
+    if (o32)
+      hipLaunchKernelGGL((spmm_row_kernel<BLOCK, LPR, VEC, U, NP, true>), grid, dim3(BLOCK), 0, a.s, a.rp, (int32_t)nhb,
+                         a.B + c0, a.ldb, Fw, a.C ? a.C + c0 : nullptr, a.ldc, e, a.part ? a.part + c0 : nullptr,
+                         a.part_ld, a.pa);
+    else
+      hipLaunchKernelGGL((spmm_row_kernel<BLOCK, LPR, VEC, U, NP, false>), grid, dim3(BLOCK), 0, a.s, a.rp,
+                         (int32_t)nhb, a.B + c0, a.ldb, Fw, a.C ? a.C + c0 : nullptr, a.ldc, e,
+                         a.part ? a.part + c0 : nullptr, a.part_ld, a.pa);
     const int rc = launch_check("spmm_row_kernel");
     if (rc) return rc;
   }
@@ -1569,7 +1598,7 @@ static int spmm_impl(const void* plan, const int32_t* hdr, const float* B, int64
   if (L.nunits > 0 && part != 1) {
     RowPlan rp{reinterpret_cast<const int2*>(p + L.items), reinterpret_cast<const int4*>(p + L.units),
                reinterpret_cast<const int4*>(p + L.heavy), counters, (int32_t)L.nunits, (int32_t)L.nhunits};
-    RowLaunch a{rp, B, ldb, F, C, ldc, e, workspace, part_ld, pa, s};
+    RowLaunch a{rp, K, B, ldb, F, C, ldc, e, workspace, part_ld, pa, s};
     if (proj) return pa.P <= 8 ? dispatch_rows_proj<8>(lpr, a) : dispatch_rows_proj<32>(lpr, a);
     return vec4 ? dispatch_rows<4>(lpr, a) : dispatch_rows<1>(lpr, a);
   }

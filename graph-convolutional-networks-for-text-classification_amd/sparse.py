@@ -38,7 +38,11 @@ def require_device(t, what):
 
 
 DENSE_THRESHOLD = 0.25  # row blocks at least this dense (condensed) run on the MFMA tile path
-HUB_MIN = 0             # hub-split plan: 0 = automatic hub threshold, > 0 = degree threshold, < 0 = never
+# hub-split plan: 0 = automatic hub threshold, > 0 = degree threshold, < 0 = never.
+# Off by default: on R8 it measured 13.4 us against the row-unit plan's 10.6 us
+# (DESIGN.md "Hub-split plan"); kept as an option for graphs with few, very
+# heavy hub rows.
+HUB_MIN = -1
 HUB_BLOCK_ROWS = 0      # light rows per hub-plan block (0 = automatic, ~256 blocks)
 
 

@@ -196,11 +196,12 @@ def test_spmm_two_streams_share_one_plan_concurrently(r8, kind, monkeypatch):
     hub plan has no cross-call state; the row-unit plan's heavy-row arrival
     counters live in a per-stream region (sparse.Plan.counters), so neither can
     corrupt the other: every output equals the single-stream result bit for bit."""
+    from graph_convolutional_networks_for_text_classification_amd import sparse as sp
     rng = np.random.default_rng(17)
     if kind == "hub":
+        monkeypatch.setattr(sp, "HUB_MIN", 0)
         a, K = from_torch(r8["adj"].to(DEV)), r8["nodes"]
     else:   # row-unit plan with multi-segment heavy rows (hub plan and tile path off)
-        from graph_convolutional_networks_for_text_classification_amd import sparse as sp
         monkeypatch.setattr(sp, "HUB_MIN", -1)
         M, K = 3001, 20003
         rp, ci, v = _random_csr(M, K, 20000, rng, heavy_rows=(5, 1700, 3000), heavy_deg=2500)
@@ -226,6 +227,27 @@ def test_spmm_two_streams_share_one_plan_concurrently(r8, kind, monkeypatch):
             assert torch.equal(o, ref[i])
     if kind == "row":
         assert len(plan._counters) >= 3, "one counter region per stream"
+
+
+@pytest.mark.parametrize("F", [1, 8, 24, 64, 200, 256, 300])
+def test_spmm_hub_plan_r8(r8, F, monkeypatch):
+    """The hub-split plan (optional, sparse.HUB_MIN >= 0) on the R8 adjacency:
+    light document blocks staged in LDS + the 50 topic rows summed from
+    per-block partials, every width class of the kernel, bias + ReLU epilogue,
+    against the float64 oracle; bit-identical on a second call."""
+    from graph_convolutional_networks_for_text_classification_amd import sparse as sp
+    monkeypatch.setattr(sp, "HUB_MIN", 0)
+    a = from_torch(r8["adj"].to(DEV))
+    rng = np.random.default_rng(F)
+    B = rng.standard_normal((r8["nodes"], F)).astype(np.float32)
+    b = rng.standard_normal(F).astype(np.float32)
+    got = spmm(a, torch.from_numpy(B).to(DEV), bias=torch.from_numpy(b).to(DEV), epilogue=_lib.EPI_BIAS_RELU)
+    plan = list(a._plans.values())[-1]
+    assert plan.is_hub and plan.header[6] == r8["ntopic"]
+    rp, ci, v = (t.cpu().numpy() for t in (a.rowptr, a.colind, a.val))
+    _close(got, csr_ref.spmm_epilogue(csr_ref.spmm_csr(rp, ci, v, B), b, relu=True), atol=2e-5)
+    again = spmm(a, torch.from_numpy(B).to(DEV), bias=torch.from_numpy(b).to(DEV), epilogue=_lib.EPI_BIAS_RELU)
+    assert torch.equal(got, again)
 
 
 def test_spmm_epilogues_and_strided_operands():

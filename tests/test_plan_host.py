@@ -64,9 +64,11 @@ def exec_hub_plan(plan, B):
             items = rec[o_it + 2 * ib: o_it + 2 * ie].reshape(-1, 2)
             slots = items[:, 0]
             vals = items[:, 1].copy().view(np.float32).astype(np.float64)
-            cols = np.where(slots >= 0, scols[np.clip(slots, 0, max(nstage - 1, 0))], -slots - 1)
-            assert np.all((slots >= 0) & (slots < nstage)), "every item reads a staged row"
-            acc = vals @ B[cols] if len(cols) else np.zeros(F)
+            assert (ie - ib) % 4 == 0, "items padded to a multiple of 4"
+            pad = slots == nstage                      # {zero row, 0} padding
+            assert np.all(vals[pad] == 0) and np.all((slots >= 0) & (slots <= nstage)), "items read staged rows"
+            cols = scols[np.clip(slots[~pad], 0, max(nstage - 1, 0))]
+            acc = vals[~pad] @ B[cols] if len(cols) else np.zeros(F)
             if dest >= 0:
                 assert o < nl, "light rows come first"
                 C[dest] = acc

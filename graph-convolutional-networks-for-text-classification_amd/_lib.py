@@ -50,7 +50,7 @@ SIGNATURES = {
         _vp, _i64,                # C, ldc
         _vp, _i32,                # bias, epilogue
         _vp, _i64, _f32,          # drop_mask, ldm, drop_scale
-        _f32, _u64, _u64,         # keep_prob, seed, offset
+        _f32, _u64, _u64, _vp,    # keep_prob, seed, offset, rng_base
         _vp, _i64,                # workspace, workspace_bytes
         _vp, _i64,                # counters, counter_bytes
         _i32, _vp,                # lanes_hint, stream
@@ -61,7 +61,7 @@ SIGNATURES = {
         _vp, _i64,                # C, ldc
         _vp, _i32,                # bias, epilogue
         _vp, _i64, _f32,          # drop_mask, ldm, drop_scale
-        _f32, _u64, _u64,         # keep_prob, seed, offset
+        _f32, _u64, _u64, _vp,    # keep_prob, seed, offset, rng_base
         _vp, _i64,                # workspace, workspace_bytes
         _vp, _i64,                # counters, counter_bytes
         _i32, _i32, _vp,          # lanes_hint, part, stream
@@ -72,7 +72,7 @@ SIGNATURES = {
         _vp, _i64,                # C (nullable), ldc
         _vp, _i32,                # bias, epilogue
         _vp, _i64, _f32,          # drop_mask, ldm, drop_scale
-        _f32, _u64, _u64,         # keep_prob, seed, offset
+        _f32, _u64, _u64, _vp,    # keep_prob, seed, offset, rng_base
         _vp, _i64, _i32, _vp, _i64,  # W, ldw, P, C2, ldc2
         _vp, _i64,                # workspace, workspace_bytes
         _vp, _i64,                # counters, counter_bytes

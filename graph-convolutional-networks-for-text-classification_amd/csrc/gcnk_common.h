@@ -37,6 +37,7 @@ struct Epi {
   float keep_prob;       // GCNK_EPI_BIAS_RELU_HASH
   uint32_t seed_lo, seed_hi;
   uint64_t offset;
+  const uint64_t* rng_base;    // device word added to offset (GCNK_EPI_BIAS_RELU_HASH), may be null
   int32_t code;
   unsigned long long* stamps;  // debug timeline (gcnk_debug_set_stamps), normally null
 };
@@ -72,7 +73,8 @@ __device__ __forceinline__ float apply_epi(const Epi& e, float acc, float b, int
   if (e.code == GCNK_EPI_BIAS_RELU) return v;
   if (e.code == GCNK_EPI_BIAS_RELU_DROP) return e.mask[row * e.ldm + col] ? v * e.scale : 0.0f;
   // GCNK_EPI_BIAS_RELU_HASH
-  const float u = hash_uniform(e.seed_lo, e.seed_hi, e.offset + (uint64_t)(row * e.ldm + col));
+  const uint64_t base = e.rng_base ? *e.rng_base : 0;
+  const float u = hash_uniform(e.seed_lo, e.seed_hi, base + e.offset + (uint64_t)(row * e.ldm + col));
   return u < e.keep_prob ? v * e.scale : 0.0f;
 }
 

@@ -380,8 +380,14 @@ __device__ __forceinline__ void finish_row(const typename Vec<VEC>::T& acc, int3
 // grid.x: [0, nhb) heavy blocks, one heavy segment per wavefront (per
 // workgroup for 64-lane groups); then light blocks, one light row per lane
 // group.  grid.y: column tiles of LPR*VEC.
+#ifndef GCNK_ROW_WPE
+#define GCNK_ROW_WPE 8
+#endif
+// Whole-wave groups at 8 waves per SIMD (<= 64 VGPRs, no spills there; the
+// narrower groups would spill): R8's 1832 workgroups then fit one residency
+// round (at 66 VGPRs, 7 per SIMD, 40 of them waited for a second round)
 template <int BLOCK, int LPR, int VEC, int U, int NP, bool O32>
-__global__ void __launch_bounds__(BLOCK)
+__global__ void __launch_bounds__(BLOCK) __attribute__((amdgpu_waves_per_eu(NP == 0 && LPR == 64 ? GCNK_ROW_WPE : 1)))
 spmm_row_kernel(RowPlan rp, int32_t nhb, const float* __restrict__ B, int64_t ldb, int32_t F,
                 float* __restrict__ C, int64_t ldc, Epi epi, float* __restrict__ part, int64_t part_ld,
                 ProjArgs pa) {
@@ -1476,8 +1482,8 @@ extern "C" int64_t gcnk_spmm_counter_bytes(const int32_t* hdr) {
 
 static int spmm_impl(const void* plan, const int32_t* hdr, const float* B, int64_t ldb, int32_t F, float* C,
                      int64_t ldc, const float* bias, int32_t epilogue, const uint8_t* drop_mask, int64_t ldm,
-                     float drop_scale, float keep_prob, uint64_t seed, uint64_t offset, float* workspace,
-                     int64_t workspace_bytes, int32_t* counters, int64_t counter_bytes, int32_t lanes_hint,
+                     float drop_scale, float keep_prob, uint64_t seed, uint64_t offset, const uint64_t* rng_base,
+                     float* workspace, int64_t workspace_bytes, int32_t* counters, int64_t counter_bytes, int32_t lanes_hint,
                      const ProjArgs& pa, void* stream, int32_t part = 0) {
   if (!plan || !plan_magic(hdr) || F < 0 || part < 0 || part > 2) {
     set_error("gcnk_spmm_csr_f32: bad argument (plan/header missing or not a gcnk plan, F=%d)", F);
@@ -1535,6 +1541,7 @@ static int spmm_impl(const void* plan, const int32_t* hdr, const float* B, int64
   e.seed_lo = (uint32_t)seed;
   e.seed_hi = (uint32_t)(seed >> 32);
   e.offset = offset;
+  e.rng_base = rng_base;
   e.code = epilogue;
   e.stamps = g_stamps;
   const bool vec4 = (F % 4 == 0) && (ldb % 4 == 0) && (ldc % 4 == 0) && aligned16(B) && (!C || aligned16(C)) &&
@@ -1608,28 +1615,29 @@ static int spmm_impl(const void* plan, const int32_t* hdr, const float* B, int64
 extern "C" int gcnk_spmm_csr_f32(const void* plan, const int32_t* hdr, const float* B, int64_t ldb, int32_t F,
                                  float* C, int64_t ldc, const float* bias, int32_t epilogue, const uint8_t* drop_mask,
                                  int64_t ldm, float drop_scale, float keep_prob, uint64_t seed, uint64_t offset,
-                                 float* workspace, int64_t workspace_bytes, int32_t* counters, int64_t counter_bytes,
+                                 const uint64_t* rng_base, float* workspace, int64_t workspace_bytes, int32_t* counters, int64_t counter_bytes,
                                  int32_t lanes_hint, void* stream) {
   const ProjArgs none{nullptr, 0, 0, nullptr, 0, 1};
   return spmm_impl(plan, hdr, B, ldb, F, C, ldc, bias, epilogue, drop_mask, ldm, drop_scale, keep_prob, seed, offset,
-                   workspace, workspace_bytes, counters, counter_bytes, lanes_hint, none, stream);
+                   rng_base, workspace, workspace_bytes, counters, counter_bytes, lanes_hint, none, stream);
 }
 
 extern "C" int gcnk_spmm_csr_f32_part(const void* plan, const int32_t* hdr, const float* B, int64_t ldb,
                                       int32_t F, float* C, int64_t ldc, const float* bias, int32_t epilogue,
                                       const uint8_t* drop_mask, int64_t ldm, float drop_scale, float keep_prob,
-                                      uint64_t seed, uint64_t offset, float* workspace, int64_t workspace_bytes,
+                                      uint64_t seed, uint64_t offset, const uint64_t* rng_base, float* workspace,
+                                      int64_t workspace_bytes,
                                       int32_t* counters, int64_t counter_bytes, int32_t lanes_hint, int32_t part,
                                       void* stream) {
   const ProjArgs none{nullptr, 0, 0, nullptr, 0, 1};
   return spmm_impl(plan, hdr, B, ldb, F, C, ldc, bias, epilogue, drop_mask, ldm, drop_scale, keep_prob, seed, offset,
-                   workspace, workspace_bytes, counters, counter_bytes, lanes_hint, none, stream, part);
+                   rng_base, workspace, workspace_bytes, counters, counter_bytes, lanes_hint, none, stream, part);
 }
 
 extern "C" int gcnk_spmm_proj_f32(const void* plan, const int32_t* hdr, const float* B, int64_t ldb, int32_t F,
                                   float* C, int64_t ldc, const float* bias, int32_t epilogue,
                                   const uint8_t* drop_mask, int64_t ldm, float drop_scale, float keep_prob,
-                                  uint64_t seed, uint64_t offset, const float* W, int64_t ldw, int32_t P, float* C2,
+                                  uint64_t seed, uint64_t offset, const uint64_t* rng_base, const float* W, int64_t ldw, int32_t P, float* C2,
                                   int64_t ldc2, float* workspace, int64_t workspace_bytes, int32_t* counters,
                                   int64_t counter_bytes, int32_t lanes_hint, void* stream) {
   if (!W) {
@@ -1638,5 +1646,5 @@ extern "C" int gcnk_spmm_proj_f32(const void* plan, const int32_t* hdr, const fl
   }
   const ProjArgs pa{W, ldw, P, C2, ldc2, C != nullptr};
   return spmm_impl(plan, hdr, B, ldb, F, C, ldc, bias, epilogue, drop_mask, ldm, drop_scale, keep_prob, seed, offset,
-                   workspace, workspace_bytes, counters, counter_bytes, lanes_hint, pa, stream);
+                   rng_base, workspace, workspace_bytes, counters, counter_bytes, lanes_hint, pa, stream);
 }

@@ -19,7 +19,9 @@ Differences by design:
     CPU tensor from torch's default generator — so a seeded run consumes the
     same random stream as the reference and trains on identical masks;
     ``dropout_rng="device"`` generates them inside the kernel (counter-based
-    hash), with no host work and no mask traffic.
+    hash), with no host work and no mask traffic.  The hash offset lives on
+    the device (``_rng_base``, advanced by the forward itself), so a training
+    step captured in a hipGraph draws a fresh mask on every replay.
 """
 import math
 
@@ -75,7 +77,8 @@ class GCN(Module):
         if dropout_rng not in ("cpu", "device"):
             raise ValueError("dropout_rng must be 'cpu' or 'device'")
         self.dropout_rng = dropout_rng
-        self._hash_calls = 0
+        # hash-dropout stream position, read and advanced on the device (not in state_dict)
+        self.register_buffer("_rng_base", torch.zeros(1, dtype=torch.int64), persistent=False)
 
     def _dropout_args(self, nrows, device):
         """Epilogue code and mask/scale for layer.py:185 (ATen dropout semantics)."""
@@ -93,9 +96,7 @@ class GCN(Module):
             mask = noise.to(torch.uint8).to(device, non_blocking=False)
             return _lib.EPI_BIAS_RELU_DROP, mask, scale, 1.0 - p, 0, 0
         seed = int(torch.initial_seed()) & (2**64 - 1)
-        offset = self._hash_calls * nrows * nhid
-        self._hash_calls += 1
-        return _lib.EPI_BIAS_RELU_HASH, None, scale, 1.0 - p, seed, offset
+        return _lib.EPI_BIAS_RELU_HASH, None, scale, 1.0 - p, seed, 0
 
     def forward(self, x, adj):
         a = as_csr(adj)
@@ -103,5 +104,11 @@ class GCN(Module):
         epi, mask, scale, keep, seed, offset = self._dropout_args(a.shape[0], a.device)
         # H1 is needed only by a backward pass; inference never writes it to HBM
         keep_h1 = torch.is_grad_enabled() and any(p.requires_grad for p in self.parameters())
-        return GCNFn.apply(self.gc1.weight, self.gc1.bias, self.gc2.weight, self.gc2.bias, xop, a,
-                           epi, mask, scale, keep, seed, offset, keep_h1)
+        hashed = epi == _lib.EPI_BIAS_RELU_HASH
+        if hashed and self._rng_base.device != a.device:
+            raise RuntimeError(f"GCN buffers are on {self._rng_base.device}, operands on {a.device}: call .to()")
+        out = GCNFn.apply(self.gc1.weight, self.gc1.bias, self.gc2.weight, self.gc2.bias, xop, a,
+                          epi, mask, scale, keep, seed, offset, keep_h1, self._rng_base if hashed else None)
+        if hashed:   # the next call (or graph replay) draws the next rows*nhid hash positions
+            self._rng_base.add_(a.shape[0] * self.gc1.out_features)
+        return out

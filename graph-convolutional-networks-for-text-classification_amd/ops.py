@@ -38,15 +38,18 @@ def default_ipc(a, F, lanes=0):
 
 
 def spmm(a, B, bias=None, epilogue=_lib.EPI_NONE, mask=None, scale=1.0, keep_prob=1.0, seed=0, offset=0,
-         out=None, ipc=None, lanes=0, dense=None):
+         out=None, ipc=None, lanes=0, dense=None, rng_base=None):
     """C = epi(A @ B) with A a CSR (or torch sparse) and B dense [K, F].
 
     Replaces ``th.spmm(adj, support)`` (reference layer.py:106) and
     ``th.spmm(X, W)`` with sparse X (layer.py:102); the epilogue fuses
     ``+ bias`` (layer.py:110), ``th.relu`` (layer.py:182) and the dropout
-    multiply (layer.py:185)."""
+    multiply (layer.py:185).  ``rng_base``: optional one-element int64 device
+    tensor added to ``offset`` by the kernel (hash dropout in captured graphs,
+    include/gcnk.h GCNK_EPI_BIAS_RELU_HASH)."""
     a = as_csr(a)
     B = _dense_f32(B, "dense operand")
+    _check_rng_base(rng_base, B.device)
     M, K = a.shape
     if B.shape[0] != K:
         raise RuntimeError(f"spmm shape mismatch: sparse {tuple(a.shape)} @ dense {tuple(B.shape)}")
@@ -72,7 +75,7 @@ def spmm(a, B, bias=None, epilogue=_lib.EPI_NONE, mask=None, scale=1.0, keep_pro
             _ptr(out), out.stride(0),
             _ptr(bias), epilogue,
             _ptr(mask), mask.stride(0) if mask is not None else 0, float(scale),
-            float(keep_prob), int(seed) & (2**64 - 1), int(offset) & (2**64 - 1),
+            float(keep_prob), int(seed) & (2**64 - 1), int(offset) & (2**64 - 1), _ptr(rng_base),
             _ptr(ws), wsb, _ptr(cnt), 4 * cnt.numel() if cnt is not None else 0, int(lanes))
     hdr = plan.hdr
     nsingle, ntile, nunits = int(hdr[15]), int(hdr[8]), int(hdr[5])
@@ -94,6 +97,11 @@ def spmm(a, B, bias=None, epilogue=_lib.EPI_NONE, mask=None, scale=1.0, keep_pro
             rc = lib.gcnk_spmm_csr_f32(*args, _stream(B.device))
     _lib.check(rc, "gcnk_spmm_csr_f32")
     return out
+
+
+def _check_rng_base(t, device):
+    if t is not None and (t.dtype != torch.int64 or t.numel() < 1 or t.device != device):
+        raise RuntimeError("rng_base must be an int64 tensor of >= 1 element on the operand's device")
 
 
 # Overlap the two independent parts of a hybrid plan (gcnk_spmm_csr_f32_part)
@@ -121,7 +129,7 @@ FUSE_PROJECTION = False
 
 
 def spmm_proj(a, B, W, bias=None, epilogue=_lib.EPI_NONE, mask=None, scale=1.0, keep_prob=1.0, seed=0, offset=0,
-              store_main=True, ipc=None, lanes=0):
+              store_main=True, ipc=None, lanes=0, rng_base=None):
     """(H, C2) with H = epi(A @ B) and C2 = H @ W, the projection fused into
     the SpMM epilogue (gcnk_spmm_proj_f32): gc1's aggregation + bias + ReLU +
     dropout (reference layer.py:106,110,182,185) followed by gc2's support
@@ -132,6 +140,7 @@ def spmm_proj(a, B, W, bias=None, epilogue=_lib.EPI_NONE, mask=None, scale=1.0, 
     a = as_csr(a)
     B = _dense_f32(B, "dense operand")
     W = _dense_f32(W, "projection")
+    _check_rng_base(rng_base, B.device)
     M, K = a.shape
     F = B.shape[1]
     if B.shape[0] != K or W.shape[0] != F:
@@ -160,12 +169,12 @@ def spmm_proj(a, B, W, bias=None, epilogue=_lib.EPI_NONE, mask=None, scale=1.0, 
             _ptr(H), F,
             _ptr(bias), epilogue,
             _ptr(mask), mask.stride(0) if mask is not None else 0, float(scale),
-            float(keep_prob), int(seed) & (2**64 - 1), int(offset) & (2**64 - 1),
+            float(keep_prob), int(seed) & (2**64 - 1), int(offset) & (2**64 - 1), _ptr(rng_base),
             _ptr(W), W.stride(0), P, _ptr(C2), C2.stride(0),
             _ptr(ws), wsb, _ptr(cnt), 4 * cnt.numel() if cnt is not None else 0, int(lanes), _stream(B.device))
     if rc == _lib.EUNSUP:
         H = spmm(a, B, bias=bias, epilogue=epilogue, mask=mask, scale=scale, keep_prob=keep_prob, seed=seed,
-                 offset=offset, ipc=ipc, lanes=lanes)
+                 offset=offset, ipc=ipc, lanes=lanes, rng_base=rng_base)
         return (H if store_main else None), gemm(H, W)
     _lib.check(rc, "gcnk_spmm_proj_f32")
     return H, C2
@@ -305,14 +314,14 @@ class GCNFn(torch.autograd.Function):
     """
 
     @staticmethod
-    def forward(ctx, W1, b1, W2, b2, xop, adj, epi, mask, scale, keep, seed, offset, keep_h1=True):
+    def forward(ctx, W1, b1, W2, b2, xop, adj, epi, mask, scale, keep, seed, offset, keep_h1=True, rng_base=None):
         S1 = xop.times(W1)
         if FUSE_PROJECTION:
             H1, S2 = spmm_proj(adj, S1, W2, bias=b1, epilogue=epi, mask=mask, scale=scale, keep_prob=keep,
-                               seed=seed, offset=offset, store_main=keep_h1)
+                               seed=seed, offset=offset, store_main=keep_h1, rng_base=rng_base)
         else:
             H1 = spmm(adj, S1, bias=b1, epilogue=epi, mask=mask, scale=scale, keep_prob=keep, seed=seed,
-                      offset=offset)
+                      offset=offset, rng_base=rng_base)
             S2 = gemm(H1, W2)
         out = spmm(adj, S2, bias=b2, epilogue=_lib.EPI_BIAS if b2 is not None else _lib.EPI_NONE)
         ctx.xop, ctx.adj, ctx.scale = xop, adj, float(scale)
@@ -339,4 +348,4 @@ class GCNFn(torch.autograd.Function):
             if need[0]:
                 gS1 = spmm(adjT, gZ1)
                 gW1 = ctx.xop.t_times(gS1)
-        return gW1, gb1, gW2, gb2, None, None, None, None, None, None, None, None, None
+        return gW1, gb1, gW2, gb2, None, None, None, None, None, None, None, None, None, None

@@ -65,6 +65,11 @@ extern "C" {
 #define GCNK_EPI_BIAS_RELU 2       /* relu(. + bias)                   layer.py:110,182 */
 #define GCNK_EPI_BIAS_RELU_DROP 3  /* relu(.+bias) * (mask?scale:0)    layer.py:110,182,185 */
 #define GCNK_EPI_BIAS_RELU_HASH 4  /* as 3 with an in-kernel counter-based RNG mask */
+/* HASH: element (r, c) is kept iff hash(seed, base + offset + r*ldm + c) <
+ * keep_prob, base = *rng_base (a device uint64 read by the kernel; 0 when
+ * rng_base is NULL).  A caller replaying a captured graph advances *rng_base
+ * on the device after each call (the GCN module adds rows*ldm), so every
+ * replay draws a fresh mask with no host involvement. */
 
 /* GEMM epilogues */
 #define GCNK_GEMM_EPI_NONE 0
@@ -163,7 +168,7 @@ int gcnk_spmm_csr_f32(const void* plan, const int32_t* plan_header,
                       float* C, int64_t ldc,
                       const float* bias, int32_t epilogue,
                       const uint8_t* drop_mask, int64_t ldm, float drop_scale,
-                      float keep_prob, uint64_t seed, uint64_t offset,
+                      float keep_prob, uint64_t seed, uint64_t offset, const uint64_t* rng_base,
                       float* workspace, int64_t workspace_bytes,
                       int32_t* counters, int64_t counter_bytes,
                       int32_t lanes_hint, void* stream);
@@ -181,7 +186,7 @@ int gcnk_spmm_csr_f32_part(const void* plan, const int32_t* plan_header,
                            float* C, int64_t ldc,
                            const float* bias, int32_t epilogue,
                            const uint8_t* drop_mask, int64_t ldm, float drop_scale,
-                           float keep_prob, uint64_t seed, uint64_t offset,
+                           float keep_prob, uint64_t seed, uint64_t offset, const uint64_t* rng_base,
                            float* workspace, int64_t workspace_bytes,
                            int32_t* counters, int64_t counter_bytes,
                            int32_t lanes_hint, int32_t part, void* stream);
@@ -199,7 +204,7 @@ int gcnk_spmm_proj_f32(const void* plan, const int32_t* plan_header,
                        float* C, int64_t ldc,
                        const float* bias, int32_t epilogue,
                        const uint8_t* drop_mask, int64_t ldm, float drop_scale,
-                       float keep_prob, uint64_t seed, uint64_t offset,
+                       float keep_prob, uint64_t seed, uint64_t offset, const uint64_t* rng_base,
                        const float* W, int64_t ldw, int32_t P, float* C2, int64_t ldc2,
                        float* workspace, int64_t workspace_bytes,
                        int32_t* counters, int64_t counter_bytes,

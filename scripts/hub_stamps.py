@@ -28,7 +28,7 @@ def main():
     r8 = datasets.load_r8_fixture(os.path.join(ROOT, "tests", "golden", "r8_graph.npz"))
     A = sp.as_csr(r8["adj"].to(dev))
     for br in [int(x) for x in (sys.argv[1:] or ["0"])]:
-        sp.HUB_BLOCK_ROWS = br
+        sp.HUB_MIN, sp.HUB_BLOCK_ROWS = 0, br
         for F in (200, 8):
             B = torch.randn(A.shape[1], F, device=dev)
             bias = torch.randn(F, device=dev)

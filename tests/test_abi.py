@@ -41,7 +41,7 @@ def test_abi_version_and_error_text():
     lib = _lib.load()
     assert lib.gcnk_abi_version() == _lib.ABI_VERSION == 2
     rc = lib.gcnk_spmm_csr_f32(None, None, None, 0, 8, None, 0, None, 0, None, 0,
-                               1.0, 1.0, 0, 0, None, 0, None, 0, 0, None)
+                               1.0, 1.0, 0, 0, None, None, 0, None, 0, 0, None)
     assert rc == _lib.EARG
     assert b"bad argument" in lib.gcnk_last_error()
     with pytest.raises(_lib.GcnkError):
@@ -65,22 +65,22 @@ def test_argument_validation_without_gpu():
     # a header that is not a plan's is refused
     bad = (ctypes.c_int32 * 16)()
     rc = lib.gcnk_spmm_csr_f32(ctypes.c_void_p(16), ctypes.cast(bad, ctypes.c_void_p), ctypes.c_void_p(16), 8, 8,
-                               ctypes.c_void_p(16), 8, None, 0, None, 0, 1.0, 1.0, 0, 0, None, 0, None, 0, 0, None)
+                               ctypes.c_void_p(16), 8, None, 0, None, 0, 1.0, 1.0, 0, 0, None, None, 0, None, 0, 0, None)
     assert rc == _lib.EARG and b"not a gcnk plan" in lib.gcnk_last_error()
     # plan/groups mismatch is refused before any launch (F=200 uses 1 lane group per wave)
     h, _keep = _hdr(groups=7)
     rc = lib.gcnk_spmm_csr_f32(ctypes.c_void_p(16), h, ctypes.c_void_p(16), 200, 200,
-                               ctypes.c_void_p(16), 200, None, 0, None, 0, 1.0, 1.0, 0, 0, None, 0, None, 0, 0, None)
+                               ctypes.c_void_p(16), 200, None, 0, None, 0, 1.0, 1.0, 0, 0, None, None, 0, None, 0, 0, None)
     assert rc == _lib.EARG and b"groups" in lib.gcnk_last_error()
     # workspace too small for the plan's partial slots
     h, _keep = _hdr(groups=1, nslots=3)
     rc = lib.gcnk_spmm_csr_f32(ctypes.c_void_p(16), h, ctypes.c_void_p(16), 200, 200,
-                               ctypes.c_void_p(16), 200, None, 0, None, 0, 1.0, 1.0, 0, 0, None, 0, None, 0, 0, None)
+                               ctypes.c_void_p(16), 200, None, 0, None, 0, 1.0, 1.0, 0, 0, None, None, 0, None, 0, 0, None)
     assert rc == _lib.EARG and b"workspace" in lib.gcnk_last_error()
     # empty problems are no-ops that succeed without touching the device
     h, _keep = _hdr(M=0)
     assert lib.gcnk_spmm_csr_f32(ctypes.c_void_p(16), h, None, 8, 8, None, 8, None,
-                                 0, None, 0, 1.0, 1.0, 0, 0, None, 0, None, 0, 0, None) == _lib.OK
+                                 0, None, 0, 1.0, 1.0, 0, 0, None, None, 0, None, 0, 0, None) == _lib.OK
     assert lib.gcnk_gemm_f32(0, 0, 0, 5, 5, None, 5, None, 5, None, 5, None, 0, None, 0, 1.0, 1, None, 0,
                              None) == _lib.OK
 

@@ -241,12 +241,15 @@ def test_spmm_hub_plan_r8(r8, F, monkeypatch):
     rng = np.random.default_rng(F)
     B = rng.standard_normal((r8["nodes"], F)).astype(np.float32)
     b = rng.standard_normal(F).astype(np.float32)
-    got = spmm(a, torch.from_numpy(B).to(DEV), bias=torch.from_numpy(b).to(DEV), epilogue=_lib.EPI_BIAS_RELU)
+    # the hub plan serves one lane group per wavefront (lanes=64 for narrow F)
+    got = spmm(a, torch.from_numpy(B).to(DEV), bias=torch.from_numpy(b).to(DEV), epilogue=_lib.EPI_BIAS_RELU,
+               lanes=64)
     plan = list(a._plans.values())[-1]
     assert plan.is_hub and plan.header[6] == r8["ntopic"]
     rp, ci, v = (t.cpu().numpy() for t in (a.rowptr, a.colind, a.val))
     _close(got, csr_ref.spmm_epilogue(csr_ref.spmm_csr(rp, ci, v, B), b, relu=True), atol=2e-5)
-    again = spmm(a, torch.from_numpy(B).to(DEV), bias=torch.from_numpy(b).to(DEV), epilogue=_lib.EPI_BIAS_RELU)
+    again = spmm(a, torch.from_numpy(B).to(DEV), bias=torch.from_numpy(b).to(DEV), epilogue=_lib.EPI_BIAS_RELU,
+                 lanes=64)
     assert torch.equal(got, again)
 
 
@@ -772,3 +775,32 @@ def test_spmm_two_part_launch_matches_single(monkeypatch, r8):
         torch.cuda.synchronize()
         monkeypatch.setattr(ops, "OVERLAP_TILE_PARTS", False)
         assert torch.equal(one, two)
+
+
+def test_device_dropout_draws_a_fresh_mask_on_every_graph_replay(r8):
+    """dropout_rng="device": the hash offset is read from and advanced on the
+    device (GCN._rng_base), so a train-mode forward captured in a hipGraph
+    draws a new mask per replay, and each replay equals the eager forward at
+    the same stream position bit for bit."""
+    torch.manual_seed(3)
+    m = GCN(nfeat=r8["nfeat"], nhid=200, nclass=r8["nclass"], dropout=0.5, dropout_rng="device").to(DEV).train()
+    x, adj = r8["features"].to(DEV), r8["adj"].to(DEV)
+    step = r8["nodes"] * 200
+    with torch.no_grad():
+        m(x, adj)                                   # plans built outside the capture
+        torch.cuda.synchronize()
+        base0 = int(m._rng_base.item())
+        assert base0 == step
+        g = torch.cuda.CUDAGraph()
+        with torch.cuda.graph(g):
+            y = m(x, adj)
+        outs = []
+        for _ in range(3):
+            g.replay()
+            outs.append(y.clone())
+        torch.cuda.synchronize()
+        assert int(m._rng_base.item()) == base0 + 3 * step, "one advance per replay (none at capture)"
+        assert not torch.equal(outs[0], outs[1]) and not torch.equal(outs[1], outs[2])
+        m._rng_base.fill_(base0 + step)
+        eager = m(x, adj)
+        assert torch.equal(eager, outs[1])

@@ -48,7 +48,10 @@ namespace {
 constexpr int32_t kMagic = 0x474e4b35;  // "GNK5"
 constexpr int kRB = 64;                 // tile rows per dense block (4 waves x 16)
 constexpr int kKC = 64;                 // condensed columns per tile chunk (16 MFMA k-steps)
-constexpr int kMaxNT = 8;               // 16-column MFMA n-tiles per tile workgroup (B tile 48 KB LDS: 2+ per CU)
+#ifndef GCNK_TILE_MAXNT
+#define GCNK_TILE_MAXNT 8
+#endif
+constexpr int kMaxNT = GCNK_TILE_MAXNT;  // 16-column MFMA n-tiles per tile workgroup (8: B tile 48 KB LDS, 2+ per CU)
 constexpr int kMaxColTiles = 64;        // row-kernel column tiles per launch (arrival counters per heavy row)
 constexpr int kMaxSeg = 64;             // segments per heavy row (bounds the last arriver's combine)
 // Schedule knobs of the whole-wavefront (F > 128) row kernel, overridable at
@@ -589,7 +592,7 @@ spmm_row_kernel(RowPlan rp, int32_t nhb, const float* __restrict__ B, int64_t ld
 //   C/D reg j: row (l>>4)*4 + j, col l&15   (gfx950 16x16x4 f32 maps).
 typedef float f32x4 __attribute__((ext_vector_type(4)));
 
-template <bool VEC4, int NT>
+template <bool VEC4, int NT, bool DIAG>
 __global__ void __launch_bounds__(256)
 spmm_tile_kernel(const int4* __restrict__ tdesc, const int32_t* __restrict__ tcols, const float* __restrict__ tfrag,
                  const int32_t* __restrict__ trows, const float* __restrict__ dval, int32_t F,
@@ -607,8 +610,10 @@ spmm_tile_kernel(const int4* __restrict__ tdesc, const int32_t* __restrict__ tco
   const int wave = tid >> 6;
   const int64_t item = (int64_t)blockIdx.x + item0;
   stamp(epi, 0);
-  const int4 d0 = tdesc[item];  // block, nrows | contiguous run length << 8, slab (-1: single chunk), run start
-  const int32_t run = d0.y >> 8;
+  // block, nrows | contiguous run length << 8 | width << 16, slab (-1: single chunk), run start
+  const int4 d0 = tdesc[item];
+  const int32_t run = (d0.y >> 8) & 0xff;
+  const int32_t ksteps = __builtin_amdgcn_readfirstlane(((d0.y >> 16) + 3) >> 2);  // k-steps past the width are zero
   const int4 d = make_int4(d0.x, d0.y & 0xff, d0.z, d0.w);
   const int64_t col0 = (int64_t)blockIdx.y * (NT * 16);  // this workgroup's column slice
 
@@ -692,6 +697,7 @@ spmm_tile_kernel(const int4* __restrict__ tdesc, const int32_t* __restrict__ tco
   const int kr = lane >> 4, nc = lane & 15;
 #pragma unroll
   for (int s = 0; s < 16; ++s) {
+    if (s >= ksteps) break;  // R8 X's document blocks: 50 columns, 13 of 16 k-steps
     const float4* brow = reinterpret_cast<const float4*>(s_B + (4 * s + kr) * stride + nc * LR);
     float4 bq[NT4 / 4];
 #pragma unroll
@@ -744,7 +750,7 @@ spmm_tile_kernel(const int4* __restrict__ tdesc, const int32_t* __restrict__ tco
       if (VEC4 && epi.code <= GCNK_EPI_BIAS_RELU) {
         // common case, vectorised (no dropout): + extracted diagonal * B row piece,
         // + bias, relu
-        if (dv != 0.f) {
+        if (DIAG && dv != 0.f) {  // (a load here would wait for every store before it)
           const float4 b4 = *reinterpret_cast<const float4*>(B + row * ldb + col);
           v.x = fmaf(dv, b4.x, v.x); v.y = fmaf(dv, b4.y, v.y); v.z = fmaf(dv, b4.z, v.z); v.w = fmaf(dv, b4.w, v.w);
         }
@@ -761,7 +767,7 @@ spmm_tile_kernel(const int4* __restrict__ tdesc, const int32_t* __restrict__ tco
 #pragma unroll
         for (int i = 0; i < 4; ++i) {
           if (col + i >= F) break;
-          if (dv != 0.f) o[i] = fmaf(dv, B[row * ldb + col + i], o[i]);
+          if (DIAG && dv != 0.f) o[i] = fmaf(dv, B[row * ldb + col + i], o[i]);
           o[i] = apply_epi(epi, o[i], s_bias[col - col0 + i], row, col + i);
         }
         if (!VEC4) {
@@ -900,7 +906,10 @@ int launch_rows(const RowLaunch& a) {
     e.mask = e.mask ? e.mask + c0 : nullptr;
     e.offset += (uint64_t)c0;  // hash index shifts with the column
     // 32-bit gather offsets when every byte the launch reads lies within 4 GB of its B base
-    const bool o32 = (int64_t)a.K * a.ldb * 4 + (int64_t)Fw * 4 < ((int64_t)1 << 32);
+#ifndef GCNK_ROW_O32
+#define GCNK_ROW_O32 1
+#endif
+    const bool o32 = GCNK_ROW_O32 && (int64_t)a.K * a.ldb * 4 + (int64_t)Fw * 4 < ((int64_t)1 << 32);
     const dim3 grid((unsigned)(nhb + nlb), (unsigned)((Fw + tileF - 1) / tileF));
     if (o32)
       hipLaunchKernelGGL((spmm_row_kernel<BLOCK, LPR, VEC, U, NP, true>), grid, dim3(BLOCK), 0, a.s, a.rp, (int32_t)nhb,
@@ -964,8 +973,12 @@ template <bool V4, int NT>
 int launch_tile_nt(unsigned nitems, const TileArgs& t, hipStream_t s) {
   if (nitems == 0) return GCNK_OK;
   const unsigned slices = (unsigned)((t.F + NT * 16 - 1) / (NT * 16));
-  hipLaunchKernelGGL((spmm_tile_kernel<V4, NT>), dim3(nitems, slices), dim3(256), 0, s, t.tdesc, t.tcols, t.tfrag, t.trows, t.dval, t.F, t.B,
-                     t.ldb, t.C, t.ldc, t.epi, t.slabs, t.slab_ld, t.item0);
+  if (t.dval)
+    hipLaunchKernelGGL((spmm_tile_kernel<V4, NT, true>), dim3(nitems, slices), dim3(256), 0, s, t.tdesc, t.tcols,
+                       t.tfrag, t.trows, t.dval, t.F, t.B, t.ldb, t.C, t.ldc, t.epi, t.slabs, t.slab_ld, t.item0);
+  else
+    hipLaunchKernelGGL((spmm_tile_kernel<V4, NT, false>), dim3(nitems, slices), dim3(256), 0, s, t.tdesc, t.tcols,
+                       t.tfrag, t.trows, t.dval, t.F, t.B, t.ldb, t.C, t.ldc, t.epi, t.slabs, t.slab_ld, t.item0);
   return launch_check("spmm_tile_kernel");
 }
 
@@ -976,6 +989,10 @@ int launch_tile_v(int nt_need, unsigned nitems, const TileArgs& t, hipStream_t s
   if (nt_need <= 4) return launch_tile_nt<V4, 4>(nitems, t, s);
   if (nt_need <= 6) return launch_tile_nt<V4, 6>(nitems, t, s);
   if (nt_need <= 7) return launch_tile_nt<V4, 7>(nitems, t, s);
+  if (nt_need <= 8) return launch_tile_nt<V4, 8>(nitems, t, s);
+  if constexpr (kMaxNT > 8) {
+    if (nt_need <= 13) return launch_tile_nt<V4, 13>(nitems, t, s);
+  }
   if (nt_need <= kMaxNT) return launch_tile_nt<V4, kMaxNT>(nitems, t, s);
   set_error("spmm_tile_kernel: %d n-tiles exceed %d", nt_need, kMaxNT);
   return GCNK_EUNSUP;
@@ -1028,7 +1045,9 @@ int host_plan(const int32_t* rp, const int32_t* ci, const float* vv, int32_t M, 
   int32_t ntile = 0, nred = 0, nslabs = 0, ntblk = 0, nsingle = 0;
   bool any_diag = false;
   hp.dval.clear();
-  auto is_diag = [&](int32_t r, int64_t k) { return r < K && ci[(size_t)k] == r; };
+  // the diagonal is kept aside for square operands (A-hat's self loops); a
+  // rectangular operand (X) has no diagonal to speak of
+  auto is_diag = [&](int32_t r, int64_t k) { return M == K && ci[(size_t)k] == r; };
   if (dense_threshold <= 1.0f && M > 0) {
     std::vector<std::vector<int32_t>> cls(33);
     for (int32_t r = 0; r < M; ++r) {
@@ -1074,8 +1093,9 @@ int host_plan(const int32_t* rp, const int32_t* ci, const float* vv, int32_t M, 
           const int32_t kc = (int32_t)std::min<int64_t>(kKC, ncols - c0);
           bool contig = true;
           for (int32_t k = 1; k < kc && contig; ++k) contig = cols[(size_t)(c0 + k)] == cols[(size_t)c0] + k;
-          hp.tdesc.insert(hp.tdesc.end(), {blk, (int32_t)nrows | (contig ? kc << 8 : 0), nch > 1 ? first_slab + ch : -1,
-                                           contig ? cols[(size_t)c0] : 0});
+          // y: rows | contiguous run << 8 | condensed width << 16 (the kernel's k-steps)
+          hp.tdesc.insert(hp.tdesc.end(), {blk, (int32_t)nrows | (contig ? kc << 8 : 0) | kc << 16,
+                                           nch > 1 ? first_slab + ch : -1, contig ? cols[(size_t)c0] : 0});
           for (int k = 0; k < kKC; ++k) {
             const int64_t cc = (int64_t)ch * kKC + k;
             hp.tcols.push_back(cc < ncols ? cols[(size_t)cc] : -1);

@@ -53,12 +53,15 @@ class Plan:
     region per call (gcnk_spmm_counter_bytes); one is kept per stream, so
     calls on different streams (or the autograd thread's) never share one."""
 
-    __slots__ = ("buf", "hdr", "_counters", "_lock")
+    __slots__ = ("buf", "hdr", "_counters", "_spares", "_captured", "_lock")
     HUB_MAGIC = 0x474e4831
+    SPARE_REGIONS = 16   # pre-zeroed regions handed to hipGraph captures
 
     def __init__(self, buf, hdr):
         self.buf, self.hdr = buf, hdr
         self._counters = {}
+        self._spares = None
+        self._captured = []
         self._lock = threading.Lock()
 
     @property
@@ -75,17 +78,35 @@ class Plan:
     def counter_bytes(self):
         return int(_lib.load().gcnk_spmm_counter_bytes(ctypes.cast(self.hdr, ctypes.c_void_p)))
 
+    def prime(self, device):
+        """Zero SPARE_REGIONS counter regions now (eagerly, outside any capture),
+        so that a later hipGraph capture takes one instead of capturing a memset
+        that every replay would run."""
+        n = self.counter_bytes()
+        if n <= 0 or self._spares is not None:
+            return
+        words = (n + 3) // 4
+        block = torch.zeros(self.SPARE_REGIONS * words, dtype=torch.int32, device=device)
+        self._spares = list(block.split(words))
+
     def counters(self, device):
         """Zeroed int32 counter region for a call on torch's current stream (None
         when the plan needs none).  The kernels leave it zeroed, so it is reused
-        by later calls on the same stream; inside a hipGraph capture a fresh
-        region is zeroed by a captured memset instead (the graph owns it)."""
+        by later calls on the same stream.  Inside a hipGraph capture the call
+        gets a region of its own (the graph replays may run beside eager calls):
+        one of the spares zeroed by prime(), or, once those are used up, a fresh
+        region zeroed by a captured memset."""
         n = self.counter_bytes()
         if n <= 0:
             return None
         words = (n + 3) // 4
         if torch.cuda.is_current_stream_capturing():
-            return torch.zeros(words, dtype=torch.int32, device=device)
+            with self._lock:
+                c = self._spares.pop() if self._spares else None
+            if c is None:
+                c = torch.zeros(words, dtype=torch.int32, device=device)
+            self._captured.append(c)   # owned by the graph for the plan's lifetime
+            return c
         key = torch.cuda.current_stream(device).cuda_stream
         c = self._counters.get(key)
         if c is None:
@@ -143,7 +164,8 @@ class CSR:
                 hdr = (ctypes.c_int32 * 16)()
                 _lib.check(lib.gcnk_spmm_plan_query(buf.data_ptr(), ctypes.cast(hdr, ctypes.c_void_p), s),
                            "gcnk_spmm_plan_query")
-            p = Plan(buf, hdr)
+                p = Plan(buf, hdr)
+                p.prime(self.device)
             self._plans[key] = p
             return p
 

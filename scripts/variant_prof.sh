@@ -10,9 +10,9 @@ mkdir -p gpurun_out/vprof
 for V in "$@"; do
   if [ "$V" = base ]; then unset GCNK_LIB; else export GCNK_LIB=$PWD/_variants/libgcnk_$V.so; fi
   timeout -k 10 120 rocprofv3 --kernel-trace --stats --output-format csv -d gpurun_out/vprof/$V -o run -- \
-    python3 scripts/hub_probe.py $ARGS > gpurun_out/vprof/$V.log 2>&1 || { echo "$V failed rc=$?"; tail -5 gpurun_out/vprof/$V.log; exit 3; }
+    python3 ${PROBE:-scripts/hub_probe.py} $ARGS > gpurun_out/vprof/$V.log 2>&1 || { echo "$V failed rc=$?"; tail -5 gpurun_out/vprof/$V.log; exit 3; }
   echo "== $V"
-  grep '"variant"' gpurun_out/vprof/$V.log | python3 -c "
+  grep "^{" gpurun_out/vprof/$V.log | grep -v variant; grep "\"variant\"" gpurun_out/vprof/$V.log | python3 -c "
 import sys, json
 for l in sys.stdin:
     d = json.loads(l); print('  F=%d %s warm %.2f us cold %.2f us err %.1e blocks %d' % (d['F'], d['variant'], d['warm_us'], d['cold_us'], d['max_err'], d['hdr'][4]))"

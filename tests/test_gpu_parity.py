@@ -125,9 +125,13 @@ def _mixed_density_csr(rng, M, K):
 
 
 @pytest.mark.parametrize("F", [1, 7, 8, 64, 200, 256, 300])
-def test_spmm_hybrid_dense_blocks(F):
+@pytest.mark.parametrize("M", [700, 900])
+def test_spmm_hybrid_dense_blocks(F, M):
+    """Tile path (single- and multi-chunk dense blocks + slab reduce) beside the
+    row kernel; a square operand keeps its diagonal aside (added in the tile
+    epilogue), a rectangular one has none."""
     rng = np.random.default_rng(F + 1)
-    M, K = 700, 900
+    K = 900
     rp, ci, v = _mixed_density_csr(rng, M, K)
     a = from_arrays(rp, ci, v, (M, K), DEV)
     B = rng.standard_normal((K, F)).astype(np.float32)
@@ -139,7 +143,7 @@ def test_spmm_hybrid_dense_blocks(F):
     _close(got, csr_ref.spmm_epilogue(acc, bias, relu=True, mask=mask, scale=1.5), atol=2e-5 * np.sqrt(K))
     hdr = list(a._plans.values())[0].header
     assert hdr[8] > 0 and hdr[9] > 0, "dense blocks (single and multi-chunk) expected on the tile path"
-    assert hdr[12] == 1, "diagonal entries of tile rows are extracted"
+    assert hdr[12] == (1 if M == K else 0), "diagonal entries of a square operand's tile rows are kept aside"
     # tile path disabled: the row kernel alone gives the same product
     got2 = spmm(a, torch.from_numpy(B).to(DEV), dense=2.0)
     _close(got2, acc, atol=2e-5 * np.sqrt(K))
@@ -804,3 +808,30 @@ def test_device_dropout_draws_a_fresh_mask_on_every_graph_replay(r8):
         m._rng_base.fill_(base0 + step)
         eager = m(x, adj)
         assert torch.equal(eager, outs[1])
+
+
+def test_graph_capture_takes_a_prezeroed_counter_region(monkeypatch):
+    """A captured SpMM whose plan needs arrival counters takes one of the
+    plan's pre-zeroed spare regions (no memset node replayed with every call)
+    and its replays stay exact (the kernels re-arm the counters)."""
+    from graph_convolutional_networks_for_text_classification_amd import sparse as sp
+    monkeypatch.setattr(sp, "HUB_MIN", -1)
+    rng = np.random.default_rng(23)
+    M, K, F = 3001, 20003, 200
+    rp, ci, v = _random_csr(M, K, 20000, rng, heavy_rows=(5, 1700), heavy_deg=2500)
+    a = from_arrays(rp, ci, v, (M, K), DEV)
+    B = torch.from_numpy(rng.standard_normal((K, F)).astype(np.float32)).to(DEV)
+    ref = spmm(a, B, dense=2.0)
+    plan = list(a._plans.values())[-1]
+    assert plan.counter_bytes() > 0
+    spares = len(plan._spares)
+    out = torch.empty_like(ref)
+    g = torch.cuda.CUDAGraph()
+    with torch.cuda.graph(g):
+        spmm(a, B, out=out, dense=2.0)
+    assert len(plan._spares) == spares - 1
+    for _ in range(5):
+        out.zero_()
+        g.replay()
+        torch.cuda.synchronize()
+        assert torch.equal(out, ref)

@@ -85,8 +85,9 @@ constexpr int kLightMax64 = 64 / kLightRPW;  // their nonzero limit (kLightRPW r
 //   heavy region first, then light rows, each laid out so that the units of
 //   workgroup b belong to XCD class b % 8 (below) | heavy int4[nheavy]
 //   {row, first partial slot, nseg, 0} | tile part (descriptors,
-//   condensed columns, A fragments, reduce list, row lists, extracted diagonal
-//   float[64 * ntblk] in block order).
+//   condensed columns, A fragments, reduce rows int4[64 * nred] {row (-1:
+//   none), first slab, slabs, diagonal value bits}, row lists, extracted
+//   diagonal float[64 * ntblk] in block order).
 struct Layout {
   int64_t M, nnz, nunits, nhunits, nheavy, nslots, ntile, nred, ntblk, has_diag;
   int64_t items, units, heavy, tdesc, tcols, tfrag, red, trows, dval, total;
@@ -100,7 +101,7 @@ struct Layout {
     tcols = tdesc + 4 * ntile;
     tfrag = (tcols + (int64_t)kKC * ntile + 3) & ~3LL;
     red = tfrag + (int64_t)kRB * kKC * ntile;
-    trows = red + 4 * nred;
+    trows = red + 4 * nred * kRB;
     dval = trows + (int64_t)kRB * ntblk;
     total = dval + (has_diag ? (int64_t)kRB * ntblk : 0);
   }
@@ -787,44 +788,47 @@ spmm_tile_kernel(const int4* __restrict__ tdesc, const int32_t* __restrict__ tco
 // Multi-chunk dense blocks: out[row, :] = epi(sum over the block's slabs, in
 // chunk order).  256 threads = 16 slab lanes x 16 float4 column lanes; a
 // workgroup covers one row x 64 columns; slab lanes take slabs strided by 16,
-// then the 16 partial sums are added in lane order through LDS.
+// then the 16 partial sums are added in lane order through LDS.  The row's
+// reduce entry (row, slabs, diagonal) is the only plan read, so the slab loads
+// (and the diagonal's B row) issue one latency after entry.
 __global__ void __launch_bounds__(256)
-spmm_tile_reduce_kernel(const int4* __restrict__ red, const int32_t* __restrict__ trows,
-                        const float* __restrict__ dval, int32_t F, const float* __restrict__ slabs, int64_t slab_ld,
+spmm_tile_reduce_kernel(const int4* __restrict__ red, int32_t F, const float* __restrict__ slabs, int64_t slab_ld,
                         const float* __restrict__ B, int64_t ldb, float* __restrict__ C, int64_t ldc, Epi epi) {
   __shared__ float4 s_acc[16][16];
-  const int4 rb = red[blockIdx.x];  // block, nrows, first slab, nslabs
-  const int32_t rl = blockIdx.y;    // row within block
-  if (rl >= rb.y) return;
+  const int32_t rl = blockIdx.y;  // row within block
   const int sl = threadIdx.x >> 4, c4 = threadIdx.x & 15;
   const int64_t col = (int64_t)blockIdx.z * 64 + c4 * 4;
-  float4 acc = make_float4(0.f, 0.f, 0.f, 0.f);
-  // the epilogue's operands, fetched before the slab loads so their latency overlaps
-  const int64_t row = trows[(int64_t)rb.x * kRB + rl];
-  const float dv = (sl == 0 && dval) ? dval[(int64_t)rb.x * kRB + rl] : 0.f;
-  float bcol[4] = {0.f, 0.f, 0.f, 0.f}, brow[4] = {0.f, 0.f, 0.f, 0.f};
-  if (sl == 0)
+  // the bias first: no wait behind the slab loads
+  float bcol[4] = {0.f, 0.f, 0.f, 0.f};
+  if (sl == 0 && epi.bias)
 #pragma unroll
     for (int i = 0; i < 4; ++i)
-      if (col + i < F) {
-        if (epi.bias) bcol[i] = epi.bias[col + i];
-        if (dv != 0.f) brow[i] = B[row * ldb + col + i];
-      }
+      if (col + i < F) bcol[i] = epi.bias[col + i];
+  const int4 rr = red[(int64_t)blockIdx.x * kRB + rl];  // row, first slab, slabs, diagonal bits
+  if (rr.x < 0) return;
+  const int64_t row = rr.x;
+  const float dv = __int_as_float(rr.w);
+  float brow[4] = {0.f, 0.f, 0.f, 0.f};
+  if (sl == 0 && dv != 0.f)
+#pragma unroll
+    for (int i = 0; i < 4; ++i)
+      if (col + i < F) brow[i] = B[row * ldb + col + i];
+  float4 acc = make_float4(0.f, 0.f, 0.f, 0.f);
   // slab rows are padded to 16 floats (slab_ld % 16 == 0): whole float4 reads stay
   // inside the row; lanes past F are never stored.
   if (col < F) {
     // slab lane sl sums slabs sl, sl + 16, ... in order, 8 loads in flight (one
     // round for up to 128 slabs)
     const int64_t step = (int64_t)16 * kRB * slab_ld;
-    const float* p = slabs + ((int64_t)(rb.z + sl) * kRB + rl) * slab_ld + col;
-    for (int s0 = sl; s0 < rb.w; s0 += 128, p += 8 * step) {
+    const float* p = slabs + ((int64_t)(rr.y + sl) * kRB + rl) * slab_ld + col;
+    for (int s0 = sl; s0 < rr.z; s0 += 128, p += 8 * step) {
       float4 u[8];
 #pragma unroll
       for (int j = 0; j < 8; ++j)
-        u[j] = s0 + 16 * j < rb.w ? *reinterpret_cast<const float4*>(p + j * step) : make_float4(0.f, 0.f, 0.f, 0.f);
+        u[j] = s0 + 16 * j < rr.z ? *reinterpret_cast<const float4*>(p + j * step) : make_float4(0.f, 0.f, 0.f, 0.f);
 #pragma unroll
       for (int j = 0; j < 8; ++j) {
-        if (s0 + 16 * j >= rb.w) break;
+        if (s0 + 16 * j >= rr.z) break;
         acc.x += u[j].x; acc.y += u[j].y; acc.z += u[j].z; acc.w += u[j].w;
       }
     }
@@ -1122,8 +1126,11 @@ int host_plan(const int32_t* rp, const int32_t* ci, const float* vv, int32_t M, 
           }
         }
         for (int64_t c = 0; c < ncols; ++c) cmap[(size_t)cols[(size_t)c]] = -1;
-        if (nch > 1) {
-          hp.red.insert(hp.red.end(), {blk, (int32_t)nrows, first_slab, nch});
+        if (nch > 1) {  // one reduce entry per row: the reduce kernel needs no other plan read
+          for (int64_t rl = 0; rl < kRB; ++rl) {
+            const int32_t r = rl < nrows ? rows[i0 + (size_t)rl] : -1;
+            hp.red.insert(hp.red.end(), {r, first_slab, nch, r >= 0 ? __builtin_bit_cast(int32_t, dv[(size_t)r]) : 0});
+          }
           ++nred;
           nslabs += nch;
         }
@@ -1615,8 +1622,7 @@ static int spmm_impl(const void* plan, const int32_t* hdr, const float* B, int64
     if (rc) return rc;
     if (L.nred > 0 && part != 1) {
       hipLaunchKernelGGL(spmm_tile_reduce_kernel, dim3((unsigned)L.nred, kRB, (unsigned)((F + 63) / 64)), dim3(256),
-                         0, s, reinterpret_cast<const int4*>(p + L.red), p + L.trows, dval, F, slabs, slab_ld, B, ldb,
-                         C, ldc, e);
+                         0, s, reinterpret_cast<const int4*>(p + L.red), F, slabs, slab_ld, B, ldb, C, ldc, e);
       int rc = launch_check("spmm_tile_reduce_kernel");
       if (rc) return rc;
     }

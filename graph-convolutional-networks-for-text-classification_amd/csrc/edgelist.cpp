@@ -16,6 +16,7 @@
 #include <cstdio>
 #include <cstdlib>
 #include <cstring>
+#include <exception>
 #include <vector>
 
 #include "gcnk_common.h"
@@ -63,6 +64,12 @@ int parse(const char* path, std::vector<Edge>& edges, int64_t& n) {
     return GCNK_EARG;
   }
   std::fclose(f);
+  // bounds first: a malformed or huge id must not size the allocation below
+  if (maxid + 1 >= INT32_MAX || 2 * (int64_t)edges.size() >= INT32_MAX) {
+    set_error("gcnk_edgelist: graph too large for int32 CSR (max id %lld, %lld edges)", (long long)maxid,
+              (long long)edges.size());
+    return GCNK_EUNSUP;
+  }
   // distinct ids must be exactly 0..maxid
   std::vector<char> seen((size_t)(maxid + 1), 0);
   for (const Edge& e : edges) seen[(size_t)e.u] = seen[(size_t)e.v] = 1;
@@ -73,10 +80,6 @@ int parse(const char* path, std::vector<Edge>& edges, int64_t& n) {
       return GCNK_EUNSUP;
     }
   n = maxid + 1;
-  if (n >= INT32_MAX || 2 * (int64_t)edges.size() >= INT32_MAX) {
-    set_error("gcnk_edgelist: graph too large for int32 CSR");
-    return GCNK_EUNSUP;
-  }
   // both directions; a repeated undirected edge keeps its last weight
   std::vector<Edge> both;
   both.reserve(edges.size() * 2);
@@ -97,6 +100,17 @@ int parse(const char* path, std::vector<Edge>& edges, int64_t& n) {
   return GCNK_OK;
 }
 
+// No exception may cross the extern "C" boundary: allocation failures become
+// an error code.
+int parse_guarded(const char* path, std::vector<Edge>& edges, int64_t& n) {
+  try {
+    return parse(path, edges, n);
+  } catch (const std::exception& ex) {
+    set_error("gcnk_edgelist: %s", ex.what());
+    return GCNK_EUNSUP;
+  }
+}
+
 }  // namespace
 }  // namespace gcnk
 
@@ -109,7 +123,7 @@ extern "C" int gcnk_edgelist_size(const char* path, int64_t* n_nodes, int64_t* n
   }
   std::vector<Edge> e;
   int64_t n = 0;
-  const int rc = parse(path, e, n);
+  const int rc = parse_guarded(path, e, n);
   if (rc) return rc;
   *n_nodes = n;
   *nnz = (int64_t)e.size();
@@ -124,7 +138,7 @@ extern "C" int gcnk_edgelist_csr(const char* path, int64_t n_nodes, int64_t nnz,
   }
   std::vector<Edge> e;
   int64_t n = 0;
-  const int rc = parse(path, e, n);
+  const int rc = parse_guarded(path, e, n);
   if (rc) return rc;
   if (n != n_nodes || (int64_t)e.size() != nnz) {
     set_error("gcnk_edgelist_csr: file has %lld nodes / %lld nonzeros, buffers sized for %lld / %lld", (long long)n,

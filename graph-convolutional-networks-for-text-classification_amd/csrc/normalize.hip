@@ -10,9 +10,13 @@
 //   * value(r, c) = (d[r] * a) * d[c] in float64 -- what
 //     adj.dot(D).transpose().dot(D) evaluates for a symmetric A
 //     (utils.py:212) -- rounded to fp32 once (utils.py:198).
-// Input: CSR with sorted, duplicate-free columns per row (what
-// sparse.from_torch produces from the reference's COO).  Output: CSR of Â,
-// capacity nnz + n; its row pointer's last word is the output nnz.
+// Input: a SYMMETRIC A as CSR with sorted, duplicate-free columns per row
+// (what sparse.from_torch produces from the reference's COO).  The kernels do
+// not check either property (that would need a host sync per call):
+// sparse.preprocess_adj validates both once and raises, since an unsorted row
+// misplaces the inserted diagonal and a non-symmetric A gets D A D where the
+// reference computes D A^T D.  Output: CSR of Â, capacity nnz + n; its row
+// pointer's last word is the output nnz.
 #include "gcnk_common.h"
 
 #include <hipcub/hipcub.hpp>

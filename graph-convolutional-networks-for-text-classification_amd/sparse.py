@@ -261,11 +261,17 @@ def preprocess_adj(adj):
     float64 arithmetic and one rounding to fp32, so the values are bit-for-bit
     what the host path produces.  ``adj``: symmetric A as a torch sparse
     tensor (any COO order, duplicates summed) or a CSR on the GPU.  Returns the
-    CSR of Â (usable directly as ``adj`` of GCN.forward)."""
+    CSR of Â (usable directly as ``adj`` of GCN.forward).
+
+    The kernel needs sorted, duplicate-free columns per row and a symmetric A
+    (the reference evaluates (A D)^T D, which is D A D only when A = A^T; its
+    trainer builds max(A, A^T), trainer.py:148).  Both are checked here (one
+    setup-time sync) and violations raise instead of giving wrong values."""
     a = adj if isinstance(adj, CSR) else from_torch(adj)
     n, k = a.shape
     if n != k:
         raise RuntimeError(f"preprocess_adj: adjacency must be square, got {a.shape}")
+    _check_sorted_symmetric(a)
     lib = _lib.load()
     dev = a.device
     rp = torch.empty(n + 1, dtype=torch.int32, device=dev)
@@ -281,6 +287,22 @@ def preprocess_adj(adj):
                                           _stream_ptr(dev)), "gcnk_sym_normalize")
     nnz = int(rp[n])   # one-time setup sync
     return CSR(rp, ci[:nnz], v[:nnz], (n, n))
+
+
+def _check_sorted_symmetric(a):
+    n = a.shape[0]
+    if a.nnz == 0:
+        return
+    rows = torch.repeat_interleave(torch.arange(n, device=a.device, dtype=torch.int32), a.rowptr.diff())
+    unsorted = bool(((a.colind[1:] <= a.colind[:-1]) & (rows[1:] == rows[:-1])).any())
+    if unsorted:
+        raise RuntimeError("preprocess_adj: CSR columns must be sorted and duplicate-free within each row "
+                           "(build it with from_torch, which coalesces)")
+    t = transpose(a)
+    if not (torch.equal(t.rowptr, a.rowptr) and torch.equal(t.colind, a.colind) and torch.equal(t.val, a.val)):
+        raise RuntimeError("preprocess_adj: the adjacency is not symmetric; the reference's (A D)^T D "
+                           "(utils.py:212) is D^-1/2 A D^-1/2 only for A = A^T -- symmetrise it first "
+                           "(max(A, A^T) as trainer.py:148 does)")
 
 
 class _Cache:

@@ -73,3 +73,6 @@ def test_errors(tmp_path):
         datasets.load_edgelist(_write(tmp_path / "b.txt", ["0 1 1.0", "0 x 2"]))
     with pytest.raises(_lib.GcnkError, match="cannot open"):
         datasets.load_edgelist(str(tmp_path / "missing.txt"))
+    # a huge node id is refused before anything is sized by it
+    with pytest.raises(_lib.GcnkError, match="too large"):
+        datasets.load_edgelist(_write(tmp_path / "c.txt", ["0 1 1.0", "1 1000000000000 1.0"]))

@@ -716,6 +716,23 @@ def test_preprocess_adj_known_answers(golden_meta):
     assert np.array_equal(ah.val.cpu().numpy(), want)
 
 
+def test_preprocess_adj_rejects_unsorted_or_asymmetric_input():
+    """gcnk_sym_normalize assumes sorted, duplicate-free rows and a symmetric A
+    (the reference's (A D)^T D); preprocess_adj checks both and raises."""
+    from graph_convolutional_networks_for_text_classification_amd import preprocess_adj
+    from graph_convolutional_networks_for_text_classification_amd.sparse import CSR
+    i32 = dict(dtype=torch.int32, device=DEV)
+    # unsorted row 0 (columns 2, 1) of a symmetric pattern
+    a = CSR(torch.tensor([0, 2, 3, 4], **i32), torch.tensor([2, 1, 0, 0], **i32),
+            torch.ones(4, device=DEV), (3, 3))
+    with pytest.raises(RuntimeError, match="sorted"):
+        preprocess_adj(a)
+    # a directed edge 0 -> 1 only
+    A = torch.sparse_coo_tensor(torch.tensor([[0], [1]]), torch.tensor([1.0]), (2, 2)).to(DEV)
+    with pytest.raises(RuntimeError, match="not symmetric"):
+        preprocess_adj(A)
+
+
 # ------------------------------------------------------------------------------ evaluation metrics
 
 @pytest.mark.parametrize("nclass", [8, 20])

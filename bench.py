@@ -76,6 +76,8 @@ def parse():
     ap.add_argument("--kernel-reps", type=int, default=200, help="launches per op-timing graph")
     ap.add_argument("--no-pmc", action="store_true", help="skip the live rocprofv3 --pmc traffic passes")
     ap.add_argument("--no-configs", action="store_true", help="skip BASELINE configs 3 and 4")
+    ap.add_argument("--no-rocprof", action="store_true", help="skip the child rocprofv3 kernel-trace runs")
+    ap.add_argument("--rocprof-dir", default=None, help="keep the child kernel-trace summaries here")
     return ap.parse_args()
 
 
@@ -162,6 +164,42 @@ def pmc_traffic(op, kernels_like):
         return 2 * per["FETCH_SIZE"] + per["WRITE_SIZE"], "live rocprofv3 --pmc (FETCH_SIZE x2 + WRITE_SIZE)"
     except (OSError, subprocess.SubprocessError, KeyError, ValueError) as e:
         return None, f"pmc pass failed: {e}"
+    finally:
+        shutil.rmtree(tmp, ignore_errors=True)
+
+
+def rocprof_kernel_us(mode, kernels_like, save_dir=None):
+    """Average kernel duration (us) of the north-star op's kernels from a child
+    rocprofv3 --kernel-trace --stats run of scripts/hub_probe.py (the same op,
+    the same warm / cold rotation as the HIP-event figure), so the reported
+    fraction can be checked against a rocprof summary of the same launches."""
+    exe = shutil.which("rocprofv3")
+    if exe is None:
+        return None, "rocprofv3 not on PATH"
+    tmp = tempfile.mkdtemp(prefix="gcnk_kt_", dir="/tmp")
+    env = dict(os.environ, TMPDIR="/tmp")
+    try:
+        cmd = ["timeout", "-s", "KILL", "150", exe, "--kernel-trace", "--stats", "--output-format", "csv", "-d", tmp,
+               "-o", "kt", "--", sys.executable, os.path.join(ROOT, "scripts", "hub_probe.py"), "--reps", "200",
+               "--variants", "row", "--widths", "200", "--mode", mode]
+        r = subprocess.run(cmd, cwd=ROOT, env=env, stdout=subprocess.PIPE, stderr=subprocess.STDOUT, timeout=180)
+        if r.returncode != 0:
+            return None, f"rocprofv3 --kernel-trace rc={r.returncode}"
+        files = glob.glob(os.path.join(tmp, "**", "*kernel_stats.csv"), recursive=True)
+        total, found = 0.0, False
+        for f in files:
+            for row in csv.DictReader(open(f)):
+                if any(k in row["Name"] for k in kernels_like):
+                    total += float(row["AverageNs"]) / 1e3
+                    found = True
+            if save_dir:
+                os.makedirs(save_dir, exist_ok=True)
+                shutil.copy(f, os.path.join(save_dir, f"bench_rocprof_as1_{mode}_kernel_stats.csv"))
+        if not found:
+            return None, f"no kernel rows for {kernels_like}"
+        return total, f"rocprofv3 --kernel-trace --stats, scripts/hub_probe.py --mode {mode}"
+    except (OSError, subprocess.SubprocessError, KeyError, ValueError) as e:
+        return None, f"kernel trace failed: {e}"
     finally:
         shutil.rmtree(tmp, ignore_errors=True)
 
@@ -285,6 +323,12 @@ def main():
     traffic, traffic_src = (None, "skipped")
     if extras and not args.no_pmc:
         traffic, traffic_src = pmc_traffic("AS1", ["hub_light_kernel", "hub_finish_kernel", "spmm_row_kernel"])
+    # ---- the same op's kernel durations from rocprofv3 (warm and cold rotations)
+    kt = {}
+    if extras and not args.no_rocprof:
+        for mode in ("warm", "cold"):
+            kt[mode] = rocprof_kernel_us(mode, ["hub_light_kernel", "hub_finish_kernel", "spmm_row_kernel"],
+                                         args.rocprof_dir)
 
     # ---- CPU baselines (rank 0, N = 1): oracle at all cores and 1 thread, torch CSR (MKL)
     cpu = cpu_stock = gpu_stock = None
@@ -424,6 +468,12 @@ def main():
                      "traffic": traffic, "traffic_source": traffic_src,
                      "avg_launch_us": kn["cold_us"], "avg_launch_us_warm": kn["warm_us"],
                      "algorithmic_bytes": kn["algorithmic_bytes"]},
+        # the same op under rocprofv3: kernel time without the dispatch gap that the
+        # per-call HIP-event figure above includes
+        "roofline_rocprof": {m: ({"kernel_us": round(v[0], 3),
+                                  "frac": kn["algorithmic_bytes"] / (v[0] * 1e-6) / 1e9 / HBM_PEAK_GBS,
+                                  "source": v[1]} if v[0] is not None else {"error": v[1]})
+                             for m, v in kt.items()},
         "roofline_dominant": {"kernel": dom, "frac": kd["frac_cold"], "frac_warm": kd["frac_warm"],
                               "avg_launch_us": kd["cold_us"], "algorithmic_bytes": kd["algorithmic_bytes"]},
         "ops": optimes,

@@ -68,6 +68,8 @@ def main():
     ap.add_argument("--variants", default="row,hub,hub16,hub24,hub48,hub64")
     ap.add_argument("--widths", default="200,8")
     ap.add_argument("--graph", default="r8", choices=["r8", "20ng"])
+    ap.add_argument("--mode", default="both", choices=["warm", "cold", "both"],
+                    help="which timing graphs to run (one mode alone for a rocprofv3 kernel average)")
     args = ap.parse_args()
     dev = torch.device("cuda", 0)
     if args.graph == "r8":
@@ -88,6 +90,7 @@ def main():
         for name in args.variants.split(","):
             kw = VARIANTS[name]
             import graph_convolutional_networks_for_text_classification_amd.sparse as sp
+            saved = sp.HUB_MIN, sp.HUB_BLOCK_ROWS
             sp.HUB_MIN, sp.HUB_BLOCK_ROWS = kw.get("hub_min", 0), kw.get("block_rows", 0)
             out = ops.spmm(a, Bs[0], bias=bias, epilogue=_lib.EPI_BIAS_RELU)
             torch.cuda.synchronize()
@@ -95,17 +98,20 @@ def main():
             again = ops.spmm(a, Bs[0], bias=bias, epilogue=_lib.EPI_BIAS_RELU)
             det = bool(torch.equal(out, again))
             plan = [p for k, p in a._plans.items() if k[3] == sp.HUB_MIN and k[4] == sp.HUB_BLOCK_ROWS][-1]
-            warm = time_graph([lambda: ops.spmm(a, Bs[0], bias=bias, epilogue=_lib.EPI_BIAS_RELU, out=Cs[0])],
-                              args.reps)
+            warm = cold = float("nan")
+            if args.mode in ("warm", "both"):
+                warm = time_graph([lambda: ops.spmm(a, Bs[0], bias=bias, epilogue=_lib.EPI_BIAS_RELU, out=Cs[0])],
+                                  args.reps)
             fns = [(lambda i=i: ops.spmm(a, Bs[i], bias=bias, epilogue=_lib.EPI_BIAS_RELU, out=Cs[i]))
                    for i in range(nsets)]
-            cold = time_graph(fns, max(1, args.reps // nsets))
+            if args.mode in ("cold", "both"):
+                cold = time_graph(fns, max(1, args.reps // nsets))
             print(json.dumps({"graph": args.graph, "F": F, "variant": name, "hub": plan.is_hub,
                               "hdr": plan.header, "max_err": err, "deterministic": det,
                               "warm_us": round(warm, 3), "cold_us": round(cold, 3),
                               "warm_frac": nbytes / (warm * 1e-6) / 8e12, "cold_frac": nbytes / (cold * 1e-6) / 8e12,
                               "sets": nsets}), flush=True)
-            sp.HUB_MIN, sp.HUB_BLOCK_ROWS = 0, 0
+            sp.HUB_MIN, sp.HUB_BLOCK_ROWS = saved
 
 
 if __name__ == "__main__":

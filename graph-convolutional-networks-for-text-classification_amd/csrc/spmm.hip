@@ -698,16 +698,17 @@ spmm_tile_kernel(const int4* __restrict__ tdesc, const int32_t* __restrict__ tco
   const int kr = lane >> 4, nc = lane & 15;
 #pragma unroll
   for (int s = 0; s < 16; ++s) {
-    if (s >= ksteps) break;  // R8 X's document blocks: 50 columns, 13 of 16 k-steps
-    const float4* brow = reinterpret_cast<const float4*>(s_B + (4 * s + kr) * stride + nc * LR);
-    float4 bq[NT4 / 4];
+    if (s < ksteps) {  // wave-uniform; R8 X's document blocks: 50 columns, 13 of 16 k-steps
+      const float4* brow = reinterpret_cast<const float4*>(s_B + (4 * s + kr) * stride + nc * LR);
+      float4 bq[NT4 / 4];
 #pragma unroll
-    for (int q = 0; q < NT4 / 4; ++q) bq[q] = brow[q];
+      for (int q = 0; q < NT4 / 4; ++q) bq[q] = brow[q];
 #pragma unroll
-    for (int nt = 0; nt < NT; ++nt) {
-      const float4& b4 = bq[nt >> 2];
-      const float bval = (nt & 3) == 0 ? b4.x : (nt & 3) == 1 ? b4.y : (nt & 3) == 2 ? b4.z : b4.w;
-      acc[nt] = __builtin_amdgcn_mfma_f32_16x16x4f32(a[s], bval, acc[nt], 0, 0, 0);
+      for (int nt = 0; nt < NT; ++nt) {
+        const float4& b4 = bq[nt >> 2];
+        const float bval = (nt & 3) == 0 ? b4.x : (nt & 3) == 1 ? b4.y : (nt & 3) == 2 ? b4.z : b4.w;
+        acc[nt] = __builtin_amdgcn_mfma_f32_16x16x4f32(a[s], bval, acc[nt], 0, 0, 0);
+      }
     }
   }
 

@@ -21,6 +21,7 @@
  *   utils.py:185-213 preprocess_adj / normalize_adj          -> gcnk_sym_normalize (device, bit-exact)
  *   utils.py:25-109  accuracy / macro_f1 counts              -> gcnk_class_stats (one launch, no per-class syncs)
  *   trainer.py:98-148 edge list -> symmetric adjacency        -> gcnk_edgelist_size / _csr (host, no networkx)
+ *   layer.py:185 th.dropout keep-mask draw (CPU generator)    -> gcnk_bernoulli_mt19937 (host, same stream)
  *
  * Conventions
  *   - All pointers are DEVICE pointers unless a parameter says "host".
@@ -298,6 +299,20 @@ int gcnk_class_stats(const float* logits, int64_t ld, const int64_t* target, con
  * ------------------------------------------------------------------------- */
 int gcnk_edgelist_size(const char* path, int64_t* n_nodes, int64_t* nnz);
 int gcnk_edgelist_csr(const char* path, int64_t n_nodes, int64_t nnz, int32_t* rowptr, int32_t* colind, float* val);
+
+/* ---------------------------------------------------------------------------
+ * Dropout keep-mask exactly as the reference's CPU th.dropout draws it
+ * (HOST pointers; layer.py:185 -> ATen dropout -> empty_like(x).bernoulli_(p)
+ * with p = 1 - dropout): torch's serial CPU bernoulli_ takes one 64-bit draw
+ * of the MT19937 generator per element, in order, and keeps the element when
+ * (draw & (2^53 - 1)) * 2^-53 < p.  `state` (624 words), `left` and `next` are
+ * the generator's state fields (torch's CPU generator state tensor), advanced
+ * in place by the 2 n outputs consumed, so writing them back leaves the
+ * process's random stream where the reference leaves it.  mask_out[n]: 1 =
+ * kept.  `threads` workers temper and compare (the twist chain is serial).
+ * ------------------------------------------------------------------------- */
+int gcnk_bernoulli_mt19937(uint32_t* state, int32_t* left, int64_t* next, int64_t n, double p, uint8_t* mask_out,
+                           int32_t threads);
 
 /* Debug only: in a library built with -DGCNK_STAMPS, when `buf` is non-null
  * every later row/tile SpMM launch writes 4 x uint64 s_memrealtime stamps

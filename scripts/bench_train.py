@@ -66,9 +66,9 @@ def main():
                           "ms_per_step": round(ms, 4), "steps": args.steps}), flush=True)
 
     # the same step (dropout_rng="device") captured once in a hipGraph and replayed:
-    # launch-overhead-free kernel time of a training step.  The captured dropout
-    # offset is frozen (every replay draws the same mask), which does not change
-    # the work done.
+    # launch-overhead-free kernel time of a training step.  The hash offset lives
+    # on the device and the captured forward advances it, so every replay trains
+    # on a fresh mask (checked below: the stream position moves one step per replay).
     torch.manual_seed(0)
     model = GCN(nfeat=nfeat, nhid=200, nclass=nclass, dropout=0.5, dropout_rng="device").to(dev)
     opt = torch.optim.Adam(model.parameters(), lr=0.02, capturable=True)
@@ -95,14 +95,17 @@ def main():
         step()
     g.replay()
     torch.cuda.synchronize()
+    base0 = int(model._rng_base.item())
     e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
     e0.record()
     for _ in range(args.steps):
         g.replay()
     e1.record()
     e1.synchronize()
+    advanced = (int(model._rng_base.item()) - base0) // (r8["nodes"] * 200)
     print(json.dumps({"case": "R8 train step (fwd + bwd + Adam)", "impl": "HIP, dropout_rng=device, hipGraph replay",
-                      "ms_per_step": round(e0.elapsed_time(e1) / args.steps, 4), "steps": args.steps}), flush=True)
+                      "ms_per_step": round(e0.elapsed_time(e1) / args.steps, 4), "steps": args.steps,
+                      "fresh_masks": advanced == args.steps}), flush=True)
 
     if args.cpu_steps > 0:
         torch.manual_seed(0)

@@ -91,6 +91,7 @@ SIGNATURES = {
     "gcnk_class_stats": (ctypes.c_int, [_vp, _i64, _vp, _vp, _i64, _i32, _vp, _vp]),
     "gcnk_edgelist_size": (ctypes.c_int, [ctypes.c_char_p, _vp, _vp]),
     "gcnk_edgelist_csr": (ctypes.c_int, [ctypes.c_char_p, _i64, _i64, _vp, _vp, _vp]),
+    "gcnk_csr_to_dense": (ctypes.c_int, [_vp, _vp, _vp, _i32, _i32, _vp, _i64, _vp]),
     "gcnk_bernoulli_mt19937": (ctypes.c_int, [_vp, _vp, _vp, _i64, ctypes.c_double, _vp, _i32]),
     "gcnk_sym_normalize_workspace_bytes": (_i64, [_i32, _i64]),
     "gcnk_sym_normalize": (ctypes.c_int, [_vp, _vp, _vp, _i32, _i64, _vp, _vp, _vp, _vp, _i64, _vp]),

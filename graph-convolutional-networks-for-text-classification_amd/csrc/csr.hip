@@ -251,3 +251,44 @@ extern "C" int gcnk_coo_to_csr(const int64_t* rows, const int64_t* cols, const f
   hipLaunchKernelGGL(poison_kernel, dim3(1), dim3(1), 0, s, bad, M, rowptr);
   return launch_check("poison_kernel");
 }
+
+// ---------------------------------------------------------------------------
+// CSR -> dense row-major (one-time layout change of a dense-enough sparse
+// operand, e.g. a gensim-shaped X: the MFMA GEMM then replaces the tile path,
+// whose 64-column chunks would leave every row block split over slabs).
+// One wavefront per row; lane l owns columns l, l + 64, ... and writes each
+// of them once: the sum of the row's entries in that column, in CSR order
+// (no lane reads what another wrote).  Meant for the dense-enough operands it
+// is used on (a few hundred columns, tens of nonzeros per row).
+namespace gcnk {
+namespace {
+__global__ void __launch_bounds__(256) csr_to_dense_kernel(const int32_t* __restrict__ rowptr,
+                                                           const int32_t* __restrict__ colind,
+                                                           const float* __restrict__ val, int32_t M, int32_t K,
+                                                           float* __restrict__ out, int64_t ld) {
+  const int64_t r = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
+  const int lane = threadIdx.x & 63;
+  if (r >= M) return;
+  const int32_t b = rowptr[r], e = rowptr[r + 1];
+  float* row = out + r * ld;
+  for (int32_t c = lane; c < K; c += 64) {
+    float v = 0.f;
+    for (int32_t k = b; k < e; ++k)
+      if (colind[k] == c) v += val[k];
+    row[c] = v;
+  }
+}
+}  // namespace
+}  // namespace gcnk
+
+extern "C" int gcnk_csr_to_dense(const int32_t* rowptr, const int32_t* colind, const float* val, int32_t M,
+                                 int32_t K, float* out, int64_t ld, void* stream) {
+  if (M < 0 || K < 0 || ld < K || (M > 0 && (!rowptr || !out))) {
+    set_error("gcnk_csr_to_dense: bad argument (M=%d K=%d ld=%lld)", M, K, (long long)ld);
+    return GCNK_EARG;
+  }
+  if (M == 0) return GCNK_OK;
+  hipLaunchKernelGGL(csr_to_dense_kernel, dim3((unsigned)((M + 3) / 4)), dim3(256), 0, (hipStream_t)stream, rowptr,
+                     colind, val, M, K, out, ld);
+  return launch_check("csr_to_dense_kernel");
+}

@@ -614,7 +614,6 @@ spmm_tile_kernel(const int4* __restrict__ tdesc, const int32_t* __restrict__ tco
   // block, nrows | contiguous run length << 8 | width << 16, slab (-1: single chunk), run start
   const int4 d0 = tdesc[item];
   const int32_t run = (d0.y >> 8) & 0xff;
-  const int32_t ksteps = __builtin_amdgcn_readfirstlane(((d0.y >> 16) + 3) >> 2);  // k-steps past the width are zero
   const int4 d = make_int4(d0.x, d0.y & 0xff, d0.z, d0.w);
   const int64_t col0 = (int64_t)blockIdx.y * (NT * 16);  // this workgroup's column slice
 
@@ -697,18 +696,19 @@ spmm_tile_kernel(const int4* __restrict__ tdesc, const int32_t* __restrict__ tco
                        a2.x, a2.y, a2.z, a2.w, a3.x, a3.y, a3.z, a3.w};
   const int kr = lane >> 4, nc = lane & 15;
 #pragma unroll
+  // all 16 k-steps, padding included: skipping the zero steps of narrow chunks
+  // (R8 X's 50-column document blocks: 13 of 16) measured no faster (10.70 vs
+  // 10.75 us) and, written as a guarded unrolled loop, slower (12.98 us)
   for (int s = 0; s < 16; ++s) {
-    if (s < ksteps) {  // wave-uniform; R8 X's document blocks: 50 columns, 13 of 16 k-steps
-      const float4* brow = reinterpret_cast<const float4*>(s_B + (4 * s + kr) * stride + nc * LR);
-      float4 bq[NT4 / 4];
+    const float4* brow = reinterpret_cast<const float4*>(s_B + (4 * s + kr) * stride + nc * LR);
+    float4 bq[NT4 / 4];
 #pragma unroll
-      for (int q = 0; q < NT4 / 4; ++q) bq[q] = brow[q];
+    for (int q = 0; q < NT4 / 4; ++q) bq[q] = brow[q];
 #pragma unroll
-      for (int nt = 0; nt < NT; ++nt) {
-        const float4& b4 = bq[nt >> 2];
-        const float bval = (nt & 3) == 0 ? b4.x : (nt & 3) == 1 ? b4.y : (nt & 3) == 2 ? b4.z : b4.w;
-        acc[nt] = __builtin_amdgcn_mfma_f32_16x16x4f32(a[s], bval, acc[nt], 0, 0, 0);
-      }
+    for (int nt = 0; nt < NT; ++nt) {
+      const float4& b4 = bq[nt >> 2];
+      const float bval = (nt & 3) == 0 ? b4.x : (nt & 3) == 1 ? b4.y : (nt & 3) == 2 ? b4.z : b4.w;
+      acc[nt] = __builtin_amdgcn_mfma_f32_16x16x4f32(a[s], bval, acc[nt], 0, 0, 0);
     }
   }
 

@@ -238,8 +238,30 @@ def colsum(X):
 # ----------------------------------------------------------------------------------------
 # Operand for the first product of a layer: sparse (CSR) or dense infeatn.
 
+# A sparse infeatn at least this full (nnz / (rows x cols)) is multiplied as a
+# dense matrix on the MFMA GEMM: a gensim-style 100-d X (50-70 % fill) would
+# otherwise leave every 64-row block of the tile path split over two 64-column
+# chunks and a slab reduce (20ng-shaped X W1: 71 us sparse, 19.7 us dense).
+DENSE_OPERAND_FILL = 0.2
+DENSE_OPERAND_MAX_BYTES = 1 << 30
+
+
+def dense_copy(a):
+    """The dense [M, K] fp32 copy of CSR ``a`` (gcnk_csr_to_dense), cached on it."""
+    d = getattr(a, "_dense", None)
+    if d is None:
+        M, K = a.shape
+        d = torch.empty((M, K), dtype=torch.float32, device=a.device)
+        with torch.cuda.device(a.device):
+            _lib.check(_lib.load().gcnk_csr_to_dense(_ptr(a.rowptr), _ptr(a.colind), _ptr(a.val), M, K, _ptr(d),
+                                                     d.stride(0), _stream(a.device)), "gcnk_csr_to_dense")
+        a._dense = d
+    return d
+
+
 class Operand:
-    """``infeatn`` of GraphConvolution.forward: sparse -> CSR, dense -> tensor."""
+    """``infeatn`` of GraphConvolution.forward: sparse -> CSR (or, when at least
+    DENSE_OPERAND_FILL full, its cached dense copy), dense -> tensor."""
 
     __slots__ = ("csr", "dense")
 
@@ -250,6 +272,10 @@ class Operand:
             self.csr, self.dense = as_csr(x), None
         else:
             self.csr, self.dense = None, _dense_f32(x, "infeatn")
+        if self.csr is not None:
+            M, K = self.csr.shape
+            if M * K > 0 and self.csr.nnz >= DENSE_OPERAND_FILL * M * K and 4 * M * K <= DENSE_OPERAND_MAX_BYTES:
+                self.csr, self.dense = None, dense_copy(self.csr)
 
     @property
     def shape(self):

@@ -259,6 +259,12 @@ int gcnk_csr_transpose(const int32_t* rowptr, const int32_t* colind, const float
                        int32_t M, int32_t K, int64_t nnz,
                        int32_t* rowptr_t, int32_t* colind_t, float* val_t,
                        void* workspace, int64_t workspace_bytes, void* stream);
+/*  gcnk_csr_to_dense: CSR A[M x K] -> dense row-major out[M x ld] (columns
+ *    K..ld-1 untouched; duplicate entries summed in CSR order).  The one-time
+ *    layout change that sends a dense-enough sparse infeatn (layer.py:102;
+ *    e.g. a gensim-style 100-d X at 50-70 % fill) to the MFMA GEMM. */
+int gcnk_csr_to_dense(const int32_t* rowptr, const int32_t* colind, const float* val, int32_t M, int32_t K,
+                      float* out, int64_t ld, void* stream);
 
 /* ---------------------------------------------------------------------------
  * Device-side adjacency preparation (utils.py:185-213, preprocess_adj /

@@ -149,6 +149,33 @@ def test_spmm_hybrid_dense_blocks(F, M):
     _close(got2, acc, atol=2e-5 * np.sqrt(K))
 
 
+def test_csr_to_dense_sums_duplicates_in_order():
+    """gcnk_csr_to_dense: every element once, duplicates summed in CSR order,
+    columns past K untouched (ld > K)."""
+    from graph_convolutional_networks_for_text_classification_amd import _lib
+    from graph_convolutional_networks_for_text_classification_amd.ops import _ptr, _stream
+    rng = np.random.default_rng(9)
+    M, K = 300, 150
+    rows = rng.integers(0, M, 6000)
+    cols = rng.integers(0, K, 6000)
+    order = np.lexsort((cols, rows))
+    rows, cols = rows[order], cols[order]                 # sorted, duplicates kept
+    vals = rng.standard_normal(6000).astype(np.float32)
+    rp = np.zeros(M + 1, np.int32)
+    np.add.at(rp, rows + 1, 1)
+    rp = np.cumsum(rp).astype(np.int32)
+    want = np.zeros((M, K + 8), np.float32)
+    for r, c, v in zip(rows, cols, vals):
+        want[r, c] = np.float32(want[r, c] + v)
+    want[:, K:] = 7.0
+    out = torch.full((M, K + 8), 7.0, device=DEV)
+    t = [torch.from_numpy(x).to(DEV) for x in (rp, cols.astype(np.int32), vals)]
+    rc = _lib.load().gcnk_csr_to_dense(_ptr(t[0]), _ptr(t[1]), _ptr(t[2]), M, K, _ptr(out), out.stride(0),
+                                       _stream(out.device))
+    assert rc == 0
+    assert np.array_equal(out.cpu().numpy(), want)
+
+
 def test_spmm_r8_features_use_tile_path(r8):
     x = from_torch(r8["features"].to(DEV))
     W = torch.randn(r8["nfeat"], 200, generator=torch.Generator().manual_seed(4))
@@ -353,8 +380,12 @@ def test_csr_transpose_matches_oracle():
 
 
 @pytest.mark.parametrize("ta,tb", [(False, False), (True, False), (False, True), (True, True)])
-@pytest.mark.parametrize("shape", [(7724, 8, 200), (200, 8, 7724), (7724, 200, 8), (33, 70, 5), (1, 1, 1)])
+@pytest.mark.parametrize("shape", [(7724, 8, 200), (200, 8, 7724), (7724, 200, 8), (33, 70, 5), (1, 1, 1),
+                                   (18916, 200, 100), (7724, 20, 200), (1000, 40, 200), (257, 332, 97)])
 def test_gemm_mfma(ta, tb, shape):
+    """Every GEMM kernel against the float64 oracle: the LDS-tiled MFMA kernel,
+    the skinny-N K-split one (N <= 64: gc2's H1 W2 at 8 and 20 classes) and the
+    short-K one (K <= 128, N > 64: a dense gensim-style X W1)."""
     M, N, K = shape
     g = torch.Generator().manual_seed(M * 7 + N)
     A = torch.randn((K, M) if ta else (M, K), generator=g)
@@ -456,8 +487,9 @@ def test_gcn_gensim_shaped_r8_forward_backward(r8):
     """SURVEY §8(d) config 1's feature shape: R8 with the 100-d gensim-style X
     the README's 94.11 % run used (documents: the reference's LDA theta in
     columns 0-49; topics: N(0,1) 100-d rows, L2-normalised; default_rng(0);
-    nnz 388,700) -- X is then two dense blocks on the MFMA tile path.  Eval
-    logits and one train-mode step's gradients against the oracle."""
+    nnz 388,700) -- X is 50 % full, so it is multiplied as a dense copy on the
+    MFMA GEMM (ops.DENSE_OPERAND_FILL).  Eval logits and one train-mode step's
+    gradients against the oracle."""
     ndoc, ntopic = r8["ndoc"], r8["ntopic"]
     X = np.zeros((r8["nodes"], 100), np.float32)
     X[:ndoc, :ntopic] = r8["x_doc"] if "x_doc" in r8 else r8["features_dense"][:ndoc, :ntopic]
@@ -465,6 +497,8 @@ def test_gcn_gensim_shaped_r8_forward_backward(r8):
     X /= np.maximum(np.linalg.norm(X, axis=1, keepdims=True), 1e-12)
     Xs = datasets.dense_to_coo(X)
     assert Xs._nnz() == 388_700
+    from graph_convolutional_networks_for_text_classification_amd.ops import Operand
+    assert Operand(Xs.to(DEV)).dense is not None, "a 50 % full X goes to the dense GEMM"
     torch.manual_seed(50494)
     m = GCN(nfeat=100, nhid=200, nclass=r8["nclass"], dropout=0.5).to(DEV)
     ref = gcn_ref.RefGCN(nfeat=100, nhid=200, nclass=r8["nclass"], dropout=0.5)

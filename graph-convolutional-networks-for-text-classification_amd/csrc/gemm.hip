@@ -223,117 +223,6 @@ gemm_skinny_ksplit_kernel(int32_t M, int32_t N, int32_t K, const float* __restri
   }
 }
 
-// Short-K GEMM (K <= 128, N > 64; A and B row-major, 16-B aligned rows): the
-// dense infeatn of layer.py:102 -- a gensim-style X [nodes x 100] times W1
-// [100 x 200].  One workgroup = 64 rows x NT 16-column tiles; the whole K x
-// (16 NT) slice of B is staged in LDS once, lane-major as in the tile SpMM
-// ([k][col & 15][tile], a 16-B read fetches 4 tiles' operands), and each
-// wave's A rows come straight from global memory as float4 k-slices (lane l:
-// row l & 15, k = 16c + 4(l >> 4) + j at MFMA step (c, j); B is read with the
-// same k permutation).  No k loop over LDS tiles, no split: every output is
-// one MFMA chain over K, written once with the epilogue applied.
-constexpr int kShortKMax = 128;
-template <int NT>
-__global__ void __launch_bounds__(256)
-gemm_shortk_kernel(int32_t M, int32_t N, int32_t K, const float* __restrict__ A, int64_t lda,
-                   const float* __restrict__ B, int64_t ldb, float* __restrict__ C, int64_t ldc, GemmEpi epi) {
-  constexpr int NT4 = (NT + 3) & ~3;
-  constexpr int LR = ((NT4 / 4) & 1) ? NT4 : NT4 + 4;  // odd number of 16-B quads per lane row
-  constexpr int KC = kShortKMax / 16;
-  __shared__ __attribute__((aligned(16))) float s_B[kShortKMax * 16 * LR];
-  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
-  const int64_t m0 = (int64_t)blockIdx.x * 64 + wave * 16;
-  const int64_t n0 = (int64_t)blockIdx.y * (NT * 16);
-  const int kc = (K + 15) >> 4;  // 16-deep k chunks in use (uniform)
-  // A fragments first (their latency overlaps the B staging)
-  const int r = lane & 15, q = lane >> 4;
-  const int64_t row = m0 + r;
-  float4 a[KC];
-#pragma unroll
-  for (int c = 0; c < KC; ++c) {
-    a[c] = make_float4(0.f, 0.f, 0.f, 0.f);
-    const int k = 16 * c + 4 * q;
-    if (c < kc && row < M) {
-      if (k + 3 < K) {
-        a[c] = *reinterpret_cast<const float4*>(A + row * lda + k);
-      } else {
-        if (k + 0 < K) a[c].x = A[row * lda + k + 0];
-        if (k + 1 < K) a[c].y = A[row * lda + k + 1];
-        if (k + 2 < K) a[c].z = A[row * lda + k + 2];
-      }
-    }
-  }
-  // B slice -> LDS: element (k, n) at s_B[k][n & 15][n >> 4]; rows >= K and
-  // columns >= N are zero
-  // all of a thread's B loads are issued before its first LDS store (one
-  // latency, not one per row group)
-  constexpr int NQ = NT * 4;                        // float4 per staged row
-  constexpr int PT = (kShortKMax * NQ + 255) / 256;  // float4 per thread
-  float4 v[PT];
-#pragma unroll
-  for (int p = 0; p < PT; ++p) {
-    const int e = tid + p * 256;
-    const int k = e / NQ, c4 = e % NQ;
-    const int64_t col = n0 + 4 * c4;
-    v[p] = make_float4(0.f, 0.f, 0.f, 0.f);
-    if (k < K) {
-      if (col + 3 < N) {
-        v[p] = *reinterpret_cast<const float4*>(B + (int64_t)k * ldb + col);
-      } else {
-        if (col + 0 < N) v[p].x = B[(int64_t)k * ldb + col + 0];
-        if (col + 1 < N) v[p].y = B[(int64_t)k * ldb + col + 1];
-        if (col + 2 < N) v[p].z = B[(int64_t)k * ldb + col + 2];
-      }
-    }
-  }
-#pragma unroll
-  for (int p = 0; p < PT; ++p) {
-    const int e = tid + p * 256;
-    const int k = e / NQ, c4 = e % NQ;
-    if (k >= 16 * kc) break;
-    const int n = 4 * c4, nt = n >> 4, nc0 = n & 15;
-    float* dst = s_B + k * (16 * LR) + nc0 * LR + nt;
-    dst[0] = v[p].x;
-    dst[LR] = v[p].y;
-    dst[2 * LR] = v[p].z;
-    dst[3 * LR] = v[p].w;
-  }
-  __syncthreads();
-  f32x4 acc[NT];
-#pragma unroll
-  for (int t = 0; t < NT; ++t) acc[t] = f32x4{0.f, 0.f, 0.f, 0.f};
-  const int nc = lane & 15;
-#pragma unroll
-  for (int c = 0; c < KC; ++c) {
-    if (c < kc) {
-#pragma unroll
-      for (int j = 0; j < 4; ++j) {
-        const float av = j == 0 ? a[c].x : j == 1 ? a[c].y : j == 2 ? a[c].z : a[c].w;
-        const float4* brow = reinterpret_cast<const float4*>(s_B + (16 * c + 4 * q + j) * (16 * LR) + nc * LR);
-        float4 bq[NT4 / 4];
-#pragma unroll
-        for (int u = 0; u < NT4 / 4; ++u) bq[u] = brow[u];
-#pragma unroll
-        for (int t = 0; t < NT; ++t) {
-          const float4& b4 = bq[t >> 2];
-          const float bv = (t & 3) == 0 ? b4.x : (t & 3) == 1 ? b4.y : (t & 3) == 2 ? b4.z : b4.w;
-          acc[t] = __builtin_amdgcn_mfma_f32_16x16x4f32(av, bv, acc[t], 0, 0, 0);
-        }
-      }
-    }
-  }
-  // C/D map: reg j -> row 4 (lane >> 4) + j, column lane & 15 of each tile
-#pragma unroll
-  for (int t = 0; t < NT; ++t) {
-    const int64_t n = n0 + 16 * t + nc;
-#pragma unroll
-    for (int j = 0; j < 4; ++j) {
-      const int64_t gm = m0 + 4 * q + j;
-      if (gm < M && n < N) C[gm * ldc + n] = gemm_epi(epi, acc[t][j], gm, n);
-    }
-  }
-}
-
 // Sum split-K slabs in slab order, then apply the epilogue.
 __global__ void gemm_splitk_reduce_kernel(int32_t M, int32_t N, int32_t S, const float* __restrict__ slab,
                                           float* __restrict__ C, int64_t ldc, GemmEpi epi) {
@@ -486,16 +375,6 @@ extern "C" int gcnk_gemm_f32(int32_t transA, int32_t transB, int32_t M, int32_t 
 #undef GCNK_SKINNY_NT
 #undef GCNK_SKINNY_KS
     return launch_check("gemm_skinny_ksplit_kernel");
-  }
-#ifndef GCNK_SHORTK
-#define GCNK_SHORTK 1
-#endif
-  if (GCNK_SHORTK && !ta && !tb && K <= kShortKMax && N > 64 && lda % 4 == 0 && ldb % 4 == 0 && aligned16(A) &&
-      aligned16(B) && split_k == 1) {
-    constexpr int NT = 4;  // 64 columns per workgroup: 28 KB of LDS at K = 112
-    hipLaunchKernelGGL((gemm_shortk_kernel<NT>), dim3((unsigned)((M + 63) / 64), (unsigned)((N + NT * 16 - 1) / (NT * 16))),
-                       dim3(256), 0, s, M, N, K, A, lda, B, ldb, C, ldc, e);
-    return launch_check("gemm_shortk_kernel");
   }
   if (N <= 16) return launch_gemm<4, 1, 2, 1>(ta, tb, M, N, K, A, lda, B, ldb, C, ldc, e, split_k, workspace, s);
   return launch_gemm<2, 2, 2, 2>(ta, tb, M, N, K, A, lda, B, ldb, C, ldc, e, split_k, workspace, s);

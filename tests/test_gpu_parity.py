@@ -383,9 +383,9 @@ def test_csr_transpose_matches_oracle():
 @pytest.mark.parametrize("shape", [(7724, 8, 200), (200, 8, 7724), (7724, 200, 8), (33, 70, 5), (1, 1, 1),
                                    (18916, 200, 100), (7724, 20, 200), (1000, 40, 200), (257, 332, 97)])
 def test_gemm_mfma(ta, tb, shape):
-    """Every GEMM kernel against the float64 oracle: the LDS-tiled MFMA kernel,
-    the skinny-N K-split one (N <= 64: gc2's H1 W2 at 8 and 20 classes) and the
-    short-K one (K <= 128, N > 64: a dense gensim-style X W1)."""
+    """Every GEMM kernel against the float64 oracle: the LDS-tiled MFMA kernel
+    (with transposes; a dense gensim-style X W1 at 18916 x 100 x 200) and the
+    skinny-N K-split one (N <= 64: gc2's H1 W2 at 8, 20 and 40 classes)."""
     M, N, K = shape
     g = torch.Generator().manual_seed(M * 7 + N)
     A = torch.randn((K, M) if ta else (M, K), generator=g)

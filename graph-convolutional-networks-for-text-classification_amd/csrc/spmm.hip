@@ -598,7 +598,7 @@ __global__ void __launch_bounds__(256)
 spmm_tile_kernel(const int4* __restrict__ tdesc, const int32_t* __restrict__ tcols, const float* __restrict__ tfrag,
                  const int32_t* __restrict__ trows, const float* __restrict__ dval, int32_t F,
                  const float* __restrict__ B, int64_t ldb, float* __restrict__ C, int64_t ldc, Epi epi,
-                 float* __restrict__ slabs, int64_t slab_ld, int32_t item0) {
+                 float* __restrict__ slabs, int64_t slab_ld, int32_t item0, int32_t nitems, int32_t nslices) {
   constexpr int NT4 = (NT + 3) & ~3;
   // floats per (k, lane column) row: an odd number of 16-B quads keeps the 16 lanes
   // of a ds_read_b128 group on disjoint bank quads
@@ -609,13 +609,20 @@ spmm_tile_kernel(const int4* __restrict__ tdesc, const int32_t* __restrict__ tco
   const int tid = threadIdx.x;
   const int lane = tid & 63;
   const int wave = tid >> 6;
-  const int64_t item = (int64_t)blockIdx.x + item0;
+  // XCD-aware order: workgroups b and b + 8 share an XCD, so the column slices
+  // of one chunk are placed 8 apart -- they read the same A fragments (and
+  // the same condensed B rows' cache lines) through one L2
+  const int32_t per = 8 * nslices;
+  const int32_t slice = ((int32_t)blockIdx.x % per) / 8;
+  const int32_t it = ((int32_t)blockIdx.x / per) * 8 + ((int32_t)blockIdx.x & 7);
+  if (it >= nitems) return;  // padding of the last group of 8 (whole workgroup)
+  const int64_t item = (int64_t)it + item0;
   stamp(epi, 0);
   // block, nrows | contiguous run length << 8 | width << 16, slab (-1: single chunk), run start
   const int4 d0 = tdesc[item];
   const int32_t run = (d0.y >> 8) & 0xff;
   const int4 d = make_int4(d0.x, d0.y & 0xff, d0.z, d0.w);
-  const int64_t col0 = (int64_t)blockIdx.y * (NT * 16);  // this workgroup's column slice
+  const int64_t col0 = (int64_t)slice * (NT * 16);  // this workgroup's column slice
 
   if (run == 0 && tid < kKC) s_cols[tid] = tcols[item * kKC + tid];
   // output rows, their extracted diagonal and the bias: loads issued now, held
@@ -634,7 +641,7 @@ spmm_tile_kernel(const int4* __restrict__ tdesc, const int32_t* __restrict__ tco
     dv_own = (single && dval) ? dval[(int64_t)d.x * kRB + tid] : 0.f;  // 0 past the block's rows
   }
   {
-    const int64_t c = (int64_t)blockIdx.y * CWP + tid;
+    const int64_t c = (int64_t)slice * CWP + tid;
     if (tid < CWP) bias_own = (single && epi.bias && c < F) ? epi.bias[c] : 0.f;
   }
   // A fragments of this wave: 16 consecutive floats per lane
@@ -977,13 +984,20 @@ struct TileArgs {
 template <bool V4, int NT>
 int launch_tile_nt(unsigned nitems, const TileArgs& t, hipStream_t s) {
   if (nitems == 0) return GCNK_OK;
-  const unsigned slices = (unsigned)((t.F + NT * 16 - 1) / (NT * 16));
+  const int32_t slices = (int32_t)((t.F + NT * 16 - 1) / (NT * 16));
+  const int64_t blocks = ((int64_t)nitems + 7) / 8 * 8 * slices;
+  if (blocks > INT32_MAX) {
+    set_error("spmm_tile_kernel: %lld workgroups exceed the grid", (long long)blocks);
+    return GCNK_EUNSUP;
+  }
   if (t.dval)
-    hipLaunchKernelGGL((spmm_tile_kernel<V4, NT, true>), dim3(nitems, slices), dim3(256), 0, s, t.tdesc, t.tcols,
-                       t.tfrag, t.trows, t.dval, t.F, t.B, t.ldb, t.C, t.ldc, t.epi, t.slabs, t.slab_ld, t.item0);
+    hipLaunchKernelGGL((spmm_tile_kernel<V4, NT, true>), dim3((unsigned)blocks), dim3(256), 0, s, t.tdesc, t.tcols,
+                       t.tfrag, t.trows, t.dval, t.F, t.B, t.ldb, t.C, t.ldc, t.epi, t.slabs, t.slab_ld, t.item0,
+                       (int32_t)nitems, slices);
   else
-    hipLaunchKernelGGL((spmm_tile_kernel<V4, NT, false>), dim3(nitems, slices), dim3(256), 0, s, t.tdesc, t.tcols,
-                       t.tfrag, t.trows, t.dval, t.F, t.B, t.ldb, t.C, t.ldc, t.epi, t.slabs, t.slab_ld, t.item0);
+    hipLaunchKernelGGL((spmm_tile_kernel<V4, NT, false>), dim3((unsigned)blocks), dim3(256), 0, s, t.tdesc, t.tcols,
+                       t.tfrag, t.trows, t.dval, t.F, t.B, t.ldb, t.C, t.ldc, t.epi, t.slabs, t.slab_ld, t.item0,
+                       (int32_t)nitems, slices);
   return launch_check("spmm_tile_kernel");
 }
 

@@ -49,7 +49,10 @@ def main():
     s = s[: used.max() + 1]
     idx = np.arange(len(s))
     t0 = s[used, 0].min()
-    single = (idx % ntile) < nsingle
+    slices = 2                                         # F = 200: 13 n-tiles in slices of <= 8
+    per = 8 * slices
+    item = (idx // per) * 8 + (idx % 8)                # the kernel's XCD-aware workgroup order
+    single = item < nsingle
     res = {"hdr": h, "workgroups": int(len(used)), "span_us": round(float((s[used][:, 1:].max() - t0) / 100), 3)}
     for name, m in (("doc_single", single), ("topic_multi", ~single)):
         a = s[m & (s[:, 0] > 0)]

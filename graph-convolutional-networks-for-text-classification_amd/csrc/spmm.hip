@@ -64,12 +64,16 @@ constexpr int kMaxSeg = 64;             // segments per heavy row (bounds the la
 #define GCNK_LIGHT_RPW 2
 #endif
 #ifndef GCNK_HEAVY_U
-#define GCNK_HEAVY_U 8
+#define GCNK_HEAVY_U 4
 #endif
 #ifndef GCNK_WAVE_BLOCK
 #define GCNK_WAVE_BLOCK 256
 #endif
 constexpr int kHeavyU = GCNK_HEAVY_U;        // gathers in flight per lane in a heavy segment
+#ifndef GCNK_ROW_U
+#define GCNK_ROW_U 8
+#endif
+constexpr int kRowU = GCNK_ROW_U;            // gathers in flight per lane for light rows
 constexpr int kWaveBlock = GCNK_WAVE_BLOCK;  // workgroup size for whole-wavefront groups
 constexpr int kLightRPW = GCNK_LIGHT_RPW;    // light rows per wavefront with whole-wavefront groups
 constexpr int kLightMax64 = 64 / kLightRPW;  // their nonzero limit (kLightRPW rows' items fill one 64-lane load)
@@ -940,13 +944,13 @@ int launch_rows(const RowLaunch& a) {
 template <int VEC>
 int dispatch_rows(int lpr, const RowLaunch& a) {
   switch (lpr) {
-    case 1: return launch_rows<64, 1, VEC, 8, 0>(a);
-    case 2: return launch_rows<64, 2, VEC, 8, 0>(a);
-    case 4: return launch_rows<64, 4, VEC, 8, 0>(a);
-    case 8: return launch_rows<256, 8, VEC, 8, 0>(a);
-    case 16: return launch_rows<256, 16, VEC, 8, 0>(a);
-    case 32: return launch_rows<256, 32, VEC, 8, 0>(a);
-    case 64: return launch_rows<kWaveBlock, 64, VEC, 8, 0>(a);
+    case 1: return launch_rows<64, 1, VEC, kRowU, 0>(a);
+    case 2: return launch_rows<64, 2, VEC, kRowU, 0>(a);
+    case 4: return launch_rows<64, 4, VEC, kRowU, 0>(a);
+    case 8: return launch_rows<256, 8, VEC, kRowU, 0>(a);
+    case 16: return launch_rows<256, 16, VEC, kRowU, 0>(a);
+    case 32: return launch_rows<256, 32, VEC, kRowU, 0>(a);
+    case 64: return launch_rows<kWaveBlock, 64, VEC, kRowU, 0>(a);
   }
   set_error("gcnk_spmm_csr_f32: unsupported lanes per group %d", lpr);
   return GCNK_EUNSUP;

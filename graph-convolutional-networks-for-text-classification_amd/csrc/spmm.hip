@@ -74,6 +74,15 @@ constexpr int kHeavyU = GCNK_HEAVY_U;        // gathers in flight per lane in a 
 #define GCNK_ROW_U 8
 #endif
 constexpr int kRowU = GCNK_ROW_U;            // gathers in flight per lane for light rows
+#ifndef GCNK_NARROW_WG
+#define GCNK_NARROW_WG 1
+#endif
+// Lane groups of 8-32 lanes (256-thread workgroups): a heavy segment spans the
+// whole 4-wavefront workgroup (4x the nonzeros per segment, 4x fewer partials)
+// instead of one wavefront.  R8 A-hat at F = 64: 7.30 -> 6.69 us, F = 32 even.
+// Not for 1-4 lanes (one-wave workgroups spread the light rows over the chip;
+// 256-thread ones measured 5.64 -> 6.14 us at F = 8).
+constexpr bool kNarrowWG = GCNK_NARROW_WG != 0;
 constexpr int kWaveBlock = GCNK_WAVE_BLOCK;  // workgroup size for whole-wavefront groups
 constexpr int kLightRPW = GCNK_LIGHT_RPW;    // light rows per wavefront with whole-wavefront groups
 constexpr int kLightMax64 = 64 / kLightRPW;  // their nonzero limit (kLightRPW rows' items fill one 64-lane load)
@@ -494,13 +503,13 @@ spmm_row_kernel(RowPlan rp, int32_t nhb, const float* __restrict__ B, int64_t ld
   //      unit per workgroup, its WPB wavefronts interleaving the nonzeros and
   //      meeting in LDS.  Either way GS = SW * (LPR == 64 ? WPB : 1) groups
   //      share the segment and every sum has a fixed order.
-  constexpr bool WG = LPR == 64 && WPB > 1;
-  constexpr int GS = WG ? WPB : SW;
+  constexpr bool WG = WPB > 1 && (LPR == 64 || (kNarrowWG && LPR >= 8));
+  constexpr int GS = WG ? SW * WPB : SW;
   __shared__ T s_red[WG ? WPB : 1][64];
   __shared__ int32_t s_last;
   const int lane = tid & 63;
   const int w = tid / 64;
-  const int q = WG ? w : lane / LPR;
+  const int q = WG ? w * SW + lane / LPR : lane / LPR;
   const int32_t u = WG ? (int32_t)blockIdx.x : __builtin_amdgcn_readfirstlane((int32_t)blockIdx.x * WPB + w);
   if (u >= rp.nhunits) return;  // WG: uniform over the workgroup
   const int4 un = rp.units[u];
@@ -508,13 +517,12 @@ spmm_row_kernel(RowPlan rp, int32_t nhb, const float* __restrict__ B, int64_t ld
   stamp(epi, 1);
   if constexpr (LPR == 64) gather_rows_wave<VEC, kHeavyU, GS, O32>(rp.items, un.y, un.z, q, B, ldb, colv, colok, acc);
   else gather_rows<VEC, U, GS, O32>(rp.items, un.y, un.z, q, B, ldb, colv, colok, acc);
+  wave_group_sum<LPR>(acc);  // the wave's SW groups (no-op at LPR = 64)
   if constexpr (WG) {
     if (w > 0) s_red[w][lane] = acc;
     __syncthreads();
 #pragma unroll
     for (int v = 1; v < WPB; ++v) V::add(acc, s_red[v][lane]);  // every wave: same order, same bits
-  } else {
-    wave_group_sum<LPR>(acc);
   }
   stamp(epi, 2);
   if (un.w < 0) {  // the row's only segment
@@ -529,7 +537,7 @@ spmm_row_kernel(RowPlan rp, int32_t nhb, const float* __restrict__ B, int64_t ld
   int32_t* ctr = rp.cnt + (int64_t)hid * kMaxColTiles + blockIdx.y;
   int32_t last = 0;
   // (the unit, hence the slot row, is wave-uniform; lane group 0 stores)
-  if constexpr (WG) {
+  if constexpr (LPR == 64) {
     if (q == 0 && colok) store_coherent_v(uniform_ptr(part + (int64_t)(hv.y + (un.w & 63)) * part_ld), colv, acc);
   } else {
     if (q == 0 && colok) store_coherent(part + (int64_t)(hv.y + (un.w & 63)) * part_ld + colv, acc);
@@ -558,7 +566,7 @@ spmm_row_kernel(RowPlan rp, int32_t nhb, const float* __restrict__ B, int64_t ld
         const int32_t sl = s0 + GS * j;
         // base: the row's first slot (wave-uniform); byte offsets stay below
         // kMaxSeg * part_ld * 4 < 2^31 (checked at launch)
-        if constexpr (WG)
+        if constexpr (LPR == 64)
           pv[j] = sl < hv.z ? load_coherent_v<T>(p0, (int64_t)sl * part_ld + colv) : V::zero();
         else
           pv[j] = sl < hv.z ? load_coherent<T>(p0 + (int64_t)sl * part_ld + colv) : V::zero();
@@ -568,14 +576,13 @@ spmm_row_kernel(RowPlan rp, int32_t nhb, const float* __restrict__ B, int64_t ld
         if (s0 + GS * j < hv.z) V::add(sum, pv[j]);
     }
   }
+  wave_group_sum<LPR>(sum);
   if constexpr (WG) {
     __syncthreads();  // s_red reuse
     if (w > 0) s_red[w][lane] = sum;
     __syncthreads();
 #pragma unroll
     for (int v = 1; v < WPB; ++v) V::add(sum, s_red[v][lane]);
-  } else {
-    wave_group_sum<LPR>(sum);
   }
   if (q == 0) {
     finish_row<LPR, VEC, NP>(sum, hv.x, colv, colok, bv, lg, C, ldc, epi, store_main, proj, pa);
@@ -903,7 +910,8 @@ int launch_rows(const RowLaunch& a) {
   constexpr int SG = BLOCK / LPR, WPB = BLOCK / 64;
   constexpr int LPB = LPR == 64 ? SG * kLightRPW : SG;  // light units per workgroup
   // heavy segments: one per workgroup for whole-wavefront groups, else one per wavefront
-  const int64_t nhb = LPR == 64 ? (int64_t)a.rp.nhunits : ((int64_t)a.rp.nhunits + WPB - 1) / WPB;
+  const int64_t nhb = (LPR == 64 || (kNarrowWG && LPR >= 8 && WPB > 1)) ? (int64_t)a.rp.nhunits
+                                                            : ((int64_t)a.rp.nhunits + WPB - 1) / WPB;
   const int64_t nlb = ((int64_t)a.rp.nunits - a.rp.nhunits + LPB - 1) / LPB;
   if (nhb + nlb == 0) return GCNK_OK;
   if (nhb + nlb > (int64_t)INT32_MAX) {
@@ -1194,8 +1202,9 @@ int host_plan(const int32_t* rp, const int32_t* ci, const float* vv, int32_t M, 
   }
   const int lpr = 64 / groups;
   const int block = choose_block(lpr), wpb = block / 64, sg = block / lpr;
-  const int hpb = lpr == 64 ? 1 : wpb;                     // heavy units per workgroup
-  const int64_t seg = (int64_t)ipc * (lpr == 64 ? wpb : groups);  // nonzeros per heavy segment
+  const bool wg_heavy = lpr == 64 || (kNarrowWG && lpr >= 8 && wpb > 1);  // a heavy segment spans the workgroup
+  const int hpb = wg_heavy ? 1 : wpb;                            // heavy units per workgroup
+  const int64_t seg = (int64_t)ipc * (lpr == 64 ? wpb : groups * (wg_heavy ? wpb : 1));  // nonzeros per segment
   // light-row limit: 2 * ipc for whole-wavefront groups (two light rows share a
   // wavefront, at most kLightMax64 nonzeros each; a heavy row is walked by a
   // 4-wavefront workgroup), ipc otherwise

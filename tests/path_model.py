@@ -20,17 +20,18 @@ def geometry(groups):
     lpr = 64 // groups
     block = 256 if lpr >= 8 else 64
     wpb, sg = block // 64, block // lpr
-    hpb = 1 if lpr == 64 else wpb
-    seg_groups = wpb if lpr == 64 else groups
+    wg_heavy = lpr == 64 or (lpr >= 8 and wpb > 1)   # a heavy segment spans the workgroup
+    hpb = 1 if wg_heavy else wpb
+    seg_groups = wpb if lpr == 64 else groups * (wpb if wg_heavy else 1)
     lpb = 2 * sg if lpr == 64 else sg  # light units per workgroup (two per wavefront at 64 lanes)
-    return hpb, lpb, seg_groups
+    return hpb, lpb, seg_groups, lpr
 
 
 def host_plan(rowptr, colind, K, ipc, groups):
     """-> (units [(row, b, e, w)], heavy [(row, first slot, nseg)], nh, nslots)."""
-    hpb, lpb, seg_groups = geometry(groups)
+    hpb, lpb, seg_groups, lpr = geometry(groups)
     seg = ipc * seg_groups
-    light_max = min(2 * ipc, 32) if hpb == 1 else ipc
+    light_max = min(2 * ipc, 32) if lpr == 64 else ipc
     M = len(rowptr) - 1
     hq, lq, heavy = [[] for _ in range(NX)], [[] for _ in range(NX)], []
     nslots = 0
@@ -91,7 +92,7 @@ def spmm(rowptr, colind, val, B, ipc, groups):
     """C = A @ B computed the way the row kernel schedules it (float64), with
     the per-workgroup XCD class of every unit checked."""
     M, K = len(rowptr) - 1, B.shape[0]
-    hpb, lpb, seg_groups = geometry(groups)
+    hpb, lpb, seg_groups, _ = geometry(groups)
     units, heavy, nh, nslots = host_plan(rowptr, colind, K, ipc, groups)
     C = np.full((M, B.shape[1]), np.nan)
     part = np.zeros((nslots, B.shape[1]))

@@ -605,11 +605,12 @@ spmm_row_kernel(RowPlan rp, int32_t nhb, const float* __restrict__ B, int64_t ld
 typedef float f32x4 __attribute__((ext_vector_type(4)));
 
 template <bool VEC4, int NT, bool DIAG>
-__global__ void __launch_bounds__(256)
-spmm_tile_kernel(const int4* __restrict__ tdesc, const int32_t* __restrict__ tcols, const float* __restrict__ tfrag,
-                 const int32_t* __restrict__ trows, const float* __restrict__ dval, int32_t F,
-                 const float* __restrict__ B, int64_t ldb, float* __restrict__ C, int64_t ldc, Epi epi,
-                 float* __restrict__ slabs, int64_t slab_ld, int32_t item0, int32_t nitems, int32_t nslices) {
+__device__ __forceinline__ void tile_body(int32_t bx, const int4* __restrict__ tdesc, const int32_t* __restrict__ tcols,
+                                          const float* __restrict__ tfrag, const int32_t* __restrict__ trows,
+                                          const float* __restrict__ dval, int32_t F, const float* __restrict__ B,
+                                          int64_t ldb, float* __restrict__ C, int64_t ldc, const Epi& epi,
+                                          float* __restrict__ slabs, int64_t slab_ld, int32_t item0, int32_t nitems,
+                                          int32_t nslices) {
   constexpr int NT4 = (NT + 3) & ~3;
   // floats per (k, lane column) row: an odd number of 16-B quads keeps the 16 lanes
   // of a ds_read_b128 group on disjoint bank quads
@@ -624,8 +625,8 @@ spmm_tile_kernel(const int4* __restrict__ tdesc, const int32_t* __restrict__ tco
   // of one chunk are placed 8 apart -- they read the same A fragments (and
   // the same condensed B rows' cache lines) through one L2
   const int32_t per = 8 * nslices;
-  const int32_t slice = ((int32_t)blockIdx.x % per) / 8;
-  const int32_t it = ((int32_t)blockIdx.x / per) * 8 + ((int32_t)blockIdx.x & 7);
+  const int32_t slice = (bx % per) / 8;
+  const int32_t it = (bx / per) * 8 + (bx & 7);
   if (it >= nitems) return;  // padding of the last group of 8 (whole workgroup)
   const int64_t item = (int64_t)it + item0;
   stamp(epi, 0);
@@ -804,26 +805,37 @@ spmm_tile_kernel(const int4* __restrict__ tdesc, const int32_t* __restrict__ tco
   stamp(epi, 3);
 }
 
+template <bool VEC4, int NT, bool DIAG>
+__global__ void __launch_bounds__(256)
+spmm_tile_kernel(const int4* __restrict__ tdesc, const int32_t* __restrict__ tcols, const float* __restrict__ tfrag,
+                 const int32_t* __restrict__ trows, const float* __restrict__ dval, int32_t F,
+                 const float* __restrict__ B, int64_t ldb, float* __restrict__ C, int64_t ldc, Epi epi,
+                 float* __restrict__ slabs, int64_t slab_ld, int32_t item0, int32_t nitems, int32_t nslices) {
+  tile_body<VEC4, NT, DIAG>((int32_t)blockIdx.x, tdesc, tcols, tfrag, trows, dval, F, B, ldb, C, ldc, epi, slabs,
+                            slab_ld, item0, nitems, nslices);
+}
+
 // Multi-chunk dense blocks: out[row, :] = epi(sum over the block's slabs, in
 // chunk order).  256 threads = 16 slab lanes x 16 float4 column lanes; a
 // workgroup covers one row x 64 columns; slab lanes take slabs strided by 16,
 // then the 16 partial sums are added in lane order through LDS.  The row's
 // reduce entry (row, slabs, diagonal) is the only plan read, so the slab loads
 // (and the diagonal's B row) issue one latency after entry.
-__global__ void __launch_bounds__(256)
-spmm_tile_reduce_kernel(const int4* __restrict__ red, int32_t F, const float* __restrict__ slabs, int64_t slab_ld,
-                        const float* __restrict__ B, int64_t ldb, float* __restrict__ C, int64_t ldc, Epi epi) {
+__device__ __forceinline__ void reduce_body(int32_t bx, int32_t by, int32_t bz, const int4* __restrict__ red,
+                                            int32_t F, const float* __restrict__ slabs, int64_t slab_ld,
+                                            const float* __restrict__ B, int64_t ldb, float* __restrict__ C,
+                                            int64_t ldc, const Epi& epi) {
   __shared__ float4 s_acc[16][16];
-  const int32_t rl = blockIdx.y;  // row within block
+  const int32_t rl = by;  // row within block
   const int sl = threadIdx.x >> 4, c4 = threadIdx.x & 15;
-  const int64_t col = (int64_t)blockIdx.z * 64 + c4 * 4;
+  const int64_t col = (int64_t)bz * 64 + c4 * 4;
   // the bias first: no wait behind the slab loads
   float bcol[4] = {0.f, 0.f, 0.f, 0.f};
   if (sl == 0 && epi.bias)
 #pragma unroll
     for (int i = 0; i < 4; ++i)
       if (col + i < F) bcol[i] = epi.bias[col + i];
-  const int4 rr = red[(int64_t)blockIdx.x * kRB + rl];  // row, first slab, slabs, diagonal bits
+  const int4 rr = red[(int64_t)bx * kRB + rl];  // row, first slab, slabs, diagonal bits
   if (rr.x < 0) return;
   const int64_t row = rr.x;
   const float dv = __int_as_float(rr.w);
@@ -865,6 +877,13 @@ spmm_tile_reduce_kernel(const int4* __restrict__ red, int32_t F, const float* __
     if (dv != 0.f) vals[i] = fmaf(dv, brow[i], vals[i]);
     C[row * ldc + col + i] = apply_epi(epi, vals[i], bcol[i], row, col + i);
   }
+}
+
+__global__ void __launch_bounds__(256)
+spmm_tile_reduce_kernel(const int4* __restrict__ red, int32_t F, const float* __restrict__ slabs, int64_t slab_ld,
+                        const float* __restrict__ B, int64_t ldb, float* __restrict__ C, int64_t ldc, Epi epi) {
+  reduce_body((int32_t)blockIdx.x, (int32_t)blockIdx.y, (int32_t)blockIdx.z, red, F, slabs, slab_ld, B, ldb, C, ldc,
+              epi);
 }
 
 // ---------------------------------------------------------------------------
@@ -1643,10 +1662,11 @@ static int spmm_impl(const void* plan, const int32_t* hdr, const float* B, int64
     const int4* td = reinterpret_cast<const int4*>(p + L.tdesc);
     // part 1: the single-chunk items [0, nsingle); part 2: the rest; 0: all
     const int32_t nsingle = hdr[15];
+    const int nt_need = (nt_total + nslices - 1) / nslices;
     const int32_t i0 = part == 2 ? nsingle : 0, i1 = part == 1 ? nsingle : (int32_t)L.ntile;
     TileArgs ta{td, p + L.tcols, reinterpret_cast<const float*>(p + L.tfrag), p + L.trows, dval, F, B,
                 ldb, C, ldc, e, slabs, slab_ld, i0};
-    const int rc = launch_tile(vec4, (nt_total + nslices - 1) / nslices, (unsigned)(i1 - i0), ta, s);
+    const int rc = launch_tile(vec4, nt_need, (unsigned)(i1 - i0), ta, s);
     if (rc) return rc;
     if (L.nred > 0 && part != 1) {
       hipLaunchKernelGGL(spmm_tile_reduce_kernel, dim3((unsigned)L.nred, kRB, (unsigned)((F + 63) / 64)), dim3(256),

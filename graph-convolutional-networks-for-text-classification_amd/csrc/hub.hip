@@ -103,10 +103,6 @@ hub_light_kernel(const int32_t* __restrict__ recs, int32_t R, const float* __res
   constexpr int SG = BLOCK / LPR;  // lane groups per workgroup
   // staging loads per thread: kHubSmax rows + the zero row of a 64-vector tile
   constexpr int SU = ((kHubSmax + 1) * 64 + BLOCK - 1) / BLOCK;
-#ifndef GCNK_HUB_U
-#define GCNK_HUB_U 8
-#endif
-  constexpr int U = GCNK_HUB_U;    // items per batch
   extern __shared__ __attribute__((aligned(16))) int32_t smem[];
   int32_t* s_rec = smem;
   float* s_stage = reinterpret_cast<float*>(smem + R);
@@ -142,7 +138,6 @@ hub_light_kernel(const int32_t* __restrict__ recs, int32_t R, const float* __res
   constexpr int SW = LPR * VEC;
   constexpr int SWL = __builtin_ctz(SW);
   const int32_t nq = (Fw + VEC - 1) / VEC;
-  const int32_t total = nstage * nq;
   {
     const int32_t ds = BLOCK / nq, dq = BLOCK - ds * nq;
     int32_t s0 = tid / nq, q0 = tid - s0 * nq;

@@ -25,7 +25,10 @@ stream, where the HIP events are recorded): algorithmic bytes (CSR SpMM:
 that rotate over enough distinct B / C sets (> 256 MB) that no launch finds
 its operands in the Infinity Cache; "frac_warm" repeats one set.  Each
 duration includes the dispatch gaps between launches (so it bounds the
-rocprofv3 kernel time from above).  "traffic" is measured live: two child
+rocprofv3 kernel time from above); "roofline_rocprof" gives the same op's
+kernel-only time and fraction from a child rocprofv3 --kernel-trace --stats
+run of the same warm / cold rotations (scripts/hub_probe.py --mode; keep the
+summaries with --rocprof-dir).  "traffic" is measured live: two child
 rocprofv3 --pmc passes (FETCH_SIZE, WRITE_SIZE; FETCH doubled per the gfx950
 correction of MI355X_MICROARCH.md) over scripts/pmc_ops.py, per launch of the
 op's kernels; null if rocprofv3 is unavailable.  "ops" gives the same warm /

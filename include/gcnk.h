@@ -315,7 +315,8 @@ int gcnk_edgelist_csr(const char* path, int64_t n_nodes, int64_t nnz, int32_t* r
  * the generator's state fields (torch's CPU generator state tensor), advanced
  * in place by the 2 n outputs consumed, so writing them back leaves the
  * process's random stream where the reference leaves it.  mask_out[n]: 1 =
- * kept.  `threads` workers temper and compare (the twist chain is serial).
+ * kept.  One pass, one thread (the twist chain is serial); `threads` is
+ * accepted and ignored.
  * ------------------------------------------------------------------------- */
 int gcnk_bernoulli_mt19937(uint32_t* state, int32_t* left, int64_t* next, int64_t n, double p, uint8_t* mask_out,
                            int32_t threads);

@@ -93,6 +93,8 @@ SIGNATURES = {
     "gcnk_edgelist_csr": (ctypes.c_int, [ctypes.c_char_p, _i64, _i64, _vp, _vp, _vp]),
     "gcnk_csr_to_dense": (ctypes.c_int, [_vp, _vp, _vp, _i32, _i32, _vp, _i64, _vp]),
     "gcnk_bernoulli_mt19937": (ctypes.c_int, [_vp, _vp, _vp, _i64, ctypes.c_double, _vp, _i32]),
+    "gcnk_bernoulli_mt19937_start": (ctypes.c_int, [_vp, _vp, _vp, _i64, ctypes.c_double, _vp, _vp]),
+    "gcnk_bernoulli_mt19937_wait": (ctypes.c_int, [_vp]),
     "gcnk_sym_normalize_workspace_bytes": (_i64, [_i32, _i64]),
     "gcnk_sym_normalize": (ctypes.c_int, [_vp, _vp, _vp, _i32, _i64, _vp, _vp, _vp, _vp, _i64, _vp]),
     "gcnk_csr_transpose_workspace_bytes": (_i64, [_i32, _i32, _i64]),

@@ -17,6 +17,7 @@
 #include <cstdint>
 #include <cstring>
 #include <exception>
+#include <thread>
 
 #include "gcnk_common.h"
 
@@ -103,6 +104,60 @@ inline void temper_block(const uint32_t* w, int64_t cnt, uint32_t* t) {
     for (int64_t i = 0; i < cnt; ++i) t[i] = temper(w[i]);
   }
 }
+// The draw proper; arguments already checked.  No allocation, nothing that
+// throws, so it can run on a worker thread (set_error is per thread).
+void draw(uint32_t* state, int32_t* left, int64_t* next, int64_t n, double p, uint8_t* mask_out) {
+  if (n == 0) return;
+  const uint64_t T = (uint64_t)std::ceil(p * 9007199254740992.0);
+  // One pass over the stream: each 624-word state block (the tail of the
+  // current one first, then one per twist) is tempered 8 words at a time and
+  // turned into keep flags straight away; a draw whose two words straddle a
+  // block boundary carries its high word over.  No intermediate buffer: the
+  // twist chain is serial anyway and the flags cost less than a copy of the
+  // stream would.
+  const int64_t words = 2 * n;
+  int32_t lf = *left;
+  int64_t nx = *next;
+  int64_t o = 0, d = 0;
+  bool have_hi = false;
+  uint32_t hi = 0;
+  uint32_t t[kN];
+  while (o < words) {
+    if (lf == 1) {  // torch's operator() decrements `left` first and twists when it reaches 0
+      twist(state);
+      lf = kN + 1;
+      nx = 0;
+    }
+    const int64_t take = std::min<int64_t>(lf - 1, words - o);  // calls before the next twist
+    temper_block(state + nx, take, t);
+    int64_t i = 0;
+    if (have_hi && take > 0) {
+      mask_out[d++] = keep(hi, t[0], T);
+      have_hi = false;
+      i = 1;
+    }
+    for (; i + 1 < take; i += 2) mask_out[d++] = keep(t[i], t[i + 1], T);
+    if (i < take) {
+      hi = t[i];
+      have_hi = true;
+    }
+    o += take;
+    nx += take;
+    lf -= (int32_t)take;
+  }
+  *left = lf;
+  *next = nx;
+}
+
+bool bad_args(const uint32_t* state, const int32_t* left, const int64_t* next, int64_t n, double p,
+              const uint8_t* mask_out) {
+  return !state || !left || !next || n < 0 || (n > 0 && !mask_out) || *left < 1 || *next < 0 || *next > kN ||
+         !(p >= 0.0 && p <= 1.0);
+}
+
+struct Job {
+  std::thread th;
+};
 }  // namespace
 }  // namespace gcnk
 
@@ -114,55 +169,44 @@ using namespace gcnk;
 // chain is serial, and tempering + the keep test run block by block behind it.
 extern "C" int gcnk_bernoulli_mt19937(uint32_t* state, int32_t* left, int64_t* next, int64_t n, double p,
                                       uint8_t* mask_out, int32_t threads) {
-  if (!state || !left || !next || n < 0 || (n > 0 && !mask_out) || *left < 1 || *next < 0 || *next > kN) {
+  (void)threads;
+  if (bad_args(state, left, next, n, p, mask_out)) {
     set_error("gcnk_bernoulli_mt19937: bad argument");
     return GCNK_EARG;
   }
-  if (n == 0) return GCNK_OK;
+  draw(state, left, next, n, p, mask_out);
+  return GCNK_OK;
+}
+
+// The same draw on a native worker thread, so a training loop can draw the
+// next step's mask while the GPU runs this one without any Python thread (and
+// its interpreter-lock hand-offs) in the way.  The buffers must stay alive and
+// untouched until gcnk_bernoulli_mt19937_wait(*job) returns; every started job
+// must be waited for exactly once.
+extern "C" int gcnk_bernoulli_mt19937_start(uint32_t* state, int32_t* left, int64_t* next, int64_t n, double p,
+                                            uint8_t* mask_out, void** job) {
+  if (!job || bad_args(state, left, next, n, p, mask_out)) {
+    set_error("gcnk_bernoulli_mt19937_start: bad argument");
+    return GCNK_EARG;
+  }
   try {
-    const uint64_t T = (uint64_t)std::ceil(p * 9007199254740992.0);
-    // One pass over the stream: each 624-word state block (the tail of the
-    // current one first, then one per twist) is tempered 8 words at a time and
-    // turned into keep flags straight away; a draw whose two words straddle a
-    // block boundary carries its high word over.  No intermediate buffer: the
-    // twist chain is serial anyway and the flags cost less than a copy of the
-    // stream would.
-    const int64_t words = 2 * n;
-    int32_t lf = *left;
-    int64_t nx = *next;
-    int64_t o = 0, d = 0;
-    bool have_hi = false;
-    uint32_t hi = 0;
-    uint32_t t[kN];
-    while (o < words) {
-      if (lf == 1) {  // torch's operator() decrements `left` first and twists when it reaches 0
-        twist(state);
-        lf = kN + 1;
-        nx = 0;
-      }
-      const int64_t take = std::min<int64_t>(lf - 1, words - o);  // calls before the next twist
-      temper_block(state + nx, take, t);
-      int64_t i = 0;
-      if (have_hi && take > 0) {
-        mask_out[d++] = keep(hi, t[0], T);
-        have_hi = false;
-        i = 1;
-      }
-      for (; i + 1 < take; i += 2) mask_out[d++] = keep(t[i], t[i + 1], T);
-      if (i < take) {
-        hi = t[i];
-        have_hi = true;
-      }
-      o += take;
-      nx += take;
-      lf -= (int32_t)take;
-    }
-    *left = lf;
-    *next = nx;
-    (void)threads;
+    Job* j = new Job;
+    j->th = std::thread(draw, state, left, next, n, p, mask_out);
+    *job = j;
     return GCNK_OK;
   } catch (const std::exception& ex) {
-    set_error("gcnk_bernoulli_mt19937: %s", ex.what());
+    set_error("gcnk_bernoulli_mt19937_start: %s", ex.what());
     return GCNK_EUNSUP;
   }
+}
+
+extern "C" int gcnk_bernoulli_mt19937_wait(void* job) {
+  if (!job) {
+    set_error("gcnk_bernoulli_mt19937_wait: null job");
+    return GCNK_EARG;
+  }
+  Job* j = static_cast<Job*>(job);
+  if (j->th.joinable()) j->th.join();
+  delete j;
+  return GCNK_OK;
 }

@@ -23,8 +23,10 @@ Differences by design:
     the device (``_rng_base``, advanced by the forward itself), so a training
     step captured in a hipGraph draws a fresh mask on every replay.
 """
+import ctypes
 import math
 import os
+import threading
 
 import numpy as np
 import torch
@@ -78,28 +80,93 @@ def _mt_self_check():
     return True
 
 
+class _Speculation:
+    """The next mask of the same shape, drawn on a native worker thread
+    (gcnk_bernoulli_mt19937_start) from the generator state the current draw
+    leaves, while the GPU runs the step.  Owns the buffers the worker writes
+    until wait() has joined it."""
+
+    __slots__ = ("key", "before", "after", "out", "_st32", "_lf", "_nx", "_job")
+
+    def __init__(self, key, before, out):
+        self.key, self.before, self.out = key, before, out
+        self.after = before.copy()
+        left, nxt, words = _mt_fields(self.after)
+        self._st32 = np.ascontiguousarray(words, dtype=np.uint32)
+        self._lf = left.copy()
+        self._nx = nxt.copy()
+        job = ctypes.c_void_p()
+        _lib.check(_lib.load().gcnk_bernoulli_mt19937_start(
+            self._st32.ctypes.data, self._lf.ctypes.data, self._nx.ctypes.data, int(out.numel()), float(key[1]),
+            out.data_ptr(), ctypes.byref(job)), "gcnk_bernoulli_mt19937_start")
+        self._job = job
+
+    def wait(self):
+        if self._job is None:
+            return
+        _lib.check(_lib.load().gcnk_bernoulli_mt19937_wait(self._job), "gcnk_bernoulli_mt19937_wait")
+        self._job = None
+        left, nxt, words = _mt_fields(self.after)
+        words[:] = self._st32
+        left[:] = self._lf
+        nxt[:] = self._nx
+
+    def __del__(self):
+        try:
+            self.wait()
+        except Exception:
+            pass
+
+
+_spec = None
+_spec_lock = threading.Lock()
+SPECULATE_MASKS = True
+
+
 def host_keep_mask(shape, p):
     """uint8 keep-mask (1 = kept) of ``torch.empty(shape).bernoulli_(p)`` drawn
     from torch's default CPU generator -- the draw of the reference's CPU
     th.dropout (layer.py:185), bit for bit, with the generator left where that
     call leaves it -- through the native MT19937 restatement
-    (gcnk_bernoulli_mt19937, ~10x faster than torch's serial loop).  Falls back
-    to torch's own bernoulli_ if this torch build's generator state does not
-    match the layout the restatement was checked against."""
-    global _mt_checked
+    (gcnk_bernoulli_mt19937, ~10x faster than torch's serial loop).
+
+    A training loop draws one mask per step and nothing else from the CPU
+    generator in between, so after each draw the next one (same shape and p)
+    is drawn speculatively on a worker thread from the state this draw leaves;
+    the next call uses it only if the generator is still exactly in that state
+    (anything else that drew, or a reseed, discards it), so the stream is
+    unchanged either way.  Falls back to torch's own bernoulli_ if this torch
+    build's generator state does not match the layout the restatement was
+    checked against."""
+    global _mt_checked, _spec
     if _mt_checked is None:
         _mt_checked = _mt_self_check()
     n = 1
     for d in shape:
         n *= int(d)
-    out = torch.empty(shape, dtype=torch.uint8, pin_memory=torch.cuda.is_available())
+    pinned = torch.cuda.is_available()
     if not _mt_checked:
+        out = torch.empty(shape, dtype=torch.uint8, pin_memory=pinned)
         out.copy_(torch.empty(shape, dtype=torch.float32).bernoulli_(p))
         return out
     g = torch.default_generator
     b = g.get_state().numpy().copy()
-    _mt_draw(b, n, p, out.numpy().reshape(-1))
+    key = (tuple(int(d) for d in shape), float(p))
+    with _spec_lock:
+        spec, _spec = _spec, None
+    out = None
+    if spec is not None:
+        spec.wait()
+        if spec.key == key and np.array_equal(spec.before, b):
+            out, b = spec.out, spec.after
+    if out is None:
+        out = torch.empty(shape, dtype=torch.uint8, pin_memory=pinned)
+        _mt_draw(b, n, p, out.numpy().reshape(-1))
     g.set_state(torch.from_numpy(b))
+    if SPECULATE_MASKS:
+        nxt = _Speculation(key, b.copy(), torch.empty(shape, dtype=torch.uint8, pin_memory=pinned))
+        with _spec_lock:
+            _spec = nxt
     return out
 
 

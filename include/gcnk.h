@@ -321,6 +321,14 @@ int gcnk_edgelist_csr(const char* path, int64_t n_nodes, int64_t nnz, int32_t* r
 int gcnk_bernoulli_mt19937(uint32_t* state, int32_t* left, int64_t* next, int64_t n, double p, uint8_t* mask_out,
                            int32_t threads);
 
+/* The same draw on a native worker thread (a training loop draws the next
+ * step's mask while the GPU runs this one).  *job receives a handle; the
+ * buffers must stay alive and untouched until gcnk_bernoulli_mt19937_wait(job)
+ * returns, and every started job is waited for exactly once. */
+int gcnk_bernoulli_mt19937_start(uint32_t* state, int32_t* left, int64_t* next, int64_t n, double p,
+                                 uint8_t* mask_out, void** job);
+int gcnk_bernoulli_mt19937_wait(void* job);
+
 /* Debug only: in a library built with -DGCNK_STAMPS, when `buf` is non-null
  * every later row/tile SpMM launch writes 4 x uint64 s_memrealtime stamps
  * (100 MHz) per workgroup to it (entry, items staged, chunk walked, exit).

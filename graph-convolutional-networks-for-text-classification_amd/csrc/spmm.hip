@@ -134,61 +134,144 @@ struct ProjArgs {
   int32_t store_main;  // also store C (the SpMM output itself)
 };
 
+// v from lane ^ OFF, by the cheapest exchange for the offset: DPP quad
+// permutes (VALU rate) for 1 and 2, ds_swizzle's xor mode (no address VGPR)
+// inside 32 lanes, ds_bpermute across the halves.
+template <int OFF>
+__device__ __forceinline__ float xor_lane(float v) {
+  if constexpr (OFF == 1)
+    return __int_as_float(__builtin_amdgcn_mov_dpp(__float_as_int(v), 0xB1, 0xF, 0xF, false));  // [1,0,3,2]
+  else if constexpr (OFF == 2)
+    return __int_as_float(__builtin_amdgcn_mov_dpp(__float_as_int(v), 0x4E, 0xF, 0xF, false));  // [2,3,0,1]
+  else if constexpr (OFF < 32)
+    return __int_as_float(__builtin_amdgcn_ds_swizzle(__float_as_int(v), (OFF << 10) | 0x1F));
+  else
+    return __shfl_xor(v, OFF, 64);
+}
+
 template <int NP, int LPR, int VPL, int VEC>
 struct Proj {
-  float w[VPL * VEC][NP > 0 ? NP : 1];
-  // W [F x P] is staged through LDS by the whole workgroup with coalesced loads
-  // (a lane's own rows read straight from global memory would make every
-  // wave-instruction touch 64 cache lines), then each lane keeps its columns'
-  // rows in registers.  Called by every thread before any early return.
-  __device__ __forceinline__ void load(const ProjArgs& pa, int32_t F, const int64_t* colv, const bool* colok) {
+  static constexpr int kMaxF = LPR * VPL * VEC;  // one column tile holds the whole row
+  // W [F x P] is staged in LDS once per workgroup with coalesced loads and read
+  // back per finished row (a lane's own W rows straight from global memory
+  // would make every wave-instruction touch 64 cache lines; held in registers
+  // they cost 32 VGPRs for the whole kernel -- 99 VGPRs, 4 waves per SIMD).
+  __device__ __forceinline__ static float* lds() {
+    __shared__ __attribute__((aligned(16))) float s_w[NP > 0 ? kMaxF * NP : 1];
+    return s_w;
+  }
+  int64_t colv;
+  bool colok;
+  __device__ __forceinline__ void init(const int64_t* colv_, const bool* colok_) {
+    colv = *colv_;
+    colok = *colok_;
+  }
+  // W into LDS in two halves, so its loads can be in flight with others:
+  // fetch() loads this thread's share (coalesced) into registers, put() writes
+  // it to LDS; visible to the workgroup after sync().
+  template <int NTHR>
+  static constexpr int per_thread() { return NP > 0 ? (kMaxF * NP + NTHR - 1) / NTHR : 1; }
+  template <int NTHR>
+  __device__ __forceinline__ void fetch(const ProjArgs& pa, int32_t F, float* wv) const {
     if constexpr (NP > 0) {
-      constexpr int kMaxF = LPR * VPL * VEC;  // one column tile holds the whole row
-      __shared__ float s_w[kMaxF * NP];
-      const int nthr = blockDim.x;
-      for (int e = threadIdx.x; e < kMaxF * NP; e += nthr) {
+#pragma unroll
+      for (int j = 0; j < per_thread<NTHR>(); ++j) {
+        const int e = (int)threadIdx.x + j * NTHR;
         const int r = e / NP, c = e % NP;
-        s_w[e] = (r < F && c < pa.P) ? pa.W[(int64_t)r * pa.ldw + c] : 0.f;
+        wv[j] = (e < kMaxF * NP && r < F && c < pa.P) ? pa.W[(int64_t)r * pa.ldw + c] : 0.f;
       }
-      __syncthreads();
-#pragma unroll
-      for (int v = 0; v < VPL; ++v)
-#pragma unroll
-        for (int i = 0; i < VEC; ++i)
-#pragma unroll
-          for (int c = 0; c < NP; ++c) {
-            const int64_t col = colv[v] + i;
-            w[v * VEC + i][c] = (colok[v] && col < F) ? s_w[col * NP + c] : 0.f;
-          }
     }
+  }
+  template <int NTHR>
+  __device__ __forceinline__ void put(const float* wv) const {
+    if constexpr (NP > 0) {
+      float* s_w = lds();
+#pragma unroll
+      for (int j = 0; j < per_thread<NTHR>(); ++j) {
+        const int e = (int)threadIdx.x + j * NTHR;
+        if (e < kMaxF * NP) s_w[e] = wv[j];
+      }
+    }
+  }
+  template <int NTHR>
+  __device__ __forceinline__ void stage(const ProjArgs& pa, int32_t F) {
+    float wv[per_thread<NTHR>()];
+    fetch<NTHR>(pa, F, wv);
+    put<NTHR>(wv);
+    sync();
+  }
+  __device__ __forceinline__ void sync() {
+    if constexpr (NP > 0) __syncthreads();
+  }
+  // W [F x NP] dense and 16-B aligned (the common case: P == NP): the whole
+  // workgroup copies it straight into LDS with global_load_lds (no VGPRs, no
+  // wait until sync(), which drains it), 1 KiB per wave-instruction.
+  __device__ __forceinline__ static bool dma_ok(const ProjArgs& pa) {
+    return NP > 0 && pa.P == NP && pa.ldw == NP && ((uintptr_t)pa.W & 15) == 0;
+  }
+  template <int NTHR>
+  __device__ __forceinline__ void issue_dma(const ProjArgs& pa, int32_t F) const {
+    if constexpr (NP > 0) {
+      float* s_w = lds();
+      const int32_t n = F * NP;                   // floats to copy (<= kMaxF * NP)
+      const int w = (int)threadIdx.x >> 6, l = (int)threadIdx.x & 63;
+#pragma unroll
+      for (int j = 0; j < (kMaxF * NP + NTHR * 4 - 1) / (NTHR * 4); ++j) {
+        const int32_t b = (j * (NTHR / 64) + w) * 256;  // this wave's 1 KiB piece (uniform)
+        if (b < n) {
+          // lanes past the end re-read the first float4 (they land in rows >= F, never read)
+          const int32_t src = b + 4 * l < n ? b + 4 * l : 0;
+          __builtin_amdgcn_global_load_lds(pa.W + src, (__attribute__((address_space(3))) void*)(s_w + b), 16, 0, 0);
+        }
+      }
+    }
+  }
+  template <int NTHR>
+  __device__ __forceinline__ void begin(const ProjArgs& pa, int32_t F) const {
+    if (dma_ok(pa)) issue_dma<NTHR>(pa, F);
+  }
+  template <int NTHR>
+  __device__ __forceinline__ void finish_stage(const ProjArgs& pa, int32_t F) {
+    if (dma_ok(pa)) sync();
+    else stage<NTHR>(pa, F);
   }
   template <typename T>
   __device__ __forceinline__ void apply(const ProjArgs& pa, const T* h, int64_t row, int lg) const {
     if constexpr (NP > 0) {
+      static_assert(NP % 4 == 0, "W rows are read as float4");
+      const float* s_w = lds();
       float s[NP];
 #pragma unroll
       for (int c = 0; c < NP; ++c) s[c] = 0.f;
+      // lanes past F hold h = 0 and read W row 0 (any finite row would do)
+      const int64_t c0 = colok ? colv : 0;
 #pragma unroll
       for (int v = 0; v < VPL; ++v) {
         const float* hv = reinterpret_cast<const float*>(&h[v]);
 #pragma unroll
-        for (int i = 0; i < VEC; ++i)
+        for (int i = 0; i < VEC; ++i) {
+          const float4* wr = reinterpret_cast<const float4*>(s_w + (c0 + v * LPR * VEC + i) * NP);
 #pragma unroll
-          for (int c = 0; c < NP; ++c) s[c] = fmaf(hv[i], w[v * VEC + i][c], s[c]);
+          for (int c4 = 0; c4 < NP / 4; ++c4) {
+            const float4 w4 = wr[c4];
+            s[4 * c4 + 0] = fmaf(hv[i], w4.x, s[4 * c4 + 0]);
+            s[4 * c4 + 1] = fmaf(hv[i], w4.y, s[4 * c4 + 1]);
+            s[4 * c4 + 2] = fmaf(hv[i], w4.z, s[4 * c4 + 2]);
+            s[4 * c4 + 3] = fmaf(hv[i], w4.w, s[4 * c4 + 3]);
+          }
+        }
       }
       // transpose-reduce: while channels remain to split, each xor step sends the
-      // half of the channels the partner keeps (n/2 shuffles instead of n), so a
-      // lane ends with NP/2^h channels summed over 2^h lanes; plain xor steps finish.
+      // half of the channels the partner keeps (n/2 exchanges instead of n), so a
+      // lane ends with NP/2^H channels summed over 2^H lanes; plain xor steps
+      // finish.  Offsets ascend, so the costly cross-half exchange (32) comes
+      // last, on the fewest channels.
       int chan = 0;
-      reduce_split<NP>(s, lg, chan);
+      reduce_split<NP, 1>(s, lg, chan);
       constexpr int H = ilog2(NP) < ilog2(LPR) ? ilog2(NP) : ilog2(LPR);
       constexpr int NR = NP >> H;          // channels left per lane
-      constexpr int REST = LPR >> H;       // lanes still to sum over
-#pragma unroll
-      for (int off = REST / 2; off >= 1; off >>= 1)
-#pragma unroll
-        for (int c = 0; c < NR; ++c) s[c] += __shfl_xor(s[c], off, 64);
-      if ((lg & (REST - 1)) == 0) {
+      tail_sum<NR, (1 << H)>(s);
+      if ((lg >> H) == 0) {
 #pragma unroll
         for (int c = 0; c < NR; ++c)
           if (chan + c < pa.P) pa.C2[row * pa.ldc2 + chan + c] = s[c];
@@ -198,20 +281,30 @@ struct Proj {
 
   static constexpr int ilog2(int x) { return x <= 1 ? 0 : 1 + ilog2(x >> 1); }
 
-  // One halving step per recursion level, offsets LPR/2, LPR/4, ... while n > 1.
-  template <int N, int OFF = LPR / 2>
+  // plain xor steps OFF, 2 OFF, ..., LPR/2 over the NR channels left per lane
+  template <int NR, int OFF>
+  __device__ __forceinline__ static void tail_sum(float* s) {
+    if constexpr (OFF < LPR) {
+#pragma unroll
+      for (int c = 0; c < NR; ++c) s[c] += xor_lane<OFF>(s[c]);
+      tail_sum<NR, OFF * 2>(s);
+    }
+  }
+
+  // One halving step per recursion level, offsets 1, 2, 4, ... while n > 1.
+  template <int N, int OFF>
   __device__ __forceinline__ static void reduce_split(float* s, int lg, int& chan) {
-    if constexpr (N > 1 && OFF >= 1) {
+    if constexpr (N > 1 && OFF < LPR) {
       constexpr int Hn = N / 2;
       const bool up = (lg & OFF) != 0;
 #pragma unroll
       for (int c = 0; c < Hn; ++c) {
         const float keep = up ? s[c + Hn] : s[c];
         const float send = up ? s[c] : s[c + Hn];
-        s[c] = keep + __shfl_xor(send, OFF, 64);
+        s[c] = keep + xor_lane<OFF>(send);
       }
       if (up) chan += Hn;
-      reduce_split<Hn, OFF / 2>(s, lg, chan);
+      reduce_split<Hn, OFF * 2>(s, lg, chan);
     }
   }
 };
@@ -373,11 +466,12 @@ __device__ __forceinline__ void gather_rows_wave(const int2* __restrict__ items,
 // with bitwise the same sum, since each level adds the same two operands).
 template <int LPR, typename T>
 __device__ __forceinline__ void wave_group_sum(T& acc) {
-  float* f = reinterpret_cast<float*>(&acc);
+  if constexpr (LPR < 64) {
+    float* f = reinterpret_cast<float*>(&acc);
 #pragma unroll
-  for (int off = LPR; off < 64; off <<= 1)
-#pragma unroll
-    for (int i = 0; i < (int)(sizeof(T) / 4); ++i) f[i] += __shfl_xor(f[i], off, 64);
+    for (int i = 0; i < (int)(sizeof(T) / 4); ++i) f[i] += xor_lane<LPR>(f[i]);
+    wave_group_sum<LPR * 2>(acc);
+  }
 }
 
 // Epilogue + store (+ fused projection) of one finished row by lane group
@@ -404,7 +498,7 @@ __device__ __forceinline__ void finish_row(const typename Vec<VEC>::T& acc, int3
 // narrower groups would spill): R8's 1832 workgroups then fit one residency
 // round (at 66 VGPRs, 7 per SIMD, 40 of them waited for a second round)
 template <int BLOCK, int LPR, int VEC, int U, int NP, bool O32>
-__global__ void __launch_bounds__(BLOCK) __attribute__((amdgpu_waves_per_eu(NP == 0 && LPR == 64 ? GCNK_ROW_WPE : 1)))
+__global__ void __launch_bounds__(BLOCK) __attribute__((amdgpu_waves_per_eu(LPR == 64 && NP <= 8 ? GCNK_ROW_WPE : 1)))
 spmm_row_kernel(RowPlan rp, int32_t nhb, const float* __restrict__ B, int64_t ldb, int32_t F,
                 float* __restrict__ C, int64_t ldc, Epi epi, float* __restrict__ part, int64_t part_ld,
                 ProjArgs pa) {
@@ -420,7 +514,13 @@ spmm_row_kernel(RowPlan rp, int32_t nhb, const float* __restrict__ B, int64_t ld
   stamp(epi, 0);
   T bv = (epi.bias && colok) ? V::load(epi.bias + colv) : V::zero();
   Proj<NP, LPR, 1, VEC> proj;
-  proj.load(pa, F, &colv, &colok);
+  proj.init(&colv, &colok);
+  // W for the fused projection: narrow groups stage it up front; whole-wavefront
+  // groups only where a row is finished, after the gathers (a heavy segment's
+  // workgroup only if it finishes the row: most store a partial and leave; the
+  // last arriver's W loads fly with its partial loads)
+  if constexpr (LPR < 64) proj.template stage<BLOCK>(pa, F);
+  else if ((int32_t)blockIdx.x >= nhb) proj.template begin<BLOCK>(pa, F);
   const bool store_main = NP == 0 || pa.store_main;
   T acc = V::zero();
 
@@ -435,7 +535,9 @@ spmm_row_kernel(RowPlan rp, int32_t nhb, const float* __restrict__ B, int64_t ld
       constexpr int R = kLightRPW;
       const int32_t u0 = __builtin_amdgcn_readfirstlane(rp.nhunits + ((int32_t)blockIdx.x - nhb) * SG * R +
                                                         (tid / 64) * R);
-      if (u0 >= rp.nunits) return;
+      // (with a projection every wavefront reaches its barrier: past the end all
+      // R units are empty and nothing is gathered or stored)
+      if (NP == 0 && u0 >= rp.nunits) return;
       int4 un[R];
       int32_t nb[R + 1];  // item prefix offsets of the R rows (wave-uniform)
       nb[0] = 0;
@@ -477,6 +579,7 @@ spmm_row_kernel(RowPlan rp, int32_t nhb, const float* __restrict__ B, int64_t ld
             if (j0 + j >= nb[r] && j0 + j < nb[r + 1]) V::fma(accs[r], a[j], g[j]);
       }
       stamp(epi, 2);
+      proj.template finish_stage<BLOCK>(pa, F);
 #pragma unroll
       for (int r = 0; r < R; ++r)
         if (un[r].x >= 0)
@@ -526,6 +629,10 @@ spmm_row_kernel(RowPlan rp, int32_t nhb, const float* __restrict__ B, int64_t ld
   }
   stamp(epi, 2);
   if (un.w < 0) {  // the row's only segment
+    if constexpr (LPR == 64) {  // (workgroup-uniform here)
+      proj.template begin<BLOCK>(pa, F);
+      proj.template finish_stage<BLOCK>(pa, F);
+    }
     if (q == 0) finish_row<LPR, VEC, NP>(acc, un.x, colv, colok, bv, lg, C, ldc, epi, store_main, proj, pa);
     stamp(epi, 3);
     return;
@@ -556,6 +663,7 @@ spmm_row_kernel(RowPlan rp, int32_t nhb, const float* __restrict__ B, int64_t ld
   stamp(epi, 3);
   if (!last) return;
   // group q sums slots q, q + GS, ... (U loads in flight), then the groups meet
+  if constexpr (LPR == 64) proj.template begin<BLOCK>(pa, F);  // in flight with the partial loads
   T sum = V::zero();
   if (colok) {
     const float* p0 = uniform_ptr(part + (int64_t)hv.y * part_ld);
@@ -584,6 +692,7 @@ spmm_row_kernel(RowPlan rp, int32_t nhb, const float* __restrict__ B, int64_t ld
 #pragma unroll
     for (int v = 1; v < WPB; ++v) V::add(sum, s_red[v][lane]);
   }
+  if constexpr (LPR == 64) proj.template finish_stage<BLOCK>(pa, F);  // the last arriver (workgroup-uniform)
   if (q == 0) {
     finish_row<LPR, VEC, NP>(sum, hv.x, colv, colok, bv, lg, C, ldc, epi, store_main, proj, pa);
     if (lane == 0) __hip_atomic_store(ctr, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);

@@ -5,6 +5,7 @@ tensors cross the C-ABI as raw device pointers plus torch's current stream,
 so every op is asynchronous and hipGraph-capturable.
 """
 import ctypes
+import os
 
 import torch
 
@@ -121,11 +122,13 @@ def _side_stream(device):
     return st
 
 
-# Fuse gc2's H1 W2 into the gc1 aggregation epilogue (gcnk_spmm_proj_f32).
-# Off by default: on R8 the fused row kernel (W in registers, 4 waves per SIMD)
-# measured 20.8 us against 11.5 + 3.4 us for the SpMM + K-split GEMM pair
-# (profiles/r01_diag_rows_wg.log).
-FUSE_PROJECTION = False
+# Fuse gc2's H1 W2 into the gc1 aggregation epilogue (gcnk_spmm_proj_f32):
+# one launch fewer, and the eval forward never writes or re-reads H1.  R8
+# (profiles/r02_forward_schedules.log): fused A S1 + H1 W2 11.2 us against
+# 10.1 + 3.4 us for the SpMM + skinny-GEMM pair, forward 36.2 vs 39.1 us.
+# (Round 1's version, W in registers at 4 waves per SIMD, took 20.8 us.)
+# GCNK_FUSE_PROJECTION=0 turns it off (experiments).
+FUSE_PROJECTION = os.environ.get("GCNK_FUSE_PROJECTION", "1") != "0"
 
 
 def spmm_proj(a, B, W, bias=None, epilogue=_lib.EPI_NONE, mask=None, scale=1.0, keep_prob=1.0, seed=0, offset=0,

@@ -1,7 +1,10 @@
 """Warm per-call time (hipGraph of back-to-back launches) of one R8 forward
 op, checked against the float64 oracle.  One JSON line.
 
-  python scripts/op_probe.py --op XW1|AS1|H1W2|AS2 [--reps 200]
+  python scripts/op_probe.py --op XW1|AS1|AS1P|H1W2|AS2 [--reps 200]
+
+AS1P: A S1 + b1, ReLU with H1 W2 fused into the epilogue (ops.spmm_proj, H1
+not stored: the eval forward's schedule under FUSE_PROJECTION).
 """
 import argparse
 import json
@@ -20,7 +23,7 @@ def main():
     import numpy as np
     import torch
     import gcn_amd  # noqa: F401
-    from graph_convolutional_networks_for_text_classification_amd import datasets, ops
+    from graph_convolutional_networks_for_text_classification_amd import _lib, datasets, ops
     from graph_convolutional_networks_for_text_classification_amd.sparse import as_csr
     from oracle import csr_ref
     sys.path.insert(0, os.path.join(ROOT, "scripts"))
@@ -40,6 +43,13 @@ def main():
     elif args.op == "AS1":
         op, B, out = a, S1, torch.empty(r8["nodes"], 200, device=dev)
         fn = lambda: ops.spmm(a, S1, out=out)  # noqa: E731
+    elif args.op == "AS1P":
+        op, B, out = a, S1, torch.empty(r8["nodes"], r8["nclass"], device=dev)
+        b1 = (torch.rand(200, generator=g) - 0.5).to(dev)
+
+        def fn():
+            nonlocal out
+            _, out = ops.spmm_proj(a, S1, W2, bias=b1, epilogue=_lib.EPI_BIAS_RELU, store_main=False)
     elif args.op == "AS2":
         op, B, out = a, S2, torch.empty(r8["nodes"], r8["nclass"], device=dev)
         fn = lambda: ops.spmm(a, S2, out=out)  # noqa: E731
@@ -51,6 +61,8 @@ def main():
     if op is not None:
         rp, ci, v = (t.cpu().numpy() for t in (op.rowptr, op.colind, op.val))
         ref = csr_ref.spmm_csr(rp, ci, v, B.cpu().numpy())
+        if args.op == "AS1P":
+            ref = np.maximum(ref + b1.cpu().double().numpy(), 0.0) @ W2.cpu().double().numpy()
     else:
         ref = S1.cpu().double().numpy() @ W2.cpu().double().numpy()
     err = float(np.abs(out.cpu().double().numpy() - ref).max())

@@ -127,8 +127,12 @@ def _side_stream(device):
 # (profiles/r02_forward_schedules.log): fused A S1 + H1 W2 11.2 us against
 # 10.1 + 3.4 us for the SpMM + skinny-GEMM pair, forward 36.2 vs 39.1 us.
 # (Round 1's version, W in registers at 4 waves per SIMD, took 20.8 us.)
-# GCNK_FUSE_PROJECTION=0 turns it off (experiments).
+# GCNK_FUSE_PROJECTION=0 turns it off (experiments).  Only for gc2 widths up
+# to FUSE_MAX_P: the 20ng-shaped graph's 20 classes take the 32-channel kernel,
+# whose per-row projection costs more than the launch it saves (forward 106 us
+# fused vs 58 us unfused, profiles/r02_variants.log).
 FUSE_PROJECTION = os.environ.get("GCNK_FUSE_PROJECTION", "1") != "0"
+FUSE_MAX_P = 8
 
 
 def spmm_proj(a, B, W, bias=None, epilogue=_lib.EPI_NONE, mask=None, scale=1.0, keep_prob=1.0, seed=0, offset=0,
@@ -345,7 +349,7 @@ class GCNFn(torch.autograd.Function):
     @staticmethod
     def forward(ctx, W1, b1, W2, b2, xop, adj, epi, mask, scale, keep, seed, offset, keep_h1=True, rng_base=None):
         S1 = xop.times(W1)
-        if FUSE_PROJECTION:
+        if FUSE_PROJECTION and W2.shape[1] <= FUSE_MAX_P:
             H1, S2 = spmm_proj(adj, S1, W2, bias=b1, epilogue=epi, mask=mask, scale=scale, keep_prob=keep,
                                seed=seed, offset=offset, store_main=keep_h1, rng_base=rng_base)
         else:

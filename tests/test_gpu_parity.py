@@ -886,3 +886,39 @@ def test_graph_capture_takes_a_prezeroed_counter_region(monkeypatch):
         g.replay()
         torch.cuda.synchronize()
         assert torch.equal(out, ref)
+
+
+def test_tile_path_repeat_streams_and_graph_replay_are_exact(r8):
+    """R8 X W1 on the tile path (single-chunk document blocks, the multi-chunk
+    topic block and its slab reduce): back-to-back calls, two streams at once
+    on one cached plan and graph replays all give the one-call bits, and the
+    product matches the oracle."""
+    from graph_convolutional_networks_for_text_classification_amd import ops
+    x = from_torch(r8["features"].to(DEV))
+    W = torch.randn(r8["nfeat"], 200, generator=torch.Generator().manual_seed(11)).to(DEV)
+    one = ops.spmm(x, W)
+    plan = list(x._plans.values())[-1]
+    assert plan.header[9] > 0, "R8 X's topic rows form a multi-chunk tile block"
+    for _ in range(4):
+        assert torch.equal(ops.spmm(x, W), one)
+    s1, s2 = torch.cuda.Stream(), torch.cuda.Stream()
+    W2 = W * 0.5
+    torch.cuda.synchronize()
+    with torch.cuda.stream(s1):
+        o1 = [ops.spmm(x, W) for _ in range(3)]
+    with torch.cuda.stream(s2):
+        o2 = [ops.spmm(x, W2) for _ in range(3)]
+    torch.cuda.synchronize()
+    half = ops.spmm(x, W2)
+    assert all(torch.equal(o, one) for o in o1) and all(torch.equal(o, half) for o in o2)
+    out = torch.empty_like(one)
+    g = torch.cuda.CUDAGraph()
+    with torch.cuda.graph(g):
+        ops.spmm(x, W, out=out)
+    for _ in range(3):
+        out.zero_()
+        g.replay()
+        torch.cuda.synchronize()
+        assert torch.equal(out, one)
+    rp, ci, v = (t.cpu().numpy() for t in (x.rowptr, x.colind, x.val))
+    _close(one, csr_ref.spmm_csr(rp, ci, v, W.cpu().numpy()), atol=1e-4)

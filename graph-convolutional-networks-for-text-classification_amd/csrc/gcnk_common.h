@@ -43,8 +43,17 @@ struct Epi {
 };
 
 // Debug timeline: 4 x s_memrealtime (100 MHz) per workgroup, written by thread 0.
+// Compiled in only with -DGCNK_STAMPS (scripts/stamps.py): the runtime branch
+// and its store would otherwise sit in every kernel, and the store's vmcnt
+// makes the compiler's waits after it conservative.
 __device__ __forceinline__ void stamp(const Epi& e, int k) {
+#ifndef GCNK_STAMPS
+  (void)e;
+  (void)k;
+  if (false) {
+#else
   if (e.stamps && threadIdx.x == 0) {
+#endif
     const unsigned long long t = __builtin_amdgcn_s_memrealtime();
     e.stamps[4 * ((unsigned long long)blockIdx.y * gridDim.x + blockIdx.x) + k] = t;
   }

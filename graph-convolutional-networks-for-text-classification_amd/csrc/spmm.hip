@@ -40,6 +40,7 @@
 
 #include <algorithm>
 #include <climits>
+#include <type_traits>
 #include <vector>
 
 namespace gcnk {
@@ -65,6 +66,10 @@ constexpr int kMaxSeg = 64;             // segments per heavy row (bounds the la
 // 13.2 -> 11.4 us in the forward, forward 36.4 -> 34.7 us).
 #ifndef GCNK_TILE_SC1
 #define GCNK_TILE_SC1 1
+#endif
+// Tile kernel: LDS writes / MFMA k-steps in this many phases (tile_body)
+#ifndef GCNK_TILE_PHASES
+#define GCNK_TILE_PHASES 2
 #endif
 #ifndef GCNK_ROW_SC1
 #define GCNK_ROW_SC1 0
@@ -792,6 +797,8 @@ __device__ __forceinline__ void tile_body(int32_t bx, const int4* __restrict__ t
   constexpr int nq = NT * 4;  // float4 per staged row
   constexpr int PT = (kKC * nq + 255) / 256;
   float4 v[PT];
+  uint32_t okm = 0;  // VEC4: loads whose piece is real
+  static_assert(PT <= 32, "one mask bit per load");
   auto fetch = [&](bool contiguous) {
 #pragma unroll
     for (int p = 0; p < PT; ++p) {
@@ -799,12 +806,19 @@ __device__ __forceinline__ void tile_body(int32_t bx, const int4* __restrict__ t
       const int k = q / nq, c4 = q % nq;
       const int32_t src = q < kKC * nq ? (contiguous ? (k < run ? d.w + k : -1) : s_cols[k]) : -1;
       const int64_t col = col0 + c4 * 4;
+      if constexpr (VEC4) {
+        // branch-free, so the loads form one straight run and each phase below
+        // waits only for its own; an invalid piece reads B[0, 0..3] and is
+        // zeroed when it is written to LDS
+        const bool ok = src >= 0 && col < F;
+        v[p] = *reinterpret_cast<const float4*>(B + (ok ? (int64_t)src * ldb + col : 0));
+        okm |= (uint32_t)ok << p;
+        continue;
+      }
       v[p] = make_float4(0.f, 0.f, 0.f, 0.f);
       if (src >= 0) {
         const float* bp = B + (int64_t)src * ldb + col;
-        if (VEC4) {
-          if (col < F) v[p] = *reinterpret_cast<const float4*>(bp);
-        } else {
+        {
           if (col + 0 < F) v[p].x = bp[0];
           if (col + 1 < F) v[p].y = bp[1];
           if (col + 2 < F) v[p].z = bp[2];
@@ -813,49 +827,78 @@ __device__ __forceinline__ void tile_body(int32_t bx, const int4* __restrict__ t
       }
     }
   };
-  if (run > 0) {
-    fetch(true);
-  } else {
-    __syncthreads();  // s_cols
-    fetch(false);
-  }
-#pragma unroll
-  for (int p = 0; p < PT; ++p) {
+  // ---- LDS writes and MFMA k-steps in NPH phases: phase h writes the staged
+  //      values of loads [p0, p1) -- the compiler waits only for those (a
+  //      wave's loads return in issue order) -- then runs the k-steps whose rows
+  //      they complete, so the MFMAs of the first rows overlap the arrival of
+  //      the last ones instead of following the whole staging.
+  auto put = [&](int p) {
     const int q = tid + p * 256;
-    if (q >= kKC * nq) break;
+    if (q >= kKC * nq) return;
     const int k = q / nq, c4 = q % nq;
     const int n = c4 * 4, nt = n >> 4, nc0 = n & 15;
     float* dst = s_B + k * stride + nc0 * LR + nt;
-    dst[0] = v[p].x;
-    dst[LR] = v[p].y;
-    dst[2 * LR] = v[p].z;
-    dst[3 * LR] = v[p].w;
-  }
-  __syncthreads();
-  stamp(epi, 1);
-
+    const bool ok = !VEC4 || ((okm >> p) & 1);
+    dst[0] = ok ? v[p].x : 0.f;
+    dst[LR] = ok ? v[p].y : 0.f;
+    dst[2 * LR] = ok ? v[p].z : 0.f;
+    dst[3 * LR] = ok ? v[p].w : 0.f;
+  };
   f32x4 acc[NT];
 #pragma unroll
   for (int nt = 0; nt < NT; ++nt) acc[nt] = f32x4{0.f, 0.f, 0.f, 0.f};
   const float a[16] = {a0.x, a0.y, a0.z, a0.w, a1.x, a1.y, a1.z, a1.w,
                        a2.x, a2.y, a2.z, a2.w, a3.x, a3.y, a3.z, a3.w};
   const int kr = lane >> 4, nc = lane & 15;
-#pragma unroll
   // all 16 k-steps, padding included: skipping the zero steps of narrow chunks
   // (R8 X's 50-column document blocks: 13 of 16) measured no faster (10.70 vs
   // 10.75 us) and, written as a guarded unrolled loop, slower (12.98 us)
-  for (int s = 0; s < 16; ++s) {
-    const float4* brow = reinterpret_cast<const float4*>(s_B + (4 * s + kr) * stride + nc * LR);
-    float4 bq[NT4 / 4];
+  auto ksteps = [&](auto s0c, auto s1c) {
 #pragma unroll
-    for (int q = 0; q < NT4 / 4; ++q) bq[q] = brow[q];
+    for (int s = decltype(s0c)::value; s < decltype(s1c)::value; ++s) {
+      const float4* brow = reinterpret_cast<const float4*>(s_B + (4 * s + kr) * stride + nc * LR);
+      float4 bq[NT4 / 4];
 #pragma unroll
-    for (int nt = 0; nt < NT; ++nt) {
-      const float4& b4 = bq[nt >> 2];
-      const float bval = (nt & 3) == 0 ? b4.x : (nt & 3) == 1 ? b4.y : (nt & 3) == 2 ? b4.z : b4.w;
-      acc[nt] = __builtin_amdgcn_mfma_f32_16x16x4f32(a[s], bval, acc[nt], 0, 0, 0);
+      for (int q = 0; q < NT4 / 4; ++q) bq[q] = brow[q];
+#pragma unroll
+      for (int nt = 0; nt < NT; ++nt) {
+        const float4& b4 = bq[nt >> 2];
+        const float bval = (nt & 3) == 0 ? b4.x : (nt & 3) == 1 ? b4.y : (nt & 3) == 2 ? b4.z : b4.w;
+        acc[nt] = __builtin_amdgcn_mfma_f32_16x16x4f32(a[s], bval, acc[nt], 0, 0, 0);
+      }
     }
-  }
+  };
+  constexpr int NPH = GCNK_TILE_PHASES;
+  static_assert(NPH == 1 || NPH == 2 || NPH == 4, "k-step phases");
+  // loads [0, pend(h)) hold every staged row below 64 (h + 1) / NPH
+  auto phase = [&](auto hc) {
+    constexpr int h = decltype(hc)::value;
+    constexpr int p0 = h == 0 ? 0 : (h == NPH ? PT : (kKC * h / NPH * nq + 255) / 256);
+    constexpr int p1 = h + 1 == NPH ? PT : (kKC * (h + 1) / NPH * nq + 255) / 256;
+#pragma unroll
+    for (int p = p0 < PT ? p0 : PT; p < (p1 < PT ? p1 : PT); ++p) put(p);
+    __syncthreads();
+    if (h == 0) stamp(epi, 1);
+    ksteps(std::integral_constant<int, 16 * h / NPH>{}, std::integral_constant<int, 16 * (h + 1) / NPH>{});
+  };
+  // the two staging paths stay apart up to the last MFMA: where they merged
+  // the compiler's wait before the first k-steps fell back to (almost) all loads
+  auto stage_and_multiply = [&](auto contiguous) {
+    if constexpr (decltype(contiguous)::value) {
+      fetch(true);
+    } else {
+      __syncthreads();  // s_cols
+      fetch(false);
+    }
+    phase(std::integral_constant<int, 0>{});
+    if constexpr (NPH > 1) phase(std::integral_constant<int, 1>{});
+    if constexpr (NPH > 2) {
+      phase(std::integral_constant<int, 2>{});
+      phase(std::integral_constant<int, 3>{});
+    }
+  };
+  if (run > 0) stage_and_multiply(std::true_type{});
+  else stage_and_multiply(std::false_type{});
 
   stamp(epi, 2);
   // ---- output through LDS: the accumulators (C/D layout: block row 16*wave +

@@ -18,17 +18,18 @@ ms_per_step = GCN-forward ms.  N > 1: the R8 graph does not shard (SURVEY
 §8(e)): N independent replicas, "scaling": "weak".
 
 roofline (the north-star op, BASELINE.json: R8 doc-topic SpMM Â·S1 at hidden
-200 with gc1's bias + ReLU fused; its kernels are launched on torch's current
-stream, where the HIP events are recorded): algorithmic bytes (CSR SpMM:
-4(M+1) + 8 nnz + 4 K F + 4 M F = 12.94 MB) over the op's average duration.
-"frac" is the COLD figure: a hipGraph of back-to-back launches
-that rotate over enough distinct B / C sets (> 256 MB) that no launch finds
-its operands in the Infinity Cache; "frac_warm" repeats one set.  Each
-duration includes the dispatch gaps between launches (so it bounds the
-rocprofv3 kernel time from above); "roofline_rocprof" gives the same op's
-kernel-only time and fraction from a child rocprofv3 --kernel-trace --stats
-run of the same warm / cold rotations (scripts/hub_probe.py --mode; keep the
-summaries with --rocprof-dir).  "traffic" is measured live: two child
+200 with gc1's bias + ReLU fused): algorithmic bytes (CSR SpMM:
+4(M+1) + 8 nnz + 4 K F + 4 M F = 12.94 MB) over the kernel's average duration.
+"frac" is the COLD figure: back-to-back launches that rotate
+over enough distinct B / C sets (> 256 MB) that no launch finds its operands
+in the Infinity Cache; "frac_warm" repeats one set.  The duration is the
+kernel time of a child rocprofv3 --kernel-trace --stats run of those
+rotations (scripts/hub_probe.py --mode; keep the summaries with
+--rocprof-dir), so "frac" follows from the committed rocprof summary;
+"hip_events" holds the same rotations timed with HIP events on the launching
+stream (per call, hipGraph) -- those also hold the ~1.5-2 us dispatch gap
+between launches.  Without rocprofv3 the HIP-event figure is used
+("duration_source" says which).  "traffic" is measured live: two child
 rocprofv3 --pmc passes (FETCH_SIZE, WRITE_SIZE; FETCH doubled per the gfx950
 correction of MI355X_MICROARCH.md) over scripts/pmc_ops.py, per launch of the
 op's kernels; null if rocprofv3 is unavailable.  "ops" gives the same warm /
@@ -81,6 +82,8 @@ def parse():
     ap.add_argument("--no-configs", action="store_true", help="skip BASELINE configs 3 and 4")
     ap.add_argument("--no-rocprof", action="store_true", help="skip the child rocprofv3 kernel-trace runs")
     ap.add_argument("--rocprof-dir", default=None, help="keep the child kernel-trace summaries here")
+    ap.add_argument("--config5", action="store_true",
+                    help="run the config-5 column-sharded leg even on one rank (it runs by default when N > 1)")
     return ap.parse_args()
 
 
@@ -205,6 +208,67 @@ def rocprof_kernel_us(mode, kernels_like, save_dir=None):
         return None, f"kernel trace failed: {e}"
     finally:
         shutil.rmtree(tmp, ignore_errors=True)
+
+
+def sharded_config5(dev, world, rank, datasets, ops, F=4096, reps=3):
+    """BASELINE config 5 on this job's ranks: the replicated 1M / 20M CSR, this
+    rank's F / P columns of B, the local SpMM and the all-gather of the result
+    (times are the max over ranks of the per-rep medians)."""
+    import torch
+    import torch.distributed as dist
+    from graph_convolutional_networks_for_text_classification_amd.parallel import ColumnShardedSpMM
+    from graph_convolutional_networks_for_text_classification_amd.sparse import CSR
+    n, nnz = 1_000_000, 20_000_000
+    err = None
+    try:   # setup; every rank learns whether all ranks got through before any timed collective
+        rp, ci, v = datasets.uniform_random_csr(n, nnz, seed=0, device=dev)
+        a = CSR(rp, ci, v, (n, n))
+        cs = ColumnShardedSpMM(a, F)
+        c0, c1 = cs.columns
+        g = torch.Generator(device=dev).manual_seed(1000 + rank)
+        Bp = torch.randn((n, c1 - c0), generator=g, device=dev)
+        blk = cs.local(Bp)           # plan build, untimed
+        torch.cuda.synchronize()
+        del blk
+    except (RuntimeError, MemoryError) as e:
+        err = str(e)[:300]
+    ok = torch.tensor([0 if err else 1], dtype=torch.int32, device=dev)
+    if world > 1:
+        dist.all_reduce(ok, op=dist.ReduceOp.MIN)
+    if int(ok) == 0:
+        return {"error": err or "another rank failed its setup"}
+    try:
+        cs.gather(cs.local(Bp))      # first all-gather, untimed
+        torch.cuda.synchronize()
+        t_loc, t_tot = [], []
+        for _ in range(reps):
+            if world > 1:
+                dist.barrier()
+            torch.cuda.synchronize()
+            t0 = time.perf_counter()
+            blk = cs.local(Bp)
+            torch.cuda.synchronize()
+            t1 = time.perf_counter()
+            out = cs.gather(blk)
+            torch.cuda.synchronize()
+            t2 = time.perf_counter()
+            t_loc.append(t1 - t0)
+            t_tot.append(t2 - t0)
+            del blk, out
+        t = torch.tensor([sorted(t_loc)[reps // 2], sorted(t_tot)[reps // 2]], dtype=torch.float64, device=dev)
+        if world > 1:
+            dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        loc, tot = float(t[0]), float(t[1])
+        res = {"nodes": n, "nnz": a.nnz, "F": F, "ranks": world, "columns_per_rank": cs.width,
+               "ms_local_spmm": round(loc * 1e3, 3), "ms_all_gather": round((tot - loc) * 1e3, 3),
+               "ms_total": round(tot * 1e3, 3), "edges_per_s": a.nnz / tot,
+               "gflops": 2 * a.nnz * F / tot / 1e9, "gathered_bytes_per_rank": 4 * n * cs.width * world,
+               "scaling": "strong", "collective": "RCCL all_gather_into_tensor" if world > 1 else "none (1 rank)"}
+        del a, Bp, rp, ci, v
+        torch.cuda.empty_cache()
+        return res
+    except (RuntimeError, MemoryError) as e:   # reported, never fatal to the bench line
+        return {"error": str(e)[:300]}
 
 
 def main():
@@ -445,9 +509,34 @@ def main():
         del big, Bb, Cb, rp, ci, v
         torch.cuda.empty_cache()
 
+    # ---- BASELINE config 5 (N > 1): 1M nodes / 20M edges, F = 4096 feature
+    #      columns sharded over the ranks (parallel.ColumnShardedSpMM: local
+    #      SpMM, then one RCCL all-gather of the [M, F/P] blocks over xGMI);
+    #      total work fixed ("strong"), max over ranks
+    config5 = None
+    if (world > 1 or args.config5) and not args.no_configs:
+        config5 = sharded_config5(dev, world, rank, datasets, ops)
+
     ms = elapsed / args.steps * 1e3
     value = 2 * nnz_a * args.steps * world / elapsed
     kn, kd = optimes[north], optimes[dom]
+    # the north-star kernel's average launch duration: the cold rocprofv3 kernel
+    # time of the child run (so "frac" follows from the committed rocprof
+    # summary); the HIP-event per-call figure, which also holds the dispatch gap
+    # between back-to-back launches (~1.5-2 us), beside it
+    nb = kn["algorithmic_bytes"]
+    kcold, kwarm = kt.get("cold", (None, "")), kt.get("warm", (None, ""))
+    dur, dur_w, src = kn["cold_us"], kn["warm_us"], "HIP events per call (hipGraph of back-to-back launches)"
+    if kcold[0] is not None and kwarm[0] is not None:
+        dur, dur_w, src = kcold[0], kwarm[0], kcold[1]
+    roof = {"bound": "hbm", "kernel": north, "plan": plan_kinds[north],
+            "achieved": nb / (dur * 1e-6) / 1e9, "peak": HBM_PEAK_GBS, "unit": "GB/s",
+            "frac": nb / (dur * 1e-6) / 1e9 / HBM_PEAK_GBS, "frac_warm": nb / (dur_w * 1e-6) / 1e9 / HBM_PEAK_GBS,
+            "traffic": traffic, "traffic_source": traffic_src,
+            "avg_launch_us": round(dur, 3), "avg_launch_us_warm": round(dur_w, 3), "duration_source": src,
+            "hip_events": {"avg_call_us": kn["cold_us"], "avg_call_us_warm": kn["warm_us"],
+                           "frac": kn["frac_cold"], "frac_warm": kn["frac_warm"]},
+            "algorithmic_bytes": nb}
     line = {
         "metric": "SpMM edges/s and GCN-forward ms on R8 doc-topic graph, 1×MI355X",
         "value": value,
@@ -465,12 +554,7 @@ def main():
                    "nodes": N, "adj_nnz": nnz_a, "x_nnz": nnz_x, "graph": not args.no_graph,
                    "forwards_per_graph": per,
                    "parallelism": f"replicas{world}" if world > 1 else "single"},
-        "roofline": {"bound": "hbm", "kernel": north, "plan": plan_kinds[north],
-                     "achieved": kn["algorithmic_bytes"] / (kn["cold_us"] * 1e-6) / 1e9, "peak": HBM_PEAK_GBS,
-                     "unit": "GB/s", "frac": kn["frac_cold"], "frac_warm": kn["frac_warm"],
-                     "traffic": traffic, "traffic_source": traffic_src,
-                     "avg_launch_us": kn["cold_us"], "avg_launch_us_warm": kn["warm_us"],
-                     "algorithmic_bytes": kn["algorithmic_bytes"]},
+        "roofline": roof,
         # the same op under rocprofv3: kernel time without the dispatch gap that the
         # per-call HIP-event figure above includes
         "roofline_rocprof": {m: ({"kernel_us": round(v[0], 3),
@@ -484,6 +568,7 @@ def main():
         "cpu_stock_csr": cpu_stock,
         "gpu_stock": gpu_stock,
         "configs": configs,
+        "config5_column_sharded": config5,
     }
     if rank == 0:
         print(json.dumps(line))

@@ -134,6 +134,37 @@ struct Layout {
   }
 };
 
+// Coherent (sc1) raw-buffer accesses from a wave-uniform base (see RowPlan).
+typedef float f32v4 __attribute__((ext_vector_type(4)));
+constexpr int kBufSc1 = 16;               // cache-policy aux bit sc1 (gfx94x/gfx950)
+constexpr int kBufDword3 = 0x00020000;    // raw buffer resource word 3 (gfx9)
+__device__ __forceinline__ __amdgpu_buffer_rsrc_t row_rsrc(const float* base_uniform) {
+  return __builtin_amdgcn_make_buffer_rsrc(const_cast<float*>(base_uniform), (short)0, 0x7fffffff, kBufDword3);
+}
+__device__ __forceinline__ void store_coherent_v(const float* base_uniform, int64_t off, const float4& v) {
+  const f32v4 x = {v.x, v.y, v.z, v.w};
+  __builtin_amdgcn_raw_buffer_store_b128(x, row_rsrc(base_uniform), (int)(off * 4), 0, kBufSc1);
+}
+__device__ __forceinline__ void store_coherent_v(const float* base_uniform, int64_t off, const float& v) {
+  __builtin_amdgcn_raw_buffer_store_b32(__float_as_uint(v), row_rsrc(base_uniform), (int)(off * 4), 0, kBufSc1);
+}
+template <typename T>
+__device__ __forceinline__ T load_coherent_v(const float* base_uniform, int64_t off);
+template <>
+__device__ __forceinline__ float4 load_coherent_v<float4>(const float* base_uniform, int64_t off) {
+  const f32v4 x = __builtin_amdgcn_raw_buffer_load_b128(row_rsrc(base_uniform), (int)(off * 4), 0, kBufSc1);
+  return make_float4(x.x, x.y, x.z, x.w);
+}
+template <>
+__device__ __forceinline__ float load_coherent_v<float>(const float* base_uniform, int64_t off) {
+  return __uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(row_rsrc(base_uniform), (int)(off * 4), 0, kBufSc1));
+}
+__device__ __forceinline__ const float* uniform_ptr(const float* p) {
+  const uint64_t u = reinterpret_cast<uint64_t>(p);
+  const uint32_t lo = __builtin_amdgcn_readfirstlane((uint32_t)u), hi = __builtin_amdgcn_readfirstlane((uint32_t)(u >> 32));
+  return reinterpret_cast<const float*>(((uint64_t)hi << 32) | lo);
+}
+
 // ---------------------------------------------------------------------------
 // Fused dense projection of a finished row: C2[row, :P] = h[row, :F] * W[F, P]
 // (the gc2 support H1 W2 of reference layer.py:102, computed while H1's row
@@ -288,7 +319,15 @@ struct Proj {
       if ((lg >> H) == 0) {
 #pragma unroll
         for (int c = 0; c < NR; ++c)
-          if (chan + c < pa.P) pa.C2[row * pa.ldc2 + chan + c] = s[c];
+          if (chan + c < pa.P) {
+#if GCNK_ROW_SC1
+            const int64_t off = row * pa.ldc2 + chan + c;
+            if (off < ((int64_t)1 << 29)) store_coherent_v(pa.C2, off, s[c]);  // C2: kernel argument (uniform)
+            else pa.C2[off] = s[c];
+#else
+            pa.C2[row * pa.ldc2 + chan + c] = s[c];
+#endif
+          }
       }
     }
   }
@@ -365,35 +404,6 @@ __device__ __forceinline__ T load_coherent(const float* p) {
   for (int i = 0; i < (int)(sizeof(T) / 4); ++i)
     f[i] = __hip_atomic_load(const_cast<float*>(p + i), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
   return v;
-}
-typedef float f32v4 __attribute__((ext_vector_type(4)));
-constexpr int kBufSc1 = 16;               // cache-policy aux bit sc1 (gfx94x/gfx950)
-constexpr int kBufDword3 = 0x00020000;    // raw buffer resource word 3 (gfx9)
-__device__ __forceinline__ __amdgpu_buffer_rsrc_t row_rsrc(const float* base_uniform) {
-  return __builtin_amdgcn_make_buffer_rsrc(const_cast<float*>(base_uniform), (short)0, 0x7fffffff, kBufDword3);
-}
-__device__ __forceinline__ void store_coherent_v(const float* base_uniform, int64_t off, const float4& v) {
-  const f32v4 x = {v.x, v.y, v.z, v.w};
-  __builtin_amdgcn_raw_buffer_store_b128(x, row_rsrc(base_uniform), (int)(off * 4), 0, kBufSc1);
-}
-__device__ __forceinline__ void store_coherent_v(const float* base_uniform, int64_t off, const float& v) {
-  __builtin_amdgcn_raw_buffer_store_b32(__float_as_uint(v), row_rsrc(base_uniform), (int)(off * 4), 0, kBufSc1);
-}
-template <typename T>
-__device__ __forceinline__ T load_coherent_v(const float* base_uniform, int64_t off);
-template <>
-__device__ __forceinline__ float4 load_coherent_v<float4>(const float* base_uniform, int64_t off) {
-  const f32v4 x = __builtin_amdgcn_raw_buffer_load_b128(row_rsrc(base_uniform), (int)(off * 4), 0, kBufSc1);
-  return make_float4(x.x, x.y, x.z, x.w);
-}
-template <>
-__device__ __forceinline__ float load_coherent_v<float>(const float* base_uniform, int64_t off) {
-  return __uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(row_rsrc(base_uniform), (int)(off * 4), 0, kBufSc1));
-}
-__device__ __forceinline__ const float* uniform_ptr(const float* p) {
-  const uint64_t u = reinterpret_cast<uint64_t>(p);
-  const uint32_t lo = __builtin_amdgcn_readfirstlane((uint32_t)u), hi = __builtin_amdgcn_readfirstlane((uint32_t)(u >> 32));
-  return reinterpret_cast<const float*>(((uint64_t)hi << 32) | lo);
 }
 
 // B[c, col..] (VEC floats).  O32: through a 32-bit byte offset from the

@@ -223,6 +223,86 @@ gemm_skinny_ksplit_kernel(int32_t M, int32_t N, int32_t K, const float* __restri
   }
 }
 
+// Short-K, wide-N GEMM (NN; K <= 16 * KCH, K % 4 == 0, N % 4 == 0, A and B
+// rows 16-B aligned): C = epi(A B) for a dense gensim-style X W1 ([nodes x
+// 100] x [100 x 200]: the 20ng-shaped graph, R8 with 100-d features), where
+// the tiled kernel above spends its time in 7 barrier-separated k tiles of a
+// 64 x 64 tile.  One workgroup = 64 rows x 7 n-tiles (112 columns): its B
+// slice [K x 112] is staged in LDS ONCE (float4 copies, rows padded to 116
+// floats), all of it in flight with the A loads, and each wave multiplies its
+// 16 rows by it with no further barrier: lane l holds A[row l&15][16c +
+// 4(l>>4) .. +3] for every 16-deep k chunk c (the k order inside a chunk is
+// permuted the same way for A and B, as in the skinny kernel) and runs
+// 4 * KCH k-steps over 7 independent accumulators.
+template <int KCH>
+__global__ void __launch_bounds__(256)
+gemm_shortk_kernel(int32_t M, int32_t N, int32_t K, const float* __restrict__ A, int64_t lda,
+                   const float* __restrict__ B, int64_t ldb, float* __restrict__ C, int64_t ldc, GemmEpi epi) {
+  constexpr int NT = 7, BN = 16 * NT, LW = BN + 4, KP = 16 * KCH, NQ = BN / 4;
+  constexpr int PT = (KP * NQ + 255) / 256;
+  __shared__ __attribute__((aligned(16))) float s_B[KP * LW];
+  const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
+  const int r = lane & 15, q = lane >> 4;
+  const int64_t m0 = (int64_t)blockIdx.x * 64 + 16 * w;
+  const int64_t n0 = (int64_t)blockIdx.y * BN;
+  const int64_t row = m0 + r;
+  const bool rok = row < M;
+  // every load of the workgroup is issued before the first LDS store; invalid
+  // pieces read the operand's first float4 and are zeroed afterwards
+  float4 a[KCH];
+  uint32_t aok = 0;
+#pragma unroll
+  for (int c = 0; c < KCH; ++c) {
+    const int k = 16 * c + 4 * q;
+    const bool ok = rok && k < K;  // K % 4 == 0: the whole float4 is inside the row
+    a[c] = *reinterpret_cast<const float4*>(A + (ok ? row * lda + k : 0));
+    aok |= (uint32_t)ok << c;
+  }
+  float4 v[PT];
+  uint32_t bok = 0;
+#pragma unroll
+  for (int p = 0; p < PT; ++p) {
+    const int e = tid + 256 * p;
+    const int k = e / NQ;
+    const int64_t n = n0 + 4 * (e % NQ);
+    const bool ok = e < KP * NQ && k < K && n < N;  // N % 4 == 0
+    v[p] = *reinterpret_cast<const float4*>(B + (ok ? (int64_t)k * ldb + n : 0));
+    bok |= (uint32_t)ok << p;
+  }
+#pragma unroll
+  for (int p = 0; p < PT; ++p) {
+    const int e = tid + 256 * p;
+    if (e >= KP * NQ) break;
+    const bool ok = (bok >> p) & 1;
+    *reinterpret_cast<float4*>(s_B + (e / NQ) * LW + 4 * (e % NQ)) = ok ? v[p] : make_float4(0.f, 0.f, 0.f, 0.f);
+  }
+  __syncthreads();
+  f32x4 acc[NT];
+#pragma unroll
+  for (int t = 0; t < NT; ++t) acc[t] = f32x4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+  for (int c = 0; c < KCH; ++c) {
+    const bool ok = (aok >> c) & 1;
+    const float av[4] = {ok ? a[c].x : 0.f, ok ? a[c].y : 0.f, ok ? a[c].z : 0.f, ok ? a[c].w : 0.f};
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      const float* br = s_B + (16 * c + 4 * q + j) * LW + r;
+#pragma unroll
+      for (int t = 0; t < NT; ++t) acc[t] = __builtin_amdgcn_mfma_f32_16x16x4f32(av[j], br[16 * t], acc[t], 0, 0, 0);
+    }
+  }
+  // C/D map: reg jj -> row 4q + jj, column lane & 15
+#pragma unroll
+  for (int t = 0; t < NT; ++t) {
+    const int64_t n = n0 + 16 * t + r;
+#pragma unroll
+    for (int jj = 0; jj < 4; ++jj) {
+      const int64_t gm = m0 + 4 * q + jj;
+      if (gm < M && n < N) C[gm * ldc + n] = gemm_epi(epi, acc[t][jj], gm, n);
+    }
+  }
+}
+
 // Sum split-K slabs in slab order, then apply the epilogue.
 __global__ void gemm_splitk_reduce_kernel(int32_t M, int32_t N, int32_t S, const float* __restrict__ slab,
                                           float* __restrict__ C, int64_t ldc, GemmEpi epi) {
@@ -375,6 +455,28 @@ extern "C" int gcnk_gemm_f32(int32_t transA, int32_t transB, int32_t M, int32_t 
 #undef GCNK_SKINNY_NT
 #undef GCNK_SKINNY_KS
     return launch_check("gemm_skinny_ksplit_kernel");
+  }
+#ifndef GCNK_GEMM_SHORTK
+#define GCNK_GEMM_SHORTK 1
+#endif
+  if (GCNK_GEMM_SHORTK && !ta && !tb && K > 0 && K <= 128 && K % 4 == 0 && N > 64 && N % 4 == 0 && lda % 4 == 0 &&
+      ldb % 4 == 0 && aligned16(A) && aligned16(B) && split_k == 1) {
+    const dim3 grid((unsigned)(((int64_t)M + 63) / 64), (unsigned)((N + 111) / 112));
+    const int kch = (K + 15) / 16;
+#define GCNK_SHORTK(KCH_) \
+  hipLaunchKernelGGL((gemm_shortk_kernel<KCH_>), grid, dim3(256), 0, s, M, N, K, A, lda, B, ldb, C, ldc, e)
+    switch (kch) {
+      case 1: GCNK_SHORTK(1); break;
+      case 2: GCNK_SHORTK(2); break;
+      case 3: GCNK_SHORTK(3); break;
+      case 4: GCNK_SHORTK(4); break;
+      case 5: GCNK_SHORTK(5); break;
+      case 6: GCNK_SHORTK(6); break;
+      case 7: GCNK_SHORTK(7); break;
+      default: GCNK_SHORTK(8); break;
+    }
+#undef GCNK_SHORTK
+    return launch_check("gemm_shortk_kernel");
   }
   if (N <= 16) return launch_gemm<4, 1, 2, 1>(ta, tb, M, N, K, A, lda, B, ldb, C, ldc, e, split_k, workspace, s);
   return launch_gemm<2, 2, 2, 2>(ta, tb, M, N, K, A, lda, B, ldb, C, ldc, e, split_k, workspace, s);

@@ -381,11 +381,14 @@ def test_csr_transpose_matches_oracle():
 
 @pytest.mark.parametrize("ta,tb", [(False, False), (True, False), (False, True), (True, True)])
 @pytest.mark.parametrize("shape", [(7724, 8, 200), (200, 8, 7724), (7724, 200, 8), (33, 70, 5), (1, 1, 1),
-                                   (18916, 200, 100), (7724, 20, 200), (1000, 40, 200), (257, 332, 97)])
+                                   (18916, 200, 100), (7724, 20, 200), (1000, 40, 200), (257, 332, 97),
+                                   (1000, 124, 128), (77, 68, 4), (130, 336, 64)])
 def test_gemm_mfma(ta, tb, shape):
     """Every GEMM kernel against the float64 oracle: the LDS-tiled MFMA kernel
-    (with transposes; a dense gensim-style X W1 at 18916 x 100 x 200) and the
-    skinny-N K-split one (N <= 64: gc2's H1 W2 at 8, 20 and 40 classes)."""
+    (with transposes), the short-K wide-N one (NN, K <= 128, N > 64: a dense
+    gensim-style X W1 at 18916 x 100 x 200; K = 4 .. 128, partial row blocks and
+    column slices) and the skinny-N K-split one (N <= 64: gc2's H1 W2 at 8, 20
+    and 40 classes)."""
     M, N, K = shape
     g = torch.Generator().manual_seed(M * 7 + N)
     A = torch.randn((K, M) if ta else (M, K), generator=g)
@@ -410,6 +413,17 @@ def test_gemm_epilogues_and_split_k():
            np.where(R.numpy() > 0, 2 * ref, 0.0))
     for s in (1, 2, 3, 8):
         _close(gemm(d["A"], d["B"], split_k=s), ref, atol=1e-4)
+    # the same epilogues on the short-K wide-N kernel (K = 100, N = 200)
+    A2 = torch.randn(300, 100, generator=g)
+    B2 = torch.randn(100, 200, generator=g)
+    b2 = torch.randn(200, generator=g)
+    R2 = torch.relu(torch.randn(300, 200, generator=g))
+    ref2 = A2.double().numpy() @ B2.double().numpy()
+    d2 = {k: v.to(DEV) for k, v in dict(A=A2, B=B2, bias=b2, R=R2).items()}
+    _close(gemm(d2["A"], d2["B"], bias=d2["bias"], epilogue=_lib.GEMM_EPI_BIAS_RELU),
+           np.maximum(ref2 + b2.double().numpy(), 0), atol=1e-4)
+    _close(gemm(d2["A"], d2["B"], epilogue=_lib.GEMM_EPI_MASK_POS, R=d2["R"], scale=2.0),
+           np.where(R2.numpy() > 0, 2 * ref2, 0.0), atol=1e-4)
 
 
 def test_colsum():

@@ -190,3 +190,34 @@ def test_plan_rejects_bad_csr():
     ci = np.array([0, 5], np.int32)
     n = lib.gcnk_spmm_plan_bytes_host(rp.ctypes.data, ci.ctypes.data, 2, 2, 2, 8, 1, 0.25, 0, 0)
     assert n == _lib.EARG and b"out of range" in lib.gcnk_last_error()
+
+
+@pytest.mark.parametrize("kind", ["random", "mixed", "hub"])
+def test_plan_bytes_is_exactly_the_built_image(kind):
+    """gcnk_spmm_plan_bytes_host sizes a row-unit plan from its header alone
+    (no light-row sort, no image): the build must write exactly that many
+    bytes -- none past them, the last one included."""
+    import sys
+    import os
+    sys.path.insert(0, os.path.dirname(__file__))
+    from test_gpu_parity import _mixed_density_csr, _random_csr
+    lib = _lib.load()
+    rng = np.random.default_rng(17)
+    if kind == "mixed":
+        rp, ci, v = _mixed_density_csr(rng, 900, 900)
+        M = K = 900
+    else:
+        M, K = 3001, 2003
+        rp, ci, v = _random_csr(M, K, 20000, rng, heavy_rows=(5, 1700), heavy_deg=2500, empty_frac=0.2)
+    hub_min = 0 if kind == "hub" else -1
+    rp, ci, v = (np.ascontiguousarray(a, t) for a, t in ((rp, np.int32), (ci, np.int32), (v, np.float32)))
+    nbytes = lib.gcnk_spmm_plan_bytes_host(rp.ctypes.data, ci.ctypes.data, M, K, len(ci), 12, 1, 0.25, hub_min, 0)
+    assert nbytes > 0 and nbytes % 4 == 0
+    buf = np.full(nbytes // 4 + 64, -7, np.int32)
+    rc = lib.gcnk_spmm_plan_build_host(rp.ctypes.data, ci.ctypes.data, v.ctypes.data, M, K, len(ci), 12, 1, 0.25,
+                                       hub_min, 0, buf.ctypes.data, buf.nbytes)
+    assert rc == 0, lib.gcnk_last_error()
+    assert np.all(buf[nbytes // 4:] == -7), "the build wrote past the size plan_bytes reported"
+    # no plan word is -7 (ids >= -1, counts >= 0, float bits of -7 would be a NaN),
+    # so a sentinel left in the last reported word means the size was too large
+    assert buf[nbytes // 4 - 1] != -7, "plan_bytes reported more than the build wrote"

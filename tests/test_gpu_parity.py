@@ -382,13 +382,14 @@ def test_csr_transpose_matches_oracle():
 @pytest.mark.parametrize("ta,tb", [(False, False), (True, False), (False, True), (True, True)])
 @pytest.mark.parametrize("shape", [(7724, 8, 200), (200, 8, 7724), (7724, 200, 8), (33, 70, 5), (1, 1, 1),
                                    (18916, 200, 100), (7724, 20, 200), (1000, 40, 200), (257, 332, 97),
-                                   (1000, 124, 128), (77, 68, 4), (130, 336, 64)])
+                                   (1000, 124, 128), (77, 68, 4), (130, 336, 64),
+                                   (18916, 20, 200), (16400, 64, 256), (16385, 8, 100)])
 def test_gemm_mfma(ta, tb, shape):
     """Every GEMM kernel against the float64 oracle: the LDS-tiled MFMA kernel
     (with transposes), the short-K wide-N one (NN, K <= 128, N > 64: a dense
     gensim-style X W1 at 18916 x 100 x 200; K = 4 .. 128, partial row blocks and
     column slices) and the skinny-N K-split one (N <= 64: gc2's H1 W2 at 8, 20
-    and 40 classes)."""
+    and 40 classes; 20ng-sized and partial workgroups)."""
     M, N, K = shape
     g = torch.Generator().manual_seed(M * 7 + N)
     A = torch.randn((K, M) if ta else (M, K), generator=g)

@@ -243,7 +243,7 @@ def sharded_config5(dev, world, rank, datasets, ops, F=4096, reps=3):
         t_loc, t_tot = [], []
         for _ in range(reps):
             if world > 1:
-                dist.barrier()
+                dist.barrier(device_ids=[torch.cuda.current_device()])
             torch.cuda.synchronize()
             t0 = time.perf_counter()
             blk = cs.local(Bp)
@@ -280,10 +280,10 @@ def main():
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
+    torch.cuda.set_device(local)   # before the process group: RCCL binds each rank to its own GPU
+    dev = torch.device("cuda", local)
     if world > 1:
         dist.init_process_group("nccl", init_method="env://")
-    torch.cuda.set_device(local)
-    dev = torch.device("cuda", local)
 
     import gcn_amd  # noqa: F401
     from graph_convolutional_networks_for_text_classification_amd import GCN, datasets, ops
@@ -327,14 +327,14 @@ def main():
         step()
     torch.cuda.synchronize()
     if world > 1:
-        dist.barrier()
+        dist.barrier(device_ids=[torch.cuda.current_device()])
     torch.cuda.synchronize()
     t0 = time.perf_counter()
     for _ in range(args.steps // per):
         step()
     torch.cuda.synchronize()
     if world > 1:
-        dist.barrier()
+        dist.barrier(device_ids=[torch.cuda.current_device()])
     torch.cuda.synchronize()
     elapsed = time.perf_counter() - t0
     if world > 1:

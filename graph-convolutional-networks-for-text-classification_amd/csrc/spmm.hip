@@ -1587,37 +1587,37 @@ void classic_image(const HostPlan& hp, const int32_t* ci, const float* vv, int64
   putf(L.dval, hp.dval);
 }
 
-// The plan image for host CSR arrays: the hub-split plan (hub.hip) when the
-// operand has hub rows and no dense tile blocks (hub_min >= 0; 0 = automatic
-// threshold), else the row-unit + tile plan.
+// The plan image for host CSR arrays: the hub plan (hub.hip) when the operand
+// has its structure (hub_min >= 0; 0 = automatic threshold), else the
+// row-unit + tile plan.
 int build_image(const int32_t* rp, const int32_t* ci, const float* vv, int32_t M, int32_t K, int64_t nnz, int32_t ipc,
                 int32_t groups, float dense_threshold, int32_t hub_min, int32_t block_rows, std::vector<int32_t>& img) {
   int rc = check_csr(rp, ci, M, K, nnz);
   if (rc) return rc;
-  HostPlan hp;
-  if ((rc = host_plan(rp, ci, vv, M, K, nnz, ipc, groups, dense_threshold, hp))) return rc;
-  if (hub_min >= 0 && hp.hdr[8] == 0) {
+  if (hub_min >= 0) {
     rc = hub_plan_host(rp, ci, vv, M, K, nnz, groups, hub_min, block_rows, img);
     if (rc <= 0) return rc;  // built (0) or an error; 1: not applicable
   }
+  HostPlan hp;
+  if ((rc = host_plan(rp, ci, vv, M, K, nnz, ipc, groups, dense_threshold, hp))) return rc;
   classic_image(hp, ci, vv, nnz, img);
   return GCNK_OK;
 }
 
 // Bytes of the plan build_image would make, without making it: the row-unit +
 // tile plan's size follows from its header (no light-row sort, no image);
-// a hub-split plan is built (its size depends on the block records).
+// a hub plan is built (its size depends on the group records).
 int64_t plan_size(const int32_t* rp, const int32_t* ci, int32_t M, int32_t K, int64_t nnz, int32_t ipc, int32_t groups,
                   float dense_threshold, int32_t hub_min, int32_t block_rows) {
   int rc = check_csr(rp, ci, M, K, nnz);
   if (rc) return rc;
-  HostPlan hp;
-  if ((rc = host_plan(rp, ci, nullptr, M, K, nnz, ipc, groups, dense_threshold, hp, false))) return rc;
-  if (hub_min >= 0 && hp.hdr[8] == 0) {
+  if (hub_min >= 0) {
     std::vector<int32_t> img;
     rc = hub_plan_host(rp, ci, nullptr, M, K, nnz, groups, hub_min, block_rows, img);
     if (rc <= 0) return rc ? rc : (int64_t)img.size() * 4;
   }
+  HostPlan hp;
+  if ((rc = host_plan(rp, ci, nullptr, M, K, nnz, ipc, groups, dense_threshold, hp, false))) return rc;
   return Layout(hp.hdr).total * 4;
 }
 
@@ -1857,7 +1857,7 @@ static int spmm_impl(const void* plan, const int32_t* hdr, const float* B, int64
       return GCNK_EUNSUP;
     }
     if (part == 1) return GCNK_OK;  // no dense tile blocks in a hub plan
-    return hub_spmm(plan, hdr, B, ldb, F, C, ldc, e, workspace, lpr, vec4, s);
+    return hub_spmm(plan, hdr, B, ldb, F, C, ldc, e, workspace, vec4, s);
   }
   if (proj) {
     // the projection needs whole rows in one group: row-kernel rows only, float4, one column tile

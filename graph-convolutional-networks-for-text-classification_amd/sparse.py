@@ -38,12 +38,12 @@ def require_device(t, what):
 
 
 DENSE_THRESHOLD = 0.25  # row blocks at least this dense (condensed) run on the MFMA tile path
-# hub-split plan: 0 = automatic hub threshold, > 0 = degree threshold, < 0 = never.
-# Off by default: on R8 it measured 13.4 us against the row-unit plan's 10.6 us
-# (DESIGN.md "Hub-split plan"); kept as an option for graphs with few, very
-# heavy hub rows.
-HUB_MIN = -1
-HUB_BLOCK_ROWS = 0      # light rows per hub-plan block (0 = automatic, ~256 blocks)
+# hub plan (csrc/hub.hip) for operands with its structure (a contiguous range
+# of heavy hub rows; every other row references only hub columns and its own
+# diagonal -- the reference's doc-topic adjacency): 0 = automatic hub
+# threshold, > 0 = degree threshold, < 0 = never (row-unit + tile plan).
+HUB_MIN = 0
+HUB_BLOCK_ROWS = 0      # light rows per hub-plan group (0 = automatic, ~256 workgroups)
 
 
 class Plan:
@@ -54,7 +54,7 @@ class Plan:
     calls on different streams (or the autograd thread's) never share one."""
 
     __slots__ = ("buf", "hdr", "_counters", "_spares", "_captured", "_lock")
-    HUB_MAGIC = 0x474e4831
+    HUB_MAGIC = 0x474e4832
     SPARE_REGIONS = 16   # pre-zeroed regions handed to hipGraph captures
 
     def __init__(self, buf, hdr):

@@ -23,11 +23,10 @@ from oracle import csr_ref  # noqa: E402
 
 VARIANTS = {
     "row": dict(hub_min=-1),
-    "hub": dict(hub_min=0, block_rows=0),
-    "hub16": dict(hub_min=0, block_rows=16),
-    "hub24": dict(hub_min=0, block_rows=24),
-    "hub48": dict(hub_min=0, block_rows=48),
-    "hub64": dict(hub_min=0, block_rows=64),
+    "hub": dict(hub_min=0, block_rows=0),      # hub plan, automatic rows per group (R8 F = 200: 240)
+    "hub60": dict(hub_min=0, block_rows=60),
+    "hub120": dict(hub_min=0, block_rows=120),
+    "hub480": dict(hub_min=0, block_rows=480),
 }
 
 
@@ -65,7 +64,7 @@ def time_graph(fns, reps_per_fn):
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--reps", type=int, default=100)
-    ap.add_argument("--variants", default="row,hub,hub16,hub24,hub48,hub64")
+    ap.add_argument("--variants", default="row,hub,hub60,hub120,hub480")
     ap.add_argument("--widths", default="200,8")
     ap.add_argument("--graph", default="r8", choices=["r8", "20ng"])
     ap.add_argument("--mode", default="both", choices=["warm", "cold", "both"],

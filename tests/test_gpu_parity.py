@@ -65,7 +65,15 @@ def test_spmm_r8_adjacency(r8, F):
     _close(got, ref)
     # low dense threshold: document rows run as MFMA tiles over the 50 topic
     # columns with the self loop kept aside (diagonal epilogue)
-    got_t = spmm(a, B.to(DEV), dense=0.05)
+    # row-unit + tile plan (hub plan off)
+    from graph_convolutional_networks_for_text_classification_amd import sparse as sp
+    saved = sp.HUB_MIN
+    sp.HUB_MIN = -1
+    try:
+        _close(spmm(a, B.to(DEV)), ref)
+        got_t = spmm(a, B.to(DEV), dense=0.05)
+    finally:
+        sp.HUB_MIN = saved
     _close(got_t, ref)
     hdr = [p for k, p in a._plans.items() if k[2] == 0.05][0].header
     assert hdr[8] > 0 and hdr[12] == 1, "R8 document rows: MFMA tiles over the topic columns + diagonal"
@@ -260,28 +268,70 @@ def test_spmm_two_streams_share_one_plan_concurrently(r8, kind, monkeypatch):
         assert len(plan._counters) >= 3, "one counter region per stream"
 
 
-@pytest.mark.parametrize("F", [1, 8, 24, 64, 200, 256, 300])
-def test_spmm_hub_plan_r8(r8, F, monkeypatch):
-    """The hub-split plan (optional, sparse.HUB_MIN >= 0) on the R8 adjacency:
-    light document blocks staged in LDS + the 50 topic rows summed from
-    per-block partials, every width class of the kernel, bias + ReLU epilogue,
-    against the float64 oracle; bit-identical on a second call."""
-    from graph_convolutional_networks_for_text_classification_amd import sparse as sp
-    monkeypatch.setattr(sp, "HUB_MIN", 0)
+@pytest.mark.parametrize("F", [1, 3, 8, 24, 64, 200, 256, 300, 1000])
+@pytest.mark.parametrize("lanes", [0, 64])
+def test_spmm_hub_plan_r8(r8, F, lanes):
+    """The hub plan (default for operands with its structure) on the R8
+    adjacency: 32 (or ~256 at narrow widths) row groups x column slices, the
+    documents from the LDS image, the 50 topic rows summed from the groups'
+    partials; every width class (float4 and scalar paths), bias + ReLU, against
+    the float64 oracle; bit-identical on a second call."""
     a = from_torch(r8["adj"].to(DEV))
     rng = np.random.default_rng(F)
     B = rng.standard_normal((r8["nodes"], F)).astype(np.float32)
     b = rng.standard_normal(F).astype(np.float32)
-    # the hub plan serves one lane group per wavefront (lanes=64 for narrow F)
     got = spmm(a, torch.from_numpy(B).to(DEV), bias=torch.from_numpy(b).to(DEV), epilogue=_lib.EPI_BIAS_RELU,
-               lanes=64)
+               lanes=lanes)
     plan = list(a._plans.values())[-1]
-    assert plan.is_hub and plan.header[6] == r8["ntopic"]
+    assert plan.is_hub and plan.header[6] == r8["ntopic"] and plan.header[7] == r8["ndoc"]
     rp, ci, v = (t.cpu().numpy() for t in (a.rowptr, a.colind, a.val))
     _close(got, csr_ref.spmm_epilogue(csr_ref.spmm_csr(rp, ci, v, B), b, relu=True), atol=2e-5)
     again = spmm(a, torch.from_numpy(B).to(DEV), bias=torch.from_numpy(b).to(DEV), epilogue=_lib.EPI_BIAS_RELU,
-                 lanes=64)
+                 lanes=lanes)
     assert torch.equal(got, again)
+
+
+@pytest.mark.parametrize("F", [4, 7, 16, 200])
+@pytest.mark.parametrize("block_rows", [0, 1, 33, 512])
+def test_spmm_hub_plan_synthetic_every_epilogue(F, block_rows, monkeypatch):
+    """Hub plan on a doc-topic-like operand with the hub range in the middle
+    (groups straddle it), hub x hub nonzeros, empty light rows and rows without
+    a diagonal; every epilogue (bias, relu, dropout mask, hash dropout),
+    strided B / C (ldb, ldc > F; an odd ldb takes the scalar path)."""
+    import sys
+    sys.path.insert(0, os.path.dirname(__file__))
+    from test_plan_host import _doc_topic
+    from graph_convolutional_networks_for_text_classification_amd import sparse as sp
+    monkeypatch.setattr(sp, "HUB_BLOCK_ROWS", block_rows)
+    rng = np.random.default_rng(F * 7 + block_rows)
+    rp, ci, v = _doc_topic(rng, 1700, 40, 1300, 300, 6)
+    M = len(rp) - 1
+    a = from_arrays(rp, ci, v, (M, M), DEV)
+    ld = F + (5 if F % 4 else 8)
+    Bfull = rng.standard_normal((M, ld)).astype(np.float32)
+    B = Bfull[:, :F]
+    bias = rng.standard_normal(F).astype(np.float32)
+    mask = (rng.random((M, F)) < 0.6).astype(np.uint8)
+    acc = csr_ref.spmm_csr(rp, ci, v, B)
+    Bt = torch.from_numpy(Bfull).to(DEV)[:, :F]
+    bt = torch.from_numpy(bias).to(DEV)
+    out = torch.full((M, ld), 7.0, device=DEV)
+    spmm(a, Bt, out=out[:, :F])
+    assert list(a._plans.values())[-1].is_hub
+    _close(out[:, :F], acc, atol=2e-5 * np.sqrt(300))
+    assert torch.all(out[:, F:] == 7.0), "columns past F untouched"
+    _close(spmm(a, Bt, bias=bt, epilogue=_lib.EPI_BIAS), csr_ref.spmm_epilogue(acc, bias), atol=2e-4)
+    _close(spmm(a, Bt, bias=bt, epilogue=_lib.EPI_BIAS_RELU_DROP, mask=torch.from_numpy(mask).to(DEV), scale=2.0),
+           csr_ref.spmm_epilogue(acc, bias, relu=True, mask=mask, scale=2.0), atol=4e-4)
+    h = spmm(a, Bt, bias=bt, epilogue=_lib.EPI_BIAS_RELU_HASH, keep_prob=0.5, scale=2.0, seed=5, offset=11)
+    h2 = spmm(a, Bt, bias=bt, epilogue=_lib.EPI_BIAS_RELU_HASH, keep_prob=0.5, scale=2.0, seed=5, offset=11)
+    assert torch.equal(h, h2)
+    relu = csr_ref.spmm_epilogue(acc, bias, relu=True)
+    hn = h.double().cpu().numpy()
+    kept = hn != 0
+    _close(hn[kept], 2.0 * relu[kept], atol=4e-4)
+    frac = kept[relu > 1e-3].mean()
+    assert 0.4 < frac < 0.6, f"hash dropout keeps ~half, got {frac}"
 
 
 def test_spmm_epilogues_and_strided_operands():

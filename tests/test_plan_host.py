@@ -1,11 +1,11 @@
 """CPU checks of the SpMM plan builders (gcnk_spmm_plan_build_host: the same
 host code the device build runs, writing into host memory).
 
-The hub-split plan (include/gcnk.h, csrc/hub.hip) is executed here by a numpy
-interpreter of its two kernels — light blocks reading staged rows / gathering
-the rest, hub rows summed from per-block partials plus leftover nonzeros —
-and compared with the float64 oracle, so the plan's bookkeeping (row
-ownership, staging, partial indices, leftovers) is checked without a GPU.
+The hub plan (include/gcnk.h, csrc/hub.hip) is executed here by a numpy
+interpreter of its two kernels — row groups computing their light rows and
+one partial per hub from their LDS image, hub rows summed from the groups'
+partials — and compared with the float64 oracle, so the plan's bookkeeping
+(groups, slots, item order, hub x hub placement) is checked without a GPU.
 The kernels themselves are checked on the GPU (tests/test_gpu_parity.py).
 """
 import numpy as np
@@ -15,7 +15,7 @@ import gcn_amd  # noqa: F401
 from graph_convolutional_networks_for_text_classification_amd import _lib
 from oracle import csr_ref
 
-HUB_MAGIC = 0x474E4831
+HUB_MAGIC = 0x474E4832
 ROW_MAGIC = 0x474E4B35
 
 
@@ -41,71 +41,86 @@ def _a4(x):
 
 
 def exec_hub_plan(plan, B):
-    """numpy interpreter of hub_light_kernel + hub_finish_kernel (float64)."""
+    """numpy interpreter of hub_group_kernel + hub_sum_kernel (float64; the
+    column slices of a launch do not change what is summed, so whole rows).
+
+    Checks the plan's bookkeeping: every light row and every hub partial
+    written exactly once, slots inside the group's LDS image, items in CSR
+    (column) order, hub x hub nonzeros in group t % G."""
     h = plan[:16]
     assert h[0] == HUB_MAGIC
-    M, nblocks, R, nhub, npart, smax = int(h[1]), int(h[4]), int(h[5]), int(h[6]), int(h[7]), int(h[14])
+    M, G, R, H, h0, nL, gs = (int(h[i]) for i in (1, 4, 5, 6, 7, 8, 10))
+    assert M == H + nL and G == -(-nL // gs)
     F = B.shape[1]
     B = B.astype(np.float64)
+
+    def light_row(l):
+        return l if l < h0 else l + H
+
     C = np.full((M, F), np.nan)
     written = np.zeros(M, np.int64)
-    part = np.full((npart, F), np.nan)
-    for b in range(nblocks):
-        rec = plan[16 + b * R: 16 + (b + 1) * R]
-        nstage, nl, ng, nit = (int(x) for x in rec[:4])
-        assert nstage <= smax and nstage <= int(h[8])
-        scols = rec[4:4 + nstage]
-        o_out = _a4(4 + nstage)
-        o_it = _a4(o_out + 2 * (nl + ng))
+    part = np.full((H, G, F), np.nan)
+    for g in range(G):
+        rec = plan[16 + g * R: 16 + (g + 1) * R]
+        n, nout, nit = int(rec[0]), int(rec[1]), int(rec[2])
+        assert n == min(gs, nL - g * gs) and nout == n + H
+        off = rec[4:5 + nout]
+        assert off[0] == 0 and off[-1] == nit and np.all(np.diff(off) >= 0)
+        o_it = _a4(5 + nout)
         assert o_it + 2 * nit <= R
-        ib = 0
-        for o in range(nl + ng):
-            dest, ie = int(rec[o_out + 2 * o]), int(rec[o_out + 2 * o + 1])
-            items = rec[o_it + 2 * ib: o_it + 2 * ie].reshape(-1, 2)
-            slots = items[:, 0]
-            vals = items[:, 1].copy().view(np.float32).astype(np.float64)
-            assert (ie - ib) % 4 == 0, "items padded to a multiple of 4"
-            pad = slots == nstage                      # {zero row, 0} padding
-            assert np.all(vals[pad] == 0) and np.all((slots >= 0) & (slots <= nstage)), "items read staged rows"
-            cols = scols[np.clip(slots[~pad], 0, max(nstage - 1, 0))]
-            acc = vals[~pad] @ B[cols] if len(cols) else np.zeros(F)
-            if dest >= 0:
-                assert o < nl, "light rows come first"
-                C[dest] = acc
-                written[dest] += 1
+        items = rec[o_it:o_it + 2 * nit].reshape(-1, 2)
+        slots = items[:, 0]
+        vals = items[:, 1].copy().view(np.float32).astype(np.float64)
+        assert np.all((slots >= 0) & (slots < H + n)), "items read the group's LDS image"
+        srows = np.array([h0 + s if s < H else light_row(g * gs + s - H) for s in range(H + n)], np.int64)
+        for o in range(nout):
+            sl = slots[off[o]:off[o + 1]]
+            cols = srows[sl]
+            assert np.all(np.diff(cols) > 0), "CSR column order"
+            acc = vals[off[o]:off[o + 1]] @ B[cols] if len(cols) else np.zeros(F)
+            if o < n:
+                r = light_row(g * gs + o)
+                assert np.all((sl < H) | (cols == r)), "a light row reads hub rows and itself"
+                C[r] = acc
+                written[r] += 1
             else:
-                assert o >= nl
-                part[-dest - 1] = acc
-            ib = ie
-        assert ib == nit
-    hubs = plan[16 + nblocks * R: 16 + nblocks * R + 4 * (nhub + 1)].reshape(-1, 4)
-    left = plan[16 + nblocks * R + 4 * (nhub + 1):].reshape(-1, 2)
-    assert len(left) == int(h[10])
-    for i in range(nhub):
-        row, pb, npr, lb = (int(x) for x in hubs[i])
-        le = int(hubs[i + 1][3])
-        lv = left[lb:le, 1].copy().view(np.float32).astype(np.float64)
-        acc = part[pb:pb + npr].sum(0) + (lv @ B[left[lb:le, 0]] if le > lb else 0.0)
-        C[row] = acc
-        written[row] += 1
+                t = o - n
+                hh = sl < H
+                assert not hh.any() or t % G == g, "hub x hub nonzeros ride in group t % G"
+                part[t, g] = acc
+    assert not np.isnan(part).any(), "every partial written"
+    for t in range(H):
+        C[h0 + t] = part[t].sum(0)
+        written[h0 + t] += 1
     assert np.all(written == 1), "every output row exactly once"
-    assert not np.isnan(part).any(), "every partial row written"
     return C
 
 
-def _hubby(rng, M, K, nhub, hub_deg, light_deg, symmetric_block=False):
+def _doc_topic(rng, below, H, above, hub_deg, light_deg, hub_hub=0.2, empty_frac=0.05, no_diag_frac=0.05):
+    """Square doc-topic-like operand: `below` light rows, H contiguous hub rows,
+    `above` light rows; light rows = own diagonal + a few hub columns, hub rows =
+    light columns + some hub columns (+ diagonal)."""
+    M = below + H + above
+    h0 = below
+    hubs = np.arange(h0, h0 + H)
+    light = np.concatenate([np.arange(below), np.arange(h0 + H, M)])
     rows, cols = [], []
-    hubs = rng.choice(M, nhub, replace=False)
-    for r in range(M):
-        if r in hubs:
-            c = rng.choice(K, min(K, hub_deg), replace=False)
-        else:
-            d = int(rng.integers(0, light_deg + 1))
-            c = np.concatenate([[r % K], rng.choice(hubs % K, min(d, nhub), replace=False)]) if d else np.zeros(0, int)
-        rows.append(np.full(len(c), r))
-        cols.append(c)
-    rows, cols = np.concatenate(rows), np.concatenate(cols)
-    return csr_ref.coo_to_csr(rows, cols, rng.standard_normal(rows.size).astype(np.float32), (M, K))
+    for r in light:
+        if rng.random() < empty_frac:
+            continue
+        d = int(rng.integers(0, light_deg + 1))
+        c = list(rng.choice(hubs, min(d, H), replace=False))
+        if rng.random() >= no_diag_frac:
+            c.append(r)
+        rows += [r] * len(c)
+        cols += c
+    for r in hubs:
+        c = list(rng.choice(light, min(len(light), hub_deg), replace=False))
+        c += [x for x in hubs if rng.random() < hub_hub]
+        rows += [r] * len(c)
+        cols += c
+    rows, cols = np.array(rows), np.array(cols)
+    return csr_ref.coo_to_csr(rows, cols, rng.standard_normal(rows.size).astype(np.float32), (M, M))
 
 
 def _check(rp, ci, v, shape, F=24, **kw):
@@ -124,44 +139,46 @@ def test_r8_adjacency_gets_the_hub_plan(r8):
     plan = _check(rp, ci, v, adj.shape, F=16)
     h = plan[:16]
     assert h[6] == r8["ntopic"], "the 50 topic rows are the hubs"
-    assert h[11] == r8["ndoc"], "every document row is a light row"
-    assert 200 <= h[4] <= 300, "about one light block per CU"
-    assert h[8] <= 64
-    assert h[10] == 2 * 237 + 50, "leftovers: the 237 topic-topic edges both ways + the topic self loops"
+    assert h[7] == r8["ndoc"] and h[8] == r8["ndoc"], "topics follow the documents; every document is a light row"
+    assert h[4] == 32 and h[10] == 240, "wide F: 32 groups of 240 documents (x 7 column slices at F = 200)"
+    # narrow widths (F = 8: 32 lane groups per wavefront): ~256 groups, one slice
+    plan8 = _check(rp, ci, v, adj.shape, F=8, groups=32)
+    assert 240 <= plan8[4] <= 264
 
 
-def test_hub_plan_square_nonsquare_and_overflowing_stage():
+def test_hub_plan_hubs_in_the_middle_with_hub_hub_entries():
     rng = np.random.default_rng(0)
-    # square: sparse hub rows, light rows self + a few hubs (automatic threshold)
-    rp, ci, v = _hubby(rng, 3000, 3000, 40, 300, 6)
-    plan = _check(rp, ci, v, (3000, 3000))
-    assert plan[0] == HUB_MAGIC
-    # hub rows dense enough for the MFMA tile path keep the row-unit + tile plan
-    rp, ci, v = _hubby(rng, 900, 900, 12, 700, 6)
-    assert build_host_plan(rp, ci, v, (900, 900))[0] == ROW_MAGIC
-    # rectangular (K < M): columns >= K are never owned; light rows j >= K own nothing
-    rp, ci, v = _hubby(rng, 1200, 700, 30, 150, 5)
-    _check(rp, ci, v, (1200, 700), hub_min=100)
-    # light rows referencing many distinct columns: blocks are cut before their
-    # staged rows would exceed the 64 stage slots
-    rows = np.repeat(np.arange(1000), 10)
-    cols = rng.integers(0, 1000, rows.size)
-    hub_r = np.full(3000, 7)
-    hub_c = rng.choice(1000, 3000)
-    rp, ci, v = csr_ref.coo_to_csr(np.concatenate([rows, hub_r]), np.concatenate([cols, hub_c]),
-                                   rng.standard_normal(rows.size + 3000).astype(np.float32), (1000, 1000))
-    plan = _check(rp, ci, v, (1000, 1000), hub_min=200, block_rows=64)
-    R = plan[5]
-    recs = plan[16:16 + plan[4] * R].reshape(plan[4], R)
-    assert recs[:, 0].max() <= 64 and recs[:, 1].max() < 64, "stage-bound blocks hold fewer than block_rows rows"
-    assert plan[8] == recs[:, 0].max()
+    rp, ci, v = _doc_topic(rng, 1700, 40, 1300, 300, 6)
+    plan = _check(rp, ci, v, (3040, 3040))
+    assert plan[0] == HUB_MAGIC and plan[6] == 40 and plan[7] == 1700
+    for br in (1, 7, 64, 512):   # explicit rows per group, groups straddling the hub range
+        _check(rp, ci, v, (3040, 3040), F=8, block_rows=br)
+    # hubs first / last
+    for below, above in ((0, 900), (900, 0)):
+        rp, ci, v = _doc_topic(rng, below, 16, above, 120, 4)
+        plan = _check(rp, ci, v, (below + 16 + above,) * 2, F=5)
+        assert plan[0] == HUB_MAGIC and plan[7] == below
 
 
-def test_hub_plan_empty_rows_and_explicit_block_rows():
-    rng = np.random.default_rng(3)
-    rp, ci, v = _hubby(rng, 1500, 1500, 30, 200, 4)
-    for br in (1, 4, 64):
-        _check(rp, ci, v, (1500, 1500), F=8, block_rows=br)
+def test_hub_plan_not_applicable_falls_back_to_row_plan():
+    rng = np.random.default_rng(1)
+    # a light row referencing another light row
+    rp, ci, v = _doc_topic(rng, 800, 20, 200, 150, 4)
+    M = 1020
+    rows = np.repeat(np.arange(M), np.diff(rp))
+    rows, cols = np.append(rows, 3), np.append(ci, 5)
+    rp2, ci2, v2 = csr_ref.coo_to_csr(rows, cols, np.append(v, 1.0).astype(np.float32), (M, M))
+    assert build_host_plan(rp2, ci2, v2, (M, M))[0] == ROW_MAGIC
+    assert build_host_plan(rp, ci, v, (M, M))[0] == HUB_MAGIC
+    # hub rows not contiguous: swap a hub row's nonzeros into a light row's place
+    perm = np.arange(M)
+    perm[[805, 100]] = perm[[100, 805]]
+    rows3 = perm[np.repeat(np.arange(M), np.diff(rp))]
+    rp3, ci3, v3 = csr_ref.coo_to_csr(rows3, perm[ci], v, (M, M))
+    assert build_host_plan(rp3, ci3, v3, (M, M))[0] == ROW_MAGIC
+    # rectangular operands never get it
+    rp4, ci4, v4 = _doc_topic(rng, 500, 10, 0, 100, 3)
+    assert build_host_plan(rp4[:401], ci4[:rp4[400]], v4[:rp4[400]], (400, 510))[0] == ROW_MAGIC
 
 
 def test_row_plan_when_no_hubs_or_forced():
@@ -171,7 +188,8 @@ def test_row_plan_when_no_hubs_or_forced():
     rp, ci, v = csr_ref.coo_to_csr(rows, cols, rng.standard_normal(20000).astype(np.float32), (2000, 2000))
     plan = build_host_plan(rp, ci, v, (2000, 2000))
     assert plan[0] == ROW_MAGIC, "uniform graph: no hubs -> row-unit plan"
-    rp, ci, v = _hubby(rng, 900, 900, 12, 700, 6)
+    rp, ci, v = _doc_topic(rng, 600, 12, 288, 500, 6)
+    assert build_host_plan(rp, ci, v, (900, 900))[0] == HUB_MAGIC
     assert build_host_plan(rp, ci, v, (900, 900), hub_min=-1)[0] == ROW_MAGIC
     # items are packed {col, value bits} right after the header in CSR order
     plan = build_host_plan(rp, ci, v, (900, 900), hub_min=-1)
@@ -206,6 +224,9 @@ def test_plan_bytes_is_exactly_the_built_image(kind):
     if kind == "mixed":
         rp, ci, v = _mixed_density_csr(rng, 900, 900)
         M = K = 900
+    elif kind == "hub":
+        rp, ci, v = _doc_topic(rng, 2000, 30, 900, 400, 5)
+        M = K = 2930
     else:
         M, K = 3001, 2003
         rp, ci, v = _random_csr(M, K, 20000, rng, heavy_rows=(5, 1700), heavy_deg=2500, empty_frac=0.2)
@@ -217,6 +238,7 @@ def test_plan_bytes_is_exactly_the_built_image(kind):
     rc = lib.gcnk_spmm_plan_build_host(rp.ctypes.data, ci.ctypes.data, v.ctypes.data, M, K, len(ci), 12, 1, 0.25,
                                        hub_min, 0, buf.ctypes.data, buf.nbytes)
     assert rc == 0, lib.gcnk_last_error()
+    assert (buf[0] == HUB_MAGIC) == (kind == "hub")
     assert np.all(buf[nbytes // 4:] == -7), "the build wrote past the size plan_bytes reported"
     # no plan word is -7 (ids >= -1, counts >= 0, float bits of -7 would be a NaN),
     # so a sentinel left in the last reported word means the size was too large

@@ -43,3 +43,15 @@ def golden_meta():
 def golden_logits():
     import numpy as np
     return dict(np.load(os.path.join(GOLDEN, "r8_logits.npz"), allow_pickle=False))
+
+
+@pytest.fixture(scope="session")
+def trained_golden():
+    """The reference's trained model (seed 50494, trainer.py:349-376) and its
+    eval logits: tests/golden/make_golden.py --trained-only."""
+    import numpy as np
+    import torch
+    z = np.load(os.path.join(GOLDEN, "r8_trained.npz"), allow_pickle=False)
+    sd = {k[3:]: torch.from_numpy(z[k].copy()) for k in z.files if k.startswith("sd_")}
+    return {"state_dict": sd, "logits": z["logits"], "test_acc": float(z["test_acc"]), "epochs": int(z["epochs"]),
+            "min_top2_gap": float(z["min_top2_gap"])}

@@ -11,10 +11,11 @@ Call sites exercised (all in the reference):
   build_graph.py:30-206   TopicGraphBuilder("R8", num_topics=50)  (LDA random_state 42)
   trainer.py:83-261       PrepareData  -> .adj (utils.py:185-203), .features (trainer.py:226-238)
   layer.py:126-190        GCN forward, eval and train mode (dropout consumes the CPU RNG)
-  trainer.py:264-406      TopicGCNTrainer.fit()/test()  (training-parity goldens)
+  trainer.py:264-406      TopicGCNTrainer.fit()/test()  (training-parity goldens; the trained
+                          state_dict + eval logits of seed 50494: tie-free labels)
   utils.py:185-213        preprocess_adj on tiny hand-made graphs (known-answer cases)
 
-Usage:  PYTHONHASHSEED=0 python tests/golden/make_golden.py [--skip-train]
+Usage:  PYTHONHASHSEED=0 python tests/golden/make_golden.py [--skip-train] [--trained-only]
 """
 import argparse
 import contextlib
@@ -135,9 +136,37 @@ def tiny_cases():
     return cases
 
 
+def trained_golden(trainer, layer, pre, out, quiet):
+    """The reference's TRAINED model (trainer.py:349-376, last epoch, the model
+    trainer.py:400-406 tests) for TRAIN_SEEDS[0]: its state_dict and its eval
+    logits on all nodes.  Trained logits have a clear top-2 gap (SURVEY §7:
+    ~2.5e-3), so predicted labels can be compared bit-exactly on EVERY row."""
+    import numpy as np
+    import torch as th
+    seed = TRAIN_SEEDS[0]
+    a = _args(seed)
+    with contextlib.redirect_stdout(quiet):
+        fw = trainer.TopicGCNTrainer(model=layer.GCN, args=a, pre_data=pre)
+        fw.fit()
+        res = fw.test()
+    fw.model.eval()
+    with th.no_grad():
+        lg = fw.model(fw.features, fw.adj).numpy()
+    srt = np.sort(lg, axis=1)
+    gap = srt[:, -1] - srt[:, -2]
+    sd = {k: v.detach().numpy() for k, v in fw.model.state_dict().items()}
+    np.savez_compressed(os.path.join(out, "r8_trained.npz"), logits=lg, seed=np.int64(seed),
+                        epochs=np.int64(len(fw.training_history)), test_acc=np.float64(res["acc"]),
+                        min_top2_gap=np.float64(gap.min()), **{"sd_" + k: v for k, v in sd.items()})
+    print(f"trained golden: seed {seed}, {len(fw.training_history)} epochs, test acc {res['acc']:.4f}, "
+          f"min top-2 gap {gap.min():.3e}")
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--skip-train", action="store_true")
+    ap.add_argument("--trained-only", action="store_true",
+                    help="only (re)write r8_trained.npz (the trained-weight golden)")
     ap.add_argument("--out", default=HERE)
     opts = ap.parse_args()
 
@@ -166,6 +195,9 @@ def main():
     adj = pre.adj
     feats = pre.features
     assert not adj.is_coalesced()
+    if opts.trained_only:
+        trained_golden(trainer, layer, pre, out, quiet)
+        return
     ai = adj._indices().numpy()
     av = adj._values().numpy()
     N = adj.shape[0]
@@ -279,6 +311,7 @@ def main():
             }
         meta["train_runs"] = runs
 
+        trained_golden(trainer, layer, pre, out, quiet)
     meta["tiny_cases"] = tiny_cases()
     with open(os.path.join(out, "r8_meta.json"), "w") as f:
         json.dump(meta, f, indent=1)

@@ -6,9 +6,10 @@ bit-exact):
   * SpMM / GEMM / colsum vs the float64 oracle: |err| <= 1e-5 * (1 + |ref|)
     scaled by the reduction length where stated;
   * GCN logits vs the reference's golden logits: max |err| <= 1e-4;
-  * predicted labels: identical for every row whose golden top-2 gap exceeds
-    2e-4 (a tie closer than the logit tolerance cannot be labelled
-    bit-exactly by any fp32 reordering; such rows are counted and reported).
+  * predicted labels: identical on EVERY row for the reference's trained model
+    (tests/golden/r8_trained.npz); for random-init weights, identical on every
+    row whose golden top-2 gap exceeds twice the measured max logit error
+    (the rows below it are counted and bounded).
 """
 import os
 
@@ -485,34 +486,56 @@ def test_colsum():
 # ------------------------------------------------------------------------------ GCN level
 
 def _labels_check(got, golden):
+    """Labels must agree on every row whose golden top-2 gap exceeds twice the
+    MEASURED max logit error (no error that small can reorder two logits
+    further apart); returns the number of rows below that gap."""
+    err = float(np.abs(got - golden).max())
     srt = np.sort(golden, axis=1)
     gap = srt[:, -1] - srt[:, -2]
-    decided = gap > 2 * LOGIT_TOL
+    decided = gap > 2 * err
     same = got.argmax(1) == golden.argmax(1)
-    assert np.all(same[decided]), f"{np.sum(~same[decided])} decided rows changed label"
+    assert np.all(same[decided]), f"{np.sum(~same[decided])} rows with top-2 gap > 2 x max err {err:.2e} changed label"
     return int(np.sum(~decided))
-
-
-# rows whose golden top-2 gap is <= 2e-4 (2x the logit tolerance): random-init
-# logits have near-ties no fp32 reordering can label bit-exactly; pinned per seed
-NEAR_TIES = {0: 11, 50494: 0, 99346: 29}
 
 
 @pytest.mark.parametrize("seed", [50494, 99346, 0])
 def test_gcn_eval_logits_match_reference(r8, golden_logits, seed):
+    """Random-init weights (the reference init for the seed): logits within
+    1e-4; labels identical wherever the golden gap exceeds 2x the measured
+    error (random-init logits have near-ties down to 1.25e-6)."""
     torch.manual_seed(seed)
     m = GCN(nfeat=r8["nfeat"], nhid=200, nclass=r8["nclass"], dropout=0.5).to(DEV)
     m.eval()
     with torch.no_grad():
         lg = m(r8["features"].to(DEV), r8["adj"].to(DEV)).cpu().numpy()
     gold = golden_logits[f"eval_{seed}"]
-    assert np.abs(lg - gold).max() <= LOGIT_TOL
+    err = float(np.abs(lg - gold).max())
+    assert err <= LOGIT_TOL
     undecided = _labels_check(lg, gold)
-    print(f"seed {seed}: labels bit-exact on {len(gold) - undecided} rows, {undecided} near-tie rows excluded, "
-          f"{int(np.sum(lg.argmax(1) != gold.argmax(1)))} labels differ overall")
-    assert undecided == NEAR_TIES[seed]
-    # even among the near ties, at most a handful may flip
-    assert int(np.sum(lg.argmax(1) != gold.argmax(1))) <= undecided
+    flips = int(np.sum(lg.argmax(1) != gold.argmax(1)))
+    print(f"seed {seed}: max err {err:.2e}; labels bit-exact on {len(gold) - undecided} rows; "
+          f"{undecided} rows within 2x that error of a tie; {flips} labels differ")
+    assert undecided <= 3 and flips <= undecided
+
+
+def test_trained_model_labels_bit_exact_on_every_row(r8, trained_golden):
+    """The reference's TRAINED model (seed 50494, 72 epochs; its min top-2 gap
+    is 5.1e-3) loaded into the HIP GCN: logits within 1e-4 and the predicted
+    label of EVERY node identical to the reference's -- no exclusions -- so
+    the test accuracy is the reference's to the last document."""
+    m = GCN(nfeat=r8["nfeat"], nhid=200, nclass=r8["nclass"], dropout=0.5).to(DEV)
+    m.load_state_dict(trained_golden["state_dict"])
+    m.eval()
+    with torch.no_grad():
+        lg = m(r8["features"].to(DEV), r8["adj"].to(DEV)).cpu().numpy()
+    gold = trained_golden["logits"]
+    err = float(np.abs(lg - gold).max())
+    print(f"trained model: max logit err {err:.2e}")
+    assert err <= LOGIT_TOL
+    assert np.array_equal(lg.argmax(1), gold.argmax(1)), f"{int(np.sum(lg.argmax(1) != gold.argmax(1)))} labels differ"
+    test = np.asarray(r8["test_lst"])
+    acc = float(np.mean(lg[test].argmax(1) == np.asarray(r8["target"])[test]))
+    assert acc == trained_golden["test_acc"]
 
 
 def test_graph_convolution_without_bias_forward_backward(r8):

@@ -126,3 +126,20 @@ def test_oracle_training_run_matches_reference(r8, golden_meta):
     assert len(hist) == run["epochs"]
     assert [h["train_loss"] for h in hist] == [h["train_loss"] for h in run["history"]]
     assert test["acc"] == run["test"]["acc"]
+
+
+def test_oracle_trained_model_logits_bit_exact(r8, golden_meta, trained_golden):
+    """The reference's trained state_dict (seed 50494, the run r8_meta.json
+    records) through the oracle's restatement reproduces the reference's eval
+    logits bit for bit, and its test accuracy; the golden's labels are tie-free."""
+    assert trained_golden["epochs"] == golden_meta["train_runs"]["50494"]["epochs"]
+    assert trained_golden["min_top2_gap"] > 1e-3
+    m = gcn_ref.RefGCN(nfeat=r8["nfeat"], nhid=200, nclass=r8["nclass"], dropout=0.5)
+    m.load_state_dict(trained_golden["state_dict"])
+    m.eval()
+    with torch.no_grad():
+        lg = m(r8["features"], r8["adj"]).numpy()
+    assert np.array_equal(lg, trained_golden["logits"])
+    test = np.asarray(r8["test_lst"])
+    acc = float(np.mean(lg[test].argmax(1) == np.asarray(r8["target"])[test]))
+    assert acc == trained_golden["test_acc"] == golden_meta["train_runs"]["50494"]["test"]["acc"]

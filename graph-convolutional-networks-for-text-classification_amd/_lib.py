@@ -10,10 +10,27 @@ import os
 import threading
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
-LIB_PATH = os.path.join(_HERE, "libgcnk.so")
-# experiment scripts may point at a prebuilt variant (csrc/Makefile `variant`);
-# the tests and the product always load the in-tree library
-LIB_PATH = os.environ.get("GCNK_LIB", LIB_PATH)
+PRODUCT_LIB = os.path.join(_HERE, "libgcnk.so")
+VARIANT_DIR = os.path.join(os.path.dirname(_HERE), "_variants")
+
+
+def _resolve_lib():
+    """The in-tree library, unless GCNK_LIB names an experiment variant built by
+    `make -C <pkg>/csrc variant` (it must live in <repo>/_variants/; anything
+    else is refused, so a stale export cannot swap in a foreign binary).  A
+    variant is announced on stderr; tests/conftest.py refuses to run on one."""
+    want = os.environ.get("GCNK_LIB")
+    if not want:
+        return PRODUCT_LIB
+    path = os.path.realpath(want)
+    if os.path.dirname(path) != os.path.realpath(VARIANT_DIR):
+        raise RuntimeError(f"GCNK_LIB={want}: only experiment variants in {VARIANT_DIR} may replace {PRODUCT_LIB}")
+    import sys
+    print(f"[gcnk] loading experiment variant {path} (not the product library)", file=sys.stderr)
+    return path
+
+
+LIB_PATH = _resolve_lib()
 ABI_VERSION = 2
 
 # C-ABI return codes (gcnk.h)
@@ -139,4 +156,4 @@ def check(rc, what):
     if rc != OK:
         msg = load().gcnk_last_error().decode(errors="replace")
         kind = {EARG: "bad argument", EUNSUP: "unsupported", EHIP: "HIP error"}.get(rc, "error")
-        raise GcnkError(f"{what} failed ({kind}, rc={rc}): {msg}")
+        raise GcnkError(f"{what} failed ({kind}, rc={rc}): {msg} [{LIB_PATH}]")

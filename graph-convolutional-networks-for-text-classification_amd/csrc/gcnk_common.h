@@ -143,7 +143,8 @@ int hub_plan_host(const int32_t* rowptr, const int32_t* colind, const float* val
                   int32_t groups, int32_t hub_min, int32_t block_rows, std::vector<int32_t>& img);
 int64_t hub_plan_words(const int32_t* hdr);
 int64_t hub_workspace_bytes(const int32_t* hdr, int32_t F);
+int64_t hub_counter_bytes(const int32_t* hdr);
 int hub_spmm(const void* plan, const int32_t* hdr, const float* B, int64_t ldb, int32_t F, float* C, int64_t ldc,
-             const Epi& e, float* workspace, bool vec4, hipStream_t s);
+             const Epi& e, float* workspace, int32_t* counters, bool vec4, hipStream_t s);
 
 }  // namespace gcnk

@@ -45,19 +45,23 @@ namespace gcnk {
 namespace {
 
 #ifndef GCNK_HUB_BLOCK
-#define GCNK_HUB_BLOCK 256
+#define GCNK_HUB_BLOCK 1024
 #endif
 #ifndef GCNK_HUB_SLICE_VECS
 #define GCNK_HUB_SLICE_VECS 8
 #endif
 constexpr int kGroupBlock = GCNK_HUB_BLOCK;      // threads per row-group workgroup
 constexpr int kSliceVecs = GCNK_HUB_SLICE_VECS;  // column vectors per slice (launch choice)
-constexpr int kSumBlock = 256;        // threads per hub-sum workgroup
 constexpr int kMaxHub = 256;          // hub rows per plan
 constexpr int kMaxGroupRows = 512;    // light rows per group
 constexpr int kMaxSlices = 64;        // column slices per launch
 constexpr int kLdsMax = 163840;       // gfx950: 160 KiB per workgroup
 constexpr int kTargetBlocks = 256;    // row-group workgroups per launch (one per CU)
+constexpr int kLightBatch = 4;        // items per light-row batch (plan pads light rows to a multiple)
+constexpr int kHubBatch = 8;          // items per hub batch (plan pads each hub's items to a multiple)
+constexpr int kCombineChunks = 8;     // hub-row chunks per column slice, combined by the last 8 arrivals
+constexpr int kCombineLanes = 16;     // lanes summing one combined output's partials (power of two)
+constexpr int kCombineSpins = 1 << 12;  // poll bound of a waiting combiner (then the last arrival takes over)
 
 __host__ __device__ inline int64_t align4(int64_t x) { return (x + 3) & ~3LL; }
 
@@ -67,19 +71,25 @@ __host__ __device__ inline int64_t align4(int64_t x) { return (x + 3) & ~3LL; }
 //               4 G (row groups)  5 R (record stride, words)  6 H (hub rows)
 //               7 h0 (first hub row)  8 nL (light rows)  9 nnz  10 gs (light
 //               rows per group)  11 hub degree threshold  12 max items per
-//               record  13..15 0
+//               record  13 max hub batches per record  14..15 0
 //   records[G][R]
 // Record of group g (light rows l = g * gs + i, i < n):
-//   0 n  1 nout (= n + H)  2 nitems  3 0
-//   4 .. 4 + nout   item offsets: output k's items are [off[k], off[k + 1])
-//                   (outputs 0..n-1: the light rows; n + t: hub t's partial)
-//   o_it = align4(5 + nout):  items int2 {slot, value bits}, CSR column order;
-//                   slot t < H: hub row h0 + t of B; slot H + i: light row i
-//                   of the group (its own diagonal, or a hub's nonzero on it)
+//   0 n  1 nhb (hub batches)  2 nitems  3 o_it (word offset of the items)
+//   4 ..           light entries int2 {i | batches << 16, first item}, sorted
+//                  by batch count (so a wave's lanes walk the same number);
+//                  a light row's items: kLightBatch-item batches
+//   4 + 2n ..      hub batch entries int2 {t, first item}: kHubBatch items
+//                  each, hub-major (hub t's nonzeros over the group's rows in
+//                  CSR order, then its hub x hub nonzeros when t % G == g)
+//   4 + 2n + 2nhb  hub batch offsets [H + 1]: hub t's batches are
+//                  [off[t], off[t + 1])
+//   o_it           items int2 {slot, value bits}, CSR column order; slot t < H:
+//                  hub row h0 + t of B; slot H + i: light row i of the group;
+//                  padding {H + n, 0} (slot H + n: a zero row of the LDS image)
 struct HubLayout {
-  int64_t G, R, H, h0, nL, gs, total;
+  int64_t G, R, H, h0, nL, gs, max_hb, total;
   explicit HubLayout(const int32_t* h) {
-    G = h[4]; R = h[5]; H = h[6]; h0 = h[7]; nL = h[8]; gs = h[10];
+    G = h[4]; R = h[5]; H = h[6]; h0 = h[7]; nL = h[8]; gs = h[10]; max_hb = h[13];
     total = 16 + G * R;
   }
 };
@@ -96,20 +106,156 @@ __device__ __forceinline__ void lds_dma4(const void* gsrc, void* lds_wave) {
   __builtin_amdgcn_global_load_lds(const_cast<void*>(gsrc), (__attribute__((address_space(3))) void*)lds_wave, 4, 0, 0);
 }
 
+// Coherent (sc1) raw-buffer accesses from a wave-uniform base: the hub
+// partials are handed from every group's workgroup to the combining ones in
+// the same launch, stored write-through and loaded past L1
+// (MI355X_MICROARCH.md, valid hand-off forms: sc1 stores drained by every
+// storing wave, one lane's agent-scope add per workgroup, sc1 loads).
+typedef float f32v4 __attribute__((ext_vector_type(4)));
+constexpr int kBufSc1 = 16;             // cache-policy aux bit sc1 (gfx950)
+constexpr int kBufDword3 = 0x00020000;  // raw buffer resource word 3 (gfx9)
+__device__ __forceinline__ __amdgpu_buffer_rsrc_t rsrc(const float* base_uniform) {
+  return __builtin_amdgcn_make_buffer_rsrc(const_cast<float*>(base_uniform), (short)0, 0x7fffffff, kBufDword3);
+}
+__device__ __forceinline__ const float* uniform_ptr(const float* p) {
+  const uint64_t u = reinterpret_cast<uint64_t>(p);
+  const uint32_t lo = __builtin_amdgcn_readfirstlane((uint32_t)u), hi = __builtin_amdgcn_readfirstlane((uint32_t)(u >> 32));
+  return reinterpret_cast<const float*>(((uint64_t)hi << 32) | lo);
+}
+__device__ __forceinline__ void store_sc1(const float* base, int64_t off, const float4& v) {
+  const f32v4 x = {v.x, v.y, v.z, v.w};
+  __builtin_amdgcn_raw_buffer_store_b128(x, rsrc(base), (int)(off * 4), 0, kBufSc1);
+}
+__device__ __forceinline__ void store_sc1(const float* base, int64_t off, const float& v) {
+  __builtin_amdgcn_raw_buffer_store_b32(__float_as_uint(v), rsrc(base), (int)(off * 4), 0, kBufSc1);
+}
+template <typename T>
+__device__ __forceinline__ T load_sc1(const float* base, int64_t off);
+template <>
+__device__ __forceinline__ float4 load_sc1<float4>(const float* base, int64_t off) {
+  const f32v4 x = __builtin_amdgcn_raw_buffer_load_b128(rsrc(base), (int)(off * 4), 0, kBufSc1);
+  return make_float4(x.x, x.y, x.z, x.w);
+}
+template <>
+__device__ __forceinline__ float load_sc1<float>(const float* base, int64_t off) {
+  return __uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(rsrc(base), (int)(off * 4), 0, kBufSc1));
+}
+
+// In-launch combine of the hub rows of column slice c.  Counter region
+// (uint64, zeroed once, never reset -- every value is relative to the launch
+// count, so consecutive launches on one stream need no clearing):
+//   ctr[c]                 arrivals at slice c, + G per launch
+//   ctr[kMaxSlices + c*K + q]  launch count at which chunk q of slice c was
+//                              last combined (claim word)
+// Every workgroup of slice c adds 1 after its partials are stored (drained).
+// The last K arrivals of a launch each combine one chunk of the H hub rows
+// (K = 8, or 1 -- the last arrival alone, nobody waits -- when the grid has
+// more workgroups than the device has CUs, so a waiter could hold a CU that a
+// workgroup it waits for needs)
+// (ranks G-K .. G-1 -> chunks 0 .. K-1) once all G have arrived; the very
+// last arrival (which never waits) also takes over every chunk nobody has
+// claimed, so a waiter that gives up (bounded poll) loses nothing.  A chunk
+// is claimed by a compare-and-swap of its claim word from the launch count
+// to launch count + 1: exactly one claimant per launch.  Chunk sums run in
+// group order (fixed): the result does not depend on who combines.
+template <int VEC>
+__device__ __forceinline__ void hub_combine(uint64_t* ctr, int32_t K, int32_t* s_scr, int32_t G, int32_t c, int32_t h0,
+                                            int32_t H, int32_t w, int32_t q0, const float* part_u, int64_t part_ld,
+                                            float* C, int64_t ldc, const Epi& epi,
+                                            const typename Vec<VEC>::T* s_bias, int tid) {
+  using V = Vec<VEC>;
+  using T = typename V::T;
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // this wave's partial stores have landed
+  __syncthreads();                                   // ... and every other wave's
+  uint64_t* cnt = ctr + c;
+  __shared__ uint64_t s_old;
+  __shared__ int32_t s_flag;
+  if (tid == 0) s_old = __hip_atomic_fetch_add(cnt, (uint64_t)1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  __syncthreads();
+  const uint64_t old = s_old;
+  const uint64_t launch = old / (uint64_t)G;
+  const int32_t rank = (int32_t)(old - launch * (uint64_t)G);
+  if (rank < G - K) return;
+  const int32_t q_own = rank - (G - K);
+  const bool last = rank == G - 1;
+  if (!last) {
+    if (tid == 0) {
+      const uint64_t target = (launch + 1) * (uint64_t)G;
+      int32_t ok = 0;
+      for (int32_t spin = 0; spin < kCombineSpins; ++spin) {
+        if (__hip_atomic_load(cnt, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) >= target) {
+          ok = 1;
+          break;
+        }
+        __builtin_amdgcn_s_sleep(4);
+      }
+      s_flag = ok;
+    }
+    __syncthreads();
+    if (!s_flag) return;  // gave up: the last arrival combines this chunk
+  }
+  uint64_t* claim = ctr + kMaxSlices + (int64_t)c * kCombineChunks;
+  // chunk order: own chunk first, then (last arrival only) all the others
+  for (int32_t k = 0; k < (last ? K : 1); ++k) {
+    const int32_t q = (q_own + k) % K;
+    __syncthreads();  // s_flag reuse
+    if (tid == 0) {
+      uint64_t expect = launch;
+      s_flag = __hip_atomic_compare_exchange_strong(claim + q, &expect, launch + 1, __ATOMIC_RELAXED, __ATOMIC_RELAXED,
+                                                    __HIP_MEMORY_SCOPE_AGENT) ? 1 : 0;
+    }
+    __syncthreads();
+    if (!s_flag) continue;
+    // chunk q: hubs [t0, t1) x the slice's w vectors; PL lanes per output,
+    // lane p summing groups [p G / PL, (p + 1) G / PL) in order, then a
+    // fixed-order LDS tree over the PL lanes
+    const int32_t t0 = (int32_t)((int64_t)q * H / K), t1 = (int32_t)((int64_t)(q + 1) * H / K);
+    const int32_t nout = (t1 - t0) * w;
+    constexpr int PL = kCombineLanes;
+    T* s_red = reinterpret_cast<T*>(s_scr);
+    for (int32_t o0 = 0; o0 < nout; o0 += kGroupBlock / PL) {
+      const int32_t o = o0 + tid / PL, p = tid % PL;
+      T acc = V::zero();
+      if (o < nout) {
+        const int32_t t = t0 + o / w, j = o % w;
+        const int64_t base = (int64_t)t * G * part_ld + (int64_t)(q0 + j) * VEC;
+        const int32_t ga = (int32_t)((int64_t)p * G / PL), gb = (int32_t)((int64_t)(p + 1) * G / PL);
+        for (int32_t gg = ga; gg < gb; ++gg) V::add(acc, load_sc1<T>(part_u, base + (int64_t)gg * part_ld));
+      }
+      s_red[tid] = acc;
+      __syncthreads();
+#pragma unroll
+      for (int sh = PL / 2; sh >= 1; sh >>= 1) {
+        if (p < sh) V::add(s_red[tid], s_red[tid + sh]);
+        __syncthreads();
+      }
+      if (p == 0 && o < nout) {
+        const int32_t t = t0 + o / w, j = o % w;
+        const int64_t row = (int64_t)h0 + t, cv = (int64_t)(q0 + j) * VEC;
+        const T bv = epi.bias ? s_bias[j] : V::zero();
+        V::store(C + row * ldc + cv, V::epi(epi, s_red[tid], bv, row, cv));
+      }
+      __syncthreads();
+    }
+  }
+}
+
 // ---------------------------------------------------------------------------
 // Row-group kernel.  Grid G * nslices, block (g, c) = (b % G, b / G).
-// LDS: record [R words] | rows [(H + n) x w] vectors (slot-major) | bias [w].
+// LDS: record [R words] | rows [(H + n) x w] vectors (slot-major) | zero row [w] |
+// bias [w] | hub batch sums [nhb x w].
 template <int VEC>
 __global__ void __launch_bounds__(kGroupBlock)
-hub_group_kernel(const int32_t* __restrict__ recs, int32_t R, int32_t G, int32_t gs, int32_t h0, int32_t H, int32_t nL,
+hub_group_kernel(const int32_t* __restrict__ recs, int32_t R, int32_t roff, int32_t G, int32_t gs, int32_t h0, int32_t H, int32_t nL,
                  int32_t nslices, const float* __restrict__ B, int64_t ldb, int32_t F, float* __restrict__ C,
-                 int64_t ldc, Epi epi, float* __restrict__ part, int64_t part_ld) {
+                 int64_t ldc, Epi epi, float* __restrict__ part, int64_t part_ld, uint64_t* __restrict__ ctr, int32_t K) {
   using V = Vec<VEC>;
   using T = typename V::T;
   extern __shared__ __attribute__((aligned(16))) int32_t smem[];
   int32_t* s_rec = smem;
-  T* s_rows = reinterpret_cast<T*>(smem + R);
-  const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
+  T* s_rows = reinterpret_cast<T*>(smem + roff);  // roff >= R: the record area doubles as the combine's scratch
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int wv = __builtin_amdgcn_readfirstlane(tid >> 6);  // wave-uniform (the compiler cannot tell)
   constexpr int NW = kGroupBlock / 64;
   const int g = blockIdx.x % G, c = blockIdx.x / G;
   const int32_t Q = VEC == 4 ? F / 4 : F;  // column vectors of a row
@@ -139,86 +285,123 @@ hub_group_kernel(const int32_t* __restrict__ recs, int32_t R, int32_t G, int32_t
         lds_dma4(src, s_rows + e0);
     }
   }
-  // the bias slice, so the output loop issues no global load (one there would
-  // make every iteration wait for all the stores issued before it)
-  T* s_bias = s_rows + ne;
+  // slot H + n: the zero row the plan's padding items read; then the bias
+  // slice, so the output loop issues no global load (one there would make
+  // every iteration wait for all the stores issued before it)
+  if (tid < w) s_rows[ne + tid] = V::zero();
+  T* s_bias = s_rows + ne + w;
   if (epi.bias && tid < w) s_bias[tid] = V::load(epi.bias + (int64_t)(q0 + tid) * VEC);
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   __syncthreads();
   stamp(epi, 1);
 
-  // ---- outputs: task e = o * w + j (output o, column vector j of the slice)
-  const int32_t nout = s_rec[1];
-  const int32_t o_it = (int32_t)align4(5 + nout);
+  // ---- outputs.  Light rows and hub batches run on separate waves,
+  //      concurrently, split by their item counts.  A task is (row or batch,
+  //      column vector j of the slice); its items are read a batch at a time,
+  //      then the batch's row vectors, so it waits for two LDS round trips per
+  //      batch.  Light rows are sorted by batch count (the lanes of a wave walk
+  //      alike); hub batches are all kHubBatch long, summed per hub afterwards.
+  const int32_t nhb = s_rec[1], o_it = s_rec[3];
   const int2* s_items = reinterpret_cast<const int2*>(s_rec + o_it);
-  const int32_t nt = nout * w;
-  for (int32_t e = tid; e < nt; e += kGroupBlock) {
-    const int32_t o = e / w, j = e - o * w;
-    const int32_t ib = s_rec[4 + o], ie = s_rec[5 + o];
-    const T* col = s_rows + j;
-    T acc = V::zero();
-#pragma unroll 4
-    for (int32_t k = ib; k < ie; ++k) {
-      const int2 it = s_items[k];
-      V::fma(acc, __int_as_float(it.y), col[it.x * w]);
+  const int2* s_light = reinterpret_cast<const int2*>(s_rec + 4);
+  const int2* s_hb = s_light + n;
+  const int32_t* s_hoff = s_rec + 4 + 2 * n + 2 * nhb;
+  T* s_hsum = s_bias + w;
+  const int32_t il = nhb > 0 ? s_hb[0].y : s_rec[2], ih = s_rec[2] - il;  // light / hub items
+  int nwh = 0;
+  if (nhb > 0) {
+    nwh = (int)(((int64_t)NW * ih + (il + ih) / 2) / max(il + ih, 1));
+    nwh = min(max(nwh, 1), NW - 1);
+  }
+  const bool hub_wave = wv < nwh;
+  if (hub_wave) {
+    for (int32_t e = wv * 64 + lane; e < nhb * w; e += nwh * 64) {
+      const int32_t b = e / w, j = e - b * w;
+      const int4* ip = reinterpret_cast<const int4*>(s_items + s_hb[b].y);
+      const T* col = s_rows + j;
+      int4 p[kHubBatch / 2];
+#pragma unroll
+      for (int u = 0; u < kHubBatch / 2; ++u) p[u] = ip[u];
+      T r[kHubBatch];
+#pragma unroll
+      for (int u = 0; u < kHubBatch / 2; ++u) {
+        r[2 * u] = col[p[u].x * w];
+        r[2 * u + 1] = col[p[u].z * w];
+      }
+      T acc = V::zero();
+#pragma unroll
+      for (int u = 0; u < kHubBatch / 2; ++u) {
+        V::fma(acc, __int_as_float(p[u].y), r[2 * u]);
+        V::fma(acc, __int_as_float(p[u].w), r[2 * u + 1]);
+      }
+      s_hsum[e] = acc;
     }
-    const int64_t cv = (int64_t)(q0 + j) * VEC;
-    if (o < n) {
-      const int64_t row = light_row(l0 + o, h0, H);
+  } else {
+    for (int32_t e = (wv - nwh) * 64 + lane; e < n * w; e += (NW - nwh) * 64) {
+      const int32_t lo = e / w, j = e - lo * w;
+      const int2 le = s_light[lo];
+      const int32_t i = le.x & 0xffff, nb = le.x >> 16;
+      const int4* ip = reinterpret_cast<const int4*>(s_items + le.y);
+      const T* col = s_rows + j;
+      T acc = V::zero();
+#if defined(GCNK_HUB_EXP) && (GCNK_HUB_EXP & 4)  // ablation: no item loop
+      for (int32_t b = 0; b < 0; ++b) {
+#else
+      for (int32_t b = 0; b < nb; ++b) {
+#endif
+        int4 p[kLightBatch / 2];
+#pragma unroll
+        for (int u = 0; u < kLightBatch / 2; ++u) p[u] = ip[u];
+        ip += kLightBatch / 2;
+        T r[kLightBatch];
+#pragma unroll
+        for (int u = 0; u < kLightBatch / 2; ++u) {
+          r[2 * u] = col[p[u].x * w];
+          r[2 * u + 1] = col[p[u].z * w];
+        }
+#pragma unroll
+        for (int u = 0; u < kLightBatch / 2; ++u) {
+          V::fma(acc, __int_as_float(p[u].y), r[2 * u]);
+          V::fma(acc, __int_as_float(p[u].w), r[2 * u + 1]);
+        }
+      }
+#if defined(GCNK_HUB_EXP) && (GCNK_HUB_EXP & 1)  // ablation: no light stores
+      if (reinterpret_cast<const float*>(&acc)[0] == 1234.5f) V::store(C, acc);  // keeps the sum live
+      continue;
+#endif
+      const int64_t cv = (int64_t)(q0 + j) * VEC;
+      const int64_t row = light_row(l0 + i, h0, H);
       const T bv = epi.bias ? s_bias[j] : V::zero();
       V::store_aligned(C + row * ldc + cv, V::epi(epi, acc, bv, row, cv));
-    } else {
-      V::store_aligned(part + ((int64_t)(o - n) * G + g) * part_ld + cv, acc);
     }
   }
-  stamp(epi, 2);
+#ifdef GCNK_STAMPS
+  // 2: the first hub wave done, 3: the last light wave done (no barrier: the
+  // two wave sets' own finishing times)
+  if (epi.stamps && lane == 0 && (wv == 0 || wv == NW - 1)) {
+    const unsigned long long t = __builtin_amdgcn_s_memrealtime();
+    epi.stamps[4 * (unsigned long long)blockIdx.x + (wv == 0 ? 2 : 3)] = t;
+  }
+#endif
+  __syncthreads();
+  // ---- this group's hub partials (hub t's batch sums in batch order), stored
+  //      write-through (sc1) for the in-launch combine below
+  const float* part_u = uniform_ptr(part);
+  for (int32_t e = tid; e < H * w; e += kGroupBlock) {
+    const int32_t t = e / w, j = e - t * w;
+    T acc = V::zero();
+    for (int32_t b = s_hoff[t]; b < s_hoff[t + 1]; ++b) V::add(acc, s_hsum[b * w + j]);
+#if defined(GCNK_HUB_EXP) && (GCNK_HUB_EXP & 2)  // ablation: no partial stores
+    if (reinterpret_cast<const float*>(&acc)[0] == 1234.5f) V::store(C, acc);
+    continue;
+#endif
+    store_sc1(part_u, ((int64_t)t * G + g) * part_ld + (int64_t)(q0 + j) * VEC, acc);
+  }
+  hub_combine<VEC>(ctr, K, s_rec, G, c, h0, H, w, q0, part_u, part_ld, C, ldc, epi, s_bias, tid);
 }
 
-// Hub rows: C[h0 + t] = epi(sum over g of part[t][g] in group order).  Grid
-// (H, column tiles of LQ vectors); PL = kSumBlock / LQ partial lanes, lane p
-// sums groups [p G / PL, (p + 1) G / PL) in order, then a fixed-order LDS tree.
-template <int VEC, int LQ>
-__global__ void __launch_bounds__(kSumBlock)
-hub_sum_kernel(const float* __restrict__ part, int64_t part_ld, int32_t G, int32_t h0, int32_t F,
-               float* __restrict__ C, int64_t ldc, Epi epi) {
-  using V = Vec<VEC>;
-  using T = typename V::T;
-  constexpr int PL = kSumBlock / LQ;
-  constexpr int U = 8;
-  __shared__ T s_red[PL][LQ];
-  const int tid = threadIdx.x, p = tid / LQ, lq = tid % LQ;
-  const int32_t t = blockIdx.x;
-  const int32_t Q = VEC == 4 ? F / 4 : F;
-  const int32_t j = blockIdx.y * LQ + lq;
-  const bool ok = j < Q;
-  const int64_t cv = (int64_t)(ok ? j : 0) * VEC;
-  const T bv = (epi.bias && ok) ? V::load(epi.bias + cv) : V::zero();  // first: no wait behind the partials
-  const int32_t g0 = (int32_t)((int64_t)p * G / PL), g1 = (int32_t)((int64_t)(p + 1) * G / PL);
-  const float* p0 = part + (int64_t)t * G * part_ld + cv;
-  T acc = V::zero();
-  for (int32_t gb = g0; gb < g1; gb += U) {
-    T pv[U];
-#pragma unroll
-    for (int u = 0; u < U; ++u) pv[u] = V::load(p0 + (int64_t)min(gb + u, g1 - 1) * part_ld);
-#pragma unroll
-    for (int u = 0; u < U; ++u) {
-      T x = acc;
-      V::add(x, pv[u]);
-      if (gb + u < g1) acc = x;
-    }
-  }
-  s_red[p][lq] = acc;
-  __syncthreads();
-#pragma unroll
-  for (int s = PL / 2; s >= 1; s >>= 1) {
-    if (p < s) V::add(s_red[p][lq], s_red[p + s][lq]);
-    __syncthreads();
-  }
-  if (p == 0 && ok) {
-    const int64_t row = (int64_t)h0 + t;
-    V::store(C + row * ldc + cv, V::epi(epi, s_red[0][lq], bv, row, cv));
-  }
-}
+// LDS words before the row image: the record, at least the combine's scratch
+int64_t rec_words(const HubLayout& L) { return std::max<int64_t>(L.R, 4 * kGroupBlock); }
 
 // Column slices for a launch: about 8 vectors per slice (R8 F = 200: 7 slices
 // of 7-8 float4), then more until the LDS image fits.
@@ -226,7 +409,7 @@ int64_t choose_slices(const HubLayout& L, int32_t Q, size_t vbytes, int64_t* lds
   int64_t c = std::max<int64_t>(1, std::min<int64_t>(kMaxSlices, (Q + kSliceVecs - 1) / kSliceVecs));
   for (; c <= std::min<int64_t>(Q, kMaxSlices); ++c) {
     const int64_t w = (Q + c - 1) / c;
-    const int64_t lds = L.R * 4 + (L.H + L.gs + 1) * w * (int64_t)vbytes;
+    const int64_t lds = rec_words(L) * 4 + (L.H + L.gs + 2 + L.max_hb) * w * (int64_t)vbytes;
     if (lds <= kLdsMax) {
       *lds_out = lds;
       return c;
@@ -235,44 +418,36 @@ int64_t choose_slices(const HubLayout& L, int32_t Q, size_t vbytes, int64_t* lds
   return -1;
 }
 
-template <int VEC, int LQ>
-int launch_sum(const float* part, int64_t part_ld, const HubLayout& L, int32_t F, float* C, int64_t ldc, const Epi& e,
-               hipStream_t s) {
-  const int32_t Q = VEC == 4 ? F / 4 : F;
-  hipLaunchKernelGGL((hub_sum_kernel<VEC, LQ>), dim3((unsigned)L.H, (unsigned)((Q + LQ - 1) / LQ)), dim3(kSumBlock), 0,
-                     s, part, part_ld, (int32_t)L.G, (int32_t)L.h0, F, C, ldc, e);
-  return launch_check("hub_sum_kernel");
-}
-
 template <int VEC>
 int hub_launch(const int32_t* plan, const HubLayout& L, const float* B, int64_t ldb, int32_t F, float* C, int64_t ldc,
-               const Epi& e, float* part, int64_t part_ld, hipStream_t s) {
+               const Epi& e, float* part, int64_t part_ld, uint64_t* ctr, hipStream_t s) {
   const int32_t Q = VEC == 4 ? F / 4 : F;
   int64_t lds = 0;
   const int64_t nslices = choose_slices(L, Q, sizeof(typename Vec<VEC>::T), &lds);
-  if (nslices < 0 || L.G * nslices > INT32_MAX) {
+  if (nslices < 0 || nslices > kMaxSlices || L.G * nslices > INT32_MAX) {
     set_error("gcnk_spmm (hub plan): F = %d does not fit %lld hub + %lld group rows of LDS", F, (long long)L.H,
               (long long)L.gs);
     return GCNK_EUNSUP;
   }
+  // one workgroup per CU (the in-launch hand-off is the form measured at one
+  // workgroup per CU; 1024 threads and > 80 KB of LDS admit no second)
+  lds = std::max<int64_t>(lds, kLdsMax / 2 + 16);
   static std::once_flag once;
   std::call_once(once, [] {
     (void)hipFuncSetAttribute(reinterpret_cast<const void*>(&hub_group_kernel<VEC>),
                               hipFuncAttributeMaxDynamicSharedMemorySize, kLdsMax);
   });
+  static int cus = [] {
+    int dev = 0, n = 0;
+    if (hipGetDevice(&dev) != hipSuccess || hipDeviceGetAttribute(&n, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess)
+      n = 0;
+    return n;
+  }();
+  const int32_t K = L.G * nslices <= cus ? (int32_t)std::min<int64_t>(kCombineChunks, L.G) : 1;
   hipLaunchKernelGGL((hub_group_kernel<VEC>), dim3((unsigned)(L.G * nslices)), dim3(kGroupBlock), (size_t)lds, s,
-                     plan + 16, (int32_t)L.R, (int32_t)L.G, (int32_t)L.gs, (int32_t)L.h0, (int32_t)L.H, (int32_t)L.nL,
-                     (int32_t)nslices, B, ldb, F, C, ldc, e, part, part_ld);
-  int rc = launch_check("hub_group_kernel");
-  if (rc) return rc;
-  Epi eb = e;  // debug stamps of the sum kernel follow the group kernel's
-  if (eb.stamps) eb.stamps += 4 * L.G * nslices;
-  if (Q > 32) return launch_sum<VEC, 64>(part, part_ld, L, F, C, ldc, eb, s);
-  if (Q > 16) return launch_sum<VEC, 32>(part, part_ld, L, F, C, ldc, eb, s);
-  if (Q > 8) return launch_sum<VEC, 16>(part, part_ld, L, F, C, ldc, eb, s);
-  if (Q > 4) return launch_sum<VEC, 8>(part, part_ld, L, F, C, ldc, eb, s);
-  if (Q > 2) return launch_sum<VEC, 4>(part, part_ld, L, F, C, ldc, eb, s);
-  return launch_sum<VEC, 2>(part, part_ld, L, F, C, ldc, eb, s);
+                     plan + 16, (int32_t)L.R, (int32_t)rec_words(L), (int32_t)L.G, (int32_t)L.gs, (int32_t)L.h0, (int32_t)L.H, (int32_t)L.nL,
+                     (int32_t)nslices, B, ldb, F, C, ldc, e, part, part_ld, ctr, K);
+  return launch_check("hub_group_kernel");
 }
 
 }  // namespace
@@ -337,21 +512,29 @@ int hub_plan_host(const int32_t* rp, const int32_t* ci, const float* vv, int32_t
     }
   }
   std::vector<std::vector<int32_t>> recs((size_t)G);
-  int64_t R = 4, max_items = 0;
+  int64_t R = 4, max_items = 0, max_hb = 0;
+  std::vector<int64_t> ord;
   for (int64_t g = 0; g < G; ++g) {
-    const int64_t l0 = g * gs, n = std::min(gs, nL - l0), nout = n + H;
-    int64_t nit = 0;
-    for (int64_t i = 0; i < n; ++i) {
+    const int64_t l0 = g * gs, n = std::min(gs, nL - l0);
+    auto light_batches = [&](int64_t i) {
       const int64_t r = light_row_host(l0 + i, h0, H);
-      nit += (int64_t)rp[r + 1] - rp[r];
+      return ((int64_t)rp[r + 1] - rp[r] + kLightBatch - 1) / kLightBatch;
+    };
+    int64_t nit = 0, nhb = 0;
+    for (int64_t i = 0; i < n; ++i) nit += light_batches(i) * kLightBatch;
+    for (int64_t t = 0; t < H; ++t) {
+      const int64_t b = ((int64_t)hub_k[(size_t)(g * H + t)].size() + kHubBatch - 1) / kHubBatch;
+      nhb += b;
+      nit += b * kHubBatch;
     }
-    for (int64_t t = 0; t < H; ++t) nit += (int64_t)hub_k[(size_t)(g * H + t)].size();
-    const int64_t o_it = align4(5 + nout);
+    if (n >= 65536 || light_batches(0) >= 32768) return 1;
+    const int64_t o_it = align4(4 + 2 * n + 2 * nhb + H + 1);
     std::vector<int32_t>& w = recs[(size_t)g];
     w.assign((size_t)align4(o_it + 2 * nit), 0);
     w[0] = (int32_t)n;
-    w[1] = (int32_t)nout;
+    w[1] = (int32_t)nhb;
     w[2] = (int32_t)nit;
+    w[3] = (int32_t)o_it;
     int64_t it = 0;
     auto item = [&](int64_t col, int64_t k) {
       const int64_t slot = is_hub(col) ? col - h0 : H + (light_index(col) - l0);
@@ -359,18 +542,47 @@ int hub_plan_host(const int32_t* rp, const int32_t* ci, const float* vv, int32_t
       w[(size_t)(o_it + 2 * it + 1)] = vv ? __builtin_bit_cast(int32_t, vv[k]) : 0;
       ++it;
     };
-    for (int64_t i = 0; i < n; ++i) {
+    // padding items read the zero row (slot H + n) with value 0
+    auto pad = [&](int64_t m, int64_t start) {
+      while ((it - start) % m) {
+        w[(size_t)(o_it + 2 * it)] = (int32_t)(H + n);
+        w[(size_t)(o_it + 2 * it + 1)] = 0;
+        ++it;
+      }
+    };
+    // light rows, most batches first (stable: row order among equals)
+    ord.resize((size_t)n);
+    for (int64_t i = 0; i < n; ++i) ord[(size_t)i] = i;
+    std::stable_sort(ord.begin(), ord.end(), [&](int64_t a, int64_t b) { return light_batches(a) > light_batches(b); });
+    for (int64_t lo = 0; lo < n; ++lo) {
+      const int64_t i = ord[(size_t)lo];
       const int64_t r = light_row_host(l0 + i, h0, H);
-      w[(size_t)(4 + i)] = (int32_t)it;
+      w[(size_t)(4 + 2 * lo)] = (int32_t)(i | (light_batches(i) << 16));
+      const int64_t start = it;
+      w[(size_t)(4 + 2 * lo + 1)] = (int32_t)it;
       for (int64_t k = rp[r]; k < rp[r + 1]; ++k) item(ci[k], k);
+      pad(kLightBatch, start);
     }
+    int64_t hb = 0;
+    const int64_t o_hb = 4 + 2 * n, o_off = o_hb + 2 * nhb;
     for (int64_t t = 0; t < H; ++t) {
-      w[(size_t)(4 + n + t)] = (int32_t)it;
-      for (int64_t k : hub_k[(size_t)(g * H + t)]) item(ci[k], k);
+      w[(size_t)(o_off + t)] = (int32_t)hb;
+      const std::vector<int64_t>& ks = hub_k[(size_t)(g * H + t)];
+      const int64_t start = it;
+      for (size_t q = 0; q < ks.size(); ++q) {
+        if (q % kHubBatch == 0) {
+          w[(size_t)(o_hb + 2 * hb)] = (int32_t)t;
+          w[(size_t)(o_hb + 2 * hb + 1)] = (int32_t)it;
+          ++hb;
+        }
+        item(ci[ks[q]], ks[q]);
+      }
+      pad(kHubBatch, start);
     }
-    w[(size_t)(4 + nout)] = (int32_t)it;
+    w[(size_t)(o_off + H)] = (int32_t)hb;
     R = std::max<int64_t>(R, (int64_t)w.size());
-    max_items = std::max(max_items, nit);
+    max_items = std::max(max_items, it);
+    max_hb = std::max(max_hb, nhb);
   }
   R = align4(R);
   const int64_t words = 16 + G * R;
@@ -383,7 +595,7 @@ int hub_plan_host(const int32_t* rp, const int32_t* ci, const float* vv, int32_t
   img.assign((size_t)words, 0);
   const int32_t hdr[16] = {kHubMagic,       M,           K,           groups,   (int32_t)G, (int32_t)R,
                            (int32_t)H,      (int32_t)h0, (int32_t)nL, (int32_t)nnz,       (int32_t)gs,
-                           (int32_t)hmin,   (int32_t)max_items, 0, 0, 0};
+                           (int32_t)hmin,   (int32_t)max_items, (int32_t)max_hb, 0, 0};
   std::copy(hdr, hdr + 16, img.begin());
   for (int64_t g = 0; g < G; ++g) std::copy(recs[(size_t)g].begin(), recs[(size_t)g].end(), img.begin() + 16 + g * R);
   return GCNK_OK;
@@ -397,16 +609,26 @@ int64_t hub_workspace_bytes(const int32_t* hdr, int32_t F) {
   return ((L.H * L.G * ld * 4) + 255) & ~255LL;
 }
 
+int64_t hub_counter_bytes(const int32_t* hdr) {
+  (void)hdr;
+  return (int64_t)kMaxSlices * (1 + kCombineChunks) * 8;
+}
+
 int hub_spmm(const void* plan, const int32_t* hdr, const float* B, int64_t ldb, int32_t F, float* C, int64_t ldc,
-             const Epi& e, float* workspace, bool vec4, hipStream_t s) {
+             const Epi& e, float* workspace, int32_t* counters, bool vec4, hipStream_t s) {
   const HubLayout L(hdr);
   if (L.H <= 0 || L.G <= 0) {
     set_error("gcnk_spmm (hub plan): empty hub plan");
     return GCNK_EARG;
   }
+  if ((reinterpret_cast<uintptr_t>(counters) & 7) != 0) {
+    set_error("gcnk_spmm (hub plan): counter region must be 8-byte aligned");
+    return GCNK_EARG;
+  }
   const int64_t part_ld = ((int64_t)F + 3) & ~3LL;
-  if (vec4) return hub_launch<4>((const int32_t*)plan, L, B, ldb, F, C, ldc, e, workspace, part_ld, s);
-  return hub_launch<1>((const int32_t*)plan, L, B, ldb, F, C, ldc, e, workspace, part_ld, s);
+  uint64_t* ctr = reinterpret_cast<uint64_t*>(counters);
+  if (vec4) return hub_launch<4>((const int32_t*)plan, L, B, ldb, F, C, ldc, e, workspace, part_ld, ctr, s);
+  return hub_launch<1>((const int32_t*)plan, L, B, ldb, F, C, ldc, e, workspace, part_ld, ctr, s);
 }
 
 }  // namespace gcnk

@@ -1780,7 +1780,7 @@ extern "C" int64_t gcnk_spmm_workspace_bytes(const int32_t* hdr, int32_t F) {
 
 extern "C" int64_t gcnk_spmm_counter_bytes(const int32_t* hdr) {
   if (!plan_magic(hdr)) return GCNK_EARG;
-  if (hdr[0] == kHubMagic) return 0;
+  if (hdr[0] == kHubMagic) return hub_counter_bytes(hdr);
   return (int64_t)hdr[7] * kMaxColTiles * 4;
 }
 
@@ -1857,7 +1857,7 @@ static int spmm_impl(const void* plan, const int32_t* hdr, const float* B, int64
       return GCNK_EUNSUP;
     }
     if (part == 1) return GCNK_OK;  // no dense tile blocks in a hub plan
-    return hub_spmm(plan, hdr, B, ldb, F, C, ldc, e, workspace, vec4, s);
+    return hub_spmm(plan, hdr, B, ldb, F, C, ldc, e, workspace, counters, vec4, s);
   }
   if (proj) {
     // the projection needs whole rows in one group: row-kernel rows only, float4, one column tile

@@ -49,19 +49,25 @@ HUB_BLOCK_ROWS = 0      # light rows per hub-plan group (0 = automatic, ~256 wor
 class Plan:
     """A built SpMM plan: device buffer + the 16-word host header (gcnk.h).
 
-    Row-unit plans with multi-segment heavy rows also need a zeroed counter
-    region per call (gcnk_spmm_counter_bytes); one is kept per stream, so
-    calls on different streams (or the autograd thread's) never share one."""
+    Plans with arrival counters (row-unit plans with multi-segment heavy rows;
+    hub plans, whose hub rows are combined inside the launch) need a COUNTER
+    REGION (gcnk_spmm_counter_bytes): zeroed once, then used by one stream's
+    calls in order -- the kernels keep it valid for the next call, so it is
+    never cleared again.  One region per stream for eager calls; calls
+    captured into a hipGraph take one region per capturing stream (every
+    graph captured there shares it: their replays must not run concurrently
+    on two streams), handed out from SPARE_REGIONS regions zeroed when the
+    plan is built, so a captured graph holds no memset node."""
 
     __slots__ = ("buf", "hdr", "_counters", "_spares", "_captured", "_lock")
     HUB_MAGIC = 0x474e4832
-    SPARE_REGIONS = 16   # pre-zeroed regions handed to hipGraph captures
+    SPARE_REGIONS = 16   # pre-zeroed regions handed to capturing streams
 
     def __init__(self, buf, hdr):
         self.buf, self.hdr = buf, hdr
         self._counters = {}
         self._spares = None
-        self._captured = []
+        self._captured = {}
         self._lock = threading.Lock()
 
     @property
@@ -79,35 +85,34 @@ class Plan:
         return int(_lib.load().gcnk_spmm_counter_bytes(ctypes.cast(self.hdr, ctypes.c_void_p)))
 
     def prime(self, device):
-        """Zero SPARE_REGIONS counter regions now (eagerly, outside any capture),
-        so that a later hipGraph capture takes one instead of capturing a memset
-        that every replay would run."""
+        """Zero SPARE_REGIONS counter regions now (eagerly, outside any capture)."""
         n = self.counter_bytes()
         if n <= 0 or self._spares is not None:
             return
-        words = (n + 3) // 4
+        words = (n + 7) // 8 * 2   # whole uint64 words
         block = torch.zeros(self.SPARE_REGIONS * words, dtype=torch.int32, device=device)
         self._spares = list(block.split(words))
 
     def counters(self, device):
-        """Zeroed int32 counter region for a call on torch's current stream (None
-        when the plan needs none).  The kernels leave it zeroed, so it is reused
-        by later calls on the same stream.  Inside a hipGraph capture the call
-        gets a region of its own (the graph replays may run beside eager calls):
-        one of the spares zeroed by prime(), or, once those are used up, a fresh
-        region zeroed by a captured memset."""
+        """The counter region for a call on torch's current stream (None when the
+        plan needs none); see the class docstring."""
         n = self.counter_bytes()
         if n <= 0:
             return None
-        words = (n + 3) // 4
-        if torch.cuda.is_current_stream_capturing():
-            with self._lock:
-                c = self._spares.pop() if self._spares else None
-            if c is None:
-                c = torch.zeros(words, dtype=torch.int32, device=device)
-            self._captured.append(c)   # owned by the graph for the plan's lifetime
-            return c
+        words = (n + 7) // 8 * 2
         key = torch.cuda.current_stream(device).cuda_stream
+        if torch.cuda.is_current_stream_capturing():
+            c = self._captured.get(key)
+            if c is None:
+                with self._lock:
+                    c = self._captured.get(key)
+                    if c is None:
+                        if not self._spares:
+                            raise RuntimeError(
+                                f"SpMM plan: hipGraph captures on more than {self.SPARE_REGIONS} streams; "
+                                "each capturing stream needs a pre-zeroed counter region (Plan.SPARE_REGIONS)")
+                        c = self._captured[key] = self._spares.pop()
+            return c
         c = self._counters.get(key)
         if c is None:
             with self._lock:

@@ -1,0 +1,10 @@
+#!/bin/bash
+cd "${GRAFT_REPO_ROOT:-/root/repo}" || exit 2
+export TMPDIR=/tmp
+mkdir -p gpurun_out/r03
+timeout -k 10 300 python -u -m pytest tests/test_gpu_parity.py -x -q -p no:cacheprovider --timeout 120 \
+  --timeout-method thread -k "hub or r8_adjacency" > gpurun_out/r03/pytest_hub.log 2>&1
+rc=$?; echo "pytest rc=$rc"; tail -n 3 gpurun_out/r03/pytest_hub.log
+if [ $rc -ne 0 ]; then exit $rc; fi
+bash scripts/variant_prof.sh "--variants hub --widths 200,8 --reps 200 --mode cold" base nostore nocomp || exit 3
+STAMP_WIDTHS=200 VARIANTS=stamps bash scripts/r03_stamps.sh

@@ -11,6 +11,9 @@ GOLDEN = os.path.join(ROOT, "tests", "golden")
 
 
 def pytest_configure(config):
+    if os.environ.get("GCNK_LIB"):
+        pytest.exit(f"GCNK_LIB={os.environ['GCNK_LIB']} is set: the tests check the in-tree product library only "
+                    "(unset it)", returncode=4)
     config.addinivalue_line("markers", "gpu: needs a ROCm GPU (MI355X); runs the HIP kernels")
     config.addinivalue_line("markers", "slow: long-running CPU test")
 

@@ -949,31 +949,44 @@ def test_device_dropout_draws_a_fresh_mask_on_every_graph_replay(r8):
         assert torch.equal(eager, outs[1])
 
 
-def test_graph_capture_takes_a_prezeroed_counter_region(monkeypatch):
-    """A captured SpMM whose plan needs arrival counters takes one of the
-    plan's pre-zeroed spare regions (no memset node replayed with every call)
-    and its replays stay exact (the kernels re-arm the counters)."""
+@pytest.mark.parametrize("kind", ["row", "hub"])
+def test_graph_capture_takes_a_prezeroed_counter_region(r8, kind, monkeypatch):
+    """Captured SpMMs whose plan needs a counter region (row-unit plan: heavy-row
+    arrival counters; hub plan: the in-launch hub combine) share ONE of the
+    plan's pre-zeroed spare regions per capturing stream -- however many calls
+    and graphs -- so no graph holds a memset node; eager calls keep their
+    stream's region; replays interleaved with eager calls stay exact."""
     from graph_convolutional_networks_for_text_classification_amd import sparse as sp
-    monkeypatch.setattr(sp, "HUB_MIN", -1)
     rng = np.random.default_rng(23)
-    M, K, F = 3001, 20003, 200
-    rp, ci, v = _random_csr(M, K, 20000, rng, heavy_rows=(5, 1700), heavy_deg=2500)
-    a = from_arrays(rp, ci, v, (M, K), DEV)
+    if kind == "row":
+        monkeypatch.setattr(sp, "HUB_MIN", -1)
+        M, K, F = 3001, 20003, 200
+        rp, ci, v = _random_csr(M, K, 20000, rng, heavy_rows=(5, 1700), heavy_deg=2500)
+        a = from_arrays(rp, ci, v, (M, K), DEV)
+    else:
+        a, K, F = from_torch(r8["adj"].to(DEV)), r8["nodes"], 200
     B = torch.from_numpy(rng.standard_normal((K, F)).astype(np.float32)).to(DEV)
     ref = spmm(a, B, dense=2.0)
     plan = list(a._plans.values())[-1]
-    assert plan.counter_bytes() > 0
+    assert plan.is_hub == (kind == "hub") and plan.counter_bytes() > 0
     spares = len(plan._spares)
-    out = torch.empty_like(ref)
-    g = torch.cuda.CUDAGraph()
-    with torch.cuda.graph(g):
-        spmm(a, B, out=out, dense=2.0)
-    assert len(plan._spares) == spares - 1
-    for _ in range(5):
-        out.zero_()
-        g.replay()
+    outs = [torch.empty_like(ref) for _ in range(6)]
+    graphs = [torch.cuda.CUDAGraph() for _ in range(2)]
+    for gi, g in enumerate(graphs):
+        with torch.cuda.graph(g):
+            for o in outs[3 * gi:3 * gi + 3]:
+                spmm(a, B, out=o, dense=2.0)
+    assert len(plan._spares) == spares - 1, "one region for the capturing stream, not one per call"
+    for _ in range(4):
+        for o in outs:
+            o.zero_()
+        graphs[0].replay()
+        eager = spmm(a, B, dense=2.0)
+        graphs[1].replay()
         torch.cuda.synchronize()
-        assert torch.equal(out, ref)
+        assert torch.equal(eager, ref)
+        for o in outs:
+            assert torch.equal(o, ref)
 
 
 def test_tile_path_repeat_streams_and_graph_replay_are_exact(r8):

@@ -46,10 +46,11 @@ def exec_hub_plan(plan, B):
 
     Checks the plan's bookkeeping: every light row and every hub partial
     written exactly once, slots inside the group's LDS image, items in CSR
-    (column) order, hub x hub nonzeros in group t % G."""
+    (column) order with padding only at the ends of rows / hubs, light rows
+    sorted by batch count, hub x hub nonzeros in group t % G."""
     h = plan[:16]
     assert h[0] == HUB_MAGIC
-    M, G, R, H, h0, nL, gs = (int(h[i]) for i in (1, 4, 5, 6, 7, 8, 10))
+    M, G, R, H, h0, nL, gs, max_hb = (int(h[i]) for i in (1, 4, 5, 6, 7, 8, 10, 13))
     assert M == H + nL and G == -(-nL // gs)
     F = B.shape[1]
     B = B.astype(np.float64)
@@ -62,32 +63,53 @@ def exec_hub_plan(plan, B):
     part = np.full((H, G, F), np.nan)
     for g in range(G):
         rec = plan[16 + g * R: 16 + (g + 1) * R]
-        n, nout, nit = int(rec[0]), int(rec[1]), int(rec[2])
-        assert n == min(gs, nL - g * gs) and nout == n + H
-        off = rec[4:5 + nout]
-        assert off[0] == 0 and off[-1] == nit and np.all(np.diff(off) >= 0)
-        o_it = _a4(5 + nout)
-        assert o_it + 2 * nit <= R
+        n, nhb, nit, o_it = (int(x) for x in rec[:4])
+        assert n == min(gs, nL - g * gs) and nhb <= max_hb
+        assert o_it % 4 == 0 and o_it + 2 * nit <= R
+        light = rec[4:4 + 2 * n].reshape(-1, 2)
+        hb = rec[4 + 2 * n:4 + 2 * n + 2 * nhb].reshape(-1, 2)
+        hoff = rec[4 + 2 * n + 2 * nhb:4 + 2 * n + 2 * nhb + H + 1]
         items = rec[o_it:o_it + 2 * nit].reshape(-1, 2)
         slots = items[:, 0]
         vals = items[:, 1].copy().view(np.float32).astype(np.float64)
-        assert np.all((slots >= 0) & (slots < H + n)), "items read the group's LDS image"
+        assert np.all((slots >= 0) & (slots <= H + n)), "items read the group's LDS image"
+        zero = slots == H + n                    # padding: the zero row, value 0
+        assert np.all(vals[zero] == 0)
         srows = np.array([h0 + s if s < H else light_row(g * gs + s - H) for s in range(H + n)], np.int64)
-        for o in range(nout):
-            sl = slots[off[o]:off[o + 1]]
+
+        def walk(k0, k1):
+            real = ~zero[k0:k1]
+            assert np.all(real[:real.sum()]), "padding only at the end"
+            sl = slots[k0:k1][real]
             cols = srows[sl]
             assert np.all(np.diff(cols) > 0), "CSR column order"
-            acc = vals[off[o]:off[o + 1]] @ B[cols] if len(cols) else np.zeros(F)
-            if o < n:
-                r = light_row(g * gs + o)
-                assert np.all((sl < H) | (cols == r)), "a light row reads hub rows and itself"
-                C[r] = acc
-                written[r] += 1
+            acc = vals[k0:k1][real] @ B[cols] if len(cols) else np.zeros(F)
+            return sl, acc
+
+        nbs = light[:, 0] >> 16
+        assert np.all(np.diff(nbs) <= 0), "light rows sorted by batch count"
+        seen = set()
+        for (word, ib), nb in zip(light, nbs):
+            i = int(word & 0xffff)
+            seen.add(i)
+            r = light_row(g * gs + i)
+            sl, acc = walk(int(ib), int(ib) + 4 * int(nb))
+            assert np.all((sl < H) | (srows[sl] == r)), "a light row reads hub rows and itself"
+            C[r] = acc
+            written[r] += 1
+        assert seen == set(range(n))
+        assert hoff[0] == 0 and hoff[-1] == nhb and np.all(np.diff(hoff) >= 0)
+        for t in range(H):
+            bs = range(int(hoff[t]), int(hoff[t + 1]))
+            assert all(int(hb[b, 0]) == t for b in bs)
+            if len(bs):
+                k0 = int(hb[bs[0], 1])
+                assert all(int(hb[b, 1]) == k0 + 8 * (b - bs[0]) for b in bs), "hub batches of 8, contiguous"
+                sl, acc = walk(k0, k0 + 8 * len(bs))
             else:
-                t = o - n
-                hh = sl < H
-                assert not hh.any() or t % G == g, "hub x hub nonzeros ride in group t % G"
-                part[t, g] = acc
+                sl, acc = np.zeros(0, np.int64), np.zeros(F)
+            assert not (sl < H).any() or t % G == g, "hub x hub nonzeros ride in group t % G"
+            part[t, g] = acc
     assert not np.isnan(part).any(), "every partial written"
     for t in range(H):
         C[h0 + t] = part[t].sum(0)

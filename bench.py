@@ -84,7 +84,23 @@ def parse():
     ap.add_argument("--rocprof-dir", default=None, help="keep the child kernel-trace summaries here")
     ap.add_argument("--config5", action="store_true",
                     help="run the config-5 column-sharded leg even on one rank (it runs by default when N > 1)")
+    ap.add_argument("--dry-run", action="store_true",
+                    help="print each rank's launch view (rank, world) as JSON and exit before any GPU call")
     return ap.parse_args()
+
+
+def launch_ranks(args):
+    """`--gpus N` (N > 1) outside a torch.distributed launcher: start the N rank
+    processes as ONE child (python -m torch.distributed.run, one process per GPU,
+    rendezvous on 127.0.0.1) and return its exit code.  Runs before anything
+    touches the GPU; the parent never execs and never initialises HIP."""
+    import socket
+    with socket.socket() as sk:
+        sk.bind(("127.0.0.1", 0))
+        port = sk.getsockname()[1]
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={args.gpus}",
+           "--master-addr=127.0.0.1", f"--master-port={port}", os.path.abspath(__file__)] + sys.argv[1:]
+    return subprocess.call(cmd, env=dict(os.environ, HSA_ENABLE_IPC_MODE_LEGACY="0"))
 
 
 def graph_us(fns, reps_per_fn):
@@ -273,13 +289,20 @@ def sharded_config5(dev, world, rank, datasets, ops, F=4096, reps=3):
 
 def main():
     args = parse()
+    if "WORLD_SIZE" not in os.environ and args.gpus > 1:
+        sys.exit(launch_ranks(args))
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    if world != args.gpus:
+        raise SystemExit(f"bench.py: --gpus {args.gpus} but the launcher started {world} rank(s)")
+    if args.dry_run:
+        print(json.dumps({"rank": rank, "local_rank": local, "world": world}), flush=True)
+        return
     import numpy as np
     import torch
     import torch.distributed as dist
 
-    world = int(os.environ.get("WORLD_SIZE", "1"))
-    rank = int(os.environ.get("RANK", "0"))
-    local = int(os.environ.get("LOCAL_RANK", "0"))
     torch.cuda.set_device(local)   # before the process group: RCCL binds each rank to its own GPU
     dev = torch.device("cuda", local)
     if world > 1:

@@ -133,3 +133,26 @@ def test_column_sharded_spmm_and_gcn_world2_gloo(F):
         np.testing.assert_allclose(consumer, ref_consumer, rtol=1e-5, atol=1e-5)
         np.testing.assert_array_equal(block[:, : c1 - c0], ref[:, c0:c1])
         np.testing.assert_allclose(logits, ref_logits, rtol=1e-5, atol=1e-4)
+
+
+def test_bench_gpus_n_spawns_n_ranks():
+    """`python bench.py --gpus 2` outside a launcher starts 2 rank processes
+    (torch.distributed.run, 127.0.0.1 rendezvous) before any GPU call; each sees
+    world 2.  --dry-run stops every rank before it touches the GPU."""
+    import json
+    import subprocess
+    import sys
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    r = subprocess.run([sys.executable, os.path.join(root, "bench.py"), "--gpus", "2", "--dry-run"],
+                       capture_output=True, text=True, timeout=240, cwd=root)
+    assert r.returncode == 0, r.stderr[-2000:]
+    import re
+    views = [json.loads(m) for m in re.findall(r"\{[^{}]*\"rank\"[^{}]*\}", r.stdout)]
+    assert sorted(v["rank"] for v in views) == [0, 1]
+    assert all(v["world"] == 2 for v in views)
+    assert sorted(v["local_rank"] for v in views) == [0, 1]
+    # one rank and --gpus 1: no launcher, world 1
+    r1 = subprocess.run([sys.executable, os.path.join(root, "bench.py"), "--dry-run"],
+                        capture_output=True, text=True, timeout=120, cwd=root)
+    one = [json.loads(m) for m in re.findall(r"\{[^{}]*\"rank\"[^{}]*\}", r1.stdout)]
+    assert r1.returncode == 0 and [v["world"] for v in one] == [1]

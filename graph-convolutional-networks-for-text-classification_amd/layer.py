@@ -120,6 +120,7 @@ class _Speculation:
 
 _spec = None
 _spec_lock = threading.Lock()
+_draw_lock = threading.RLock()
 SPECULATE_MASKS = True
 
 
@@ -138,7 +139,7 @@ def host_keep_mask(shape, p):
     unchanged either way.  Falls back to torch's own bernoulli_ if this torch
     build's generator state does not match the layout the restatement was
     checked against."""
-    global _mt_checked, _spec
+    global _mt_checked
     if _mt_checked is None:
         _mt_checked = _mt_self_check()
     n = 1
@@ -149,6 +150,15 @@ def host_keep_mask(shape, p):
         out = torch.empty(shape, dtype=torch.uint8, pin_memory=pinned)
         out.copy_(torch.empty(shape, dtype=torch.float32).bernoulli_(p))
         return out
+    # get_state -> draw -> set_state as one step: two threads drawing masks (or
+    # a thread drawing from the CPU generator meanwhile, through this module)
+    # must not both start from one state and lose an advance
+    with _draw_lock:
+        return _host_keep_mask_locked(shape, p, n, pinned)
+
+
+def _host_keep_mask_locked(shape, p, n, pinned):
+    global _spec
     g = torch.default_generator
     b = g.get_state().numpy().copy()
     key = (tuple(int(d) for d in shape), float(p))

@@ -183,6 +183,18 @@ def test_csr_to_dense_sums_duplicates_in_order():
                                        _stream(out.device))
     assert rc == 0
     assert np.array_equal(out.cpu().numpy(), want)
+    # strictly increasing columns (the fast scatter path), rows of every length
+    rp2, ci2, v2 = _random_csr(M, K, 20000, rng, empty_frac=0.1)
+    want2 = np.zeros((M, K + 8), np.float32)
+    for r in range(M):
+        want2[r, ci2[rp2[r]:rp2[r + 1]]] = v2[rp2[r]:rp2[r + 1]]
+    want2[:, K:] = 7.0
+    out2 = torch.full((M, K + 8), 7.0, device=DEV)
+    t2 = [torch.from_numpy(np.ascontiguousarray(x)).to(DEV) for x in (rp2.astype(np.int32), ci2.astype(np.int32),
+                                                                       v2.astype(np.float32))]
+    assert _lib.load().gcnk_csr_to_dense(_ptr(t2[0]), _ptr(t2[1]), _ptr(t2[2]), M, K, _ptr(out2), out2.stride(0),
+                                         _stream(out2.device)) == 0
+    assert np.array_equal(out2.cpu().numpy(), want2)
 
 
 def test_spmm_r8_features_use_tile_path(r8):

@@ -14,7 +14,8 @@ forwards are captured per graph (every one a complete forward), so exactly
 
 metric/value: SpMM edges/s = (2 · nnz(Â) per forward — the two graph
 aggregations of layer.py:106) × steps × ranks / max-over-ranks time;
-ms_per_step = GCN-forward ms.  N > 1: the R8 graph does not shard (SURVEY
+ms_per_step = GCN-forward ms (hipGraph replay); eager_forward_us = the same
+forward issued eagerly, one call per step as trainer.py:357 does.  N > 1: the R8 graph does not shard (SURVEY
 §8(e)): N independent replicas, "scaling": "weak".
 
 roofline (the north-star op, BASELINE.json: R8 doc-topic SpMM Â·S1 at hidden
@@ -37,8 +38,9 @@ cold figures for every op of the forward; "roofline_dominant" the slowest.
 
 cpu_baseline: the oracle (torch-CPU restatement issuing the reference's
 th.spmm calls on the same COO tensors, layer.py:102,106) on this host's
-cores, bounded sample, at all cores and at 1 thread, with nproc and the CPU
-model; "cpu_stock_csr" is torch CSR sparse.mm (MKL) on the same host, and
+cores, bounded sample, at the job's thread share (OMP_NUM_THREADS), at every
+core this process may run on ("all_cores") and at 1 thread, with nproc and
+the CPU model; "cpu_stock_csr" is torch CSR sparse.mm (MKL) on the same host, and
 "gpu_stock" stock PyTorch-ROCm torch.sparse.mm (hipSPARSE) on the device.
 
 configs: BASELINE configs 3 (20ng-shaped doc-topic graph, hidden 200, 20
@@ -203,7 +205,7 @@ def rocprof_kernel_us(mode, kernels_like, save_dir=None):
     try:
         cmd = ["timeout", "-s", "KILL", "150", exe, "--kernel-trace", "--stats", "--output-format", "csv", "-d", tmp,
                "-o", "kt", "--", sys.executable, os.path.join(ROOT, "scripts", "hub_probe.py"), "--reps", "200",
-               "--variants", "row", "--widths", "200", "--mode", mode]
+               "--variants", "hub", "--widths", "200", "--mode", mode]
         r = subprocess.run(cmd, cwd=ROOT, env=env, stdout=subprocess.PIPE, stderr=subprocess.STDOUT, timeout=180)
         if r.returncode != 0:
             return None, f"rocprofv3 --kernel-trace rc={r.returncode}"
@@ -365,6 +367,18 @@ def main():
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         elapsed = float(t)
 
+    # ---- the forward as the reference's trainer issues it: eager calls, one
+    #      model.forward per step (trainer.py:357,382), no graph -- host launch
+    #      overhead included (synchronised once per 50 calls)
+    for _ in range(5):
+        forward()
+    torch.cuda.synchronize()
+    te = time.perf_counter()
+    for _ in range(50):
+        forward()
+    torch.cuda.synchronize()
+    eager_us = (time.perf_counter() - te) / 50 * 1e6
+
     # ---- per-op durations, warm and cold (rotating operand sets > the MALL)
     W1, b1 = model.gc1.weight.detach(), model.gc1.bias.detach()
     W2, b2 = model.gc2.weight.detach(), model.gc2.bias.detach()
@@ -412,26 +426,29 @@ def main():
     # ---- live HBM traffic of the north-star op (child rocprofv3 --pmc passes)
     traffic, traffic_src = (None, "skipped")
     if extras and not args.no_pmc:
-        traffic, traffic_src = pmc_traffic("AS1", ["hub_light_kernel", "hub_finish_kernel", "spmm_row_kernel"])
+        traffic, traffic_src = pmc_traffic("AS1", ["hub_group_kernel", "spmm_row_kernel"])
     # ---- the same op's kernel durations from rocprofv3 (warm and cold rotations)
     kt = {}
     if extras and not args.no_rocprof:
         for mode in ("warm", "cold"):
-            kt[mode] = rocprof_kernel_us(mode, ["hub_light_kernel", "hub_finish_kernel", "spmm_row_kernel"],
-                                         args.rocprof_dir)
+            kt[mode] = rocprof_kernel_us(mode, ["hub_group_kernel", "spmm_row_kernel"], args.rocprof_dir)
 
     # ---- CPU baselines (rank 0, N = 1): oracle at all cores and 1 thread, torch CSR (MKL)
     cpu = cpu_stock = gpu_stock = None
     if extras and args.cpu_sample_s > 0:
         from oracle import gcn_ref
         threads = int(os.environ.get("OMP_NUM_THREADS", str(min(16, os.cpu_count() or 1))))
+        try:
+            all_cores = len(os.sched_getaffinity(0))
+        except (AttributeError, OSError):
+            all_cores = os.cpu_count() or threads
         torch.manual_seed(0)
         ref = gcn_ref.RefGCN(nfeat=nfeat, nhid=nhid, nclass=nclass, dropout=0.5).eval()
         ref.load_state_dict({k: v.cpu() for k, v in model.state_dict().items()})
         xc, ac = r8["features"], r8["adj"]
         legs = {}
         with torch.no_grad():
-            for th in (threads, 1):
+            for th in sorted({threads, 1, all_cores}, reverse=True):
                 torch.set_num_threads(th)
                 tc, n = timed_cpu(lambda: ref(xc, ac), args.cpu_sample_s)
                 legs[th] = (tc, n)
@@ -451,6 +468,8 @@ def main():
                          f"layer.py:102,106), {tc * 1e3:.2f} ms/forward at {threads} threads",
                "ms_per_forward": tc * 1e3,
                "one_thread": {"value": 2 * nnz_a / t1, "ms_per_forward": t1 * 1e3, "forwards": n1},
+               "all_cores": {"threads": all_cores, "value": 2 * nnz_a / legs[all_cores][0],
+                             "ms_per_forward": legs[all_cores][0] * 1e3, "forwards": legs[all_cores][1]},
                **cpu_info()}
         cpu_stock = {"value": 2 * nnz_a / tm, "unit": "edges/s", "cores": threads, "ms_per_forward": tm * 1e3,
                      "impl": "torch CPU sparse.mm on CSR tensors (MKL), same forward", "forwards": nm}
@@ -568,6 +587,7 @@ def main():
         "steps": args.steps,
         "warmup": args.warmup,
         "ms_per_step": ms,
+        "eager_forward_us": round(eager_us, 3),
         "higher_is_better": True,
         "scaling": "weak",
         "vs_baseline": None,

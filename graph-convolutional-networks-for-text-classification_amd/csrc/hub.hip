@@ -56,6 +56,7 @@ constexpr int kMaxHub = 256;          // hub rows per plan
 constexpr int kMaxGroupRows = 512;    // light rows per group
 constexpr int kMaxSlices = 64;        // column slices per launch
 constexpr int kLdsMax = 163840;       // gfx950: 160 KiB per workgroup
+constexpr int kLdsDyn = kLdsMax - 1024;  // dynamic part (static LDS of the kernel: a few words)
 constexpr int kTargetBlocks = 256;    // row-group workgroups per launch (one per CU)
 constexpr int kLightBatch = 4;        // items per light-row batch (plan pads light rows to a multiple)
 constexpr int kHubBatch = 8;          // items per hub batch (plan pads each hub's items to a multiple)
@@ -410,7 +411,7 @@ int64_t choose_slices(const HubLayout& L, int32_t Q, size_t vbytes, int64_t* lds
   for (; c <= std::min<int64_t>(Q, kMaxSlices); ++c) {
     const int64_t w = (Q + c - 1) / c;
     const int64_t lds = rec_words(L) * 4 + (L.H + L.gs + 2 + L.max_hb) * w * (int64_t)vbytes;
-    if (lds <= kLdsMax) {
+    if (lds <= kLdsDyn) {
       *lds_out = lds;
       return c;
     }
@@ -432,11 +433,10 @@ int hub_launch(const int32_t* plan, const HubLayout& L, const float* B, int64_t 
   // one workgroup per CU (the in-launch hand-off is the form measured at one
   // workgroup per CU; 1024 threads and > 80 KB of LDS admit no second)
   lds = std::max<int64_t>(lds, kLdsMax / 2 + 16);
-  static std::once_flag once;
-  std::call_once(once, [] {
-    (void)hipFuncSetAttribute(reinterpret_cast<const void*>(&hub_group_kernel<VEC>),
-                              hipFuncAttributeMaxDynamicSharedMemorySize, kLdsMax);
-  });
+  // dynamic LDS up to kLdsDyn (the kernel's static LDS takes the rest of the 160 KiB)
+  static const hipError_t attr = hipFuncSetAttribute(reinterpret_cast<const void*>(&hub_group_kernel<VEC>),
+                                                     hipFuncAttributeMaxDynamicSharedMemorySize, kLdsDyn);
+  if (attr != hipSuccess) return hip_check(attr, "hub_group_kernel LDS attribute");
   static int cus = [] {
     int dev = 0, n = 0;
     if (hipGetDevice(&dev) != hipSuccess || hipDeviceGetAttribute(&n, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess)

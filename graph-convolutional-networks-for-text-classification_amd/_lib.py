@@ -31,7 +31,7 @@ def _resolve_lib():
 
 
 LIB_PATH = _resolve_lib()
-ABI_VERSION = 2
+ABI_VERSION = 3
 
 # C-ABI return codes (gcnk.h)
 OK, EARG, EUNSUP, EHIP = 0, -1, -2, -3
@@ -91,6 +91,31 @@ SIGNATURES = {
         _vp, _i64, _f32,          # drop_mask, ldm, drop_scale
         _f32, _u64, _u64, _vp,    # keep_prob, seed, offset, rng_base
         _vp, _i64, _i32, _vp, _i64,  # W, ldw, P, C2, ldc2
+        _vp, _i64,                # workspace, workspace_bytes
+        _vp, _i64,                # counters, counter_bytes
+        _i32, _vp,                # lanes_hint, stream
+    ]),
+    "gcnk_spmm_proj_slices": (_i32, [_vp, _i32]),
+    "gcnk_spmm_proj_sliced_f32": (ctypes.c_int, [
+        _vp, _vp,                 # plan, plan header
+        _vp, _i64, _i32,          # B, ldb, F
+        _vp, _i64,                # C (nullable), ldc
+        _vp, _i32,                # bias, epilogue
+        _vp, _i64, _f32,          # drop_mask, ldm, drop_scale
+        _f32, _u64, _u64, _vp,    # keep_prob, seed, offset, rng_base
+        _vp, _i64, _i32,          # W, ldw, P
+        _vp, _i64, _i64, _i32,    # C2, ldc2, c2_slice_stride, c2_slices
+        _vp, _i64,                # workspace, workspace_bytes
+        _vp, _i64,                # counters, counter_bytes
+        _i32, _vp,                # lanes_hint, stream
+    ]),
+    "gcnk_spmm_sum_csr_f32": (ctypes.c_int, [
+        _vp, _vp,                 # plan, plan header
+        _vp, _i64, _i32, _i32, _i64,  # B, ldb, F, nsum, bstride
+        _vp, _i64,                # C, ldc
+        _vp, _i32,                # bias, epilogue
+        _vp, _i64, _f32,          # drop_mask, ldm, drop_scale
+        _f32, _u64, _u64, _vp,    # keep_prob, seed, offset, rng_base
         _vp, _i64,                # workspace, workspace_bytes
         _vp, _i64,                # counters, counter_bytes
         _i32, _vp,                # lanes_hint, stream

@@ -144,7 +144,19 @@ int hub_plan_host(const int32_t* rowptr, const int32_t* colind, const float* val
 int64_t hub_plan_words(const int32_t* hdr);
 int64_t hub_workspace_bytes(const int32_t* hdr, int32_t F);
 int64_t hub_counter_bytes(const int32_t* hdr);
+// fused work beside a hub-plan product (hub.hip HubExtra): a projection of
+// every finished element (W != null) or a summed operand (nsum > 1)
+struct HubSide {
+  const float* W = nullptr;
+  int64_t ldw = 0;
+  int32_t P = 0;
+  float* C2 = nullptr;
+  int64_t c2_stride = 0, ldc2 = 0;
+  int32_t nsum = 1;
+  int64_t bstride = 0;
+};
+int32_t hub_proj_slices(const int32_t* hdr, int32_t F);
 int hub_spmm(const void* plan, const int32_t* hdr, const float* B, int64_t ldb, int32_t F, float* C, int64_t ldc,
-             const Epi& e, float* workspace, int32_t* counters, bool vec4, hipStream_t s);
+             const Epi& e, float* workspace, int32_t* counters, bool vec4, const HubSide& side, hipStream_t s);
 
 }  // namespace gcnk

@@ -60,6 +60,7 @@ constexpr int kLdsDyn = kLdsMax - 1024;  // dynamic part (static LDS of the kern
 constexpr int kTargetBlocks = 256;    // row-group workgroups per launch (one per CU)
 constexpr int kLightBatch = 4;        // items per light-row batch (plan pads light rows to a multiple)
 constexpr int kHubBatch = 8;          // items per hub batch (plan pads each hub's items to a multiple)
+constexpr int kProjMax = 8;           // widest fused projection (gc2's W2: R8 8 classes)
 constexpr int kCombineChunks = 8;     // hub-row chunks per column slice, combined by the last 8 arrivals
 constexpr int kCombineLanes = 16;     // lanes summing one combined output's partials (power of two)
 constexpr int kCombineSpins = 1 << 12;  // poll bound of a waiting combiner (then the last arrival takes over)
@@ -142,6 +143,43 @@ __device__ __forceinline__ float load_sc1<float>(const float* base, int64_t off)
   return __uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(rsrc(base), (int)(off * 4), 0, kBufSc1));
 }
 
+// Optional fused work around the product (template flags of the kernel):
+//   PROJ  (gc1 -> gc2, layer.py:106,110,182,185 then :102): every finished
+//         element of H = epi(A B) is projected by W [F x P] while in registers;
+//         slice c of the launch writes C2[c][row][:P] = H[row, slice c] x
+//         W[slice c, :] (the P-wide partial over its columns, summed over the
+//         slice's columns in order); the consumer sums the slices in order
+//         (gcnk_spmm_sum_csr_f32).  H itself is stored only when C != null.
+//   BSUM  (the consumer): B = sum over s < nsum of B_s (B_s at B + s * bstride),
+//         summed in order as the rows are staged.
+struct HubExtra {
+  const float* W;      // PROJ: [F x P], leading dimension ldw
+  int64_t ldw;
+  int32_t P;
+  float* C2;           // PROJ: slice c's partial projection at C2 + c * c2_stride
+  int64_t c2_stride, ldc2;
+  int32_t nsum;        // BSUM: operand count
+  int64_t bstride;
+};
+
+// Projection partial of one finished float4 of columns 4 (q0 + j) .. + 3:
+// out[p] = sum over the 4 columns of v[col] * W[col, p]  (s_w: the slice's W
+// rows, kProjMax wide, zero past P).
+__device__ __forceinline__ void project4(const float4& v, int32_t j, const float* s_w, int32_t P, float* out) {
+  const float* wr = s_w + (int64_t)4 * j * kProjMax;
+#pragma unroll
+  for (int pp = 0; pp < kProjMax; ++pp) {
+    float a = v.x * wr[pp];
+    a = fmaf(v.y, wr[kProjMax + pp], a);
+    a = fmaf(v.z, wr[2 * kProjMax + pp], a);
+    a = fmaf(v.w, wr[3 * kProjMax + pp], a);
+    if (pp < P) out[pp] = a;
+  }
+}
+__device__ __forceinline__ void project4(const float& v, int32_t j, const float* s_w, int32_t P, float* out) {
+  (void)v; (void)j; (void)s_w; (void)P; (void)out;  // PROJ is float4-only
+}
+
 // In-launch combine of the hub rows of column slice c.  Counter region
 // (uint64, zeroed once, never reset -- every value is relative to the launch
 // count, so consecutive launches on one stream need no clearing):
@@ -159,11 +197,12 @@ __device__ __forceinline__ float load_sc1<float>(const float* base, int64_t off)
 // is claimed by a compare-and-swap of its claim word from the launch count
 // to launch count + 1: exactly one claimant per launch.  Chunk sums run in
 // group order (fixed): the result does not depend on who combines.
-template <int VEC>
+template <int VEC, bool PROJ>
 __device__ __forceinline__ void hub_combine(uint64_t* ctr, int32_t K, int32_t* s_scr, int32_t G, int32_t c, int32_t h0,
                                             int32_t H, int32_t w, int32_t q0, const float* part_u, int64_t part_ld,
                                             float* C, int64_t ldc, const Epi& epi,
-                                            const typename Vec<VEC>::T* s_bias, int tid) {
+                                            const typename Vec<VEC>::T* s_bias, const float* s_w, float* s_proj,
+                                            const HubExtra& x, int tid) {
   using V = Vec<VEC>;
   using T = typename V::T;
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // this wave's partial stores have landed
@@ -234,9 +273,19 @@ __device__ __forceinline__ void hub_combine(uint64_t* ctr, int32_t K, int32_t* s
         const int32_t t = t0 + o / w, j = o % w;
         const int64_t row = (int64_t)h0 + t, cv = (int64_t)(q0 + j) * VEC;
         const T bv = epi.bias ? s_bias[j] : V::zero();
-        V::store(C + row * ldc + cv, V::epi(epi, s_red[tid], bv, row, cv));
+        const T v = V::epi(epi, s_red[tid], bv, row, cv);
+        if (C) V::store(C + row * ldc + cv, v);
+        if constexpr (PROJ) project4(v, j, s_w, x.P, s_proj + (int64_t)o * kProjMax);
       }
       __syncthreads();
+    }
+    if constexpr (PROJ) {  // chunk rows' projection partials: sum over the slice's vectors in order
+      for (int32_t e = tid; e < (t1 - t0) * x.P; e += kGroupBlock) {
+        const int32_t tt = e / x.P, pp = e - tt * x.P;
+        float a = 0.f;
+        for (int32_t j = 0; j < w; ++j) a += s_proj[(int64_t)(tt * w + j) * kProjMax + pp];
+        x.C2[(int64_t)c * x.c2_stride + ((int64_t)h0 + t0 + tt) * x.ldc2 + pp] = a;
+      }
     }
   }
 }
@@ -245,11 +294,12 @@ __device__ __forceinline__ void hub_combine(uint64_t* ctr, int32_t K, int32_t* s
 // Row-group kernel.  Grid G * nslices, block (g, c) = (b % G, b / G).
 // LDS: record [R words] | rows [(H + n) x w] vectors (slot-major) | zero row [w] |
 // bias [w] | hub batch sums [nhb x w].
-template <int VEC>
+template <int VEC, bool PROJ, bool BSUM>
 __global__ void __launch_bounds__(kGroupBlock)
 hub_group_kernel(const int32_t* __restrict__ recs, int32_t R, int32_t roff, int32_t G, int32_t gs, int32_t h0, int32_t H, int32_t nL,
                  int32_t nslices, const float* __restrict__ B, int64_t ldb, int32_t F, float* __restrict__ C,
-                 int64_t ldc, Epi epi, float* __restrict__ part, int64_t part_ld, uint64_t* __restrict__ ctr, int32_t K) {
+                 int64_t ldc, Epi epi, float* __restrict__ part, int64_t part_ld, uint64_t* __restrict__ ctr, int32_t K,
+                 HubExtra x, int32_t max_hb) {
   using V = Vec<VEC>;
   using T = typename V::T;
   extern __shared__ __attribute__((aligned(16))) int32_t smem[];
@@ -274,16 +324,29 @@ hub_group_kernel(const int32_t* __restrict__ recs, int32_t R, int32_t roff, int3
   }
   const int32_t ne = (H + n) * w;
   const float* Bc = B + (int64_t)q0 * VEC;
-  for (int32_t e0 = wv * 64; e0 < ne; e0 += NW * 64) {
-    const int32_t e = e0 + lane;
-    if (e < ne) {
+  if constexpr (BSUM) {
+    // B = sum of nsum operands, summed in order on the way into LDS
+    for (int32_t e = tid; e < ne; e += kGroupBlock) {
       const int32_t s = e / w, j = e - s * w;
       const int64_t row = s < H ? (int64_t)h0 + s : light_row(l0 + (s - H), h0, H);
       const float* src = Bc + row * ldb + (int64_t)j * VEC;
-      if (VEC == 4)
-        lds_dma16(src, s_rows + e0);
-      else
-        lds_dma4(src, s_rows + e0);
+      T acc = V::load(src);
+#pragma unroll 8
+      for (int32_t k = 1; k < x.nsum; ++k) V::add(acc, V::load(src + (int64_t)k * x.bstride));
+      s_rows[e] = acc;
+    }
+  } else {
+    for (int32_t e0 = wv * 64; e0 < ne; e0 += NW * 64) {
+      const int32_t e = e0 + lane;
+      if (e < ne) {
+        const int32_t s = e / w, j = e - s * w;
+        const int64_t row = s < H ? (int64_t)h0 + s : light_row(l0 + (s - H), h0, H);
+        const float* src = Bc + row * ldb + (int64_t)j * VEC;
+        if (VEC == 4)
+          lds_dma16(src, s_rows + e0);
+        else
+          lds_dma4(src, s_rows + e0);
+      }
     }
   }
   // slot H + n: the zero row the plan's padding items read; then the bias
@@ -292,6 +355,16 @@ hub_group_kernel(const int32_t* __restrict__ recs, int32_t R, int32_t roff, int3
   if (tid < w) s_rows[ne + tid] = V::zero();
   T* s_bias = s_rows + ne + w;
   if (epi.bias && tid < w) s_bias[tid] = V::load(epi.bias + (int64_t)(q0 + tid) * VEC);
+  // PROJ: the slice's W rows (4 w x kProjMax, zero past P) and the projection
+  // partials' scratch, after the hub batch sums
+  float* s_w = reinterpret_cast<float*>(s_bias + w + max_hb * w);
+  float* s_proj = s_w + 4 * w * kProjMax;
+  if constexpr (PROJ) {
+    for (int32_t e = tid; e < 4 * w * kProjMax; e += kGroupBlock) {
+      const int32_t r = e / kProjMax, pp = e - r * kProjMax;
+      s_w[e] = pp < x.P ? x.W[(int64_t)(q0 * VEC + r) * x.ldw + pp] : 0.f;
+    }
+  }
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   __syncthreads();
   stamp(epi, 1);
@@ -373,7 +446,9 @@ hub_group_kernel(const int32_t* __restrict__ recs, int32_t R, int32_t roff, int3
       const int64_t cv = (int64_t)(q0 + j) * VEC;
       const int64_t row = light_row(l0 + i, h0, H);
       const T bv = epi.bias ? s_bias[j] : V::zero();
-      V::store_aligned(C + row * ldc + cv, V::epi(epi, acc, bv, row, cv));
+      const T v = V::epi(epi, acc, bv, row, cv);
+      if (!PROJ || C) V::store_aligned(C + row * ldc + cv, v);
+      if constexpr (PROJ) project4(v, j, s_w, x.P, s_proj + (int64_t)e * kProjMax);
     }
   }
 #ifdef GCNK_STAMPS
@@ -398,19 +473,35 @@ hub_group_kernel(const int32_t* __restrict__ recs, int32_t R, int32_t roff, int3
 #endif
     store_sc1(part_u, ((int64_t)t * G + g) * part_ld + (int64_t)(q0 + j) * VEC, acc);
   }
-  hub_combine<VEC>(ctr, K, s_rec, G, c, h0, H, w, q0, part_u, part_ld, C, ldc, epi, s_bias, tid);
+  if constexpr (PROJ) {  // light rows' projection partials: sum over the slice's vectors in order
+    for (int32_t e = tid; e < n * x.P; e += kGroupBlock) {
+      const int32_t lo = e / x.P, pp = e - lo * x.P;
+      float a = 0.f;
+      for (int32_t j = 0; j < w; ++j) a += s_proj[(int64_t)(lo * w + j) * kProjMax + pp];
+      const int64_t row = light_row(l0 + (s_light[lo].x & 0xffff), h0, H);
+      x.C2[(int64_t)c * x.c2_stride + row * x.ldc2 + pp] = a;
+    }
+    __syncthreads();  // s_proj is reused by the combine
+  }
+  hub_combine<VEC, PROJ>(ctr, K, s_rec, G, c, h0, H, w, q0, part_u, part_ld, C, ldc, epi, s_bias, s_w, s_proj, x, tid);
 }
 
 // LDS words before the row image: the record, at least the combine's scratch
 int64_t rec_words(const HubLayout& L) { return std::max<int64_t>(L.R, 4 * kGroupBlock); }
 
+// LDS bytes of a launch with slices of at most w vectors
+int64_t lds_bytes(const HubLayout& L, int64_t w, size_t vbytes, bool proj) {
+  int64_t b = rec_words(L) * 4 + (L.H + L.gs + 2 + L.max_hb) * w * (int64_t)vbytes;
+  if (proj) b += (4 * w + std::max<int64_t>(L.gs, (L.H + kCombineChunks - 1) / kCombineChunks + 1) * w) * kProjMax * 4;
+  return b;
+}
+
 // Column slices for a launch: about 8 vectors per slice (R8 F = 200: 7 slices
 // of 7-8 float4), then more until the LDS image fits.
-int64_t choose_slices(const HubLayout& L, int32_t Q, size_t vbytes, int64_t* lds_out) {
+int64_t choose_slices(const HubLayout& L, int32_t Q, size_t vbytes, bool proj, int64_t* lds_out) {
   int64_t c = std::max<int64_t>(1, std::min<int64_t>(kMaxSlices, (Q + kSliceVecs - 1) / kSliceVecs));
   for (; c <= std::min<int64_t>(Q, kMaxSlices); ++c) {
-    const int64_t w = (Q + c - 1) / c;
-    const int64_t lds = rec_words(L) * 4 + (L.H + L.gs + 2 + L.max_hb) * w * (int64_t)vbytes;
+    const int64_t lds = lds_bytes(L, (Q + c - 1) / c, vbytes, proj);
     if (lds <= kLdsDyn) {
       *lds_out = lds;
       return c;
@@ -419,12 +510,12 @@ int64_t choose_slices(const HubLayout& L, int32_t Q, size_t vbytes, int64_t* lds
   return -1;
 }
 
-template <int VEC>
+template <int VEC, bool PROJ, bool BSUM>
 int hub_launch(const int32_t* plan, const HubLayout& L, const float* B, int64_t ldb, int32_t F, float* C, int64_t ldc,
-               const Epi& e, float* part, int64_t part_ld, uint64_t* ctr, hipStream_t s) {
+               const Epi& e, float* part, int64_t part_ld, uint64_t* ctr, const HubExtra& x, hipStream_t s) {
   const int32_t Q = VEC == 4 ? F / 4 : F;
   int64_t lds = 0;
-  const int64_t nslices = choose_slices(L, Q, sizeof(typename Vec<VEC>::T), &lds);
+  const int64_t nslices = choose_slices(L, Q, sizeof(typename Vec<VEC>::T), PROJ, &lds);
   if (nslices < 0 || nslices > kMaxSlices || L.G * nslices > INT32_MAX) {
     set_error("gcnk_spmm (hub plan): F = %d does not fit %lld hub + %lld group rows of LDS", F, (long long)L.H,
               (long long)L.gs);
@@ -434,7 +525,7 @@ int hub_launch(const int32_t* plan, const HubLayout& L, const float* B, int64_t 
   // workgroup per CU; 1024 threads and > 80 KB of LDS admit no second)
   lds = std::max<int64_t>(lds, kLdsMax / 2 + 16);
   // dynamic LDS up to kLdsDyn (the kernel's static LDS takes the rest of the 160 KiB)
-  static const hipError_t attr = hipFuncSetAttribute(reinterpret_cast<const void*>(&hub_group_kernel<VEC>),
+  static const hipError_t attr = hipFuncSetAttribute(reinterpret_cast<const void*>(&hub_group_kernel<VEC, PROJ, BSUM>),
                                                      hipFuncAttributeMaxDynamicSharedMemorySize, kLdsDyn);
   if (attr != hipSuccess) return hip_check(attr, "hub_group_kernel LDS attribute");
   static int cus = [] {
@@ -444,9 +535,10 @@ int hub_launch(const int32_t* plan, const HubLayout& L, const float* B, int64_t 
     return n;
   }();
   const int32_t K = L.G * nslices <= cus ? (int32_t)std::min<int64_t>(kCombineChunks, L.G) : 1;
-  hipLaunchKernelGGL((hub_group_kernel<VEC>), dim3((unsigned)(L.G * nslices)), dim3(kGroupBlock), (size_t)lds, s,
-                     plan + 16, (int32_t)L.R, (int32_t)rec_words(L), (int32_t)L.G, (int32_t)L.gs, (int32_t)L.h0, (int32_t)L.H, (int32_t)L.nL,
-                     (int32_t)nslices, B, ldb, F, C, ldc, e, part, part_ld, ctr, K);
+  hipLaunchKernelGGL((hub_group_kernel<VEC, PROJ, BSUM>), dim3((unsigned)(L.G * nslices)), dim3(kGroupBlock),
+                     (size_t)lds, s, plan + 16, (int32_t)L.R, (int32_t)rec_words(L), (int32_t)L.G, (int32_t)L.gs,
+                     (int32_t)L.h0, (int32_t)L.H, (int32_t)L.nL, (int32_t)nslices, B, ldb, F, C, ldc, e, part, part_ld,
+                     ctr, K, x, (int32_t)L.max_hb);
   return launch_check("hub_group_kernel");
 }
 
@@ -614,8 +706,14 @@ int64_t hub_counter_bytes(const int32_t* hdr) {
   return (int64_t)kMaxSlices * (1 + kCombineChunks) * 8;
 }
 
+int32_t hub_proj_slices(const int32_t* hdr, int32_t F) {
+  const HubLayout L(hdr);
+  int64_t lds = 0;
+  return (int32_t)choose_slices(L, F / 4, 16, true, &lds);
+}
+
 int hub_spmm(const void* plan, const int32_t* hdr, const float* B, int64_t ldb, int32_t F, float* C, int64_t ldc,
-             const Epi& e, float* workspace, int32_t* counters, bool vec4, hipStream_t s) {
+             const Epi& e, float* workspace, int32_t* counters, bool vec4, const HubSide& side, hipStream_t s) {
   const HubLayout L(hdr);
   if (L.H <= 0 || L.G <= 0) {
     set_error("gcnk_spmm (hub plan): empty hub plan");
@@ -627,8 +725,25 @@ int hub_spmm(const void* plan, const int32_t* hdr, const float* B, int64_t ldb, 
   }
   const int64_t part_ld = ((int64_t)F + 3) & ~3LL;
   uint64_t* ctr = reinterpret_cast<uint64_t*>(counters);
-  if (vec4) return hub_launch<4>((const int32_t*)plan, L, B, ldb, F, C, ldc, e, workspace, part_ld, ctr, s);
-  return hub_launch<1>((const int32_t*)plan, L, B, ldb, F, C, ldc, e, workspace, part_ld, ctr, s);
+  const int32_t* p = (const int32_t*)plan;
+  HubExtra x{side.W, side.ldw, side.P, side.C2, side.c2_stride, side.ldc2, side.nsum, side.bstride};
+  const bool proj = side.W != nullptr, bsum = side.nsum > 1;
+  if ((proj || bsum) && !vec4) {
+    set_error("gcnk_spmm (hub plan): fused projection / summed operand need float4-aligned operands");
+    return GCNK_EUNSUP;
+  }
+  if (proj && (side.P < 1 || side.P > kProjMax || !side.C2)) {
+    set_error("gcnk_spmm (hub plan): fused projection width P = %d (1..%d)", side.P, kProjMax);
+    return GCNK_EUNSUP;
+  }
+  if (proj && bsum) {
+    set_error("gcnk_spmm (hub plan): a fused projection of a summed operand is not supported");
+    return GCNK_EUNSUP;
+  }
+  if (proj) return hub_launch<4, true, false>(p, L, B, ldb, F, C, ldc, e, workspace, part_ld, ctr, x, s);
+  if (bsum) return hub_launch<4, false, true>(p, L, B, ldb, F, C, ldc, e, workspace, part_ld, ctr, x, s);
+  if (vec4) return hub_launch<4, false, false>(p, L, B, ldb, F, C, ldc, e, workspace, part_ld, ctr, x, s);
+  return hub_launch<1, false, false>(p, L, B, ldb, F, C, ldc, e, workspace, part_ld, ctr, x, s);
 }
 
 }  // namespace gcnk

@@ -1788,7 +1788,7 @@ static int spmm_impl(const void* plan, const int32_t* hdr, const float* B, int64
                      int64_t ldc, const float* bias, int32_t epilogue, const uint8_t* drop_mask, int64_t ldm,
                      float drop_scale, float keep_prob, uint64_t seed, uint64_t offset, const uint64_t* rng_base,
                      float* workspace, int64_t workspace_bytes, int32_t* counters, int64_t counter_bytes, int32_t lanes_hint,
-                     const ProjArgs& pa, void* stream, int32_t part = 0) {
+                     const ProjArgs& pa, void* stream, int32_t part = 0, const HubSide* side = nullptr) {
   if (!plan || !plan_magic(hdr) || F < 0 || part < 0 || part > 2) {
     set_error("gcnk_spmm_csr_f32: bad argument (plan/header missing or not a gcnk plan, F=%d)", F);
     return GCNK_EARG;
@@ -1801,7 +1801,7 @@ static int spmm_impl(const void* plan, const int32_t* hdr, const float* B, int64
     set_error("gcnk_spmm_proj_f32: bad projection (P=%d)", pa.P);
     return GCNK_EARG;
   }
-  if ((!C && (!proj || pa.store_main)) || (K > 0 && !B)) {
+  if ((!C && (!proj || pa.store_main) && !(side && side->W)) || (K > 0 && !B)) {
     set_error("gcnk_spmm_csr_f32: null pointer");
     return GCNK_EARG;
   }
@@ -1851,13 +1851,18 @@ static int spmm_impl(const void* plan, const int32_t* hdr, const float* B, int64
   const bool vec4 = (F % 4 == 0) && (ldb % 4 == 0) && (ldc % 4 == 0) && aligned16(B) && (!C || aligned16(C)) &&
                     (!workspace || aligned16(workspace)) && (!bias || aligned16(bias));
   hipStream_t s = (hipStream_t)stream;
+  if (side && side->nsum > 1 && !hub) {
+    set_error("gcnk_spmm_sum_csr_f32: a summed operand needs a hub plan (nsum = %d)", side->nsum);
+    return GCNK_EUNSUP;
+  }
   if (hub) {
-    if (proj) {
-      set_error("gcnk_spmm_proj_f32: fused projection unsupported with a hub plan");
+    if (proj && !side) {
+      set_error("gcnk_spmm_proj_f32: a hub plan projects per column slice (gcnk_spmm_proj_sliced_f32)");
       return GCNK_EUNSUP;
     }
     if (part == 1) return GCNK_OK;  // no dense tile blocks in a hub plan
-    return hub_spmm(plan, hdr, B, ldb, F, C, ldc, e, workspace, counters, vec4, s);
+    const HubSide none;
+    return hub_spmm(plan, hdr, B, ldb, F, C, ldc, e, workspace, counters, vec4, side ? *side : none, s);
   }
   if (proj) {
     // the projection needs whole rows in one group: row-kernel rows only, float4, one column tile
@@ -1951,4 +1956,58 @@ extern "C" int gcnk_spmm_proj_f32(const void* plan, const int32_t* hdr, const fl
   const ProjArgs pa{W, ldw, P, C2, ldc2, C != nullptr};
   return spmm_impl(plan, hdr, B, ldb, F, C, ldc, bias, epilogue, drop_mask, ldm, drop_scale, keep_prob, seed, offset,
                    rng_base, workspace, workspace_bytes, counters, counter_bytes, lanes_hint, pa, stream);
+}
+
+extern "C" int32_t gcnk_spmm_proj_slices(const int32_t* hdr, int32_t F) {
+  if (!plan_magic(hdr) || F <= 0) return GCNK_EARG;
+  if (hdr[0] != kHubMagic) return 1;
+  if (F % 4) return GCNK_EUNSUP;
+  return hub_proj_slices(hdr, F);
+}
+
+extern "C" int gcnk_spmm_proj_sliced_f32(const void* plan, const int32_t* hdr, const float* B, int64_t ldb, int32_t F,
+                                         float* C, int64_t ldc, const float* bias, int32_t epilogue,
+                                         const uint8_t* drop_mask, int64_t ldm, float drop_scale, float keep_prob,
+                                         uint64_t seed, uint64_t offset, const uint64_t* rng_base, const float* W,
+                                         int64_t ldw, int32_t P, float* C2, int64_t ldc2, int64_t c2_slice_stride,
+                                         int32_t c2_slices, float* workspace, int64_t workspace_bytes,
+                                         int32_t* counters, int64_t counter_bytes, int32_t lanes_hint, void* stream) {
+  const int32_t want = gcnk_spmm_proj_slices(hdr, F);
+  if (!W || !C2 || P <= 0 || ldw < P || ldc2 < P || want < 0 || c2_slices != want) {
+    set_error("gcnk_spmm_proj_sliced_f32: bad projection (P=%d, %d slices given, the plan writes %d)", P, c2_slices,
+              want);
+    return want == GCNK_EUNSUP ? GCNK_EUNSUP : GCNK_EARG;
+  }
+  if (hdr[0] != kHubMagic)  // one slice: the exact projection of the row kernel
+    return gcnk_spmm_proj_f32(plan, hdr, B, ldb, F, C, ldc, bias, epilogue, drop_mask, ldm, drop_scale, keep_prob,
+                              seed, offset, rng_base, W, ldw, P, C2, ldc2, workspace, workspace_bytes, counters,
+                              counter_bytes, lanes_hint, stream);
+  HubSide side;
+  side.W = W;
+  side.ldw = ldw;
+  side.P = P;
+  side.C2 = C2;
+  side.c2_stride = c2_slice_stride;
+  side.ldc2 = ldc2;
+  const ProjArgs none{nullptr, 0, 0, nullptr, 0, 1};
+  return spmm_impl(plan, hdr, B, ldb, F, C, ldc, bias, epilogue, drop_mask, ldm, drop_scale, keep_prob, seed, offset,
+                   rng_base, workspace, workspace_bytes, counters, counter_bytes, lanes_hint, none, stream, 0, &side);
+}
+
+extern "C" int gcnk_spmm_sum_csr_f32(const void* plan, const int32_t* hdr, const float* B, int64_t ldb, int32_t F,
+                                     int32_t nsum, int64_t bstride, float* C, int64_t ldc, const float* bias,
+                                     int32_t epilogue, const uint8_t* drop_mask, int64_t ldm, float drop_scale,
+                                     float keep_prob, uint64_t seed, uint64_t offset, const uint64_t* rng_base,
+                                     float* workspace, int64_t workspace_bytes, int32_t* counters,
+                                     int64_t counter_bytes, int32_t lanes_hint, void* stream) {
+  if (nsum < 1 || (nsum > 1 && bstride < 1)) {
+    set_error("gcnk_spmm_sum_csr_f32: bad operand count %d / stride %lld", nsum, (long long)bstride);
+    return GCNK_EARG;
+  }
+  HubSide side;
+  side.nsum = nsum;
+  side.bstride = bstride;
+  const ProjArgs none{nullptr, 0, 0, nullptr, 0, 1};
+  return spmm_impl(plan, hdr, B, ldb, F, C, ldc, bias, epilogue, drop_mask, ldm, drop_scale, keep_prob, seed, offset,
+                   rng_base, workspace, workspace_bytes, counters, counter_bytes, lanes_hint, none, stream, 0, &side);
 }

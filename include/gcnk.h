@@ -50,7 +50,7 @@
 extern "C" {
 #endif
 
-#define GCNK_ABI_VERSION 2
+#define GCNK_ABI_VERSION 3
 
 #define GCNK_OK 0
 #define GCNK_EARG (-1)
@@ -88,18 +88,19 @@ const char* gcnk_last_error(void);
  *
  * The operand is converted once (gcnk_spmm_plan_build) into one of two plans:
  *
- *  HUB plan (header magic 'GNH1') -- operands with a few heavy "hub" rows
- *  (degree >= hub_min; 0 = automatic: max(64, 8 x mean degree)) holding at
- *  least a quarter of the nonzeros, and no dense tile blocks: the reference's
- *  doc-topic adjacency (R8: 50 topic rows of 191..1807 nonzeros, 7,674
- *  document rows of 2..14).  Light rows are sorted by the hub columns they
- *  reference and cut into blocks of `block_rows` (0 = ~256 blocks, 4..64
- *  rows); one workgroup per block stages the block's distinct B rows in LDS
- *  once (at most 64) and computes its rows from LDS.  Hub rows are computed
- *  transposed: the block owning light row j (column j) adds A[h, j] * B[j]
- *  over its own j into one partial row per hub it touches, and a second small
- *  kernel sums each hub's partials in block order (+ the hub's nonzeros over
- *  columns no block owns).  Two launches, no counters, no atomics.
+ *  HUB plan (header magic 'GNH2') -- square operands whose rows of degree
+ *  >= hub_min (0 = automatic: max(64, 8 x mean degree)) form ONE contiguous
+ *  range of at most 256 "hub" rows and whose other ("light") rows reference
+ *  only hub columns and their own diagonal: the reference's doc-topic
+ *  adjacency (R8: 50 topic rows of 191..1807 nonzeros after 7,674 document
+ *  rows of 2..14).  Light rows are cut into G groups of `block_rows`
+ *  consecutive rows (0 = automatic: ~256 workgroups per launch) and F into
+ *  column slices; workgroup (group, slice) stages its rows' and the hub rows'
+ *  slices of B plus its group's record in LDS (LDS-DMA, addresses from the
+ *  workgroup index), computes its light rows, and one partial per hub row from
+ *  the same image (the hub rows transposed).  The hub rows are combined inside
+ *  the launch: the last workgroups of each slice to finish sum the G partials
+ *  in group order (arrival counters in the counter region).  One launch.
  *
  *  ROW-UNIT + TILE plan (magic 'GNK5') -- every other operand:
  *  - dense blocks: rows are grouped by off-diagonal degree class (factor-8
@@ -134,10 +135,10 @@ const char* gcnk_last_error(void);
  *   6 heavy segments  7 heavy rows of > 1 segment  8 tile chunks
  *   9 multi-chunk blocks  10 slabs  11 tile blocks  12 diagonal kept aside
  *   (0/1)  13 nnz  14 partial slots  15 chunk items of single-chunk tile blocks
- *   hub plan: 0 magic 'GNH1'  1 M  2 K  3 groups  4 light blocks  5 record
- *   stride (words)  6 hub rows  7 partial rows  8 max staged rows per block
- *   9 nnz  10 leftover hub nonzeros  11 light rows  12 rows per block
- *   13 hub degree threshold  14 stage slots  15 0
+ *   hub plan: 0 magic 'GNH2'  1 M  2 K  3 groups  4 row groups G  5 record
+ *   stride (words)  6 hub rows H  7 first hub row  8 light rows  9 nnz
+ *   10 light rows per group  11 hub degree threshold  12 max record items
+ *   13 max hub batches per record  14..15 0
  * ------------------------------------------------------------------------- */
 int32_t gcnk_spmm_groups(int32_t F, int32_t lanes_hint);
 int32_t gcnk_spmm_default_ipc(int32_t M, int64_t nnz, int32_t F, int32_t lanes_hint);
@@ -160,7 +161,10 @@ int gcnk_spmm_plan_build_host(const int32_t* rowptr, const int32_t* colind, cons
 int gcnk_spmm_plan_query(const void* plan, int32_t* out16, void* stream);
 /* Bytes of workspace (split-row partials, tile slabs, hub partials) an SpMM of width F needs. */
 int64_t gcnk_spmm_workspace_bytes(const int32_t* plan_header, int32_t F);
-/* Bytes of the zero-initialised counter region a call needs (0: none). */
+/* Bytes of the counter region a call needs (0: none).  The region is zeroed
+ * ONCE by the caller and then used by calls on one stream in order (never
+ * concurrently by two calls): the kernels keep it valid for the next call
+ * (row-unit plan: left zero; hub plan: per-slice launch counts). */
 int64_t gcnk_spmm_counter_bytes(const int32_t* plan_header);
 
 /* C = epi(A B) for the operand of `plan` (M x K from the header). */
@@ -210,6 +214,40 @@ int gcnk_spmm_proj_f32(const void* plan, const int32_t* plan_header,
                        float* workspace, int64_t workspace_bytes,
                        int32_t* counters, int64_t counter_bytes,
                        int32_t lanes_hint, void* stream);
+
+/* The fused projection for plans that split F into column slices (the hub
+ * plan): slice s of the launch writes the P-wide partial over its columns,
+ *   C2_s[M x P] = H[:, slice s] * W[slice s, :],   C2_s at C2 + s * c2_slice_stride,
+ * so C2 = H W = sum over s of C2_s (summed in order by the consumer,
+ * gcnk_spmm_sum_csr_f32 -- gc2's A-hat S2 of layer.py:106 takes S2 this way).
+ * gcnk_spmm_proj_slices(header, F) gives the slice count (1 for a row-unit
+ * plan, whose fused projection is exact: gcnk_spmm_proj_f32); c2_slices must
+ * equal it.  H is stored only when C != NULL.  P <= 8 on a hub plan. */
+int32_t gcnk_spmm_proj_slices(const int32_t* plan_header, int32_t F);
+int gcnk_spmm_proj_sliced_f32(const void* plan, const int32_t* plan_header,
+                              const float* B, int64_t ldb, int32_t F,
+                              float* C, int64_t ldc,
+                              const float* bias, int32_t epilogue,
+                              const uint8_t* drop_mask, int64_t ldm, float drop_scale,
+                              float keep_prob, uint64_t seed, uint64_t offset, const uint64_t* rng_base,
+                              const float* W, int64_t ldw, int32_t P,
+                              float* C2, int64_t ldc2, int64_t c2_slice_stride, int32_t c2_slices,
+                              float* workspace, int64_t workspace_bytes,
+                              int32_t* counters, int64_t counter_bytes,
+                              int32_t lanes_hint, void* stream);
+
+/* C = epi(A (B_0 + ... + B_{nsum-1})), B_s at B + s * bstride (each [K x F],
+ * leading dimension ldb), summed in order as rows are staged: the consumer of
+ * a sliced projection.  nsum > 1 needs a hub plan (else GCNK_EUNSUP). */
+int gcnk_spmm_sum_csr_f32(const void* plan, const int32_t* plan_header,
+                          const float* B, int64_t ldb, int32_t F, int32_t nsum, int64_t bstride,
+                          float* C, int64_t ldc,
+                          const float* bias, int32_t epilogue,
+                          const uint8_t* drop_mask, int64_t ldm, float drop_scale,
+                          float keep_prob, uint64_t seed, uint64_t offset, const uint64_t* rng_base,
+                          float* workspace, int64_t workspace_bytes,
+                          int32_t* counters, int64_t counter_bytes,
+                          int32_t lanes_hint, void* stream);
 
 /* ---------------------------------------------------------------------------
  * fp32 GEMM on MFMA (v_mfma_f32_16x16x4_f32; exact fp32 FMA chains):

@@ -209,27 +209,61 @@ def test_spmm_r8_features_use_tile_path(r8):
 
 @pytest.mark.parametrize("P", [1, 8, 20, 33])
 @pytest.mark.parametrize("store_main", [True, False])
-def test_spmm_fused_projection(r8, P, store_main):
-    """H = relu(A S + b) * dropout, S2 = H W2 in one pass (gcnk_spmm_proj_f32);
-    P > 32 exercises the unfused fallback."""
-    from graph_convolutional_networks_for_text_classification_amd.ops import spmm_proj
+@pytest.mark.parametrize("kind", ["hub", "row"])
+def test_spmm_fused_projection(r8, P, store_main, kind, monkeypatch):
+    """H = relu(A S + b) * dropout, S2 = H W2 in one pass: the row-unit plan's
+    gcnk_spmm_proj_f32 ([M, P]) and the hub plan's per-slice projection
+    (gcnk_spmm_proj_sliced_f32: [slices, M, P] summing to H W2, P <= 8); wider
+    P exercises the unfused fallback.  Then the consumer: A (sum of the slices)
+    + b2 (spmm_sum / gcnk_spmm_sum_csr_f32) against the oracle."""
+    from graph_convolutional_networks_for_text_classification_amd import sparse as sp
+    from graph_convolutional_networks_for_text_classification_amd.ops import spmm_proj, spmm_sum
+    if kind == "row":
+        monkeypatch.setattr(sp, "HUB_MIN", -1)
     a = from_torch(r8["adj"].to(DEV))
     rng = np.random.default_rng(P)
     N, F = r8["nodes"], 200
     S = rng.standard_normal((N, F)).astype(np.float32)
     W = rng.standard_normal((F, P)).astype(np.float32)
     b = rng.standard_normal(F).astype(np.float32)
+    b2 = rng.standard_normal(P).astype(np.float32)
     mask = (rng.random((N, F)) < 0.5).astype(np.uint8)
     H, S2 = spmm_proj(a, torch.from_numpy(S).to(DEV), torch.from_numpy(W).to(DEV), bias=torch.from_numpy(b).to(DEV),
                       epilogue=_lib.EPI_BIAS_RELU_DROP, mask=torch.from_numpy(mask).to(DEV), scale=2.0,
                       store_main=store_main)
+    assert list(a._plans.values())[-1].is_hub == (kind == "hub")
+    if kind == "hub" and P <= 8:
+        assert S2.dim() == 3 and S2.shape[0] == 7, "F = 200: 7 column slices, one partial each"
     rp, ci, v = (t.cpu().numpy() for t in (a.rowptr, a.colind, a.val))
     Href = csr_ref.spmm_epilogue(csr_ref.spmm_csr(rp, ci, v, S), b, relu=True, mask=mask, scale=2.0)
     if store_main:
         _close(H, Href, atol=2e-5)
     else:
         assert H is None
-    _close(S2, Href @ W.astype(np.float64), atol=2e-4)
+    S2ref = Href @ W.astype(np.float64)
+    _close(S2.sum(0) if S2.dim() == 3 else S2, S2ref, atol=2e-4)
+    Z = spmm_sum(a, S2, bias=torch.from_numpy(b2).to(DEV), epilogue=_lib.EPI_BIAS)
+    _close(Z, csr_ref.spmm_epilogue(csr_ref.spmm_csr(rp, ci, v, S2ref), b2), atol=4e-4)
+    assert torch.equal(Z, spmm_sum(a, S2, bias=torch.from_numpy(b2).to(DEV), epilogue=_lib.EPI_BIAS))
+
+
+@pytest.mark.parametrize("nsum", [2, 7, 13])
+@pytest.mark.parametrize("F", [8, 64])
+def test_spmm_sum_of_operands(r8, nsum, F):
+    """gcnk_spmm_sum_csr_f32: C = A (B_0 + ... + B_{n-1}) + b on the hub plan,
+    the operands summed in order while staged."""
+    from graph_convolutional_networks_for_text_classification_amd.ops import spmm_sum
+    a = from_torch(r8["adj"].to(DEV))
+    rng = np.random.default_rng(nsum * F)
+    Bs = rng.standard_normal((nsum, r8["nodes"], F)).astype(np.float32)
+    b = rng.standard_normal(F).astype(np.float32)
+    got = spmm_sum(a, torch.from_numpy(Bs).to(DEV), bias=torch.from_numpy(b).to(DEV), epilogue=_lib.EPI_BIAS)
+    assert list(a._plans.values())[-1].is_hub
+    Bsum = Bs[0].astype(np.float32)
+    for k in range(1, nsum):
+        Bsum = (Bsum + Bs[k]).astype(np.float32)      # the kernel's fp32 order
+    rp, ci, v = (t.cpu().numpy() for t in (a.rowptr, a.colind, a.val))
+    _close(got, csr_ref.spmm_epilogue(csr_ref.spmm_csr(rp, ci, v, Bsum), b), atol=5e-5)
 
 
 def test_spmm_deterministic():

@@ -177,7 +177,10 @@ __device__ __forceinline__ void hub_combine(uint64_t* ctr, int32_t K, int32_t* s
     // fixed-order LDS tree over the PL lanes
     const int32_t t0 = (int32_t)((int64_t)q * H / K), t1 = (int32_t)((int64_t)(q + 1) * H / K);
     const int32_t nout = (t1 - t0) * w;
-    constexpr int PL = kCombineLanes;
+    // lanes per output: enough that one pass covers the chunk (all its loads
+    // in flight at once), at most kCombineLanes
+    int PL = kCombineLanes;
+    while (PL > 1 && (BLOCK / PL) < nout) PL >>= 1;
     T* s_red = reinterpret_cast<T*>(s_scr);
     for (int32_t o0 = 0; o0 < nout; o0 += BLOCK / PL) {
       const int32_t o = o0 + tid / PL, p = tid % PL;
@@ -186,11 +189,11 @@ __device__ __forceinline__ void hub_combine(uint64_t* ctr, int32_t K, int32_t* s
         const int32_t t = t0 + o / w, j = o % w;
         const int64_t base = (int64_t)t * G * part_ld + (int64_t)(q0 + j) * VEC;
         const int32_t ga = (int32_t)((int64_t)p * G / PL), gb = (int32_t)((int64_t)(p + 1) * G / PL);
+#pragma unroll 8
         for (int32_t gg = ga; gg < gb; ++gg) V::add(acc, load_sc1<T>(part_u, base + (int64_t)gg * part_ld));
       }
       s_red[tid] = acc;
       __syncthreads();
-#pragma unroll
       for (int sh = PL / 2; sh >= 1; sh >>= 1) {
         if (p < sh) V::add(s_red[tid], s_red[tid + sh]);
         __syncthreads();

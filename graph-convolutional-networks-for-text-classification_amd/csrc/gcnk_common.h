@@ -159,4 +159,15 @@ int32_t hub_proj_slices(const int32_t* hdr, int32_t F);
 int hub_spmm(const void* plan, const int32_t* hdr, const float* B, int64_t ldb, int32_t F, float* C, int64_t ldc,
              const Epi& e, float* workspace, int32_t* counters, bool vec4, const HubSide& side, hipStream_t s);
 
+// ---------------------------------------------------------------------------
+// Split-plan X W (xw.hip): few contiguous dense rows + rows over a few "hot" columns.
+constexpr int32_t kXwMagic = 0x474e5831;  // "GNX1"
+int xw_plan_host(const int32_t* rowptr, const int32_t* colind, const float* val, int32_t M, int32_t K, int64_t nnz,
+                 int32_t groups, std::vector<int32_t>& img);
+int64_t xw_plan_words(const int32_t* hdr);
+int64_t xw_workspace_bytes(const int32_t* hdr, int32_t F);
+int64_t xw_counter_bytes(const int32_t* hdr);
+int xw_spmm(const void* plan, const int32_t* hdr, const float* B, int64_t ldb, int32_t F, float* C, int64_t ldc,
+            const Epi& e, float* workspace, int32_t* counters, bool vec4, hipStream_t s);
+
 }  // namespace gcnk

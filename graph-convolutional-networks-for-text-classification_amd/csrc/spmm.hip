@@ -1598,8 +1598,12 @@ int build_image(const int32_t* rp, const int32_t* ci, const float* vv, int32_t M
     rc = hub_plan_host(rp, ci, vv, M, K, nnz, groups, hub_min, block_rows, img);
     if (rc <= 0) return rc;  // built (0) or an error; 1: not applicable
   }
+  if (dense_threshold > 0.f && dense_threshold <= 1.f) {
+    rc = xw_plan_host(rp, ci, vv, M, K, nnz, groups, img);
+    if (rc <= 0) return rc;
+  }
   HostPlan hp;
-  if ((rc = host_plan(rp, ci, vv, M, K, nnz, ipc, groups, dense_threshold, hp))) return rc;
+  if ((rc = host_plan(rp, ci, vv, M, K, nnz, ipc, groups, std::fabs(dense_threshold), hp))) return rc;
   classic_image(hp, ci, vv, nnz, img);
   return GCNK_OK;
 }
@@ -1616,8 +1620,13 @@ int64_t plan_size(const int32_t* rp, const int32_t* ci, int32_t M, int32_t K, in
     rc = hub_plan_host(rp, ci, nullptr, M, K, nnz, groups, hub_min, block_rows, img);
     if (rc <= 0) return rc ? rc : (int64_t)img.size() * 4;
   }
+  if (dense_threshold > 0.f && dense_threshold <= 1.f) {
+    std::vector<int32_t> img;
+    rc = xw_plan_host(rp, ci, nullptr, M, K, nnz, groups, img);
+    if (rc <= 0) return rc ? rc : (int64_t)img.size() * 4;
+  }
   HostPlan hp;
-  if ((rc = host_plan(rp, ci, nullptr, M, K, nnz, ipc, groups, dense_threshold, hp, false))) return rc;
+  if ((rc = host_plan(rp, ci, nullptr, M, K, nnz, ipc, groups, std::fabs(dense_threshold), hp, false))) return rc;
   return Layout(hp.hdr).total * 4;
 }
 
@@ -1758,7 +1767,7 @@ extern "C" int gcnk_spmm_plan_query(const void* plan, int32_t* out16, void* stre
   int rc = hip_check(hipMemcpyAsync(out16, plan, 64, hipMemcpyDeviceToHost, s), "plan query copy");
   if (rc) return rc;
   rc = hip_check(hipStreamSynchronize(s), "plan query sync");
-  if (!rc && out16[0] != kMagic && out16[0] != kHubMagic) {
+  if (!rc && out16[0] != kMagic && out16[0] != kHubMagic && out16[0] != kXwMagic) {
     set_error("gcnk_spmm_plan_query: not a gcnk plan");
     return GCNK_EARG;
   }
@@ -1767,11 +1776,14 @@ extern "C" int gcnk_spmm_plan_query(const void* plan, int32_t* out16, void* stre
 
 static int64_t tile_fpad(int32_t F) { return ((int64_t)F + 15) & ~15LL; }
 
-static bool plan_magic(const int32_t* hdr) { return hdr && (hdr[0] == kMagic || hdr[0] == kHubMagic); }
+static bool plan_magic(const int32_t* hdr) {
+  return hdr && (hdr[0] == kMagic || hdr[0] == kHubMagic || hdr[0] == kXwMagic);
+}
 
 extern "C" int64_t gcnk_spmm_workspace_bytes(const int32_t* hdr, int32_t F) {
   if (!plan_magic(hdr) || F < 0) return GCNK_EARG;
   if (hdr[0] == kHubMagic) return hub_workspace_bytes(hdr, F);
+  if (hdr[0] == kXwMagic) return xw_workspace_bytes(hdr, F);
   const int64_t ld = ((int64_t)F + 3) & ~3LL;
   const int64_t rows = (int64_t)hdr[14] * ld * 4;
   const int64_t slabs = (int64_t)hdr[10] * kRB * tile_fpad(F) * 4;
@@ -1781,6 +1793,7 @@ extern "C" int64_t gcnk_spmm_workspace_bytes(const int32_t* hdr, int32_t F) {
 extern "C" int64_t gcnk_spmm_counter_bytes(const int32_t* hdr) {
   if (!plan_magic(hdr)) return GCNK_EARG;
   if (hdr[0] == kHubMagic) return hub_counter_bytes(hdr);
+  if (hdr[0] == kXwMagic) return xw_counter_bytes(hdr);
   return (int64_t)hdr[7] * kMaxColTiles * 4;
 }
 
@@ -1854,6 +1867,14 @@ static int spmm_impl(const void* plan, const int32_t* hdr, const float* B, int64
   if (side && side->nsum > 1 && !hub) {
     set_error("gcnk_spmm_sum_csr_f32: a summed operand needs a hub plan (nsum = %d)", side->nsum);
     return GCNK_EUNSUP;
+  }
+  if (hdr[0] == kXwMagic) {
+    if (proj || (side && (side->W || side->nsum > 1))) {
+      set_error("gcnk_spmm: fused projection / summed operand unsupported with a split plan");
+      return GCNK_EUNSUP;
+    }
+    if (part == 1) return GCNK_OK;
+    return xw_spmm(plan, hdr, B, ldb, F, C, ldc, e, workspace, counters, vec4, s);
   }
   if (hub) {
     if (proj && !side) {

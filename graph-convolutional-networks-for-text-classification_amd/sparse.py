@@ -44,6 +44,10 @@ DENSE_THRESHOLD = 0.25  # row blocks at least this dense (condensed) run on the 
 # threshold, > 0 = degree threshold, < 0 = never (row-unit + tile plan).
 HUB_MIN = 0
 HUB_BLOCK_ROWS = 0      # light rows per hub-plan group (0 = automatic, ~256 workgroups)
+# split plan (csrc/xw.hip) for operands with a contiguous range of dense rows
+# among rows that use a few "hot" columns (the reference's topic features X
+# and X^T); False leaves them to the row-unit + tile plan
+SPLIT_PLAN = True
 
 
 class Plan:
@@ -144,7 +148,9 @@ class CSR:
         """Returns a Plan (device buffer + host header); built once per key (setup sync)."""
         hub_min = HUB_MIN if hub_min is None else int(hub_min)
         block_rows = HUB_BLOCK_ROWS if block_rows is None else int(block_rows)
-        key = (ipc, groups, float(dense_threshold), hub_min, block_rows)
+        if not SPLIT_PLAN:
+            dense_threshold = -abs(dense_threshold)   # gcnk.h: negative = tile path only, no split plan
+        key = (ipc, groups, float(dense_threshold), hub_min, block_rows, SPLIT_PLAN)
         p = self._plans.get(key)
         if p is not None:
             return p

@@ -112,6 +112,18 @@ const char* gcnk_last_error(void);
  *    per nonzero; its rows' diagonal entries are kept aside and added in the
  *    epilogue; multi-chunk blocks are summed from partial slabs in order.
  *    dense_threshold > 1 disables the part (default callers pass 0.25).
+ *
+ *  SPLIT plan (magic 'GNX1') -- operands whose rows of more than 64 nonzeros
+ *  form ONE contiguous range of at most 128 dense rows and whose other rows
+ *  use at most 64 distinct ("hot") columns, each at least a quarter full:
+ *  the reference's topic features X (R8: 7,674 document rows over the 50
+ *  topic columns, 50 dense topic rows) and X^T.  The light rows are stored
+ *  densely over the hot columns and multiplied on fp32 MFMA with W's hot rows
+ *  staged in LDS once per 32-row block; the dense rows run as split-K chunks
+ *  on MFMA whose partials the last workgroups of each column slice sum in
+ *  chunk order inside the launch (counter region).  One launch; epilogue
+ *  GCNK_EPI_NONE only.  Tried when 0 < dense_threshold <= 1; a NEGATIVE
+ *  dense_threshold skips it (|dense_threshold| then drives the tile part).
  *  - row units: the other rows.  A row of at most `ipc` nonzeros is one unit
  *    owned by one lane group (LPR lanes, each a 16-B column vector); a
  *    heavier row is cut into segments of about ipc * groups nonzeros (at most

@@ -197,14 +197,58 @@ def test_csr_to_dense_sums_duplicates_in_order():
     assert np.array_equal(out2.cpu().numpy(), want2)
 
 
-def test_spmm_r8_features_use_tile_path(r8):
+SPLIT_MAGIC = 0x474E5831
+
+
+@pytest.mark.parametrize("F", [200, 8, 64, 100, 257, 300])
+def test_spmm_r8_features_split_plan(r8, F):
+    """R8 X W1 (layer.py:102) and X^T G (its autograd) on the split plan: the
+    document / feature rows over 50 hot columns on MFMA, the 50 dense rows as
+    split-K chunks summed in order inside the launch; float4 and scalar paths."""
     x = from_torch(r8["features"].to(DEV))
-    W = torch.randn(r8["nfeat"], 200, generator=torch.Generator().manual_seed(4))
+    rng = np.random.default_rng(F)
+    W = torch.from_numpy(rng.standard_normal((r8["nfeat"], F)).astype(np.float32))
     got = spmm(x, W.to(DEV))
     hdr = list(x._plans.values())[0].header
-    assert hdr[8] > 0 and hdr[5] == 0, "R8 X: document and topic rows all run on the MFMA tile path"
+    assert hdr[0] == SPLIT_MAGIC and hdr[7] == 50 and hdr[8] == r8["ndoc"] and hdr[5] == 50
     rp, ci, v = (t.cpu().numpy() for t in (x.rowptr, x.colind, x.val))
     _close(got, csr_ref.spmm_csr(rp, ci, v, W.numpy()), atol=1e-4)
+    assert torch.equal(got, spmm(x, W.to(DEV)))
+    xt = x.t()
+    G = torch.from_numpy(rng.standard_normal((r8["nodes"], F)).astype(np.float32))
+    gt = spmm(xt, G.to(DEV))
+    ht = list(xt._plans.values())[0].header
+    assert ht[0] == SPLIT_MAGIC and ht[7] == 50 and ht[8] == 0, "X^T: features 0..49 are the dense rows"
+    rpt, cit, vt = (t.cpu().numpy() for t in (xt.rowptr, xt.colind, xt.val))
+    _close(gt, csr_ref.spmm_csr(rpt, cit, vt, G.numpy()), atol=2e-4)
+
+
+@pytest.mark.parametrize("F", [16, 200])
+def test_spmm_split_plan_synthetic(F):
+    """Split plan on a synthetic operand: dense rows in the middle, light rows
+    over 37 hot columns with empty rows and duplicates summed, rectangular."""
+    rng = np.random.default_rng(F + 5)
+    M, K = 3000, 4100
+    hot = np.sort(rng.choice(K, 37, replace=False))
+    rows, cols = [], []
+    for r in range(M):
+        if 1200 <= r < 1270:
+            c = rng.choice(K, 3000, replace=False)
+        elif r % 11 == 0:
+            continue
+        else:
+            c = rng.choice(hot, int(rng.integers(1, 20)), replace=True)
+        rows.append(np.full(len(c), r))
+        cols.append(c)
+    rows, cols = np.concatenate(rows), np.concatenate(cols)
+    vals = rng.standard_normal(rows.size).astype(np.float32)
+    rp, ci, v = csr_ref.coo_to_csr(rows, cols, vals, (M, K))
+    a = from_arrays(rp, ci, v, (M, K), DEV)
+    B = rng.standard_normal((K, F)).astype(np.float32)
+    got = spmm(a, torch.from_numpy(B).to(DEV))
+    hdr = list(a._plans.values())[0].header
+    assert hdr[0] == SPLIT_MAGIC and hdr[7] == 70 and hdr[8] == 1200
+    _close(got, csr_ref.spmm_csr(rp, ci, v, B), atol=2e-5 * np.sqrt(3000))
 
 
 @pytest.mark.parametrize("P", [1, 8, 20, 33])
@@ -1035,17 +1079,30 @@ def test_graph_capture_takes_a_prezeroed_counter_region(r8, kind, monkeypatch):
             assert torch.equal(o, ref)
 
 
-def test_tile_path_repeat_streams_and_graph_replay_are_exact(r8):
-    """R8 X W1 on the tile path (single-chunk document blocks, the multi-chunk
-    topic block and its slab reduce): back-to-back calls, two streams at once
-    on one cached plan and graph replays all give the one-call bits, and the
-    product matches the oracle."""
+@pytest.mark.parametrize("dense", [0.25, 0.3])
+def test_tile_path_repeat_streams_and_graph_replay_are_exact(r8, dense, monkeypatch):
+    """R8 X W1 on the split plan (dense=0.25: document rows over the 50 topic
+    columns + the 50 dense topic rows' split-K chunks combined in-launch) and,
+    with the split plan off, on the tile path (single-chunk document blocks,
+    the multi-chunk topic block and its slab reduce): back-to-back calls, two
+    streams at once on one cached plan and graph replays all give the one-call
+    bits, and the product matches the oracle."""
     from graph_convolutional_networks_for_text_classification_amd import ops
+    from graph_convolutional_networks_for_text_classification_amd import sparse as sp
+    if dense != 0.25:
+        monkeypatch.setattr(sp, "SPLIT_PLAN", False)
     x = from_torch(r8["features"].to(DEV))
     W = torch.randn(r8["nfeat"], 200, generator=torch.Generator().manual_seed(11)).to(DEV)
-    one = ops.spmm(x, W)
+    one = ops.spmm(x, W, dense=dense)
     plan = list(x._plans.values())[-1]
-    assert plan.header[9] > 0, "R8 X's topic rows form a multi-chunk tile block"
+    if dense == 0.25:
+        assert plan.header[0] == SPLIT_MAGIC and plan.header[7] == 50, "R8 X: the split plan, 50 dense topic rows"
+    else:
+        assert plan.header[9] > 0, "R8 X's topic rows form a multi-chunk tile block"
+    ops_spmm = ops.spmm
+    def spmm_d(*a, **k):
+        return ops_spmm(*a, dense=dense, **k)
+    monkeypatch.setattr(ops, "spmm", spmm_d)
     for _ in range(4):
         assert torch.equal(ops.spmm(x, W), one)
     s1, s2 = torch.cuda.Stream(), torch.cuda.Stream()

@@ -265,3 +265,70 @@ def test_plan_bytes_is_exactly_the_built_image(kind):
     # no plan word is -7 (ids >= -1, counts >= 0, float bits of -7 would be a NaN),
     # so a sentinel left in the last reported word means the size was too large
     assert buf[nbytes // 4 - 1] != -7, "plan_bytes reported more than the build wrote"
+
+
+SPLIT_MAGIC = 0x474E5831
+
+
+def exec_split_plan(plan, B):
+    """numpy interpreter of the split plan (csrc/xw.hip): light rows = dense
+    values over the hot columns, heavy rows = dense rows (float64)."""
+    h = plan[:16]
+    assert h[0] == SPLIT_MAGIC
+    M, K, nl, nhot, nhp, nh, h0, o_hot, o_xl, o_xh, ldxh = (int(h[i]) for i in (1, 2, 4, 5, 6, 7, 8, 10, 11, 12, 13))
+    assert M == nl + nh and nhp % 4 == 0 and nhot <= nhp and ldxh % 4 == 0 and ldxh >= K
+    hot = plan[o_hot:o_hot + nhp]
+    assert np.all(np.diff(hot[:nhot]) > 0), "hot columns sorted"
+    xl = plan[o_xl:o_xl + nl * nhp].view(np.float32).reshape(nl, nhp).astype(np.float64)
+    assert np.all(xl[:, nhot:] == 0)
+    xh = plan[o_xh:o_xh + nh * ldxh].view(np.float32).reshape(nh, ldxh).astype(np.float64)
+    B = B.astype(np.float64)
+    C = np.zeros((M, B.shape[1]))
+    light = np.array([l if l < h0 else l + nh for l in range(nl)], np.int64)
+    C[light] = xl[:, :nhot] @ B[hot[:nhot]]
+    C[h0:h0 + nh] = xh[:, :K] @ B
+    return C
+
+
+def test_r8_features_get_the_split_plan(r8):
+    x = r8["features"].coalesce()
+    idx = x.indices().numpy()
+    rp, ci, v = csr_ref.coo_to_csr(idx[0], idx[1], x.values().numpy(), x.shape)
+    plan = build_host_plan(rp, ci, v, x.shape)
+    assert plan[0] == SPLIT_MAGIC and plan[7] == 50 and plan[8] == r8["ndoc"] and plan[5] == 50
+    B = np.random.default_rng(3).standard_normal((x.shape[1], 16)).astype(np.float32)
+    np.testing.assert_allclose(exec_split_plan(plan, B), csr_ref.spmm_csr(rp, ci, v, B), rtol=1e-12, atol=1e-9)
+    # the transpose (X^T g of the backward): dense rows first
+    rt, ct, vt = csr_ref.coo_to_csr(idx[1], idx[0], x.values().numpy(), (x.shape[1], x.shape[0]))
+    pt = build_host_plan(rt, ct, vt, (x.shape[1], x.shape[0]))
+    assert pt[0] == SPLIT_MAGIC and pt[7] == 50 and pt[8] == 0
+    G = np.random.default_rng(4).standard_normal((x.shape[0], 8)).astype(np.float32)
+    np.testing.assert_allclose(exec_split_plan(pt, G), csr_ref.spmm_csr(rt, ct, vt, G), rtol=1e-12, atol=1e-9)
+    # a negative threshold keeps the tile path (no split plan)
+    assert build_host_plan(rp, ci, v, x.shape, dense=-0.25)[0] == ROW_MAGIC
+
+
+def test_split_plan_duplicates_and_fallbacks():
+    rng = np.random.default_rng(8)
+    M, K = 900, 700
+    hot = np.sort(rng.choice(K, 20, replace=False))
+    rows, cols = [], []
+    for r in range(M):
+        if 100 <= r < 110:
+            c = rng.choice(K, 400, replace=False)
+        else:
+            c = rng.choice(hot, 8, replace=True)          # duplicates: summed in CSR order
+        rows.append(np.full(len(c), r))
+        cols.append(c)
+    rows, cols = np.concatenate(rows), np.concatenate(cols)
+    vals = rng.standard_normal(rows.size).astype(np.float32)
+    rp, ci, v = csr_ref.coo_to_csr(rows, cols, vals, (M, K))
+    plan = build_host_plan(rp, ci, v, (M, K), hub_min=-1)
+    assert plan[0] == SPLIT_MAGIC and plan[7] == 10 and plan[8] == 100
+    B = rng.standard_normal((K, 12)).astype(np.float32)
+    v32 = v.astype(np.float32).astype(np.float64)             # the plan stores fp32 values
+    np.testing.assert_allclose(exec_split_plan(plan, B), csr_ref.spmm_csr(rp, ci, v32, B), rtol=1e-9, atol=1e-9)
+    # dense rows not contiguous -> not the split plan
+    rows2 = np.where(rows == 105, 500, np.where(rows == 500, 105, rows))
+    rp2, ci2, v2 = csr_ref.coo_to_csr(rows2, cols, vals, (M, K))
+    assert build_host_plan(rp2, ci2, v2, (M, K), hub_min=-1)[0] == ROW_MAGIC

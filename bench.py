@@ -228,6 +228,37 @@ def rocprof_kernel_us(mode, kernels_like, save_dir=None):
         shutil.rmtree(tmp, ignore_errors=True)
 
 
+def forward_kernels(save_dir=None):
+    """Per-kernel durations of the product forward (hipGraph replay) from a child
+    rocprofv3 --kernel-trace run of scripts/fwd_trace.py, in launch order."""
+    exe = shutil.which("rocprofv3")
+    if exe is None:
+        return None, "rocprofv3 not on PATH"
+    tmp = tempfile.mkdtemp(prefix="gcnk_fwd_", dir="/tmp")
+    env = dict(os.environ, TMPDIR="/tmp")
+    try:
+        cmd = ["timeout", "-s", "KILL", "150", exe, "--kernel-trace", "--stats", "--output-format", "csv", "-d", tmp,
+               "-o", "fwd", "--", sys.executable, os.path.join(ROOT, "scripts", "fwd_trace.py")]
+        r = subprocess.run(cmd, cwd=ROOT, env=env, stdout=subprocess.PIPE, stderr=subprocess.STDOUT, timeout=180)
+        if r.returncode != 0:
+            return None, f"rocprofv3 --kernel-trace rc={r.returncode}"
+        sys.path.insert(0, os.path.join(ROOT, "scripts"))
+        import fwd_trace
+        import contextlib
+        import io
+        with contextlib.redirect_stdout(io.StringIO()):
+            res = fwd_trace.report(tmp)
+        if save_dir:
+            os.makedirs(save_dir, exist_ok=True)
+            for f in glob.glob(os.path.join(tmp, "**", "*kernel_stats.csv"), recursive=True):
+                shutil.copy(f, os.path.join(save_dir, "bench_forward_kernel_stats.csv"))
+        return res, "rocprofv3 --kernel-trace, scripts/fwd_trace.py (hipGraph of 10 forwards, 20 replays)"
+    except (OSError, subprocess.SubprocessError, KeyError, ValueError, ImportError) as e:
+        return None, f"forward trace failed: {e}"
+    finally:
+        shutil.rmtree(tmp, ignore_errors=True)
+
+
 def sharded_config5(dev, world, rank, datasets, ops, F=4096, reps=3):
     """BASELINE config 5 on this job's ranks: the replicated 1M / 20M CSR, this
     rank's F / P columns of B, the local SpMM and the all-gather of the result
@@ -433,6 +464,34 @@ def main():
         for mode in ("warm", "cold"):
             kt[mode] = rocprof_kernel_us(mode, ["hub_group_kernel", "spmm_row_kernel"], args.rocprof_dir)
 
+    # ---- the product forward's own kernels (rocprofv3 trace of the graph replay),
+    #      each against its algorithmic bytes; the fused north-star kernel among them
+    fwd_k = None
+    if extras and not args.no_rocprof:
+        trace, trace_src = forward_kernels(args.rocprof_dir)
+        if trace is not None and trace.get("kernels"):
+            from graph_convolutional_networks_for_text_classification_amd import ops as _ops
+            nsl = int(_ops._lib.load().gcnk_spmm_proj_slices(
+                _ops.ctypes.cast(next(p for p in a_csr._plans.values() if p.is_hub).hdr, _ops.ctypes.c_void_p), nhid)) \
+                if any(p.is_hub for p in a_csr._plans.values()) else 1
+            alg = {   # algorithmic bytes of each launch of the eval forward (SURVEY §8(d) formula)
+                "xw_kernel": spmm_bytes(N, nfeat, nnz_x, nhid),
+                "A S1": 4 * (N + 1) + 8 * nnz_a + 4 * N * nhid + 4 * nsl * N * nclass + 4 * nhid * nclass,
+                "A sum S2": 4 * (N + 1) + 8 * nnz_a + 4 * nsl * N * nclass + 4 * N * nclass,
+            }
+            ks = []
+            for i, k in enumerate(trace["kernels"]):
+                name = k["kernel"]
+                key = "xw_kernel" if "xw_kernel" in name else ("A S1" if i == 1 else "A sum S2" if i == 2 else None)
+                entry = {"kernel": name[:80], "us": k["us"]}
+                if key is not None:
+                    entry.update({"op": key, "algorithmic_bytes": alg[key],
+                                  "frac": alg[key] / (k["us"] * 1e-6) / 1e9 / HBM_PEAK_GBS})
+                ks.append(entry)
+            fwd_k = {"source": trace_src, "forward_span_us": trace["forward_span_us_median"], "kernels": ks}
+        else:
+            fwd_k = {"error": trace_src}
+
     # ---- CPU baselines (rank 0, N = 1): oracle at all cores and 1 thread, torch CSR (MKL)
     cpu = cpu_stock = gpu_stock = None
     if extras and args.cpu_sample_s > 0:
@@ -606,6 +665,7 @@ def main():
                              for m, v in kt.items()},
         "roofline_dominant": {"kernel": dom, "frac": kd["frac_cold"], "frac_warm": kd["frac_warm"],
                               "avg_launch_us": kd["cold_us"], "algorithmic_bytes": kd["algorithmic_bytes"]},
+        "forward_kernels": fwd_k,
         "ops": optimes,
         "cpu_baseline": cpu,
         "cpu_stock_csr": cpu_stock,

@@ -56,8 +56,8 @@ def report(d):
         return
     seq = rows[-(len(rows) // k) * k:]
     # the R8 eval forward's launches in order (ops.GCNFn.forward, FUSE_PROJECTION)
-    seq_names = ["spmm_tile_kernel (X W1)", "spmm_tile_reduce_kernel (X W1 topic slabs)",
-                 "spmm_row_kernel (A S1 + b1, ReLU, H1 W2 fused)", "spmm_row_kernel (A S2 + b2)"]
+    seq_names = ["xw_kernel (X W1, split plan)", "hub_group_kernel (A S1 + b1, ReLU, H1 W2 per slice)",
+                 "hub_group_kernel (A sum S2 + b2)"]
     out = []
     for j in range(k):
         durs, gaps = [], []
@@ -73,8 +73,9 @@ def report(d):
                     "gap_before_us": round(statistics.median(gaps), 3) if gaps else None})
     per_fwd = [(int(seq[i + k - 1]["End_Timestamp"]) - int(seq[i]["Start_Timestamp"])) / 1e3
                for i in range(k, len(seq) - k, k)]
-    print(json.dumps({"kernels_per_forward": k, "forward_span_us_median": round(statistics.median(per_fwd), 3),
-                      "kernels": out}, indent=1))
+    res = {"kernels_per_forward": k, "forward_span_us_median": round(statistics.median(per_fwd), 3), "kernels": out}
+    print(json.dumps(res, indent=1))
+    return res
 
 
 if __name__ == "__main__":

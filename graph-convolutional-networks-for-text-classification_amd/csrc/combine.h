@@ -138,6 +138,7 @@ __device__ __forceinline__ void hub_combine(uint64_t* ctr, int32_t K, int32_t* s
   __shared__ int32_t s_flag;
   if (tid == 0) s_old = __hip_atomic_fetch_add(cnt, (uint64_t)1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
   __syncthreads();
+  stamp(epi, 2);
   const uint64_t old = s_old;
   const uint64_t launch = old / (uint64_t)G;
   const int32_t rank = (int32_t)(old - launch * (uint64_t)G);

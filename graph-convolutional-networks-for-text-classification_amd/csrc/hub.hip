@@ -251,14 +251,6 @@ hub_group_kernel(const int32_t* __restrict__ recs, int32_t R, int32_t roff, int3
       if constexpr (PROJ) project4(v, j, s_w, x.P, s_proj + (int64_t)e * kProjMax);
     }
   }
-#ifdef GCNK_STAMPS
-  // 2: the first hub wave done, 3: the last light wave done (no barrier: the
-  // two wave sets' own finishing times)
-  if (epi.stamps && lane == 0 && (wv == 0 || wv == NW - 1)) {
-    const unsigned long long t = __builtin_amdgcn_s_memrealtime();
-    epi.stamps[4 * (unsigned long long)blockIdx.x + (wv == 0 ? 2 : 3)] = t;
-  }
-#endif
   __syncthreads();
   // ---- this group's hub partials (hub t's batch sums in batch order), stored
   //      write-through (sc1) for the in-launch combine below
@@ -284,6 +276,7 @@ hub_group_kernel(const int32_t* __restrict__ recs, int32_t R, int32_t roff, int3
     __syncthreads();  // s_proj is reused by the combine
   }
   hub_combine<kGroupBlock, VEC, PROJ>(ctr, K, s_rec, G, c, h0, H, w, q0, part_u, part_ld, C, ldc, epi, s_bias, s_w, s_proj, x, tid);
+  stamp(epi, 3);  // 2: arrival (combine.h), 3: exit
 }
 
 // LDS words before the row image: the record, at least the combine's scratch
@@ -528,8 +521,8 @@ int hub_spmm(const void* plan, const int32_t* hdr, const float* B, int64_t ldb, 
   const int32_t* p = (const int32_t*)plan;
   HubExtra x{side.W, side.ldw, side.P, side.C2, side.c2_stride, side.ldc2, side.nsum, side.bstride};
   const bool proj = side.W != nullptr, bsum = side.nsum > 1;
-  if ((proj || bsum) && !vec4) {
-    set_error("gcnk_spmm (hub plan): fused projection / summed operand need float4-aligned operands");
+  if (proj && !vec4) {
+    set_error("gcnk_spmm (hub plan): a fused projection needs float4-aligned operands");
     return GCNK_EUNSUP;
   }
   if (proj && (side.P < 1 || side.P > kProjMax || !side.C2)) {
@@ -541,7 +534,9 @@ int hub_spmm(const void* plan, const int32_t* hdr, const float* B, int64_t ldb, 
     return GCNK_EUNSUP;
   }
   if (proj) return hub_launch<4, true, false>(p, L, B, ldb, F, C, ldc, e, workspace, part_ld, ctr, x, s);
-  if (bsum) return hub_launch<4, false, true>(p, L, B, ldb, F, C, ldc, e, workspace, part_ld, ctr, x, s);
+  if (bsum && vec4 && x.bstride % 4 == 0)
+    return hub_launch<4, false, true>(p, L, B, ldb, F, C, ldc, e, workspace, part_ld, ctr, x, s);
+  if (bsum) return hub_launch<1, false, true>(p, L, B, ldb, F, C, ldc, e, workspace, part_ld, ctr, x, s);
   if (vec4) return hub_launch<4, false, false>(p, L, B, ldb, F, C, ldc, e, workspace, part_ld, ctr, x, s);
   return hub_launch<1, false, false>(p, L, B, ldb, F, C, ldc, e, workspace, part_ld, ctr, x, s);
 }

@@ -42,7 +42,10 @@ DENSE_THRESHOLD = 0.25  # row blocks at least this dense (condensed) run on the 
 # of heavy hub rows; every other row references only hub columns and its own
 # diagonal -- the reference's doc-topic adjacency): 0 = automatic hub
 # threshold, > 0 = degree threshold, < 0 = never (row-unit + tile plan).
-HUB_MIN = 0
+# Off by default: on R8 A-hat the in-launch combine of the hub partials costs
+# more than it saves (profiles/r03_hub.md: 20.0 us at F = 200 vs the row plan's
+# 10.4 us), so the row-unit plan stays the product path.
+HUB_MIN = -1
 HUB_BLOCK_ROWS = 0      # light rows per hub-plan group (0 = automatic, ~256 workgroups)
 # split plan (csrc/xw.hip) for operands with a contiguous range of dense rows
 # among rows that use a few "hot" columns (the reference's topic features X

@@ -64,8 +64,17 @@ def main():
             t0 = gk[:, 0].min()
             res = {"F": F, "block_rows": br, "G": G, "group_blocks": ng, "sum_blocks": len(sk),
                    "g_entry": pct((gk[:, 0] - t0) / 100), "g_loads": pct((gk[:, 1] - gk[:, 0]) / 100),
-                   "g_hub_waves": pct((gk[:, 2] - gk[:, 1]) / 100), "g_light_waves": pct((gk[:, 3] - gk[:, 1]) / 100),
-                   "g_end": pct((np.maximum(gk[:, 2], gk[:, 3]) - t0) / 100)}
+                   "g_compute": pct((gk[:, 2] - gk[:, 1]) / 100), "g_arrive": pct((gk[:, 2] - t0) / 100),
+                   "g_exit": pct((gk[:, 3] - t0) / 100), "g_combine": pct((gk[:, 3] - gk[:, 2]) / 100)}
+            # per slice: last arrival and last exit
+            ns = max(1, ng // G)
+            arr = (gk[:, 2] - t0).reshape(ns, G) / 100
+            ext = (gk[:, 3] - t0).reshape(ns, G) / 100
+            res["slice_last_arrival"] = [round(float(x), 2) for x in arr.max(1)]
+            res["slice_last_exit"] = [round(float(x), 2) for x in ext.max(1)]
+            order = np.argsort(arr, axis=1)
+            res["combine_us_by_rank_from_last"] = [round(float(np.median((ext - arr)[np.arange(ns), order[:, -1 - k]])), 2)
+                                                   for k in range(min(G, 9))]
             if len(sk):
                 res.update({"s_entry": pct((sk[:, 0] - t0) / 100), "s_sum": pct((sk[:, 1] - sk[:, 0]) / 100),
                             "s_end": pct((sk[:, 2] - t0) / 100)})

@@ -48,6 +48,13 @@ def _random_csr(M, K, nnz, rng, heavy_rows=(), heavy_deg=0, empty_frac=0.0):
     return csr_ref.coo_to_csr(rows, cols, vals, (M, K))
 
 
+@pytest.fixture
+def hub_on(monkeypatch):
+    """The hub plan is opt-in (sparse.HUB_MIN = -1 by default); its tests turn it on."""
+    from graph_convolutional_networks_for_text_classification_amd import sparse as sp
+    monkeypatch.setattr(sp, "HUB_MIN", 0)
+
+
 def test_native_library_is_loaded():
     lib = _lib.load()
     assert lib.gcnk_abi_version() == _lib.ABI_VERSION
@@ -237,7 +244,7 @@ def test_spmm_split_plan_synthetic(F):
         elif r % 11 == 0:
             continue
         else:
-            c = rng.choice(hot, int(rng.integers(1, 20)), replace=True)
+            c = rng.choice(hot, int(rng.integers(15, 40)), replace=True)   # duplicates summed; >= 1/4 full
         rows.append(np.full(len(c), r))
         cols.append(c)
     rows, cols = np.concatenate(rows), np.concatenate(cols)
@@ -262,8 +269,7 @@ def test_spmm_fused_projection(r8, P, store_main, kind, monkeypatch):
     + b2 (spmm_sum / gcnk_spmm_sum_csr_f32) against the oracle."""
     from graph_convolutional_networks_for_text_classification_amd import sparse as sp
     from graph_convolutional_networks_for_text_classification_amd.ops import spmm_proj, spmm_sum
-    if kind == "row":
-        monkeypatch.setattr(sp, "HUB_MIN", -1)
+    monkeypatch.setattr(sp, "HUB_MIN", 0 if kind == "hub" else -1)
     a = from_torch(r8["adj"].to(DEV))
     rng = np.random.default_rng(P)
     N, F = r8["nodes"], 200
@@ -293,7 +299,7 @@ def test_spmm_fused_projection(r8, P, store_main, kind, monkeypatch):
 
 @pytest.mark.parametrize("nsum", [2, 7, 13])
 @pytest.mark.parametrize("F", [8, 64])
-def test_spmm_sum_of_operands(r8, nsum, F):
+def test_spmm_sum_of_operands(r8, nsum, F, hub_on):
     """gcnk_spmm_sum_csr_f32: C = A (B_0 + ... + B_{n-1}) + b on the hub plan,
     the operands summed in order while staged."""
     from graph_convolutional_networks_for_text_classification_amd.ops import spmm_sum
@@ -361,8 +367,8 @@ def test_spmm_two_streams_share_one_plan_concurrently(r8, kind, monkeypatch):
 
 @pytest.mark.parametrize("F", [1, 3, 8, 24, 64, 200, 256, 300, 1000])
 @pytest.mark.parametrize("lanes", [0, 64])
-def test_spmm_hub_plan_r8(r8, F, lanes):
-    """The hub plan (default for operands with its structure) on the R8
+def test_spmm_hub_plan_r8(r8, F, lanes, hub_on):
+    """The hub plan (opt-in, sparse.HUB_MIN >= 0) on the R8
     adjacency: 32 (or ~256 at narrow widths) row groups x column slices, the
     documents from the LDS image, the 50 topic rows summed from the groups'
     partials; every width class (float4 and scalar paths), bias + ReLU, against
@@ -384,7 +390,7 @@ def test_spmm_hub_plan_r8(r8, F, lanes):
 
 @pytest.mark.parametrize("F", [4, 7, 16, 200])
 @pytest.mark.parametrize("block_rows", [0, 1, 33, 512])
-def test_spmm_hub_plan_synthetic_every_epilogue(F, block_rows, monkeypatch):
+def test_spmm_hub_plan_synthetic_every_epilogue(F, block_rows, monkeypatch, hub_on):
     """Hub plan on a doc-topic-like operand with the hub range in the middle
     (groups straddle it), hub x hub nonzeros, empty light rows and rows without
     a diagonal; every epilogue (bias, relu, dropout mask, hash dropout),
@@ -610,18 +616,38 @@ def test_gcn_eval_logits_match_reference(r8, golden_logits, seed):
 
 def test_trained_model_labels_bit_exact_on_every_row(r8, trained_golden):
     """The reference's TRAINED model (seed 50494, 72 epochs; its min top-2 gap
-    is 5.1e-3) loaded into the HIP GCN: logits within 1e-4 and the predicted
-    label of EVERY node identical to the reference's -- no exclusions -- so
-    the test accuracy is the reference's to the last document."""
+    is 5.1e-3) loaded into the HIP GCN: the predicted label of EVERY node is
+    the reference's -- no exclusions -- so the test accuracy is the
+    reference's to the last document.
+
+    Logits: trained logits reach |190|, where fp32 itself is coarse -- the
+    reference's own CPU result is 1.9e-4 away from the float64 forward (its
+    7,463-term dot products accumulate in one serial fp32 chain).  A 1e-4
+    bound against the reference would demand reproducing its rounding
+    sequence; instead the HIP forward must be at least as close to the
+    float64 truth as the reference is (and within that distance of it twice
+    over), and within 1e-4 relative to the logit scale."""
+    import scipy.sparse as ssp
     m = GCN(nfeat=r8["nfeat"], nhid=200, nclass=r8["nclass"], dropout=0.5).to(DEV)
     m.load_state_dict(trained_golden["state_dict"])
     m.eval()
     with torch.no_grad():
         lg = m(r8["features"].to(DEV), r8["adj"].to(DEV)).cpu().numpy()
     gold = trained_golden["logits"]
+    sd = {k: v.double().numpy() for k, v in trained_golden["state_dict"].items()}
+    x = r8["features"].coalesce()
+    X = ssp.csr_matrix((x.values().double().numpy(), x.indices().numpy()), shape=tuple(x.shape))
+    a = r8["adj"].coalesce()
+    A = ssp.csr_matrix((a.values().double().numpy(), a.indices().numpy()), shape=tuple(a.shape))
+    H1 = np.maximum(A @ (X @ sd["gc1.weight"]) + sd["gc1.bias"], 0.0)
+    truth = A @ (H1 @ sd["gc2.weight"]) + sd["gc2.bias"]
+    err_ref = float(np.abs(gold - truth).max())
+    err_hip = float(np.abs(lg - truth).max())
     err = float(np.abs(lg - gold).max())
-    print(f"trained model: max logit err {err:.2e}")
-    assert err <= LOGIT_TOL
+    scale = float(np.abs(gold).max())
+    print(f"trained model: |logit| <= {scale:.1f}; max err vs reference {err:.2e}; vs float64: reference "
+          f"{err_ref:.2e}, HIP {err_hip:.2e}")
+    assert err_hip <= err_ref and err <= 2 * err_ref and err <= 1e-4 * scale
     assert np.array_equal(lg.argmax(1), gold.argmax(1)), f"{int(np.sum(lg.argmax(1) != gold.argmax(1)))} labels differ"
     test = np.asarray(r8["test_lst"])
     acc = float(np.mean(lg[test].argmax(1) == np.asarray(r8["target"])[test]))
@@ -994,6 +1020,8 @@ def test_spmm_two_part_launch_matches_single(monkeypatch, r8):
     """gcnk_spmm_csr_f32_part: the single-chunk tile blocks on a side stream and
     the rest on the caller's stream give the one-launch result bit for bit."""
     from graph_convolutional_networks_for_text_classification_amd import ops
+    from graph_convolutional_networks_for_text_classification_amd import sparse as sp
+    monkeypatch.setattr(sp, "SPLIT_PLAN", False)   # R8 X on the tile path
     rng = np.random.default_rng(7)
     for a, K in ((from_torch(r8["features"].to(DEV)), r8["nfeat"]), (None, 900)):
         if a is None:
@@ -1054,6 +1082,7 @@ def test_graph_capture_takes_a_prezeroed_counter_region(r8, kind, monkeypatch):
         rp, ci, v = _random_csr(M, K, 20000, rng, heavy_rows=(5, 1700), heavy_deg=2500)
         a = from_arrays(rp, ci, v, (M, K), DEV)
     else:
+        monkeypatch.setattr(sp, "HUB_MIN", 0)
         a, K, F = from_torch(r8["adj"].to(DEV)), r8["nodes"], 200
     B = torch.from_numpy(rng.standard_normal((K, F)).astype(np.float32)).to(DEV)
     ref = spmm(a, B, dense=2.0)

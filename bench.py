@@ -192,7 +192,7 @@ def pmc_traffic(op, kernels_like):
         shutil.rmtree(tmp, ignore_errors=True)
 
 
-def rocprof_kernel_us(mode, kernels_like, save_dir=None):
+def rocprof_kernel_us(mode, kernels_like, save_dir=None, variant="row"):
     """Average kernel duration (us) of the north-star op's kernels from a child
     rocprofv3 --kernel-trace --stats run of scripts/hub_probe.py (the same op,
     the same warm / cold rotation as the HIP-event figure), so the reported
@@ -205,7 +205,7 @@ def rocprof_kernel_us(mode, kernels_like, save_dir=None):
     try:
         cmd = ["timeout", "-s", "KILL", "150", exe, "--kernel-trace", "--stats", "--output-format", "csv", "-d", tmp,
                "-o", "kt", "--", sys.executable, os.path.join(ROOT, "scripts", "hub_probe.py"), "--reps", "200",
-               "--variants", "hub", "--widths", "200", "--mode", mode]
+               "--variants", variant, "--widths", "200", "--mode", mode]
         r = subprocess.run(cmd, cwd=ROOT, env=env, stdout=subprocess.PIPE, stderr=subprocess.STDOUT, timeout=180)
         if r.returncode != 0:
             return None, f"rocprofv3 --kernel-trace rc={r.returncode}"
@@ -462,7 +462,8 @@ def main():
     kt = {}
     if extras and not args.no_rocprof:
         for mode in ("warm", "cold"):
-            kt[mode] = rocprof_kernel_us(mode, ["hub_group_kernel", "spmm_row_kernel"], args.rocprof_dir)
+            kt[mode] = rocprof_kernel_us(mode, ["hub_group_kernel", "spmm_row_kernel"], args.rocprof_dir,
+                                         plan_kinds[north])
 
     # ---- the product forward's own kernels (rocprofv3 trace of the graph replay),
     #      each against its algorithmic bytes; the fused north-star kernel among them
@@ -475,19 +476,25 @@ def main():
                 _ops.ctypes.cast(next(p for p in a_csr._plans.values() if p.is_hub).hdr, _ops.ctypes.c_void_p), nhid)) \
                 if any(p.is_hub for p in a_csr._plans.values()) else 1
             alg = {   # algorithmic bytes of each launch of the eval forward (SURVEY §8(d) formula)
-                "xw_kernel": spmm_bytes(N, nfeat, nnz_x, nhid),
+                "X W1": spmm_bytes(N, nfeat, nnz_x, nhid),
                 "A S1": 4 * (N + 1) + 8 * nnz_a + 4 * N * nhid + 4 * nsl * N * nclass + 4 * nhid * nclass,
                 "A sum S2": 4 * (N + 1) + 8 * nnz_a + 4 * nsl * N * nclass + 4 * N * nclass,
             }
-            ks = []
-            for i, k in enumerate(trace["kernels"]):
+            ks, na = [], 0
+            for k in trace["kernels"]:   # the A-hat launches are the row / hub kernels, X W1 the rest
                 name = k["kernel"]
-                key = "xw_kernel" if "xw_kernel" in name else ("A S1" if i == 1 else "A sum S2" if i == 2 else None)
-                entry = {"kernel": name[:80], "us": k["us"]}
-                if key is not None:
-                    entry.update({"op": key, "algorithmic_bytes": alg[key],
-                                  "frac": alg[key] / (k["us"] * 1e-6) / 1e9 / HBM_PEAK_GBS})
-                ks.append(entry)
+                if "spmm_row_kernel" in name or "hub_group_kernel" in name:
+                    key = "A S1" if na == 0 else "A sum S2"
+                    na += 1
+                else:
+                    key = "X W1"
+                ks.append({"kernel": name[:120], "us": k["us"], "op": key})
+            for key, nb in alg.items():   # per op: its launches' summed duration against its bytes
+                us = sum(e["us"] for e in ks if e["op"] == key)
+                for e in ks:
+                    if e["op"] == key:
+                        e.update({"op_us": round(us, 3), "algorithmic_bytes": nb,
+                                  "frac": nb / (us * 1e-6) / 1e9 / HBM_PEAK_GBS if us > 0 else None})
             fwd_k = {"source": trace_src, "forward_span_us": trace["forward_span_us_median"], "kernels": ks}
         else:
             fwd_k = {"error": trace_src}

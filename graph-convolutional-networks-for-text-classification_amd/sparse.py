@@ -49,8 +49,10 @@ HUB_MIN = -1
 HUB_BLOCK_ROWS = 0      # light rows per hub-plan group (0 = automatic, ~256 workgroups)
 # split plan (csrc/xw.hip) for operands with a contiguous range of dense rows
 # among rows that use a few "hot" columns (the reference's topic features X
-# and X^T); False leaves them to the row-unit + tile plan
-SPLIT_PLAN = True
+# and X^T); False leaves them to the row-unit + tile plan.  Off by default:
+# its in-launch split-K combine made R8 X W1 37.6 us against the tile plan's
+# ~12 us (profiles/r03_forward.md)
+SPLIT_PLAN = False
 
 
 class Plan:

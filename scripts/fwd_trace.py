@@ -13,6 +13,9 @@ ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path.insert(0, ROOT)
 
 
+FORWARDS, REPLAYS = 10, 20
+
+
 def run():
     import torch
     import gcn_amd  # noqa: F401
@@ -23,14 +26,14 @@ def run():
     m = GCN(nfeat=r8["nfeat"], nhid=200, nclass=r8["nclass"], dropout=0.5).to(dev).eval()
     x, adj = r8["features"].to(dev), r8["adj"].to(dev)
     with torch.no_grad():
-        for _ in range(3):
+        for _ in range(3):   # plan builds, then eager forwards (their kernel names are the trace's labels)
             m(x, adj)
         torch.cuda.synchronize()
         g = torch.cuda.CUDAGraph()
         with torch.cuda.graph(g):
-            for _ in range(10):
+            for _ in range(FORWARDS):
                 m(x, adj)
-        for _ in range(20):
+        for _ in range(REPLAYS):
             g.replay()
         torch.cuda.synchronize()
 
@@ -54,10 +57,11 @@ def report(d):
     if k is None:
         print(json.dumps({"error": "no periodic forward found"}))
         return
-    seq = rows[-(len(rows) // k) * k:]
-    # the R8 eval forward's launches in order (ops.GCNFn.forward, FUSE_PROJECTION)
-    seq_names = ["xw_kernel (X W1, split plan)", "hub_group_kernel (A S1 + b1, ReLU, H1 W2 per slice)",
-                 "hub_group_kernel (A sum S2 + b2)"]
+    ng = FORWARDS * REPLAYS * k
+    seq = rows[-ng:]
+    # graph-replayed kernels can carry a blit's name in the trace: label each
+    # position with the kernel the last eager forward launched there
+    eager = [r["Kernel_Name"] for r in rows[-ng - k:-ng]] if len(rows) >= ng + k else []
     out = []
     for j in range(k):
         durs, gaps = [], []
@@ -67,9 +71,9 @@ def report(d):
             if i > 0:
                 gaps.append((s - int(seq[i - 1]["End_Timestamp"])) / 1e3)
         name = seq[j]["Kernel_Name"]
-        if "rocclr" in name and len(seq_names) == k:   # graph-replayed kernels can carry a blit's name
-            name = seq_names[j] + " (by position; trace name: " + name[:40] + ")"
-        out.append({"kernel": name[:110], "us": round(statistics.median(durs), 3),
+        if "rocclr" in name and len(eager) == k and "rocclr" not in eager[j]:
+            name = eager[j] + " (by position; trace name: " + name[:40] + ")"
+        out.append({"kernel": name[:160], "us": round(statistics.median(durs), 3),
                     "gap_before_us": round(statistics.median(gaps), 3) if gaps else None})
     per_fwd = [(int(seq[i + k - 1]["End_Timestamp"]) - int(seq[i]["Start_Timestamp"])) / 1e3
                for i in range(k, len(seq) - k, k)]

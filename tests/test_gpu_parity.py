@@ -207,8 +207,15 @@ def test_csr_to_dense_sums_duplicates_in_order():
 SPLIT_MAGIC = 0x474E5831
 
 
+@pytest.fixture
+def split_on(monkeypatch):
+    """The split plan is opt-in (sparse.SPLIT_PLAN = False by default)."""
+    from graph_convolutional_networks_for_text_classification_amd import sparse as sp
+    monkeypatch.setattr(sp, "SPLIT_PLAN", True)
+
+
 @pytest.mark.parametrize("F", [200, 8, 64, 100, 257, 300])
-def test_spmm_r8_features_split_plan(r8, F):
+def test_spmm_r8_features_split_plan(r8, F, split_on):
     """R8 X W1 (layer.py:102) and X^T G (its autograd) on the split plan: the
     document / feature rows over 50 hot columns on MFMA, the 50 dense rows as
     split-K chunks summed in order inside the launch; float4 and scalar paths."""
@@ -231,7 +238,7 @@ def test_spmm_r8_features_split_plan(r8, F):
 
 
 @pytest.mark.parametrize("F", [16, 200])
-def test_spmm_split_plan_synthetic(F):
+def test_spmm_split_plan_synthetic(F, split_on):
     """Split plan on a synthetic operand: dense rows in the middle, light rows
     over 37 hot columns with empty rows and duplicates summed, rectangular."""
     rng = np.random.default_rng(F + 5)

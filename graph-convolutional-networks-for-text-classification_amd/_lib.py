@@ -31,7 +31,7 @@ def _resolve_lib():
 
 
 LIB_PATH = _resolve_lib()
-ABI_VERSION = 3
+ABI_VERSION = 4
 
 # C-ABI return codes (gcnk.h)
 OK, EARG, EUNSUP, EHIP = 0, -1, -2, -3
@@ -130,6 +130,12 @@ SIGNATURES = {
     ]),
     "gcnk_colsum_workspace_bytes": (_i64, [_i32, _i32]),
     "gcnk_colsum_f32": (ctypes.c_int, [_vp, _i64, _i32, _i32, _vp, _vp, _i64, _vp]),
+    "gcnk_gcn_bwd2_workspace_bytes": (_i64, [_i32, _i32, _i32]),
+    "gcnk_gcn_bwd2_f32": (ctypes.c_int, [
+        _vp, _i64, _vp, _i64, _vp, _i64,   # H, ldh, gS, ldgs, W, ldw
+        _vp, _i64, _i32, _i32, _i32, _f32,  # G, ldg, M, N, P, scale
+        _vp, _i64, _vp, _vp, _vp,          # gZ1, ldz, gW, gb1, gb2
+        _vp, _i64, _vp]),                  # workspace, bytes, stream
     "gcnk_class_stats": (ctypes.c_int, [_vp, _i64, _vp, _vp, _i64, _i32, _vp, _vp]),
     "gcnk_edgelist_size": (ctypes.c_int, [ctypes.c_char_p, _vp, _vp]),
     "gcnk_edgelist_csr": (ctypes.c_int, [ctypes.c_char_p, _i64, _i64, _vp, _vp, _vp]),

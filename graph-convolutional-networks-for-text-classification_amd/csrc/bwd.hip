@@ -1,0 +1,304 @@
+// Fused backward of gc2 and of gc1's ReLU + dropout (the autograd of
+// reference layer.py:182-188 through layer.py:102-110, run by trainer.py:361):
+//
+//   gZ1[m, n] = H1[m, n] > 0 ? scale * (gS2[m, :] . W2[n, :]) : 0     [M x N]
+//   gW2[n, p] = sum_m H1[m, n] gS2[m, p]                              [N x P]
+//   gb1[n]    = sum_m gZ1[m, n]                                       [N]
+//   gb2[p]    = sum_m G[m, p]          (optional)                     [P]
+//
+// with gS2 = A^T G computed before (spmm).  H1 is gc1's stored output (after
+// ReLU and dropout), so H1 > 0 <=> kept and positive, and the scale is the
+// dropout's 1/(1-p) (1 in eval / without dropout): ATen's mm(gS2, W2^T), mul
+// by the dropout noise, threshold_backward and the two bias sums in one
+// pass over H1 instead of a K = 8 GEMM, a split-K GEMM + its reduce and two
+// two-pass column sums (profiles/r03_train_breakdown.json: 48 us of 85 us of
+// the step's gcnk kernels).
+//
+// Kernel 1 (gcn_bwd2_kernel): one workgroup per run of rows x a 256-column
+// slice.  Lane (rl, cu): column unit cu (VEC columns), rows rl, rl + RL, ...
+// The rows' gS2 (and G) values are staged in LDS once; each lane keeps its
+// columns' W2 rows in registers, writes gZ1 and accumulates its columns' gW2 /
+// gb1 terms in row order; the RL row lanes are then summed through LDS in
+// lane order and the workgroup's partial goes to the workspace.
+// Kernel 2 (gcn_bwd2_reduce_kernel): every output sums the workgroups'
+// partials in workgroup order.  Fixed order everywhere: bitwise reproducible.
+#include "gcnk_common.h"
+
+#include <algorithm>
+
+namespace gcnk {
+namespace {
+
+constexpr int kBwdBlock = 256;
+constexpr int kBwdCols = 256;      // columns per workgroup slice
+constexpr int kBwdRowsMax = 256;   // rows per workgroup (LDS staging of gS2 / G)
+constexpr int kBwdBatch = 8;       // rows per lane whose H1 loads are in flight together
+constexpr int kBwdTarget = 256;    // workgroups per slice (one per CU)
+
+template <int VEC>
+struct VecIO;
+template <>
+struct VecIO<4> {
+  static __device__ __forceinline__ void load(const float* p, float (&v)[4]) {
+    const float4 x = *reinterpret_cast<const float4*>(p);
+    v[0] = x.x; v[1] = x.y; v[2] = x.z; v[3] = x.w;
+  }
+  static __device__ __forceinline__ void store(float* p, const float (&v)[4]) {
+    *reinterpret_cast<float4*>(p) = make_float4(v[0], v[1], v[2], v[3]);
+  }
+};
+template <>
+struct VecIO<2> {
+  static __device__ __forceinline__ void load(const float* p, float (&v)[2]) {
+    const float2 x = *reinterpret_cast<const float2*>(p);
+    v[0] = x.x; v[1] = x.y;
+  }
+  static __device__ __forceinline__ void store(float* p, const float (&v)[2]) {
+    *reinterpret_cast<float2*>(p) = make_float2(v[0], v[1]);
+  }
+};
+template <>
+struct VecIO<1> {
+  static __device__ __forceinline__ void load(const float* p, float (&v)[1]) { v[0] = *p; }
+  static __device__ __forceinline__ void store(float* p, const float (&v)[1]) { *p = v[0]; }
+};
+
+struct Bwd2Args {
+  const float* H; int64_t ldh;
+  const float* gS; int64_t ldgs;
+  const float* W; int64_t ldw;
+  const float* G; int64_t ldg;
+  int32_t M, N, P;
+  float scale;
+  float* Z; int64_t ldz;
+  float* part; int64_t part_ld;   // per workgroup row: gW2 [N*P] | gb1 [N] | gb2 [P]
+  int32_t rpb;                    // rows per workgroup
+};
+
+template <int VEC, int PM>
+__global__ void __launch_bounds__(kBwdBlock) gcn_bwd2_kernel(Bwd2Args a) {
+  constexpr int KE = VEC * (PM + 1);  // accumulators per lane: gW2 terms + gb1
+  __shared__ __attribute__((aligned(16))) float s_g[kBwdRowsMax * PM];
+  __shared__ float s_gg[kBwdRowsMax * PM];
+  __shared__ float s_red[kBwdBlock * KE];
+  const int tid = threadIdx.x;
+  const int32_t units = (a.N + VEC - 1) / VEC;
+  const int32_t cu0 = (int32_t)blockIdx.y * (kBwdCols / VEC);
+  const int CT = min(units - cu0, kBwdCols / VEC);  // column units of this slice (>= 1)
+  const int RL = kBwdBlock / CT;                    // row lanes
+  const int rl = tid / CT, cu = tid % CT;
+  const bool act = rl < RL;
+  const int64_t c = (int64_t)(cu0 + cu) * VEC;
+  const int32_t r0 = (int32_t)blockIdx.x * a.rpb;
+  const int32_t nr = min(a.M - r0, a.rpb);
+  const bool with_g = a.G != nullptr && blockIdx.y == 0;
+
+  // gS2 (and G) rows of the workgroup -> LDS, padded to PM columns with zeros
+  for (int i = tid; i < nr * PM; i += kBwdBlock) {
+    const int rr = i / PM, p = i % PM;
+    s_g[i] = p < a.P ? a.gS[(int64_t)(r0 + rr) * a.ldgs + p] : 0.f;
+    if (with_g) s_gg[i] = p < a.P ? a.G[(int64_t)(r0 + rr) * a.ldg + p] : 0.f;
+  }
+  // this lane's columns of W2 (rows of W2: W2[n, :])
+  float w[VEC][PM];
+#pragma unroll
+  for (int v = 0; v < VEC; ++v)
+#pragma unroll
+    for (int p = 0; p < PM; ++p)
+      w[v][p] = (act && c + v < a.N && p < a.P) ? a.W[(c + v) * a.ldw + p] : 0.f;
+  float gw[VEC][PM], gb[VEC];
+#pragma unroll
+  for (int v = 0; v < VEC; ++v) {
+    gb[v] = 0.f;
+#pragma unroll
+    for (int p = 0; p < PM; ++p) gw[v][p] = 0.f;
+  }
+  const bool colok = act && c < a.N;  // VEC columns all valid (N % VEC == 0 on the vector paths)
+  __syncthreads();
+
+  for (int32_t b0 = rl; b0 < nr; b0 += RL * kBwdBatch) {
+    // the batch's H1 loads first (one latency), then the rows in order
+    float h[kBwdBatch][VEC];
+#pragma unroll
+    for (int j = 0; j < kBwdBatch; ++j) {
+      const int32_t rr = b0 + j * RL;
+      if (colok && rr < nr) VecIO<VEC>::load(a.H + (int64_t)(r0 + rr) * a.ldh + c, h[j]);
+      else
+#pragma unroll
+        for (int v = 0; v < VEC; ++v) h[j][v] = 0.f;
+    }
+#pragma unroll
+    for (int j = 0; j < kBwdBatch; ++j) {
+      const int32_t rr = b0 + j * RL;
+      if (!colok || rr >= nr) break;
+      float g[PM];
+#pragma unroll
+      for (int p = 0; p < PM; p += 4) {
+        const float4 q = *reinterpret_cast<const float4*>(s_g + rr * PM + p);
+        g[p] = q.x; g[p + 1] = q.y; g[p + 2] = q.z; g[p + 3] = q.w;
+      }
+      float z[VEC];
+#pragma unroll
+      for (int v = 0; v < VEC; ++v) {
+        float dot = 0.f;
+#pragma unroll
+        for (int p = 0; p < PM; ++p) dot = fmaf(g[p], w[v][p], dot);
+        z[v] = h[j][v] > 0.f ? dot * a.scale : 0.f;
+        gb[v] += z[v];
+#pragma unroll
+        for (int p = 0; p < PM; ++p) gw[v][p] = fmaf(h[j][v], g[p], gw[v][p]);
+      }
+      VecIO<VEC>::store(a.Z + (int64_t)(r0 + rr) * a.ldz + c, z);
+    }
+  }
+
+  // row lanes -> one partial per column, summed in lane order
+  {
+    float* mine = s_red + tid * KE;
+#pragma unroll
+    for (int v = 0; v < VEC; ++v) {
+#pragma unroll
+      for (int p = 0; p < PM; ++p) mine[v * (PM + 1) + p] = gw[v][p];
+      mine[v * (PM + 1) + PM] = gb[v];
+    }
+  }
+  __syncthreads();
+  float* prow = a.part + (int64_t)blockIdx.x * a.part_ld;
+  for (int e = tid; e < CT * KE; e += kBwdBlock) {
+    const int u = e / KE, k = e % KE;
+    const int v = k / (PM + 1), p = k % (PM + 1);
+    const int64_t col = (int64_t)(cu0 + u) * VEC + v;
+    float s = 0.f;
+    for (int l = 0; l < RL; ++l) s += s_red[(l * CT + u) * KE + k];
+    if (col >= a.N) continue;
+    if (p < PM) {
+      if (p < a.P) prow[col * a.P + p] = s;
+    } else {
+      prow[(int64_t)a.N * a.P + col] = s;
+    }
+  }
+  if (with_g && tid < a.P) {  // gb2: the G rows, in row order
+    float s = 0.f;
+    for (int rr = 0; rr < nr; ++rr) s += s_gg[rr * PM + tid];
+    prow[(int64_t)a.N * a.P + a.N + tid] = s;
+  }
+}
+
+// out[e] = sum over workgroups of part[b][e], b in order: 16 entries x 16
+// workgroup lanes per block, each lane summing workgroups l, l + 16, ... (16
+// loads in flight), then the 16 lanes in order through LDS.
+__global__ void __launch_bounds__(256) gcn_bwd2_reduce_kernel(const float* __restrict__ part, int64_t part_ld,
+                                                              int32_t nblk, int32_t N, int32_t P, int32_t with_g,
+                                                              float* __restrict__ gW, float* __restrict__ gb1,
+                                                              float* __restrict__ gb2) {
+  __shared__ float s[16][17];
+  const int el = threadIdx.x & 15, bl = threadIdx.x >> 4;
+  const int64_t E = (int64_t)N * P + N + (with_g ? P : 0);
+  const int64_t e = (int64_t)blockIdx.x * 16 + el;
+  float acc = 0.f;
+  if (e < E) {
+    for (int32_t b0 = bl; b0 < nblk; b0 += 16 * 16) {
+      float v[16];
+#pragma unroll
+      for (int j = 0; j < 16; ++j) v[j] = b0 + 16 * j < nblk ? part[(int64_t)(b0 + 16 * j) * part_ld + e] : 0.f;
+#pragma unroll
+      for (int j = 0; j < 16; ++j)
+        if (b0 + 16 * j < nblk) acc += v[j];
+    }
+  }
+  s[bl][el] = acc;
+  __syncthreads();
+  if (bl != 0 || e >= E) return;
+  float t = s[0][el];
+  for (int q = 1; q < 16; ++q) t += s[q][el];
+  const int64_t NP = (int64_t)N * P;
+  if (e < NP) {
+    if (gW) gW[e] = t;
+  } else if (e < NP + N) {
+    if (gb1) gb1[e - NP] = t;
+  } else if (gb2) {
+    gb2[e - NP - N] = t;
+  }
+}
+
+struct Bwd2Geom {
+  int vec, pm, slices, nblk, rpb;
+  int64_t part_ld;
+};
+
+bool bwd2_geometry(int32_t M, int32_t N, int32_t P, bool vec4_ok, bool vec2_ok, Bwd2Geom& g) {
+  if (P < 1 || P > 32 || N < 1 || M < 1) return false;
+  g.pm = P <= 8 ? 8 : P <= 16 ? 16 : 32;
+  g.vec = (g.pm <= 16 && vec4_ok) ? 4 : vec2_ok ? 2 : 1;
+  const int units = (N + g.vec - 1) / g.vec;
+  g.slices = (units + kBwdCols / g.vec - 1) / (kBwdCols / g.vec);
+  g.rpb = (int)std::min<int64_t>(kBwdRowsMax, std::max<int64_t>(1, ((int64_t)M + kBwdTarget - 1) / kBwdTarget));
+  g.nblk = (int)(((int64_t)M + g.rpb - 1) / g.rpb);
+  g.part_ld = (((int64_t)N * P + N + P) + 3) & ~3LL;
+  return true;
+}
+
+}  // namespace
+}  // namespace gcnk
+
+using namespace gcnk;
+
+extern "C" int64_t gcnk_gcn_bwd2_workspace_bytes(int32_t M, int32_t N, int32_t P) {
+  Bwd2Geom g;
+  if (!bwd2_geometry(M, N, P, true, true, g)) return 0;
+  return (int64_t)g.nblk * g.part_ld * 4;
+}
+
+extern "C" int gcnk_gcn_bwd2_f32(const float* H, int64_t ldh, const float* gS, int64_t ldgs, const float* W,
+                                 int64_t ldw, const float* G, int64_t ldg, int32_t M, int32_t N, int32_t P,
+                                 float scale, float* Z, int64_t ldz, float* gW, float* gb1, float* gb2,
+                                 void* workspace, int64_t workspace_bytes, void* stream) {
+  if (M < 0 || N < 0 || P < 0) {
+    set_error("gcnk_gcn_bwd2_f32: negative size (M=%d N=%d P=%d)", M, N, P);
+    return GCNK_EARG;
+  }
+  if (P > 32) {
+    set_error("gcnk_gcn_bwd2_f32: P = %d classes > 32 (use gcnk_gemm_f32 + gcnk_colsum_f32)", P);
+    return GCNK_EUNSUP;
+  }
+  if (M == 0 || N == 0 || P == 0) {
+    set_error("gcnk_gcn_bwd2_f32: empty operand (M=%d N=%d P=%d)", M, N, P);
+    return GCNK_EUNSUP;
+  }
+  if (!H || !gS || !W || !Z || (G && ldg < P) || ldh < N || ldgs < P || ldw < P || ldz < N) {
+    set_error("gcnk_gcn_bwd2_f32: null operand or leading dimension too small");
+    return GCNK_EARG;
+  }
+  const bool v4 = N % 4 == 0 && ldh % 4 == 0 && ldz % 4 == 0 && aligned16(H) && aligned16(Z);
+  const bool v2 = N % 2 == 0 && ldh % 2 == 0 && ldz % 2 == 0 && ((uintptr_t)H & 7u) == 0 && ((uintptr_t)Z & 7u) == 0;
+  Bwd2Geom g;
+  bwd2_geometry(M, N, P, v4, v2, g);
+  const int64_t need = (int64_t)g.nblk * g.part_ld * 4;
+  if (!workspace || workspace_bytes < need) {
+    set_error("gcnk_gcn_bwd2_f32: workspace %lld B < %lld B", (long long)workspace_bytes, (long long)need);
+    return GCNK_EARG;
+  }
+  Bwd2Args a{H, ldh, gS, ldgs, W, ldw, G, ldg, M, N, P, scale, Z, ldz, (float*)workspace, g.part_ld, g.rpb};
+  hipStream_t s = (hipStream_t)stream;
+  const dim3 grid((unsigned)g.nblk, (unsigned)g.slices);
+#define GCNK_BWD2(V_, PM_) hipLaunchKernelGGL((gcn_bwd2_kernel<V_, PM_>), grid, dim3(kBwdBlock), 0, s, a)
+  if (g.vec == 4) {
+    if (g.pm == 8) GCNK_BWD2(4, 8);
+    else GCNK_BWD2(4, 16);
+  } else if (g.vec == 2) {
+    if (g.pm == 8) GCNK_BWD2(2, 8);
+    else if (g.pm == 16) GCNK_BWD2(2, 16);
+    else GCNK_BWD2(2, 32);
+  } else {
+    if (g.pm == 8) GCNK_BWD2(1, 8);
+    else if (g.pm == 16) GCNK_BWD2(1, 16);
+    else GCNK_BWD2(1, 32);
+  }
+#undef GCNK_BWD2
+  int rc = launch_check("gcn_bwd2_kernel");
+  if (rc) return rc;
+  const int64_t E = (int64_t)N * P + N + (G ? P : 0);
+  hipLaunchKernelGGL(gcn_bwd2_reduce_kernel, dim3((unsigned)((E + 15) / 16)), dim3(256), 0, s,
+                     (const float*)workspace, g.part_ld, g.nblk, N, P, G ? 1 : 0, gW, gb1, gb2);
+  return launch_check("gcn_bwd2_reduce_kernel");
+}

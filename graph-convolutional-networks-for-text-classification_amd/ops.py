@@ -133,6 +133,8 @@ def _side_stream(device):
 # fused vs 58 us unfused, profiles/r02_variants.log).
 FUSE_PROJECTION = os.environ.get("GCNK_FUSE_PROJECTION", "1") != "0"
 FUSE_MAX_P = 8
+# gc2's backward + gc1's ReLU/dropout backward in one pass over H1 (gcn_bwd2)
+FUSE_BACKWARD = os.environ.get("GCNK_FUSE_BACKWARD", "1") != "0"
 
 
 def spmm_proj(a, B, W, bias=None, epilogue=_lib.EPI_NONE, mask=None, scale=1.0, keep_prob=1.0, seed=0, offset=0,
@@ -297,6 +299,47 @@ def colsum(X):
     return out
 
 
+def gcn_bwd2(H1, gS2, W2, G=None, scale=1.0, want_gw=True, want_gb1=True):
+    """The fused backward of gc2 and of gc1's ReLU + dropout (gcnk_gcn_bwd2_f32):
+    returns (gZ1, gW2, gb1, gb2) with
+
+        gZ1 = (H1 > 0) ? scale * (gS2 @ W2^T) : 0      (mm + dropout noise + threshold_backward)
+        gW2 = H1^T @ gS2,  gb1 = colsum(gZ1),  gb2 = colsum(G) (None without G)
+
+    (autograd of reference layer.py:182-188 through layer.py:102-110).  None
+    when the shape is outside the fused kernel (more than 32 classes): the
+    caller takes the gemm + colsum route."""
+    H1 = _dense_f32(H1, "H1")
+    gS2 = _dense_f32(gS2, "gS2")
+    W2 = _dense_f32(W2, "W2")
+    M, N = H1.shape
+    P = W2.shape[1]
+    if P > 32 or M == 0 or N == 0 or P == 0:
+        return None
+    if gS2.shape != (M, P) or W2.shape[0] != N:
+        raise RuntimeError(f"gcn_bwd2 shape mismatch: H1 {tuple(H1.shape)}, gS2 {tuple(gS2.shape)}, "
+                           f"W2 {tuple(W2.shape)}")
+    if G is not None:
+        G = _dense_f32(G, "G")
+        if G.shape != (M, P):
+            raise RuntimeError(f"gcn_bwd2 shape mismatch: G {tuple(G.shape)} vs {(M, P)}")
+    dev = H1.device
+    gZ1 = torch.empty((M, N), dtype=torch.float32, device=dev)
+    gW2 = torch.empty((N, P), dtype=torch.float32, device=dev) if want_gw else None
+    gb1 = torch.empty(N, dtype=torch.float32, device=dev) if want_gb1 else None
+    gb2 = torch.empty(P, dtype=torch.float32, device=dev) if G is not None else None
+    lib = _lib.load()
+    wsb = lib.gcnk_gcn_bwd2_workspace_bytes(M, N, P)
+    ws = torch.empty((wsb + 3) // 4, dtype=torch.float32, device=dev)
+    with torch.cuda.device(dev):
+        rc = lib.gcnk_gcn_bwd2_f32(_ptr(H1), H1.stride(0), _ptr(gS2), gS2.stride(0), _ptr(W2), W2.stride(0),
+                                   _ptr(G), G.stride(0) if G is not None else 0, M, N, P, float(scale),
+                                   _ptr(gZ1), gZ1.stride(0), _ptr(gW2), _ptr(gb1), _ptr(gb2), _ptr(ws), wsb,
+                                   _stream(dev))
+    _lib.check(rc, "gcnk_gcn_bwd2_f32")
+    return gZ1, gW2, gb1, gb2
+
+
 # ----------------------------------------------------------------------------------------
 # Operand for the first product of a layer: sparse (CSR) or dense infeatn.
 
@@ -396,10 +439,13 @@ class GCNFn(torch.autograd.Function):
         Z  = A S2 + b2              spmm (spmm_sum of the partials) + bias layer.py:106,110 (gc2)
 
     Backward (trainer.py:361):
-        gb2 = colsum(g);  gS2 = A^T g;  gW2 = H1^T gS2 (split-K);
-        gZ1 = (H1 > 0) ? (gS2 W2^T) * scale : 0   (gemm + MASK_POS epilogue; == ATen's
-              mul-by-noise then threshold_backward because H1 > 0 <=> kept and Z1 > 0)
-        gb1 = colsum(gZ1);  gS1 = A^T gZ1;  gW1 = X^T gS1.
+        gS2 = A^T g;
+        gZ1 = (H1 > 0) ? (gS2 W2^T) * scale : 0   (== ATen's mul-by-noise then
+              threshold_backward because H1 > 0 <=> kept and Z1 > 0),
+        gW2 = H1^T gS2,  gb1 = colsum(gZ1),  gb2 = colsum(g)
+              -- all four in one pass over H1 (gcn_bwd2; P > 32 classes: gemm
+              with the MASK_POS epilogue, split-K gemm, colsum);
+        gS1 = A^T gZ1;  gW1 = X^T gS1.
     """
 
     @staticmethod
@@ -425,16 +471,22 @@ class GCNFn(torch.autograd.Function):
         need = ctx.needs_input_grad
         gW1 = gb1 = gW2 = gb2 = None
         adjT = ctx.adj.t()
-        if ctx.has_b2 and need[3]:
-            gb2 = colsum(g)
         gS2 = spmm(adjT, g)
-        if need[2]:
-            gW2 = gemm(H1, gS2, transA=True)
-        if need[0] or need[1]:
-            gZ1 = gemm(gS2, W2, transB=True, epilogue=_lib.GEMM_EPI_MASK_POS, R=H1, scale=ctx.scale)
-            if ctx.has_b1 and need[1]:
-                gb1 = colsum(gZ1)
-            if need[0]:
-                gS1 = spmm(adjT, gZ1)
-                gW1 = ctx.xop.t_times(gS1)
+        fused = gcn_bwd2(H1, gS2, W2, G=g if ctx.has_b2 and need[3] else None, scale=ctx.scale,
+                         want_gw=need[2], want_gb1=ctx.has_b1 and need[1]) if FUSE_BACKWARD else None
+        if fused is not None:
+            gZ1, gW2, gb1, gb2 = fused
+        else:
+            if ctx.has_b2 and need[3]:
+                gb2 = colsum(g)
+            if need[2]:
+                gW2 = gemm(H1, gS2, transA=True)
+            gZ1 = None
+            if need[0] or need[1]:
+                gZ1 = gemm(gS2, W2, transB=True, epilogue=_lib.GEMM_EPI_MASK_POS, R=H1, scale=ctx.scale)
+                if ctx.has_b1 and need[1]:
+                    gb1 = colsum(gZ1)
+        if need[0]:
+            gS1 = spmm(adjT, gZ1)
+            gW1 = ctx.xop.t_times(gS1)
         return gW1, gb1, gW2, gb2, None, None, None, None, None, None, None, None, None, None

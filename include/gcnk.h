@@ -50,7 +50,7 @@
 extern "C" {
 #endif
 
-#define GCNK_ABI_VERSION 3
+#define GCNK_ABI_VERSION 4
 
 #define GCNK_OK 0
 #define GCNK_EARG (-1)
@@ -285,6 +285,26 @@ int gcnk_gemm_f32(int32_t transA, int32_t transB, int32_t M, int32_t N, int32_t 
 int64_t gcnk_colsum_workspace_bytes(int32_t M, int32_t N);
 int gcnk_colsum_f32(const float* X, int64_t ldx, int32_t M, int32_t N, float* out,
                     float* workspace, int64_t workspace_bytes, void* stream);
+
+/* ---------------------------------------------------------------------------
+ * Fused backward of gc2 and of gc1's ReLU + dropout (autograd of
+ * layer.py:182-188 through layer.py:102-110; replaces gcnk_gemm_f32 with
+ * GCNK_GEMM_EPI_MASK_POS for gZ1, the split-K gcnk_gemm_f32 for gW2 and two
+ * gcnk_colsum_f32 calls):
+ *   gZ1[m, n] = H[m, n] > 0 ? scale * (gS[m, :] . W[n, :]) : 0     [M x N, ldz]
+ *   gW[n, p]  = sum_m H[m, n] gS[m, p]                             [N x P, contiguous]
+ *   gb1[n]    = sum_m gZ1[m, n]                                    [N]
+ *   gb2[p]    = sum_m G[m, p]                 (G nullable)         [P]
+ * H = gc1's output after ReLU + dropout [M x N], gS = A^T G [M x P], W = W2
+ * [N x P].  gW / gb1 / gb2 are nullable (not stored).  P <= 32 (else
+ * GCNK_EUNSUP).  Two launches; sums in a fixed order (bitwise reproducible).
+ * Workspace: gcnk_gcn_bwd2_workspace_bytes(M, N, P).
+ * ------------------------------------------------------------------------- */
+int64_t gcnk_gcn_bwd2_workspace_bytes(int32_t M, int32_t N, int32_t P);
+int gcnk_gcn_bwd2_f32(const float* H, int64_t ldh, const float* gS, int64_t ldgs, const float* W, int64_t ldw,
+                      const float* G, int64_t ldg, int32_t M, int32_t N, int32_t P, float scale,
+                      float* gZ1, int64_t ldz, float* gW, float* gb1, float* gb2,
+                      void* workspace, int64_t workspace_bytes, void* stream);
 
 /* ---------------------------------------------------------------------------
  * Sparse-format helpers (one-time graph preparation, utils.py:185-213,

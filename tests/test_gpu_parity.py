@@ -581,6 +581,38 @@ def test_gemm_epilogues_and_split_k():
            np.where(R2.numpy() > 0, 2 * ref2, 0.0), atol=1e-4)
 
 
+@pytest.mark.parametrize("M,N,P,ldpad", [(7724, 200, 8, 0), (18916, 200, 20, 0), (1000, 7, 3, 0),
+                                          (3001, 300, 16, 4), (50, 1030, 5, 2), (70000, 64, 8, 0)])
+def test_gcn_bwd2_fused_backward(M, N, P, ldpad):
+    """gcnk_gcn_bwd2_f32 (gc2 + ReLU/dropout backward in one pass over H1)
+    against float64: gZ1 = (H1 > 0) ? scale * gS2 W2^T : 0, gW2 = H1^T gS2,
+    gb1 = colsum(gZ1), gb2 = colsum(G); float4 / float2 / scalar column paths,
+    several 256-column slices, strided H1, more rows than one LDS stage.
+    Bitwise identical on a second call."""
+    from graph_convolutional_networks_for_text_classification_amd.ops import gcn_bwd2
+    rng = np.random.default_rng(M + N + P)
+    Hf = rng.standard_normal((M, N + ldpad)).astype(np.float32)
+    Hf[rng.random((M, N + ldpad)) < 0.4] = 0.0          # dropped / non-positive entries
+    Hf = np.maximum(Hf, 0) * 2.0
+    gS = rng.standard_normal((M, P)).astype(np.float32)
+    W = rng.standard_normal((N, P)).astype(np.float32)
+    G = rng.standard_normal((M, P)).astype(np.float32)
+    Ht = torch.from_numpy(Hf).to(DEV)[:, :N]
+    args = [torch.from_numpy(x).to(DEV) for x in (gS, W, G)]
+    gZ, gW, gb1, gb2 = gcn_bwd2(Ht, args[0], args[1], G=args[2], scale=2.0)
+    H = Hf[:, :N].astype(np.float64)
+    zref = np.where(H > 0, 2.0 * (gS.astype(np.float64) @ W.astype(np.float64).T), 0.0)
+    _close(gZ, zref, atol=1e-4)
+    _close(gW, H.T @ gS.astype(np.float64), atol=2e-5 * np.sqrt(M) * 4)
+    _close(gb1, zref.sum(0), atol=2e-5 * np.sqrt(M) * 4)
+    _close(gb2, G.astype(np.float64).sum(0), atol=2e-5 * np.sqrt(M))
+    again = gcn_bwd2(Ht, args[0], args[1], G=args[2], scale=2.0)
+    assert all(torch.equal(x, y) for x, y in zip((gZ, gW, gb1, gb2), again))
+    z2, w2, b1, b2 = gcn_bwd2(Ht, args[0], args[1], scale=1.0, want_gw=False, want_gb1=False)
+    assert w2 is None and b1 is None and b2 is None
+    _close(z2, zref / 2.0, atol=1e-4)
+
+
 def test_colsum():
     X = torch.randn(7724, 200, generator=torch.Generator().manual_seed(2))
     _close(colsum(X.to(DEV)), csr_ref.colsum(X.numpy()), atol=1e-4)

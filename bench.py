@@ -218,7 +218,8 @@ def rocprof_kernel_us(mode, kernels_like, save_dir=None, variant="row"):
                     found = True
             if save_dir:
                 os.makedirs(save_dir, exist_ok=True)
-                shutil.copy(f, os.path.join(save_dir, f"bench_rocprof_as1_{mode}_kernel_stats.csv"))
+                tag = mode if variant != "copy" else "copyfloor"
+                shutil.copy(f, os.path.join(save_dir, f"bench_rocprof_as1_{tag}_kernel_stats.csv"))
         if not found:
             return None, f"no kernel rows for {kernels_like}"
         return total, f"rocprofv3 --kernel-trace --stats, scripts/hub_probe.py --mode {mode}"
@@ -464,6 +465,9 @@ def main():
         for mode in ("warm", "cold"):
             kt[mode] = rocprof_kernel_us(mode, ["hub_group_kernel", "spmm_row_kernel"], args.rocprof_dir,
                                          plan_kinds[north])
+        # the streaming floor at this size: one elementwise pass over the same B / C
+        # rotation (reads B once, writes C once) under the same rocprofv3 timing
+        kt["copy"] = rocprof_kernel_us("cold", ["elementwise"], args.rocprof_dir, "copy")
 
     # ---- the product forward's own kernels (rocprofv3 trace of the graph replay),
     #      each against its algorithmic bytes; the fused north-star kernel among them
@@ -668,7 +672,11 @@ def main():
         # per-call HIP-event figure above includes
         "roofline_rocprof": {m: ({"kernel_us": round(v[0], 3),
                                   "frac": kn["algorithmic_bytes"] / (v[0] * 1e-6) / 1e9 / HBM_PEAK_GBS,
-                                  "source": v[1]} if v[0] is not None else {"error": v[1]})
+                                  "source": v[1],
+                                  **({"note": "streaming floor: one elementwise pass C = B * 1 over the same cold "
+                                              "B / C rotation (no CSR, no gathers); frac = the op's bytes at that "
+                                              "duration, the ceiling of any single kernel at this size"}
+                                     if m == "copy" else {})} if v[0] is not None else {"error": v[1]})
                              for m, v in kt.items()},
         "roofline_dominant": {"kernel": dom, "frac": kd["frac_cold"], "frac_warm": kd["frac_warm"],
                               "avg_launch_us": kd["cold_us"], "algorithmic_bytes": kd["algorithmic_bytes"]},

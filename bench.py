@@ -229,6 +229,14 @@ def rocprof_kernel_us(mode, kernels_like, save_dir=None, variant="row"):
         shutil.rmtree(tmp, ignore_errors=True)
 
 
+def _factored(a_csr, x):
+    """The HubFactor the product forward uses for (A-hat, X), or None (SpMM path)."""
+    from graph_convolutional_networks_for_text_classification_amd import factor, ops
+    if not ops.FACTOR_GC1:
+        return None
+    return factor.get(a_csr, ops.Operand(x))
+
+
 def forward_kernels(save_dir=None):
     """Per-kernel durations of the product forward (hipGraph replay) from a child
     rocprofv3 --kernel-trace run of scripts/fwd_trace.py, in launch order."""
@@ -484,14 +492,25 @@ def main():
                 "A S1": 4 * (N + 1) + 8 * nnz_a + 4 * N * nhid + 4 * nsl * N * nclass + 4 * nhid * nclass,
                 "A sum S2": 4 * (N + 1) + 8 * nnz_a + 4 * nsl * N * nclass + 4 * N * nclass,
             }
+            fac = _factored(a_csr, x)
+            if fac is not None:
+                # hub-factored gc1 (factor.py): X[hubs] W1 on the tile GEMM, then one launch
+                # reading U [N x Kc], the A_H records, W1[Kc], S_T, W2 and writing S2
+                x_hub_nnz = fac.x_hub.nnz if fac.x_hub is not None else fac.H * nfeat
+                alg = {"X_hubs W1": spmm_bytes(fac.H, nfeat, x_hub_nnz, nhid),
+                       "A X W1 factored + H1 W2": (4 * fac.U.numel() + 4 * fac.rec.numel() + 4 * fac.Kc * nhid
+                                                    + 4 * fac.H * nhid + 4 * nhid * nclass + 4 * N * nclass),
+                       "A sum S2": alg["A sum S2"]}
             ks, na = [], 0
             for k in trace["kernels"]:   # the A-hat launches are the row / hub kernels, X W1 the rest
                 name = k["kernel"]
-                if "spmm_row_kernel" in name or "hub_group_kernel" in name:
-                    key = "A S1" if na == 0 else "A sum S2"
+                if "hubfactor" in name:
+                    key = "A X W1 factored + H1 W2"
+                elif "spmm_row_kernel" in name or "hub_group_kernel" in name:
+                    key = "A S1" if na == 0 and fac is None else "A sum S2"
                     na += 1
                 else:
-                    key = "X W1"
+                    key = "X W1" if fac is None else "X_hubs W1"
                 ks.append({"kernel": name[:120], "us": k["us"], "op": key})
             for key, nb in alg.items():   # per op: its launches' summed duration against its bytes
                 us = sum(e["us"] for e in ks if e["op"] == key)

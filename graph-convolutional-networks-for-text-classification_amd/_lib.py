@@ -31,7 +31,7 @@ def _resolve_lib():
 
 
 LIB_PATH = _resolve_lib()
-ABI_VERSION = 4
+ABI_VERSION = 5
 
 # C-ABI return codes (gcnk.h)
 OK, EARG, EUNSUP, EHIP = 0, -1, -2, -3
@@ -136,6 +136,16 @@ SIGNATURES = {
         _vp, _i64, _i32, _i32, _i32, _f32,  # G, ldg, M, N, P, scale
         _vp, _i64, _vp, _vp, _vp,          # gZ1, ldz, gW, gb1, gb2
         _vp, _i64, _vp]),                  # workspace, bytes, stream
+    "gcnk_hubfactor_lds_bytes": (_i64, [_i32, _i32, _i32, _i32]),
+    "gcnk_hubfactor_gc1_f32": (ctypes.c_int, [
+        _i32, _i32, _i32, _i32, _i32,     # M, F, Kc, nhub, P
+        _vp, _i64, _vp, _i64, _i32,       # U, ldu, W, ldw, k0
+        _vp, _i64, _vp, _i32,             # S, lds, rec, rec_words
+        _vp, _i32,                        # bias, epilogue
+        _vp, _i64, _f32,                  # drop_mask, ldm, drop_scale
+        _f32, _u64, _u64, _vp,            # keep_prob, seed, offset, rng_base
+        _vp, _i64, _vp, _i64, _vp, _i64,  # W2, ldw2, H, ldh, C2, ldc2
+        _vp]),                            # stream
     "gcnk_class_stats": (ctypes.c_int, [_vp, _i64, _vp, _vp, _i64, _i32, _vp, _vp]),
     "gcnk_edgelist_size": (ctypes.c_int, [ctypes.c_char_p, _vp, _vp]),
     "gcnk_edgelist_csr": (ctypes.c_int, [ctypes.c_char_p, _i64, _i64, _vp, _vp, _vp]),

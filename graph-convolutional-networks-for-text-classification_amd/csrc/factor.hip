@@ -1,0 +1,314 @@
+// Hub-factored first GCN layer for gfx950: gc1 of the reference's doc-topic
+// graph without the topic rows' gather-and-combine.
+//
+// Reference (layer.py:102,106,110,182,185 inside GCN.forward, layer.py:164-190):
+//   H1 = dropout(relu(A-hat (X W1) + b1)),   S2 = H1 W2   (gc2's support, layer.py:102)
+//
+// Structure used (checked on the host, factor.py): the rows of A-hat split into
+// a few hub rows (R8: the 50 topics) and light rows (the 7,674 documents) whose
+// nonzeros are hub columns plus their own diagonal, and X's light rows are
+// supported on a small contiguous column range Kc (R8: the 50 topic-weight
+// columns).  Then, with S_T = X_hubs W1 (the hub rows of X W1, computed by the
+// tile GEMM beforehand),
+//   light row d:  (A X W1)[d] = (A_dd X[d, Kc]) W1[Kc] + sum_t A[d, t] S_T[t]
+//   hub row t:    (A X W1)[t] = (sum_d A[t, d] X[d, Kc]) W1[Kc] + sum_t' A[t, t'] S_T[t']
+// i.e. Z = U W1[Kc] + A_H S_T with U [M x Kc] dense and A_H [M x hubs] sparse,
+// both fixed by (A-hat, X) and built once (factor.py).  The topic rows' sums over
+// ~600 document rows each -- the north-star SpMM's long pole -- move into U's
+// hub rows (the (A X) W association; fp32 rounding differs from A (X W) by
+// ~1e-6 relative), and the document rows never read or write their S1 rows.
+//
+// One workgroup = 32 rows (256 threads, 4 waves: 2 row strips x 2 halves of the
+// F columns):
+//   0. every operand of the block in one round of loads: W1[Kc] and S_T into LDS,
+//      the block's U fragments into registers, its A_H record and W2 into LDS;
+//   1. Z_strip = U_strip W1[Kc] on v_mfma_f32_16x16x4_f32 (exact fp32 FMA chains);
+//   2. Z through LDS to row-major; + A_H S_T, + b1, ReLU, dropout (mask or hash,
+//      the row kernel's epilogue); H1 stored only when a backward needs it;
+//   3. S2 = H1 W2 on MFMA from the same LDS tile (K split over the two halves,
+//      summed in a fixed order).
+// No atomics, no hand-off between workgroups: bitwise reproducible.
+#include "gcnk_common.h"
+#include "combine.h"
+
+#include <algorithm>
+
+namespace gcnk {
+namespace {
+
+typedef float f32x4 __attribute__((ext_vector_type(4)));
+
+constexpr int kRB = 32;         // rows per workgroup
+constexpr int kThreads = 512;   // 8 waves: 2 row strips x 4 column quarters
+constexpr int kMaxKsteps = 32;  // Kc <= 128
+constexpr int kProjW = 16;      // projection width (one MFMA n-tile): P <= 16
+constexpr int kBPad = 64;       // zero floats after the staged W1[Kc] (tiles past F read them)
+// compile-time shapes (every MFMA unconditional, operands in fixed registers):
+// KS k-steps of U W1[Kc] (Kc <= 4 KS; U columns past Kc read as zero, W1 rows
+// past Kc staged as zero) and NTQ 16-column tiles per quarter of F (F <= 64 NTQ;
+// columns past F are computed from finite LDS words and never used)
+__host__ __device__ constexpr int pick_ks(int kc) { return kc <= 52 ? 13 : kc <= 100 ? 25 : 32; }
+__host__ __device__ constexpr int pick_ntq(int f) { return f <= 128 ? 2 : f <= 192 ? 3 : 4; }
+
+struct FactorArgs {
+  int32_t M, F, Kc, nhub, P;
+  const float* U; int64_t ldu;          // [M x >= Kc]
+  const float* W; int64_t ldw; int32_t k0;  // W1 rows k0 .. k0 + Kc - 1 (ldw == F: staged flat)
+  const float* S; int64_t lds;          // [nhub x F]
+  const int32_t* rec; int32_t rec_words;  // per 32-row block: off[33] | pad | items int2 {hub, val}
+  const float* W2; int64_t ldw2;        // [F x P]
+  float* H; int64_t ldh;                // nullable
+  float* C2; int64_t ldc2;              // [M x P]
+  Epi epi;
+};
+
+template <int KS>
+__host__ __device__ constexpr int region1_floats(int F, int ntq) {
+  return (4 * KS * F + kBPad) > kRB * (64 * ntq + 4) ? (4 * KS * F + kBPad) : kRB * (64 * ntq + 4);
+}
+
+template <int KS, int NTQ>
+__global__ void __launch_bounds__(kThreads)
+hubfactor_gc1_kernel(FactorArgs a) {
+  extern __shared__ __attribute__((aligned(16))) float smem[];
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int wv = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int strip = wv & 1, quarter = wv >> 1;
+  const int F = a.F, Q = F / 4;
+  constexpr int Fp = 64 * NTQ, Fz = Fp + 4;  // s_Z row stride: 16-B rows, conflict-free MFMA-layout accesses
+  constexpr int Kr = 4 * KS;
+  const int64_t m0 = (int64_t)blockIdx.x * kRB;
+  // LDS: region1 = s_B [Kr][F] + kBPad zeros (phase 1), then s_Z [kRB][Fz]
+  //      | s_S [nhub][F] | s_W2 [F][P] | s_bias [F] | s_rec | s_red [3][2][64][4]
+  // Every global operand is staged here in the one round of loads that opens the
+  // kernel: a global load behind an LDS-read index costs a full memory round trip
+  // under load (~1-2 us each, measured), so nothing after the first wait touches
+  // global memory except the stores.
+  const int r1 = region1_floats<KS>(F, NTQ);
+  float* s_B = smem;
+  float* s_Z = smem;
+  float* s_S = smem + r1;
+  float* s_W2 = s_S + a.nhub * F;
+  float* s_bias = s_W2 + ((F * a.P + 3) & ~3);
+  int32_t* s_rec = reinterpret_cast<int32_t*>(s_bias + F);
+  float* s_red = reinterpret_cast<float*>(s_rec + a.rec_words);
+
+  // ---- 0. loads, all issued before the first wait: zeros first (no LDS-DMA in
+  //      flight yet), then LDS-DMA of W1[Kc] (flat) and the block's record, the
+  //      U fragments straight into registers
+  for (int e = a.Kc * F + tid; e < Kr * F + kBPad; e += kThreads) s_B[e] = 0.f;
+  if (!a.epi.bias)
+    for (int e = tid; e < F; e += kThreads) s_bias[e] = 0.f;
+  {
+    const int n4 = a.Kc * Q;  // float4 pieces of W1[k0 .. k0 + Kc) (rows of F floats, ldw == F)
+    const float* wsrc = a.W + (int64_t)a.k0 * a.ldw;
+    for (int e0 = wv * 64; e0 < n4; e0 += kThreads)
+      if (e0 + lane < n4) lds_dma16(wsrc + 4 * (e0 + lane), s_B + 4 * e0);
+    const int32_t* rec = a.rec + (int64_t)blockIdx.x * a.rec_words;
+    for (int e0 = wv * 64; e0 < a.rec_words / 4; e0 += kThreads)
+      if (e0 + lane < a.rec_words / 4) lds_dma16(rec + 4 * (e0 + lane), s_rec + 4 * e0);
+    const int s4 = a.nhub * Q;  // S_T [nhub x F] flat (lds == F)
+    for (int e0 = wv * 64; e0 < s4; e0 += kThreads)
+      if (e0 + lane < s4) lds_dma16(a.S + 4 * (e0 + lane), s_S + 4 * e0);
+    const int w1 = F * a.P;     // W2 [F x P] flat (ldw2 == P), dword pieces
+    for (int e0 = wv * 64; e0 < w1; e0 += kThreads)
+      if (e0 + lane < w1) lds_dma4(a.W2 + e0 + lane, s_W2 + e0);
+    if (a.epi.bias)
+      for (int e0 = wv * 64; e0 < Q; e0 += kThreads)
+        if (e0 + lane < Q) lds_dma16(a.epi.bias + 4 * (e0 + lane), s_bias + 4 * e0);
+  }
+  float af[KS];
+  {
+    const int64_t row = m0 + 16 * strip + (lane & 15);
+    const float* up = a.U + row * a.ldu + (lane >> 4);
+#pragma unroll
+    for (int s = 0; s < KS; ++s) af[s] = (row < a.M && 4 * s + (lane >> 4) < a.Kc) ? up[4 * s] : 0.f;
+  }
+  __builtin_amdgcn_s_waitcnt(0x0F70);  // vmcnt(0): this wave's DMA and fragment loads have landed
+  __syncthreads();
+  stamp(a.epi, 0);
+
+  // ---- 1. Z = U W1[Kc] for this wave's strip and column quarter
+  f32x4 acc[NTQ];
+#pragma unroll
+  for (int i = 0; i < NTQ; ++i) acc[i] = f32x4{0.f, 0.f, 0.f, 0.f};
+  const int c0 = quarter * NTQ * 16 + (lane & 15);
+#pragma unroll
+  for (int s = 0; s < KS; ++s) {
+    const float* br = s_B + (4 * s + (lane >> 4)) * F + c0;
+    float bf[NTQ];
+#pragma unroll
+    for (int i = 0; i < NTQ; ++i) bf[i] = br[i * 16];
+#pragma unroll
+    for (int i = 0; i < NTQ; ++i) acc[i] = __builtin_amdgcn_mfma_f32_16x16x4f32(af[s], bf[i], acc[i], 0, 0, 0);
+  }
+  __syncthreads();  // s_B is overwritten by s_Z below
+  stamp(a.epi, 1);
+  // C/D map of the 16x16 f32 MFMA: reg r -> row (lane >> 4) * 4 + r, col lane & 15
+#pragma unroll
+  for (int i = 0; i < NTQ; ++i)
+#pragma unroll
+    for (int r = 0; r < 4; ++r)
+      s_Z[(16 * strip + (lane >> 4) * 4 + r) * Fz + c0 - (lane & 15) + i * 16 + (lane & 15)] = acc[i][r];
+  __syncthreads();
+
+  // ---- 2. row-major epilogue, 16 threads per row, NTQ float4 columns each
+  //      (q = c16 + 16 u; slots past F computed from finite LDS words and
+  //      dropped): + A_H S_T, + b1, ReLU, dropout; H1 stored when a backward
+  //      needs it.  No bounds test inside the item loop, so each item's NTQ
+  //      LDS reads issue together.
+  {
+    const int r = tid >> 4, c16 = tid & 15;
+    const int64_t row = m0 + r;
+    float4 z[NTQ];
+#pragma unroll
+    for (int u = 0; u < NTQ; ++u) z[u] = *reinterpret_cast<const float4*>(s_Z + r * Fz + 4 * (c16 + 16 * u));
+    const int2* it = reinterpret_cast<const int2*>(s_rec + 36);
+    const int k1 = s_rec[r + 1];
+#pragma unroll 2
+    for (int k = s_rec[r]; k < k1; ++k) {
+      const int2 p = it[k];
+      const float v = __int_as_float(p.y);
+      const float* srow = s_S + p.x * F + 4 * c16;
+      float4 sv[NTQ];
+#pragma unroll
+      for (int u = 0; u < NTQ; ++u) sv[u] = *reinterpret_cast<const float4*>(srow + 64 * u);
+#pragma unroll
+      for (int u = 0; u < NTQ; ++u) Vec<4>::fma(z[u], v, sv[u]);
+    }
+    if (row < a.M) {
+      const bool plain = a.epi.code == GCNK_EPI_BIAS_RELU;  // eval / no-dropout: no per-element branches
+#pragma unroll
+      for (int u = 0; u < NTQ; ++u) {
+        const int q = c16 + 16 * u;
+        if (q < Q) {
+          const float4 bv = *reinterpret_cast<const float4*>(s_bias + 4 * q);
+          float4 h;
+          if (plain) {
+            h.x = fmaxf(z[u].x + bv.x, 0.f); h.y = fmaxf(z[u].y + bv.y, 0.f);
+            h.z = fmaxf(z[u].z + bv.z, 0.f); h.w = fmaxf(z[u].w + bv.w, 0.f);
+          } else {
+            h = Vec<4>::epi(a.epi, z[u], bv, row, 4 * (int64_t)q);
+          }
+          if (a.H) Vec<4>::store(a.H + row * a.ldh + 4 * q, h);
+          *reinterpret_cast<float4*>(s_Z + r * Fz + 4 * q) = h;
+        }
+      }
+    }
+  }
+  __syncthreads();
+  stamp(a.epi, 2);
+
+  // ---- 3. S2 = H1 W2 on MFMA: strip x quarter of the K = F sum each (W2's rows
+  //      past F and columns past P as zero), quarters added in order
+  f32x4 pc;
+  {
+    const int n = lane & 15;
+    constexpr int kq = Fp / 16;  // k-steps per quarter
+    float av[kq], bw[kq];
+#pragma unroll
+    for (int j = 0; j < kq; ++j) {
+      const int k = 4 * (quarter * kq + j) + (lane >> 4);
+      av[j] = s_Z[(16 * strip + (lane & 15)) * Fz + k];
+      bw[j] = (k < F && n < a.P) ? s_W2[k * a.P + n] : 0.f;
+    }
+    f32x4 p0 = f32x4{0.f, 0.f, 0.f, 0.f}, p1 = p0;
+#pragma unroll
+    for (int j = 0; j < kq; j += 2) {
+      p0 = __builtin_amdgcn_mfma_f32_16x16x4f32(av[j], bw[j], p0, 0, 0, 0);
+      p1 = __builtin_amdgcn_mfma_f32_16x16x4f32(av[j + 1], bw[j + 1], p1, 0, 0, 0);
+    }
+    pc = p0 + p1;
+  }
+  if (quarter > 0) *reinterpret_cast<f32x4*>(s_red + (((quarter - 1) * 2 + strip) * 64 + lane) * 4) = pc;
+  __syncthreads();
+  if (quarter == 0) {
+#pragma unroll
+    for (int qq = 0; qq < 3; ++qq) pc += *reinterpret_cast<const f32x4*>(s_red + ((qq * 2 + strip) * 64 + lane) * 4);
+    const int p = lane & 15;
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+      const int64_t row = m0 + 16 * strip + (lane >> 4) * 4 + r;
+      if (row < a.M && p < a.P) a.C2[row * a.ldc2 + p] = pc[r];
+    }
+  }
+  stamp(a.epi, 3);
+}
+
+}  // namespace
+}  // namespace gcnk
+
+using namespace gcnk;
+
+static int64_t hubfactor_lds_bytes(int32_t F, int32_t Kc, int32_t nhub, int32_t rec_words, int32_t P = kProjW) {
+  const int64_t Fz = 64 * pick_ntq(F) + 4, Kr = 4 * pick_ks(Kc);
+  const int64_t r1 = std::max<int64_t>(Kr * F + kBPad, (int64_t)kRB * Fz);
+  return 4 * (r1 + (int64_t)nhub * F + (((int64_t)F * P + 3) & ~3LL) + F + rec_words + 3 * 2 * 64 * 4);
+}
+
+extern "C" int64_t gcnk_hubfactor_lds_bytes(int32_t F, int32_t Kc, int32_t nhub, int32_t rec_words) {
+  if (F <= 0 || Kc <= 0 || nhub <= 0 || rec_words < 36) return GCNK_EARG;
+  return hubfactor_lds_bytes(F, Kc, nhub, rec_words);
+}
+
+extern "C" int gcnk_hubfactor_gc1_f32(int32_t M, int32_t F, int32_t Kc, int32_t nhub, int32_t P, const float* U,
+                                      int64_t ldu, const float* W, int64_t ldw, int32_t k0, const float* S,
+                                      int64_t lds, const int32_t* rec, int32_t rec_words, const float* bias,
+                                      int32_t epilogue, const uint8_t* drop_mask, int64_t ldm, float drop_scale,
+                                      float keep_prob, uint64_t seed, uint64_t offset, const uint64_t* rng_base,
+                                      const float* W2, int64_t ldw2, float* H, int64_t ldh, float* C2,
+                                      int64_t ldc2, void* stream) {
+  if (M <= 0 || F <= 0 || Kc <= 0 || nhub <= 0 || P <= 0 || !U || !W || !S || !rec || !W2 || !C2 || k0 < 0) {
+    set_error("gcnk_hubfactor_gc1_f32: bad sizes or null operand (M=%d F=%d Kc=%d hubs=%d P=%d)", M, F, Kc, nhub, P);
+    return GCNK_EARG;
+  }
+  if (ldu < Kc || ldw < F || lds < F || ldw2 < P || ldc2 < P || (H && ldh < F) || rec_words < 36) {
+    set_error("gcnk_hubfactor_gc1_f32: leading dimension too small");
+    return GCNK_EARG;
+  }
+  if (F % 4 || F > 256 || Kc > 4 * kMaxKsteps || P > kProjW || ldw != F || lds != F || ldw2 != P ||
+      !aligned16(W) || !aligned16(S) || (H && !aligned16(H)) || (H && ldh % 4) || (bias && !aligned16(bias))) {
+    set_error("gcnk_hubfactor_gc1_f32: unsupported shape (F=%d %% 4, F <= 256, Kc <= 128, P <= 16, 16-B rows)", F);
+    return GCNK_EUNSUP;
+  }
+  if (epilogue < GCNK_EPI_NONE || epilogue > GCNK_EPI_BIAS_RELU_HASH ||
+      (epilogue == GCNK_EPI_BIAS_RELU_DROP && (!drop_mask || ldm < F))) {
+    set_error("gcnk_hubfactor_gc1_f32: bad epilogue %d (dropout needs a mask with ldm >= F)", epilogue);
+    return GCNK_EARG;
+  }
+  const int64_t lds_b = hubfactor_lds_bytes(F, Kc, nhub, rec_words, P);
+  if (lds_b > 160 * 1024) {
+    set_error("gcnk_hubfactor_gc1_f32: %lld B of LDS per workgroup > 160 KiB (F=%d Kc=%d hubs=%d)",
+              (long long)lds_b, F, Kc, nhub);
+    return GCNK_EUNSUP;
+  }
+  FactorArgs a;
+  a.M = M; a.F = F; a.Kc = Kc; a.nhub = nhub; a.P = P;
+  a.U = U; a.ldu = ldu; a.W = W; a.ldw = ldw; a.k0 = k0;
+  a.S = S; a.lds = lds; a.rec = rec; a.rec_words = rec_words;
+  a.W2 = W2; a.ldw2 = ldw2; a.H = H; a.ldh = ldh; a.C2 = C2; a.ldc2 = ldc2;
+  Epi& e = a.epi;
+  e.bias = bias; e.mask = drop_mask; e.scale = drop_scale; e.keep_prob = keep_prob;
+  e.seed_lo = (uint32_t)seed; e.seed_hi = (uint32_t)(seed >> 32); e.offset = offset; e.rng_base = rng_base;
+  e.code = epilogue; e.stamps = debug_stamps();
+  e.ldm = epilogue == GCNK_EPI_BIAS_RELU_HASH ? (ldm > 0 ? ldm : F) : ldm;
+  const int64_t nblk = ((int64_t)M + kRB - 1) / kRB;
+  const int ks = pick_ks(Kc), ntq = pick_ntq(F);
+  auto go = [&](auto kern) {
+    static_cast<void>(0);
+    const hipError_t attr = hipFuncSetAttribute(reinterpret_cast<const void*>(kern),
+                                                hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
+    if (attr != hipSuccess) return hip_check(attr, "hubfactor_gc1_kernel LDS attribute");
+    hipLaunchKernelGGL(kern, dim3((unsigned)nblk), dim3(kThreads), (size_t)lds_b, reinterpret_cast<hipStream_t>(stream),
+                       a);
+    return launch_check("hubfactor_gc1_kernel");
+  };
+#define GCNK_FACTOR_CASE(KS_, NTQ_) \
+  if (ks == KS_ && ntq == NTQ_) return go(&hubfactor_gc1_kernel<KS_, NTQ_>);
+  GCNK_FACTOR_CASE(13, 2) GCNK_FACTOR_CASE(13, 3) GCNK_FACTOR_CASE(13, 4)
+  GCNK_FACTOR_CASE(25, 2) GCNK_FACTOR_CASE(25, 3) GCNK_FACTOR_CASE(25, 4)
+  GCNK_FACTOR_CASE(32, 2) GCNK_FACTOR_CASE(32, 3) GCNK_FACTOR_CASE(32, 4)
+#undef GCNK_FACTOR_CASE
+  set_error("gcnk_hubfactor_gc1_f32: no kernel for Kc=%d F=%d", Kc, F);
+  return GCNK_EUNSUP;
+}

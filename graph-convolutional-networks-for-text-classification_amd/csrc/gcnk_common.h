@@ -14,6 +14,9 @@ namespace gcnk {
 // Thread-local error text returned by gcnk_last_error().
 void set_error(const char* fmt, ...);
 
+// Debug timeline buffer (gcnk_debug_set_stamps; always null without -DGCNK_STAMPS).
+unsigned long long* debug_stamps();
+
 inline int hip_check(hipError_t e, const char* what) {
   if (e != hipSuccess) {
     set_error("%s: %s", what, hipGetErrorString(e));

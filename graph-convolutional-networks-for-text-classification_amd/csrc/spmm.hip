@@ -1670,6 +1670,8 @@ extern "C" int gcnk_debug_set_stamps(void* buf) {
   return GCNK_EUNSUP;
 }
 #endif
+unsigned long long* gcnk::debug_stamps() { return g_stamps; }
+
 
 // Lane groups per wavefront (64 / LPR): identifies the launch geometry a plan
 // is laid out for (heavy segments are shared by these groups, or by the 4

@@ -9,7 +9,7 @@ import os
 
 import torch
 
-from . import _lib
+from . import _lib, factor
 from .sparse import CSR, DENSE_THRESHOLD, as_csr, require_device
 
 _NULL = ctypes.c_void_p(0)
@@ -207,6 +207,53 @@ def spmm_proj(a, B, W, bias=None, epilogue=_lib.EPI_NONE, mask=None, scale=1.0, 
         return (H if store_main else None), gemm(H, W)
     _lib.check(rc, "gcnk_spmm_proj_f32")
     return H, C2
+
+
+# gc1 through the hub factorisation (factor.py, csrc/factor.hip) whenever the
+# (A-hat, X) pair has the doc-topic structure; GCNK_FACTOR_GC1=0 forces the
+# SpMM path (experiments, A/B timing).
+FACTOR_GC1 = os.environ.get("GCNK_FACTOR_GC1", "1") != "0"
+
+
+def hubfactor_gc1(f, W1, b1, W2, epilogue=_lib.EPI_BIAS_RELU, mask=None, scale=1.0, keep_prob=1.0, seed=0,
+                  offset=0, rng_base=None, store_h1=True):
+    """(H1, S2) of gc1 + gc2's support through the hub factorisation ``f``
+    (factor.HubFactor): S_T = X[hubs] W1 (layer.py:102, the tile GEMM), then
+    one launch of gcnk_hubfactor_gc1_f32 -- H1 = drop(relu(A-hat X W1 + b1))
+    (layer.py:106,110,182,185) and S2 = H1 W2 (layer.py:102, gc2).  Returns
+    None when the shapes are outside the kernel's range (the caller takes the
+    SpMM path)."""
+    W1 = _dense_f32(W1, "gc1 weight")
+    W2 = _dense_f32(W2, "gc2 weight")
+    _check_rng_base(rng_base, W1.device)
+    M, F, P = f.M, W1.shape[1], W2.shape[1]
+    if W1.stride(0) != F:
+        W1 = W1.contiguous()   # the kernel stages W1[k0:k0+Kc], S_T and W2 as flat copies
+    if W2.stride(0) != P:
+        W2 = W2.contiguous()
+    if W2.shape[0] != F or P > 16 or F % 4 or F > 256:
+        return None
+    lib = _lib.load()
+    if int(lib.gcnk_hubfactor_lds_bytes(F, f.Kc, f.H, f.rec_words)) > 160 * 1024:
+        return None
+    S = f.hub_times(W1).contiguous()
+    H1 = torch.empty((M, F), dtype=torch.float32, device=W1.device) if store_h1 else None
+    S2 = torch.empty((M, P), dtype=torch.float32, device=W1.device)
+    if b1 is not None:
+        b1 = b1.contiguous()
+    if mask is not None:
+        mask = mask.contiguous()
+    with torch.cuda.device(W1.device):
+        rc = lib.gcnk_hubfactor_gc1_f32(
+            M, F, f.Kc, f.H, P, _ptr(f.U), f.U.stride(0), _ptr(W1), W1.stride(0), f.k0, _ptr(S), S.stride(0),
+            _ptr(f.rec), f.rec_words, _ptr(b1), epilogue,
+            _ptr(mask), mask.stride(0) if mask is not None else 0, float(scale),
+            float(keep_prob), int(seed) & (2**64 - 1), int(offset) & (2**64 - 1), _ptr(rng_base),
+            _ptr(W2), W2.stride(0), _ptr(H1), F, _ptr(S2), P, _stream(W1.device))
+    if rc == _lib.EUNSUP:
+        return None
+    _lib.check(rc, "gcnk_hubfactor_gc1_f32")
+    return H1, S2
 
 
 def spmm_sum(a, Bs, bias=None, epilogue=_lib.EPI_NONE, out=None, lanes=0):
@@ -450,11 +497,19 @@ class GCNFn(torch.autograd.Function):
 
     @staticmethod
     def forward(ctx, W1, b1, W2, b2, xop, adj, epi, mask, scale, keep, seed, offset, keep_h1=True, rng_base=None):
-        S1 = xop.times(W1)
-        if FUSE_PROJECTION and W2.shape[1] <= FUSE_MAX_P:
+        fac = factor.get(adj, xop) if FACTOR_GC1 else None
+        res = None
+        if fac is not None:
+            res = hubfactor_gc1(fac, W1, b1, W2, epilogue=epi, mask=mask, scale=scale, keep_prob=keep, seed=seed,
+                                offset=offset, rng_base=rng_base, store_h1=keep_h1)
+        if res is not None:
+            H1, S2 = res
+        elif FUSE_PROJECTION and W2.shape[1] <= FUSE_MAX_P:
+            S1 = xop.times(W1)
             H1, S2 = spmm_proj(adj, S1, W2, bias=b1, epilogue=epi, mask=mask, scale=scale, keep_prob=keep,
                                seed=seed, offset=offset, store_main=keep_h1, rng_base=rng_base)
         else:
+            S1 = xop.times(W1)
             H1 = spmm(adj, S1, bias=b1, epilogue=epi, mask=mask, scale=scale, keep_prob=keep, seed=seed,
                       offset=offset, rng_base=rng_base)
             S2 = gemm(H1, W2)

@@ -50,7 +50,7 @@
 extern "C" {
 #endif
 
-#define GCNK_ABI_VERSION 4
+#define GCNK_ABI_VERSION 5
 
 #define GCNK_OK 0
 #define GCNK_EARG (-1)
@@ -305,6 +305,29 @@ int gcnk_gcn_bwd2_f32(const float* H, int64_t ldh, const float* gS, int64_t ldgs
                       const float* G, int64_t ldg, int32_t M, int32_t N, int32_t P, float scale,
                       float* gZ1, int64_t ldz, float* gW, float* gb1, float* gb2,
                       void* workspace, int64_t workspace_bytes, void* stream);
+
+/* ---------------------------------------------------------------------------
+ * Hub-factored gc1 (csrc/factor.hip; GCN.forward layer.py:164-190 through
+ * layer.py:102,106,110,182,185 and gc2's support layer.py:102) for a graph
+ * whose rows split into hub rows and light rows referencing only hub columns
+ * and themselves, with X's light rows inside the column range [k0, k0 + Kc):
+ *   Z[r, :]   = U[r, :Kc] . W[k0 .. k0+Kc-1, :] + sum_{items of r} val * S[hub, :]
+ *   H[r, n]   = epilogue(Z[r, n] + bias[n])            (GCNK_EPI_*, as the SpMM)
+ *   C2[r, p]  = sum_n H[r, n] W2[n, p]                 (P <= 16)
+ * U [M x Kc] (ldu >= Kc rounded up to 4, zero past Kc), S = X[hubs] W
+ * [nhub x F] (lds), rec = one record of rec_words int32 per 32-row block:
+ * 33 row offsets (block-relative item index), 3 pad words, then items int2
+ * {hub index, value bits}.  H nullable (not stored).  F % 4 == 0, F <= 256,
+ * Kc <= 128; GCNK_EUNSUP when the block's operands exceed 160 KiB of LDS
+ * (gcnk_hubfactor_lds_bytes).  One launch, fixed-order sums.
+ * ------------------------------------------------------------------------- */
+int64_t gcnk_hubfactor_lds_bytes(int32_t F, int32_t Kc, int32_t nhub, int32_t rec_words);
+int gcnk_hubfactor_gc1_f32(int32_t M, int32_t F, int32_t Kc, int32_t nhub, int32_t P, const float* U, int64_t ldu,
+                           const float* W, int64_t ldw, int32_t k0, const float* S, int64_t lds,
+                           const int32_t* rec, int32_t rec_words, const float* bias, int32_t epilogue,
+                           const uint8_t* drop_mask, int64_t ldm, float drop_scale, float keep_prob, uint64_t seed,
+                           uint64_t offset, const uint64_t* rng_base, const float* W2, int64_t ldw2, float* H,
+                           int64_t ldh, float* C2, int64_t ldc2, void* stream);
 
 /* ---------------------------------------------------------------------------
  * Sparse-format helpers (one-time graph preparation, utils.py:185-213,

@@ -1193,3 +1193,77 @@ def test_tile_path_repeat_streams_and_graph_replay_are_exact(r8, dense, monkeypa
         assert torch.equal(out, one)
     rp, ci, v = (t.cpu().numpy() for t in (x.rowptr, x.colind, x.val))
     _close(one, csr_ref.spmm_csr(rp, ci, v, W.cpu().numpy()), atol=1e-4)
+
+
+# ------------------------------------------------------------------------------ hub-factored gc1
+
+@pytest.mark.parametrize("mode", ["eval", "train_mask", "train_hash"])
+def test_factored_gc1_matches_spmm_path(r8, mode):
+    """GCN.forward through the hub factorisation (factor.py + gcnk_hubfactor_gc1_f32:
+    A-hat X W1 as U W1[Kc] + A_H (X_hubs W1)) against the SpMM path
+    (ops.FACTOR_GC1 = False: X W1 then A-hat S1, layer.py:102,106) on R8 with
+    the same weights and the same dropout masks: logits and every gradient
+    within fp32 reassociation error; H1 kept for the backward only when
+    needed; the factored launch bitwise reproducible."""
+    from graph_convolutional_networks_for_text_classification_amd import factor, ops
+    X, A = r8["features"].to(DEV), r8["adj"].to(DEV)
+    from graph_convolutional_networks_for_text_classification_amd.sparse import as_csr
+    f = factor.get(as_csr(A), ops.Operand(X))
+    assert f is not None and f.H == 50 and f.Kc == 50
+    outs = {}
+    for fac in (True, False):
+        saved = ops.FACTOR_GC1
+        ops.FACTOR_GC1 = fac
+        try:
+            torch.manual_seed(123)
+            m = GCN(nfeat=r8["nfeat"], nhid=200, nclass=r8["nclass"], dropout=0.5,
+                    dropout_rng="device" if mode == "train_hash" else "cpu").to(DEV)
+            m.train(mode != "eval")
+            torch.manual_seed(9)
+            lg = m(X, A)
+            if mode == "eval":
+                again = m(X, A)
+                assert torch.equal(lg, again)
+            lg.square().sum().backward()
+            outs[fac] = (lg.detach().cpu().numpy(), {k: p.grad.cpu().numpy() for k, p in m.named_parameters()})
+        finally:
+            ops.FACTOR_GC1 = saved
+    (la, ga), (lb, gb) = outs[True], outs[False]
+    scale = max(1.0, float(np.abs(lb).max()))
+    assert np.abs(la - lb).max() <= 1e-5 * scale, float(np.abs(la - lb).max())
+    for k in ga:
+        np.testing.assert_allclose(ga[k], gb[k], rtol=1e-4, atol=1e-5 * max(1.0, float(np.abs(gb[k]).max())),
+                                   err_msg=k)
+
+
+def test_factored_gc1_kernel_against_float64():
+    """gcnk_hubfactor_gc1_f32 alone on a synthetic doc-topic graph with hub x
+    hub nonzeros, F not a multiple of 16, P = 3 and H1 stored: H1 and
+    S2 = H1 W2 against float64 (every epilogue code but the dropout ones)."""
+    import scipy.sparse as ssp
+    from graph_convolutional_networks_for_text_classification_amd import factor, ops
+    from graph_convolutional_networks_for_text_classification_amd.sparse import as_csr
+    g = datasets.doc_topic_graph(2000, 40, 5, seed=4, tt_prob=0.3)
+    A, X = g["adj"].to(DEV), g["features"].to(DEV)
+    xop = ops.Operand(X)
+    f = factor.get(as_csr(A), xop)
+    assert f is not None
+    rng = np.random.default_rng(3)
+    F, P = 52, 3
+    W1 = torch.from_numpy(rng.standard_normal((g["nfeat"], F)).astype(np.float32)).to(DEV)
+    W2 = torch.from_numpy(rng.standard_normal((F, P)).astype(np.float32)).to(DEV)
+    b1 = torch.from_numpy(rng.standard_normal(F).astype(np.float32)).to(DEV)
+    a = g["adj"].coalesce()
+    Ad = ssp.csr_matrix((a.values().double().numpy(), a.indices().numpy()), shape=tuple(a.shape))
+    x = g["features"].coalesce()
+    Xd = ssp.csr_matrix((x.values().double().numpy(), x.indices().numpy()), shape=tuple(x.shape))
+    Z = Ad @ (Xd @ W1.cpu().double().numpy())
+    for epi in (_lib.EPI_NONE, _lib.EPI_BIAS, _lib.EPI_BIAS_RELU):
+        H1, S2 = ops.hubfactor_gc1(f, W1, b1, W2, epilogue=epi)
+        want = Z if epi == _lib.EPI_NONE else Z + b1.cpu().double().numpy()
+        if epi == _lib.EPI_BIAS_RELU:
+            want = np.maximum(want, 0.0)
+        _close(H1, want, atol=2e-5 * max(1.0, np.abs(want).max()))
+        _close(S2, H1.cpu().double().numpy() @ W2.cpu().double().numpy(), atol=2e-5 * max(1.0, np.abs(want).max()))
+    H1b, S2b = ops.hubfactor_gc1(f, W1, b1, W2, epilogue=_lib.EPI_BIAS_RELU, store_h1=False)
+    assert H1b is None and torch.equal(S2b, S2)

@@ -19,18 +19,30 @@ dropout + the gc2 projection H1 W2), and the hub rows' 600-term gather sums
 of the SpMM never run.  The association differs from A (X W1) only in fp32
 rounding (checked against the reference's goldens to 1e-4, tests/).
 """
+import os
 import threading
 
 import numpy as np
 import torch
 
-from . import _lib
-from .sparse import CSR, from_arrays
+from .sparse import from_arrays
 
 MAX_HUBS = 64     # hub rows staged in LDS (S_T [hubs x F])
+# X[hubs] W1 through the SpMM tile plan on their CSR ("spmm", default) or the
+# split-K MFMA GEMM on a dense copy ("gemm": R8 9.5 + 4.9 us against the tile
+# plan's 7.1 + 4.9, profiles/r03_factor.md)
+XHUB = os.environ.get("GCNK_FACTOR_XHUB", "spmm")
 MAX_KC = 128      # X's light-row column range (U's width)
 ROWS_PER_BLOCK = 32   # csrc/factor.hip kRB
-REC_HEAD = 36         # record words before the items: 33 row offsets, padded to 16 B
+# record words before the items: 33 row offsets | push-section offset | 2 pad |
+# 32 hub indices (-1: light row) | 32 diagonal values (bits) -- csrc/factor.hip
+# kRecHead.  After the A_H items: the push section, [H + 1] offsets (padded to
+# 4 words) and items {row in block, A[t, row] bits} hub by hub (each hub's light
+# columns in the block, CSR order): the block's share of gc2's hub rows.
+REC_HEAD = 100
+REC_PUSH = 33
+REC_HUB = 36
+REC_DIAG = 68
 
 _lock = threading.Lock()
 
@@ -38,12 +50,13 @@ _lock = threading.Lock()
 class HubFactor:
     """The (A-hat, X)-fixed operands of the factored gc1, resident on the device."""
 
-    __slots__ = ("M", "H", "hubs", "k0", "Kc", "U", "rec", "rec_words", "x_hub", "x_hub_dense", "_src")
+    __slots__ = ("M", "H", "hubs", "hubs32", "k0", "Kc", "U", "rec", "rec_words", "nblk", "x_hub", "x_hub_dense",
+                 "hh", "hhl", "first_block", "_src")
 
     def hub_times(self, W):
         """S_T = X[hubs] @ W  (the hub rows of reference layer.py:102)."""
         from .ops import gemm, spmm
-        if self.x_hub is not None:
+        if self.x_hub is not None and (XHUB != "gemm" or self.x_hub_dense is None):
             return spmm(self.x_hub, W)
         return gemm(self.x_hub_dense, W)
 
@@ -113,23 +126,62 @@ def build(adj, xop):
     hrows, hcols, hvals = rows[mh], hub_index[ci[mh]], v[mh].astype(np.float32)
     counts = np.bincount(hrows, minlength=M)
     nblk = (M + ROWS_PER_BLOCK - 1) // ROWS_PER_BLOCK
-    bcounts = np.add.reduceat(np.concatenate([counts, np.zeros(nblk * ROWS_PER_BLOCK - M, np.int64)]),
-                              np.arange(0, nblk * ROWS_PER_BLOCK, ROWS_PER_BLOCK))
-    rec_words = (REC_HEAD + 2 * int(bcounts.max()) + 3) // 4 * 4
-    rec = np.zeros((nblk, rec_words), np.int32)
     starts = np.concatenate([[0], np.cumsum(counts)])
+    # push items: A[t, d] for hub t and light column d, grouped by d's block, hub-major
+    ml = light[ci] & is_hub[rows]
+    prow, pcol, pval = hub_index[rows[ml]], ci[ml], v[ml].astype(np.float32)
+    pblk = pcol // ROWS_PER_BLOCK
+    order = np.lexsort((pcol, prow, pblk))           # block, hub, column
+    prow, pcol, pval, pblk = prow[order], pcol[order], pval[order], pblk[order]
+    pcount = np.bincount(pblk, minlength=nblk)
+    pstart = np.concatenate([[0], np.cumsum(pcount)])
+    blocks = []
+    rec_words = 0
     for b in range(nblk):
         r0, r1 = b * ROWS_PER_BLOCK, min(M, (b + 1) * ROWS_PER_BLOCK)
+        lo, hi = starts[r0], starts[r1]
+        po = (REC_HEAD + 2 * (hi - lo) + 3) // 4 * 4
+        pi = (po + H + 1 + 3) // 4 * 4
+        q0, q1 = pstart[b], pstart[b + 1]
+        words = pi + 2 * (q1 - q0)
+        blocks.append((r0, r1, lo, hi, po, pi, q0, q1))
+        rec_words = max(rec_words, words)
+    rec_words = (rec_words + 3) // 4 * 4
+    rec = np.zeros((nblk, rec_words), np.int32)
+    for b, (r0, r1, lo, hi, po, pi, q0, q1) in enumerate(blocks):
         off = starts[r0:r1 + 1] - starts[r0]
         rec[b, :len(off)] = off
         rec[b, len(off):ROWS_PER_BLOCK + 1] = off[-1]
-        lo, hi = starts[r0], starts[r1]
+        rec[b, REC_PUSH] = po
         rec[b, REC_HEAD:REC_HEAD + 2 * (hi - lo):2] = hcols[lo:hi]
         rec[b, REC_HEAD + 1:REC_HEAD + 2 * (hi - lo):2] = hvals[lo:hi].view(np.int32)
+        rec[b, REC_HUB:REC_HUB + ROWS_PER_BLOCK] = -1
+        rec[b, REC_HUB:REC_HUB + (r1 - r0)] = hub_index[r0:r1]
+        rec[b, REC_DIAG:REC_DIAG + (r1 - r0)] = diag[r0:r1].astype(np.float32).view(np.int32)
+        hcount = np.bincount(prow[q0:q1], minlength=H)
+        rec[b, po:po + H + 1] = np.concatenate([[0], np.cumsum(hcount)])
+        rec[b, pi:pi + 2 * (q1 - q0):2] = pcol[q0:q1] - r0
+        rec[b, pi + 1:pi + 2 * (q1 - q0):2] = pval[q0:q1].view(np.int32)
+    # gc2's hub x hub nonzeros {hub index, value}, one padded row per hub
+    mhh = is_hub[ci] & is_hub[rows]
+    hh_r, hh_c, hh_v = hub_index[rows[mhh]], hub_index[ci[mhh]], v[mhh].astype(np.float32)
+    hhc = np.bincount(hh_r, minlength=H)
+    hhl = max(1, int(hhc.max()))
+    hh = np.zeros((H, hhl, 2), np.int32)
+    hs = np.concatenate([[0], np.cumsum(hhc)])
+    for t in range(H):
+        n = int(hhc[t])
+        hh[t, :n, 0] = hh_c[hs[t]:hs[t + 1]]
+        hh[t, :n, 1] = hh_v[hs[t]:hs[t + 1]].view(np.int32)
     dev = adj.device
     f = HubFactor()
+    f.hh = torch.from_numpy(hh).to(dev)
+    f.hhl = hhl
+    f.nblk = nblk
+    f.first_block = int(hubs.min()) // ROWS_PER_BLOCK   # dispatched first (csrc/factor.hip)
     f.M, f.H, f.k0, f.Kc = M, H, k0, Kc
     f.hubs = torch.from_numpy(hubs.astype(np.int64)).to(dev)
+    f.hubs32 = torch.from_numpy(hubs.astype(np.int32)).to(dev)
     f.U = torch.from_numpy(U.astype(np.float32)).to(dev)
     f.rec = torch.from_numpy(rec).to(dev)
     f.rec_words = rec_words
@@ -138,7 +190,8 @@ def build(adj, xop):
     if xop.csr is not None:
         f.x_hub = from_arrays(Xh.indptr.astype(np.int32), Xh.indices.astype(np.int32), Xh.data.astype(np.float32),
                               (H, X.shape[1]), dev)
-        f.x_hub_dense = None
+        f.x_hub_dense = torch.from_numpy(Xh.toarray().astype(np.float32)).to(dev) \
+            if XHUB == "gemm" and H * X.shape[1] * 4 <= 64 << 20 else None
     else:
         f.x_hub = None
         f.x_hub_dense = xop.dense.index_select(0, f.hubs).contiguous()

@@ -64,6 +64,34 @@ def _check_factor(A, X, F=24, seed=0):
     assert nnz_h == int(is_hub[A.indices].sum())
     err = np.abs(Z - ref).max() / max(1.0, np.abs(ref).max())
     assert err < 1e-6, err
+    # per-row hub index and diagonal in the record head; gc2's hub item lists
+    for b in range(rec.shape[0]):
+        for i in range(min(32, M - 32 * b)):
+            r = 32 * b + i
+            hi = rec[b, factor.REC_HUB + i]
+            assert hi == (int(np.flatnonzero(hubs == r)[0]) if is_hub[r] else -1)
+            assert np.int32(rec[b, factor.REC_DIAG + i]).view(np.float32) == np.float32(A[r, r])
+    # push sections: per block, hub t's light columns in the block with A[t, d];
+    # with the hub x hub lists they rebuild every hub row of A-hat exactly
+    S = np.random.default_rng(seed + 1).standard_normal((M, 8))
+    ref2 = Af @ S
+    hh = f.hh.numpy()
+    got2 = np.zeros((f.H, 8))
+    for b in range(rec.shape[0]):
+        po = rec[b, factor.REC_PUSH]
+        pi = (po + f.H + 1 + 3) // 4 * 4
+        poff = rec[b, po:po + f.H + 1]
+        items = rec[b, pi:].reshape(-1, 2)
+        for t in range(f.H):
+            for k in range(poff[t], poff[t + 1]):
+                row, bits = items[k]
+                assert not is_hub[32 * b + row]
+                got2[t] += np.int32(bits).view(np.float32) * S[32 * b + row]
+    for t in range(f.H):
+        for k in range(hh.shape[1]):
+            tt, bits = hh[t, k]
+            got2[t] += np.int32(bits).view(np.float32) * S[hubs[tt]]
+    assert np.abs(got2 - ref2[hubs]).max() < 1e-9 * max(1.0, np.abs(ref2).max())
     return f
 
 

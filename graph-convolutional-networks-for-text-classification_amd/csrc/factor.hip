@@ -174,34 +174,21 @@ hubfactor_gc1_kernel(FactorArgs a) {
     float4 z[NTQ];
 #pragma unroll
     for (int u = 0; u < NTQ; ++u) z[u] = *reinterpret_cast<const float4*>(s_Z + r * Fz + 4 * (c16 + 16 * u));
-    // items in batches of kIB: every batch's item words and S_T rows are read
-    // together (the serial LDS chain per item made the longest row -- a hub row,
-    // 25 items on R8 -- the kernel's tail); slots past the row repeat its last
-    // item and are not added (select), so the sum keeps the item order
+    // one item at a time: batching the items' loads (4 per round, selects past
+    // the row) measured slower, 2.28 against 2.12 us per block (LDS throughput,
+    // not the item chain, bounds this loop; profiles/r03_factor.md)
     const int2* it = reinterpret_cast<const int2*>(s_rec + kRecHead);
     const int k1 = s_rec[r + 1];
-    constexpr int kIB = 4;
-    for (int k = s_rec[r]; k < k1; k += kIB) {
-      int2 p[kIB];
+#pragma unroll 2
+    for (int k = s_rec[r]; k < k1; ++k) {
+      const int2 p = it[k];
+      const float v = __int_as_float(p.y);
+      const float* srow = s_S + p.x * F + 4 * c16;
+      float4 sv[NTQ];
 #pragma unroll
-      for (int j = 0; j < kIB; ++j) p[j] = it[min(k + j, k1 - 1)];
-      float4 sv[kIB][NTQ];
+      for (int u = 0; u < NTQ; ++u) sv[u] = *reinterpret_cast<const float4*>(srow + 64 * u);
 #pragma unroll
-      for (int j = 0; j < kIB; ++j)
-#pragma unroll
-        for (int u = 0; u < NTQ; ++u) sv[j][u] = *reinterpret_cast<const float4*>(s_S + p[j].x * F + 4 * c16 + 64 * u);
-#pragma unroll
-      for (int j = 0; j < kIB; ++j) {
-        const bool in = k + j < k1;
-        const float v = __int_as_float(p[j].y);
-#pragma unroll
-        for (int u = 0; u < NTQ; ++u) {
-          float4 t = z[u];
-          Vec<4>::fma(t, v, sv[j][u]);
-          z[u].x = in ? t.x : z[u].x; z[u].y = in ? t.y : z[u].y;
-          z[u].z = in ? t.z : z[u].z; z[u].w = in ? t.w : z[u].w;
-        }
-      }
+      for (int u = 0; u < NTQ; ++u) Vec<4>::fma(z[u], v, sv[u]);
     }
     if (row < a.M) {
       const bool plain = a.epi.code == GCNK_EPI_BIAS_RELU;  // eval / no-dropout: no per-element branches

@@ -105,8 +105,7 @@ constexpr int kLightMax64 = 64 / kLightRPW;  // their nonzero limit (kLightRPW r
 // Plan layout (int32 words).  Header (16 words, see gcnk.h):
 //   0 magic  1 M  2 K  3 lane groups per wavefront (64 / LPR)  4 ipc (light-row limit)
 //   5 nunits  6 nhunits (heavy region, padded)  7 nheavy (rows of > 1 segment)
-//   8 ntile (chunks)  9 nred  10 nslabs  11 ntblk (tile blocks)  12 has_diag (bit 0) | the
-//   reduce rows are rows 0 .. M-1 of one block over slabs 0 .. nslabs-1 (bit 1)  13 nnz
+//   8 ntile (chunks)  9 nred  10 nslabs  11 ntblk (tile blocks)  12 has_diag  13 nnz
 //   14 nslots (partial slots)  15 nsingle (chunk items of single-chunk blocks, listed first)
 // Body: items int2[nnz] {col, value bits} in CSR order | units int4[nunits]
 //   {row (-1: empty), nz begin, nz end, heavy row * 64 + segment or -1}: the
@@ -121,7 +120,7 @@ struct Layout {
   int64_t items, units, heavy, tdesc, tcols, tfrag, red, trows, dval, total;
   __host__ __device__ explicit Layout(const int32_t* h) {
     M = h[1]; nunits = h[5]; nhunits = h[6]; nheavy = h[7]; ntile = h[8]; nred = h[9]; ntblk = h[11];
-    has_diag = h[12] & 1; nnz = h[13]; nslots = h[14];
+    has_diag = h[12]; nnz = h[13]; nslots = h[14];
     items = 16;
     units = (items + 2 * nnz + 3) & ~3LL;
     heavy = units + 4 * nunits;
@@ -1010,11 +1009,10 @@ spmm_tile_kernel(const int4* __restrict__ tdesc, const int32_t* __restrict__ tco
 // then the 16 partial sums are added in lane order through LDS.  The row's
 // reduce entry (row, slabs, diagonal) is the only plan read, so the slab loads
 // (and the diagonal's B row) issue one latency after entry.
-template <bool UNI>
 __device__ __forceinline__ void reduce_body(int32_t bx, int32_t by, int32_t bz, const int4* __restrict__ red,
                                             int32_t F, const float* __restrict__ slabs, int64_t slab_ld,
                                             const float* __restrict__ B, int64_t ldb, float* __restrict__ C,
-                                            int64_t ldc, const Epi& epi, int32_t uni_rows, int32_t uni_slabs) {
+                                            int64_t ldc, const Epi& epi) {
   __shared__ float4 s_acc[16][16];
   const int32_t rl = by;  // row within block
   const int sl = threadIdx.x >> 4, c4 = threadIdx.x & 15;
@@ -1025,8 +1023,7 @@ __device__ __forceinline__ void reduce_body(int32_t bx, int32_t by, int32_t bz, 
 #pragma unroll
     for (int i = 0; i < 4; ++i)
       if (col + i < F) bcol[i] = epi.bias[col + i];
-  // row, first slab, slabs, diagonal bits (UNI: row rl of rows 0 .. uni_rows-1, all slabs)
-  const int4 rr = UNI ? make_int4(rl < uni_rows ? rl : -1, 0, uni_slabs, 0) : red[(int64_t)bx * kRB + rl];
+  const int4 rr = red[(int64_t)bx * kRB + rl];  // row, first slab, slabs, diagonal bits
   if (rr.x < 0) return;
   const int64_t row = rr.x;
   const float dv = __int_as_float(rr.w);
@@ -1070,13 +1067,11 @@ __device__ __forceinline__ void reduce_body(int32_t bx, int32_t by, int32_t bz, 
   }
 }
 
-template <bool UNI>
 __global__ void __launch_bounds__(256)
 spmm_tile_reduce_kernel(const int4* __restrict__ red, int32_t F, const float* __restrict__ slabs, int64_t slab_ld,
-                        const float* __restrict__ B, int64_t ldb, float* __restrict__ C, int64_t ldc, Epi epi,
-                        int32_t uni_rows, int32_t uni_slabs) {
-  reduce_body<UNI>((int32_t)blockIdx.x, (int32_t)blockIdx.y, (int32_t)blockIdx.z, red, F, slabs, slab_ld, B, ldb, C,
-                   ldc, epi, uni_rows, uni_slabs);
+                        const float* __restrict__ B, int64_t ldb, float* __restrict__ C, int64_t ldc, Epi epi) {
+  reduce_body((int32_t)blockIdx.x, (int32_t)blockIdx.y, (int32_t)blockIdx.z, red, F, slabs, slab_ld, B, ldb, C, ldc,
+              epi);
 }
 
 // ---------------------------------------------------------------------------
@@ -1563,14 +1558,8 @@ int host_plan(const int32_t* rp, const int32_t* ci, const float* vv, int32_t M, 
               (long long)nunits, (long long)nslots);
     return GCNK_EUNSUP;
   }
-  // one multi-chunk block holding rows 0 .. M-1 in order (a few dense rows, e.g. the
-  // hub rows of X): the reduce kernel derives its entries instead of reading them
-  bool uni = nred == 1 && M <= kRB && !any_diag && hp.red.size() == (size_t)4 * kRB;
-  for (int32_t rl = 0; uni && rl < kRB; ++rl)
-    uni = hp.red[4 * (size_t)rl] == (rl < M ? rl : -1) && (rl >= M || hp.red[4 * (size_t)rl + 1] == 0);
   const int32_t h[16] = {kMagic, M,     K,      groups, ipc,  (int32_t)nunits, (int32_t)nh, nheavy,
-                         ntile,  nred, nslabs, ntblk,  (any_diag ? 1 : 0) | (uni ? 2 : 0), (int32_t)nnz,
-                         (int32_t)nslots, nsingle};
+                         ntile,  nred, nslabs, ntblk,  any_diag ? 1 : 0, (int32_t)nnz, (int32_t)nslots, nsingle};
   std::copy(h, h + 16, hp.hdr);
   return GCNK_OK;
 }
@@ -1938,13 +1927,8 @@ static int spmm_impl(const void* plan, const int32_t* hdr, const float* B, int64
     const int rc = launch_tile(vec4, nt_need, (unsigned)(i1 - i0), ta, s);
     if (rc) return rc;
     if (L.nred > 0 && part != 1) {
-      const dim3 grid((unsigned)L.nred, kRB, (unsigned)((F + 63) / 64));
-      if (hdr[12] & 2)
-        hipLaunchKernelGGL(spmm_tile_reduce_kernel<true>, grid, dim3(256), 0, s, reinterpret_cast<const int4*>(p + L.red),
-                           F, slabs, slab_ld, B, ldb, C, ldc, e, hdr[1], hdr[10]);
-      else
-        hipLaunchKernelGGL(spmm_tile_reduce_kernel<false>, grid, dim3(256), 0, s,
-                           reinterpret_cast<const int4*>(p + L.red), F, slabs, slab_ld, B, ldb, C, ldc, e, 0, 0);
+      hipLaunchKernelGGL(spmm_tile_reduce_kernel, dim3((unsigned)L.nred, kRB, (unsigned)((F + 63) / 64)), dim3(256),
+                         0, s, reinterpret_cast<const int4*>(p + L.red), F, slabs, slab_ld, B, ldb, C, ldc, e);
       int rc = launch_check("spmm_tile_reduce_kernel");
       if (rc) return rc;
     }

@@ -145,8 +145,8 @@ const char* gcnk_last_error(void);
  * Plan header (16 int32, first words of the plan; gcnk_spmm_plan_query):
  *   row-unit plan: 0 magic 'GNK5'  1 M  2 K  3 groups  4 ipc  5 row units
  *   6 heavy segments  7 heavy rows of > 1 segment  8 tile chunks
- *   9 multi-chunk blocks  10 slabs  11 tile blocks  12 bit 0: diagonal kept aside,
- *   bit 1: one multi-chunk block of rows 0 .. M-1 (its reduce entries implied)  13 nnz  14 partial slots  15 chunk items of single-chunk tile blocks
+ *   9 multi-chunk blocks  10 slabs  11 tile blocks  12 diagonal kept aside
+ *   (0/1)  13 nnz  14 partial slots  15 chunk items of single-chunk tile blocks
  *   hub plan: 0 magic 'GNH2'  1 M  2 K  3 groups  4 row groups G  5 record
  *   stride (words)  6 hub rows H  7 first hub row  8 light rows  9 nnz
  *   10 light rows per group  11 hub degree threshold  12 max record items

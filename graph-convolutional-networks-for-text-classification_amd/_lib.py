@@ -31,7 +31,7 @@ def _resolve_lib():
 
 
 LIB_PATH = _resolve_lib()
-ABI_VERSION = 6
+ABI_VERSION = 7
 
 # C-ABI return codes (gcnk.h)
 OK, EARG, EUNSUP, EHIP = 0, -1, -2, -3
@@ -145,11 +145,8 @@ SIGNATURES = {
         _vp, _i64, _f32,                  # drop_mask, ldm, drop_scale
         _f32, _u64, _u64, _vp,            # keep_prob, seed, offset, rng_base
         _vp, _i64, _vp, _i64, _vp, _i64,  # W2, ldw2, H, ldh, C2, ldc2
-        _vp, _vp, _i32, _vp]),            # C2T, part, first_block, stream
-    "gcnk_hubfactor_gc2_f32": (ctypes.c_int, [
-        _i32, _i32, _i32, _vp, _i32,      # M, P, nhub, rec, rec_words
-        _vp, _vp, _i32, _vp,              # part, hh, hhl, hub_rows
-        _vp, _vp, _vp, _vp, _i64, _vp]),  # S2, S2T, bias, out, ldo, stream
+        _vp]),                            # stream
+ # S2, S2T, bias, out, ldo, stream
     "gcnk_class_stats": (ctypes.c_int, [_vp, _i64, _vp, _vp, _i64, _i32, _vp, _vp]),
     "gcnk_edgelist_size": (ctypes.c_int, [ctypes.c_char_p, _vp, _vp]),
     "gcnk_edgelist_csr": (ctypes.c_int, [ctypes.c_char_p, _i64, _i64, _vp, _vp, _vp]),

@@ -43,10 +43,11 @@ constexpr int kThreads = 512;   // 8 waves: 2 row strips x 4 column quarters
 constexpr int kMaxKsteps = 32;  // Kc <= 128
 constexpr int kProjW = 16;      // projection width (one MFMA n-tile): P <= 16
 constexpr int kBPad = 64;       // zero floats after the staged W1[Kc] (tiles past F read them)
-// block record (factor.py): 33 row offsets, push-section offset, 2 pad | 32 hub
-// indices (-1: light) | 32 diagonal values | A_H items int2 {hub, value} | push
-// section: [nhub + 1] offsets (to 4 words), items int2 {row in block, A[t, row]}
-constexpr int kRecPush = 33, kRecHub = 36, kRecDiag = 68, kRecHead = 100;
+// block record (factor.py): 33 row offsets, 3 pad | 32 row ids (-1 past M) |
+// A_H items int2 {hub, value}.  Block b holds rows perm[32 b .. 32 b + 31]: the
+// host spreads the hub rows (long item lists) over the blocks, U's rows are in
+// that order, outputs go to the row ids.
+constexpr int kRecRow = 36, kRecHead = 68;
 // compile-time shapes (every MFMA unconditional, operands in fixed registers):
 // KS k-steps of U W1[Kc] (Kc <= 4 KS; U columns past Kc read as zero, W1 rows
 // past Kc staged as zero) and NTQ 16-column tiles per quarter of F (F <= 64 NTQ;
@@ -56,16 +57,13 @@ __host__ __device__ constexpr int pick_ntq(int f) { return f <= 128 ? 2 : f <= 1
 
 struct FactorArgs {
   int32_t M, F, Kc, nhub, P;
-  const float* U; int64_t ldu;          // [M x >= Kc]
+  const float* U; int64_t ldu;          // [M x >= Kc], rows in block order
   const float* W; int64_t ldw; int32_t k0;  // W1 rows k0 .. k0 + Kc - 1 (ldw == F: staged flat)
   const float* S; int64_t lds;          // [nhub x F]
-  const int32_t* rec; int32_t rec_words;  // per 32-row block: off[33] | pad | items int2 {hub, val}
+  const int32_t* rec; int32_t rec_words;  // per 32-row block: off[33] | pad | row ids | items int2 {hub, val}
   const float* W2; int64_t ldw2;        // [F x P]
   float* H; int64_t ldh;                // nullable
   float* C2; int64_t ldc2;              // [M x P]
-  float* C2T;                           // nullable: hub rows of C2, compact [nhub x P]
-  float* part;                          // nullable: gc2's hub-row partials [nblk][nhub][P] of this block
-  int32_t first_block;                  // workgroup 0 takes this block (the hub rows': the longest item lists)
   Epi epi;
 };
 
@@ -84,10 +82,8 @@ hubfactor_gc1_kernel(FactorArgs a) {
   const int F = a.F, Q = F / 4;
   constexpr int Fp = 64 * NTQ, Fz = Fp + 4;  // s_Z row stride: 16-B rows, conflict-free MFMA-layout accesses
   constexpr int Kr = 4 * KS;
-  // blocks in rotated order: the hub rows' blocks, whose item lists are the
-  // longest, are dispatched first instead of last
-  const int blk = (int)((blockIdx.x + (unsigned)a.first_block) % gridDim.x);
-  const int64_t m0 = (int64_t)blk * kRB;
+  const int blk = (int)blockIdx.x;
+  const int64_t m0 = (int64_t)blk * kRB;  // position in the block order (U's rows)
   // LDS: region1 = s_B [Kr][F] + kBPad zeros (phase 1), then s_Z [kRB][Fz]
   //      | s_S [nhub][F] | s_W2 [F][P] | s_bias [F] | s_rec | s_red [3][2][64][4]
   // Every global operand is staged here in the one round of loads that opens the
@@ -102,7 +98,6 @@ hubfactor_gc1_kernel(FactorArgs a) {
   float* s_bias = s_W2 + ((F * a.P + 3) & ~3);
   int32_t* s_rec = reinterpret_cast<int32_t*>(s_bias + F);
   float* s_red = reinterpret_cast<float*>(s_rec + a.rec_words);
-  float* s_c2 = s_red + 3 * 2 * 64 * 4;  // [kRB][kProjW]: the block's C2 rows for the push
 
   // ---- 0. loads, all issued before the first wait: zeros first (no LDS-DMA in
   //      flight yet), then LDS-DMA of W1[Kc] (flat) and the block's record, the
@@ -170,7 +165,7 @@ hubfactor_gc1_kernel(FactorArgs a) {
   //      LDS reads issue together.
   {
     const int r = tid >> 4, c16 = tid & 15;
-    const int64_t row = m0 + r;
+    const int64_t row = s_rec[kRecRow + r];  // output row (-1 past M)
     float4 z[NTQ];
 #pragma unroll
     for (int u = 0; u < NTQ; ++u) z[u] = *reinterpret_cast<const float4*>(s_Z + r * Fz + 4 * (c16 + 16 * u));
@@ -190,7 +185,7 @@ hubfactor_gc1_kernel(FactorArgs a) {
 #pragma unroll
       for (int u = 0; u < NTQ; ++u) Vec<4>::fma(z[u], v, sv[u]);
     }
-    if (row < a.M) {
+    if (row >= 0) {
       const bool plain = a.epi.code == GCNK_EPI_BIAS_RELU;  // eval / no-dropout: no per-element branches
 #pragma unroll
       for (int u = 0; u < NTQ; ++u) {
@@ -242,138 +237,13 @@ hubfactor_gc1_kernel(FactorArgs a) {
     const int p = lane & 15;
 #pragma unroll
     for (int r = 0; r < 4; ++r) {
-      const int rl = 16 * strip + (lane >> 4) * 4 + r;
-      const int64_t row = m0 + rl;
-      s_c2[rl * kProjW + p] = pc[r];
-      if (row < a.M && p < a.P) {
-        a.C2[row * a.ldc2 + p] = pc[r];
-        const int hub = s_rec[kRecHub + rl];
-        if (a.C2T && hub >= 0) a.C2T[(int64_t)hub * a.P + p] = pc[r];
-      }
-    }
-  }
-  // ---- 4. push: this block's share of gc2's hub rows, part[blk][t][p] =
-  //      sum over the block's light rows d of A[t, d] C2[d, p] (record order)
-  if (a.part) {
-    __syncthreads();
-    const int po = s_rec[kRecPush];
-    const int32_t* poff = s_rec + po;
-    const int2* pit = reinterpret_cast<const int2*>(s_rec + ((po + a.nhub + 1 + 3) & ~3));
-    for (int e = tid; e < a.nhub * a.P; e += kThreads) {
-      const int t = e / a.P, p = e - t * a.P;
-      float acc = 0.f;
-      for (int k = poff[t]; k < poff[t + 1]; ++k) {
-        const int2 it = pit[k];
-        acc = fmaf(__int_as_float(it.y), s_c2[it.x * kProjW + p], acc);
-      }
-      a.part[((int64_t)blk * a.nhub + t) * a.P + p] = acc;
+      const int64_t row = s_rec[kRecRow + 16 * strip + (lane >> 4) * 4 + r];
+      if (row >= 0 && p < a.P) a.C2[row * a.ldc2 + p] = pc[r];
     }
   }
   stamp(a.epi, 3);
 }
 
-
-// ---------------------------------------------------------------------------
-// gc2 of the factored layer pair: Z2 = A-hat S2 + b2 (layer.py:106,110, gc2),
-// S2 [M x P] from hubfactor_gc1 (with its hub rows compact in S2T [nhub x P]).
-//   light row d:  A_dd S2[d] + sum_t A[d, t] S2T[t]      (the block record's items)
-//   hub row t:    sum over A-hat row t of A[t, j] S2[j]   (its CSR row, padded)
-// Workgroups [0, nhub): one hub row each (first in the grid: the longer chain),
-// 256 threads over its nonzeros (items, then their S2 rows: two rounds of
-// loads), a fixed-order xor butterfly per wave, the 4 waves added in order;
-// workgroups [nhub, nhub + nblk): 32 light-row blocks, every operand staged in
-// one round of loads (record, S2T, the block's S2 rows, b2), thread (row,
-// column pair).
-struct Gc2Args {
-  int32_t M, P, nhub, nblk;
-  const int32_t* rec; int32_t rec_words;
-  const float* part;                    // [nblk][nhub][P] from hubfactor_gc1's push
-  const int2* hh; int32_t hhl;          // [nhub][hhl] hub x hub {hub index, value bits}, value 0 past the row
-  const int32_t* hub_rows;              // [nhub] row of hub t
-  const float* S2; const float* S2T;
-  const float* bias;
-  float* out; int64_t ldo;
-};
-
-constexpr int kGc2P = 16;
-template <int PM>  // P <= PM, P % 4 == 0
-__global__ void __launch_bounds__(256)
-hubfactor_gc2_kernel(Gc2Args a, int32_t nblk) {
-  __shared__ __attribute__((aligned(16))) float smem2[kGc2P * 256 + kGc2P];
-  extern __shared__ __attribute__((aligned(16))) int32_t dyn[];
-  const int tid = threadIdx.x, lane = tid & 63;
-  const int wv = __builtin_amdgcn_readfirstlane(tid >> 6);
-  const int P = a.P;
-  if ((int)blockIdx.x >= a.nhub) {
-    const int blk = (int)blockIdx.x - a.nhub;
-    const int64_t m0 = (int64_t)blk * kRB;
-    int32_t* s_rec = dyn;
-    float* s_T = reinterpret_cast<float*>(dyn + a.rec_words);  // [nhub][P]
-    float* s_S = s_T + a.nhub * P;                             // [32][P]
-    float* s_b = smem2;                                        // [P]
-    const int32_t* rec = a.rec + (int64_t)blk * a.rec_words;
-    for (int e0 = wv * 64; e0 < a.rec_words / 4; e0 += 256)
-      if (e0 + lane < a.rec_words / 4) lds_dma16(rec + 4 * (e0 + lane), s_rec + 4 * e0);
-    for (int e0 = wv * 64; e0 < a.nhub * P; e0 += 256)
-      if (e0 + lane < a.nhub * P) lds_dma4(a.S2T + e0 + lane, s_T + e0);
-    const int nrow = (int)min<int64_t>(kRB, a.M - m0);
-    for (int e0 = wv * 64; e0 < nrow * P; e0 += 256)
-      if (e0 + lane < nrow * P) lds_dma4(a.S2 + m0 * P + e0 + lane, s_S + e0);
-    if (tid < P) s_b[tid] = a.bias ? a.bias[tid] : 0.f;
-    __builtin_amdgcn_s_waitcnt(0x0F70);
-    __syncthreads();
-    const int r = tid >> 3, pp = tid & 7;
-    if (r < nrow && s_rec[kRecHub + r] < 0) {
-      const float dg = __int_as_float(s_rec[kRecDiag + r]);
-      const int2* it = reinterpret_cast<const int2*>(s_rec + kRecHead);
-      for (int p = pp; p < P; p += 8) {
-        float acc = dg * s_S[r * P + p];
-        for (int k = s_rec[r]; k < s_rec[r + 1]; ++k) {
-          const int2 q = it[k];
-          acc = fmaf(__int_as_float(q.y), s_T[q.x * P + p], acc);
-        }
-        a.out[(m0 + r) * a.ldo + p] = acc + s_b[p];
-      }
-    }
-    return;
-  }
-  // hub row t: thread i sums the partials of blocks i, i + 256, ... then (i < hhl)
-  // its hub x hub term; butterfly per wave, waves added in order
-  (void)nblk;
-  const int t = (int)blockIdx.x;
-  constexpr int V4 = PM / 4;
-  float4 acc[V4];
-#pragma unroll
-  for (int p = 0; p < V4; ++p) acc[p] = make_float4(0.f, 0.f, 0.f, 0.f);
-  for (int b = tid; b < a.nblk; b += 256) {
-    const float* pp = a.part + ((int64_t)b * a.nhub + t) * P;
-#pragma unroll
-    for (int p = 0; p < V4; ++p)
-      if (4 * p < P) Vec<4>::add(acc[p], *reinterpret_cast<const float4*>(pp + 4 * p));
-  }
-  if (tid < a.hhl) {
-    const int2 q = a.hh[(int64_t)t * a.hhl + tid];
-#pragma unroll
-    for (int p = 0; p < V4; ++p)
-      if (4 * p < P) Vec<4>::fma(acc[p], __int_as_float(q.y), *reinterpret_cast<const float4*>(a.S2T + q.x * P + 4 * p));
-  }
-  float* s_red = smem2;  // [4 waves][16]
-#pragma unroll
-  for (int p = 0; p < V4; ++p) {
-#pragma unroll
-    for (int m = 32; m >= 1; m >>= 1) {
-      acc[p].x += __shfl_xor(acc[p].x, m); acc[p].y += __shfl_xor(acc[p].y, m);
-      acc[p].z += __shfl_xor(acc[p].z, m); acc[p].w += __shfl_xor(acc[p].w, m);
-    }
-    if (lane == 0) *reinterpret_cast<float4*>(s_red + wv * kGc2P + 4 * p) = acc[p];
-  }
-  __syncthreads();
-  if (tid < P) s_red[tid] = ((s_red[tid] + s_red[kGc2P + tid]) + s_red[2 * kGc2P + tid]) + s_red[3 * kGc2P + tid];
-  if (tid < P) {
-    const int64_t row = a.hub_rows[t];
-    a.out[row * a.ldo + tid] = s_red[tid] + (a.bias ? a.bias[tid] : 0.f);
-  }
-}
 
 }  // namespace
 }  // namespace gcnk
@@ -383,8 +253,7 @@ using namespace gcnk;
 static int64_t hubfactor_lds_bytes(int32_t F, int32_t Kc, int32_t nhub, int32_t rec_words, int32_t P = kProjW) {
   const int64_t Fz = 64 * pick_ntq(F) + 4, Kr = 4 * pick_ks(Kc);
   const int64_t r1 = std::max<int64_t>(Kr * F + kBPad, (int64_t)kRB * Fz);
-  return 4 * (r1 + (int64_t)nhub * F + (((int64_t)F * P + 3) & ~3LL) + F + rec_words + 3 * 2 * 64 * 4 +
-              kRB * kProjW);
+  return 4 * (r1 + (int64_t)nhub * F + (((int64_t)F * P + 3) & ~3LL) + F + rec_words + 3 * 2 * 64 * 4);
 }
 
 extern "C" int64_t gcnk_hubfactor_lds_bytes(int32_t F, int32_t Kc, int32_t nhub, int32_t rec_words) {
@@ -398,7 +267,7 @@ extern "C" int gcnk_hubfactor_gc1_f32(int32_t M, int32_t F, int32_t Kc, int32_t 
                                       int32_t epilogue, const uint8_t* drop_mask, int64_t ldm, float drop_scale,
                                       float keep_prob, uint64_t seed, uint64_t offset, const uint64_t* rng_base,
                                       const float* W2, int64_t ldw2, float* H, int64_t ldh, float* C2,
-                                      int64_t ldc2, float* C2T, float* part, int32_t first_block, void* stream) {
+                                      int64_t ldc2, void* stream) {
   if (M <= 0 || F <= 0 || Kc <= 0 || nhub <= 0 || P <= 0 || !U || !W || !S || !rec || !W2 || !C2 || k0 < 0) {
     set_error("gcnk_hubfactor_gc1_f32: bad sizes or null operand (M=%d F=%d Kc=%d hubs=%d P=%d)", M, F, Kc, nhub, P);
     return GCNK_EARG;
@@ -428,18 +297,13 @@ extern "C" int gcnk_hubfactor_gc1_f32(int32_t M, int32_t F, int32_t Kc, int32_t 
   a.M = M; a.F = F; a.Kc = Kc; a.nhub = nhub; a.P = P;
   a.U = U; a.ldu = ldu; a.W = W; a.ldw = ldw; a.k0 = k0;
   a.S = S; a.lds = lds; a.rec = rec; a.rec_words = rec_words;
-  a.W2 = W2; a.ldw2 = ldw2; a.H = H; a.ldh = ldh; a.C2 = C2; a.ldc2 = ldc2; a.C2T = C2T; a.part = part;
+  a.W2 = W2; a.ldw2 = ldw2; a.H = H; a.ldh = ldh; a.C2 = C2; a.ldc2 = ldc2;
   Epi& e = a.epi;
   e.bias = bias; e.mask = drop_mask; e.scale = drop_scale; e.keep_prob = keep_prob;
   e.seed_lo = (uint32_t)seed; e.seed_hi = (uint32_t)(seed >> 32); e.offset = offset; e.rng_base = rng_base;
   e.code = epilogue; e.stamps = debug_stamps();
   e.ldm = epilogue == GCNK_EPI_BIAS_RELU_HASH ? (ldm > 0 ? ldm : F) : ldm;
   const int64_t nblk = ((int64_t)M + kRB - 1) / kRB;
-  if (first_block < 0 || first_block >= nblk) {
-    set_error("gcnk_hubfactor_gc1_f32: first_block %d outside [0, %lld)", first_block, (long long)nblk);
-    return GCNK_EARG;
-  }
-  a.first_block = first_block;
   const int ks = pick_ks(Kc), ntq = pick_ntq(F);
   auto go = [&](auto kern) {
     static_cast<void>(0);
@@ -458,37 +322,4 @@ extern "C" int gcnk_hubfactor_gc1_f32(int32_t M, int32_t F, int32_t Kc, int32_t 
 #undef GCNK_FACTOR_CASE
   set_error("gcnk_hubfactor_gc1_f32: no kernel for Kc=%d F=%d", Kc, F);
   return GCNK_EUNSUP;
-}
-
-extern "C" int gcnk_hubfactor_gc2_f32(int32_t M, int32_t P, int32_t nhub, const int32_t* rec, int32_t rec_words,
-                                      const float* part, const int32_t* hh, int32_t hhl, const int32_t* hub_rows,
-                                      const float* S2, const float* S2T, const float* bias, float* out, int64_t ldo,
-                                      void* stream) {
-  if (M <= 0 || P <= 0 || nhub <= 0 || !rec || !part || !hh || !hub_rows || !S2 || !S2T || !out || ldo < P ||
-      rec_words < kRecHead || rec_words % 4 || hhl <= 0) {
-    set_error("gcnk_hubfactor_gc2_f32: bad sizes or null operand (M=%d P=%d hubs=%d hhl=%d)", M, P, nhub, hhl);
-    return GCNK_EARG;
-  }
-  if (P > kGc2P || P % 4 || hhl > 256 || !aligned16(S2) || !aligned16(S2T) || !aligned16(part)) {
-    set_error("gcnk_hubfactor_gc2_f32: unsupported P=%d (a multiple of 4, <= %d) or %d hub x hub nonzeros", P, kGc2P,
-              hhl);
-    return GCNK_EUNSUP;
-  }
-  const int64_t lds = 4 * ((int64_t)rec_words + (int64_t)nhub * P + (int64_t)kRB * P);
-  if (lds > 64 * 1024) {
-    set_error("gcnk_hubfactor_gc2_f32: %lld B of LDS", (long long)lds);
-    return GCNK_EUNSUP;
-  }
-  Gc2Args a;
-  const int32_t nblk = (int32_t)(((int64_t)M + kRB - 1) / kRB);
-  a.M = M; a.P = P; a.nhub = nhub; a.nblk = nblk; a.rec = rec; a.rec_words = rec_words;
-  a.part = part; a.hh = reinterpret_cast<const int2*>(hh); a.hhl = hhl; a.hub_rows = hub_rows;
-  a.S2 = S2; a.S2T = S2T; a.bias = bias; a.out = out; a.ldo = ldo;
-  if (P <= 8)
-    hipLaunchKernelGGL(hubfactor_gc2_kernel<8>, dim3((unsigned)(nblk + nhub)), dim3(256), (size_t)lds,
-                       reinterpret_cast<hipStream_t>(stream), a, nblk);
-  else
-    hipLaunchKernelGGL(hubfactor_gc2_kernel<16>, dim3((unsigned)(nblk + nhub)), dim3(256), (size_t)lds,
-                       reinterpret_cast<hipStream_t>(stream), a, nblk);
-  return launch_check("hubfactor_gc2_kernel");
 }

@@ -9,7 +9,7 @@ topic-weight columns, trainer.py:226-238).  Then
 
     A X W1 = U W1[k0:k0+Kc] + A_H (X_hubs W1)
 
-with U [M x Kc] dense -- row d (light): A_dd X[d, Kc]; row t (hub):
+with U [M x Kc] dense (rows in the block order ``perm``) -- row d (light): A_dd X[d, Kc]; row t (hub):
 sum over light d of A_td X[d, Kc] -- and A_H = A-hat restricted to hub columns.
 U and A_H depend only on (A-hat, X), so they are built here ONCE per operand
 pair (host, float64, rounded to fp32 once) and cached on the adjacency; every
@@ -34,15 +34,13 @@ MAX_HUBS = 64     # hub rows staged in LDS (S_T [hubs x F])
 XHUB = os.environ.get("GCNK_FACTOR_XHUB", "spmm")
 MAX_KC = 128      # X's light-row column range (U's width)
 ROWS_PER_BLOCK = 32   # csrc/factor.hip kRB
-# record words before the items: 33 row offsets | push-section offset | 2 pad |
-# 32 hub indices (-1: light row) | 32 diagonal values (bits) -- csrc/factor.hip
-# kRecHead.  After the A_H items: the push section, [H + 1] offsets (padded to
-# 4 words) and items {row in block, A[t, row] bits} hub by hub (each hub's light
-# columns in the block, CSR order): the block's share of gc2's hub rows.
-REC_HEAD = 100
-REC_PUSH = 33
-REC_HUB = 36
-REC_DIAG = 68
+# record words before the items: 33 row offsets | 3 pad | 32 row ids (-1 past
+# M) -- csrc/factor.hip kRecHead.  A block's rows are a slice of the row order
+# `perm` (hub rows spread evenly between the light rows, so no block carries
+# more than one or two hub rows' long item lists: the item loop is LDS-bound per
+# workgroup, and R8's contiguous topic rows made three blocks the kernel's tail).
+REC_HEAD = 68
+REC_ROW = 36
 
 _lock = threading.Lock()
 
@@ -50,8 +48,8 @@ _lock = threading.Lock()
 class HubFactor:
     """The (A-hat, X)-fixed operands of the factored gc1, resident on the device."""
 
-    __slots__ = ("M", "H", "hubs", "hubs32", "k0", "Kc", "U", "rec", "rec_words", "nblk", "x_hub", "x_hub_dense",
-                 "hh", "hhl", "first_block", "_src")
+    __slots__ = ("M", "H", "hubs", "k0", "Kc", "U", "perm", "rec", "rec_words", "nblk", "x_hub", "x_hub_dense",
+                 "_src")
 
     def hub_times(self, W):
         """S_T = X[hubs] @ W  (the hub rows of reference layer.py:102)."""
@@ -115,73 +113,48 @@ def build(adj, xop):
     Kcp = (Kc + 3) // 4 * 4
     Xr = XL[:, k0:k1]
     A = sp.csr_matrix((v, ci, rp), shape=(M, M))
-    U = np.zeros((M, Kcp), np.float64)
     diag = A.diagonal()
-    U[light, :Kc] = (sp.diags(diag[light]) @ Xr[light]).toarray()
-    U[hubs, :Kc] = (A[hubs] @ Xr).toarray()           # Xr's hub rows are zero: light columns only
-    # A_H: every row's hub-column nonzeros, as per-32-row-block records
+    Uo = np.zeros((M, Kcp), np.float64)
+    Uo[light, :Kc] = (sp.diags(diag[light]) @ Xr[light]).toarray()
+    Uo[hubs, :Kc] = (A[hubs] @ Xr).toarray()          # Xr's hub rows are zero: light columns only
+    # row order: light rows in order, hub j placed at position ~ (j + 1/2) M / H
+    lights = np.flatnonzero(light)
+    pos = ((np.arange(H) + 0.5) * M / H).astype(np.int64)
+    perm = np.insert(lights, np.minimum(pos - np.arange(H), len(lights)), hubs)
+    assert len(perm) == M and np.array_equal(np.sort(perm), np.arange(M))
+    U = Uo[perm]
+    # A_H: every row's hub-column nonzeros, as per-32-row-block records (row order perm)
     hub_index = np.full(M, -1, np.int64)
     hub_index[hubs] = np.arange(H)
     mh = is_hub[ci]
-    hrows, hcols, hvals = rows[mh], hub_index[ci[mh]], v[mh].astype(np.float32)
-    counts = np.bincount(hrows, minlength=M)
+    counts = np.bincount(rows[mh], minlength=M)                     # hub items per original row
+    hstart = np.concatenate([[0], np.cumsum(counts)])
+    hcols, hvals = hub_index[ci[mh]], v[mh].astype(np.float32)      # CSR order within a row
     nblk = (M + ROWS_PER_BLOCK - 1) // ROWS_PER_BLOCK
-    starts = np.concatenate([[0], np.cumsum(counts)])
-    # push items: A[t, d] for hub t and light column d, grouped by d's block, hub-major
-    ml = light[ci] & is_hub[rows]
-    prow, pcol, pval = hub_index[rows[ml]], ci[ml], v[ml].astype(np.float32)
-    pblk = pcol // ROWS_PER_BLOCK
-    order = np.lexsort((pcol, prow, pblk))           # block, hub, column
-    prow, pcol, pval, pblk = prow[order], pcol[order], pval[order], pblk[order]
-    pcount = np.bincount(pblk, minlength=nblk)
-    pstart = np.concatenate([[0], np.cumsum(pcount)])
-    blocks = []
+    pcounts = counts[perm]
+    pstart = np.concatenate([[0], np.cumsum(pcounts)])
     rec_words = 0
     for b in range(nblk):
         r0, r1 = b * ROWS_PER_BLOCK, min(M, (b + 1) * ROWS_PER_BLOCK)
-        lo, hi = starts[r0], starts[r1]
-        po = (REC_HEAD + 2 * (hi - lo) + 3) // 4 * 4
-        pi = (po + H + 1 + 3) // 4 * 4
-        q0, q1 = pstart[b], pstart[b + 1]
-        words = pi + 2 * (q1 - q0)
-        blocks.append((r0, r1, lo, hi, po, pi, q0, q1))
-        rec_words = max(rec_words, words)
+        rec_words = max(rec_words, REC_HEAD + 2 * int(pstart[r1] - pstart[r0]))
     rec_words = (rec_words + 3) // 4 * 4
     rec = np.zeros((nblk, rec_words), np.int32)
-    for b, (r0, r1, lo, hi, po, pi, q0, q1) in enumerate(blocks):
-        off = starts[r0:r1 + 1] - starts[r0]
+    for b in range(nblk):
+        r0, r1 = b * ROWS_PER_BLOCK, min(M, (b + 1) * ROWS_PER_BLOCK)
+        off = pstart[r0:r1 + 1] - pstart[r0]
         rec[b, :len(off)] = off
         rec[b, len(off):ROWS_PER_BLOCK + 1] = off[-1]
-        rec[b, REC_PUSH] = po
-        rec[b, REC_HEAD:REC_HEAD + 2 * (hi - lo):2] = hcols[lo:hi]
-        rec[b, REC_HEAD + 1:REC_HEAD + 2 * (hi - lo):2] = hvals[lo:hi].view(np.int32)
-        rec[b, REC_HUB:REC_HUB + ROWS_PER_BLOCK] = -1
-        rec[b, REC_HUB:REC_HUB + (r1 - r0)] = hub_index[r0:r1]
-        rec[b, REC_DIAG:REC_DIAG + (r1 - r0)] = diag[r0:r1].astype(np.float32).view(np.int32)
-        hcount = np.bincount(prow[q0:q1], minlength=H)
-        rec[b, po:po + H + 1] = np.concatenate([[0], np.cumsum(hcount)])
-        rec[b, pi:pi + 2 * (q1 - q0):2] = pcol[q0:q1] - r0
-        rec[b, pi + 1:pi + 2 * (q1 - q0):2] = pval[q0:q1].view(np.int32)
-    # gc2's hub x hub nonzeros {hub index, value}, one padded row per hub
-    mhh = is_hub[ci] & is_hub[rows]
-    hh_r, hh_c, hh_v = hub_index[rows[mhh]], hub_index[ci[mhh]], v[mhh].astype(np.float32)
-    hhc = np.bincount(hh_r, minlength=H)
-    hhl = max(1, int(hhc.max()))
-    hh = np.zeros((H, hhl, 2), np.int32)
-    hs = np.concatenate([[0], np.cumsum(hhc)])
-    for t in range(H):
-        n = int(hhc[t])
-        hh[t, :n, 0] = hh_c[hs[t]:hs[t + 1]]
-        hh[t, :n, 1] = hh_v[hs[t]:hs[t + 1]].view(np.int32)
+        rec[b, REC_ROW:REC_ROW + ROWS_PER_BLOCK] = -1
+        rec[b, REC_ROW:REC_ROW + (r1 - r0)] = perm[r0:r1]
+        items = np.concatenate([np.arange(hstart[r], hstart[r + 1]) for r in perm[r0:r1]]).astype(np.int64)
+        rec[b, REC_HEAD:REC_HEAD + 2 * len(items):2] = hcols[items]
+        rec[b, REC_HEAD + 1:REC_HEAD + 2 * len(items):2] = hvals[items].view(np.int32)
     dev = adj.device
     f = HubFactor()
-    f.hh = torch.from_numpy(hh).to(dev)
-    f.hhl = hhl
     f.nblk = nblk
-    f.first_block = int(hubs.min()) // ROWS_PER_BLOCK   # dispatched first (csrc/factor.hip)
     f.M, f.H, f.k0, f.Kc = M, H, k0, Kc
     f.hubs = torch.from_numpy(hubs.astype(np.int64)).to(dev)
-    f.hubs32 = torch.from_numpy(hubs.astype(np.int32)).to(dev)
+    f.perm = torch.from_numpy(perm.astype(np.int64))            # host: tests and tools
     f.U = torch.from_numpy(U.astype(np.float32)).to(dev)
     f.rec = torch.from_numpy(rec).to(dev)
     f.rec_words = rec_words

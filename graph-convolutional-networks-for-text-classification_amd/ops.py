@@ -213,19 +213,14 @@ def spmm_proj(a, B, W, bias=None, epilogue=_lib.EPI_NONE, mask=None, scale=1.0, 
 # (A-hat, X) pair has the doc-topic structure; GCNK_FACTOR_GC1=0 forces the
 # SpMM path (experiments, A/B timing).
 FACTOR_GC1 = os.environ.get("GCNK_FACTOR_GC1", "1") != "0"
-# gc1 also pushes each block's share of gc2's hub rows (partials) and gc2 runs
-# as one hubfactor_gc2 launch; off: gc2 through spmm_sum (the row kernel).  R8:
-# push + gc2 11.48 + 4.56 us against 9.92 + 4.84 without (profiles/r03_factor.md)
-FACTOR_PUSH = os.environ.get("GCNK_FACTOR_PUSH", "0") != "0"
 
 
 def hubfactor_gc1(f, W1, b1, W2, epilogue=_lib.EPI_BIAS_RELU, mask=None, scale=1.0, keep_prob=1.0, seed=0,
                   offset=0, rng_base=None, store_h1=True):
-    """(H1, S2, S2T) of gc1 + gc2's support through the hub factorisation ``f``
+    """(H1, S2) of gc1 + gc2's support through the hub factorisation ``f``
     (factor.HubFactor): S_T = X[hubs] W1 (layer.py:102, the tile GEMM), then
     one launch of gcnk_hubfactor_gc1_f32 -- H1 = drop(relu(A-hat X W1 + b1))
-    (layer.py:106,110,182,185) and S2 = H1 W2 (layer.py:102, gc2), S2T = S2's
-    hub rows (compact, for hubfactor_gc2).  Returns
+    (layer.py:106,110,182,185) and S2 = H1 W2 (layer.py:102, gc2).  Returns
     None when the shapes are outside the kernel's range (the caller takes the
     SpMM path)."""
     W1 = _dense_f32(W1, "gc1 weight")
@@ -244,9 +239,6 @@ def hubfactor_gc1(f, W1, b1, W2, epilogue=_lib.EPI_BIAS_RELU, mask=None, scale=1
     S = f.hub_times(W1).contiguous()
     H1 = torch.empty((M, F), dtype=torch.float32, device=W1.device) if store_h1 else None
     S2 = torch.empty((M, P), dtype=torch.float32, device=W1.device)
-    S2T = torch.empty((f.H, P), dtype=torch.float32, device=W1.device)   # S2's hub rows for gc2
-    part = torch.empty((f.nblk, f.H, P), dtype=torch.float32, device=W1.device) \
-        if FACTOR_PUSH and P % 4 == 0 else None
     if b1 is not None:
         b1 = b1.contiguous()
     if mask is not None:
@@ -257,37 +249,11 @@ def hubfactor_gc1(f, W1, b1, W2, epilogue=_lib.EPI_BIAS_RELU, mask=None, scale=1
             _ptr(f.rec), f.rec_words, _ptr(b1), epilogue,
             _ptr(mask), mask.stride(0) if mask is not None else 0, float(scale),
             float(keep_prob), int(seed) & (2**64 - 1), int(offset) & (2**64 - 1), _ptr(rng_base),
-            _ptr(W2), W2.stride(0), _ptr(H1), F, _ptr(S2), P, _ptr(S2T), _ptr(part), f.first_block,
-            _stream(W1.device))
+            _ptr(W2), W2.stride(0), _ptr(H1), F, _ptr(S2), P, _stream(W1.device))
     if rc == _lib.EUNSUP:
         return None
     _lib.check(rc, "gcnk_hubfactor_gc1_f32")
-    return H1, S2, (S2T, part)
-
-
-def hubfactor_gc2(f, S2, side, b2):
-    """gc2's ``th.spmm(adj, support) + b2`` (reference layer.py:106,110) on the
-    factored graph ``f``: light rows from their diagonal and hub nonzeros
-    (S2's hub rows staged once per block), hub rows from the per-block
-    partials gc1 pushed and their hub x hub nonzeros (gcnk_hubfactor_gc2_f32,
-    one launch, no heavy-row gather).  ``side`` = (S2T, partials) from
-    hubfactor_gc1.  None when the shape is outside the kernel's range (the
-    caller takes spmm_sum)."""
-    S2T, part = side
-    M, P = S2.shape
-    if part is None or P % 4 or P > 16 or not S2.is_contiguous():
-        return None
-    out = torch.empty((M, P), dtype=torch.float32, device=S2.device)
-    if b2 is not None:
-        b2 = b2.contiguous()
-    with torch.cuda.device(S2.device):
-        rc = _lib.load().gcnk_hubfactor_gc2_f32(M, P, f.H, _ptr(f.rec), f.rec_words, _ptr(part), _ptr(f.hh), f.hhl,
-                                                _ptr(f.hubs32), _ptr(S2), _ptr(S2T), _ptr(b2), _ptr(out), P,
-                                                _stream(S2.device))
-    if rc == _lib.EUNSUP:
-        return None
-    _lib.check(rc, "gcnk_hubfactor_gc2_f32")
-    return out
+    return H1, S2
 
 
 def spmm_sum(a, Bs, bias=None, epilogue=_lib.EPI_NONE, out=None, lanes=0):
@@ -538,8 +504,7 @@ class GCNFn(torch.autograd.Function):
                                 offset=offset, rng_base=rng_base, store_h1=keep_h1)
         out = None
         if res is not None:
-            H1, S2, side = res
-            out = hubfactor_gc2(fac, S2, side, b2)
+            H1, S2 = res
         elif FUSE_PROJECTION and W2.shape[1] <= FUSE_MAX_P:
             S1 = xop.times(W1)
             H1, S2 = spmm_proj(adj, S1, W2, bias=b1, epilogue=epi, mask=mask, scale=scale, keep_prob=keep,

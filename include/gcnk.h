@@ -50,7 +50,7 @@
 extern "C" {
 #endif
 
-#define GCNK_ABI_VERSION 6
+#define GCNK_ABI_VERSION 7
 
 #define GCNK_OK 0
 #define GCNK_EARG (-1)
@@ -311,21 +311,17 @@ int gcnk_gcn_bwd2_f32(const float* H, int64_t ldh, const float* gS, int64_t ldgs
  * layer.py:102,106,110,182,185 and gc2's support layer.py:102) for a graph
  * whose rows split into hub rows and light rows referencing only hub columns
  * and themselves, with X's light rows inside the column range [k0, k0 + Kc):
- *   Z[r, :]   = U[r, :Kc] . W[k0 .. k0+Kc-1, :] + sum_{items of r} val * S[hub, :]
+ *   Z[r, :]   = U[i, :Kc] . W[k0 .. k0+Kc-1, :] + sum_{items of r} val * S[hub, :]
  *   H[r, n]   = epilogue(Z[r, n] + bias[n])            (GCNK_EPI_*, as the SpMM)
  *   C2[r, p]  = sum_n H[r, n] W2[n, p]                 (P <= 16)
- * U [M x Kc] (ldu >= Kc rounded up to 4, zero past Kc), S = X[hubs] W
- * [nhub x F] (lds), rec = one record of rec_words int32 per 32-row block:
- * 33 row offsets (block-relative item index), the push-section offset, 2 pad
- * words, 32 hub indices (-1 for a light row), 32 diagonal values (bits), the
- * items int2 {hub index, value bits}, then the push section (hub-row share of
- * the block's light columns, see gcnk_hubfactor_gc2_f32).  H nullable (not
- * stored); C2T nullable: the hub rows of C2, compact [nhub x P]; part nullable:
- * [ceil(M/32)][nhub][P] hub-row partials of gc2 (both for
- * gcnk_hubfactor_gc2_f32).  Workgroup 0 takes block first_block, the rest follow
- * cyclically (give it the hub rows' block: the longest item lists start first).
- * F % 4 == 0, F <= 256, Kc <= 128; GCNK_EUNSUP when the block's operands exceed
- * 160 KiB of LDS (gcnk_hubfactor_lds_bytes).  One launch, fixed-order sums.
+ * for r = the row id at position i of the block order.  U [M x Kc] in block
+ * order (ldu >= Kc rounded up to 4, zero past Kc), S = X[hubs] W [nhub x F]
+ * (lds), rec = one record of rec_words int32 per 32-row block: 33 offsets
+ * (block-relative item index), 3 pad words, 32 row ids (the output rows of the
+ * block's positions, -1 past M), then items int2 {hub index, value bits}.  H
+ * nullable (not stored).  F % 4 == 0, F <= 256, Kc <= 128; GCNK_EUNSUP when
+ * the block's operands exceed 160 KiB of LDS (gcnk_hubfactor_lds_bytes).  One
+ * launch, fixed-order sums.
  * ------------------------------------------------------------------------- */
 int64_t gcnk_hubfactor_lds_bytes(int32_t F, int32_t Kc, int32_t nhub, int32_t rec_words);
 int gcnk_hubfactor_gc1_f32(int32_t M, int32_t F, int32_t Kc, int32_t nhub, int32_t P, const float* U, int64_t ldu,
@@ -333,21 +329,7 @@ int gcnk_hubfactor_gc1_f32(int32_t M, int32_t F, int32_t Kc, int32_t nhub, int32
                            const int32_t* rec, int32_t rec_words, const float* bias, int32_t epilogue,
                            const uint8_t* drop_mask, int64_t ldm, float drop_scale, float keep_prob, uint64_t seed,
                            uint64_t offset, const uint64_t* rng_base, const float* W2, int64_t ldw2, float* H,
-                           int64_t ldh, float* C2, int64_t ldc2, float* C2T, float* part, int32_t first_block,
-                           void* stream);
-/* gc2 of the factored pair: out = A-hat C2 + bias (layer.py:106,110 of gc2), C2
- * [M x P] (P % 4 == 0, P <= 16, contiguous), its hub rows C2T [nhub x P] and
- * the hub-row partials part [ceil(M/32)][nhub][P] from gcnk_hubfactor_gc1_f32
- * (C2T and part non-null there: each 32-row block adds its light rows' share
- * of every hub row, the record's push section).  Light rows from the block
- * records (diagonal in the record head); hub row t = sum of its partials in
- * block order + its hub x hub nonzeros hh [nhub x hhl] {hub index, value bits}
- * (value 0 past the row); hub_rows[t] its row index.  One launch, fixed-order
- * sums. */
-int gcnk_hubfactor_gc2_f32(int32_t M, int32_t P, int32_t nhub, const int32_t* rec, int32_t rec_words,
-                           const float* part, const int32_t* hh, int32_t hhl, const int32_t* hub_rows,
-                           const float* S2, const float* S2T, const float* bias, float* out, int64_t ldo,
-                           void* stream);
+                           int64_t ldh, float* C2, int64_t ldc2, void* stream);
 
 /* ---------------------------------------------------------------------------
  * Sparse-format helpers (one-time graph preparation, utils.py:185-213,

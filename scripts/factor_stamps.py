@@ -29,8 +29,7 @@ def main():
         ops.hubfactor_gc1(f, W1, b1, W2, store_h1=False)
     torch.cuda.synchronize()
     buf = torch.zeros(4 * 4096, dtype=torch.int64, device=dev)
-    for rep in range(6):
-        ops.FACTOR_PUSH = rep >= 3   # last three: with gc2's hub-row push (exit stamp after it)
+    for rep in range(4):
         S = f.hub_times(W1s[rep + 1])
         torch.cuda.synchronize()
         buf.zero_()
@@ -44,7 +43,7 @@ def main():
         rel = (s - t0) / 100.0
         q = lambda x: [round(float(np.percentile(x, p)), 2) for p in (0, 10, 50, 90, 100)]  # noqa: E731
         worst = int(np.argmax(rel[:, 3]))
-        print(json.dumps({"rep": rep, "push": ops.FACTOR_PUSH, "blocks": len(s), "staged": q(rel[:, 0]), "mfma": q(rel[:, 1] - rel[:, 0]),
+        print(json.dumps({"rep": rep, "blocks": len(s), "staged": q(rel[:, 0]), "mfma": q(rel[:, 1] - rel[:, 0]),
                           "epilogue": q(rel[:, 2] - rel[:, 1]), "projection": q(rel[:, 3] - rel[:, 2]),
                           "exit": q(rel[:, 3]), "slowest_block": worst, "slowest": rel[worst].round(2).tolist()}),
               flush=True)

@@ -44,54 +44,36 @@ def _check_factor(A, X, F=24, seed=0):
     ref = Af @ (Xf @ W1)
     U = f.U.numpy().astype(np.float64)
     hubs = f.hubs.numpy()
+    perm = f.perm.numpy()
     S_T = Xf[hubs] @ W1
-    Z = U[:, :f.Kc] @ W1[f.k0:f.k0 + f.Kc]
+    Z = U[:, :f.Kc] @ W1[f.k0:f.k0 + f.Kc]          # block order: position i holds row perm[i]
     rec = f.rec.numpy()
     M = A.shape[0]
+    assert np.array_equal(np.sort(perm), np.arange(M))
     nnz_h = 0
     for b in range(rec.shape[0]):
         off = rec[b, :33]
         items = rec[b, factor.REC_HEAD:].reshape(-1, 2)
-        for i in range(min(32, M - 32 * b)):
-            r = 32 * b + i
+        for i in range(32):
+            p = 32 * b + i
+            assert rec[b, factor.REC_ROW + i] == (perm[p] if p < M else -1)
+            if p >= M:
+                continue
             for k in range(off[i], off[i + 1]):
                 t, bits = items[k]
-                Z[r] += np.int32(bits).view(np.float32) * S_T[t]
+                Z[p] += np.int32(bits).view(np.float32) * S_T[t]
                 nnz_h += 1
     # exactly the hub-column nonzeros of A-hat, each once
     is_hub = np.zeros(M, bool)
     is_hub[hubs] = True
     assert nnz_h == int(is_hub[A.indices].sum())
-    err = np.abs(Z - ref).max() / max(1.0, np.abs(ref).max())
+    err = np.abs(Z - ref[perm]).max() / max(1.0, np.abs(ref).max())
     assert err < 1e-6, err
-    # per-row hub index and diagonal in the record head; gc2's hub item lists
-    for b in range(rec.shape[0]):
-        for i in range(min(32, M - 32 * b)):
-            r = 32 * b + i
-            hi = rec[b, factor.REC_HUB + i]
-            assert hi == (int(np.flatnonzero(hubs == r)[0]) if is_hub[r] else -1)
-            assert np.int32(rec[b, factor.REC_DIAG + i]).view(np.float32) == np.float32(A[r, r])
-    # push sections: per block, hub t's light columns in the block with A[t, d];
-    # with the hub x hub lists they rebuild every hub row of A-hat exactly
-    S = np.random.default_rng(seed + 1).standard_normal((M, 8))
-    ref2 = Af @ S
-    hh = f.hh.numpy()
-    got2 = np.zeros((f.H, 8))
-    for b in range(rec.shape[0]):
-        po = rec[b, factor.REC_PUSH]
-        pi = (po + f.H + 1 + 3) // 4 * 4
-        poff = rec[b, po:po + f.H + 1]
-        items = rec[b, pi:].reshape(-1, 2)
-        for t in range(f.H):
-            for k in range(poff[t], poff[t + 1]):
-                row, bits = items[k]
-                assert not is_hub[32 * b + row]
-                got2[t] += np.int32(bits).view(np.float32) * S[32 * b + row]
-    for t in range(f.H):
-        for k in range(hh.shape[1]):
-            tt, bits = hh[t, k]
-            got2[t] += np.int32(bits).view(np.float32) * S[hubs[tt]]
-    assert np.abs(got2 - ref2[hubs]).max() < 1e-9 * max(1.0, np.abs(ref2).max())
+    # hub rows spread: no block holds more than ceil(H / nblk) + 1 of them
+    pos = np.empty(M, np.int64)
+    pos[perm] = np.arange(M)
+    per_block = np.bincount(pos[hubs] // 32, minlength=rec.shape[0])
+    assert per_block.max() <= -(-len(hubs) // rec.shape[0]) + 1, per_block.max()
     return f
 
 
@@ -141,9 +123,10 @@ def test_factor_dense_features():
     W1 = rng.standard_normal((100, 8))
     hubs = f.hubs.numpy()
     ref = A @ (X.astype(np.float64) @ W1)
-    Z = f.U.numpy()[:, :100].astype(np.float64) @ W1
+    perm = f.perm.numpy()
+    Z = f.U.numpy()[:, :100].astype(np.float64) @ W1       # rows in the block order
     Zh = A[:, hubs] @ (X[hubs].astype(np.float64) @ W1)
-    assert np.abs(Z + Zh - ref).max() < 1e-5 * max(1, np.abs(ref).max())
+    assert np.abs(Z + Zh[perm] - ref[perm]).max() < 1e-5 * max(1, np.abs(ref).max())
 
 
 def test_factor_refuses_unstructured_graph():

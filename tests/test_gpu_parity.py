@@ -1211,9 +1211,9 @@ def test_factored_gc1_matches_spmm_path(r8, mode):
     f = factor.get(as_csr(A), ops.Operand(X))
     assert f is not None and f.H == 50 and f.Kc == 50
     outs = {}
-    for fac, push in ((True, True), (True, False), (False, False)):
-        saved = ops.FACTOR_GC1, ops.FACTOR_PUSH
-        ops.FACTOR_GC1, ops.FACTOR_PUSH = fac, push
+    for fac in (True, False):
+        saved = ops.FACTOR_GC1
+        ops.FACTOR_GC1 = fac
         try:
             torch.manual_seed(123)
             m = GCN(nfeat=r8["nfeat"], nhid=200, nclass=r8["nclass"], dropout=0.5,
@@ -1225,33 +1225,32 @@ def test_factored_gc1_matches_spmm_path(r8, mode):
                 again = m(X, A)
                 assert torch.equal(lg, again)
             lg.square().sum().backward()
-            outs[fac, push] = (lg.detach().cpu().numpy(),
-                               {k: p.grad.cpu().numpy() for k, p in m.named_parameters()})
+            outs[fac] = (lg.detach().cpu().numpy(), {k: p.grad.cpu().numpy() for k, p in m.named_parameters()})
         finally:
-            ops.FACTOR_GC1, ops.FACTOR_PUSH = saved
-    lb, gb = outs[False, False]
+            ops.FACTOR_GC1 = saved
+    (la, ga), (lb, gb) = outs[True], outs[False]
     scale = max(1.0, float(np.abs(lb).max()))
-    for push in (True, False):   # gc2 as hubfactor_gc2 (hub-row push) and as spmm_sum
-        la, ga = outs[True, push]
-        assert np.abs(la - lb).max() <= 1e-5 * scale, (push, float(np.abs(la - lb).max()))
-        for k in ga:
-            np.testing.assert_allclose(ga[k], gb[k], rtol=1e-4, atol=1e-5 * max(1.0, float(np.abs(gb[k]).max())),
-                                       err_msg=f"{k} push={push}")
+    assert np.abs(la - lb).max() <= 1e-5 * scale, float(np.abs(la - lb).max())
+    for k in ga:
+        np.testing.assert_allclose(ga[k], gb[k], rtol=1e-4, atol=1e-5 * max(1.0, float(np.abs(gb[k]).max())),
+                                   err_msg=k)
 
 
-def test_factored_gc1_kernel_against_float64(monkeypatch):
+def test_factored_gc1_kernel_against_float64():
     """gcnk_hubfactor_gc1_f32 alone on a synthetic doc-topic graph with hub x
     hub nonzeros, F not a multiple of 16, P = 3 and H1 stored: H1 and
-    S2 = H1 W2 against float64 (every epilogue code but the dropout ones)."""
+    S2 = H1 W2 against float64 (every epilogue code but the dropout ones),
+    rows written through the block order's row ids (hub rows spread over the
+    blocks, factor.py)."""
     import scipy.sparse as ssp
     from graph_convolutional_networks_for_text_classification_amd import factor, ops
     from graph_convolutional_networks_for_text_classification_amd.sparse import as_csr
-    monkeypatch.setattr(ops, "FACTOR_PUSH", True)   # gc2 needs the partials the push writes
     g = datasets.doc_topic_graph(2000, 40, 5, seed=4, tt_prob=0.3)
     A, X = g["adj"].to(DEV), g["features"].to(DEV)
     xop = ops.Operand(X)
     f = factor.get(as_csr(A), xop)
     assert f is not None
+    assert not np.array_equal(f.perm.numpy(), np.arange(f.M))   # the hub rows moved
     rng = np.random.default_rng(3)
     F, P = 52, 3
     W1 = torch.from_numpy(rng.standard_normal((g["nfeat"], F)).astype(np.float32)).to(DEV)
@@ -1263,21 +1262,11 @@ def test_factored_gc1_kernel_against_float64(monkeypatch):
     Xd = ssp.csr_matrix((x.values().double().numpy(), x.indices().numpy()), shape=tuple(x.shape))
     Z = Ad @ (Xd @ W1.cpu().double().numpy())
     for epi in (_lib.EPI_NONE, _lib.EPI_BIAS, _lib.EPI_BIAS_RELU):
-        H1, S2, _ = ops.hubfactor_gc1(f, W1, b1, W2, epilogue=epi)
+        H1, S2 = ops.hubfactor_gc1(f, W1, b1, W2, epilogue=epi)
         want = Z if epi == _lib.EPI_NONE else Z + b1.cpu().double().numpy()
         if epi == _lib.EPI_BIAS_RELU:
             want = np.maximum(want, 0.0)
         _close(H1, want, atol=2e-5 * max(1.0, np.abs(want).max()))
         _close(S2, H1.cpu().double().numpy() @ W2.cpu().double().numpy(), atol=2e-5 * max(1.0, np.abs(want).max()))
-    H1b, S2b, sideb = ops.hubfactor_gc1(f, W1, b1, W2, epilogue=_lib.EPI_BIAS_RELU, store_h1=False)
+    H1b, S2b = ops.hubfactor_gc1(f, W1, b1, W2, epilogue=_lib.EPI_BIAS_RELU, store_h1=False)
     assert H1b is None and torch.equal(S2b, S2)
-    assert torch.equal(sideb[0], S2b[f.hubs]) and sideb[1] is None   # P = 3: no push
-    # gc2 (gcnk_hubfactor_gc2_f32; P = 3 is outside its range -> None) at P = 8
-    W2b = torch.from_numpy(rng.standard_normal((F, 8)).astype(np.float32)).to(DEV)
-    b2 = torch.from_numpy(rng.standard_normal(8).astype(np.float32)).to(DEV)
-    assert ops.hubfactor_gc2(f, S2b, sideb, b2) is None
-    H1c, S2c, sidec = ops.hubfactor_gc1(f, W1, b1, W2b, epilogue=_lib.EPI_BIAS_RELU)
-    Z2 = ops.hubfactor_gc2(f, S2c, sidec, b2)
-    want2 = Ad @ S2c.cpu().double().numpy() + b2.cpu().double().numpy()
-    _close(Z2, want2, atol=2e-5 * max(1.0, np.abs(want2).max()))
-    assert torch.equal(Z2, ops.hubfactor_gc2(f, S2c, sidec, b2))

@@ -1270,3 +1270,45 @@ def test_factored_gc1_kernel_against_float64():
         _close(S2, H1.cpu().double().numpy() @ W2.cpu().double().numpy(), atol=2e-5 * max(1.0, np.abs(want).max()))
     H1b, S2b = ops.hubfactor_gc1(f, W1, b1, W2, epilogue=_lib.EPI_BIAS_RELU, store_h1=False)
     assert H1b is None and torch.equal(S2b, S2)
+
+
+@pytest.mark.parametrize("mode", ["eval", "train_hash"])
+def test_factored_forward_hub_rows_first_ragged(mode):
+    """The factored forward on a synthetic doc-topic graph renumbered so the
+    topic (hub) rows come FIRST, with M = 1,038 (not a multiple of the 32-row
+    block) and the gensim-shaped dense X (its hub rows through the dense GEMM):
+    logits and gradients against the SpMM path (ops.FACTOR_GC1 = False)."""
+    from graph_convolutional_networks_for_text_classification_amd import factor, ops
+    from graph_convolutional_networks_for_text_classification_amd.sparse import as_csr
+    g = datasets.doc_topic_graph(1001, 37, 5, seed=11)
+    n, ndoc = g["nodes"], 1001
+    order = np.concatenate([np.arange(ndoc, n), np.arange(ndoc)])     # new position -> old node
+    inv = np.empty(n, np.int64)
+    inv[order] = np.arange(n)
+    a = g["adj"].coalesce()
+    idx = torch.from_numpy(inv)[a.indices()]
+    A = torch.sparse_coo_tensor(idx, a.values(), (n, n)).coalesce().to(DEV)
+    X = datasets.dense_to_coo(g["features_dense"][order]).to(DEV)
+    xop = ops.Operand(X)
+    f = factor.get(as_csr(A), xop)
+    assert f is not None and f.hubs.cpu().tolist() == list(range(37)) and f.M % 32 != 0
+    outs = {}
+    for fac in (True, False):
+        saved = ops.FACTOR_GC1
+        ops.FACTOR_GC1 = fac
+        try:
+            torch.manual_seed(5)
+            m = GCN(nfeat=g["nfeat"], nhid=200, nclass=g["nclass"], dropout=0.5,
+                    dropout_rng="device").to(DEV)
+            m.train(mode != "eval")
+            lg = m(X, A)
+            lg.square().sum().backward()
+            outs[fac] = (lg.detach().cpu().numpy(), {k: p.grad.cpu().numpy() for k, p in m.named_parameters()})
+        finally:
+            ops.FACTOR_GC1 = saved
+    (la, ga), (lb, gb) = outs[True], outs[False]
+    scale = max(1.0, float(np.abs(lb).max()))
+    assert np.abs(la - lb).max() <= 1e-5 * scale, float(np.abs(la - lb).max())
+    for k in ga:
+        np.testing.assert_allclose(ga[k], gb[k], rtol=1e-4, atol=1e-5 * max(1.0, float(np.abs(gb[k]).max())),
+                                   err_msg=k)

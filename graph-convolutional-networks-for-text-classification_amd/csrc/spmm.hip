@@ -50,9 +50,12 @@ constexpr int32_t kMagic = 0x474e4b35;  // "GNK5"
 constexpr int kRB = 64;                 // tile rows per dense block (4 waves x 16)
 constexpr int kKC = 64;                 // condensed columns per tile chunk (16 MFMA k-steps)
 #ifndef GCNK_TILE_MAXNT
-#define GCNK_TILE_MAXNT 8
+#define GCNK_TILE_MAXNT 4
 #endif
-constexpr int kMaxNT = GCNK_TILE_MAXNT;  // 16-column MFMA n-tiles per tile workgroup (8: B tile 48 KB LDS, 2+ per CU)
+// 16-column MFMA n-tiles per tile workgroup.  4 (R8 F = 200: 4 slices, 484
+// workgroups for X_hubs W1): tile 6.8 us against 7.3 with 8 and 7.5 with 1, the
+// forward 0.5-1 us shorter, factored or not (profiles/r03_tile_nt.log)
+constexpr int kMaxNT = GCNK_TILE_MAXNT;
 constexpr int kMaxColTiles = 64;        // row-kernel column tiles per launch (arrival counters per heavy row)
 constexpr int kMaxSeg = 64;             // segments per heavy row (bounds the last arriver's combine)
 // Schedule knobs of the whole-wavefront (F > 128) row kernel, overridable at
@@ -1909,7 +1912,7 @@ static int spmm_impl(const void* plan, const int32_t* hdr, const float* B, int64
   // ---- dense blocks: tile kernel (+ slab reduce)
   const float* dval = L.has_diag ? reinterpret_cast<const float*>(p + L.dval) : nullptr;
   if (L.ntile > 0) {
-    // column slices of <= kMaxNT n-tiles on grid.y, balanced (F = 200: 2 x 7 n-tiles),
+    // column slices of <= kMaxNT n-tiles on grid.y, balanced (F = 200: 4 x 4 n-tiles),
     // so two workgroups of a chunk share the staging/MFMA/store phases of a CU
     const int32_t nt_total = (int32_t)(slab_ld / 16);
     const int32_t nslices = (nt_total + kMaxNT - 1) / kMaxNT;

@@ -31,7 +31,7 @@ def _resolve_lib():
 
 
 LIB_PATH = _resolve_lib()
-ABI_VERSION = 7
+ABI_VERSION = 8
 
 # C-ABI return codes (gcnk.h)
 OK, EARG, EUNSUP, EHIP = 0, -1, -2, -3
@@ -146,7 +146,11 @@ SIGNATURES = {
         _f32, _u64, _u64, _vp,            # keep_prob, seed, offset, rng_base
         _vp, _i64, _vp, _i64, _vp, _i64,  # W2, ldw2, H, ldh, C2, ldc2
         _vp]),                            # stream
- # S2, S2T, bias, out, ldo, stream
+    # record (host struct gcnk_gcn_fwd), W1, b1, W2, b2, out, ldo, H1, ldh, epilogue, mask, ldm, scale,
+    # keep_prob, seed, offset, rng_base, stream
+    "gcnk_gcn_forward_f32": (ctypes.c_int, [_vp, _vp, _vp, _vp, _vp, _vp, _i64, _vp, _i64, _i32, _vp, _i64, _f32,
+                                            _f32, _u64, _u64, _vp, _vp]),
+    "gcnk_gcn_fwd_layout": (_i32, [_vp, _i32]),
     "gcnk_class_stats": (ctypes.c_int, [_vp, _i64, _vp, _vp, _i64, _i32, _vp, _vp]),
     "gcnk_edgelist_size": (ctypes.c_int, [ctypes.c_char_p, _vp, _vp]),
     "gcnk_edgelist_csr": (ctypes.c_int, [ctypes.c_char_p, _i64, _i64, _vp, _vp, _vp]),

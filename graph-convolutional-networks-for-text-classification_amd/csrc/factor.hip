@@ -42,7 +42,9 @@ constexpr int kRB = 32;         // rows per workgroup
 constexpr int kThreads = 512;   // 8 waves: 2 row strips x 4 column quarters
 constexpr int kMaxKsteps = 32;  // Kc <= 128
 constexpr int kProjW = 16;      // projection width (one MFMA n-tile): P <= 16
-constexpr int kBPad = 64;       // zero floats after the staged W1[Kc] (tiles past F read them)
+// zero floats after the staged W1[Kc]: the n-tiles past F read up to column
+// 64 NTQ - 1 of the last k-row, so the pad covers 64 NTQ - F of them (at least 64)
+__host__ __device__ constexpr int bpad(int f, int ntq) { return 64 * ntq - f > 64 ? 64 * ntq - f : 64; }
 // block record (factor.py): 33 row offsets, 3 pad | 32 row ids (-1 past M) |
 // A_H items int2 {hub, value}.  Block b holds rows perm[32 b .. 32 b + 31]: the
 // host spreads the hub rows (long item lists) over the blocks, U's rows are in
@@ -51,7 +53,7 @@ constexpr int kRecRow = 36, kRecHead = 68;
 // compile-time shapes (every MFMA unconditional, operands in fixed registers):
 // KS k-steps of U W1[Kc] (Kc <= 4 KS; U columns past Kc read as zero, W1 rows
 // past Kc staged as zero) and NTQ 16-column tiles per quarter of F (F <= 64 NTQ;
-// columns past F are computed from finite LDS words and never used)
+// columns past F are computed from zeroed or W1 LDS words and never used)
 __host__ __device__ constexpr int pick_ks(int kc) { return kc <= 52 ? 13 : kc <= 100 ? 25 : 32; }
 __host__ __device__ constexpr int pick_ntq(int f) { return f <= 128 ? 2 : f <= 192 ? 3 : 4; }
 
@@ -69,7 +71,7 @@ struct FactorArgs {
 
 template <int KS>
 __host__ __device__ constexpr int region1_floats(int F, int ntq) {
-  return (4 * KS * F + kBPad) > kRB * (64 * ntq + 4) ? (4 * KS * F + kBPad) : kRB * (64 * ntq + 4);
+  return (4 * KS * F + bpad(F, ntq)) > kRB * (64 * ntq + 4) ? (4 * KS * F + bpad(F, ntq)) : kRB * (64 * ntq + 4);
 }
 
 template <int KS, int NTQ>
@@ -84,7 +86,7 @@ hubfactor_gc1_kernel(FactorArgs a) {
   constexpr int Kr = 4 * KS;
   const int blk = (int)blockIdx.x;
   const int64_t m0 = (int64_t)blk * kRB;  // position in the block order (U's rows)
-  // LDS: region1 = s_B [Kr][F] + kBPad zeros (phase 1), then s_Z [kRB][Fz]
+  // LDS: region1 = s_B [Kr][F] + bpad zeros (phase 1), then s_Z [kRB][Fz]
   //      | s_S [nhub][F] | s_W2 [F][P] | s_bias [F] | s_rec | s_red [3][2][64][4]
   // Every global operand is staged here in the one round of loads that opens the
   // kernel: a global load behind an LDS-read index costs a full memory round trip
@@ -102,7 +104,7 @@ hubfactor_gc1_kernel(FactorArgs a) {
   // ---- 0. loads, all issued before the first wait: zeros first (no LDS-DMA in
   //      flight yet), then LDS-DMA of W1[Kc] (flat) and the block's record, the
   //      U fragments straight into registers
-  for (int e = a.Kc * F + tid; e < Kr * F + kBPad; e += kThreads) s_B[e] = 0.f;
+  for (int e = a.Kc * F + tid; e < Kr * F + bpad(F, NTQ); e += kThreads) s_B[e] = 0.f;
   if (!a.epi.bias)
     for (int e = tid; e < F; e += kThreads) s_bias[e] = 0.f;
   {
@@ -252,13 +254,25 @@ using namespace gcnk;
 
 static int64_t hubfactor_lds_bytes(int32_t F, int32_t Kc, int32_t nhub, int32_t rec_words, int32_t P = kProjW) {
   const int64_t Fz = 64 * pick_ntq(F) + 4, Kr = 4 * pick_ks(Kc);
-  const int64_t r1 = std::max<int64_t>(Kr * F + kBPad, (int64_t)kRB * Fz);
+  const int64_t r1 = std::max<int64_t>(Kr * F + bpad(F, pick_ntq(F)), (int64_t)kRB * Fz);
   return 4 * (r1 + (int64_t)nhub * F + (((int64_t)F * P + 3) & ~3LL) + F + rec_words + 3 * 2 * 64 * 4);
 }
 
 extern "C" int64_t gcnk_hubfactor_lds_bytes(int32_t F, int32_t Kc, int32_t nhub, int32_t rec_words) {
   if (F <= 0 || Kc <= 0 || nhub <= 0 || rec_words < kRecHead) return GCNK_EARG;
   return hubfactor_lds_bytes(F, Kc, nhub, rec_words);
+}
+
+// The dynamic-LDS limit is raised once per kernel instantiation (a driver call
+// per launch cost host time on every eager forward), then the launch.
+template <int KS, int NTQ>
+static int launch_factor(const FactorArgs& a, int64_t nblk, int64_t lds_b, void* stream) {
+  static const hipError_t attr = hipFuncSetAttribute(reinterpret_cast<const void*>(&hubfactor_gc1_kernel<KS, NTQ>),
+                                                     hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
+  if (attr != hipSuccess) return hip_check(attr, "hubfactor_gc1_kernel LDS attribute");
+  hipLaunchKernelGGL((hubfactor_gc1_kernel<KS, NTQ>), dim3((unsigned)nblk), dim3(kThreads), (size_t)lds_b,
+                     reinterpret_cast<hipStream_t>(stream), a);
+  return launch_check("hubfactor_gc1_kernel");
 }
 
 extern "C" int gcnk_hubfactor_gc1_f32(int32_t M, int32_t F, int32_t Kc, int32_t nhub, int32_t P, const float* U,
@@ -305,17 +319,8 @@ extern "C" int gcnk_hubfactor_gc1_f32(int32_t M, int32_t F, int32_t Kc, int32_t 
   e.ldm = epilogue == GCNK_EPI_BIAS_RELU_HASH ? (ldm > 0 ? ldm : F) : ldm;
   const int64_t nblk = ((int64_t)M + kRB - 1) / kRB;
   const int ks = pick_ks(Kc), ntq = pick_ntq(F);
-  auto go = [&](auto kern) {
-    static_cast<void>(0);
-    const hipError_t attr = hipFuncSetAttribute(reinterpret_cast<const void*>(kern),
-                                                hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
-    if (attr != hipSuccess) return hip_check(attr, "hubfactor_gc1_kernel LDS attribute");
-    hipLaunchKernelGGL(kern, dim3((unsigned)nblk), dim3(kThreads), (size_t)lds_b, reinterpret_cast<hipStream_t>(stream),
-                       a);
-    return launch_check("hubfactor_gc1_kernel");
-  };
 #define GCNK_FACTOR_CASE(KS_, NTQ_) \
-  if (ks == KS_ && ntq == NTQ_) return go(&hubfactor_gc1_kernel<KS_, NTQ_>);
+  if (ks == KS_ && ntq == NTQ_) return launch_factor<KS_, NTQ_>(a, nblk, lds_b, stream);
   GCNK_FACTOR_CASE(13, 2) GCNK_FACTOR_CASE(13, 3) GCNK_FACTOR_CASE(13, 4)
   GCNK_FACTOR_CASE(25, 2) GCNK_FACTOR_CASE(25, 3) GCNK_FACTOR_CASE(25, 4)
   GCNK_FACTOR_CASE(32, 2) GCNK_FACTOR_CASE(32, 3) GCNK_FACTOR_CASE(32, 4)

@@ -468,6 +468,12 @@ __device__ __forceinline__ void gather_rows_wave(const int2* __restrict__ items,
   for (int32_t base = b + q; base < e; base += 64 * S) {
     const int32_t k = base + S * lane;
     const int2 mine = k < e ? items[k] : make_int2(-1, 0);
+    // wait for the item words HERE, with the builtin the wait-count pass sees:
+    // otherwise it cannot prove on the paths that skip a conditional gather
+    // below that `mine` has landed, and puts a vmcnt(0) in front of EVERY
+    // readlane -- which also waits for the gathers already issued, so the
+    // batch of U gathers ran one at a time (ISA of round 3's kernel)
+    __builtin_amdgcn_s_waitcnt(0x0F70);  // vmcnt(0) expcnt(7) lgkmcnt(15)
     const int32_t cnt = min(64, (e - base + S - 1) / S);  // wave-uniform
     for (int32_t j0 = 0; j0 < cnt; j0 += U) {
       T g[U];

@@ -33,6 +33,7 @@ import torch
 from torch.nn import Module, Parameter
 
 from . import _lib
+from . import ops
 from .ops import GCNFn, GraphConvFn, Operand
 from .sparse import as_csr
 
@@ -180,6 +181,21 @@ def _host_keep_mask_locked(shape, p, n, pinned):
     return out
 
 
+def _aliases(t):
+    """The tensors whose version counters track in-place changes of t's data."""
+    if isinstance(t, torch.Tensor):
+        if t.layout == torch.sparse_coo:
+            return (t._indices(), t._values())
+        if t.layout == torch.sparse_csr:
+            return (t.crow_indices(), t.col_indices(), t.values())
+        return (t,)
+    return ()
+
+
+def _vkey(t, aliases):
+    return (getattr(t, "_version", None),) + tuple(p._version for p in aliases)
+
+
 class GraphConvolution(Module):
     """out = adj @ (infeatn @ weight) + bias   (reference layer.py:25-123)."""
 
@@ -226,6 +242,7 @@ class GCN(Module):
         self.dropout_rng = dropout_rng
         # hash-dropout stream position, read and advanced on the device (not in state_dict)
         self.register_buffer("_rng_base", torch.zeros(1, dtype=torch.int64), persistent=False)
+        self._memo = None   # (x, adj, version keys, Operand, CSR) of the last call
 
     def _dropout_args(self, nrows, device):
         """Epilogue code and mask/scale for layer.py:185 (ATen dropout semantics)."""
@@ -244,17 +261,37 @@ class GCN(Module):
         seed = int(torch.initial_seed()) & (2**64 - 1)
         return _lib.EPI_BIAS_RELU_HASH, None, scale, 1.0 - p, seed, 0
 
-    def forward(self, x, adj):
+    def _operands(self, x, adj):
+        """(Operand of x, CSR of adj), memoised for the inputs of the previous
+        call: the trainer passes the same two tensors every epoch
+        (trainer.py:357,382), and re-deriving the cache keys cost ~10 us."""
+        m = self._memo
+        if m is not None and m[0] is x and m[1] is adj and m[2] == _vkey(x, m[5]) and m[3] == _vkey(adj, m[6]):
+            return m[4], m[7]
         a = as_csr(adj)
         xop = Operand(x)
+        xa, aa = _aliases(x), _aliases(adj)
+        self._memo = (x, adj, _vkey(x, xa), _vkey(adj, aa), xop, xa, aa, a)
+        return xop, a
+
+    def forward(self, x, adj):
+        xop, a = self._operands(x, adj)
         epi, mask, scale, keep, seed, offset = self._dropout_args(a.shape[0], a.device)
+        W1, b1, W2, b2 = self.gc1.weight, self.gc1.bias, self.gc2.weight, self.gc2.bias
         # H1 is needed only by a backward pass; inference never writes it to HBM
-        keep_h1 = torch.is_grad_enabled() and any(p.requires_grad for p in self.parameters())
+        keep_h1 = torch.is_grad_enabled() and (W1.requires_grad or W2.requires_grad or
+                                               (b1 is not None and b1.requires_grad) or
+                                               (b2 is not None and b2.requires_grad))
         hashed = epi == _lib.EPI_BIAS_RELU_HASH
         if hashed and self._rng_base.device != a.device:
             raise RuntimeError(f"GCN buffers are on {self._rng_base.device}, operands on {a.device}: call .to()")
-        out = GCNFn.apply(self.gc1.weight, self.gc1.bias, self.gc2.weight, self.gc2.bias, xop, a,
-                          epi, mask, scale, keep, seed, offset, keep_h1, self._rng_base if hashed else None)
+        rng = self._rng_base if hashed else None
+        out = None
+        if not keep_h1:   # inference (trainer.py:382 under no_grad): no autograd node, one C call
+            res = ops.record_forward(W1, b1, W2, b2, xop, a, epi, mask, scale, keep, seed, offset, False, rng)
+            out = res[0] if res is not None else None
+        if out is None:
+            out = GCNFn.apply(W1, b1, W2, b2, xop, a, epi, mask, scale, keep, seed, offset, keep_h1, rng)
         if hashed:   # the next call (or graph replay) draws the next rows*nhid hash positions
             self._rng_base.add_(a.shape[0] * self.gc1.out_features)
         return out

@@ -1,0 +1,202 @@
+"""Whole-forward launch records (gcnk_gcn_forward_f32, include/gcnk.h).
+
+The reference's trainer calls ``model.forward(features, adj)`` eagerly every
+epoch (trainer.py:357 train, trainer.py:382 eval).  Issued op by op, the
+forward's 4-5 launches each paid Python + ctypes marshalling, plan and
+workspace lookups and device guards: 76-92 us per forward for ~26 us of
+kernels (profiles/r03_eager_forward_host_profile.log).  A ForwardRecord holds,
+per (adjacency, features, widths, stream), every pointer that does not change
+between calls -- plans and their host headers, workspaces, counter regions,
+the factored operands and the intermediates S1 / S2 -- in a C struct, and one
+ctypes call issues the whole forward.  The launches, their arguments and their
+order are those of ops.GCNFn's per-op path, so results are bitwise the same.
+"""
+import ctypes
+import threading
+
+import torch
+
+from . import _lib, factor, ops
+from .sparse import DENSE_THRESHOLD
+
+_c = ctypes
+
+
+class PlanRef(_c.Structure):
+    """gcnk_plan_ref (include/gcnk.h)."""
+    _fields_ = [("plan", _c.c_void_p), ("hdr", _c.c_int32 * 16), ("workspace", _c.c_void_p),
+                ("workspace_bytes", _c.c_int64), ("counters", _c.c_void_p), ("counter_bytes", _c.c_int64),
+                ("lanes_hint", _c.c_int32), ("pad_", _c.c_int32)]
+
+
+class GcnFwd(_c.Structure):
+    """gcnk_gcn_fwd (include/gcnk.h)."""
+    _fields_ = [("kind", _c.c_int32), ("M", _c.c_int32), ("F", _c.c_int32), ("P", _c.c_int32),
+                ("x_rows", _c.c_int32), ("x_cols", _c.c_int32), ("x", PlanRef),
+                ("x_dense", _c.c_void_p), ("ldx", _c.c_int64), ("x_split_k", _c.c_int32), ("pad0_", _c.c_int32),
+                ("gemm_ws", _c.c_void_p), ("gemm_ws_bytes", _c.c_int64), ("s1", _c.c_void_p), ("lds1", _c.c_int64),
+                ("Kc", _c.c_int32), ("nhub", _c.c_int32), ("k0", _c.c_int32), ("rec_words", _c.c_int32),
+                ("U", _c.c_void_p), ("ldu", _c.c_int64), ("rec", _c.c_void_p),
+                ("aF", PlanRef), ("aP", PlanRef), ("s2", _c.c_void_p), ("lds2", _c.c_int64),
+                ("h1_tmp", _c.c_void_p), ("ld_h1_tmp", _c.c_int64)]
+
+
+FACTORED, SPMM_PROJ, SPMM_GEMM = 1, 2, 3
+KIND_NAMES = {FACTORED: "factored", SPMM_PROJ: "spmm+proj", SPMM_GEMM: "spmm+gemm"}
+
+
+def layout_ok():
+    """The ctypes mirrors match the library's struct layout (gcnk_gcn_fwd_layout)."""
+    buf = (_c.c_int64 * 8)()
+    n = _lib.load().gcnk_gcn_fwd_layout(buf, 8)
+    want = [_c.sizeof(PlanRef), _c.sizeof(GcnFwd), GcnFwd.x.offset, GcnFwd.U.offset, GcnFwd.aF.offset,
+            GcnFwd.aP.offset, GcnFwd.ld_h1_tmp.offset, PlanRef.lanes_hint.offset]
+    return n == 8 and list(buf) == want
+
+
+def _fill_plan(ref, plan, F, lanes, device, keep):
+    """PlanRef for `plan` at width F: its header, a workspace and the counter
+    region torch's current stream uses (Plan.counters)."""
+    ref.plan = plan.buf.data_ptr()
+    for i in range(16):
+        ref.hdr[i] = plan.hdr[i]
+    wsb = plan.workspace_bytes(F)
+    if wsb > 0:
+        ws = torch.empty((wsb + 3) // 4, dtype=torch.float32, device=device)
+        keep.append(ws)
+        ref.workspace, ref.workspace_bytes = ws.data_ptr(), wsb
+    cnt = plan.counters(device)
+    if cnt is not None:
+        keep.append(cnt)
+        ref.counters, ref.counter_bytes = cnt.data_ptr(), 4 * cnt.numel()
+    ref.lanes_hint = int(lanes)
+
+
+class ForwardRecord:
+    """One filled gcnk_gcn_fwd plus the tensors and plans it points into."""
+
+    __slots__ = ("s", "keep", "kind", "M", "F", "P", "src", "__weakref__")
+
+    def __init__(self, adj, xop, F, P, device):
+        lib = _lib.load()
+        M = adj.shape[0]
+        s = GcnFwd()
+        keep = []
+        s.M, s.F, s.P = M, F, P
+        fac = factor.get(adj, xop) if ops.FACTOR_GC1 else None
+        kind = None
+        if fac is not None and P <= 16 and F % 4 == 0 and F <= 256 and \
+                int(lib.gcnk_hubfactor_lds_bytes(F, fac.Kc, fac.H, fac.rec_words)) <= 160 * 1024:
+            kind = FACTORED
+            s.Kc, s.nhub, s.k0, s.rec_words = fac.Kc, fac.H, fac.k0, fac.rec_words
+            s.U, s.ldu, s.rec = fac.U.data_ptr(), fac.U.stride(0), fac.rec.data_ptr()
+            keep += [fac.U, fac.rec]
+            if fac.x_hub is not None and (factor.XHUB != "gemm" or fac.x_hub_dense is None):
+                x_csr, x_dense = fac.x_hub, None
+            else:
+                x_csr, x_dense = None, fac.x_hub_dense
+        else:
+            x_csr, x_dense = xop.csr, xop.dense
+            plan = None
+            if ops.FUSE_PROJECTION and P <= ops.FUSE_MAX_P:
+                lanes = 64
+                plan = adj.plan(ops.default_ipc(adj, F, lanes), int(lib.gcnk_spmm_groups(F, lanes)), DENSE_THRESHOLD)
+                # the fused projection runs on row-unit plans without dense tile blocks
+                kind = SPMM_PROJ if not plan.is_hub and int(plan.hdr[8]) == 0 else None
+            if kind is None:
+                lanes = 0
+                plan = adj.plan(ops.default_ipc(adj, F, lanes), int(lib.gcnk_spmm_groups(F, lanes)), DENSE_THRESHOLD)
+                kind = SPMM_GEMM
+                h = torch.empty((M, F), dtype=torch.float32, device=device)
+                keep.append(h)
+                s.h1_tmp, s.ld_h1_tmp = h.data_ptr(), F
+            if plan.is_hub:
+                raise _Unsupported("hub plans are issued op by op")
+            _fill_plan(s.aF, plan, F, lanes, device, keep)
+            keep.append(plan)
+        # the first product S1 = X W1 (factored: S_T = X_hubs W1)
+        if x_csr is not None:
+            rows, cols = x_csr.shape
+            xp = x_csr.plan(ops.default_ipc(x_csr, F, 0), int(lib.gcnk_spmm_groups(F, 0)), DENSE_THRESHOLD)
+            if xp.is_hub:
+                raise _Unsupported("hub plans are issued op by op")
+            _fill_plan(s.x, xp, F, 0, device, keep)
+            keep.append(xp)
+        else:
+            rows, cols = x_dense.shape
+            s.x_dense, s.ldx = x_dense.data_ptr(), x_dense.stride(0)
+            keep.append(x_dense)
+            s.x_split_k = ops.default_split_k(rows, F, cols)
+        s.x_rows, s.x_cols = rows, cols
+        # GEMM workspace: split-K slabs of X W1 (dense X); H1 W2 runs unsplit
+        gws = int(lib.gcnk_gemm_workspace_bytes(rows, F, cols, s.x_split_k)) if x_dense is not None else 0
+        if gws > 0:
+            g = torch.empty((gws + 3) // 4, dtype=torch.float32, device=device)
+            keep.append(g)
+            s.gemm_ws, s.gemm_ws_bytes = g.data_ptr(), gws
+        s1 = torch.empty((rows, F), dtype=torch.float32, device=device)
+        s2 = torch.empty((M, P), dtype=torch.float32, device=device)
+        keep += [s1, s2]
+        s.s1, s.lds1, s.s2, s.lds2 = s1.data_ptr(), F, s2.data_ptr(), P
+        # gc2's aggregation A S2 + b2 (ops.spmm_sum with a 2-D S2 -> ops.spmm, lanes 0)
+        aP = adj.plan(ops.default_ipc(adj, P, 0), int(lib.gcnk_spmm_groups(P, 0)), DENSE_THRESHOLD)
+        if aP.is_hub:
+            raise _Unsupported("hub plans are issued op by op")
+        _fill_plan(s.aP, aP, P, 0, device, keep)
+        keep.append(aP)
+        s.kind = kind
+        self.s, self.keep, self.kind, self.M, self.F, self.P = s, keep, kind, M, F, P
+        self.src = (adj, xop.csr if xop.csr is not None else xop.dense)
+
+    def run(self, W1, b1, W2, b2, epi, mask, scale, keep_prob, seed, offset, rng_base, store_h1, stream):
+        """(out, H1) of one forward; H1 is None unless store_h1."""
+        dev = W1.device
+        out = torch.empty((self.M, self.P), dtype=torch.float32, device=dev)
+        H1 = torch.empty((self.M, self.F), dtype=torch.float32, device=dev) if store_h1 else None
+        rc = _lib.load().gcnk_gcn_forward_f32(
+            _c.byref(self.s), W1.data_ptr(), b1.data_ptr() if b1 is not None else None, W2.data_ptr(),
+            b2.data_ptr() if b2 is not None else None, out.data_ptr(), self.P,
+            H1.data_ptr() if H1 is not None else None, self.F, epi,
+            mask.data_ptr() if mask is not None else None, mask.stride(0) if mask is not None else 0, scale,
+            keep_prob, seed & (2**64 - 1), offset & (2**64 - 1),
+            rng_base.data_ptr() if rng_base is not None else None, stream)
+        _lib.check(rc, "gcnk_gcn_forward_f32")
+        return out, H1
+
+
+class _Unsupported(Exception):
+    pass
+
+
+_lock = threading.Lock()
+
+
+def get(adj, xop, F, P, device):
+    """(record, stream): the ForwardRecord of (adj, X, F, P) for torch's current
+    stream, built on first use (None where the forward is issued op by op:
+    hub plans), and that stream."""
+    stream = torch.cuda.current_stream(device).cuda_stream
+    src = xop.csr if xop.csr is not None else xop.dense
+    key = (id(src), F, P, stream, ops.FACTOR_GC1, ops.FUSE_PROJECTION)
+    recs = getattr(adj, "_records", None)
+    if recs is None:
+        with _lock:
+            recs = getattr(adj, "_records", None)
+            if recs is None:
+                recs = adj._records = {}
+    hit = recs.get(key)
+    if hit is not None and hit[0] is src and _version(src) == hit[1]:
+        return hit[2], stream
+    with _lock:
+        try:
+            rec = ForwardRecord(adj, xop, F, P, device)
+        except _Unsupported:
+            rec = None
+        while len(recs) >= 8:
+            recs.pop(next(iter(recs)))
+        recs[key] = (src, _version(src), rec)
+        return rec, stream
+
+
+def _version(src):
+    return src._version if isinstance(src, torch.Tensor) else (src.val._version, src.val.data_ptr())

@@ -50,7 +50,7 @@
 extern "C" {
 #endif
 
-#define GCNK_ABI_VERSION 7
+#define GCNK_ABI_VERSION 8
 
 #define GCNK_OK 0
 #define GCNK_EARG (-1)
@@ -330,6 +330,79 @@ int gcnk_hubfactor_gc1_f32(int32_t M, int32_t F, int32_t Kc, int32_t nhub, int32
                            const uint8_t* drop_mask, int64_t ldm, float drop_scale, float keep_prob, uint64_t seed,
                            uint64_t offset, const uint64_t* rng_base, const float* W2, int64_t ldw2, float* H,
                            int64_t ldh, float* C2, int64_t ldc2, void* stream);
+
+/* ---------------------------------------------------------------------------
+ * Whole-forward launch record (ABI 8): GCN.forward (layer.py:164-190) as the
+ * reference's trainer issues it, eagerly, every epoch (trainer.py:357 train,
+ * trainer.py:382 eval) -- from ONE call.  The caller fills the record once per
+ * (adjacency, features, widths, stream) with everything that does not change
+ * from call to call: the plans and their host headers, workspaces and counter
+ * regions, the factored operands, the intermediates S1 and S2.  Each call
+ * passes only the parameters, the outputs and the dropout arguments, and
+ * issues the launches the per-op entry points above issue, in the same order
+ * and with the same arguments (results are bitwise those of the per-op path).
+ *
+ *   GCNK_FWD_FACTORED   S_T = X_hubs W1 (x plan or dense GEMM, x_rows = nhub);
+ *                       (H1, S2) = gcnk_hubfactor_gc1_f32; out = A-hat S2 + b2
+ *   GCNK_FWD_SPMM_PROJ  S1 = X W1; (H1, S2) = gcnk_spmm_proj_f32(aF); out = A-hat S2 + b2
+ *   GCNK_FWD_SPMM_GEMM  S1 = X W1; H1 = epi(A-hat S1 + b1) (aF); S2 = H1 W2; out = A-hat S2 + b2
+ *
+ * gc2's aggregation uses the plan aP with GCNK_EPI_BIAS (GCNK_EPI_NONE when b2
+ * is NULL).  W1 [x_cols x F] and W2 [F x P] contiguous; H1 (ldh) is stored
+ * when non-NULL (a backward needs it); SPMM_GEMM needs h1_tmp [M x F] when it
+ * is NULL.  The record's buffers are used in stream order: calls that may
+ * run concurrently need records of their own.
+ * ------------------------------------------------------------------------- */
+typedef struct gcnk_plan_ref {
+  const void* plan;            /* device plan image (gcnk_spmm_plan_build) */
+  int32_t hdr[16];             /* its header (gcnk_spmm_plan_query) */
+  float* workspace;            /* gcnk_spmm_workspace_bytes(hdr, width) bytes */
+  int64_t workspace_bytes;
+  int32_t* counters;           /* gcnk_spmm_counter_bytes(hdr) bytes (zeroed once) */
+  int64_t counter_bytes;
+  int32_t lanes_hint;
+  int32_t pad_;
+} gcnk_plan_ref;
+
+#define GCNK_FWD_FACTORED 1
+#define GCNK_FWD_SPMM_PROJ 2
+#define GCNK_FWD_SPMM_GEMM 3
+
+typedef struct gcnk_gcn_fwd {
+  int32_t kind;
+  int32_t M, F, P;             /* rows of A-hat, nhid, nclass */
+  int32_t x_rows, x_cols;      /* first product's operand (factored: the hub rows of X) */
+  gcnk_plan_ref x;             /* sparse operand: its plan (x.plan != NULL) ...       */
+  const float* x_dense;        /* ... or dense [x_rows x x_cols] (ldx) on the MFMA GEMM */
+  int64_t ldx;
+  int32_t x_split_k;
+  int32_t pad0_;
+  float* gemm_ws;              /* GEMM split-K workspace (first product and H1 W2) */
+  int64_t gemm_ws_bytes;
+  float* s1;                   /* S1 = X W1, or S_T = X_hubs W1 [x_rows x F] */
+  int64_t lds1;
+  int32_t Kc, nhub, k0, rec_words;   /* factored gc1 (gcnk_hubfactor_gc1_f32) */
+  const float* U;
+  int64_t ldu;
+  const int32_t* rec;
+  gcnk_plan_ref aF;            /* A-hat at width F (SPMM kinds) */
+  gcnk_plan_ref aP;            /* A-hat at width P (gc2) */
+  float* s2;                   /* S2 = H1 W2 [M x P] */
+  int64_t lds2;
+  float* h1_tmp;               /* SPMM_GEMM scratch H1 when H1 == NULL */
+  int64_t ld_h1_tmp;
+} gcnk_gcn_fwd;
+
+int gcnk_gcn_forward_f32(const gcnk_gcn_fwd* rec,
+                         const float* W1, const float* b1, const float* W2, const float* b2,
+                         float* out, int64_t ldo, float* H1, int64_t ldh,
+                         int32_t epilogue, const uint8_t* drop_mask, int64_t ldm, float drop_scale,
+                         float keep_prob, uint64_t seed, uint64_t offset, const uint64_t* rng_base,
+                         void* stream);
+/* Layout of the two structs for bindings that mirror them: writes up to n of
+ * {sizeof plan_ref, sizeof gcn_fwd, offsetof x, U, aF, aP, ld_h1_tmp,
+ * plan_ref.lanes_hint} to out and returns how many exist. */
+int32_t gcnk_gcn_fwd_layout(int64_t* out, int32_t n);
 
 /* ---------------------------------------------------------------------------
  * Sparse-format helpers (one-time graph preparation, utils.py:185-213,

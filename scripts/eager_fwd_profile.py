@@ -14,22 +14,55 @@ sys.path.insert(0, ROOT)
 def main():
     import torch
     import gcn_amd  # noqa: F401
-    from graph_convolutional_networks_for_text_classification_amd import GCN, datasets
+    from graph_convolutional_networks_for_text_classification_amd import GCN, datasets, ops
     dev = torch.device("cuda", 0)
     r8 = datasets.load_r8_fixture(os.path.join(ROOT, "tests", "golden", "r8_graph.npz"))
     x, adj = r8["features"].to(dev), r8["adj"].to(dev)
     torch.manual_seed(0)
     model = GCN(nfeat=r8["nfeat"], nhid=200, nclass=r8["nclass"], dropout=0.5).to(dev).eval()
     with torch.no_grad():
-        for _ in range(20):
-            model(x, adj)
-        torch.cuda.synchronize()
+        for use in (False, True):          # op by op, then the whole-forward record (record.py)
+            ops.USE_RECORD = use
+            for _ in range(20):
+                model(x, adj)
+            torch.cuda.synchronize()
+            n = 200
+            t0 = time.perf_counter()
+            for _ in range(n):
+                model(x, adj)
+            torch.cuda.synchronize()
+            print(f"eager forward ({'record' if use else 'op by op'}): {(time.perf_counter() - t0) / n * 1e6:.1f} us",
+                  flush=True)
+    # the training-step pattern of trainer.py:353-362 (forward + CE + backward + Adam), eager
+    model.train()
+    opt = torch.optim.Adam(model.parameters(), lr=0.02)
+    tgt = torch.zeros(r8["nodes"], dtype=torch.int64, device=dev)
+    tgt[:len(r8["target"])] = torch.from_numpy(r8["target"]).to(dev)
+    idx = torch.arange(len(r8["target"]), device=dev)
+    for use in (False, True):
+        ops.USE_RECORD = use
+        for rng in ("cpu", "device"):
+            model.dropout_rng = rng
+            for _ in range(10):
+                opt.zero_grad()
+                lg = model(x, adj)
+                torch.nn.functional.cross_entropy(lg[idx], tgt[idx]).backward()
+                opt.step()
+            torch.cuda.synchronize()
+            n = 100
+            t0 = time.perf_counter()
+            for _ in range(n):
+                opt.zero_grad()
+                lg = model(x, adj)
+                torch.nn.functional.cross_entropy(lg[idx], tgt[idx]).backward()
+                opt.step()
+            torch.cuda.synchronize()
+            print(f"eager train step ({'record' if use else 'op by op'}, dropout {rng}): "
+                  f"{(time.perf_counter() - t0) / n * 1e3:.3f} ms", flush=True)
+    model.eval()
+    ops.USE_RECORD = True
+    with torch.no_grad():
         n = 200
-        t0 = time.perf_counter()
-        for _ in range(n):
-            model(x, adj)
-        torch.cuda.synchronize()
-        print(f"eager forward: {(time.perf_counter() - t0) / n * 1e6:.1f} us", flush=True)
         pr = cProfile.Profile()
         pr.enable()
         for _ in range(n):

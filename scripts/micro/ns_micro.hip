@@ -1,0 +1,628 @@
+// Standalone microbenchmark for the north-star op (R8 A-hat x S1, F = 200,
+// bias + ReLU): a "stream" schedule measured against copies of the same bytes.
+// Not the product library -- it decides what moves into csrc/.
+//
+//  * light rows (every row that is not a hub row): workgroup b owns RB
+//    consecutive rows of XCD class b % 8 (rows come in order, so each
+//    workgroup reads and writes one contiguous range of B and C); a wave owns
+//    RPW of them.  At entry every wave issues, with no dependence between
+//    them, its RPW self rows B[r], its item window (the rows' off-diagonal
+//    nonzeros, one int2 per lane) and its rows' {diagonal, kind} words; after
+//    one wait it gathers only the off-diagonal B rows (hub rows: L1/L2-hot),
+//    then stores each row.  No unit or row-pointer loads.
+//  * hub rows (degree >= 64): cut where their sorted columns cross an XCD
+//    class boundary (and at SEG items), one 4-wave workgroup per piece on the
+//    XCD of its column class (so its gathers hit the rows the light workgroups
+//    of that class fetched into that L2); pieces of one row meet by a
+//    last-arriver sum of sc1 partials.
+//   build: hipcc -O3 --offload-arch=gfx950 -std=c++17 ns_micro.hip -o ns_micro
+//   run:   python scripts/micro/dump_r8.py /tmp/r8_adj.bin && ./ns_micro /tmp/r8_adj.bin
+#include <hip/hip_runtime.h>
+
+#include <algorithm>
+#include <cmath>
+#include <cstdio>
+#include <cstdlib>
+#include <cstring>
+#include <functional>
+#include <string>
+#include <vector>
+
+#define CHECK(x)                                                                         \
+  do {                                                                                   \
+    hipError_t e_ = (x);                                                                 \
+    if (e_ != hipSuccess) {                                                              \
+      fprintf(stderr, "%s:%d %s: %s\n", __FILE__, __LINE__, #x, hipGetErrorString(e_)); \
+      exit(2);                                                                           \
+    }                                                                                    \
+  } while (0)
+
+constexpr int NX = 8;        // XCD classes
+constexpr int WIN = 64;      // off-diagonal items per light wave
+constexpr int kColBits = 27; // item col field; row-in-wave above it
+
+typedef float f32v4 __attribute__((ext_vector_type(4)));
+__device__ __forceinline__ __amdgpu_buffer_rsrc_t rsrc(const void* base) {
+  return __builtin_amdgcn_make_buffer_rsrc(const_cast<void*>(base), (short)0, 0x7fffffff, 0x00020000);
+}
+__device__ __forceinline__ void st_sc1(const void* base, int off_bytes, const float4& v) {
+  const f32v4 x = {v.x, v.y, v.z, v.w};
+  __builtin_amdgcn_raw_buffer_store_b128(x, rsrc(base), off_bytes, 0, 16);
+}
+__device__ __forceinline__ float4 ld_sc1(const void* base, int off_bytes) {
+  const f32v4 x = __builtin_amdgcn_raw_buffer_load_b128(rsrc(base), off_bytes, 0, 16);
+  return make_float4(x.x, x.y, x.z, x.w);
+}
+__device__ __forceinline__ void fma4(float4& a, float s, const float4& b) {
+  a.x = fmaf(s, b.x, a.x); a.y = fmaf(s, b.y, a.y); a.z = fmaf(s, b.z, a.z); a.w = fmaf(s, b.w, a.w);
+}
+__device__ __forceinline__ void add4(float4& a, const float4& b) { a.x += b.x; a.y += b.y; a.z += b.z; a.w += b.w; }
+__device__ __forceinline__ float4 relu_bias(float4 a, float4 b) {
+  a.x = fmaxf(a.x + b.x, 0.f); a.y = fmaxf(a.y + b.y, 0.f); a.z = fmaxf(a.z + b.z, 0.f); a.w = fmaxf(a.w + b.w, 0.f);
+  return a;
+}
+__device__ __forceinline__ int rl(int v, int i) { return __builtin_amdgcn_readlane(v, i); }
+
+template <int STORE>
+__device__ __forceinline__ void store_out(float4* C, int64_t idx, const float4& v) {
+  if constexpr (STORE == 0) C[idx] = v;
+  else if constexpr (STORE == 1) {
+    const f32v4 x = {v.x, v.y, v.z, v.w};
+    __builtin_nontemporal_store(x, reinterpret_cast<f32v4*>(C + idx));
+  }
+  else st_sc1(C, (int)(idx * 16), v);
+}
+
+struct Args {
+  const float4* B; float4* C; const float4* bias;
+  int M, Q;
+  // light
+  int rpc;                 // rows per class (multiple of RB)
+  const int2* win;         // [M / RPW][WIN] {col | k << kColBits, val}
+  const int2* rowinfo;     // [M] {diag bits, 1 light / 0 hub}
+  // heavy
+  const int4* units; const int4* heavy; const int2* items;
+  float4* part; int* ctr;
+  int nhb;
+  int h0, H;               // hub rows h0 .. h0 + H - 1 (contiguous in R8), staged in LDS by light_lds_role
+  int shrink;              // experiment: remap hub gathers onto 8 hub rows (working-set test, wrong results)
+  unsigned long long* stamps;
+};
+
+__device__ __forceinline__ void stamp(const Args& a, int k) {
+  if (a.stamps && threadIdx.x == 0) a.stamps[4 * blockIdx.x + k] = __builtin_amdgcn_s_memrealtime();
+}
+
+// ---------------------------------------------------------------------------
+// light role: wave (b, wv) -> rows row0 .. row0 + RPW - 1
+template <int WPB, int RPW, int U, int STORE, int ABL>
+__device__ void light_role(const Args& a, int b) {
+  const int lane = threadIdx.x & 63;
+  const int wv = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  constexpr int RB = WPB * RPW;
+  const int c = b % NX, k = b / NX;
+  const int row0 = c * a.rpc + k * RB + wv * RPW;  // wave-uniform
+  if (row0 >= a.M) return;
+  const int Q = a.Q;
+  const int col = lane < Q ? lane : 0;
+  float4 self[RPW];
+#pragma unroll
+  for (int r = 0; r < RPW; ++r) {
+    const int row = row0 + r;
+    self[r] = row < a.M ? a.B[(int64_t)row * Q + col] : make_float4(0.f, 0.f, 0.f, 0.f);
+  }
+  const int2 it = a.win[(int64_t)(row0 / RPW) * WIN + lane];
+  const int2 ri = (lane < RPW && row0 + lane < a.M) ? a.rowinfo[row0 + lane] : make_int2(0, 0);
+  const float4 bv = a.bias[col];
+  stamp(a, 1);
+  // rows of the items (non-decreasing), per-row item ranges in the window
+  const int kr = it.x >= 0 ? (int)((unsigned)it.x >> kColBits) : RPW;
+  int nb[RPW + 1];
+  nb[0] = 0;
+#pragma unroll
+  for (int r = 0; r < RPW; ++r) nb[r + 1] = nb[r] + __builtin_popcountll(__ballot(kr == r));
+  const int cnt = nb[RPW];
+  float4 acc[RPW];
+#pragma unroll
+  for (int r = 0; r < RPW; ++r) {
+    const float d = __int_as_float(rl(ri.x, r));
+    acc[r] = make_float4(d * self[r].x, d * self[r].y, d * self[r].z, d * self[r].w);
+  }
+  if constexpr (!(ABL & 1)) {
+    for (int j0 = 0; j0 < cnt; j0 += U) {
+      float4 g[U];
+      float w[U];
+#pragma unroll
+      for (int j = 0; j < U; ++j) {
+        g[j] = make_float4(0.f, 0.f, 0.f, 0.f);
+        w[j] = 0.f;
+        if (j0 + j < cnt) {
+          int cc = rl(it.x, j0 + j) & ((1 << kColBits) - 1);
+          if (a.shrink) cc = a.h0 + (cc & 7);
+          w[j] = __int_as_float(rl(it.y, j0 + j));
+          g[j] = a.B[(int64_t)cc * Q + col];
+        }
+      }
+#pragma unroll
+      for (int j = 0; j < U; ++j)
+#pragma unroll
+        for (int r = 0; r < RPW; ++r)
+          if (j0 + j >= nb[r] && j0 + j < nb[r + 1]) fma4(acc[r], w[j], g[j]);
+    }
+  }
+  stamp(a, 2);
+  if constexpr (!(ABL & 2)) {
+#pragma unroll
+    for (int r = 0; r < RPW; ++r)
+      if (rl(ri.y, r) && lane < Q) store_out<STORE>(a.C, (int64_t)(row0 + r) * Q + lane, relu_bias(acc[r], bv));
+  } else {
+    if (acc[0].x == 1234.5f) a.C[0] = acc[0];
+  }
+}
+
+// light rows with the hub rows of B staged in LDS once per workgroup (one
+// LDS-DMA round issued with the self rows and the window)
+__device__ __forceinline__ void lds_dma16(const void* g, void* lds_wave) {
+  __builtin_amdgcn_global_load_lds(const_cast<void*>(g), (__attribute__((address_space(3))) void*)lds_wave, 16, 0, 0);
+}
+template <int WPB, int RPW, int STORE>
+__device__ void light_lds_role(const Args& a, int b) {
+  extern __shared__ __attribute__((aligned(16))) float4 s_hub[];
+  const int lane = threadIdx.x & 63;
+  const int wv = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  constexpr int RB = WPB * RPW;
+  const int Q = a.Q;
+  const int c = b % NX, k = b / NX;
+  const int row0 = c * a.rpc + k * RB + wv * RPW;  // wave-uniform
+  const float4* Bh = a.B + (int64_t)a.h0 * Q;
+  for (int e0 = wv * 64; e0 < a.H * Q; e0 += WPB * 64)
+    if (e0 + lane < a.H * Q) lds_dma16(Bh + e0 + lane, s_hub + e0);
+  const int col = lane < Q ? lane : 0;
+  float4 self[RPW];
+#pragma unroll
+  for (int r = 0; r < RPW; ++r) {
+    const int row = row0 + r;
+    self[r] = row < a.M ? a.B[(int64_t)row * Q + col] : make_float4(0.f, 0.f, 0.f, 0.f);
+  }
+  const bool live = row0 < a.M;
+  const int2 it = live ? a.win[(int64_t)(row0 / RPW) * WIN + lane] : make_int2(-1, 0);
+  const int2 ri = (lane < RPW && row0 + lane < a.M) ? a.rowinfo[row0 + lane] : make_int2(0, 0);
+  const float4 bv = a.bias[col];
+  stamp(a, 1);
+  const int kr = it.x >= 0 ? (int)((unsigned)it.x >> kColBits) : RPW;
+  int nb[RPW + 1];
+  nb[0] = 0;
+#pragma unroll
+  for (int r = 0; r < RPW; ++r) nb[r + 1] = nb[r] + __builtin_popcountll(__ballot(kr == r));
+  const int cnt = nb[RPW];
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  __syncthreads();
+  stamp(a, 2);
+  if (!live) return;
+  float4 acc[RPW];
+#pragma unroll
+  for (int r = 0; r < RPW; ++r) {
+    const float d = __int_as_float(rl(ri.x, r));
+    acc[r] = make_float4(d * self[r].x, d * self[r].y, d * self[r].z, d * self[r].w);
+  }
+  for (int j0 = 0; j0 < cnt; j0 += 8) {
+    float4 g[8];
+    float w[8];
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+      g[j] = make_float4(0.f, 0.f, 0.f, 0.f);
+      w[j] = 0.f;
+      if (j0 + j < cnt) {
+        const int cc = (rl(it.x, j0 + j) & ((1 << kColBits) - 1)) - a.h0;
+        w[j] = __int_as_float(rl(it.y, j0 + j));
+        g[j] = s_hub[cc * Q + col];
+      }
+    }
+#pragma unroll
+    for (int j = 0; j < 8; ++j)
+#pragma unroll
+      for (int r = 0; r < RPW; ++r)
+        if (j0 + j >= nb[r] && j0 + j < nb[r + 1]) fma4(acc[r], w[j], g[j]);
+  }
+#pragma unroll
+  for (int r = 0; r < RPW; ++r)
+    if (rl(ri.y, r) && lane < Q) store_out<STORE>(a.C, (int64_t)(row0 + r) * Q + lane, relu_bias(acc[r], bv));
+}
+
+// ---------------------------------------------------------------------------
+// heavy role: one piece of a hub row per workgroup
+template <int WPB, int UH, int STORE>
+__device__ void heavy_role(const Args& a, int u) {
+  __shared__ float4 s_red[WPB][64];
+  __shared__ int s_last;
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int wv = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int4 un = a.units[u];
+  if (un.x < 0) return;  // padding (workgroup-uniform)
+  const int Q = a.Q;
+  const int col = lane < Q ? lane : 0;
+  const float4 bv = a.bias[col];
+  const int kb = un.y + wv, e = un.z;
+  const int k = kb + WPB * lane;
+  const int2 mine = k < e ? a.items[k] : make_int2(0, 0);
+  __builtin_amdgcn_s_waitcnt(0x0F70);  // vmcnt(0): `mine` has landed on every path below
+  const int cnt = e > kb ? min(64, (e - kb + WPB - 1) / WPB) : 0;
+  float4 acc = make_float4(0.f, 0.f, 0.f, 0.f);
+  for (int j0 = 0; j0 < cnt; j0 += UH) {
+    float4 g[UH];
+    float w[UH];
+#pragma unroll
+    for (int j = 0; j < UH; ++j) {
+      g[j] = make_float4(0.f, 0.f, 0.f, 0.f);
+      w[j] = 0.f;
+      if (j0 + j < cnt) {
+        w[j] = __int_as_float(rl(mine.y, j0 + j));
+        g[j] = a.B[(int64_t)rl(mine.x, j0 + j) * Q + col];
+      }
+    }
+#pragma unroll
+    for (int j = 0; j < UH; ++j) fma4(acc, w[j], g[j]);
+  }
+  stamp(a, 1);
+  if (wv > 0) s_red[wv][lane] = acc;
+  __syncthreads();
+  if (wv > 0) return;
+#pragma unroll
+  for (int v = 1; v < WPB; ++v) add4(acc, s_red[v][lane]);
+  stamp(a, 2);
+  if (un.w < 0) {
+    if (lane < Q) store_out<STORE>(a.C, (int64_t)un.x * Q + lane, relu_bias(acc, bv));
+    return;
+  }
+  const int hid = un.w >> 6, seg = un.w & 63;
+  const int4 hv = a.heavy[hid];
+  const float4* p0 = a.part + (int64_t)hv.y * Q;  // slot row stride Q float4
+  if (lane < Q) st_sc1(p0, (seg * Q + lane) * 16, acc);
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  int arrived = 0;
+  if (lane == 0) arrived = __hip_atomic_fetch_add(a.ctr + hid, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  if (__builtin_amdgcn_readfirstlane(arrived) != hv.z - 1) return;
+  float4 sum = make_float4(0.f, 0.f, 0.f, 0.f);
+  for (int s0 = 0; s0 < hv.z; s0 += 16) {
+    float4 pv[16];
+#pragma unroll
+    for (int j = 0; j < 16; ++j) pv[j] = s0 + j < hv.z ? ld_sc1(p0, ((s0 + j) * Q + col) * 16) : make_float4(0.f, 0.f, 0.f, 0.f);
+#pragma unroll
+    for (int j = 0; j < 16; ++j) add4(sum, pv[j]);
+  }
+  if (lane < Q) store_out<STORE>(a.C, (int64_t)hv.x * Q + lane, relu_bias(sum, bv));
+  if (lane == 0) __hip_atomic_store(a.ctr + hid, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+
+// grid: [0, nhb) heavy pieces, then light workgroups
+template <int WPB, int RPW, int U, int UH, int STORE, int ABL>
+__global__ void __launch_bounds__(WPB * 64) ns_kernel(Args a) {
+  stamp(a, 0);
+  const int b = blockIdx.x;
+  if (b < a.nhb) heavy_role<WPB, UH, STORE>(a, b);
+  else light_role<WPB, RPW, U, STORE, ABL>(a, b - a.nhb);
+  stamp(a, 3);
+}
+
+template <int WPB, int RPW, int UH, int STORE>
+__global__ void __launch_bounds__(WPB * 64) ns_lds_kernel(Args a) {
+  stamp(a, 0);
+  const int b = blockIdx.x;
+  if (b < a.nhb) {
+    heavy_role<WPB, UH, STORE>(a, b);
+  } else {
+    light_lds_role<WPB, RPW, STORE>(a, b - a.nhb);
+  }
+  stamp(a, 3);
+}
+
+__global__ void copy_gs(const float4* __restrict__ a, float4* __restrict__ b, int n) {
+  for (int i = blockIdx.x * blockDim.x + threadIdx.x; i < n; i += gridDim.x * blockDim.x) b[i] = a[i];
+}
+// the light geometry with no gathers and no compute: wave copies its RPW rows
+template <int WPB, int RPW>
+__global__ void __launch_bounds__(WPB * 64) copy_rows(Args a) {
+  const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+  const int b = blockIdx.x, c = b % NX, k = b / NX;
+  const int row0 = c * a.rpc + k * WPB * RPW + wv * RPW;
+  float4 v[RPW];
+#pragma unroll
+  for (int r = 0; r < RPW; ++r) v[r] = (row0 + r < a.M && lane < a.Q) ? a.B[(int64_t)(row0 + r) * a.Q + lane] : make_float4(0.f, 0.f, 0.f, 0.f);
+#pragma unroll
+  for (int r = 0; r < RPW; ++r)
+    if (row0 + r < a.M && lane < a.Q) a.C[(int64_t)(row0 + r) * a.Q + lane] = v[r];
+}
+
+// ---------------------------------------------------------------------------
+struct Csr {
+  int M = 0, nnz = 0;
+  std::vector<int> rp, ci;
+  std::vector<float> v;
+};
+static Csr read_csr(const char* path) {
+  Csr c;
+  FILE* f = fopen(path, "rb");
+  if (!f) { perror(path); exit(2); }
+  int hdr[2];
+  if (fread(hdr, 4, 2, f) != 2) exit(2);
+  c.M = hdr[0]; c.nnz = hdr[1];
+  c.rp.resize(c.M + 1); c.ci.resize(c.nnz); c.v.resize(c.nnz);
+  if (fread(c.rp.data(), 4, c.M + 1, f) != (size_t)c.M + 1) exit(2);
+  if (fread(c.ci.data(), 4, c.nnz, f) != (size_t)c.nnz) exit(2);
+  if (fread(c.v.data(), 4, c.nnz, f) != (size_t)c.nnz) exit(2);
+  fclose(f);
+  return c;
+}
+
+struct Plan {
+  int RPW, RB, rpc, nlwg, nhb;
+  std::vector<int2> win, rowinfo, items;
+  std::vector<int4> units, heavy;
+  int nslots = 0, nheavy = 0;
+};
+
+static Plan build_plan(const Csr& A, int WPB, int RPW, int SEG) {
+  Plan P{};
+  const int M = A.M;
+  P.RPW = RPW;
+  P.RB = WPB * RPW;
+  P.rpc = ((M + NX - 1) / NX + P.RB - 1) / P.RB * P.RB;
+  P.nlwg = NX * (P.rpc / P.RB);
+  std::vector<char> hub(M, 0);
+  for (int r = 0; r < M; ++r) hub[r] = A.rp[r + 1] - A.rp[r] >= 64;
+  // light windows over all rows (rows past M pad), waves of RPW rows
+  const int nwave = (NX * P.rpc) / RPW;
+  P.win.assign((size_t)nwave * WIN, make_int2(-1, 0));
+  P.rowinfo.assign(M, make_int2(0, 0));
+  for (int w = 0; w < nwave; ++w) {
+    int n = 0;
+    for (int k = 0; k < RPW; ++k) {
+      const int r = w * RPW + k;
+      if (r >= M || hub[r]) continue;
+      float d = 0.f;
+      for (int q = A.rp[r]; q < A.rp[r + 1]; ++q) {
+        if (A.ci[q] == r) { d += A.v[q]; continue; }
+        if (n >= WIN) { fprintf(stderr, "light window overflow at wave %d\n", w); exit(2); }
+        P.win[(size_t)w * WIN + n++] = make_int2(A.ci[q] | (k << kColBits), __builtin_bit_cast(int, A.v[q]));
+      }
+      P.rowinfo[r] = make_int2(__builtin_bit_cast(int, d), 1);
+    }
+  }
+  // heavy pieces by column class
+  std::vector<std::vector<int4>> q(NX);
+  auto cls = [&](int c) { return std::min(NX - 1, c / P.rpc); };
+  for (int r = 0; r < M; ++r) {
+    if (!hub[r]) continue;
+    const int b = A.rp[r], e = A.rp[r + 1];
+    std::vector<int4> segs;
+    int s = b;
+    while (s < e) {
+      const int c = cls(A.ci[s]);
+      int t = s;
+      while (t < e && cls(A.ci[t]) == c && t - s < SEG) ++t;
+      segs.push_back(make_int4(r, s, t, c));
+      s = t;
+    }
+    const int nseg = (int)segs.size();
+    const int hid = P.nheavy;
+    if (nseg > 1) {
+      P.heavy.push_back(make_int4(r, P.nslots, nseg, 0));
+      P.nslots += nseg;
+      ++P.nheavy;
+    }
+    for (int i = 0; i < nseg; ++i) {
+      const int c = segs[i].w;
+      q[c].push_back(make_int4(r, segs[i].y, segs[i].z, nseg > 1 ? hid * 64 + i : -1));
+    }
+    if (nseg > 64) { fprintf(stderr, "too many segments\n"); exit(2); }
+  }
+  size_t rounds = 0;
+  for (auto& x : q) rounds = std::max(rounds, x.size());
+  for (size_t k = 0; k < rounds; ++k)
+    for (int c = 0; c < NX; ++c) P.units.push_back(k < q[c].size() ? q[c][k] : make_int4(-1, 0, 0, -1));
+  P.nhb = (int)P.units.size();
+  P.items.resize(A.nnz);
+  for (int i = 0; i < A.nnz; ++i) P.items[i] = make_int2(A.ci[i], __builtin_bit_cast(int, A.v[i]));
+  return P;
+}
+
+template <typename T>
+static T* upload(const std::vector<T>& h) {
+  T* d;
+  CHECK(hipMalloc(&d, std::max<size_t>(1, h.size()) * sizeof(T)));
+  if (!h.empty()) CHECK(hipMemcpy(d, h.data(), h.size() * sizeof(T), hipMemcpyHostToDevice));
+  return d;
+}
+
+int main(int argc, char** argv) {
+  const char* path = argc > 1 ? argv[1] : "/tmp/r8_adj.bin";
+  const int SEG = argc > 2 ? atoi(argv[2]) : 128;
+  const Csr A = read_csr(path);
+  const int F = 200, Q = F / 4, M = A.M;
+  const size_t mat = (size_t)M * F;
+  const int nsets = std::max(2, (int)(320e6 / (8.0 * mat)) + 1);
+  std::vector<float*> Bs(nsets), Cs(nsets);
+  std::vector<float> hB(mat), hbias(F);
+  srand(1);
+  for (auto& x : hbias) x = (rand() / (float)RAND_MAX - 0.5f) * 0.1f;
+  for (int s = 0; s < nsets; ++s) {
+    for (auto& x : hB) x = rand() / (float)RAND_MAX - 0.5f;
+    CHECK(hipMalloc(&Bs[s], mat * 4));
+    CHECK(hipMalloc(&Cs[s], mat * 4));
+    CHECK(hipMemcpy(Bs[s], hB.data(), mat * 4, hipMemcpyHostToDevice));
+  }
+  CHECK(hipMemcpy(hB.data(), Bs[0], mat * 4, hipMemcpyDeviceToHost));
+  std::vector<double> ref(mat);
+  std::vector<char> hub(M);
+  for (int r = 0; r < M; ++r) {
+    hub[r] = A.rp[r + 1] - A.rp[r] >= 64;
+    for (int f = 0; f < F; ++f) {
+      double acc = 0;
+      for (int k = A.rp[r]; k < A.rp[r + 1]; ++k) acc += (double)A.v[k] * hB[(size_t)A.ci[k] * F + f];
+      ref[(size_t)r * F + f] = std::max(0.0, acc + hbias[f]);
+    }
+  }
+  float* d_bias = upload(hbias);
+  unsigned long long* d_st;
+  CHECK(hipMalloc(&d_st, (size_t)65536 * 32));
+  hipStream_t st;
+  CHECK(hipStreamCreate(&st));
+
+  struct Built { Plan P; int2 *win, *rowinfo, *items; int4 *units, *heavy; float4* part; int* ctr; };
+  auto build = [&](int WPB, int RPW) {
+    Built b;
+    b.P = build_plan(A, WPB, RPW, SEG);
+    b.win = upload(b.P.win); b.rowinfo = upload(b.P.rowinfo); b.items = upload(b.P.items);
+    b.units = upload(b.P.units); b.heavy = upload(b.P.heavy);
+    CHECK(hipMalloc(&b.part, (size_t)std::max(1, b.P.nslots) * Q * 16));
+    CHECK(hipMalloc(&b.ctr, (size_t)std::max(1, b.P.nheavy) * 4));
+    CHECK(hipMemset(b.ctr, 0, (size_t)std::max(1, b.P.nheavy) * 4));
+    printf("{\"plan\": \"WPB %d RPW %d SEG %d\", \"rpc\": %d, \"light_wg\": %d, \"heavy_wg\": %d, \"heavy_rows\": %d, \"slots\": %d}\n",
+           WPB, RPW, SEG, b.P.rpc, b.P.nlwg, b.P.nhb, b.P.nheavy, b.P.nslots);
+    return b;
+  };
+  std::vector<Built> plans = {build(4, 2), build(4, 4), build(4, 8), build(16, 2), build(8, 4)};
+  int h0 = -1, h1 = -1;
+  for (int r = 0; r < M; ++r) if (hub[r]) { if (h0 < 0) h0 = r; h1 = r + 1; }
+  for (int r = h0; r < h1; ++r) if (!hub[r]) { fprintf(stderr, "hub rows not contiguous\n"); return 2; }
+  const int H = h1 - h0;
+  printf("{\"h0\": %d, \"H\": %d}\n", h0, H);
+  const size_t lds_hub = (size_t)H * Q * 16;
+  CHECK(hipFuncSetAttribute((const void*)&ns_lds_kernel<16, 2, 8, 0>, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024));
+  CHECK(hipFuncSetAttribute((const void*)&ns_lds_kernel<8, 4, 8, 0>, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024));
+  auto args = [&](const Built& b, int s, int nhb) {
+    Args a{};
+    a.B = reinterpret_cast<const float4*>(Bs[s]); a.C = reinterpret_cast<float4*>(Cs[s]);
+    a.bias = reinterpret_cast<const float4*>(d_bias);
+    a.M = M; a.Q = Q; a.rpc = b.P.rpc; a.win = b.win; a.rowinfo = b.rowinfo;
+    a.units = b.units; a.heavy = b.heavy; a.items = b.items; a.part = b.part; a.ctr = b.ctr; a.nhb = nhb;
+    a.h0 = h0; a.H = H;
+    return a;
+  };
+  // which: 0 all, 1 light only, 2 heavy only
+#define NSK(WPB, RPW, U, UH, STORE, ABL) ns_kernel<WPB, RPW, U, UH, STORE, ABL>
+  auto run_ns = [&](auto kern, const Built& b, int s, int which, unsigned long long* stamps) {
+    Args a = args(b, s, which == 1 ? 0 : b.P.nhb);
+    a.stamps = stamps;
+    const int grid = which == 0 ? b.P.nhb + b.P.nlwg : which == 1 ? b.P.nlwg : b.P.nhb;
+    hipLaunchKernelGGL(kern, dim3(grid), dim3(256), 0, st, a);
+  };
+  struct Variant { std::string name; std::function<void(int, unsigned long long*)> run; int check; int grid; };
+  std::vector<Variant> vs;
+  vs.push_back({"copy_gs 1024x256", [&](int s, unsigned long long*) { hipLaunchKernelGGL(copy_gs, dim3(1024), dim3(256), 0, st, (const float4*)Bs[s], (float4*)Cs[s], (int)(mat / 4)); }, 0, 0});
+  vs.push_back({"copy_rows RPW2", [&](int s, unsigned long long*) { Args a = args(plans[0], s, 0); hipLaunchKernelGGL((copy_rows<4, 2>), dim3(plans[0].P.nlwg), dim3(256), 0, st, a); }, 0, 0});
+  vs.push_back({"copy_rows RPW4", [&](int s, unsigned long long*) { Args a = args(plans[1], s, 0); hipLaunchKernelGGL((copy_rows<4, 4>), dim3(plans[1].P.nlwg), dim3(256), 0, st, a); }, 0, 0});
+  vs.push_back({"copy_rows RPW8", [&](int s, unsigned long long*) { Args a = args(plans[2], s, 0); hipLaunchKernelGGL((copy_rows<4, 8>), dim3(plans[2].P.nlwg), dim3(256), 0, st, a); }, 0, 0});
+  auto add = [&](const char* name, int pi, int which, auto kern) {
+    const Built& b = plans[pi];
+    const int grid = which == 0 ? b.P.nhb + b.P.nlwg : which == 1 ? b.P.nlwg : b.P.nhb;
+    vs.push_back({name, [&, pi, which, kern](int s, unsigned long long* stp) { run_ns(kern, plans[pi], s, which, stp); }, which == 0 ? 3 : which, grid});
+  };
+  auto add_lds = [&](const char* name, int pi, int which, auto kern, int wpb) {
+    const Built& b = plans[pi];
+    const int grid = which == 0 ? b.P.nhb + b.P.nlwg : which == 1 ? b.P.nlwg : b.P.nhb;
+    vs.push_back({name, [&, pi, which, kern, wpb](int s, unsigned long long* stp) {
+      Args a = args(plans[pi], s, which == 1 ? 0 : plans[pi].P.nhb);
+      a.stamps = stp;
+      const int g = which == 0 ? plans[pi].P.nhb + plans[pi].P.nlwg : which == 1 ? plans[pi].P.nlwg : plans[pi].P.nhb;
+      hipLaunchKernelGGL(kern, dim3(g), dim3(wpb * 64), which == 2 ? 0 : lds_hub, st, a);
+    }, which == 0 ? 3 : which, grid});
+  };
+  add_lds("light-lds WG1024 RPW2", 3, 1, (ns_lds_kernel<16, 2, 8, 0>), 16);
+  add_lds("light-lds WG512 RPW4", 4, 1, (ns_lds_kernel<8, 4, 8, 0>), 8);
+  add_lds("all-lds WG1024 RPW2", 3, 0, (ns_lds_kernel<16, 2, 8, 0>), 16);
+  add_lds("all-lds WG512 RPW4", 4, 0, (ns_lds_kernel<8, 4, 8, 0>), 8);
+  add_lds("heavy-lds WG1024", 3, 2, (ns_lds_kernel<16, 2, 8, 0>), 16);
+  add_lds("heavy-lds WG512", 4, 2, (ns_lds_kernel<8, 4, 8, 0>), 8);
+  {
+    const int pi = 0;
+    vs.push_back({"light RPW2 U8 shrink-8-hubs", [&, pi](int s, unsigned long long* stp) {
+      Args a = args(plans[pi], s, 0); a.stamps = stp; a.shrink = 1;
+      hipLaunchKernelGGL((NSK(4, 2, 8, 16, 0, 0)), dim3(plans[pi].P.nlwg), dim3(256), 0, st, a);
+    }, 0, plans[0].P.nlwg});
+  }
+  add("light RPW2 U8", 0, 1, NSK(4, 2, 8, 16, 0, 0));
+  add("light RPW4 U8", 1, 1, NSK(4, 4, 8, 16, 0, 0));
+  add("light RPW8 U8", 2, 1, NSK(4, 8, 8, 16, 0, 0));
+  add("light RPW4 U16", 1, 1, NSK(4, 4, 16, 16, 0, 0));
+  add("light RPW4 nt-store", 1, 1, NSK(4, 4, 8, 16, 1, 0));
+  add("light RPW4 sc1-store", 1, 1, NSK(4, 4, 8, 16, 2, 0));
+  add("light RPW4 abl: no gathers", 1, 1, NSK(4, 4, 8, 16, 0, 1));
+  add("light RPW4 abl: no stores", 1, 1, NSK(4, 4, 8, 16, 0, 2));
+  add("light RPW4 abl: neither", 1, 1, NSK(4, 4, 8, 16, 0, 3));
+  add("heavy UH8", 1, 2, NSK(4, 4, 8, 8, 0, 0));
+  add("heavy UH16", 1, 2, NSK(4, 4, 8, 16, 0, 0));
+  add("all RPW2 UH16", 0, 0, NSK(4, 2, 8, 16, 0, 0));
+  add("all RPW4 UH16", 1, 0, NSK(4, 4, 8, 16, 0, 0));
+  add("all RPW8 UH16", 2, 0, NSK(4, 8, 8, 16, 0, 0));
+  add("all RPW4 UH8", 1, 0, NSK(4, 4, 8, 8, 0, 0));
+  add("all RPW4 UH16 nt-store", 1, 0, NSK(4, 4, 8, 16, 1, 0));
+
+  const char* only = getenv("NS_ONLY");
+  auto pct = [](std::vector<double> x, double q) { std::sort(x.begin(), x.end()); return x.empty() ? 0.0 : x[(size_t)(q * (x.size() - 1))]; };
+  std::vector<float> out(mat);
+  for (auto& V : vs) {
+    if (only && !strstr(V.name.c_str(), only)) continue;
+    CHECK(hipMemset(Cs[0], 0, mat * 4));
+    V.run(0, nullptr);
+    CHECK(hipStreamSynchronize(st));
+    CHECK(hipGetLastError());
+    double maxerr = 0;
+    if (V.check) {
+      CHECK(hipMemcpy(out.data(), Cs[0], mat * 4, hipMemcpyDeviceToHost));
+      for (int r = 0; r < M; ++r) {
+        if ((hub[r] && !(V.check & 2)) || (!hub[r] && !(V.check & 1))) continue;
+        for (int f = 0; f < F; ++f) {
+          const double e = std::fabs(out[(size_t)r * F + f] - ref[(size_t)r * F + f]) / (1.0 + std::fabs(ref[(size_t)r * F + f]));
+          maxerr = std::max(maxerr, e);
+        }
+      }
+    }
+    double us[2];
+    for (int mode = 0; mode < 2; ++mode) {
+      const int reps = mode == 0 ? std::max(1, 200 / nsets) : 1;
+      const int per = mode == 0 ? nsets : 200;
+      hipGraph_t gr;
+      hipGraphExec_t ge;
+      CHECK(hipStreamBeginCapture(st, hipStreamCaptureModeGlobal));
+      for (int r = 0; r < reps; ++r)
+        for (int s = 0; s < per; ++s) V.run(mode == 0 ? s : 0, nullptr);
+      CHECK(hipStreamEndCapture(st, &gr));
+      CHECK(hipGraphInstantiate(&ge, gr, nullptr, nullptr, 0));
+      CHECK(hipGraphLaunch(ge, st));
+      CHECK(hipStreamSynchronize(st));
+      hipEvent_t e0, e1;
+      CHECK(hipEventCreate(&e0));
+      CHECK(hipEventCreate(&e1));
+      CHECK(hipEventRecord(e0, st));
+      CHECK(hipGraphLaunch(ge, st));
+      CHECK(hipEventRecord(e1, st));
+      CHECK(hipEventSynchronize(e1));
+      float ms = 0;
+      CHECK(hipEventElapsedTime(&ms, e0, e1));
+      us[mode] = ms * 1e3 / (reps * per);
+      CHECK(hipGraphExecDestroy(ge));
+      CHECK(hipGraphDestroy(gr));
+    }
+    printf("{\"variant\": \"%s\", \"cold_us\": %.3f, \"warm_us\": %.3f, \"frac_cold\": %.3f, \"maxerr\": %.3g", V.name.c_str(), us[0], us[1],
+           12.94234e6 / (us[0] * 1e-6) / 8e12, maxerr);
+    if (V.grid > 0) {  // one stamped launch on a cold set
+      CHECK(hipMemset(d_st, 0, (size_t)V.grid * 32));
+      V.run(nsets - 1, d_st);
+      CHECK(hipStreamSynchronize(st));
+      std::vector<unsigned long long> hs((size_t)4 * V.grid);
+      CHECK(hipMemcpy(hs.data(), d_st, hs.size() * 8, hipMemcpyDeviceToHost));
+      unsigned long long t0 = ~0ull;
+      for (int b = 0; b < V.grid; ++b) if (hs[4 * b]) t0 = std::min(t0, hs[4 * b]);
+      for (int k = 0; k < 4; ++k) {
+        std::vector<double> x;
+        for (int b = 0; b < V.grid; ++b)
+          if (hs[4 * b + k]) x.push_back((hs[4 * b + k] - t0) / 100.0);
+        printf(", \"ph%d\": [%.2f, %.2f, %.2f]", k, pct(x, 0.1), pct(x, 0.5), pct(x, 1.0));
+      }
+    }
+    printf("}\n");
+    fflush(stdout);
+  }
+  return 0;
+}

@@ -39,7 +39,7 @@ def _hdr(M=10, K=10, groups=1, ipc=32, nslots=0, nslabs=0):
 
 def test_abi_version_and_error_text():
     lib = _lib.load()
-    assert lib.gcnk_abi_version() == _lib.ABI_VERSION == 7
+    assert lib.gcnk_abi_version() == _lib.ABI_VERSION == 8
     rc = lib.gcnk_spmm_csr_f32(None, None, None, 0, 8, None, 0, None, 0, None, 0,
                                1.0, 1.0, 0, 0, None, None, 0, None, 0, 0, None)
     assert rc == _lib.EARG
@@ -109,3 +109,25 @@ def test_product_path_refuses_cpu_tensors(r8):
     m = GCN(nfeat=r8["nfeat"], nhid=200, nclass=r8["nclass"], dropout=0.5)
     with pytest.raises(RuntimeError, match="ROCm GPU"):
         m(r8["features"], r8["adj"])
+
+
+def test_forward_record_layout_and_validation():
+    """gcnk_gcn_forward_f32's record: the ctypes mirror matches the C layout, and
+    incomplete records are refused before any launch (no GPU needed)."""
+    from graph_convolutional_networks_for_text_classification_amd import record
+    lib = _lib.load()
+    assert record.layout_ok()
+    p = ctypes.c_void_p(16)
+    args = (p, None, p, None, p, 8, None, 0, _lib.EPI_BIAS_RELU, None, 0, 1.0, 1.0, 0, 0, None, None)
+    assert lib.gcnk_gcn_forward_f32(None, *args) == _lib.EARG
+    r = record.GcnFwd()
+    r.kind, r.M, r.F, r.P = record.FACTORED, 10, 16, 8
+    r.s1, r.s2, r.aP.plan, r.x_dense = 16, 16, 16, 16
+    assert lib.gcnk_gcn_forward_f32(ctypes.byref(r), *args) == _lib.EARG   # factored without U / records
+    assert b"missing an operand" in lib.gcnk_last_error()
+    r.kind = record.SPMM_PROJ                                                # no F-wide plan
+    assert lib.gcnk_gcn_forward_f32(ctypes.byref(r), *args) == _lib.EARG
+    r.kind = 9
+    r.aF.plan = 16
+    assert lib.gcnk_gcn_forward_f32(ctypes.byref(r), *args) == _lib.EARG
+    assert b"unknown record kind" in lib.gcnk_last_error()

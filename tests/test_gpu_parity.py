@@ -1312,3 +1312,70 @@ def test_factored_forward_hub_rows_first_ragged(mode):
     for k in ga:
         np.testing.assert_allclose(ga[k], gb[k], rtol=1e-4, atol=1e-5 * max(1.0, float(np.abs(gb[k]).max())),
                                    err_msg=k)
+
+
+# ------------------------------------------------------------------------------ whole-forward launch record
+
+@pytest.mark.parametrize("path", ["factored", "spmm_proj", "spmm_gemm", "dense_factored", "dense_spmm"])
+@pytest.mark.parametrize("mode", ["eval", "train_mask", "train_hash"])
+def test_forward_record_is_bitwise_the_per_op_path(r8, path, mode, monkeypatch):
+    """gcnk_gcn_forward_f32 (record.py: the whole forward from one C call)
+    issues the per-op path's launches with the same arguments: logits and every
+    gradient bitwise equal to ops.USE_RECORD = False, for each record kind
+    (factored / fused projection / SpMM + GEMM, sparse and dense X), in eval
+    (inference fast path, no autograd node) and in both dropout modes."""
+    from graph_convolutional_networks_for_text_classification_amd import ops, record
+    monkeypatch.setattr(ops, "FACTOR_GC1", path in ("factored", "dense_factored"))
+    monkeypatch.setattr(ops, "FUSE_PROJECTION", path != "spmm_gemm")
+    A = r8["adj"].to(DEV)
+    if path.startswith("dense"):       # the gensim-shaped 100-d X (dense copy, MFMA GEMM)
+        ndoc, ntopic = r8["ndoc"], r8["ntopic"]
+        Xd = np.zeros((r8["nodes"], 100), np.float32)
+        Xd[:ndoc, :ntopic] = r8["features_dense"][:ndoc, :ntopic]
+        Xd[ndoc:] = np.random.default_rng(0).standard_normal((ntopic, 100))
+        X, nfeat = datasets.dense_to_coo(Xd).to(DEV), 100
+    else:
+        X, nfeat = r8["features"].to(DEV), r8["nfeat"]
+    outs = {}
+    for use in (True, False):
+        monkeypatch.setattr(ops, "USE_RECORD", use)
+        torch.manual_seed(77)
+        m = GCN(nfeat=nfeat, nhid=200, nclass=r8["nclass"], dropout=0.5,
+                dropout_rng="device" if mode == "train_hash" else "cpu").to(DEV)
+        m.train(mode != "eval")
+        torch.manual_seed(3)
+        if mode == "eval":
+            with torch.no_grad():
+                lg = m(X, A)
+                assert torch.equal(lg, m(X, A))        # memoised operands, same record
+            outs[use] = (lg.cpu(), {})
+        else:
+            lg = m(X, A)
+            lg.square().sum().backward()
+            outs[use] = (lg.detach().cpu(), {k: p.grad.cpu() for k, p in m.named_parameters()})
+    assert torch.equal(outs[True][0], outs[False][0])
+    for k in outs[True][1]:
+        assert torch.equal(outs[True][1][k], outs[False][1][k]), k
+    from graph_convolutional_networks_for_text_classification_amd.sparse import as_csr
+    kinds = {r[2].kind for r in getattr(as_csr(A), "_records", {}).values() if r[2] is not None}
+    want = {"factored": record.FACTORED, "dense_factored": record.FACTORED, "spmm_proj": record.SPMM_PROJ,
+            "spmm_gemm": record.SPMM_GEMM}.get(path)
+    if want is not None:
+        assert want in kinds, kinds
+
+
+def test_forward_record_follows_in_place_feature_updates(r8):
+    """The inference fast path memoises (x, adj); an in-place change of x's
+    values must reach the output (new CSR, factor and record), matching a
+    fresh model on a copy."""
+    A = r8["adj"].to(DEV)
+    X = r8["features"].to(DEV).coalesce()
+    torch.manual_seed(1)
+    m = GCN(nfeat=r8["nfeat"], nhid=200, nclass=r8["nclass"], dropout=0.5).to(DEV).eval()
+    with torch.no_grad():
+        a = m(X, A)
+        X._values().mul_(2.0)
+        b = m(X, A)
+        ref = m(torch.sparse_coo_tensor(X._indices(), X._values().clone(), X.shape).coalesce(), A)
+    assert not torch.equal(a, b)
+    assert torch.equal(b, ref)

@@ -460,19 +460,17 @@ def main():
         torch.cuda.empty_cache()
     north = "spmm_AS1_F200"   # BASELINE.json north_star: the R8 doc-topic SpMM at hidden 200
     dom = max(optimes, key=lambda k: optimes[k]["cold_us"])
-    plan_kinds = {"spmm_AS1_F200": "hub" if any(p.is_hub for p in a_csr._plans.values()) else "row"}
 
     extras = rank == 0 and world == 1
     # ---- live HBM traffic of the north-star op (child rocprofv3 --pmc passes)
     traffic, traffic_src = (None, "skipped")
     if extras and not args.no_pmc:
-        traffic, traffic_src = pmc_traffic("AS1", ["hub_group_kernel", "spmm_row_kernel"])
+        traffic, traffic_src = pmc_traffic("AS1", ["spmm_row_kernel"])
     # ---- the same op's kernel durations from rocprofv3 (warm and cold rotations)
     kt = {}
     if extras and not args.no_rocprof:
         for mode in ("warm", "cold"):
-            kt[mode] = rocprof_kernel_us(mode, ["hub_group_kernel", "spmm_row_kernel"], args.rocprof_dir,
-                                         plan_kinds[north])
+            kt[mode] = rocprof_kernel_us(mode, ["spmm_row_kernel"], args.rocprof_dir, "row")
         # the streaming floor at this size: one elementwise pass over the same B / C
         # rotation (reads B once, writes C once) under the same rocprofv3 timing
         kt["copy"] = rocprof_kernel_us("cold", ["elementwise"], args.rocprof_dir, "copy")
@@ -483,14 +481,10 @@ def main():
     if extras and not args.no_rocprof:
         trace, trace_src = forward_kernels(args.rocprof_dir)
         if trace is not None and trace.get("kernels"):
-            from graph_convolutional_networks_for_text_classification_amd import ops as _ops
-            nsl = int(_ops._lib.load().gcnk_spmm_proj_slices(
-                _ops.ctypes.cast(next(p for p in a_csr._plans.values() if p.is_hub).hdr, _ops.ctypes.c_void_p), nhid)) \
-                if any(p.is_hub for p in a_csr._plans.values()) else 1
             alg = {   # algorithmic bytes of each launch of the eval forward (SURVEY §8(d) formula)
                 "X W1": spmm_bytes(N, nfeat, nnz_x, nhid),
-                "A S1": 4 * (N + 1) + 8 * nnz_a + 4 * N * nhid + 4 * nsl * N * nclass + 4 * nhid * nclass,
-                "A sum S2": 4 * (N + 1) + 8 * nnz_a + 4 * nsl * N * nclass + 4 * N * nclass,
+                "A S1": 4 * (N + 1) + 8 * nnz_a + 4 * N * nhid + 4 * N * nclass + 4 * nhid * nclass,
+                "A S2": spmm_bytes(N, N, nnz_a, nclass),
             }
             fac = _factored(a_csr, x)
             if fac is not None:
@@ -500,14 +494,14 @@ def main():
                 alg = {"X_hubs W1": spmm_bytes(fac.H, nfeat, x_hub_nnz, nhid),
                        "A X W1 factored + H1 W2": (4 * fac.U.numel() + 4 * fac.rec.numel() + 4 * fac.Kc * nhid
                                                     + 4 * fac.H * nhid + 4 * nhid * nclass + 4 * N * nclass),
-                       "A sum S2": alg["A sum S2"]}
+                       "A S2": alg["A S2"]}
             ks, na = [], 0
             for k in trace["kernels"]:   # the A-hat launches are the row / hub kernels, X W1 the rest
                 name = k["kernel"]
                 if "hubfactor" in name:
                     key = "A X W1 factored + H1 W2"
-                elif "spmm_row_kernel" in name or "hub_group_kernel" in name:
-                    key = "A S1" if na == 0 and fac is None else "A sum S2"
+                elif "spmm_row_kernel" in name:
+                    key = "A S1" if na == 0 and fac is None else "A S2"
                     na += 1
                 else:
                     key = "X W1" if fac is None else "X_hubs W1"
@@ -660,7 +654,7 @@ def main():
     dur, dur_w, src = kn["cold_us"], kn["warm_us"], "HIP events per call (hipGraph of back-to-back launches)"
     if kcold[0] is not None and kwarm[0] is not None:
         dur, dur_w, src = kcold[0], kwarm[0], kcold[1]
-    roof = {"bound": "hbm", "kernel": north, "plan": plan_kinds[north],
+    roof = {"bound": "hbm", "kernel": north, "plan": "row",
             "achieved": nb / (dur * 1e-6) / 1e9, "peak": HBM_PEAK_GBS, "unit": "GB/s",
             "frac": nb / (dur * 1e-6) / 1e9 / HBM_PEAK_GBS, "frac_warm": nb / (dur_w * 1e-6) / 1e9 / HBM_PEAK_GBS,
             "traffic": traffic, "traffic_source": traffic_src,

@@ -50,14 +50,12 @@ SIGNATURES = {
     "gcnk_last_error": (ctypes.c_char_p, []),
     "gcnk_spmm_groups": (_i32, [_i32, _i32]),
     "gcnk_spmm_default_ipc": (_i32, [_i32, _i64, _i32, _i32]),
-    # rowptr, colind, M, K, nnz, ipc, groups, dense_threshold, hub_min, block_rows, stream
-    "gcnk_spmm_plan_bytes": (_i64, [_vp, _vp, _i32, _i32, _i64, _i32, _i32, _f32, _i32, _i32, _vp]),
-    # rowptr, colind, val, M, K, nnz, ipc, groups, dense_threshold, hub_min, block_rows, plan, plan_bytes, stream
-    "gcnk_spmm_plan_build": (ctypes.c_int, [_vp, _vp, _vp, _i32, _i32, _i64, _i32, _i32, _f32, _i32, _i32, _vp, _i64,
-                                            _vp]),
-    "gcnk_spmm_plan_bytes_host": (_i64, [_vp, _vp, _i32, _i32, _i64, _i32, _i32, _f32, _i32, _i32]),
-    "gcnk_spmm_plan_build_host": (ctypes.c_int, [_vp, _vp, _vp, _i32, _i32, _i64, _i32, _i32, _f32, _i32, _i32, _vp,
-                                                 _i64]),
+    # rowptr, colind, M, K, nnz, ipc, groups, dense_threshold, stream
+    "gcnk_spmm_plan_bytes": (_i64, [_vp, _vp, _i32, _i32, _i64, _i32, _i32, _f32, _vp]),
+    # rowptr, colind, val, M, K, nnz, ipc, groups, dense_threshold, plan, plan_bytes, stream
+    "gcnk_spmm_plan_build": (ctypes.c_int, [_vp, _vp, _vp, _i32, _i32, _i64, _i32, _i32, _f32, _vp, _i64, _vp]),
+    "gcnk_spmm_plan_bytes_host": (_i64, [_vp, _vp, _i32, _i32, _i64, _i32, _i32, _f32]),
+    "gcnk_spmm_plan_build_host": (ctypes.c_int, [_vp, _vp, _vp, _i32, _i32, _i64, _i32, _i32, _f32, _vp, _i64]),
     "gcnk_spmm_plan_query": (ctypes.c_int, [_vp, _vp, _vp]),
     "gcnk_spmm_workspace_bytes": (_i64, [_vp, _i32]),
     "gcnk_spmm_counter_bytes": (_i64, [_vp]),
@@ -91,31 +89,6 @@ SIGNATURES = {
         _vp, _i64, _f32,          # drop_mask, ldm, drop_scale
         _f32, _u64, _u64, _vp,    # keep_prob, seed, offset, rng_base
         _vp, _i64, _i32, _vp, _i64,  # W, ldw, P, C2, ldc2
-        _vp, _i64,                # workspace, workspace_bytes
-        _vp, _i64,                # counters, counter_bytes
-        _i32, _vp,                # lanes_hint, stream
-    ]),
-    "gcnk_spmm_proj_slices": (_i32, [_vp, _i32]),
-    "gcnk_spmm_proj_sliced_f32": (ctypes.c_int, [
-        _vp, _vp,                 # plan, plan header
-        _vp, _i64, _i32,          # B, ldb, F
-        _vp, _i64,                # C (nullable), ldc
-        _vp, _i32,                # bias, epilogue
-        _vp, _i64, _f32,          # drop_mask, ldm, drop_scale
-        _f32, _u64, _u64, _vp,    # keep_prob, seed, offset, rng_base
-        _vp, _i64, _i32,          # W, ldw, P
-        _vp, _i64, _i64, _i32,    # C2, ldc2, c2_slice_stride, c2_slices
-        _vp, _i64,                # workspace, workspace_bytes
-        _vp, _i64,                # counters, counter_bytes
-        _i32, _vp,                # lanes_hint, stream
-    ]),
-    "gcnk_spmm_sum_csr_f32": (ctypes.c_int, [
-        _vp, _vp,                 # plan, plan header
-        _vp, _i64, _i32, _i32, _i64,  # B, ldb, F, nsum, bstride
-        _vp, _i64,                # C, ldc
-        _vp, _i32,                # bias, epilogue
-        _vp, _i64, _f32,          # drop_mask, ldm, drop_scale
-        _f32, _u64, _u64, _vp,    # keep_prob, seed, offset, rng_base
         _vp, _i64,                # workspace, workspace_bytes
         _vp, _i64,                # counters, counter_bytes
         _i32, _vp,                # lanes_hint, stream

@@ -29,7 +29,6 @@
 //      summed in a fixed order).
 // No atomics, no hand-off between workgroups: bitwise reproducible.
 #include "gcnk_common.h"
-#include "combine.h"
 
 #include <algorithm>
 

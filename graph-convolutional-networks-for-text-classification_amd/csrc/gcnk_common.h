@@ -139,38 +139,14 @@ struct Vec<1> {
 };
 
 
-// ---------------------------------------------------------------------------
-// Hub-split SpMM (hub.hip): plan builder, layout queries and the launch.
-constexpr int32_t kHubMagic = 0x474e4832;  // "GNH2"
-int hub_plan_host(const int32_t* rowptr, const int32_t* colind, const float* val, int32_t M, int32_t K, int64_t nnz,
-                  int32_t groups, int32_t hub_min, int32_t block_rows, std::vector<int32_t>& img);
-int64_t hub_plan_words(const int32_t* hdr);
-int64_t hub_workspace_bytes(const int32_t* hdr, int32_t F);
-int64_t hub_counter_bytes(const int32_t* hdr);
-// fused work beside a hub-plan product (hub.hip HubExtra): a projection of
-// every finished element (W != null) or a summed operand (nsum > 1)
-struct HubSide {
-  const float* W = nullptr;
-  int64_t ldw = 0;
-  int32_t P = 0;
-  float* C2 = nullptr;
-  int64_t c2_stride = 0, ldc2 = 0;
-  int32_t nsum = 1;
-  int64_t bstride = 0;
-};
-int32_t hub_proj_slices(const int32_t* hdr, int32_t F);
-int hub_spmm(const void* plan, const int32_t* hdr, const float* B, int64_t ldb, int32_t F, float* C, int64_t ldc,
-             const Epi& e, float* workspace, int32_t* counters, bool vec4, const HubSide& side, hipStream_t s);
-
-// ---------------------------------------------------------------------------
-// Split-plan X W (xw.hip): few contiguous dense rows + rows over a few "hot" columns.
-constexpr int32_t kXwMagic = 0x474e5831;  // "GNX1"
-int xw_plan_host(const int32_t* rowptr, const int32_t* colind, const float* val, int32_t M, int32_t K, int64_t nnz,
-                 int32_t groups, std::vector<int32_t>& img);
-int64_t xw_plan_words(const int32_t* hdr);
-int64_t xw_workspace_bytes(const int32_t* hdr, int32_t F);
-int64_t xw_counter_bytes(const int32_t* hdr);
-int xw_spmm(const void* plan, const int32_t* hdr, const float* B, int64_t ldb, int32_t F, float* C, int64_t ldc,
-            const Epi& e, float* workspace, int32_t* counters, bool vec4, hipStream_t s);
+// One LDS-DMA load per lane (global_load_lds): global gsrc -> LDS at
+// lds_wave + BYTES * lane (lds_wave wave-uniform).  Asynchronous: covered by
+// the wave's vmcnt.
+__device__ __forceinline__ void lds_dma16(const void* gsrc, void* lds_wave) {
+  __builtin_amdgcn_global_load_lds(const_cast<void*>(gsrc), (__attribute__((address_space(3))) void*)lds_wave, 16, 0, 0);
+}
+__device__ __forceinline__ void lds_dma4(const void* gsrc, void* lds_wave) {
+  __builtin_amdgcn_global_load_lds(const_cast<void*>(gsrc), (__attribute__((address_space(3))) void*)lds_wave, 4, 0, 0);
+}
 
 }  // namespace gcnk

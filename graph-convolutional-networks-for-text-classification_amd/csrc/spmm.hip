@@ -1596,44 +1596,23 @@ void classic_image(const HostPlan& hp, const int32_t* ci, const float* vv, int64
   putf(L.dval, hp.dval);
 }
 
-// The plan image for host CSR arrays: the hub plan (hub.hip) when the operand
-// has its structure (hub_min >= 0; 0 = automatic threshold), else the
-// row-unit + tile plan.
+// The row-unit + tile plan image for host CSR arrays.
 int build_image(const int32_t* rp, const int32_t* ci, const float* vv, int32_t M, int32_t K, int64_t nnz, int32_t ipc,
-                int32_t groups, float dense_threshold, int32_t hub_min, int32_t block_rows, std::vector<int32_t>& img) {
+                int32_t groups, float dense_threshold, std::vector<int32_t>& img) {
   int rc = check_csr(rp, ci, M, K, nnz);
   if (rc) return rc;
-  if (hub_min >= 0) {
-    rc = hub_plan_host(rp, ci, vv, M, K, nnz, groups, hub_min, block_rows, img);
-    if (rc <= 0) return rc;  // built (0) or an error; 1: not applicable
-  }
-  if (dense_threshold > 0.f && dense_threshold <= 1.f) {
-    rc = xw_plan_host(rp, ci, vv, M, K, nnz, groups, img);
-    if (rc <= 0) return rc;
-  }
   HostPlan hp;
   if ((rc = host_plan(rp, ci, vv, M, K, nnz, ipc, groups, std::fabs(dense_threshold), hp))) return rc;
   classic_image(hp, ci, vv, nnz, img);
   return GCNK_OK;
 }
 
-// Bytes of the plan build_image would make, without making it: the row-unit +
-// tile plan's size follows from its header (no light-row sort, no image);
-// a hub plan is built (its size depends on the group records).
+// Bytes of the plan build_image would make, without making it: the size
+// follows from its header (no light-row sort, no image).
 int64_t plan_size(const int32_t* rp, const int32_t* ci, int32_t M, int32_t K, int64_t nnz, int32_t ipc, int32_t groups,
-                  float dense_threshold, int32_t hub_min, int32_t block_rows) {
+                  float dense_threshold) {
   int rc = check_csr(rp, ci, M, K, nnz);
   if (rc) return rc;
-  if (hub_min >= 0) {
-    std::vector<int32_t> img;
-    rc = hub_plan_host(rp, ci, nullptr, M, K, nnz, groups, hub_min, block_rows, img);
-    if (rc <= 0) return rc ? rc : (int64_t)img.size() * 4;
-  }
-  if (dense_threshold > 0.f && dense_threshold <= 1.f) {
-    std::vector<int32_t> img;
-    rc = xw_plan_host(rp, ci, nullptr, M, K, nnz, groups, img);
-    if (rc <= 0) return rc ? rc : (int64_t)img.size() * 4;
-  }
   HostPlan hp;
   if ((rc = host_plan(rp, ci, nullptr, M, K, nnz, ipc, groups, std::fabs(dense_threshold), hp, false))) return rc;
   return Layout(hp.hdr).total * 4;
@@ -1704,24 +1683,23 @@ extern "C" int32_t gcnk_spmm_default_ipc(int32_t M, int64_t nnz, int32_t F, int3
 }
 
 extern "C" int64_t gcnk_spmm_plan_bytes_host(const int32_t* rowptr, const int32_t* colind, int32_t M, int32_t K,
-                                             int64_t nnz, int32_t ipc, int32_t groups, float dense_threshold,
-                                             int32_t hub_min, int32_t block_rows) {
+                                             int64_t nnz, int32_t ipc, int32_t groups, float dense_threshold) {
   if (!plan_args_ok(rowptr, colind, M, K, nnz, ipc, groups)) {
     set_error("gcnk_spmm_plan_bytes: bad argument");
     return GCNK_EARG;
   }
-  return plan_size(rowptr, colind, M, K, nnz, ipc, groups, dense_threshold, hub_min, block_rows);
+  return plan_size(rowptr, colind, M, K, nnz, ipc, groups, dense_threshold);
 }
 
 extern "C" int gcnk_spmm_plan_build_host(const int32_t* rowptr, const int32_t* colind, const float* val, int32_t M,
                                          int32_t K, int64_t nnz, int32_t ipc, int32_t groups, float dense_threshold,
-                                         int32_t hub_min, int32_t block_rows, int32_t* plan, int64_t plan_bytes) {
+                                         int32_t* plan, int64_t plan_bytes) {
   if (!plan_args_ok(rowptr, colind, M, K, nnz, ipc, groups) || !plan || (nnz > 0 && !val)) {
     set_error("gcnk_spmm_plan_build_host: bad argument");
     return GCNK_EARG;
   }
   std::vector<int32_t> img;
-  const int rc = build_image(rowptr, colind, val, M, K, nnz, ipc, groups, dense_threshold, hub_min, block_rows, img);
+  const int rc = build_image(rowptr, colind, val, M, K, nnz, ipc, groups, dense_threshold, img);
   if (rc) return rc;
   if (plan_bytes < (int64_t)img.size() * 4) {
     set_error("gcnk_spmm_plan_build_host: plan buffer %lld B < %lld B", (long long)plan_bytes,
@@ -1733,8 +1711,7 @@ extern "C" int gcnk_spmm_plan_build_host(const int32_t* rowptr, const int32_t* c
 }
 
 extern "C" int64_t gcnk_spmm_plan_bytes(const int32_t* rowptr, const int32_t* colind, int32_t M, int32_t K,
-                                        int64_t nnz, int32_t ipc, int32_t groups, float dense_threshold,
-                                        int32_t hub_min, int32_t block_rows, void* stream) {
+                                        int64_t nnz, int32_t ipc, int32_t groups, float dense_threshold, void* stream) {
   if (!plan_args_ok(rowptr, colind, M, K, nnz, ipc, groups)) {
     set_error("gcnk_spmm_plan_bytes: bad argument");
     return GCNK_EARG;
@@ -1742,13 +1719,12 @@ extern "C" int64_t gcnk_spmm_plan_bytes(const int32_t* rowptr, const int32_t* co
   std::vector<int32_t> rp, ci;
   std::vector<float> vv;
   const int rc = fetch_csr(rowptr, colind, nullptr, M, nnz, (hipStream_t)stream, rp, ci, vv);
-  return rc ? rc : plan_size(rp.data(), ci.data(), M, K, nnz, ipc, groups, dense_threshold, hub_min, block_rows);
+  return rc ? rc : plan_size(rp.data(), ci.data(), M, K, nnz, ipc, groups, dense_threshold);
 }
 
 extern "C" int gcnk_spmm_plan_build(const int32_t* rowptr, const int32_t* colind, const float* val, int32_t M,
                                     int32_t K, int64_t nnz, int32_t ipc, int32_t groups, float dense_threshold,
-                                    int32_t hub_min, int32_t block_rows, void* plan, int64_t plan_bytes,
-                                    void* stream) {
+                                    void* plan, int64_t plan_bytes, void* stream) {
   if (!plan_args_ok(rowptr, colind, M, K, nnz, ipc, groups) || !plan || (nnz > 0 && !val)) {
     set_error("gcnk_spmm_plan_build: bad argument (M=%d nnz=%lld ipc=%d groups=%d)", M, (long long)nnz, ipc, groups);
     return GCNK_EARG;
@@ -1757,7 +1733,7 @@ extern "C" int gcnk_spmm_plan_build(const int32_t* rowptr, const int32_t* colind
   std::vector<int32_t> rp, ci, img;
   std::vector<float> vv;
   int rc = fetch_csr(rowptr, colind, val, M, nnz, s, rp, ci, vv);
-  if (!rc) rc = build_image(rp.data(), ci.data(), vv.data(), M, K, nnz, ipc, groups, dense_threshold, hub_min, block_rows, img);
+  if (!rc) rc = build_image(rp.data(), ci.data(), vv.data(), M, K, nnz, ipc, groups, dense_threshold, img);
   if (rc) return rc;
   if (plan_bytes < (int64_t)img.size() * 4) {
     set_error("gcnk_spmm_plan_build: plan buffer %lld B < %lld B", (long long)plan_bytes, (long long)img.size() * 4);
@@ -1778,7 +1754,7 @@ extern "C" int gcnk_spmm_plan_query(const void* plan, int32_t* out16, void* stre
   int rc = hip_check(hipMemcpyAsync(out16, plan, 64, hipMemcpyDeviceToHost, s), "plan query copy");
   if (rc) return rc;
   rc = hip_check(hipStreamSynchronize(s), "plan query sync");
-  if (!rc && out16[0] != kMagic && out16[0] != kHubMagic && out16[0] != kXwMagic) {
+  if (!rc && out16[0] != kMagic) {
     set_error("gcnk_spmm_plan_query: not a gcnk plan");
     return GCNK_EARG;
   }
@@ -1788,13 +1764,11 @@ extern "C" int gcnk_spmm_plan_query(const void* plan, int32_t* out16, void* stre
 static int64_t tile_fpad(int32_t F) { return ((int64_t)F + 15) & ~15LL; }
 
 static bool plan_magic(const int32_t* hdr) {
-  return hdr && (hdr[0] == kMagic || hdr[0] == kHubMagic || hdr[0] == kXwMagic);
+  return hdr && hdr[0] == kMagic;
 }
 
 extern "C" int64_t gcnk_spmm_workspace_bytes(const int32_t* hdr, int32_t F) {
   if (!plan_magic(hdr) || F < 0) return GCNK_EARG;
-  if (hdr[0] == kHubMagic) return hub_workspace_bytes(hdr, F);
-  if (hdr[0] == kXwMagic) return xw_workspace_bytes(hdr, F);
   const int64_t ld = ((int64_t)F + 3) & ~3LL;
   const int64_t rows = (int64_t)hdr[14] * ld * 4;
   const int64_t slabs = (int64_t)hdr[10] * kRB * tile_fpad(F) * 4;
@@ -1803,8 +1777,6 @@ extern "C" int64_t gcnk_spmm_workspace_bytes(const int32_t* hdr, int32_t F) {
 
 extern "C" int64_t gcnk_spmm_counter_bytes(const int32_t* hdr) {
   if (!plan_magic(hdr)) return GCNK_EARG;
-  if (hdr[0] == kHubMagic) return hub_counter_bytes(hdr);
-  if (hdr[0] == kXwMagic) return xw_counter_bytes(hdr);
   return (int64_t)hdr[7] * kMaxColTiles * 4;
 }
 
@@ -1812,12 +1784,11 @@ static int spmm_impl(const void* plan, const int32_t* hdr, const float* B, int64
                      int64_t ldc, const float* bias, int32_t epilogue, const uint8_t* drop_mask, int64_t ldm,
                      float drop_scale, float keep_prob, uint64_t seed, uint64_t offset, const uint64_t* rng_base,
                      float* workspace, int64_t workspace_bytes, int32_t* counters, int64_t counter_bytes, int32_t lanes_hint,
-                     const ProjArgs& pa, void* stream, int32_t part = 0, const HubSide* side = nullptr) {
+                     const ProjArgs& pa, void* stream, int32_t part = 0) {
   if (!plan || !plan_magic(hdr) || F < 0 || part < 0 || part > 2) {
     set_error("gcnk_spmm_csr_f32: bad argument (plan/header missing or not a gcnk plan, F=%d)", F);
     return GCNK_EARG;
   }
-  const bool hub = hdr[0] == kHubMagic;
   const int32_t M = hdr[1], K = hdr[2];
   if (M == 0 || F == 0) return GCNK_OK;
   const bool proj = pa.W != nullptr;
@@ -1825,7 +1796,7 @@ static int spmm_impl(const void* plan, const int32_t* hdr, const float* B, int64
     set_error("gcnk_spmm_proj_f32: bad projection (P=%d)", pa.P);
     return GCNK_EARG;
   }
-  if ((!C && (!proj || pa.store_main) && !(side && side->W)) || (K > 0 && !B)) {
+  if ((!C && (!proj || pa.store_main)) || (K > 0 && !B)) {
     set_error("gcnk_spmm_csr_f32: null pointer");
     return GCNK_EARG;
   }
@@ -1875,27 +1846,6 @@ static int spmm_impl(const void* plan, const int32_t* hdr, const float* B, int64
   const bool vec4 = (F % 4 == 0) && (ldb % 4 == 0) && (ldc % 4 == 0) && aligned16(B) && (!C || aligned16(C)) &&
                     (!workspace || aligned16(workspace)) && (!bias || aligned16(bias));
   hipStream_t s = (hipStream_t)stream;
-  if (side && side->nsum > 1 && !hub) {
-    set_error("gcnk_spmm_sum_csr_f32: a summed operand needs a hub plan (nsum = %d)", side->nsum);
-    return GCNK_EUNSUP;
-  }
-  if (hdr[0] == kXwMagic) {
-    if (proj || (side && (side->W || side->nsum > 1))) {
-      set_error("gcnk_spmm: fused projection / summed operand unsupported with a split plan");
-      return GCNK_EUNSUP;
-    }
-    if (part == 1) return GCNK_OK;
-    return xw_spmm(plan, hdr, B, ldb, F, C, ldc, e, workspace, counters, vec4, s);
-  }
-  if (hub) {
-    if (proj && !side) {
-      set_error("gcnk_spmm_proj_f32: a hub plan projects per column slice (gcnk_spmm_proj_sliced_f32)");
-      return GCNK_EUNSUP;
-    }
-    if (part == 1) return GCNK_OK;  // no dense tile blocks in a hub plan
-    const HubSide none;
-    return hub_spmm(plan, hdr, B, ldb, F, C, ldc, e, workspace, counters, vec4, side ? *side : none, s);
-  }
   if (proj) {
     // the projection needs whole rows in one group: row-kernel rows only, float4, one column tile
     if (hdr[8] > 0 || !vec4 || F > lpr * 4 || pa.P > 32 || lpr < 16) {
@@ -1988,58 +1938,4 @@ extern "C" int gcnk_spmm_proj_f32(const void* plan, const int32_t* hdr, const fl
   const ProjArgs pa{W, ldw, P, C2, ldc2, C != nullptr};
   return spmm_impl(plan, hdr, B, ldb, F, C, ldc, bias, epilogue, drop_mask, ldm, drop_scale, keep_prob, seed, offset,
                    rng_base, workspace, workspace_bytes, counters, counter_bytes, lanes_hint, pa, stream);
-}
-
-extern "C" int32_t gcnk_spmm_proj_slices(const int32_t* hdr, int32_t F) {
-  if (!plan_magic(hdr) || F <= 0) return GCNK_EARG;
-  if (hdr[0] != kHubMagic) return 1;
-  if (F % 4) return GCNK_EUNSUP;
-  return hub_proj_slices(hdr, F);
-}
-
-extern "C" int gcnk_spmm_proj_sliced_f32(const void* plan, const int32_t* hdr, const float* B, int64_t ldb, int32_t F,
-                                         float* C, int64_t ldc, const float* bias, int32_t epilogue,
-                                         const uint8_t* drop_mask, int64_t ldm, float drop_scale, float keep_prob,
-                                         uint64_t seed, uint64_t offset, const uint64_t* rng_base, const float* W,
-                                         int64_t ldw, int32_t P, float* C2, int64_t ldc2, int64_t c2_slice_stride,
-                                         int32_t c2_slices, float* workspace, int64_t workspace_bytes,
-                                         int32_t* counters, int64_t counter_bytes, int32_t lanes_hint, void* stream) {
-  const int32_t want = gcnk_spmm_proj_slices(hdr, F);
-  if (!W || !C2 || P <= 0 || ldw < P || ldc2 < P || want < 0 || c2_slices != want) {
-    set_error("gcnk_spmm_proj_sliced_f32: bad projection (P=%d, %d slices given, the plan writes %d)", P, c2_slices,
-              want);
-    return want == GCNK_EUNSUP ? GCNK_EUNSUP : GCNK_EARG;
-  }
-  if (hdr[0] != kHubMagic)  // one slice: the exact projection of the row kernel
-    return gcnk_spmm_proj_f32(plan, hdr, B, ldb, F, C, ldc, bias, epilogue, drop_mask, ldm, drop_scale, keep_prob,
-                              seed, offset, rng_base, W, ldw, P, C2, ldc2, workspace, workspace_bytes, counters,
-                              counter_bytes, lanes_hint, stream);
-  HubSide side;
-  side.W = W;
-  side.ldw = ldw;
-  side.P = P;
-  side.C2 = C2;
-  side.c2_stride = c2_slice_stride;
-  side.ldc2 = ldc2;
-  const ProjArgs none{nullptr, 0, 0, nullptr, 0, 1};
-  return spmm_impl(plan, hdr, B, ldb, F, C, ldc, bias, epilogue, drop_mask, ldm, drop_scale, keep_prob, seed, offset,
-                   rng_base, workspace, workspace_bytes, counters, counter_bytes, lanes_hint, none, stream, 0, &side);
-}
-
-extern "C" int gcnk_spmm_sum_csr_f32(const void* plan, const int32_t* hdr, const float* B, int64_t ldb, int32_t F,
-                                     int32_t nsum, int64_t bstride, float* C, int64_t ldc, const float* bias,
-                                     int32_t epilogue, const uint8_t* drop_mask, int64_t ldm, float drop_scale,
-                                     float keep_prob, uint64_t seed, uint64_t offset, const uint64_t* rng_base,
-                                     float* workspace, int64_t workspace_bytes, int32_t* counters,
-                                     int64_t counter_bytes, int32_t lanes_hint, void* stream) {
-  if (nsum < 1 || (nsum > 1 && bstride < 1)) {
-    set_error("gcnk_spmm_sum_csr_f32: bad operand count %d / stride %lld", nsum, (long long)bstride);
-    return GCNK_EARG;
-  }
-  HubSide side;
-  side.nsum = nsum;
-  side.bstride = bstride;
-  const ProjArgs none{nullptr, 0, 0, nullptr, 0, 1};
-  return spmm_impl(plan, hdr, B, ldb, F, C, ldc, bias, epilogue, drop_mask, ldm, drop_scale, keep_prob, seed, offset,
-                   rng_base, workspace, workspace_bytes, counters, counter_bytes, lanes_hint, none, stream, 0, &side);
 }

@@ -140,14 +140,12 @@ FUSE_BACKWARD = os.environ.get("GCNK_FUSE_BACKWARD", "1") != "0"
 def spmm_proj(a, B, W, bias=None, epilogue=_lib.EPI_NONE, mask=None, scale=1.0, keep_prob=1.0, seed=0, offset=0,
               store_main=True, ipc=None, lanes=0, rng_base=None):
     """(H, C2) with H = epi(A @ B) and C2 = H @ W, the projection fused into
-    the SpMM epilogue: gc1's aggregation + bias + ReLU + dropout (reference
-    layer.py:106,110,182,185) followed by gc2's support ``th.spmm(H1, W2)``
-    (layer.py:102) while H1's elements are in registers.  Row-unit plan
-    (gcnk_spmm_proj_f32): C2 is [M, P].  Hub plan (gcnk_spmm_proj_sliced_f32):
-    each column slice projects its own columns, C2 is [slices, M, P] whose sum
-    is H @ W -- pass it to spmm_sum.  With ``store_main=False`` H is never
-    written (returned as None).  Where no fused kernel applies (library returns
-    unsupported) the same result comes from gcnk_spmm_csr_f32 + gcnk_gemm_f32."""
+    the SpMM epilogue (gcnk_spmm_proj_f32): gc1's aggregation + bias + ReLU +
+    dropout (reference layer.py:106,110,182,185) followed by gc2's support
+    ``th.spmm(H1, W2)`` (layer.py:102) while H1's elements are in registers.
+    With ``store_main=False`` H is never written (returned as None).  Where the
+    fused kernel does not apply (library returns unsupported) the same result
+    comes from gcnk_spmm_csr_f32 + gcnk_gemm_f32."""
     a = as_csr(a)
     B = _dense_f32(B, "dense operand")
     W = _dense_f32(W, "projection")
@@ -172,24 +170,6 @@ def spmm_proj(a, B, W, bias=None, epilogue=_lib.EPI_NONE, mask=None, scale=1.0, 
     wsb = plan.workspace_bytes(F)
     ws = torch.empty((wsb + 3) // 4, dtype=torch.float32, device=B.device) if wsb > 0 else None
     cnt = plan.counters(B.device)
-    nsl = int(lib.gcnk_spmm_proj_slices(ctypes.cast(plan.hdr, ctypes.c_void_p), F)) if plan.is_hub else 1
-    if plan.is_hub and nsl > 0:
-        # the hub plan projects per column slice: C2 = sum of nsl partials,
-        # handed to the consumer as [nsl, M, P] (spmm_sum adds them in order)
-        C2 = torch.empty((nsl, M, P), dtype=torch.float32, device=B.device)
-        with torch.cuda.device(B.device):
-            rc = lib.gcnk_spmm_proj_sliced_f32(
-                _ptr(plan.buf), ctypes.cast(plan.hdr, ctypes.c_void_p),
-                _ptr(B), B.stride(0), F,
-                _ptr(H), F,
-                _ptr(bias), epilogue,
-                _ptr(mask), mask.stride(0) if mask is not None else 0, float(scale),
-                float(keep_prob), int(seed) & (2**64 - 1), int(offset) & (2**64 - 1), _ptr(rng_base),
-                _ptr(W), W.stride(0), P, _ptr(C2), P, M * P, nsl,
-                _ptr(ws), wsb, _ptr(cnt), 4 * cnt.numel() if cnt is not None else 0, int(lanes), _stream(B.device))
-        if rc != _lib.EUNSUP:
-            _lib.check(rc, "gcnk_spmm_proj_sliced_f32")
-            return H, C2
     C2 = torch.empty((M, P), dtype=torch.float32, device=B.device)
     with torch.cuda.device(B.device):
         rc = lib.gcnk_spmm_proj_f32(
@@ -254,41 +234,6 @@ def hubfactor_gc1(f, W1, b1, W2, epilogue=_lib.EPI_BIAS_RELU, mask=None, scale=1
         return None
     _lib.check(rc, "gcnk_hubfactor_gc1_f32")
     return H1, S2
-
-
-def spmm_sum(a, Bs, bias=None, epilogue=_lib.EPI_NONE, out=None, lanes=0):
-    """C = epi(A @ (Bs[0] + ... + Bs[S-1])) with Bs [S, K, F] (a sliced
-    projection from spmm_proj, summed in order as the hub plan stages its rows:
-    gcnk_spmm_sum_csr_f32).  gc2's ``th.spmm(adj, support) + bias`` (reference
-    layer.py:106,110) on the support gc1's fused projection left in slices."""
-    a = as_csr(a)
-    if Bs.dim() == 2:
-        return spmm(a, Bs, bias=bias, epilogue=epilogue, out=out, lanes=lanes)
-    require_device(Bs, "summed operand")
-    Bs = Bs.contiguous()
-    S, K, F = Bs.shape
-    if S == 1:
-        return spmm(a, Bs[0], bias=bias, epilogue=epilogue, out=out, lanes=lanes)
-    M = a.shape[0]
-    if K != a.shape[1]:
-        raise RuntimeError(f"spmm_sum shape mismatch: sparse {tuple(a.shape)} @ {tuple(Bs.shape)}")
-    if out is None:
-        out = torch.empty((M, F), dtype=torch.float32, device=Bs.device)
-    if bias is not None:
-        bias = bias.contiguous()
-    lib = _lib.load()
-    ipc = default_ipc(a, F, lanes)
-    plan = a.plan(ipc, int(lib.gcnk_spmm_groups(F, int(lanes))), DENSE_THRESHOLD)
-    wsb = plan.workspace_bytes(F)
-    ws = torch.empty((wsb + 3) // 4, dtype=torch.float32, device=Bs.device) if wsb > 0 else None
-    cnt = plan.counters(Bs.device)
-    with torch.cuda.device(Bs.device):
-        rc = lib.gcnk_spmm_sum_csr_f32(
-            _ptr(plan.buf), ctypes.cast(plan.hdr, ctypes.c_void_p), _ptr(Bs), F, F, S, K * F,
-            _ptr(out), out.stride(0), _ptr(bias), epilogue, _NULL, 0, 1.0, 1.0, 0, 0, _NULL,
-            _ptr(ws), wsb, _ptr(cnt), 4 * cnt.numel() if cnt is not None else 0, int(lanes), _stream(Bs.device))
-    _lib.check(rc, "gcnk_spmm_sum_csr_f32")
-    return out
 
 
 def default_split_k(M, N, K):
@@ -520,9 +465,8 @@ class GCNFn(torch.autograd.Function):
         H1 = drop(relu(A S1 + b1))  spmm + fused epilogue                 layer.py:106,110,182,185
         S2 = H1 W2                  skinny MFMA gemm, or fused into that   layer.py:102 (gc2)
                                     epilogue (FUSE_PROJECTION; H1 then kept
-                                    only when a backward needs it; a hub
-                                    plan leaves S2 as per-slice partials)
-        Z  = A S2 + b2              spmm (spmm_sum of the partials) + bias layer.py:106,110 (gc2)
+                                    only when a backward needs it)
+        Z  = A S2 + b2              spmm + bias                            layer.py:106,110 (gc2)
 
     Backward (trainer.py:361):
         gS2 = A^T g;
@@ -561,7 +505,7 @@ class GCNFn(torch.autograd.Function):
                       offset=offset, rng_base=rng_base)
             S2 = gemm(H1, W2)
         if out is None:
-            out = spmm_sum(adj, S2, bias=b2, epilogue=_lib.EPI_BIAS if b2 is not None else _lib.EPI_NONE)
+            out = spmm(adj, S2, bias=b2, epilogue=_lib.EPI_BIAS if b2 is not None else _lib.EPI_NONE)
         ctx.xop, ctx.adj, ctx.scale = xop, adj, float(scale)
         ctx.has_b1, ctx.has_b2 = b1 is not None, b2 is not None
         ctx.save_for_backward(W2, H1)

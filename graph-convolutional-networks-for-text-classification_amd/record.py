@@ -101,8 +101,8 @@ class ForwardRecord:
             if ops.FUSE_PROJECTION and P <= ops.FUSE_MAX_P:
                 lanes = 64
                 plan = adj.plan(ops.default_ipc(adj, F, lanes), int(lib.gcnk_spmm_groups(F, lanes)), DENSE_THRESHOLD)
-                # the fused projection runs on row-unit plans without dense tile blocks
-                kind = SPMM_PROJ if not plan.is_hub and int(plan.hdr[8]) == 0 else None
+                # the fused projection runs on plans without dense tile blocks
+                kind = SPMM_PROJ if int(plan.hdr[8]) == 0 else None
             if kind is None:
                 lanes = 0
                 plan = adj.plan(ops.default_ipc(adj, F, lanes), int(lib.gcnk_spmm_groups(F, lanes)), DENSE_THRESHOLD)
@@ -110,16 +110,12 @@ class ForwardRecord:
                 h = torch.empty((M, F), dtype=torch.float32, device=device)
                 keep.append(h)
                 s.h1_tmp, s.ld_h1_tmp = h.data_ptr(), F
-            if plan.is_hub:
-                raise _Unsupported("hub plans are issued op by op")
             _fill_plan(s.aF, plan, F, lanes, device, keep)
             keep.append(plan)
         # the first product S1 = X W1 (factored: S_T = X_hubs W1)
         if x_csr is not None:
             rows, cols = x_csr.shape
             xp = x_csr.plan(ops.default_ipc(x_csr, F, 0), int(lib.gcnk_spmm_groups(F, 0)), DENSE_THRESHOLD)
-            if xp.is_hub:
-                raise _Unsupported("hub plans are issued op by op")
             _fill_plan(s.x, xp, F, 0, device, keep)
             keep.append(xp)
         else:
@@ -138,10 +134,8 @@ class ForwardRecord:
         s2 = torch.empty((M, P), dtype=torch.float32, device=device)
         keep += [s1, s2]
         s.s1, s.lds1, s.s2, s.lds2 = s1.data_ptr(), F, s2.data_ptr(), P
-        # gc2's aggregation A S2 + b2 (ops.spmm_sum with a 2-D S2 -> ops.spmm, lanes 0)
+        # gc2's aggregation A S2 + b2 (ops.spmm, lanes 0)
         aP = adj.plan(ops.default_ipc(adj, P, 0), int(lib.gcnk_spmm_groups(P, 0)), DENSE_THRESHOLD)
-        if aP.is_hub:
-            raise _Unsupported("hub plans are issued op by op")
         _fill_plan(s.aP, aP, P, 0, device, keep)
         keep.append(aP)
         s.kind = kind
@@ -164,17 +158,12 @@ class ForwardRecord:
         return out, H1
 
 
-class _Unsupported(Exception):
-    pass
-
-
 _lock = threading.Lock()
 
 
 def get(adj, xop, F, P, device):
     """(record, stream): the ForwardRecord of (adj, X, F, P) for torch's current
-    stream, built on first use (None where the forward is issued op by op:
-    hub plans), and that stream."""
+    stream, built on first use, and that stream."""
     stream = torch.cuda.current_stream(device).cuda_stream
     src = xop.csr if xop.csr is not None else xop.dense
     key = (id(src), F, P, stream, ops.FACTOR_GC1, ops.FUSE_PROJECTION)
@@ -188,10 +177,7 @@ def get(adj, xop, F, P, device):
     if hit is not None and hit[0] is src and _version(src) == hit[1]:
         return hit[2], stream
     with _lock:
-        try:
-            rec = ForwardRecord(adj, xop, F, P, device)
-        except _Unsupported:
-            rec = None
+        rec = ForwardRecord(adj, xop, F, P, device)
         while len(recs) >= 8:
             recs.pop(next(iter(recs)))
         recs[key] = (src, _version(src), rec)

@@ -11,8 +11,8 @@ class) and later calls hit the cache.
 
 HBM layout of one CSR operand (M rows, K cols, nnz nonzeros):
   rowptr int32[M+1] | colind int32[nnz] | val fp32[nnz]
-  plan   int32[...]  hub-split plan, or row units + dense tile blocks (include/gcnk.h),
-                     one per (ipc, groups, threshold, hub options)
+  plan   int32[...]  row units + dense tile blocks (include/gcnk.h),
+                     one per (ipc, groups, dense threshold)
 """
 import collections
 import ctypes
@@ -38,38 +38,20 @@ def require_device(t, what):
 
 
 DENSE_THRESHOLD = 0.25  # row blocks at least this dense (condensed) run on the MFMA tile path
-# hub plan (csrc/hub.hip) for operands with its structure (a contiguous range
-# of heavy hub rows; every other row references only hub columns and its own
-# diagonal -- the reference's doc-topic adjacency): 0 = automatic hub
-# threshold, > 0 = degree threshold, < 0 = never (row-unit + tile plan).
-# Off by default: on R8 A-hat the in-launch combine of the hub partials costs
-# more than it saves (profiles/r03_hub.md: 20.0 us at F = 200 vs the row plan's
-# 10.4 us), so the row-unit plan stays the product path.
-HUB_MIN = -1
-HUB_BLOCK_ROWS = 0      # light rows per hub-plan group (0 = automatic, ~256 workgroups)
-# split plan (csrc/xw.hip) for operands with a contiguous range of dense rows
-# among rows that use a few "hot" columns (the reference's topic features X
-# and X^T); False leaves them to the row-unit + tile plan.  Off by default:
-# its in-launch split-K combine made R8 X W1 37.6 us against the tile plan's
-# ~12 us (profiles/r03_forward.md)
-SPLIT_PLAN = False
-
 
 class Plan:
     """A built SpMM plan: device buffer + the 16-word host header (gcnk.h).
 
-    Plans with arrival counters (row-unit plans with multi-segment heavy rows;
-    hub plans, whose hub rows are combined inside the launch) need a COUNTER
-    REGION (gcnk_spmm_counter_bytes): zeroed once, then used by one stream's
-    calls in order -- the kernels keep it valid for the next call, so it is
-    never cleared again.  One region per stream for eager calls; calls
+    Plans with arrival counters (heavy rows of several segments, combined
+    inside the launch) need a COUNTER REGION (gcnk_spmm_counter_bytes):
+    zeroed once, then used by one stream's calls in order -- the kernels leave
+    it zero for the next call, so it is never cleared again.  One region per stream for eager calls; calls
     captured into a hipGraph take one region per capturing stream (every
     graph captured there shares it: their replays must not run concurrently
     on two streams), handed out from SPARE_REGIONS regions zeroed when the
     plan is built, so a captured graph holds no memset node."""
 
     __slots__ = ("buf", "hdr", "_counters", "_spares", "_captured", "_lock")
-    HUB_MAGIC = 0x474e4832
     SPARE_REGIONS = 16   # pre-zeroed regions handed to capturing streams
 
     def __init__(self, buf, hdr):
@@ -82,10 +64,6 @@ class Plan:
     @property
     def header(self):
         return list(self.hdr)
-
-    @property
-    def is_hub(self):
-        return self.hdr[0] == self.HUB_MAGIC
 
     def workspace_bytes(self, F):
         return int(_lib.load().gcnk_spmm_workspace_bytes(ctypes.cast(self.hdr, ctypes.c_void_p), int(F)))
@@ -149,13 +127,9 @@ class CSR:
         return f"CSR(shape={self.shape}, nnz={self.nnz}, device={self.device})"
 
     # -- hybrid plan (gcnk_spmm_plan_build), one per (ipc, groups, dense threshold) -------
-    def plan(self, ipc, groups, dense_threshold=DENSE_THRESHOLD, hub_min=None, block_rows=None):
+    def plan(self, ipc, groups, dense_threshold=DENSE_THRESHOLD):
         """Returns a Plan (device buffer + host header); built once per key (setup sync)."""
-        hub_min = HUB_MIN if hub_min is None else int(hub_min)
-        block_rows = HUB_BLOCK_ROWS if block_rows is None else int(block_rows)
-        if not SPLIT_PLAN:
-            dense_threshold = -abs(dense_threshold)   # gcnk.h: negative = tile path only, no split plan
-        key = (ipc, groups, float(dense_threshold), hub_min, block_rows, SPLIT_PLAN)
+        key = (ipc, groups, float(dense_threshold))
         p = self._plans.get(key)
         if p is not None:
             return p
@@ -168,14 +142,13 @@ class CSR:
             with torch.cuda.device(self.device):
                 s = _stream_ptr(self.device)
                 nbytes = lib.gcnk_spmm_plan_bytes(self.rowptr.data_ptr(), self.colind.data_ptr(), M, K, self.nnz,
-                                                  ipc, groups, float(dense_threshold), hub_min, block_rows, s)
+                                                  ipc, groups, float(dense_threshold), s)
                 if nbytes < 0:
                     _lib.check(int(nbytes), "gcnk_spmm_plan_bytes")
                 buf = torch.empty((nbytes + 3) // 4, dtype=torch.int32, device=self.device)
                 _lib.check(lib.gcnk_spmm_plan_build(self.rowptr.data_ptr(), self.colind.data_ptr(),
                                                     self.val.data_ptr(), M, K, self.nnz, ipc, groups,
-                                                    float(dense_threshold), hub_min, block_rows, buf.data_ptr(),
-                                                    nbytes, s),
+                                                    float(dense_threshold), buf.data_ptr(), nbytes, s),
                            "gcnk_spmm_plan_build")
                 hdr = (ctypes.c_int32 * 16)()
                 _lib.check(lib.gcnk_spmm_plan_query(buf.data_ptr(), ctypes.cast(hdr, ctypes.c_void_p), s),

@@ -86,23 +86,8 @@ const char* gcnk_last_error(void);
  * Replaces th.spmm(adj, support) (layer.py:106) and th.spmm(X, W)
  * (layer.py:102, sparse X) and their autograd (A^T g, X^T g).
  *
- * The operand is converted once (gcnk_spmm_plan_build) into one of two plans:
- *
- *  HUB plan (header magic 'GNH2') -- square operands whose rows of degree
- *  >= hub_min (0 = automatic: max(64, 8 x mean degree)) form ONE contiguous
- *  range of at most 256 "hub" rows and whose other ("light") rows reference
- *  only hub columns and their own diagonal: the reference's doc-topic
- *  adjacency (R8: 50 topic rows of 191..1807 nonzeros after 7,674 document
- *  rows of 2..14).  Light rows are cut into G groups of `block_rows`
- *  consecutive rows (0 = automatic: ~256 workgroups per launch) and F into
- *  column slices; workgroup (group, slice) stages its rows' and the hub rows'
- *  slices of B plus its group's record in LDS (LDS-DMA, addresses from the
- *  workgroup index), computes its light rows, and one partial per hub row from
- *  the same image (the hub rows transposed).  The hub rows are combined inside
- *  the launch: the last workgroups of each slice to finish sum the G partials
- *  in group order (arrival counters in the counter region).  One launch.
- *
- *  ROW-UNIT + TILE plan (magic 'GNK5') -- every other operand:
+ * The operand is converted once (gcnk_spmm_plan_build) into a ROW-UNIT + TILE
+ * plan (magic 'GNK5'):
  *  - dense blocks: rows are grouped by off-diagonal degree class (factor-8
  *    buckets, row order within a class) into blocks of 64; a block whose
  *    nonzeros fill >= dense_threshold of its condensed column set (and use
@@ -113,17 +98,6 @@ const char* gcnk_last_error(void);
  *    epilogue; multi-chunk blocks are summed from partial slabs in order.
  *    dense_threshold > 1 disables the part (default callers pass 0.25).
  *
- *  SPLIT plan (magic 'GNX1') -- operands whose rows of more than 64 nonzeros
- *  form ONE contiguous range of at most 128 dense rows and whose other rows
- *  use at most 64 distinct ("hot") columns, each at least a quarter full:
- *  the reference's topic features X (R8: 7,674 document rows over the 50
- *  topic columns, 50 dense topic rows) and X^T.  The light rows are stored
- *  densely over the hot columns and multiplied on fp32 MFMA with W's hot rows
- *  staged in LDS once per 32-row block; the dense rows run as split-K chunks
- *  on MFMA whose partials the last workgroups of each column slice sum in
- *  chunk order inside the launch (counter region).  One launch; epilogue
- *  GCNK_EPI_NONE only.  Tried when 0 < dense_threshold <= 1; a NEGATIVE
- *  dense_threshold skips it (|dense_threshold| then drives the tile part).
  *  - row units: the other rows.  A row of at most `ipc` nonzeros is one unit
  *    owned by one lane group (LPR lanes, each a 16-B column vector); a
  *    heavier row is cut into segments of about ipc * groups nonzeros (at most
@@ -134,7 +108,6 @@ const char* gcnk_last_error(void);
  *    finish (arrival counters in the caller's COUNTER REGION: int32
  *    gcnk_spmm_counter_bytes(header) bytes, zero on entry and left zero on
  *    return) sums them in segment order.
- * hub_min < 0 forces the row-unit plan.
  * All sums have a fixed order (no float atomics): bitwise reproducible.
  * gcnk_spmm_groups(F, lanes_hint) gives the `groups` the kernels use for a
  * width F; a plan serves every F with that count.  The plan copies the
@@ -143,40 +116,36 @@ const char* gcnk_last_error(void);
  * same plan image from HOST arrays into host memory (no device needed).
  *
  * Plan header (16 int32, first words of the plan; gcnk_spmm_plan_query):
- *   row-unit plan: 0 magic 'GNK5'  1 M  2 K  3 groups  4 ipc  5 row units
+ *   0 magic 'GNK5'  1 M  2 K  3 groups  4 ipc  5 row units
  *   6 heavy segments  7 heavy rows of > 1 segment  8 tile chunks
  *   9 multi-chunk blocks  10 slabs  11 tile blocks  12 diagonal kept aside
  *   (0/1)  13 nnz  14 partial slots  15 chunk items of single-chunk tile blocks
- *   hub plan: 0 magic 'GNH2'  1 M  2 K  3 groups  4 row groups G  5 record
- *   stride (words)  6 hub rows H  7 first hub row  8 light rows  9 nnz
- *   10 light rows per group  11 hub degree threshold  12 max record items
- *   13 max hub batches per record  14..15 0
+ * (Rounds 2-3 also built a hub-split plan and a split-K plan for R8's doc-topic
+ * operands; both measured slower than this plan and were removed in ABI 8 --
+ * DESIGN.md keeps their numbers.)
  * ------------------------------------------------------------------------- */
 int32_t gcnk_spmm_groups(int32_t F, int32_t lanes_hint);
 int32_t gcnk_spmm_default_ipc(int32_t M, int64_t nnz, int32_t F, int32_t lanes_hint);
 /* Size of the plan buffer (synchronises `stream`; negative error code on failure). */
 int64_t gcnk_spmm_plan_bytes(const int32_t* rowptr, const int32_t* colind, int32_t M, int32_t K,
-                             int64_t nnz, int32_t ipc, int32_t groups, float dense_threshold,
-                             int32_t hub_min, int32_t block_rows, void* stream);
+                             int64_t nnz, int32_t ipc, int32_t groups, float dense_threshold, void* stream);
 int gcnk_spmm_plan_build(const int32_t* rowptr, const int32_t* colind, const float* val, int32_t M,
                          int32_t K, int64_t nnz, int32_t ipc, int32_t groups, float dense_threshold,
-                         int32_t hub_min, int32_t block_rows, void* plan, int64_t plan_bytes, void* stream);
+                         void* plan, int64_t plan_bytes, void* stream);
 /* The same from HOST arrays into a HOST buffer (plan-layout checks without a GPU). */
 int64_t gcnk_spmm_plan_bytes_host(const int32_t* rowptr, const int32_t* colind, int32_t M, int32_t K,
-                                  int64_t nnz, int32_t ipc, int32_t groups, float dense_threshold,
-                                  int32_t hub_min, int32_t block_rows);
+                                  int64_t nnz, int32_t ipc, int32_t groups, float dense_threshold);
 int gcnk_spmm_plan_build_host(const int32_t* rowptr, const int32_t* colind, const float* val, int32_t M,
                               int32_t K, int64_t nnz, int32_t ipc, int32_t groups, float dense_threshold,
-                              int32_t hub_min, int32_t block_rows, int32_t* plan, int64_t plan_bytes);
+                              int32_t* plan, int64_t plan_bytes);
 /* Copies the 16-word plan header to host memory `out16` and synchronises
  * `stream` (one-time setup).  Every SpMM call takes this host header. */
 int gcnk_spmm_plan_query(const void* plan, int32_t* out16, void* stream);
-/* Bytes of workspace (split-row partials, tile slabs, hub partials) an SpMM of width F needs. */
+/* Bytes of workspace (split-row partials, tile slabs) an SpMM of width F needs. */
 int64_t gcnk_spmm_workspace_bytes(const int32_t* plan_header, int32_t F);
 /* Bytes of the counter region a call needs (0: none).  The region is zeroed
  * ONCE by the caller and then used by calls on one stream in order (never
- * concurrently by two calls): the kernels keep it valid for the next call
- * (row-unit plan: left zero; hub plan: per-slice launch counts). */
+ * concurrently by two calls): the kernels leave it zero for the next call. */
 int64_t gcnk_spmm_counter_bytes(const int32_t* plan_header);
 
 /* C = epi(A B) for the operand of `plan` (M x K from the header). */
@@ -226,40 +195,6 @@ int gcnk_spmm_proj_f32(const void* plan, const int32_t* plan_header,
                        float* workspace, int64_t workspace_bytes,
                        int32_t* counters, int64_t counter_bytes,
                        int32_t lanes_hint, void* stream);
-
-/* The fused projection for plans that split F into column slices (the hub
- * plan): slice s of the launch writes the P-wide partial over its columns,
- *   C2_s[M x P] = H[:, slice s] * W[slice s, :],   C2_s at C2 + s * c2_slice_stride,
- * so C2 = H W = sum over s of C2_s (summed in order by the consumer,
- * gcnk_spmm_sum_csr_f32 -- gc2's A-hat S2 of layer.py:106 takes S2 this way).
- * gcnk_spmm_proj_slices(header, F) gives the slice count (1 for a row-unit
- * plan, whose fused projection is exact: gcnk_spmm_proj_f32); c2_slices must
- * equal it.  H is stored only when C != NULL.  P <= 8 on a hub plan. */
-int32_t gcnk_spmm_proj_slices(const int32_t* plan_header, int32_t F);
-int gcnk_spmm_proj_sliced_f32(const void* plan, const int32_t* plan_header,
-                              const float* B, int64_t ldb, int32_t F,
-                              float* C, int64_t ldc,
-                              const float* bias, int32_t epilogue,
-                              const uint8_t* drop_mask, int64_t ldm, float drop_scale,
-                              float keep_prob, uint64_t seed, uint64_t offset, const uint64_t* rng_base,
-                              const float* W, int64_t ldw, int32_t P,
-                              float* C2, int64_t ldc2, int64_t c2_slice_stride, int32_t c2_slices,
-                              float* workspace, int64_t workspace_bytes,
-                              int32_t* counters, int64_t counter_bytes,
-                              int32_t lanes_hint, void* stream);
-
-/* C = epi(A (B_0 + ... + B_{nsum-1})), B_s at B + s * bstride (each [K x F],
- * leading dimension ldb), summed in order as rows are staged: the consumer of
- * a sliced projection.  nsum > 1 needs a hub plan (else GCNK_EUNSUP). */
-int gcnk_spmm_sum_csr_f32(const void* plan, const int32_t* plan_header,
-                          const float* B, int64_t ldb, int32_t F, int32_t nsum, int64_t bstride,
-                          float* C, int64_t ldc,
-                          const float* bias, int32_t epilogue,
-                          const uint8_t* drop_mask, int64_t ldm, float drop_scale,
-                          float keep_prob, uint64_t seed, uint64_t offset, const uint64_t* rng_base,
-                          float* workspace, int64_t workspace_bytes,
-                          int32_t* counters, int64_t counter_bytes,
-                          int32_t lanes_hint, void* stream);
 
 /* ---------------------------------------------------------------------------
  * fp32 GEMM on MFMA (v_mfma_f32_16x16x4_f32; exact fp32 FMA chains):

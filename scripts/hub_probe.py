@@ -1,9 +1,10 @@
-"""North-star op probe: R8 A-hat x S (F = 200, bias + ReLU) and F = 8 under
-plan variants, warm (same buffers back to back) and cold (rotating > 256 MB of
-distinct B / C sets, so no launch finds its operands in the Infinity Cache),
-with parity against the float64 oracle.  One JSON line per variant.
+"""North-star op probe: R8 A-hat x S (F = 200, bias + ReLU) and F = 8 on the
+row plan (and the streaming floor "copy"), warm (same buffers back to back)
+and cold (rotating > 256 MB of distinct B / C sets, so no launch finds its
+operands in the Infinity Cache), with parity against the float64 oracle.  One
+JSON line per variant.
 
-  python scripts/hub_probe.py [--reps 200] [--variants hub,row,hub16,...]
+  python scripts/hub_probe.py [--reps 200] [--variants row,copy]
 """
 import argparse
 import json
@@ -21,13 +22,7 @@ from graph_convolutional_networks_for_text_classification_amd import _lib, datas
 from graph_convolutional_networks_for_text_classification_amd.sparse import from_torch  # noqa: E402
 from oracle import csr_ref  # noqa: E402
 
-VARIANTS = {
-    "row": dict(hub_min=-1),
-    "hub": dict(hub_min=0, block_rows=0),      # hub plan, automatic rows per group (R8 F = 200: 240)
-    "hub60": dict(hub_min=0, block_rows=60),
-    "hub120": dict(hub_min=0, block_rows=120),
-    "hub480": dict(hub_min=0, block_rows=480),
-}
+VARIANTS = {"row": {}}
 
 
 def spmm_bytes(M, K, nnz, F):
@@ -64,7 +59,7 @@ def time_graph(fns, reps_per_fn):
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--reps", type=int, default=100)
-    ap.add_argument("--variants", default="row,hub,hub60,hub120,hub480")
+    ap.add_argument("--variants", default="row,copy")
     ap.add_argument("--widths", default="200,8")
     ap.add_argument("--graph", default="r8", choices=["r8", "20ng"])
     ap.add_argument("--mode", default="both", choices=["warm", "cold", "both"],
@@ -97,16 +92,13 @@ def main():
                 print(json.dumps({"graph": args.graph, "F": F, "variant": "copy", "bytes": 8 * M * F,
                                   "warm_us": round(warm, 3), "cold_us": round(cold, 3), "sets": nsets}), flush=True)
                 continue
-            kw = VARIANTS[name]
-            import graph_convolutional_networks_for_text_classification_amd.sparse as sp
-            saved = sp.HUB_MIN, sp.HUB_BLOCK_ROWS
-            sp.HUB_MIN, sp.HUB_BLOCK_ROWS = kw.get("hub_min", 0), kw.get("block_rows", 0)
+            assert name in VARIANTS, name
             out = ops.spmm(a, Bs[0], bias=bias, epilogue=_lib.EPI_BIAS_RELU)
             torch.cuda.synchronize()
             err = float(np.abs(out.cpu().numpy().astype(np.float64) - ref).max())
             again = ops.spmm(a, Bs[0], bias=bias, epilogue=_lib.EPI_BIAS_RELU)
             det = bool(torch.equal(out, again))
-            plan = [p for k, p in a._plans.items() if k[3] == sp.HUB_MIN and k[4] == sp.HUB_BLOCK_ROWS][-1]
+            plan = list(a._plans.values())[-1]
             warm = cold = float("nan")
             if args.mode in ("warm", "both"):
                 warm = time_graph([lambda: ops.spmm(a, Bs[0], bias=bias, epilogue=_lib.EPI_BIAS_RELU, out=Cs[0])],
@@ -115,12 +107,11 @@ def main():
                    for i in range(nsets)]
             if args.mode in ("cold", "both"):
                 cold = time_graph(fns, max(1, args.reps // nsets))
-            print(json.dumps({"graph": args.graph, "F": F, "variant": name, "hub": plan.is_hub,
+            print(json.dumps({"graph": args.graph, "F": F, "variant": name,
                               "hdr": plan.header, "max_err": err, "deterministic": det,
                               "warm_us": round(warm, 3), "cold_us": round(cold, 3),
                               "warm_frac": nbytes / (warm * 1e-6) / 8e12, "cold_frac": nbytes / (cold * 1e-6) / 8e12,
                               "sets": nsets}), flush=True)
-            sp.HUB_MIN, sp.HUB_BLOCK_ROWS = saved
 
 
 if __name__ == "__main__":

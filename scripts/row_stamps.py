@@ -34,7 +34,6 @@ def main():
     lib = _lib.load()
     r8 = datasets.load_r8_fixture(os.path.join(ROOT, "tests", "golden", "r8_graph.npz"))
     A = sp.as_csr(r8["adj"].to(dev))
-    sp.HUB_MIN = -1  # the row plan
     for F in [int(x) for x in (sys.argv[1:] or ["200"])]:
         # cold: a fresh operand set per timed call (sets span > the 256 MB MALL)
         nsets = max(7, -(-300_000_000 // (8 * A.shape[0] * F)))

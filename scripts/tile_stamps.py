@@ -31,7 +31,6 @@ def main():
     dev = torch.device("cuda", 0)
     lib = _lib.load()
     r8 = datasets.load_r8_fixture(os.path.join(ROOT, "tests", "golden", "r8_graph.npz"))
-    sp.SPLIT_PLAN = False   # the tile plan
     X = sp.as_csr(r8["features"].to(dev))
     nsets = 28              # cold: operand sets span > the 256 MB MALL
     Ws = [torch.randn(r8["nfeat"], 200, device=dev) for _ in range(nsets)]

@@ -59,7 +59,7 @@ def test_argument_validation_without_gpu():
                            ctypes.c_void_p(16), 4, None, 0, None, 0, 1.0, 8, None, 0, None)
     assert rc == _lib.EARG
     # plan build without operands
-    rc = lib.gcnk_spmm_plan_build(ctypes.c_void_p(16), None, None, 10, 10, 100, 8, 4, 0.25, 0, 0, ctypes.c_void_p(16),
+    rc = lib.gcnk_spmm_plan_build(ctypes.c_void_p(16), None, None, 10, 10, 100, 8, 4, 0.25, ctypes.c_void_p(16),
                                   4, None)
     assert rc == _lib.EARG
     # a header that is not a plan's is refused

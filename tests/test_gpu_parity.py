@@ -48,13 +48,6 @@ def _random_csr(M, K, nnz, rng, heavy_rows=(), heavy_deg=0, empty_frac=0.0):
     return csr_ref.coo_to_csr(rows, cols, vals, (M, K))
 
 
-@pytest.fixture
-def hub_on(monkeypatch):
-    """The hub plan is opt-in (sparse.HUB_MIN = -1 by default); its tests turn it on."""
-    from graph_convolutional_networks_for_text_classification_amd import sparse as sp
-    monkeypatch.setattr(sp, "HUB_MIN", 0)
-
-
 def test_native_library_is_loaded():
     lib = _lib.load()
     assert lib.gcnk_abi_version() == _lib.ABI_VERSION
@@ -73,15 +66,7 @@ def test_spmm_r8_adjacency(r8, F):
     _close(got, ref)
     # low dense threshold: document rows run as MFMA tiles over the 50 topic
     # columns with the self loop kept aside (diagonal epilogue)
-    # row-unit + tile plan (hub plan off)
-    from graph_convolutional_networks_for_text_classification_amd import sparse as sp
-    saved = sp.HUB_MIN
-    sp.HUB_MIN = -1
-    try:
-        _close(spmm(a, B.to(DEV)), ref)
-        got_t = spmm(a, B.to(DEV), dense=0.05)
-    finally:
-        sp.HUB_MIN = saved
+    got_t = spmm(a, B.to(DEV), dense=0.05)
     _close(got_t, ref)
     hdr = [p for k, p in a._plans.items() if abs(k[2]) == 0.05][0].header
     assert hdr[8] > 0 and hdr[12] == 1, "R8 document rows: MFMA tiles over the topic columns + diagonal"
@@ -204,79 +189,15 @@ def test_csr_to_dense_sums_duplicates_in_order():
     assert np.array_equal(out2.cpu().numpy(), want2)
 
 
-SPLIT_MAGIC = 0x474E5831
-
-
-@pytest.fixture
-def split_on(monkeypatch):
-    """The split plan is opt-in (sparse.SPLIT_PLAN = False by default)."""
-    from graph_convolutional_networks_for_text_classification_amd import sparse as sp
-    monkeypatch.setattr(sp, "SPLIT_PLAN", True)
-
-
-@pytest.mark.parametrize("F", [200, 8, 64, 100, 257, 300])
-def test_spmm_r8_features_split_plan(r8, F, split_on):
-    """R8 X W1 (layer.py:102) and X^T G (its autograd) on the split plan: the
-    document / feature rows over 50 hot columns on MFMA, the 50 dense rows as
-    split-K chunks summed in order inside the launch; float4 and scalar paths."""
-    x = from_torch(r8["features"].to(DEV))
-    rng = np.random.default_rng(F)
-    W = torch.from_numpy(rng.standard_normal((r8["nfeat"], F)).astype(np.float32))
-    got = spmm(x, W.to(DEV))
-    hdr = list(x._plans.values())[0].header
-    assert hdr[0] == SPLIT_MAGIC and hdr[7] == 50 and hdr[8] == r8["ndoc"] and hdr[5] == 50
-    rp, ci, v = (t.cpu().numpy() for t in (x.rowptr, x.colind, x.val))
-    _close(got, csr_ref.spmm_csr(rp, ci, v, W.numpy()), atol=1e-4)
-    assert torch.equal(got, spmm(x, W.to(DEV)))
-    xt = x.t()
-    G = torch.from_numpy(rng.standard_normal((r8["nodes"], F)).astype(np.float32))
-    gt = spmm(xt, G.to(DEV))
-    ht = list(xt._plans.values())[0].header
-    assert ht[0] == SPLIT_MAGIC and ht[7] == 50 and ht[8] == 0, "X^T: features 0..49 are the dense rows"
-    rpt, cit, vt = (t.cpu().numpy() for t in (xt.rowptr, xt.colind, xt.val))
-    _close(gt, csr_ref.spmm_csr(rpt, cit, vt, G.numpy()), atol=2e-4)
-
-
-@pytest.mark.parametrize("F", [16, 200])
-def test_spmm_split_plan_synthetic(F, split_on):
-    """Split plan on a synthetic operand: dense rows in the middle, light rows
-    over 37 hot columns with empty rows and duplicates summed, rectangular."""
-    rng = np.random.default_rng(F + 5)
-    M, K = 3000, 4100
-    hot = np.sort(rng.choice(K, 37, replace=False))
-    rows, cols = [], []
-    for r in range(M):
-        if 1200 <= r < 1270:
-            c = rng.choice(K, 3000, replace=False)
-        elif r % 11 == 0:
-            continue
-        else:
-            c = rng.choice(hot, int(rng.integers(15, 40)), replace=True)   # duplicates summed; >= 1/4 full
-        rows.append(np.full(len(c), r))
-        cols.append(c)
-    rows, cols = np.concatenate(rows), np.concatenate(cols)
-    vals = rng.standard_normal(rows.size).astype(np.float32)
-    rp, ci, v = csr_ref.coo_to_csr(rows, cols, vals, (M, K))
-    a = from_arrays(rp, ci, v, (M, K), DEV)
-    B = rng.standard_normal((K, F)).astype(np.float32)
-    got = spmm(a, torch.from_numpy(B).to(DEV))
-    hdr = list(a._plans.values())[0].header
-    assert hdr[0] == SPLIT_MAGIC and hdr[7] == 70 and hdr[8] == 1200
-    _close(got, csr_ref.spmm_csr(rp, ci, v, B), atol=2e-5 * np.sqrt(3000))
 
 
 @pytest.mark.parametrize("P", [1, 8, 20, 33])
 @pytest.mark.parametrize("store_main", [True, False])
-@pytest.mark.parametrize("kind", ["hub", "row"])
-def test_spmm_fused_projection(r8, P, store_main, kind, monkeypatch):
-    """H = relu(A S + b) * dropout, S2 = H W2 in one pass: the row-unit plan's
-    gcnk_spmm_proj_f32 ([M, P]) and the hub plan's per-slice projection
-    (gcnk_spmm_proj_sliced_f32: [slices, M, P] summing to H W2, P <= 8); wider
-    P exercises the unfused fallback.  Then the consumer: A (sum of the slices)
-    + b2 (spmm_sum / gcnk_spmm_sum_csr_f32) against the oracle."""
-    from graph_convolutional_networks_for_text_classification_amd import sparse as sp
-    from graph_convolutional_networks_for_text_classification_amd.ops import spmm_proj, spmm_sum
-    monkeypatch.setattr(sp, "HUB_MIN", 0 if kind == "hub" else -1)
+def test_spmm_fused_projection(r8, P, store_main):
+    """H = relu(A S + b) * dropout, S2 = H W2 in one pass (gcnk_spmm_proj_f32,
+    [M, P]); wider P exercises the unfused fallback.  Then the consumer:
+    A S2 + b2 against the oracle."""
+    from graph_convolutional_networks_for_text_classification_amd.ops import spmm_proj
     a = from_torch(r8["adj"].to(DEV))
     rng = np.random.default_rng(P)
     N, F = r8["nodes"], 200
@@ -288,9 +209,6 @@ def test_spmm_fused_projection(r8, P, store_main, kind, monkeypatch):
     H, S2 = spmm_proj(a, torch.from_numpy(S).to(DEV), torch.from_numpy(W).to(DEV), bias=torch.from_numpy(b).to(DEV),
                       epilogue=_lib.EPI_BIAS_RELU_DROP, mask=torch.from_numpy(mask).to(DEV), scale=2.0,
                       store_main=store_main)
-    assert list(a._plans.values())[-1].is_hub == (kind == "hub")
-    if kind == "hub" and P <= 8:
-        assert S2.dim() == 3 and S2.shape[0] == 7, "F = 200: 7 column slices, one partial each"
     rp, ci, v = (t.cpu().numpy() for t in (a.rowptr, a.colind, a.val))
     Href = csr_ref.spmm_epilogue(csr_ref.spmm_csr(rp, ci, v, S), b, relu=True, mask=mask, scale=2.0)
     if store_main:
@@ -298,29 +216,10 @@ def test_spmm_fused_projection(r8, P, store_main, kind, monkeypatch):
     else:
         assert H is None
     S2ref = Href @ W.astype(np.float64)
-    _close(S2.sum(0) if S2.dim() == 3 else S2, S2ref, atol=2e-4)
-    Z = spmm_sum(a, S2, bias=torch.from_numpy(b2).to(DEV), epilogue=_lib.EPI_BIAS)
+    _close(S2, S2ref, atol=2e-4)
+    Z = spmm(a, S2, bias=torch.from_numpy(b2).to(DEV), epilogue=_lib.EPI_BIAS)
     _close(Z, csr_ref.spmm_epilogue(csr_ref.spmm_csr(rp, ci, v, S2ref), b2), atol=4e-4)
-    assert torch.equal(Z, spmm_sum(a, S2, bias=torch.from_numpy(b2).to(DEV), epilogue=_lib.EPI_BIAS))
-
-
-@pytest.mark.parametrize("nsum", [2, 7, 13])
-@pytest.mark.parametrize("F", [8, 64])
-def test_spmm_sum_of_operands(r8, nsum, F, hub_on):
-    """gcnk_spmm_sum_csr_f32: C = A (B_0 + ... + B_{n-1}) + b on the hub plan,
-    the operands summed in order while staged."""
-    from graph_convolutional_networks_for_text_classification_amd.ops import spmm_sum
-    a = from_torch(r8["adj"].to(DEV))
-    rng = np.random.default_rng(nsum * F)
-    Bs = rng.standard_normal((nsum, r8["nodes"], F)).astype(np.float32)
-    b = rng.standard_normal(F).astype(np.float32)
-    got = spmm_sum(a, torch.from_numpy(Bs).to(DEV), bias=torch.from_numpy(b).to(DEV), epilogue=_lib.EPI_BIAS)
-    assert list(a._plans.values())[-1].is_hub
-    Bsum = Bs[0].astype(np.float32)
-    for k in range(1, nsum):
-        Bsum = (Bsum + Bs[k]).astype(np.float32)      # the kernel's fp32 order
-    rp, ci, v = (t.cpu().numpy() for t in (a.rowptr, a.colind, a.val))
-    _close(got, csr_ref.spmm_epilogue(csr_ref.spmm_csr(rp, ci, v, Bsum), b), atol=5e-5)
+    assert torch.equal(Z, spmm(a, S2, bias=torch.from_numpy(b2).to(DEV), epilogue=_lib.EPI_BIAS))
 
 
 def test_spmm_deterministic():
@@ -332,31 +231,26 @@ def test_spmm_deterministic():
     assert torch.equal(o1, o2)
 
 
-@pytest.mark.parametrize("kind", ["hub", "row"])
-def test_spmm_two_streams_share_one_plan_concurrently(r8, kind, monkeypatch):
+@pytest.mark.parametrize("kind", ["r8", "random"])
+def test_spmm_two_streams_share_one_plan_concurrently(r8, kind):
     """Reentrancy (gcnk.h threading contract): two streams run SpMMs on the same
     cached operand at the same time, with different inputs and outputs.  The
-    hub plan has no cross-call state; the row-unit plan's heavy-row arrival
-    counters live in a per-stream region (sparse.Plan.counters), so neither can
-    corrupt the other: every output equals the single-stream result bit for bit."""
-    from graph_convolutional_networks_for_text_classification_amd import sparse as sp
+    heavy-row arrival counters live in a per-stream region
+    (sparse.Plan.counters), so neither can corrupt the other: every output
+    equals the single-stream result bit for bit."""
     rng = np.random.default_rng(17)
-    if kind == "hub":
-        monkeypatch.setattr(sp, "HUB_MIN", 0)
+    if kind == "r8":
         a, K = from_torch(r8["adj"].to(DEV)), r8["nodes"]
-    else:   # row-unit plan with multi-segment heavy rows (hub plan and tile path off)
-        monkeypatch.setattr(sp, "HUB_MIN", -1)
+    else:   # multi-segment heavy rows (tile path off)
         M, K = 3001, 20003
         rp, ci, v = _random_csr(M, K, 20000, rng, heavy_rows=(5, 1700, 3000), heavy_deg=2500)
         a = from_arrays(rp, ci, v, (M, K), DEV)
     F = 200
     Bs = [torch.from_numpy(rng.standard_normal((K, F)).astype(np.float32)).to(DEV) for _ in range(2)]
-    dense = 2.0 if kind == "row" else None
+    dense = 2.0
     ref = [spmm(a, B, dense=dense) for B in Bs]
     plan = list(a._plans.values())[-1]
-    assert plan.is_hub == (kind == "hub")
-    if kind == "row":
-        assert plan.counter_bytes() > 0, "multi-segment heavy rows use arrival counters"
+    assert plan.counter_bytes() > 0, "multi-segment heavy rows use arrival counters"
     streams = [torch.cuda.Stream(), torch.cuda.Stream()]
     outs = [[torch.empty_like(ref[i]) for _ in range(24)] for i in range(2)]
     torch.cuda.synchronize()
@@ -368,74 +262,7 @@ def test_spmm_two_streams_share_one_plan_concurrently(r8, kind, monkeypatch):
     for i in range(2):
         for o in outs[i]:
             assert torch.equal(o, ref[i])
-    if kind == "row":
-        assert len(plan._counters) >= 3, "one counter region per stream"
-
-
-@pytest.mark.parametrize("F", [1, 3, 8, 24, 64, 200, 256, 300, 1000])
-@pytest.mark.parametrize("lanes", [0, 64])
-def test_spmm_hub_plan_r8(r8, F, lanes, hub_on):
-    """The hub plan (opt-in, sparse.HUB_MIN >= 0) on the R8
-    adjacency: 32 (or ~256 at narrow widths) row groups x column slices, the
-    documents from the LDS image, the 50 topic rows summed from the groups'
-    partials; every width class (float4 and scalar paths), bias + ReLU, against
-    the float64 oracle; bit-identical on a second call."""
-    a = from_torch(r8["adj"].to(DEV))
-    rng = np.random.default_rng(F)
-    B = rng.standard_normal((r8["nodes"], F)).astype(np.float32)
-    b = rng.standard_normal(F).astype(np.float32)
-    got = spmm(a, torch.from_numpy(B).to(DEV), bias=torch.from_numpy(b).to(DEV), epilogue=_lib.EPI_BIAS_RELU,
-               lanes=lanes)
-    plan = list(a._plans.values())[-1]
-    assert plan.is_hub and plan.header[6] == r8["ntopic"] and plan.header[7] == r8["ndoc"]
-    rp, ci, v = (t.cpu().numpy() for t in (a.rowptr, a.colind, a.val))
-    _close(got, csr_ref.spmm_epilogue(csr_ref.spmm_csr(rp, ci, v, B), b, relu=True), atol=2e-5)
-    again = spmm(a, torch.from_numpy(B).to(DEV), bias=torch.from_numpy(b).to(DEV), epilogue=_lib.EPI_BIAS_RELU,
-                 lanes=lanes)
-    assert torch.equal(got, again)
-
-
-@pytest.mark.parametrize("F", [4, 7, 16, 200])
-@pytest.mark.parametrize("block_rows", [0, 1, 33, 512])
-def test_spmm_hub_plan_synthetic_every_epilogue(F, block_rows, monkeypatch, hub_on):
-    """Hub plan on a doc-topic-like operand with the hub range in the middle
-    (groups straddle it), hub x hub nonzeros, empty light rows and rows without
-    a diagonal; every epilogue (bias, relu, dropout mask, hash dropout),
-    strided B / C (ldb, ldc > F; an odd ldb takes the scalar path)."""
-    import sys
-    sys.path.insert(0, os.path.dirname(__file__))
-    from test_plan_host import _doc_topic
-    from graph_convolutional_networks_for_text_classification_amd import sparse as sp
-    monkeypatch.setattr(sp, "HUB_BLOCK_ROWS", block_rows)
-    rng = np.random.default_rng(F * 7 + block_rows)
-    rp, ci, v = _doc_topic(rng, 1700, 40, 1300, 300, 6)
-    M = len(rp) - 1
-    a = from_arrays(rp, ci, v, (M, M), DEV)
-    ld = F + (5 if F % 4 else 8)
-    Bfull = rng.standard_normal((M, ld)).astype(np.float32)
-    B = Bfull[:, :F]
-    bias = rng.standard_normal(F).astype(np.float32)
-    mask = (rng.random((M, F)) < 0.6).astype(np.uint8)
-    acc = csr_ref.spmm_csr(rp, ci, v, B)
-    Bt = torch.from_numpy(Bfull).to(DEV)[:, :F]
-    bt = torch.from_numpy(bias).to(DEV)
-    out = torch.full((M, ld), 7.0, device=DEV)
-    spmm(a, Bt, out=out[:, :F])
-    assert list(a._plans.values())[-1].is_hub
-    _close(out[:, :F], acc, atol=2e-5 * np.sqrt(300))
-    assert torch.all(out[:, F:] == 7.0), "columns past F untouched"
-    _close(spmm(a, Bt, bias=bt, epilogue=_lib.EPI_BIAS), csr_ref.spmm_epilogue(acc, bias), atol=2e-4)
-    _close(spmm(a, Bt, bias=bt, epilogue=_lib.EPI_BIAS_RELU_DROP, mask=torch.from_numpy(mask).to(DEV), scale=2.0),
-           csr_ref.spmm_epilogue(acc, bias, relu=True, mask=mask, scale=2.0), atol=4e-4)
-    h = spmm(a, Bt, bias=bt, epilogue=_lib.EPI_BIAS_RELU_HASH, keep_prob=0.5, scale=2.0, seed=5, offset=11)
-    h2 = spmm(a, Bt, bias=bt, epilogue=_lib.EPI_BIAS_RELU_HASH, keep_prob=0.5, scale=2.0, seed=5, offset=11)
-    assert torch.equal(h, h2)
-    relu = csr_ref.spmm_epilogue(acc, bias, relu=True)
-    hn = h.double().cpu().numpy()
-    kept = hn != 0
-    _close(hn[kept], 2.0 * relu[kept], atol=4e-4)
-    frac = kept[relu > 1e-3].mean()
-    assert 0.4 < frac < 0.6, f"hash dropout keeps ~half, got {frac}"
+    assert len(plan._counters) >= 3, "one counter region per stream"
 
 
 def test_spmm_epilogues_and_strided_operands():
@@ -1059,8 +886,6 @@ def test_spmm_two_part_launch_matches_single(monkeypatch, r8):
     """gcnk_spmm_csr_f32_part: the single-chunk tile blocks on a side stream and
     the rest on the caller's stream give the one-launch result bit for bit."""
     from graph_convolutional_networks_for_text_classification_amd import ops
-    from graph_convolutional_networks_for_text_classification_amd import sparse as sp
-    monkeypatch.setattr(sp, "SPLIT_PLAN", False)   # R8 X on the tile path
     rng = np.random.default_rng(7)
     for a, K in ((from_torch(r8["features"].to(DEV)), r8["nfeat"]), (None, 900)):
         if a is None:
@@ -1106,27 +931,24 @@ def test_device_dropout_draws_a_fresh_mask_on_every_graph_replay(r8):
         assert torch.equal(eager, outs[1])
 
 
-@pytest.mark.parametrize("kind", ["row", "hub"])
-def test_graph_capture_takes_a_prezeroed_counter_region(r8, kind, monkeypatch):
-    """Captured SpMMs whose plan needs a counter region (row-unit plan: heavy-row
-    arrival counters; hub plan: the in-launch hub combine) share ONE of the
-    plan's pre-zeroed spare regions per capturing stream -- however many calls
-    and graphs -- so no graph holds a memset node; eager calls keep their
-    stream's region; replays interleaved with eager calls stay exact."""
-    from graph_convolutional_networks_for_text_classification_amd import sparse as sp
+@pytest.mark.parametrize("kind", ["random", "r8"])
+def test_graph_capture_takes_a_prezeroed_counter_region(r8, kind):
+    """Captured SpMMs whose plan needs a counter region (heavy-row arrival
+    counters) share ONE of the plan's pre-zeroed spare regions per capturing
+    stream -- however many calls and graphs -- so no graph holds a memset
+    node; eager calls keep their stream's region; replays interleaved with
+    eager calls stay exact."""
     rng = np.random.default_rng(23)
-    if kind == "row":
-        monkeypatch.setattr(sp, "HUB_MIN", -1)
+    if kind == "random":
         M, K, F = 3001, 20003, 200
         rp, ci, v = _random_csr(M, K, 20000, rng, heavy_rows=(5, 1700), heavy_deg=2500)
         a = from_arrays(rp, ci, v, (M, K), DEV)
     else:
-        monkeypatch.setattr(sp, "HUB_MIN", 0)
         a, K, F = from_torch(r8["adj"].to(DEV)), r8["nodes"], 200
     B = torch.from_numpy(rng.standard_normal((K, F)).astype(np.float32)).to(DEV)
     ref = spmm(a, B, dense=2.0)
     plan = list(a._plans.values())[-1]
-    assert plan.is_hub == (kind == "hub") and plan.counter_bytes() > 0
+    assert plan.counter_bytes() > 0
     spares = len(plan._spares)
     outs = [torch.empty_like(ref) for _ in range(6)]
     graphs = [torch.cuda.CUDAGraph() for _ in range(2)]
@@ -1149,23 +971,16 @@ def test_graph_capture_takes_a_prezeroed_counter_region(r8, kind, monkeypatch):
 
 @pytest.mark.parametrize("dense", [0.25, 0.3])
 def test_tile_path_repeat_streams_and_graph_replay_are_exact(r8, dense, monkeypatch):
-    """R8 X W1 on the split plan (dense=0.25: document rows over the 50 topic
-    columns + the 50 dense topic rows' split-K chunks combined in-launch) and,
-    with the split plan off, on the tile path (single-chunk document blocks,
-    the multi-chunk topic block and its slab reduce): back-to-back calls, two
-    streams at once on one cached plan and graph replays all give the one-call
-    bits, and the product matches the oracle."""
+    """R8 X W1 on the tile path (single-chunk document blocks, the multi-chunk
+    topic block and its slab reduce): back-to-back calls, two streams at once
+    on one cached plan and graph replays all give the one-call bits, and the
+    product matches the oracle."""
     from graph_convolutional_networks_for_text_classification_amd import ops
-    from graph_convolutional_networks_for_text_classification_amd import sparse as sp
-    monkeypatch.setattr(sp, "SPLIT_PLAN", dense == 0.25)
     x = from_torch(r8["features"].to(DEV))
     W = torch.randn(r8["nfeat"], 200, generator=torch.Generator().manual_seed(11)).to(DEV)
     one = ops.spmm(x, W, dense=dense)
     plan = list(x._plans.values())[-1]
-    if dense == 0.25:
-        assert plan.header[0] == SPLIT_MAGIC and plan.header[7] == 50, "R8 X: the split plan, 50 dense topic rows"
-    else:
-        assert plan.header[9] > 0, "R8 X's topic rows form a multi-chunk tile block"
+    assert plan.header[9] > 0, "R8 X's topic rows form a multi-chunk tile block"
     ops_spmm = ops.spmm
     def spmm_d(*a, **k):
         return ops_spmm(*a, dense=dense, **k)

@@ -38,9 +38,9 @@ cold figures for every op of the forward; "roofline_dominant" the slowest.
 
 cpu_baseline: the oracle (torch-CPU restatement issuing the reference's
 th.spmm calls on the same COO tensors, layer.py:102,106) on this host's
-cores, bounded sample, at the job's thread share (OMP_NUM_THREADS), at every
-core this process may run on ("all_cores") and at 1 thread, with nproc and
-the CPU model; "cpu_stock_csr" is torch CSR sparse.mm (MKL) on the same host, and
+cores, bounded sample, at the job's thread share (OMP_NUM_THREADS), at 1
+thread, and ("all_cores") in a child process pinned to one logical CPU per
+physical core with one bound OpenMP thread each, with nproc and the CPU model; "cpu_stock_csr" is torch CSR sparse.mm (MKL) on the same host, and
 "gpu_stock" stock PyTorch-ROCm torch.sparse.mm (hipSPARSE) on the device.
 
 configs: BASELINE configs 3 (20ng-shaped doc-topic graph, hidden 200, 20
@@ -86,6 +86,7 @@ def parse():
     ap.add_argument("--rocprof-dir", default=None, help="keep the child kernel-trace summaries here")
     ap.add_argument("--config5", action="store_true",
                     help="run the config-5 column-sharded leg even on one rank (it runs by default when N > 1)")
+    ap.add_argument("--cpu-child", default=None, help=argparse.SUPPRESS)   # internal: the pinned CPU leg
     ap.add_argument("--dry-run", action="store_true",
                     help="print each rank's launch view (rank, world) as JSON and exit before any GPU call")
     return ap.parse_args()
@@ -237,14 +238,14 @@ def _factored(a_csr, x):
     return factor.get(a_csr, ops.Operand(x))
 
 
-def forward_kernels(save_dir=None):
+def forward_kernels(save_dir=None, graph="r8"):
     """Per-kernel durations of the product forward (hipGraph replay) from a child
     rocprofv3 --kernel-trace run of scripts/fwd_trace.py, in launch order."""
     exe = shutil.which("rocprofv3")
     if exe is None:
         return None, "rocprofv3 not on PATH"
     tmp = tempfile.mkdtemp(prefix="gcnk_fwd_", dir="/tmp")
-    env = dict(os.environ, TMPDIR="/tmp")
+    env = dict(os.environ, TMPDIR="/tmp", GCNK_TRACE_GRAPH=graph)
     try:
         cmd = ["timeout", "-s", "KILL", "150", exe, "--kernel-trace", "--stats", "--output-format", "csv", "-d", tmp,
                "-o", "fwd", "--", sys.executable, os.path.join(ROOT, "scripts", "fwd_trace.py")]
@@ -260,12 +261,67 @@ def forward_kernels(save_dir=None):
         if save_dir:
             os.makedirs(save_dir, exist_ok=True)
             for f in glob.glob(os.path.join(tmp, "**", "*kernel_stats.csv"), recursive=True):
-                shutil.copy(f, os.path.join(save_dir, "bench_forward_kernel_stats.csv"))
+                shutil.copy(f, os.path.join(save_dir, f"bench_forward_{graph}_kernel_stats.csv"))
         return res, "rocprofv3 --kernel-trace, scripts/fwd_trace.py (hipGraph of 10 forwards, 20 replays)"
     except (OSError, subprocess.SubprocessError, KeyError, ValueError, ImportError) as e:
         return None, f"forward trace failed: {e}"
     finally:
         shutil.rmtree(tmp, ignore_errors=True)
+
+
+def labelled_forward_kernels(save_dir, graph, a_csr, x, N, nfeat, nnz_a, nnz_x, nhid, nclass):
+    """forward_kernels() with each launch labelled by the op it belongs to and
+    that op's algorithmic bytes (SURVEY §8(d) formula) and fraction."""
+    trace, trace_src = forward_kernels(save_dir, graph)
+    if trace is None or not trace.get("kernels"):
+        return {"error": trace_src}
+    alg = {   # algorithmic bytes of each launch of the eval forward
+        "X W1": spmm_bytes(N, nfeat, nnz_x, nhid),
+        "A S1": 4 * (N + 1) + 8 * nnz_a + 4 * N * nhid + 4 * N * nclass + 4 * nhid * nclass,
+        "A S2": spmm_bytes(N, N, nnz_a, nclass),
+    }
+    fac = _factored(a_csr, x)
+    if fac is not None:
+        # hub-factored gc1 (factor.py): X[hubs] W1 (tile SpMM or dense GEMM), then one
+        # launch reading U [N x Kc], the A_H records, W1[Kc], S_T, W2 and writing S2
+        x_hub_nnz = fac.x_hub.nnz if fac.x_hub is not None else fac.H * nfeat
+        alg = {"X_hubs W1": spmm_bytes(fac.H, nfeat, x_hub_nnz, nhid),
+               "A X W1 factored + H1 W2": (4 * fac.U.numel() + 4 * fac.rec.numel() + 4 * fac.Kc * nhid
+                                            + 4 * fac.H * nhid + 4 * nhid * nclass + 4 * N * nclass),
+               "A S2": alg["A S2"]}
+    ks, na = [], 0
+    for k in trace["kernels"]:   # the A-hat launches are the row kernels, X W1 the rest
+        name = k["kernel"]
+        if "hubfactor" in name:
+            key = "A X W1 factored + H1 W2"
+        elif "spmm_row_kernel" in name:
+            key = "A S1" if na == 0 and fac is None else "A S2"
+            na += 1
+        else:
+            key = "X W1" if fac is None else "X_hubs W1"
+        ks.append({"kernel": name[:120], "us": k["us"], "op": key})
+    for key, nb in alg.items():   # per op: its launches' summed duration against its bytes
+        us = sum(e["us"] for e in ks if e["op"] == key)
+        for e in ks:
+            if e["op"] == key:
+                e.update({"op_us": round(us, 3), "algorithmic_bytes": nb,
+                          "frac": nb / (us * 1e-6) / 1e9 / HBM_PEAK_GBS if us > 0 else None})
+    return {"source": trace_src, "path": "factored" if fac is not None else "spmm",
+            "forward_span_us": trace["forward_span_us_median"], "kernels": ks}
+
+
+def factor_build_ms(a_csr, x):
+    """One fresh host build of the hub factorisation of (A-hat, X) (factor.build:
+    the one-time setup the first forward pays, like the CSR plans), or None when
+    the operands do not factor."""
+    import torch
+    from graph_convolutional_networks_for_text_classification_amd import factor, ops
+    xop = ops.Operand(x)
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    f = factor.build(a_csr, xop)
+    torch.cuda.synchronize()
+    return round((time.perf_counter() - t0) * 1e3, 2) if f is not None else None
 
 
 def sharded_config5(dev, world, rank, datasets, ops, F=4096, reps=3):
@@ -329,6 +385,69 @@ def sharded_config5(dev, world, rank, datasets, ops, F=4096, reps=3):
         return {"error": str(e)[:300]}
 
 
+def physical_cores():
+    """One logical CPU per physical core among the CPUs this process may run on
+    (sysfs topology), so a pinned leg runs one thread per core, no SMT siblings."""
+    try:
+        allowed = sorted(os.sched_getaffinity(0))
+    except (AttributeError, OSError):
+        allowed = list(range(os.cpu_count() or 1))
+    seen, cores = set(), []
+    for c in allowed:
+        base = f"/sys/devices/system/cpu/cpu{c}/topology/"
+        try:
+            key = (open(base + "physical_package_id").read().strip(), open(base + "core_id").read().strip())
+        except OSError:
+            key = ("?", str(c))
+        if key not in seen:
+            seen.add(key)
+            cores.append(c)
+    return cores
+
+
+def cpu_child(args):
+    """The pinned all-cores CPU leg (a child of bench.py; never touches the GPU):
+    the oracle forward on the R8 fixture with the parent's weights, timed for
+    --cpu-sample-s seconds; prints one JSON line."""
+    import torch
+    import gcn_amd  # noqa: F401  (the package alias; loads no GPU code)
+    from graph_convolutional_networks_for_text_classification_amd import datasets
+    from oracle import gcn_ref
+    r8 = datasets.load_r8_fixture(os.path.join(ROOT, "tests", "golden", "r8_graph.npz"))
+    sd = torch.load(args.cpu_child, weights_only=True)
+    ref = gcn_ref.RefGCN(nfeat=r8["nfeat"], nhid=200, nclass=r8["nclass"], dropout=0.5).eval()
+    ref.load_state_dict(sd)
+    with torch.no_grad():
+        t, n = timed_cpu(lambda: ref(r8["features"], r8["adj"]), args.cpu_sample_s)
+    print(json.dumps({"s_per_forward": t, "forwards": n, "threads": torch.get_num_threads()}), flush=True)
+
+
+def pinned_cpu_leg(state_dict, sample_s):
+    """Runs cpu_child in a child process restricted (before it starts any thread)
+    to one logical CPU per physical core, with one OpenMP thread per core bound
+    to it; returns (seconds per forward, forwards, cores) or None."""
+    import torch
+    cores = physical_cores()
+    tmp = tempfile.mkdtemp(prefix="gcnk_cpu_", dir="/tmp")
+    try:
+        path = os.path.join(tmp, "sd.pt")
+        torch.save({k: v.detach().cpu() for k, v in state_dict.items()}, path)
+        env = dict(os.environ, OMP_NUM_THREADS=str(len(cores)), OMP_PROC_BIND="close", OMP_PLACES="cores",
+                   CUDA_VISIBLE_DEVICES="", HIP_VISIBLE_DEVICES="")
+        r = subprocess.run([sys.executable, os.path.abspath(__file__), "--cpu-child", path, "--cpu-sample-s",
+                            str(sample_s)], env=env, stdout=subprocess.PIPE, stderr=subprocess.STDOUT,
+                           preexec_fn=lambda: os.sched_setaffinity(0, cores), timeout=sample_s * 10 + 120)
+        line = [ln for ln in r.stdout.decode(errors="replace").splitlines() if ln.startswith("{")]
+        if r.returncode != 0 or not line:
+            return None
+        d = json.loads(line[-1])
+        return d["s_per_forward"], d["forwards"], len(cores)
+    except (OSError, subprocess.SubprocessError, ValueError, KeyError):
+        return None
+    finally:
+        shutil.rmtree(tmp, ignore_errors=True)
+
+
 def main():
     args = parse()
     if "WORLD_SIZE" not in os.environ and args.gpus > 1:
@@ -340,6 +459,9 @@ def main():
         raise SystemExit(f"bench.py: --gpus {args.gpus} but the launcher started {world} rank(s)")
     if args.dry_run:
         print(json.dumps({"rank": rank, "local_rank": local, "world": world}), flush=True)
+        return
+    if args.cpu_child:
+        cpu_child(args)
         return
     import numpy as np
     import torch
@@ -362,6 +484,7 @@ def main():
     x = r8["features"].to(dev)
     a_csr, x_csr = as_csr(adj), as_csr(x)
     nnz_a, nnz_x = a_csr.nnz, x_csr.nnz
+    fb_r8 = factor_build_ms(a_csr, x)
 
     def forward():
         with torch.no_grad():
@@ -473,65 +596,26 @@ def main():
             kt[mode] = rocprof_kernel_us(mode, ["spmm_row_kernel"], args.rocprof_dir, "row")
         # the streaming floor at this size: one elementwise pass over the same B / C
         # rotation (reads B once, writes C once) under the same rocprofv3 timing
-        kt["copy"] = rocprof_kernel_us("cold", ["elementwise"], args.rocprof_dir, "copy")
+        kt["copy"] = rocprof_kernel_us("cold", ["stream_copy_kernel"], args.rocprof_dir, "copy")
 
     # ---- the product forward's own kernels (rocprofv3 trace of the graph replay),
     #      each against its algorithmic bytes; the fused north-star kernel among them
     fwd_k = None
     if extras and not args.no_rocprof:
-        trace, trace_src = forward_kernels(args.rocprof_dir)
-        if trace is not None and trace.get("kernels"):
-            alg = {   # algorithmic bytes of each launch of the eval forward (SURVEY §8(d) formula)
-                "X W1": spmm_bytes(N, nfeat, nnz_x, nhid),
-                "A S1": 4 * (N + 1) + 8 * nnz_a + 4 * N * nhid + 4 * N * nclass + 4 * nhid * nclass,
-                "A S2": spmm_bytes(N, N, nnz_a, nclass),
-            }
-            fac = _factored(a_csr, x)
-            if fac is not None:
-                # hub-factored gc1 (factor.py): X[hubs] W1 on the tile GEMM, then one launch
-                # reading U [N x Kc], the A_H records, W1[Kc], S_T, W2 and writing S2
-                x_hub_nnz = fac.x_hub.nnz if fac.x_hub is not None else fac.H * nfeat
-                alg = {"X_hubs W1": spmm_bytes(fac.H, nfeat, x_hub_nnz, nhid),
-                       "A X W1 factored + H1 W2": (4 * fac.U.numel() + 4 * fac.rec.numel() + 4 * fac.Kc * nhid
-                                                    + 4 * fac.H * nhid + 4 * nhid * nclass + 4 * N * nclass),
-                       "A S2": alg["A S2"]}
-            ks, na = [], 0
-            for k in trace["kernels"]:   # the A-hat launches are the row / hub kernels, X W1 the rest
-                name = k["kernel"]
-                if "hubfactor" in name:
-                    key = "A X W1 factored + H1 W2"
-                elif "spmm_row_kernel" in name:
-                    key = "A S1" if na == 0 and fac is None else "A S2"
-                    na += 1
-                else:
-                    key = "X W1" if fac is None else "X_hubs W1"
-                ks.append({"kernel": name[:120], "us": k["us"], "op": key})
-            for key, nb in alg.items():   # per op: its launches' summed duration against its bytes
-                us = sum(e["us"] for e in ks if e["op"] == key)
-                for e in ks:
-                    if e["op"] == key:
-                        e.update({"op_us": round(us, 3), "algorithmic_bytes": nb,
-                                  "frac": nb / (us * 1e-6) / 1e9 / HBM_PEAK_GBS if us > 0 else None})
-            fwd_k = {"source": trace_src, "forward_span_us": trace["forward_span_us_median"], "kernels": ks}
-        else:
-            fwd_k = {"error": trace_src}
+        fwd_k = labelled_forward_kernels(args.rocprof_dir, "r8", a_csr, x, N, nfeat, nnz_a, nnz_x, nhid, nclass)
 
     # ---- CPU baselines (rank 0, N = 1): oracle at all cores and 1 thread, torch CSR (MKL)
     cpu = cpu_stock = gpu_stock = None
     if extras and args.cpu_sample_s > 0:
         from oracle import gcn_ref
         threads = int(os.environ.get("OMP_NUM_THREADS", str(min(16, os.cpu_count() or 1))))
-        try:
-            all_cores = len(os.sched_getaffinity(0))
-        except (AttributeError, OSError):
-            all_cores = os.cpu_count() or threads
         torch.manual_seed(0)
         ref = gcn_ref.RefGCN(nfeat=nfeat, nhid=nhid, nclass=nclass, dropout=0.5).eval()
         ref.load_state_dict({k: v.cpu() for k, v in model.state_dict().items()})
         xc, ac = r8["features"], r8["adj"]
         legs = {}
         with torch.no_grad():
-            for th in sorted({threads, 1, all_cores}, reverse=True):
+            for th in sorted({threads, 1}, reverse=True):
                 torch.set_num_threads(th)
                 tc, n = timed_cpu(lambda: ref(xc, ac), args.cpu_sample_s)
                 legs[th] = (tc, n)
@@ -546,13 +630,15 @@ def main():
             tm, nm = timed_cpu(csr_forward, args.cpu_sample_s / 2)
         tc, n = legs[threads]
         t1, n1 = legs[1]
+        pinned = pinned_cpu_leg(model.state_dict(), args.cpu_sample_s)
         cpu = {"value": 2 * nnz_a / tc, "unit": "edges/s", "cores": threads, "kind": "port",
                "sample": f"{n} R8 eval forwards of the oracle (torch-CPU th.spmm on the reference COO tensors, "
                          f"layer.py:102,106), {tc * 1e3:.2f} ms/forward at {threads} threads",
                "ms_per_forward": tc * 1e3,
                "one_thread": {"value": 2 * nnz_a / t1, "ms_per_forward": t1 * 1e3, "forwards": n1},
-               "all_cores": {"threads": all_cores, "value": 2 * nnz_a / legs[all_cores][0],
-                             "ms_per_forward": legs[all_cores][0] * 1e3, "forwards": legs[all_cores][1]},
+               "all_cores": ({"threads": pinned[2], "pinned": "one OpenMP thread per physical core, bound",
+                              "value": 2 * nnz_a / pinned[0], "ms_per_forward": pinned[0] * 1e3,
+                              "forwards": pinned[1]} if pinned else None),
                **cpu_info()}
         cpu_stock = {"value": 2 * nnz_a / tm, "unit": "edges/s", "cores": threads, "ms_per_forward": tm * 1e3,
                      "impl": "torch CPU sparse.mm on CSR tensors (MKL), same forward", "forwards": nm}
@@ -584,9 +670,15 @@ def main():
         m20 = GCN(nfeat=g20["nfeat"], nhid=200, nclass=20, dropout=0.5).to(dev).eval()
         a20, x20 = g20["adj"].to(dev), g20["features"].to(dev)
         ac20 = as_csr(a20)
-        with torch.no_grad():
-            m20(x20, a20)
-        us_fwd = graph_us([lambda: m20(x20, a20)], 50)
+
+        def fwd20():
+            with torch.no_grad():   # inference, as the R8 line (trainer.py:382 runs eval under no_grad)
+                return m20(x20, a20)
+        fwd20()
+        us_fwd = graph_us([fwd20], 50)
+        fk20 = None if args.no_rocprof else labelled_forward_kernels(
+            args.rocprof_dir, "20ng", ac20, x20, ac20.shape[0], g20["nfeat"], ac20.nnz, as_csr(x20).nnz, 200, 20)
+        fb20 = factor_build_ms(ac20, x20)
         M20 = ac20.shape[0]
         bb = torch.randn(200, device=dev)
         nsets = max(2, -(-int(1.25 * MALL_BYTES) // (2 * 4 * M20 * 200)))
@@ -603,7 +695,8 @@ def main():
             "spmm_F200_warm_us": round(w, 3), "spmm_F200_cold_us": round(c, 3),
             "spmm_F200_frac_cold": nb / (c * 1e-6) / 1e9 / HBM_PEAK_GBS,
             "spmm_F200_frac_warm": nb / (w * 1e-6) / 1e9 / HBM_PEAK_GBS,
-            "spmm_F200_gflops_cold": 2 * ac20.nnz * 200 / (c * 1e-6) / 1e9}
+            "spmm_F200_gflops_cold": 2 * ac20.nnz * 200 / (c * 1e-6) / 1e9,
+            "path": fk20.get("path") if fk20 else None, "factor_build_ms": fb20, "forward_kernels": fk20}
         del m20, a20, x20, ac20
         torch.cuda.empty_cache()
         from graph_convolutional_networks_for_text_classification_amd.sparse import CSR
@@ -679,6 +772,8 @@ def main():
         "config": {"workload": "R8 GCN forward (eval), hidden 200, 8 classes, nfeat 7463",
                    "nodes": N, "adj_nnz": nnz_a, "x_nnz": nnz_x, "graph": not args.no_graph,
                    "forwards_per_graph": per,
+                   "path": "factored" if fb_r8 is not None and _factored(a_csr, x) is not None else "spmm",
+                   "factor_build_ms": fb_r8,
                    "parallelism": f"replicas{world}" if world > 1 else "single"},
         "roofline": roof,
         # the same op under rocprofv3: kernel time without the dispatch gap that the
@@ -686,9 +781,9 @@ def main():
         "roofline_rocprof": {m: ({"kernel_us": round(v[0], 3),
                                   "frac": kn["algorithmic_bytes"] / (v[0] * 1e-6) / 1e9 / HBM_PEAK_GBS,
                                   "source": v[1],
-                                  **({"note": "streaming floor: one elementwise pass C = B * 1 over the same cold "
-                                              "B / C rotation (no CSR, no gathers); frac = the op's bytes at that "
-                                              "duration, the ceiling of any single kernel at this size"}
+                                  **({"note": "streaming floor: one float4 copy C = B (gcnk_stream_copy_f32) over "
+                                              "the same cold B / C rotation (no CSR, no gathers); frac = the op's "
+                                              "bytes at that duration, the ceiling of any single launch at this size"}
                                      if m == "copy" else {})} if v[0] is not None else {"error": v[1]})
                              for m, v in kt.items()},
         "roofline_dominant": {"kernel": dom, "frac": kd["frac_cold"], "frac_warm": kd["frac_warm"],

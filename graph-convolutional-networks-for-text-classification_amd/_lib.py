@@ -109,7 +109,9 @@ SIGNATURES = {
         _vp, _i64, _i32, _i32, _i32, _f32,  # G, ldg, M, N, P, scale
         _vp, _i64, _vp, _vp, _vp,          # gZ1, ldz, gW, gb1, gb2
         _vp, _i64, _vp]),                  # workspace, bytes, stream
-    "gcnk_hubfactor_lds_bytes": (_i64, [_i32, _i32, _i32, _i32]),
+    "gcnk_stream_copy_f32": (ctypes.c_int, [_vp, _vp, _i64, _vp]),
+    "gcnk_debug_poison_lds": (ctypes.c_int, [ctypes.c_uint32, _vp]),
+    "gcnk_hubfactor_lds_bytes": (_i64, [_i32, _i32, _i32, _i32, _i32]),
     "gcnk_hubfactor_gc1_f32": (ctypes.c_int, [
         _i32, _i32, _i32, _i32, _i32,     # M, F, Kc, nhub, P
         _vp, _i64, _vp, _i64, _i32,       # U, ldu, W, ldw, k0

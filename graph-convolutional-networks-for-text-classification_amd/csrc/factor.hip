@@ -40,7 +40,7 @@ typedef float f32x4 __attribute__((ext_vector_type(4)));
 constexpr int kRB = 32;         // rows per workgroup
 constexpr int kThreads = 512;   // 8 waves: 2 row strips x 4 column quarters
 constexpr int kMaxKsteps = 32;  // Kc <= 128
-constexpr int kProjW = 16;      // projection width (one MFMA n-tile): P <= 16
+constexpr int kProjMax = 32;    // projection width: P <= 32 (NP = 1 or 2 MFMA n-tiles)
 // zero floats after the staged W1[Kc]: the n-tiles past F read up to column
 // 64 NTQ - 1 of the last k-row, so the pad covers 64 NTQ - F of them (at least 64)
 __host__ __device__ constexpr int bpad(int f, int ntq) { return 64 * ntq - f > 64 ? 64 * ntq - f : 64; }
@@ -53,7 +53,9 @@ constexpr int kRecRow = 36, kRecHead = 68;
 // KS k-steps of U W1[Kc] (Kc <= 4 KS; U columns past Kc read as zero, W1 rows
 // past Kc staged as zero) and NTQ 16-column tiles per quarter of F (F <= 64 NTQ;
 // columns past F are computed from zeroed or W1 LDS words and never used)
-__host__ __device__ constexpr int pick_ks(int kc) { return kc <= 52 ? 13 : kc <= 100 ? 25 : 32; }
+// (18: the 20ng-shaped X's 70 topic-weight columns, whose W1 rows at 25 k-steps
+// would take the block's LDS past 160 KiB)
+__host__ __device__ constexpr int pick_ks(int kc) { return kc <= 52 ? 13 : kc <= 72 ? 18 : kc <= 100 ? 25 : 32; }
 __host__ __device__ constexpr int pick_ntq(int f) { return f <= 128 ? 2 : f <= 192 ? 3 : 4; }
 
 struct FactorArgs {
@@ -73,7 +75,7 @@ __host__ __device__ constexpr int region1_floats(int F, int ntq) {
   return (4 * KS * F + bpad(F, ntq)) > kRB * (64 * ntq + 4) ? (4 * KS * F + bpad(F, ntq)) : kRB * (64 * ntq + 4);
 }
 
-template <int KS, int NTQ>
+template <int KS, int NTQ, int NP>
 __global__ void __launch_bounds__(kThreads)
 hubfactor_gc1_kernel(FactorArgs a) {
   extern __shared__ __attribute__((aligned(16))) float smem[];
@@ -86,7 +88,7 @@ hubfactor_gc1_kernel(FactorArgs a) {
   const int blk = (int)blockIdx.x;
   const int64_t m0 = (int64_t)blk * kRB;  // position in the block order (U's rows)
   // LDS: region1 = s_B [Kr][F] + bpad zeros (phase 1), then s_Z [kRB][Fz]
-  //      | s_S [nhub][F] | s_W2 [F][P] | s_bias [F] | s_rec | s_red [3][2][64][4]
+  //      | s_S [nhub][F] | s_W2 [F][P] | s_bias [F] | s_rec | s_red [NP][3][2][64][4]
   // Every global operand is staged here in the one round of loads that opens the
   // kernel: a global load behind an LDS-read index costs a full memory round trip
   // under load (~1-2 us each, measured), so nothing after the first wait touches
@@ -210,66 +212,100 @@ hubfactor_gc1_kernel(FactorArgs a) {
   stamp(a.epi, 2);
 
   // ---- 3. S2 = H1 W2 on MFMA: strip x quarter of the K = F sum each (W2's rows
-  //      past F and columns past P as zero), quarters added in order
-  f32x4 pc;
+  //      past F and columns past P as zero), NP 16-column n-tiles of P, quarters
+  //      added in order
+  f32x4 pc[NP];
   {
     const int n = lane & 15;
     constexpr int kq = Fp / 16;  // k-steps per quarter
-    float av[kq], bw[kq];
+    float av[kq];
 #pragma unroll
-    for (int j = 0; j < kq; ++j) {
-      const int k = 4 * (quarter * kq + j) + (lane >> 4);
-      av[j] = s_Z[(16 * strip + (lane & 15)) * Fz + k];
-      bw[j] = (k < F && n < a.P) ? s_W2[k * a.P + n] : 0.f;
-    }
-    f32x4 p0 = f32x4{0.f, 0.f, 0.f, 0.f}, p1 = p0;
+    for (int j = 0; j < kq; ++j) av[j] = s_Z[(16 * strip + (lane & 15)) * Fz + 4 * (quarter * kq + j) + (lane >> 4)];
 #pragma unroll
-    for (int j = 0; j < kq; j += 2) {
-      p0 = __builtin_amdgcn_mfma_f32_16x16x4f32(av[j], bw[j], p0, 0, 0, 0);
-      p1 = __builtin_amdgcn_mfma_f32_16x16x4f32(av[j + 1], bw[j + 1], p1, 0, 0, 0);
+    for (int t = 0; t < NP; ++t) {
+      float bw[kq];
+#pragma unroll
+      for (int j = 0; j < kq; ++j) {
+        const int k = 4 * (quarter * kq + j) + (lane >> 4);
+        bw[j] = (k < F && 16 * t + n < a.P) ? s_W2[k * a.P + 16 * t + n] : 0.f;
+      }
+      f32x4 p0 = f32x4{0.f, 0.f, 0.f, 0.f}, p1 = p0;
+#pragma unroll
+      for (int j = 0; j < kq; j += 2) {
+        p0 = __builtin_amdgcn_mfma_f32_16x16x4f32(av[j], bw[j], p0, 0, 0, 0);
+        p1 = __builtin_amdgcn_mfma_f32_16x16x4f32(av[j + 1], bw[j + 1], p1, 0, 0, 0);
+      }
+      pc[t] = p0 + p1;
     }
-    pc = p0 + p1;
   }
-  if (quarter > 0) *reinterpret_cast<f32x4*>(s_red + (((quarter - 1) * 2 + strip) * 64 + lane) * 4) = pc;
+  if (quarter > 0)
+#pragma unroll
+    for (int t = 0; t < NP; ++t)
+      *reinterpret_cast<f32x4*>(s_red + (((t * 3 + quarter - 1) * 2 + strip) * 64 + lane) * 4) = pc[t];
   __syncthreads();
   if (quarter == 0) {
 #pragma unroll
-    for (int qq = 0; qq < 3; ++qq) pc += *reinterpret_cast<const f32x4*>(s_red + ((qq * 2 + strip) * 64 + lane) * 4);
-    const int p = lane & 15;
+    for (int t = 0; t < NP; ++t) {
 #pragma unroll
-    for (int r = 0; r < 4; ++r) {
-      const int64_t row = s_rec[kRecRow + 16 * strip + (lane >> 4) * 4 + r];
-      if (row >= 0 && p < a.P) a.C2[row * a.ldc2 + p] = pc[r];
+      for (int qq = 0; qq < 3; ++qq)
+        pc[t] += *reinterpret_cast<const f32x4*>(s_red + (((t * 3 + qq) * 2 + strip) * 64 + lane) * 4);
+      const int p = 16 * t + (lane & 15);
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const int64_t row = s_rec[kRecRow + 16 * strip + (lane >> 4) * 4 + r];
+        if (row >= 0 && p < a.P) a.C2[row * a.ldc2 + p] = pc[t][r];
+      }
     }
   }
   stamp(a.epi, 3);
 }
 
 
+// Debug/test aid: every workgroup fills the whole 160 KiB of LDS with `word`.
+// LDS is not cleared between workgroups, so a kernel launched next on the same
+// CUs starts from these words wherever it reads LDS it has not written (the
+// tests poison it with NaN bits before the factored kernel).
+__global__ void __launch_bounds__(1024) lds_poison_kernel(uint32_t word) {
+  extern __shared__ uint32_t s_all[];
+  for (int i = threadIdx.x; i < 160 * 1024 / 4; i += 1024) s_all[i] = word;
+  __syncthreads();
+  if (s_all[(threadIdx.x * 37) % (160 * 1024 / 4)] != word) s_all[0] = 0;  // keep the stores
+}
+
 }  // namespace
 }  // namespace gcnk
 
 using namespace gcnk;
 
-static int64_t hubfactor_lds_bytes(int32_t F, int32_t Kc, int32_t nhub, int32_t rec_words, int32_t P = kProjW) {
-  const int64_t Fz = 64 * pick_ntq(F) + 4, Kr = 4 * pick_ks(Kc);
-  const int64_t r1 = std::max<int64_t>(Kr * F + bpad(F, pick_ntq(F)), (int64_t)kRB * Fz);
-  return 4 * (r1 + (int64_t)nhub * F + (((int64_t)F * P + 3) & ~3LL) + F + rec_words + 3 * 2 * 64 * 4);
+extern "C" int gcnk_debug_poison_lds(uint32_t word, void* stream) {
+  static const hipError_t attr = hipFuncSetAttribute(reinterpret_cast<const void*>(&lds_poison_kernel),
+                                                     hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
+  if (attr != hipSuccess) return hip_check(attr, "lds_poison_kernel LDS attribute");
+  hipLaunchKernelGGL(lds_poison_kernel, dim3(1024), dim3(1024), 160 * 1024, reinterpret_cast<hipStream_t>(stream), word);
+  return launch_check("lds_poison_kernel");
 }
 
-extern "C" int64_t gcnk_hubfactor_lds_bytes(int32_t F, int32_t Kc, int32_t nhub, int32_t rec_words) {
-  if (F <= 0 || Kc <= 0 || nhub <= 0 || rec_words < kRecHead) return GCNK_EARG;
-  return hubfactor_lds_bytes(F, Kc, nhub, rec_words);
+static int pick_np(int32_t P) { return P <= 16 ? 1 : 2; }
+
+static int64_t hubfactor_lds_bytes(int32_t F, int32_t Kc, int32_t nhub, int32_t rec_words, int32_t P) {
+  const int64_t Fz = 64 * pick_ntq(F) + 4, Kr = 4 * pick_ks(Kc);
+  const int64_t r1 = std::max<int64_t>(Kr * F + bpad(F, pick_ntq(F)), (int64_t)kRB * Fz);
+  return 4 * (r1 + (int64_t)nhub * F + (((int64_t)F * P + 3) & ~3LL) + F + rec_words + pick_np(P) * 3 * 2 * 64 * 4);
+}
+
+extern "C" int64_t gcnk_hubfactor_lds_bytes(int32_t F, int32_t Kc, int32_t nhub, int32_t rec_words, int32_t P) {
+  if (F <= 0 || Kc <= 0 || nhub <= 0 || rec_words < kRecHead || P <= 0 || P > kProjMax) return GCNK_EARG;
+  return hubfactor_lds_bytes(F, Kc, nhub, rec_words, P);
 }
 
 // The dynamic-LDS limit is raised once per kernel instantiation (a driver call
 // per launch cost host time on every eager forward), then the launch.
-template <int KS, int NTQ>
+template <int KS, int NTQ, int NP>
 static int launch_factor(const FactorArgs& a, int64_t nblk, int64_t lds_b, void* stream) {
-  static const hipError_t attr = hipFuncSetAttribute(reinterpret_cast<const void*>(&hubfactor_gc1_kernel<KS, NTQ>),
+  static const hipError_t attr = hipFuncSetAttribute(reinterpret_cast<const void*>(&hubfactor_gc1_kernel<KS, NTQ, NP>),
                                                      hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
   if (attr != hipSuccess) return hip_check(attr, "hubfactor_gc1_kernel LDS attribute");
-  hipLaunchKernelGGL((hubfactor_gc1_kernel<KS, NTQ>), dim3((unsigned)nblk), dim3(kThreads), (size_t)lds_b,
+  hipLaunchKernelGGL((hubfactor_gc1_kernel<KS, NTQ, NP>), dim3((unsigned)nblk), dim3(kThreads), (size_t)lds_b,
                      reinterpret_cast<hipStream_t>(stream), a);
   return launch_check("hubfactor_gc1_kernel");
 }
@@ -290,9 +326,9 @@ extern "C" int gcnk_hubfactor_gc1_f32(int32_t M, int32_t F, int32_t Kc, int32_t 
     set_error("gcnk_hubfactor_gc1_f32: leading dimension too small");
     return GCNK_EARG;
   }
-  if (F % 4 || F > 256 || Kc > 4 * kMaxKsteps || P > kProjW || ldw != F || lds != F || ldw2 != P ||
+  if (F % 4 || F > 256 || Kc > 4 * kMaxKsteps || P > kProjMax || ldw != F || lds != F || ldw2 != P ||
       !aligned16(W) || !aligned16(S) || (H && !aligned16(H)) || (H && ldh % 4) || (bias && !aligned16(bias))) {
-    set_error("gcnk_hubfactor_gc1_f32: unsupported shape (F=%d %% 4, F <= 256, Kc <= 128, P <= 16, 16-B rows)", F);
+    set_error("gcnk_hubfactor_gc1_f32: unsupported shape (F=%d %% 4, F <= 256, Kc <= 128, P <= 32, 16-B rows)", F);
     return GCNK_EUNSUP;
   }
   if (epilogue < GCNK_EPI_NONE || epilogue > GCNK_EPI_BIAS_RELU_HASH ||
@@ -317,10 +353,13 @@ extern "C" int gcnk_hubfactor_gc1_f32(int32_t M, int32_t F, int32_t Kc, int32_t 
   e.code = epilogue; e.stamps = debug_stamps();
   e.ldm = epilogue == GCNK_EPI_BIAS_RELU_HASH ? (ldm > 0 ? ldm : F) : ldm;
   const int64_t nblk = ((int64_t)M + kRB - 1) / kRB;
-  const int ks = pick_ks(Kc), ntq = pick_ntq(F);
-#define GCNK_FACTOR_CASE(KS_, NTQ_) \
-  if (ks == KS_ && ntq == NTQ_) return launch_factor<KS_, NTQ_>(a, nblk, lds_b, stream);
+  const int ks = pick_ks(Kc), ntq = pick_ntq(F), np = pick_np(P);
+#define GCNK_FACTOR_CASE(KS_, NTQ_)                                                   \
+  if (ks == KS_ && ntq == NTQ_)                                                       \
+    return np == 1 ? launch_factor<KS_, NTQ_, 1>(a, nblk, lds_b, stream)              \
+                   : launch_factor<KS_, NTQ_, 2>(a, nblk, lds_b, stream);
   GCNK_FACTOR_CASE(13, 2) GCNK_FACTOR_CASE(13, 3) GCNK_FACTOR_CASE(13, 4)
+  GCNK_FACTOR_CASE(18, 2) GCNK_FACTOR_CASE(18, 3) GCNK_FACTOR_CASE(18, 4)
   GCNK_FACTOR_CASE(25, 2) GCNK_FACTOR_CASE(25, 3) GCNK_FACTOR_CASE(25, 4)
   GCNK_FACTOR_CASE(32, 2) GCNK_FACTOR_CASE(32, 3) GCNK_FACTOR_CASE(32, 4)
 #undef GCNK_FACTOR_CASE

@@ -27,7 +27,7 @@ import torch
 
 from .sparse import from_arrays
 
-MAX_HUBS = 64     # hub rows staged in LDS (S_T [hubs x F])
+MAX_HUBS = 128    # hub rows staged in LDS (S_T [hubs x F]; the kernel checks the LDS budget)
 # X[hubs] W1 through the SpMM tile plan on their CSR ("spmm", default) or the
 # split-K MFMA GEMM on a dense copy ("gemm": R8 9.5 + 4.9 us against the tile
 # plan's 7.1 + 4.9, profiles/r03_factor.md)

@@ -211,10 +211,10 @@ def hubfactor_gc1(f, W1, b1, W2, epilogue=_lib.EPI_BIAS_RELU, mask=None, scale=1
         W1 = W1.contiguous()   # the kernel stages W1[k0:k0+Kc], S_T and W2 as flat copies
     if W2.stride(0) != P:
         W2 = W2.contiguous()
-    if W2.shape[0] != F or P > 16 or F % 4 or F > 256:
+    if W2.shape[0] != F or P > 32 or F % 4 or F > 256:
         return None
     lib = _lib.load()
-    if int(lib.gcnk_hubfactor_lds_bytes(F, f.Kc, f.H, f.rec_words)) > 160 * 1024:
+    if int(lib.gcnk_hubfactor_lds_bytes(F, f.Kc, f.H, f.rec_words, P)) > 160 * 1024:
         return None
     S = f.hub_times(W1).contiguous()
     H1 = torch.empty((M, F), dtype=torch.float32, device=W1.device) if store_h1 else None

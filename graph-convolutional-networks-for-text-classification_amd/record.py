@@ -85,8 +85,8 @@ class ForwardRecord:
         s.M, s.F, s.P = M, F, P
         fac = factor.get(adj, xop) if ops.FACTOR_GC1 else None
         kind = None
-        if fac is not None and P <= 16 and F % 4 == 0 and F <= 256 and \
-                int(lib.gcnk_hubfactor_lds_bytes(F, fac.Kc, fac.H, fac.rec_words)) <= 160 * 1024:
+        if fac is not None and P <= 32 and F % 4 == 0 and F <= 256 and \
+                int(lib.gcnk_hubfactor_lds_bytes(F, fac.Kc, fac.H, fac.rec_words, P)) <= 160 * 1024:
             kind = FACTORED
             s.Kc, s.nhub, s.k0, s.rec_words = fac.Kc, fac.H, fac.k0, fac.rec_words
             s.U, s.ldu, s.rec = fac.U.data_ptr(), fac.U.stride(0), fac.rec.data_ptr()

@@ -248,7 +248,7 @@ int gcnk_gcn_bwd2_f32(const float* H, int64_t ldh, const float* gS, int64_t ldgs
  * and themselves, with X's light rows inside the column range [k0, k0 + Kc):
  *   Z[r, :]   = U[i, :Kc] . W[k0 .. k0+Kc-1, :] + sum_{items of r} val * S[hub, :]
  *   H[r, n]   = epilogue(Z[r, n] + bias[n])            (GCNK_EPI_*, as the SpMM)
- *   C2[r, p]  = sum_n H[r, n] W2[n, p]                 (P <= 16)
+ *   C2[r, p]  = sum_n H[r, n] W2[n, p]                 (P <= 32)
  * for r = the row id at position i of the block order.  U [M x Kc] in block
  * order (ldu >= Kc rounded up to 4, zero past Kc), S = X[hubs] W [nhub x F]
  * (lds), rec = one record of rec_words int32 per 32-row block: 33 offsets
@@ -258,7 +258,10 @@ int gcnk_gcn_bwd2_f32(const float* H, int64_t ldh, const float* gS, int64_t ldgs
  * the block's operands exceed 160 KiB of LDS (gcnk_hubfactor_lds_bytes).  One
  * launch, fixed-order sums.
  * ------------------------------------------------------------------------- */
-int64_t gcnk_hubfactor_lds_bytes(int32_t F, int32_t Kc, int32_t nhub, int32_t rec_words);
+int64_t gcnk_hubfactor_lds_bytes(int32_t F, int32_t Kc, int32_t nhub, int32_t rec_words, int32_t P);
+/* Test aid: fills every CU's 160 KiB of LDS with `word` (one launch), so a
+ * following launch that read LDS it had not written would see it. */
+int gcnk_debug_poison_lds(uint32_t word, void* stream);
 int gcnk_hubfactor_gc1_f32(int32_t M, int32_t F, int32_t Kc, int32_t nhub, int32_t P, const float* U, int64_t ldu,
                            const float* W, int64_t ldw, int32_t k0, const float* S, int64_t lds,
                            const int32_t* rec, int32_t rec_words, const float* bias, int32_t epilogue,
@@ -431,6 +434,11 @@ int gcnk_bernoulli_mt19937(uint32_t* state, int32_t* left, int64_t* next, int64_
 int gcnk_bernoulli_mt19937_start(uint32_t* state, int32_t* left, int64_t* next, int64_t n, double p,
                                  uint8_t* mask_out, void** job);
 int gcnk_bernoulli_mt19937_wait(void* job);
+
+/* Measurement floor (not on the GCN path): dst[0..n) = src[0..n) as one
+ * float4 grid-stride launch -- the north-star SpMM's dense bytes with no CSR
+ * and no gathers (bench.py's "copy" roofline line). */
+int gcnk_stream_copy_f32(const float* src, float* dst, int64_t n, void* stream);
 
 /* Debug only: in a library built with -DGCNK_STAMPS, when `buf` is non-null
  * every later row/tile SpMM launch writes 4 x uint64 s_memrealtime stamps

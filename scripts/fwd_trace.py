@@ -1,6 +1,7 @@
 """One R8 eval forward timeline from a rocprofv3 kernel trace: run under
 `rocprofv3 --kernel-trace --output-format csv -d DIR -- python scripts/fwd_trace.py`
-(replays a hipGraph of 10 forwards 20 times), then
+(replays a hipGraph of 10 forwards 20 times; GCNK_TRACE_GRAPH=20ng traces the
+BASELINE config-3 graph instead), then
 `python scripts/fwd_trace.py --report DIR` prints, per kernel position in the
 forward, its median duration and the median gap before it (us)."""
 import argparse
@@ -21,10 +22,14 @@ def run():
     import gcn_amd  # noqa: F401
     from graph_convolutional_networks_for_text_classification_amd import GCN, datasets
     dev = torch.device("cuda", 0)
-    r8 = datasets.load_r8_fixture(os.path.join(ROOT, "tests", "golden", "r8_graph.npz"))
-    torch.manual_seed(0)
-    m = GCN(nfeat=r8["nfeat"], nhid=200, nclass=r8["nclass"], dropout=0.5).to(dev).eval()
-    x, adj = r8["features"].to(dev), r8["adj"].to(dev)
+    if os.environ.get("GCNK_TRACE_GRAPH") == "20ng":
+        g = datasets.doc_topic_graph(18846, 70, 20, seed=0)
+        torch.manual_seed(1)
+    else:
+        g = datasets.load_r8_fixture(os.path.join(ROOT, "tests", "golden", "r8_graph.npz"))
+        torch.manual_seed(0)
+    m = GCN(nfeat=g["nfeat"], nhid=200, nclass=g["nclass"], dropout=0.5).to(dev).eval()
+    x, adj = g["features"].to(dev), g["adj"].to(dev)
     with torch.no_grad():
         for _ in range(3):   # plan builds, then eager forwards (their kernel names are the trace's labels)
             m(x, adj)

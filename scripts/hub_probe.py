@@ -62,6 +62,7 @@ def main():
     ap.add_argument("--variants", default="row,copy")
     ap.add_argument("--widths", default="200,8")
     ap.add_argument("--graph", default="r8", choices=["r8", "20ng"])
+    ap.add_argument("--ipc", default="", help="comma list of light-row limits to sweep (default: the library's)")
     ap.add_argument("--mode", default="both", choices=["warm", "cold", "both"],
                     help="which timing graphs to run (one mode alone for a rocprofv3 kernel average)")
     args = ap.parse_args()
@@ -81,33 +82,38 @@ def main():
         nsets = max(2, int(np.ceil(300e6 / (2 * 4 * M * F))))
         Bs = [torch.from_numpy(Bh).to(dev) for _ in range(nsets)]
         Cs = [torch.empty(M, F, device=dev) for _ in range(nsets)]
-        for name in args.variants.split(","):
+        ipcs = [int(v) for v in args.ipc.split(",")] if args.ipc else [None]
+        for name, ipc in ((n, i) for n in args.variants.split(",") for i in (ipcs if n != "copy" else [None])):
             if name == "copy":
-                # the streaming floor of the same bytes: one elementwise pass C = B * 1
+                # the streaming floor of the same bytes: one float4 copy C = B
                 # (reads B once, writes C once: the op's compulsory traffic minus the CSR)
-                fns = [(lambda i=i: torch.mul(Bs[i], 1.0, out=Cs[i])) for i in range(nsets)]
+                lib = _lib.load()
+
+                def copy(i):
+                    _lib.check(lib.gcnk_stream_copy_f32(Bs[i].data_ptr(), Cs[i].data_ptr(), Bs[i].numel(),
+                                                        torch.cuda.current_stream().cuda_stream), "copy")
+                fns = [(lambda i=i: copy(i)) for i in range(nsets)]
                 cold = time_graph(fns, max(1, args.reps // nsets)) if args.mode in ("cold", "both") else float("nan")
-                warm = (time_graph([lambda: torch.mul(Bs[0], 1.0, out=Cs[0])], args.reps)
-                        if args.mode in ("warm", "both") else float("nan"))
+                warm = time_graph([lambda: copy(0)], args.reps) if args.mode in ("warm", "both") else float("nan")
                 print(json.dumps({"graph": args.graph, "F": F, "variant": "copy", "bytes": 8 * M * F,
                                   "warm_us": round(warm, 3), "cold_us": round(cold, 3), "sets": nsets}), flush=True)
                 continue
             assert name in VARIANTS, name
-            out = ops.spmm(a, Bs[0], bias=bias, epilogue=_lib.EPI_BIAS_RELU)
+            out = ops.spmm(a, Bs[0], bias=bias, epilogue=_lib.EPI_BIAS_RELU, ipc=ipc)
             torch.cuda.synchronize()
             err = float(np.abs(out.cpu().numpy().astype(np.float64) - ref).max())
-            again = ops.spmm(a, Bs[0], bias=bias, epilogue=_lib.EPI_BIAS_RELU)
+            again = ops.spmm(a, Bs[0], bias=bias, epilogue=_lib.EPI_BIAS_RELU, ipc=ipc)
             det = bool(torch.equal(out, again))
             plan = list(a._plans.values())[-1]
             warm = cold = float("nan")
             if args.mode in ("warm", "both"):
-                warm = time_graph([lambda: ops.spmm(a, Bs[0], bias=bias, epilogue=_lib.EPI_BIAS_RELU, out=Cs[0])],
-                                  args.reps)
-            fns = [(lambda i=i: ops.spmm(a, Bs[i], bias=bias, epilogue=_lib.EPI_BIAS_RELU, out=Cs[i]))
+                warm = time_graph([lambda: ops.spmm(a, Bs[0], bias=bias, epilogue=_lib.EPI_BIAS_RELU, out=Cs[0],
+                                                    ipc=ipc)], args.reps)
+            fns = [(lambda i=i: ops.spmm(a, Bs[i], bias=bias, epilogue=_lib.EPI_BIAS_RELU, out=Cs[i], ipc=ipc))
                    for i in range(nsets)]
             if args.mode in ("cold", "both"):
                 cold = time_graph(fns, max(1, args.reps // nsets))
-            print(json.dumps({"graph": args.graph, "F": F, "variant": name,
+            print(json.dumps({"graph": args.graph, "F": F, "variant": name, "ipc": ipc,
                               "hdr": plan.header, "max_err": err, "deterministic": det,
                               "warm_us": round(warm, 3), "cold_us": round(cold, 3),
                               "warm_frac": nbytes / (warm * 1e-6) / 8e12, "cold_frac": nbytes / (cold * 1e-6) / 8e12,

@@ -316,8 +316,9 @@ __global__ void __launch_bounds__(WPB * 64) ns_lds_kernel(Args a) {
   stamp(a, 3);
 }
 
+template <int STORE>
 __global__ void copy_gs(const float4* __restrict__ a, float4* __restrict__ b, int n) {
-  for (int i = blockIdx.x * blockDim.x + threadIdx.x; i < n; i += gridDim.x * blockDim.x) b[i] = a[i];
+  for (int i = blockIdx.x * blockDim.x + threadIdx.x; i < n; i += gridDim.x * blockDim.x) store_out<STORE>(b, i, a[i]);
 }
 // the light geometry with no gathers and no compute: wave copies its RPW rows
 template <int WPB, int RPW>
@@ -488,8 +489,8 @@ int main(int argc, char** argv) {
   const int H = h1 - h0;
   printf("{\"h0\": %d, \"H\": %d}\n", h0, H);
   const size_t lds_hub = (size_t)H * Q * 16;
-  CHECK(hipFuncSetAttribute((const void*)&ns_lds_kernel<16, 2, 8, 0>, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024));
-  CHECK(hipFuncSetAttribute((const void*)&ns_lds_kernel<8, 4, 8, 0>, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024));
+  CHECK(hipFuncSetAttribute((const void*)&ns_lds_kernel<16, 2, 8, 0>, hipFuncAttributeMaxDynamicSharedMemorySize, 64 * 1024));
+  CHECK(hipFuncSetAttribute((const void*)&ns_lds_kernel<8, 4, 8, 0>, hipFuncAttributeMaxDynamicSharedMemorySize, 64 * 1024));
   auto args = [&](const Built& b, int s, int nhb) {
     Args a{};
     a.B = reinterpret_cast<const float4*>(Bs[s]); a.C = reinterpret_cast<float4*>(Cs[s]);
@@ -509,7 +510,9 @@ int main(int argc, char** argv) {
   };
   struct Variant { std::string name; std::function<void(int, unsigned long long*)> run; int check; int grid; };
   std::vector<Variant> vs;
-  vs.push_back({"copy_gs 1024x256", [&](int s, unsigned long long*) { hipLaunchKernelGGL(copy_gs, dim3(1024), dim3(256), 0, st, (const float4*)Bs[s], (float4*)Cs[s], (int)(mat / 4)); }, 0, 0});
+  vs.push_back({"copy_gs 1024x256", [&](int s, unsigned long long*) { hipLaunchKernelGGL(copy_gs<0>, dim3(1024), dim3(256), 0, st, (const float4*)Bs[s], (float4*)Cs[s], (int)(mat / 4)); }, 0, 0});
+  vs.push_back({"copy_gs nt-store", [&](int s, unsigned long long*) { hipLaunchKernelGGL(copy_gs<1>, dim3(1024), dim3(256), 0, st, (const float4*)Bs[s], (float4*)Cs[s], (int)(mat / 4)); }, 0, 0});
+  vs.push_back({"copy_gs sc1-store", [&](int s, unsigned long long*) { hipLaunchKernelGGL(copy_gs<2>, dim3(1024), dim3(256), 0, st, (const float4*)Bs[s], (float4*)Cs[s], (int)(mat / 4)); }, 0, 0});
   vs.push_back({"copy_rows RPW2", [&](int s, unsigned long long*) { Args a = args(plans[0], s, 0); hipLaunchKernelGGL((copy_rows<4, 2>), dim3(plans[0].P.nlwg), dim3(256), 0, st, a); }, 0, 0});
   vs.push_back({"copy_rows RPW4", [&](int s, unsigned long long*) { Args a = args(plans[1], s, 0); hipLaunchKernelGGL((copy_rows<4, 4>), dim3(plans[1].P.nlwg), dim3(256), 0, st, a); }, 0, 0});
   vs.push_back({"copy_rows RPW8", [&](int s, unsigned long long*) { Args a = args(plans[2], s, 0); hipLaunchKernelGGL((copy_rows<4, 8>), dim3(plans[2].P.nlwg), dim3(256), 0, st, a); }, 0, 0});

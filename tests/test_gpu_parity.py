@@ -26,6 +26,7 @@ from oracle import csr_ref, gcn_ref
 pytestmark = pytest.mark.gpu
 DEV = "cuda"
 LOGIT_TOL = 1e-4
+TRAINED_LOGIT_TOL = 3e-4   # absolute, trained-model logits up to |190| (see the test)
 
 
 def _close(got, ref, rtol=1e-5, atol=1e-5):
@@ -491,8 +492,9 @@ def test_trained_model_labels_bit_exact_on_every_row(r8, trained_golden):
     7,463-term dot products accumulate in one serial fp32 chain).  A 1e-4
     bound against the reference would demand reproducing its rounding
     sequence; instead the HIP forward must be at least as close to the
-    float64 truth as the reference is (and within that distance of it twice
-    over), and within 1e-4 relative to the logit scale."""
+    float64 truth as the reference is, and within TRAINED_LOGIT_TOL of the
+    reference's logits in absolute terms (observed on MI355X: 2.7e-4, printed
+    below; the reference's own distance to float64 is 1.9e-4)."""
     import scipy.sparse as ssp
     m = GCN(nfeat=r8["nfeat"], nhid=200, nclass=r8["nclass"], dropout=0.5).to(DEV)
     m.load_state_dict(trained_golden["state_dict"])
@@ -513,7 +515,7 @@ def test_trained_model_labels_bit_exact_on_every_row(r8, trained_golden):
     scale = float(np.abs(gold).max())
     print(f"trained model: |logit| <= {scale:.1f}; max err vs reference {err:.2e}; vs float64: reference "
           f"{err_ref:.2e}, HIP {err_hip:.2e}")
-    assert err_hip <= err_ref and err <= 2 * err_ref and err <= 1e-4 * scale
+    assert err_hip <= err_ref and err <= TRAINED_LOGIT_TOL
     assert np.array_equal(lg.argmax(1), gold.argmax(1)), f"{int(np.sum(lg.argmax(1) != gold.argmax(1)))} labels differ"
     test = np.asarray(r8["test_lst"])
     acc = float(np.mean(lg[test].argmax(1) == np.asarray(r8["target"])[test]))
@@ -668,20 +670,51 @@ def test_r8_training_accuracy_parity(r8, golden_meta, seed):
 
 # ------------------------------------------------------------------------------ BASELINE configs 3-5 at full size
 
-def test_gcn_20ng_shaped_forward_matches_oracle():
+@pytest.mark.parametrize("mode", ["eval", "train_hash"])
+def test_gcn_20ng_shaped_forward_matches_oracle(mode, monkeypatch):
     """BASELINE config 3: 20ng-shaped doc-topic graph (18,846 docs, 70 topics,
-    nclass 20, gensim-shaped nfeat 100 -> dense-block X), eval logits vs the
-    oracle's reference-equivalent forward on the same tensors."""
+    nclass 20, gensim-shaped nfeat 100 -> dense X).  The default forward takes
+    the hub-factored first layer (70 hubs, Kc = 70, P = 20: the 18-k-step,
+    two-n-tile gcnk_hubfactor_gc1_f32): eval logits vs the oracle's
+    reference-equivalent forward on the same tensors; logits and every
+    gradient of a train-mode step (device dropout) vs the SpMM path
+    (ops.FACTOR_GC1 = False)."""
+    from graph_convolutional_networks_for_text_classification_amd import factor, ops, record
+    from graph_convolutional_networks_for_text_classification_amd.sparse import as_csr
     g = datasets.doc_topic_graph(18846, 70, 20, seed=0)
-    torch.manual_seed(11)
-    m = GCN(nfeat=g["nfeat"], nhid=200, nclass=20, dropout=0.5).to(DEV).eval()
-    ref = gcn_ref.RefGCN(nfeat=g["nfeat"], nhid=200, nclass=20, dropout=0.5).eval()
-    ref.load_state_dict({k: v.cpu() for k, v in m.state_dict().items()})
-    with torch.no_grad():
-        got = m(g["features"].to(DEV), g["adj"].to(DEV)).cpu().numpy()
-        want = ref(g["features"], g["adj"]).numpy()
-    assert np.abs(got - want).max() <= LOGIT_TOL
-    _labels_check(got, want)
+    X, A = g["features"].to(DEV), g["adj"].to(DEV)
+    f = factor.get(as_csr(A), ops.Operand(X))
+    assert f is not None and f.H == 70 and f.Kc == 70
+    outs = {}
+    for fac in (True, False):
+        monkeypatch.setattr(ops, "FACTOR_GC1", fac)
+        torch.manual_seed(11)
+        m = GCN(nfeat=g["nfeat"], nhid=200, nclass=20, dropout=0.5,
+                dropout_rng="device" if mode == "train_hash" else "cpu").to(DEV)
+        m.train(mode != "eval")
+        if mode == "eval":
+            with torch.no_grad():
+                got = m(X, A)
+            outs[fac] = (got.cpu().numpy(), {})
+            if fac:
+                kinds = {r[2].kind for r in as_csr(A)._records.values() if r[2] is not None}
+                assert record.FACTORED in kinds, "config 3 takes the factored first layer"
+                ref = gcn_ref.RefGCN(nfeat=g["nfeat"], nhid=200, nclass=20, dropout=0.5).eval()
+                ref.load_state_dict({k: v.cpu() for k, v in m.state_dict().items()})
+                with torch.no_grad():
+                    want = ref(g["features"], g["adj"]).numpy()
+                assert np.abs(outs[fac][0] - want).max() <= LOGIT_TOL
+                _labels_check(outs[fac][0], want)
+        else:
+            lg = m(X, A)
+            lg.square().sum().backward()
+            outs[fac] = (lg.detach().cpu().numpy(), {k: p.grad.cpu().numpy() for k, p in m.named_parameters()})
+    (la, ga), (lb, gb) = outs[True], outs[False]
+    scale = max(1.0, float(np.abs(lb).max()))
+    assert np.abs(la - lb).max() <= 1e-5 * scale, float(np.abs(la - lb).max())
+    for k in ga:
+        np.testing.assert_allclose(ga[k], gb[k], rtol=1e-4, atol=1e-5 * max(1.0, float(np.abs(gb[k]).max())),
+                                   err_msg=k)
 
 
 @pytest.fixture(scope="module")
@@ -1051,12 +1084,17 @@ def test_factored_gc1_matches_spmm_path(r8, mode):
                                    err_msg=k)
 
 
-def test_factored_gc1_kernel_against_float64():
+@pytest.mark.parametrize("F,P", [(52, 3), (200, 20), (36, 32)])
+def test_factored_gc1_kernel_against_float64(F, P):
     """gcnk_hubfactor_gc1_f32 alone on a synthetic doc-topic graph with hub x
-    hub nonzeros, F not a multiple of 16, P = 3 and H1 stored: H1 and
-    S2 = H1 W2 against float64 (every epilogue code but the dropout ones),
-    rows written through the block order's row ids (hub rows spread over the
-    blocks, factor.py)."""
+    hub nonzeros, F not a multiple of 16 (and F < 64, where the n-tiles past F
+    read the zero pad after W1[Kc]), P of one and two MFMA n-tiles, H1 stored:
+    H1 and S2 = H1 W2 against float64 (every epilogue code but the dropout
+    ones), rows written through the block order's row ids (hub rows spread over
+    the blocks, factor.py).  Every launch follows one that filled all LDS with
+    NaN bits (gcnk_debug_poison_lds): a read of LDS the kernel did not write
+    would surface as NaN."""
+    import ctypes
     import scipy.sparse as ssp
     from graph_convolutional_networks_for_text_classification_amd import factor, ops
     from graph_convolutional_networks_for_text_classification_amd.sparse import as_csr
@@ -1067,7 +1105,6 @@ def test_factored_gc1_kernel_against_float64():
     assert f is not None
     assert not np.array_equal(f.perm.numpy(), np.arange(f.M))   # the hub rows moved
     rng = np.random.default_rng(3)
-    F, P = 52, 3
     W1 = torch.from_numpy(rng.standard_normal((g["nfeat"], F)).astype(np.float32)).to(DEV)
     W2 = torch.from_numpy(rng.standard_normal((F, P)).astype(np.float32)).to(DEV)
     b1 = torch.from_numpy(rng.standard_normal(F).astype(np.float32)).to(DEV)
@@ -1076,15 +1113,33 @@ def test_factored_gc1_kernel_against_float64():
     x = g["features"].coalesce()
     Xd = ssp.csr_matrix((x.values().double().numpy(), x.indices().numpy()), shape=tuple(x.shape))
     Z = Ad @ (Xd @ W1.cpu().double().numpy())
+    lib = _lib.load()
+
+    S_T = f.hub_times(W1).contiguous()
+    stream = ctypes.c_void_p(torch.cuda.current_stream().cuda_stream)
+
+    def launch(epi, store_h1=True):
+        """gcnk_hubfactor_gc1_f32 right after an LDS poison launch (as ops.hubfactor_gc1 calls it)."""
+        H1 = torch.empty((f.M, F), device=DEV) if store_h1 else None
+        S2 = torch.empty((f.M, P), device=DEV)
+        _lib.check(lib.gcnk_debug_poison_lds(0xFFFFFFFF, stream), "gcnk_debug_poison_lds")
+        p = lambda t: ctypes.c_void_p(t.data_ptr()) if t is not None else None
+        _lib.check(lib.gcnk_hubfactor_gc1_f32(
+            f.M, F, f.Kc, f.H, P, p(f.U), f.U.stride(0), p(W1), F, f.k0, p(S_T), F, p(f.rec), f.rec_words, p(b1), epi,
+            None, 0, 1.0, 1.0, 0, 0, None, p(W2), P, p(H1), F, p(S2), P, stream), "gcnk_hubfactor_gc1_f32")
+        return H1, S2
     for epi in (_lib.EPI_NONE, _lib.EPI_BIAS, _lib.EPI_BIAS_RELU):
-        H1, S2 = ops.hubfactor_gc1(f, W1, b1, W2, epilogue=epi)
+        H1, S2 = launch(epi)
+        assert bool(torch.isfinite(H1).all()) and bool(torch.isfinite(S2).all())
         want = Z if epi == _lib.EPI_NONE else Z + b1.cpu().double().numpy()
         if epi == _lib.EPI_BIAS_RELU:
             want = np.maximum(want, 0.0)
         _close(H1, want, atol=2e-5 * max(1.0, np.abs(want).max()))
         _close(S2, H1.cpu().double().numpy() @ W2.cpu().double().numpy(), atol=2e-5 * max(1.0, np.abs(want).max()))
-    H1b, S2b = ops.hubfactor_gc1(f, W1, b1, W2, epilogue=_lib.EPI_BIAS_RELU, store_h1=False)
+    H1b, S2b = launch(_lib.EPI_BIAS_RELU, store_h1=False)
     assert H1b is None and torch.equal(S2b, S2)
+    H1c, S2c = ops.hubfactor_gc1(f, W1, b1, W2, epilogue=_lib.EPI_BIAS_RELU)   # the op wrapper: same bits
+    assert torch.equal(H1c, H1) and torch.equal(S2c, S2)
 
 
 @pytest.mark.parametrize("mode", ["eval", "train_hash"])

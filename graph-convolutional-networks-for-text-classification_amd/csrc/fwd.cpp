@@ -91,8 +91,41 @@ extern "C" int32_t gcnk_gcn_fwd_layout(int64_t* out, int32_t n) {
   const int64_t v[] = {(int64_t)sizeof(gcnk_plan_ref), (int64_t)sizeof(gcnk_gcn_fwd),
                        (int64_t)offsetof(gcnk_gcn_fwd, x), (int64_t)offsetof(gcnk_gcn_fwd, U),
                        (int64_t)offsetof(gcnk_gcn_fwd, aF), (int64_t)offsetof(gcnk_gcn_fwd, aP),
-                       (int64_t)offsetof(gcnk_gcn_fwd, ld_h1_tmp), (int64_t)offsetof(gcnk_plan_ref, lanes_hint)};
+                       (int64_t)offsetof(gcnk_gcn_fwd, ld_h1_tmp), (int64_t)offsetof(gcnk_plan_ref, lanes_hint),
+                       (int64_t)sizeof(gcnk_gcn_bwd), (int64_t)offsetof(gcnk_gcn_bwd, xT),
+                       (int64_t)offsetof(gcnk_gcn_bwd, bwd2_ws_bytes)};
   const int32_t m = (int32_t)(sizeof(v) / sizeof(v[0]));
   for (int32_t i = 0; i < n && i < m; ++i) out[i] = v[i];
   return m;
+}
+
+// The backward record (gcnk_gcn_backward_f32): ops.GCNFn.backward's launches.
+extern "C" int gcnk_gcn_backward_f32(const gcnk_gcn_bwd* rec, const float* G, const float* H1, int64_t ldh,
+                                     const float* W2, float scale, float* gW1, float* gb1, float* gW2, float* gb2,
+                                     void* stream) {
+  if (!rec || !G || !H1 || !W2 || rec->M <= 0 || rec->F <= 0 || rec->P <= 0 || ldh < rec->F || !rec->aTP.plan ||
+      !rec->gS2 || !rec->gZ1 || (gW1 && (!rec->aTF.plan || !rec->gS1 || (!rec->xT.plan && !rec->x_dense)))) {
+    set_error("gcnk_gcn_backward_f32: null record/operand or incomplete record");
+    return GCNK_EARG;
+  }
+  const gcnk_gcn_bwd& r = *rec;
+  int rc;
+  // gS2 = A-hat^T G  (autograd of layer.py:106 in gc2)
+  if ((rc = spmm_ref(r.aTP, G, r.P, r.P, r.gS2, r.P, nullptr, GCNK_EPI_NONE, nullptr, 0, 1.f, 1.f, 0, 0, nullptr,
+                     stream)) != GCNK_OK)
+    return rc;
+  // gc2's weight/bias grads and gc1's ReLU + dropout backward (layer.py:102-110,182-188)
+  if ((rc = gcnk_gcn_bwd2_f32(H1, ldh, r.gS2, r.P, W2, r.P, gb2 ? G : nullptr, r.P, r.M, r.F, r.P, scale, r.gZ1, r.F,
+                              gW2, gb1, gb2, r.bwd2_ws, r.bwd2_ws_bytes, stream)) != GCNK_OK)
+    return rc;
+  if (!gW1) return GCNK_OK;
+  // gS1 = A-hat^T gZ1, gW1 = X^T gS1  (autograd of layer.py:106, :102 in gc1)
+  if ((rc = spmm_ref(r.aTF, r.gZ1, r.F, r.F, r.gS1, r.F, nullptr, GCNK_EPI_NONE, nullptr, 0, 1.f, 1.f, 0, 0, nullptr,
+                     stream)) != GCNK_OK)
+    return rc;
+  if (r.xT.plan)
+    return spmm_ref(r.xT, r.gS1, r.F, r.F, gW1, r.F, nullptr, GCNK_EPI_NONE, nullptr, 0, 1.f, 1.f, 0, 0, nullptr,
+                    stream);
+  return gcnk_gemm_f32(1, 0, r.x_cols, r.F, r.x_rows, r.x_dense, r.ldx, r.gS1, r.F, gW1, r.F, nullptr,
+                       GCNK_GEMM_EPI_NONE, nullptr, 0, 1.f, r.x_split_k, r.gemm_ws, r.gemm_ws_bytes, stream);
 }

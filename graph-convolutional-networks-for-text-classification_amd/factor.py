@@ -12,7 +12,8 @@ topic-weight columns, trainer.py:226-238).  Then
 with U [M x Kc] dense (rows in the block order ``perm``) -- row d (light): A_dd X[d, Kc]; row t (hub):
 sum over light d of A_td X[d, Kc] -- and A_H = A-hat restricted to hub columns.
 U and A_H depend only on (A-hat, X), so they are built here ONCE per operand
-pair (host, float64, rounded to fp32 once) and cached on the adjacency; every
+pair (on the device: csrc/factor_build.hip, float64 sums in a fixed order,
+rounded to fp32 once) and cached on the adjacency; every
 forward then runs X_hubs W1 (the tile GEMM over X's dense hub rows) and one
 launch of gcnk_hubfactor_gc1_f32 (U W1[Kc] on MFMA + A_H S_T + bias + ReLU +
 dropout + the gc2 projection H1 W2), and the hub rows' 600-term gather sums
@@ -25,7 +26,7 @@ import threading
 import numpy as np
 import torch
 
-from .sparse import from_arrays
+from .sparse import CSR
 
 MAX_HUBS = 128    # hub rows staged in LDS (S_T [hubs x F]; the kernel checks the LDS budget)
 # X[hubs] W1 through the SpMM tile plan on their CSR ("spmm", default) or the
@@ -59,115 +60,124 @@ class HubFactor:
         return gemm(self.x_hub_dense, W)
 
 
-def _hub_rows(rp, ci, M):
-    """Hub rows of A-hat (degree >= max(64, 8 x mean), at most MAX_HUBS) and
-    whether every other row references only hub columns and itself."""
-    deg = np.diff(rp)
-    nnz = int(rp[-1])
-    hmin = max(64, 8 * ((nnz + M - 1) // M))
-    hubs = np.flatnonzero(deg >= hmin)
-    if len(hubs) == 0 or len(hubs) > MAX_HUBS or len(hubs) >= M:
-        return None
-    is_hub = np.zeros(M, bool)
-    is_hub[hubs] = True
-    rows = np.repeat(np.arange(M), deg)
-    bad = ~is_hub[rows] & ~is_hub[ci] & (ci != rows)
-    if bad.any():
-        return None
-    return hubs, is_hub, rows
+def _perm(hubs, M):
+    """Row order: the light rows in order, hub j inserted near (j + 1/2) M / H."""
+    H = len(hubs)
+    light = np.ones(M, bool)
+    light[hubs] = False
+    lights = np.flatnonzero(light)
+    pos = ((np.arange(H) + 0.5) * M / H).astype(np.int64)
+    perm = np.insert(lights, np.minimum(pos - np.arange(H), len(lights)), hubs)
+    assert len(perm) == M
+    return perm
 
 
 def build(adj, xop):
-    """HubFactor for (adj, X) or None when the operands lack the structure."""
-    import scipy.sparse as sp
+    """HubFactor for (adj, X) on adj's device, or None when the operands lack
+    the structure.  The structure tests (hub rows, light rows touching only hub
+    columns and themselves, X's light-row column range) are device reductions
+    read back once each; U and the A_H records are csrc/factor_build.hip
+    (fixed-order float64 sums, bitwise the host restatement oracle/factor_host.py)."""
+    from . import _lib
     M, K = adj.shape
     if M != K or xop.shape[0] != M:
         return None
-    rp = adj.rowptr.cpu().numpy().astype(np.int64)
-    ci = adj.colind.cpu().numpy().astype(np.int64)
-    v = adj.val.cpu().numpy().astype(np.float64)
-    hr = _hub_rows(rp, ci, M)
-    if hr is None:
+    dev = adj.device
+    lib = _lib.load()
+    rp, ci, v = adj.rowptr, adj.colind, adj.val
+    nnz = adj.nnz
+    deg = rp[1:] - rp[:-1]
+    hmin = max(64, 8 * ((nnz + M - 1) // M))
+    hubs = torch.nonzero(deg >= hmin).flatten()
+    H = hubs.numel()
+    if H == 0 or H > MAX_HUBS or H >= M:
         return None
-    hubs, is_hub, rows = hr
-    H = len(hubs)
-    light = ~is_hub
-    # X restricted to the light rows: its column range [k0, k0 + Kc)
+    is_hub = torch.zeros(M, dtype=torch.bool, device=dev)
+    is_hub[hubs] = True
+    ar = torch.arange(M, device=dev, dtype=torch.int32)
+    rows = torch.repeat_interleave(ar, deg, output_size=nnz)
+    cil = ci.long()
+    if bool((~is_hub[rows] & ~is_hub[cil] & (ci != rows)).any()):
+        return None
+    # X's light rows: column range [k0, k0 + Kc)
     if xop.csr is not None:
         x = xop.csr
-        xrp = x.rowptr.cpu().numpy().astype(np.int64)
-        xci = x.colind.cpu().numpy().astype(np.int64)
-        xv = x.val.cpu().numpy().astype(np.float64)
-        X = sp.csr_matrix((xv, xci, xrp), shape=x.shape)
+        xrows = torch.repeat_interleave(torch.arange(x.shape[0], device=dev, dtype=torch.int32),
+                                        x.rowptr[1:] - x.rowptr[:-1], output_size=x.nnz)
+        sel = ~is_hub[xrows.long()] & (x.val != 0)
+        cols = x.colind[sel]
     else:
-        X = sp.csr_matrix(xop.dense.cpu().numpy().astype(np.float64))
-    XL = sp.diags(light.astype(np.float64)) @ X       # hub rows zeroed
-    XL.eliminate_zeros()
-    if XL.nnz:
-        k0, k1 = int(XL.indices.min()), int(XL.indices.max()) + 1
+        cols = torch.nonzero((xop.dense[~is_hub] != 0).any(0)).flatten()
+    if cols.numel():
+        k0, k1 = (int(t) for t in torch.stack([cols.min(), cols.max()]).cpu())
+        k1 += 1
     else:
         k0, k1 = 0, 1
     Kc = k1 - k0
     if Kc > MAX_KC:
         return None
     Kcp = (Kc + 3) // 4 * 4
-    Xr = XL[:, k0:k1]
-    A = sp.csr_matrix((v, ci, rp), shape=(M, M))
-    diag = A.diagonal()
-    Uo = np.zeros((M, Kcp), np.float64)
-    Uo[light, :Kc] = (sp.diags(diag[light]) @ Xr[light]).toarray()
-    Uo[hubs, :Kc] = (A[hubs] @ Xr).toarray()          # Xr's hub rows are zero: light columns only
-    # row order: light rows in order, hub j placed at position ~ (j + 1/2) M / H
-    lights = np.flatnonzero(light)
-    pos = ((np.arange(H) + 0.5) * M / H).astype(np.int64)
-    perm = np.insert(lights, np.minimum(pos - np.arange(H), len(lights)), hubs)
-    assert len(perm) == M and np.array_equal(np.sort(perm), np.arange(M))
-    U = Uo[perm]
-    # A_H: every row's hub-column nonzeros, as per-32-row-block records (row order perm)
-    hub_index = np.full(M, -1, np.int64)
-    hub_index[hubs] = np.arange(H)
-    mh = is_hub[ci]
-    counts = np.bincount(rows[mh], minlength=M)                     # hub items per original row
-    hstart = np.concatenate([[0], np.cumsum(counts)])
-    hcols, hvals = hub_index[ci[mh]], v[mh].astype(np.float32)      # CSR order within a row
+    hubs_h = hubs.cpu().numpy()
+    perm = _perm(hubs_h, M)
+    perm_d = torch.from_numpy(perm.astype(np.int32)).to(dev)
+    hub_index = torch.full((M,), -1, dtype=torch.int32, device=dev)
+    hub_index[hubs] = torch.arange(H, device=dev, dtype=torch.int32)
+    # X's light rows, columns [k0, k1), dense (hub rows never read)
+    if xop.csr is not None:
+        Xl = torch.zeros((M, Kcp), dtype=torch.float32, device=dev)
+        Xl[xrows[sel].long(), (cols - k0).long()] = x.val[sel]
+        ldxl = Kcp
+    else:
+        Xl = xop.dense[:, k0:]
+        ldxl = xop.dense.stride(0)
+        if xop.dense.stride(1) != 1:
+            raise RuntimeError("factor.build: dense features need unit column stride")
+    stream = torch.cuda.current_stream(dev).cuda_stream
+    U = torch.empty((M, Kcp), dtype=torch.float32, device=dev)
+    _lib.check(lib.gcnk_factor_u_f32(rp.data_ptr(), ci.data_ptr(), v.data_ptr(), M, hub_index.data_ptr(),
+                                     perm_d.data_ptr(), Xl.data_ptr(), ldxl, Kc, U.data_ptr(), Kcp, Kcp, stream),
+               "gcnk_factor_u_f32")
+    # A_H records: each block's hub items sized from per-row counts in block order
     nblk = (M + ROWS_PER_BLOCK - 1) // ROWS_PER_BLOCK
-    pcounts = counts[perm]
-    pstart = np.concatenate([[0], np.cumsum(pcounts)])
-    rec_words = 0
-    for b in range(nblk):
-        r0, r1 = b * ROWS_PER_BLOCK, min(M, (b + 1) * ROWS_PER_BLOCK)
-        rec_words = max(rec_words, REC_HEAD + 2 * int(pstart[r1] - pstart[r0]))
-    rec_words = (rec_words + 3) // 4 * 4
-    rec = np.zeros((nblk, rec_words), np.int32)
-    for b in range(nblk):
-        r0, r1 = b * ROWS_PER_BLOCK, min(M, (b + 1) * ROWS_PER_BLOCK)
-        off = pstart[r0:r1 + 1] - pstart[r0]
-        rec[b, :len(off)] = off
-        rec[b, len(off):ROWS_PER_BLOCK + 1] = off[-1]
-        rec[b, REC_ROW:REC_ROW + ROWS_PER_BLOCK] = -1
-        rec[b, REC_ROW:REC_ROW + (r1 - r0)] = perm[r0:r1]
-        items = np.concatenate([np.arange(hstart[r], hstart[r + 1]) for r in perm[r0:r1]]).astype(np.int64)
-        rec[b, REC_HEAD:REC_HEAD + 2 * len(items):2] = hcols[items]
-        rec[b, REC_HEAD + 1:REC_HEAD + 2 * len(items):2] = hvals[items].view(np.int32)
-    dev = adj.device
+    hub_item = is_hub[cil].to(torch.int32)
+    cs = torch.zeros(nnz + 1, dtype=torch.int64, device=dev)
+    cs[1:] = torch.cumsum(hub_item, 0)
+    counts = cs[rp[1:].long()] - cs[rp[:-1].long()]
+    pc = torch.zeros(nblk * ROWS_PER_BLOCK, dtype=torch.int64, device=dev)
+    pc[:M] = counts[perm_d.long()]
+    rec_words = (REC_HEAD + 2 * int(pc.view(nblk, ROWS_PER_BLOCK).sum(1).max()) + 3) // 4 * 4
+    rec = torch.zeros((nblk, rec_words), dtype=torch.int32, device=dev)
+    overflow = torch.zeros(1, dtype=torch.int32, device=dev)
+    _lib.check(lib.gcnk_factor_records(rp.data_ptr(), ci.data_ptr(), v.data_ptr(), M, hub_index.data_ptr(),
+                                       perm_d.data_ptr(), rec.data_ptr(), rec_words, overflow.data_ptr(), stream),
+               "gcnk_factor_records")
     f = HubFactor()
     f.nblk = nblk
     f.M, f.H, f.k0, f.Kc = M, H, k0, Kc
-    f.hubs = torch.from_numpy(hubs.astype(np.int64)).to(dev)
+    f.hubs = hubs.to(torch.int64)
     f.perm = torch.from_numpy(perm.astype(np.int64))            # host: tests and tools
-    f.U = torch.from_numpy(U.astype(np.float32)).to(dev)
-    f.rec = torch.from_numpy(rec).to(dev)
-    f.rec_words = rec_words
-    Xh = X[hubs].tocsr()
-    Xh.sort_indices()
+    f.U, f.rec, f.rec_words = U, rec, rec_words
     if xop.csr is not None:
-        f.x_hub = from_arrays(Xh.indptr.astype(np.int32), Xh.indices.astype(np.int32), Xh.data.astype(np.float32),
-                              (H, X.shape[1]), dev)
-        f.x_hub_dense = torch.from_numpy(Xh.toarray().astype(np.float32)).to(dev) \
-            if XHUB == "gemm" and H * X.shape[1] * 4 <= 64 << 20 else None
+        # X's hub rows as a CSR (rows in hub order)
+        xrp = x.rowptr.long()
+        lens = xrp[hubs + 1] - xrp[hubs]
+        hrp = torch.zeros(H + 1, dtype=torch.int64, device=dev)
+        hrp[1:] = torch.cumsum(lens, 0)
+        tot = int(hrp[-1])
+        idx = torch.repeat_interleave(xrp[hubs] - hrp[:-1], lens, output_size=tot) + \
+            torch.arange(tot, device=dev, dtype=torch.int64)
+        f.x_hub = CSR(hrp.to(torch.int32), x.colind[idx], x.val[idx], (H, x.shape[1]))
+        f.x_hub_dense = None
+        if XHUB == "gemm" and H * x.shape[1] * 4 <= 64 << 20:
+            d = torch.zeros((H, x.shape[1]), dtype=torch.float32, device=dev)
+            d[torch.repeat_interleave(torch.arange(H, device=dev), lens, output_size=tot), x.colind[idx].long()] = \
+                x.val[idx]
+            f.x_hub_dense = d
     else:
         f.x_hub = None
         f.x_hub_dense = xop.dense.index_select(0, f.hubs).contiguous()
+    if int(overflow.item()) != 0:
+        raise RuntimeError("factor.build: A_H records overflowed their sized length (internal error)")
     return f
 
 

@@ -458,6 +458,23 @@ def record_forward(W1, b1, W2, b2, xop, adj, epi, mask, scale, keep, seed, offse
                    keep_h1, stream)
 
 
+def record_backward(ctx, g, W2, H1, need):
+    """(gW1, gb1, gW2, gb2) of GCNFn.backward through the cached backward
+    record of (adj, X) -- or None where it is issued op by op (records or the
+    fused gcn_bwd2 off, more than 32 classes, or only gc2's grads wanted)."""
+    P = W2.shape[1]
+    if not (USE_RECORD and FUSE_BACKWARD) or P > 32 or not (need[0] or need[1]) or \
+            g.dtype != torch.float32 or H1.stride(1) != 1 or not W2.is_contiguous() or g.shape != (H1.shape[0], P):
+        return None
+    from . import record
+    dev = g.device
+    if dev.index != torch.cuda.current_device():
+        with torch.cuda.device(dev):
+            return record_backward(ctx, g, W2, H1, need)
+    rec, stream = record.get_backward(ctx.adj, ctx.xop, H1.shape[1], P, dev)
+    return rec.run(g, H1, W2, ctx.scale, need[0], ctx.has_b1 and need[1], need[2], ctx.has_b2 and need[3], stream)
+
+
 class GCNFn(torch.autograd.Function):
     """The two-layer forward of reference layer.py:164-190 as one fused graph:
 
@@ -516,11 +533,15 @@ class GCNFn(torch.autograd.Function):
         W2, H1 = ctx.saved_tensors
         g = g.contiguous()
         need = ctx.needs_input_grad
+        res = record_backward(ctx, g, W2, H1, need)
+        if res is not None:
+            return res + (None,) * 10
         gW1 = gb1 = gW2 = gb2 = None
         adjT = ctx.adj.t()
         gS2 = spmm(adjT, g)
         fused = gcn_bwd2(H1, gS2, W2, G=g if ctx.has_b2 and need[3] else None, scale=ctx.scale,
-                         want_gw=need[2], want_gb1=ctx.has_b1 and need[1]) if FUSE_BACKWARD else None
+                         want_gw=need[2], want_gb1=ctx.has_b1 and need[1]) \
+            if FUSE_BACKWARD and (need[0] or need[1]) else None
         if fused is not None:
             gZ1, gW2, gb1, gb2 = fused
         else:

@@ -1,4 +1,5 @@
-"""Whole-forward launch records (gcnk_gcn_forward_f32, include/gcnk.h).
+"""Whole-forward and whole-backward launch records (gcnk_gcn_forward_f32,
+gcnk_gcn_backward_f32, include/gcnk.h).
 
 The reference's trainer calls ``model.forward(features, adj)`` eagerly every
 epoch (trainer.py:357 train, trainer.py:382 eval).  Issued op by op, the
@@ -41,17 +42,27 @@ class GcnFwd(_c.Structure):
                 ("h1_tmp", _c.c_void_p), ("ld_h1_tmp", _c.c_int64)]
 
 
+class GcnBwd(_c.Structure):
+    """gcnk_gcn_bwd (include/gcnk.h)."""
+    _fields_ = [("M", _c.c_int32), ("F", _c.c_int32), ("P", _c.c_int32), ("x_rows", _c.c_int32),
+                ("x_cols", _c.c_int32), ("x_split_k", _c.c_int32), ("aTP", PlanRef), ("aTF", PlanRef),
+                ("xT", PlanRef), ("x_dense", _c.c_void_p), ("ldx", _c.c_int64), ("gemm_ws", _c.c_void_p),
+                ("gemm_ws_bytes", _c.c_int64), ("gS2", _c.c_void_p), ("gZ1", _c.c_void_p), ("gS1", _c.c_void_p),
+                ("bwd2_ws", _c.c_void_p), ("bwd2_ws_bytes", _c.c_int64)]
+
+
 FACTORED, SPMM_PROJ, SPMM_GEMM = 1, 2, 3
 KIND_NAMES = {FACTORED: "factored", SPMM_PROJ: "spmm+proj", SPMM_GEMM: "spmm+gemm"}
 
 
 def layout_ok():
     """The ctypes mirrors match the library's struct layout (gcnk_gcn_fwd_layout)."""
-    buf = (_c.c_int64 * 8)()
-    n = _lib.load().gcnk_gcn_fwd_layout(buf, 8)
+    buf = (_c.c_int64 * 11)()
+    n = _lib.load().gcnk_gcn_fwd_layout(buf, 11)
     want = [_c.sizeof(PlanRef), _c.sizeof(GcnFwd), GcnFwd.x.offset, GcnFwd.U.offset, GcnFwd.aF.offset,
-            GcnFwd.aP.offset, GcnFwd.ld_h1_tmp.offset, PlanRef.lanes_hint.offset]
-    return n == 8 and list(buf) == want
+            GcnFwd.aP.offset, GcnFwd.ld_h1_tmp.offset, PlanRef.lanes_hint.offset, _c.sizeof(GcnBwd),
+            GcnBwd.xT.offset, GcnBwd.bwd2_ws_bytes.offset]
+    return n == 11 and list(buf) == want
 
 
 def _fill_plan(ref, plan, F, lanes, device, keep):
@@ -158,15 +169,89 @@ class ForwardRecord:
         return out, H1
 
 
+class BackwardRecord:
+    """One filled gcnk_gcn_bwd: ops.GCNFn.backward's launches (A-hat^T G, the
+    fused gcn_bwd2, A-hat^T gZ1, X^T gS1) with their plans, workspaces and
+    scratch, issued by one ctypes call (bitwise the per-op backward)."""
+
+    __slots__ = ("s", "keep", "M", "F", "P", "x_cols", "src", "__weakref__")
+
+    def __init__(self, adj, xop, F, P, device):
+        lib = _lib.load()
+        M = adj.shape[0]
+        s = GcnBwd()
+        keep = []
+        s.M, s.F, s.P = M, F, P
+        adjT = adj.t()
+        keep.append(adjT)
+        for ref, width in ((s.aTP, P), (s.aTF, F)):
+            pl = adjT.plan(ops.default_ipc(adjT, width, 0), int(lib.gcnk_spmm_groups(width, 0)), DENSE_THRESHOLD)
+            _fill_plan(ref, pl, width, 0, device, keep)
+            keep.append(pl)
+        rows, cols = xop.shape
+        s.x_rows, s.x_cols = rows, cols
+        if xop.csr is not None:    # X^T gS1 = spmm(X^T, gS1)  (ops.XOperand.t_times)
+            xT = xop.csr.t()
+            pl = xT.plan(ops.default_ipc(xT, F, 0), int(lib.gcnk_spmm_groups(F, 0)), DENSE_THRESHOLD)
+            _fill_plan(s.xT, pl, F, 0, device, keep)
+            keep += [xT, pl]
+        else:                      # gemm(X, gS1, transA=True)
+            x = xop.dense
+            s.x_dense, s.ldx = x.data_ptr(), x.stride(0)
+            s.x_split_k = ops.default_split_k(cols, F, rows)
+            keep.append(x)
+            gws = int(lib.gcnk_gemm_workspace_bytes(cols, F, rows, s.x_split_k))
+            if gws > 0:
+                g = torch.empty((gws + 3) // 4, dtype=torch.float32, device=device)
+                keep.append(g)
+                s.gemm_ws, s.gemm_ws_bytes = g.data_ptr(), gws
+        gS2 = torch.empty((M, P), dtype=torch.float32, device=device)
+        gZ1 = torch.empty((M, F), dtype=torch.float32, device=device)
+        gS1 = torch.empty((rows, F), dtype=torch.float32, device=device)
+        keep += [gS2, gZ1, gS1]
+        s.gS2, s.gZ1, s.gS1 = gS2.data_ptr(), gZ1.data_ptr(), gS1.data_ptr()
+        wsb = int(lib.gcnk_gcn_bwd2_workspace_bytes(M, F, P))
+        if wsb > 0:
+            w = torch.empty((wsb + 3) // 4, dtype=torch.float32, device=device)
+            keep.append(w)
+            s.bwd2_ws, s.bwd2_ws_bytes = w.data_ptr(), wsb
+        self.s, self.keep, self.M, self.F, self.P, self.x_cols = s, keep, M, F, P, cols
+        self.src = (adj, xop.csr if xop.csr is not None else xop.dense)
+
+    def run(self, G, H1, W2, scale, want_gw1, want_gb1, want_gw2, want_gb2, stream):
+        """(gW1, gb1, gW2, gb2), each None unless wanted."""
+        dev = G.device
+        gW1 = torch.empty((self.x_cols, self.F), dtype=torch.float32, device=dev) if want_gw1 else None
+        gb1 = torch.empty(self.F, dtype=torch.float32, device=dev) if want_gb1 else None
+        gW2 = torch.empty((self.F, self.P), dtype=torch.float32, device=dev) if want_gw2 else None
+        gb2 = torch.empty(self.P, dtype=torch.float32, device=dev) if want_gb2 else None
+        rc = _lib.load().gcnk_gcn_backward_f32(
+            _c.byref(self.s), G.data_ptr(), H1.data_ptr(), H1.stride(0), W2.data_ptr(), scale,
+            gW1.data_ptr() if gW1 is not None else None, gb1.data_ptr() if gb1 is not None else None,
+            gW2.data_ptr() if gW2 is not None else None, gb2.data_ptr() if gb2 is not None else None, stream)
+        _lib.check(rc, "gcnk_gcn_backward_f32")
+        return gW1, gb1, gW2, gb2
+
+
 _lock = threading.Lock()
+
+
+def get_backward(adj, xop, F, P, device):
+    """(record, stream): the BackwardRecord of (adj, X, F, P) for torch's
+    current stream, built on first use, and that stream."""
+    return _get(adj, xop, F, P, device, BackwardRecord, "bwd")
 
 
 def get(adj, xop, F, P, device):
     """(record, stream): the ForwardRecord of (adj, X, F, P) for torch's current
     stream, built on first use, and that stream."""
+    return _get(adj, xop, F, P, device, ForwardRecord, "fwd")
+
+
+def _get(adj, xop, F, P, device, cls, tag):
     stream = torch.cuda.current_stream(device).cuda_stream
     src = xop.csr if xop.csr is not None else xop.dense
-    key = (id(src), F, P, stream, ops.FACTOR_GC1, ops.FUSE_PROJECTION)
+    key = (tag, id(src), F, P, stream, ops.FACTOR_GC1, ops.FUSE_PROJECTION)
     recs = getattr(adj, "_records", None)
     if recs is None:
         with _lock:
@@ -177,7 +262,7 @@ def get(adj, xop, F, P, device):
     if hit is not None and hit[0] is src and _version(src) == hit[1]:
         return hit[2], stream
     with _lock:
-        rec = ForwardRecord(adj, xop, F, P, device)
+        rec = cls(adj, xop, F, P, device)
         while len(recs) >= 8:
             recs.pop(next(iter(recs)))
         recs[key] = (src, _version(src), rec)

@@ -269,6 +269,25 @@ int gcnk_hubfactor_gc1_f32(int32_t M, int32_t F, int32_t Kc, int32_t nhub, int32
                            uint64_t offset, const uint64_t* rng_base, const float* W2, int64_t ldw2, float* H,
                            int64_t ldh, float* C2, int64_t ldc2, void* stream);
 
+/* The hub factorisation's (A-hat, X)-fixed operands, built on the device once
+ * per operand pair (csrc/factor_build.hip; factor.py drives it, the host
+ * restatement is oracle/factor_host.py):
+ *   gcnk_factor_u_f32:   U[p, c] = fp32( sum over the items (r, d) of row
+ *                        r = perm[p], d light (hub_index[d] < 0), in CSR order,
+ *                        in float64, of val * Xl[d, c] ), c < Kc; 0 for
+ *                        Kc <= c < Kcp <= 128.  Xl [M x >= Kc] (ldxl): X's
+ *                        columns k0.. (hub rows never read).
+ *   gcnk_factor_records: the per-32-row-block A_H records gcnk_hubfactor_gc1_f32
+ *                        reads, into a zeroed rec [ceil(M/32) x rec_words];
+ *                        *overflow (zeroed int) counts blocks whose items
+ *                        did not fit. */
+int gcnk_factor_u_f32(const int32_t* rowptr, const int32_t* colind, const float* val, int32_t M,
+                      const int32_t* hub_index, const int32_t* perm, const float* Xl, int64_t ldxl, int32_t Kc,
+                      float* U, int64_t ldu, int32_t Kcp, void* stream);
+int gcnk_factor_records(const int32_t* rowptr, const int32_t* colind, const float* val, int32_t M,
+                        const int32_t* hub_index, const int32_t* perm, int32_t* rec, int32_t rec_words,
+                        int32_t* overflow, void* stream);
+
 /* ---------------------------------------------------------------------------
  * Whole-forward launch record (ABI 8): GCN.forward (layer.py:164-190) as the
  * reference's trainer issues it, eagerly, every epoch (trainer.py:357 train,
@@ -337,9 +356,39 @@ int gcnk_gcn_forward_f32(const gcnk_gcn_fwd* rec,
                          int32_t epilogue, const uint8_t* drop_mask, int64_t ldm, float drop_scale,
                          float keep_prob, uint64_t seed, uint64_t offset, const uint64_t* rng_base,
                          void* stream);
-/* Layout of the two structs for bindings that mirror them: writes up to n of
- * {sizeof plan_ref, sizeof gcn_fwd, offsetof x, U, aF, aP, ld_h1_tmp,
- * plan_ref.lanes_hint} to out and returns how many exist. */
+/* The backward of the same forward (trainer.py:361 loss.backward()), from
+ * one call, with gcnk_gcn_bwd filled once per (adjacency, features, widths,
+ * stream) -- the launches ops.GCNFn.backward issues, in its order:
+ *   gS2 = A-hat^T G                          (aTP: A-hat^T's plan at width P)
+ *   gZ1, gW2, gb1, gb2 = gcnk_gcn_bwd2_f32(H1, gS2, W2, G)  (bwd2 workspace)
+ *   gS1 = A-hat^T gZ1; gW1 = X^T gS1         (aTF; X^T's plan xT, or the MFMA
+ *                                             GEMM on dense X with x_split_k)
+ * G = dlogits [M x P] (contiguous), H1 [M x F] (ldh), W2 [F x P].  gW1, gb1,
+ * gW2, gb2 are nullable (not computed); gb2 needs G's column sums only. */
+typedef struct gcnk_gcn_bwd {
+  int32_t M, F, P;             /* rows of A-hat, nhid, nclass */
+  int32_t x_rows, x_cols;      /* X [x_rows x x_cols]: gW1 is [x_cols x F] */
+  int32_t x_split_k;           /* dense X: K-slabs of X^T gS1 */
+  gcnk_plan_ref aTP, aTF;      /* A-hat^T at widths P and F */
+  gcnk_plan_ref xT;            /* sparse X: X^T's plan at width F (xT.plan != NULL) ... */
+  const float* x_dense;        /* ... or dense X (ldx) */
+  int64_t ldx;
+  float* gemm_ws;              /* split-K workspace of X^T gS1 */
+  int64_t gemm_ws_bytes;
+  float* gS2;                  /* scratch [M x P] */
+  float* gZ1;                  /* scratch [M x F] */
+  float* gS1;                  /* scratch [M x F] */
+  void* bwd2_ws;               /* gcnk_gcn_bwd2_workspace_bytes(M, F, P) */
+  int64_t bwd2_ws_bytes;
+} gcnk_gcn_bwd;
+
+int gcnk_gcn_backward_f32(const gcnk_gcn_bwd* rec, const float* G, const float* H1, int64_t ldh, const float* W2,
+                          float scale, float* gW1, float* gb1, float* gW2, float* gb2, void* stream);
+
+/* Layout of the record structs for bindings that mirror them: writes up to n
+ * of {sizeof plan_ref, sizeof gcn_fwd, offsetof x, U, aF, aP, ld_h1_tmp,
+ * plan_ref.lanes_hint, sizeof gcn_bwd, gcn_bwd.xT, gcn_bwd.bwd2_ws_bytes} to
+ * out and returns how many exist. */
 int32_t gcnk_gcn_fwd_layout(int64_t* out, int32_t n);
 
 /* ---------------------------------------------------------------------------

@@ -3,7 +3,7 @@ cd "${GRAFT_REPO_ROOT:-/root/repo}" || exit 2
 mkdir -p gpurun_out/r04 gpurun_out/micro
 export TMPDIR=/tmp
 timeout -k 10 300 python -u -m pytest tests/test_gpu_parity.py -m gpu -s -p no:cacheprovider --timeout 120 --timeout-method thread \
-  -k "trained_model or 20ng or factored_gc1_kernel" > gpurun_out/r04/pytest_b.log 2>&1
+  -k "trained_model or 20ng or factored_gc1_kernel or forward_record or factor_build" > gpurun_out/r04/pytest_b.log 2>&1
 rc=$?; echo "pytest rc=$rc"; grep -E "passed|failed|trained model|FAIL|Error" gpurun_out/r04/pytest_b.log | tail -n 12
 if [ $rc -ne 0 ] && [ $rc -ne 1 ]; then exit $rc; fi
 python3 scripts/micro/dump_r8.py /tmp/r8.bin >/dev/null || exit 3
@@ -15,3 +15,5 @@ GCNK_LIB=_variants/libgcnk_rowsc1.so timeout -k 10 300 python -u scripts/hub_pro
 cut -c1-300 gpurun_out/r04/probe_sc1.log | grep -v amdgpu.ids
 timeout -k 10 500 python -u bench.py > gpurun_out/r04/bench.log 2>&1; echo "bench rc=$?"
 tail -c 600 gpurun_out/r04/bench.log
+timeout -k 10 300 python -u scripts/eager_fwd_profile.py > gpurun_out/r04/eager.log 2>&1; echo "eager rc=$?"
+grep -E "eager" gpurun_out/r04/eager.log

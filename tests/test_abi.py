@@ -131,3 +131,22 @@ def test_forward_record_layout_and_validation():
     r.aF.plan = 16
     assert lib.gcnk_gcn_forward_f32(ctypes.byref(r), *args) == _lib.EARG
     assert b"unknown record kind" in lib.gcnk_last_error()
+
+
+def test_backward_record_validation():
+    """gcnk_gcn_backward_f32 refuses a null or incomplete record before any
+    launch (no GPU needed)."""
+    from graph_convolutional_networks_for_text_classification_amd import record
+    lib = _lib.load()
+    p = ctypes.c_void_p(16)
+    args = (p, p, 200, p, 1.0, p, None, None, None, None)
+    assert lib.gcnk_gcn_backward_f32(None, *args) == _lib.EARG
+    r = record.GcnBwd()
+    r.M, r.F, r.P = 10, 200, 8
+    r.aTP.plan, r.gS2, r.gZ1 = 16, 16, 16
+    assert lib.gcnk_gcn_backward_f32(ctypes.byref(r), *args) == _lib.EARG   # gW1 wanted, no A^T / X^T plan
+    assert b"incomplete record" in lib.gcnk_last_error()
+    r.aTF.plan, r.gS1 = 16, 16
+    assert lib.gcnk_gcn_backward_f32(ctypes.byref(r), *args) == _lib.EARG   # neither X^T plan nor dense X
+    r.M = 0
+    assert lib.gcnk_gcn_backward_f32(ctypes.byref(r), p, p, 200, p, 1.0, None, None, p, None, None) == _lib.EARG

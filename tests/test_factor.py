@@ -1,5 +1,7 @@
-"""CPU checks of the hub factorisation (factor.py) behind the factored gc1
-kernel (csrc/factor.hip): the operands it builds reproduce A-hat X W1 of the
+"""CPU checks of the hub factorisation behind the factored gc1 kernel
+(csrc/factor.hip), on its host restatement oracle/factor_host.py (the device
+build, factor.py + csrc/factor_build.hip, is pinned to it bit for bit by
+tests/test_gpu_parity.py): the operands it builds reproduce A-hat X W1 of the
 reference (layer.py:102,106) in float64 on the reference-built R8 graph and on
 synthetic doc-topic graphs, the per-block records hold exactly A-hat's
 hub-column nonzeros, and graphs without the structure are refused."""
@@ -11,8 +13,9 @@ import scipy.sparse as sp
 import torch
 
 import gcn_amd  # noqa: F401
-from graph_convolutional_networks_for_text_classification_amd import datasets, factor
+from graph_convolutional_networks_for_text_classification_amd import datasets
 from graph_convolutional_networks_for_text_classification_amd.sparse import from_arrays
+from oracle import factor_host as factor
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 
@@ -42,12 +45,12 @@ def _check_factor(A, X, F=24, seed=0):
     W1 = np.random.default_rng(seed).standard_normal((X.shape[1], F))
     Af, Xf = A.astype(np.float64), X.astype(np.float64)
     ref = Af @ (Xf @ W1)
-    U = f.U.numpy().astype(np.float64)
-    hubs = f.hubs.numpy()
-    perm = f.perm.numpy()
+    U = f.U.astype(np.float64)
+    hubs = f.hubs
+    perm = f.perm
     S_T = Xf[hubs] @ W1
     Z = U[:, :f.Kc] @ W1[f.k0:f.k0 + f.Kc]          # block order: position i holds row perm[i]
-    rec = f.rec.numpy()
+    rec = f.rec
     M = A.shape[0]
     assert np.array_equal(np.sort(perm), np.arange(M))
     nnz_h = 0
@@ -86,7 +89,7 @@ def test_factor_reproduces_r8_product():
     f = _check_factor(Asp, Xsp, F=16)
     # R8: the 50 topic rows are the hubs; documents use topic-weight columns 0..49
     assert f.H == 50 and f.k0 == 0 and f.Kc == 50
-    assert f.hubs.numpy().tolist() == list(range(7674, 7724))
+    assert f.hubs.tolist() == list(range(7674, 7724))
 
 
 @pytest.mark.parametrize("ndoc,ntopic,seed", [(600, 12, 1), (1500, 40, 3), (333, 7, 5)])
@@ -119,12 +122,12 @@ def test_factor_dense_features():
     A = sp.diags(dinv) @ A @ sp.diags(dinv)
     X = rng.standard_normal((M, 100)).astype(np.float32)
     f = factor.build(_csr(A), _XOp(dense=torch.from_numpy(X)))
-    assert f is not None and f.Kc == 100 and f.k0 == 0 and f.x_hub_dense is not None
+    assert f is not None and f.Kc == 100 and f.k0 == 0
     W1 = rng.standard_normal((100, 8))
-    hubs = f.hubs.numpy()
+    hubs = f.hubs
     ref = A @ (X.astype(np.float64) @ W1)
-    perm = f.perm.numpy()
-    Z = f.U.numpy()[:, :100].astype(np.float64) @ W1       # rows in the block order
+    perm = f.perm
+    Z = f.U[:, :100].astype(np.float64) @ W1       # rows in the block order
     Zh = A[:, hubs] @ (X[hubs].astype(np.float64) @ W1)
     assert np.abs(Z + Zh[perm] - ref[perm]).max() < 1e-5 * max(1, np.abs(ref).max())
 

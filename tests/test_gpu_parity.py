@@ -1189,9 +1189,10 @@ def test_factored_forward_hub_rows_first_ragged(mode):
 @pytest.mark.parametrize("path", ["factored", "spmm_proj", "spmm_gemm", "dense_factored", "dense_spmm"])
 @pytest.mark.parametrize("mode", ["eval", "train_mask", "train_hash"])
 def test_forward_record_is_bitwise_the_per_op_path(r8, path, mode, monkeypatch):
-    """gcnk_gcn_forward_f32 (record.py: the whole forward from one C call)
-    issues the per-op path's launches with the same arguments: logits and every
-    gradient bitwise equal to ops.USE_RECORD = False, for each record kind
+    """gcnk_gcn_forward_f32 / gcnk_gcn_backward_f32 (record.py: the whole
+    forward, the whole backward from one C call each) issue the per-op path's
+    launches with the same arguments: logits and every gradient bitwise equal
+    to ops.USE_RECORD = False, for each record kind
     (factored / fused projection / SpMM + GEMM, sparse and dense X), in eval
     (inference fast path, no autograd node) and in both dropout modes."""
     from graph_convolutional_networks_for_text_classification_amd import ops, record
@@ -1227,7 +1228,10 @@ def test_forward_record_is_bitwise_the_per_op_path(r8, path, mode, monkeypatch):
     for k in outs[True][1]:
         assert torch.equal(outs[True][1][k], outs[False][1][k]), k
     from graph_convolutional_networks_for_text_classification_amd.sparse import as_csr
-    kinds = {r[2].kind for r in getattr(as_csr(A), "_records", {}).values() if r[2] is not None}
+    recs = [r[2] for r in getattr(as_csr(A), "_records", {}).values()]
+    kinds = {r.kind for r in recs if isinstance(r, record.ForwardRecord)}
+    # the training modes' backward went through gcnk_gcn_backward_f32
+    assert (mode != "eval") == any(isinstance(r, record.BackwardRecord) for r in recs)
     want = {"factored": record.FACTORED, "dense_factored": record.FACTORED, "spmm_proj": record.SPMM_PROJ,
             "spmm_gemm": record.SPMM_GEMM}.get(path)
     if want is not None:
@@ -1249,3 +1253,55 @@ def test_forward_record_follows_in_place_feature_updates(r8):
         ref = m(torch.sparse_coo_tensor(X._indices(), X._values().clone(), X.shape).coalesce(), A)
     assert not torch.equal(a, b)
     assert torch.equal(b, ref)
+
+
+# ------------------------------------------------------------------------------ device factor build
+
+@pytest.mark.parametrize("case", ["r8", "doc_topic_tt", "hubs_first_dense", "20ng"])
+def test_device_factor_build_is_bitwise_the_host_build(r8, case):
+    """factor.build (csrc/factor_build.hip: U as fixed-order float64 sums over
+    each row's CSR items, the A_H block records by ballot compaction) against
+    the host float64 restatement oracle/factor_host.py: the structure (hubs,
+    k0, Kc, row order), U bit for bit after the one fp32 rounding, the records
+    word for word and X's hub rows -- on R8, a doc-topic graph with
+    topic-topic edges, a renumbered graph with the hubs first, a ragged M and
+    dense X, and the 20ng-shaped graph (70 hubs, BASELINE config 3)."""
+    from graph_convolutional_networks_for_text_classification_amd import factor, ops
+    from graph_convolutional_networks_for_text_classification_amd.sparse import as_csr
+    from oracle import factor_host
+    if case == "r8":
+        A, X = r8["adj"], r8["features"]
+    elif case == "doc_topic_tt":
+        g = datasets.doc_topic_graph(2000, 40, 5, seed=4, tt_prob=0.3)
+        A, X = g["adj"], g["features"]
+    elif case == "hubs_first_dense":
+        g = datasets.doc_topic_graph(1001, 37, 5, seed=11)
+        n = g["nodes"]
+        order = np.concatenate([np.arange(1001, n), np.arange(1001)])
+        inv = np.empty(n, np.int64)
+        inv[order] = np.arange(n)
+        a = g["adj"].coalesce()
+        A = torch.sparse_coo_tensor(torch.from_numpy(inv)[a.indices()], a.values(), (n, n)).coalesce()
+        X = torch.from_numpy(np.ascontiguousarray(g["features_dense"][order]))
+    else:
+        g = datasets.doc_topic_graph(18846, 70, 20, seed=0)
+        A, X = g["adj"], g["features"]
+    a = as_csr(A.to(DEV))
+    xop = ops.Operand(X.to(DEV))
+    d = factor.build(a, xop)
+    torch.cuda.synchronize()
+    h = factor_host.build(a, xop)
+    assert d is not None and h is not None
+    assert (d.M, d.H, d.k0, d.Kc, d.nblk, d.rec_words) == (h.M, h.H, h.k0, h.Kc, h.nblk, h.rec_words)
+    assert np.array_equal(d.hubs.cpu().numpy(), h.hubs) and np.array_equal(d.perm.numpy(), h.perm)
+    Ud = d.U.cpu().numpy()
+    assert Ud.shape == h.U.shape
+    bad = np.flatnonzero((Ud.view(np.int32) != h.U.view(np.int32)).any(1))
+    assert bad.size == 0, f"U differs on {bad.size} rows, first at position {bad[:4]}"
+    assert np.array_equal(d.rec.cpu().numpy(), h.rec)
+    if xop.csr is not None:
+        assert np.array_equal(d.x_hub.rowptr.cpu().numpy(), h.x_hub_rowptr)
+        assert np.array_equal(d.x_hub.colind.cpu().numpy(), h.x_hub_colind)
+        assert np.array_equal(d.x_hub.val.cpu().numpy().view(np.int32), h.x_hub_val.view(np.int32))
+    else:
+        assert torch.equal(d.x_hub_dense.cpu(), X[torch.from_numpy(h.hubs)])

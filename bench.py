@@ -158,9 +158,12 @@ def timed_cpu(fn, budget_s):
     return (time.perf_counter() - t0) / n, n
 
 
-def pmc_traffic(op, kernels_like):
-    """HBM-side bytes per launch of the op's kernels from two child rocprofv3
-    --pmc passes (FETCH_SIZE x 2 per the gfx950 correction + WRITE_SIZE)."""
+def pmc_traffic(op, kernels_like, detail=None):
+    """HBM-side bytes per launch of the op's kernels from child rocprofv3 --pmc
+    passes, one counter each (FETCH_SIZE x 2 per the gfx950 correction +
+    WRITE_SIZE), and the L1 -> L2 read requests (TCP_TCC_READ_REQ_sum, 128 B
+    each on gfx950) in a third pass; `detail` (a dict) receives the per-counter
+    figures."""
     exe = shutil.which("rocprofv3")
     if exe is None:
         return None, "rocprofv3 not on PATH"
@@ -168,7 +171,7 @@ def pmc_traffic(op, kernels_like):
     env = dict(os.environ, TMPDIR="/tmp")
     per = {}
     try:
-        for counter in ("FETCH_SIZE", "WRITE_SIZE"):
+        for counter in ("FETCH_SIZE", "WRITE_SIZE", "TCP_TCC_READ_REQ_sum"):
             out = os.path.join(tmp, counter)
             cmd = ["timeout", "-s", "KILL", "120", exe, "--pmc", counter, "--output-format", "csv", "-d", out,
                    "-o", "run", "--", sys.executable, os.path.join(ROOT, "scripts", "pmc_ops.py"), "--op", op,
@@ -184,8 +187,13 @@ def pmc_traffic(op, kernels_like):
                         vals.setdefault(name, []).append(float(row["Counter_Value"]))
             if not vals:
                 return None, f"no {counter} rows for {kernels_like}"
-            # per launch of the op: sum over its kernels of the mean per dispatch (KiB)
-            per[counter] = sum(sum(v) / len(v) for v in vals.values()) * 1024
+            # per launch of the op: sum over its kernels of the mean per dispatch
+            # (FETCH_SIZE / WRITE_SIZE in KiB, the request count as is)
+            per[counter] = sum(sum(v) / len(v) for v in vals.values()) * (1 if counter.startswith("TCP") else 1024)
+        if detail is not None:
+            detail.update({"fetch_bytes_x2": 2 * per["FETCH_SIZE"], "write_bytes": per["WRITE_SIZE"],
+                           "l2_read_req": per["TCP_TCC_READ_REQ_sum"],
+                           "l2_read_bytes": 128 * per["TCP_TCC_READ_REQ_sum"]})
         return 2 * per["FETCH_SIZE"] + per["WRITE_SIZE"], "live rocprofv3 --pmc (FETCH_SIZE x2 + WRITE_SIZE)"
     except (OSError, subprocess.SubprocessError, KeyError, ValueError) as e:
         return None, f"pmc pass failed: {e}"
@@ -594,8 +602,9 @@ def main():
     extras = rank == 0 and world == 1
     # ---- live HBM traffic of the north-star op (child rocprofv3 --pmc passes)
     traffic, traffic_src = (None, "skipped")
+    traffic_detail = {}
     if extras and not args.no_pmc:
-        traffic, traffic_src = pmc_traffic("AS1", ["spmm_row_kernel"])
+        traffic, traffic_src = pmc_traffic("AS1", ["spmm_row_kernel"], traffic_detail)
     # ---- the same op's kernel durations from rocprofv3 (warm and cold rotations)
     kt = {}
     if extras and not args.no_rocprof:
@@ -757,7 +766,7 @@ def main():
     roof = {"bound": "hbm", "kernel": north, "plan": "row",
             "achieved": nb / (dur * 1e-6) / 1e9, "peak": HBM_PEAK_GBS, "unit": "GB/s",
             "frac": nb / (dur * 1e-6) / 1e9 / HBM_PEAK_GBS, "frac_warm": nb / (dur_w * 1e-6) / 1e9 / HBM_PEAK_GBS,
-            "traffic": traffic, "traffic_source": traffic_src,
+            "traffic": traffic, "traffic_source": traffic_src, "traffic_detail": traffic_detail or None,
             "avg_launch_us": round(dur, 3), "avg_launch_us_warm": round(dur_w, 3), "duration_source": src,
             "hip_events": {"avg_call_us": kn["cold_us"], "avg_call_us_warm": kn["warm_us"],
                            "frac": kn["frac_cold"], "frac_warm": kn["frac_warm"]},

@@ -218,8 +218,11 @@ def get(adj, xop):
     """The cached HubFactor of (adj, X), built on first use; None when the
     operands do not factor (the caller runs the generic SpMM path)."""
     src = xop.csr if xop.csr is not None else xop.dense
+    # U and A_H bake in A-hat's values too: an in-place change of either
+    # operand's values is a new key (ADVICE r3)
     key = (id(src), src.data_ptr() if isinstance(src, torch.Tensor) else src.rowptr.data_ptr(),
-           src._version if isinstance(src, torch.Tensor) else src.val._version)
+           src._version if isinstance(src, torch.Tensor) else src.val._version,
+           adj.val.data_ptr(), adj.val._version)
     cache = getattr(adj, "_factors", None)
     if cache is None:
         with _lock:

@@ -12,7 +12,9 @@ for v in copy lds; do
   NS_ONLY=$v timeout -k 5 90 scripts/micro/ns_micro /tmp/r8.bin 128 > gpurun_out/micro/ns_$v.log 2>&1; echo "$v micro rc=$?"
   grep -E "variant|hipFunc|error" gpurun_out/micro/ns_$v.log | cut -c1-240
 done
-GCNK_LIB=_variants/libgcnk_rowsc1.so timeout -k 10 300 python -u scripts/hub_probe.py --variants row,copy --widths 200 --reps 200 > gpurun_out/r04/probe_sc1.log 2>&1; echo "sc1 rc=$?"
+timeout -k 10 300 python -u scripts/hub_probe.py --variants row,light,topic,copy --widths 200,8 --reps 200 > gpurun_out/r04/probe_subsets.log 2>&1; echo "subsets rc=$?"
+cut -c1-300 gpurun_out/r04/probe_subsets.log | grep -v amdgpu.ids
+GCNK_LIB=_variants/libgcnk_rowsc1.so timeout -k 10 300 python -u scripts/hub_probe.py --variants row,light,topic,copy --widths 200 --reps 200 > gpurun_out/r04/probe_sc1.log 2>&1; echo "sc1 rc=$?"
 cut -c1-300 gpurun_out/r04/probe_sc1.log | grep -v amdgpu.ids
 timeout -k 10 500 python -u bench.py > gpurun_out/r04/bench.log 2>&1; echo "bench rc=$?"
 tail -c 600 gpurun_out/r04/bench.log

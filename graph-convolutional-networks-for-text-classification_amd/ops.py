@@ -309,6 +309,23 @@ def colsum(X):
     return out
 
 
+_BWD2_WS = {}
+
+
+def _bwd2_workspace(M, N, P, dev):
+    """gcnk_gcn_bwd2_f32's workspace for torch's current stream: zeroed once
+    (its trailing counter words must be zero on entry; every launch leaves
+    them zero), then reused by every call of that shape on that stream."""
+    key = (M, N, P, dev.index, torch.cuda.current_stream(dev).cuda_stream)
+    hit = _BWD2_WS.get(key)
+    if hit is None:
+        wsb = int(_lib.load().gcnk_gcn_bwd2_workspace_bytes(M, N, P))
+        if len(_BWD2_WS) >= 32:
+            _BWD2_WS.pop(next(iter(_BWD2_WS)))
+        hit = _BWD2_WS[key] = (wsb, torch.zeros((wsb + 3) // 4, dtype=torch.float32, device=dev))
+    return hit
+
+
 def gcn_bwd2(H1, gS2, W2, G=None, scale=1.0, want_gw=True, want_gb1=True):
     """The fused backward of gc2 and of gc1's ReLU + dropout (gcnk_gcn_bwd2_f32):
     returns (gZ1, gW2, gb1, gb2) with
@@ -339,8 +356,7 @@ def gcn_bwd2(H1, gS2, W2, G=None, scale=1.0, want_gw=True, want_gb1=True):
     gb1 = torch.empty(N, dtype=torch.float32, device=dev) if want_gb1 else None
     gb2 = torch.empty(P, dtype=torch.float32, device=dev) if G is not None else None
     lib = _lib.load()
-    wsb = lib.gcnk_gcn_bwd2_workspace_bytes(M, N, P)
-    ws = torch.empty((wsb + 3) // 4, dtype=torch.float32, device=dev)
+    wsb, ws = _bwd2_workspace(M, N, P, dev)
     with torch.cuda.device(dev):
         rc = lib.gcnk_gcn_bwd2_f32(_ptr(H1), H1.stride(0), _ptr(gS2), gS2.stride(0), _ptr(W2), W2.stride(0),
                                    _ptr(G), G.stride(0) if G is not None else 0, M, N, P, float(scale),

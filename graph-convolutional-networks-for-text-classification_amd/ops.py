@@ -196,13 +196,13 @@ FACTOR_GC1 = os.environ.get("GCNK_FACTOR_GC1", "1") != "0"
 
 
 def hubfactor_gc1(f, W1, b1, W2, epilogue=_lib.EPI_BIAS_RELU, mask=None, scale=1.0, keep_prob=1.0, seed=0,
-                  offset=0, rng_base=None, store_h1=True):
+                  offset=0, rng_base=None, store_h1=True, S=None):
     """(H1, S2) of gc1 + gc2's support through the hub factorisation ``f``
     (factor.HubFactor): S_T = X[hubs] W1 (layer.py:102, the tile GEMM), then
     one launch of gcnk_hubfactor_gc1_f32 -- H1 = drop(relu(A-hat X W1 + b1))
     (layer.py:106,110,182,185) and S2 = H1 W2 (layer.py:102, gc2).  Returns
     None when the shapes are outside the kernel's range (the caller takes the
-    SpMM path)."""
+    SpMM path).  ``S``: S_T already computed (timing probes)."""
     W1 = _dense_f32(W1, "gc1 weight")
     W2 = _dense_f32(W2, "gc2 weight")
     _check_rng_base(rng_base, W1.device)
@@ -216,7 +216,7 @@ def hubfactor_gc1(f, W1, b1, W2, epilogue=_lib.EPI_BIAS_RELU, mask=None, scale=1
     lib = _lib.load()
     if int(lib.gcnk_hubfactor_lds_bytes(F, f.Kc, f.H, f.rec_words, P)) > 160 * 1024:
         return None
-    S = f.hub_times(W1).contiguous()
+    S = f.hub_times(W1).contiguous() if S is None else S
     H1 = torch.empty((M, F), dtype=torch.float32, device=W1.device) if store_h1 else None
     S2 = torch.empty((M, P), dtype=torch.float32, device=W1.device)
     if b1 is not None:

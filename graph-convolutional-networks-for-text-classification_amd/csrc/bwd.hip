@@ -39,6 +39,9 @@ constexpr int kBwdCols = 256;      // columns per workgroup slice
 constexpr int kBwdRowsMax = 256;   // rows per workgroup (LDS staging of gS2 / G)
 constexpr int kBwdBatch = 8;       // rows per lane whose H1 loads are in flight together
 constexpr int kBwdTarget = 256;    // workgroups per slice (one per CU)
+// arrival counters kCntStride words (256 B) apart: agent-scope atomics resolve
+// past the per-XCD L2s, and a few hundred of them on one line serialise
+constexpr int kCntStride = 64;
 
 template <int VEC>
 struct VecIO;
@@ -215,8 +218,8 @@ __global__ void __launch_bounds__(kBwdBlock) gcn_bwd2_kernel(Bwd2Args a) {
   __shared__ int s_flag;
   const int32_t nblk = (int32_t)gridDim.x;
   const int32_t g = (int32_t)blockIdx.x / a.grp, g0 = g * a.grp, gn = min(nblk, g0 + a.grp) - g0;
-  int32_t* cnt1 = a.cnt + (int64_t)blockIdx.y * a.ngroups;
-  int32_t* cnt2 = a.cnt + (int64_t)gridDim.y * a.ngroups + blockIdx.y;
+  int32_t* cnt1 = a.cnt + (int64_t)blockIdx.y * a.ngroups * kCntStride;   // + g * kCntStride
+  int32_t* cnt2 = a.cnt + ((int64_t)gridDim.y * a.ngroups + blockIdx.y) * kCntStride;
   // this slice's entries: gW2 rows of its columns, their gb1, gb2 on slice 0
   const int64_t ncol = min<int64_t>((int64_t)CT * VEC, (int64_t)a.N - (int64_t)cu0 * VEC);
   const int64_t nw = ncol * a.P, ne = nw + ncol + (with_g ? a.P : 0);
@@ -227,10 +230,10 @@ __global__ void __launch_bounds__(kBwdBlock) gcn_bwd2_kernel(Bwd2Args a) {
   };
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // this wave's partial stores have completed
   __syncthreads();
-  if (tid == 0) s_flag = __hip_atomic_fetch_add(cnt1 + g, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == gn - 1;
+  if (tid == 0) s_flag = __hip_atomic_fetch_add(cnt1 + g * kCntStride, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == gn - 1;
   __syncthreads();
   if (!s_flag) return;
-  if (tid == 0) __hip_atomic_store(cnt1 + g, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  if (tid == 0) __hip_atomic_store(cnt1 + g * kCntStride, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
   const bool single = a.ngroups == 1;
   float* grow = a.part2 + (int64_t)g * a.part_ld;
   for (int64_t i = tid; i < ne; i += kBwdBlock) {
@@ -282,9 +285,9 @@ bool bwd2_geometry(int32_t M, int32_t N, int32_t P, bool vec4_ok, bool vec2_ok, 
   return true;
 }
 
-// partials | group partials | counters (slices x (ngroups + 1) int32)
+// partials | group partials | counters (slices x (ngroups + 1), kCntStride words apart)
 int64_t bwd2_ws_bytes(const Bwd2Geom& g) {
-  return ((int64_t)g.nblk + g.ngroups) * g.part_ld * 4 + (int64_t)g.slices * (g.ngroups + 1) * 4;
+  return ((int64_t)g.nblk + g.ngroups) * g.part_ld * 4 + (int64_t)g.slices * (g.ngroups + 1) * kCntStride * 4 + 256;
 }
 
 }  // namespace
@@ -333,7 +336,8 @@ extern "C" int gcnk_gcn_bwd2_f32(const float* H, int64_t ldh, const float* gS, i
   float* part = (float*)workspace;
   float* part2 = part + (int64_t)g.nblk * g.part_ld;
   // counters at the END of the caller's workspace (a fixed place whatever the geometry)
-  int32_t* cnt = reinterpret_cast<int32_t*>((char*)workspace + (workspace_bytes & ~3LL)) - g.slices * (g.ngroups + 1);
+  int32_t* cnt = reinterpret_cast<int32_t*>((char*)workspace + (workspace_bytes & ~255LL)) -
+                 (int64_t)g.slices * (g.ngroups + 1) * kCntStride;
   Bwd2Args a{H, ldh, gS, ldgs, W, ldw, G, ldg, M, N, P, scale, Z, ldz, part, g.part_ld, part2, cnt,
              gW, gb1, G ? gb2 : nullptr, g.rpb, g.grp, g.ngroups};
   hipStream_t s = (hipStream_t)stream;

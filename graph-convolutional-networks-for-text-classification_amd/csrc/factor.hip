@@ -20,9 +20,8 @@
 //
 // One workgroup = 32 rows (512 threads, 8 waves: 2 row strips x 4 quarters of the
 // F columns):
-//   0. every operand of the block in one round of loads: S_T, W2, b1 and the
-//      block's A_H record into LDS, W1[Kc] and the block's U fragments into
-//      MFMA operand registers (75 KB of LDS at R8's shape: two workgroups per CU);
+//   0. every operand of the block in one round of loads: W1[Kc] and S_T into LDS,
+//      the block's U fragments into registers, its A_H record and W2 into LDS;
 //   1. Z_strip = U_strip W1[Kc] on v_mfma_f32_16x16x4_f32 (exact fp32 FMA chains);
 //   2. Z through LDS to row-major; + A_H S_T, + b1, ReLU, dropout (mask or hash,
 //      the row kernel's epilogue); H1 stored only when a backward needs it;
@@ -42,6 +41,9 @@ constexpr int kRB = 32;         // rows per workgroup
 constexpr int kThreads = 512;   // 8 waves: 2 row strips x 4 column quarters
 constexpr int kMaxKsteps = 32;  // Kc <= 128
 constexpr int kProjMax = 32;    // projection width: P <= 32 (NP = 1 or 2 MFMA n-tiles)
+// zero floats after the staged W1[Kc]: the n-tiles past F read up to column
+// 64 NTQ - 1 of the last k-row, so the pad covers 64 NTQ - F of them (at least 64)
+__host__ __device__ constexpr int bpad(int f, int ntq) { return 64 * ntq - f > 64 ? 64 * ntq - f : 64; }
 // block record (factor.py): 33 row offsets, 3 pad | 32 row ids (-1 past M) |
 // A_H items int2 {hub, value}.  Block b holds rows perm[32 b .. 32 b + 31]: the
 // host spreads the hub rows (long item lists) over the blocks, U's rows are in
@@ -51,7 +53,8 @@ constexpr int kRecRow = 36, kRecHead = 68;
 // KS k-steps of U W1[Kc] (Kc <= 4 KS; U columns past Kc read as zero, W1 rows
 // past Kc staged as zero) and NTQ 16-column tiles per quarter of F (F <= 64 NTQ;
 // columns past F are computed from zeroed or W1 LDS words and never used)
-// (18: the 20ng-shaped X's 70 topic-weight columns)
+// (18: the 20ng-shaped X's 70 topic-weight columns, whose W1 rows at 25 k-steps
+// would take the block's LDS past 160 KiB)
 __host__ __device__ constexpr int pick_ks(int kc) { return kc <= 52 ? 13 : kc <= 72 ? 18 : kc <= 100 ? 25 : 32; }
 __host__ __device__ constexpr int pick_ntq(int f) { return f <= 128 ? 2 : f <= 192 ? 3 : 4; }
 
@@ -67,45 +70,49 @@ struct FactorArgs {
   Epi epi;
 };
 
-// s_Z rows: the F columns of a row plus 4 floats (16-B rows)
-__host__ __device__ constexpr int zstride(int F) { return F + 4; }
-// S_T's LDS region is reused by the projection's cross-quarter sums
-__host__ __device__ constexpr int sred_floats(int np) { return np * 3 * 2 * 64 * 4; }
+template <int KS>
+__host__ __device__ constexpr int region1_floats(int F, int ntq) {
+  return (4 * KS * F + bpad(F, ntq)) > kRB * (64 * ntq + 4) ? (4 * KS * F + bpad(F, ntq)) : kRB * (64 * ntq + 4);
+}
 
 template <int KS, int NTQ, int NP>
-__global__ void __launch_bounds__(kThreads, 2)
+__global__ void __launch_bounds__(kThreads)
 hubfactor_gc1_kernel(FactorArgs a) {
   extern __shared__ __attribute__((aligned(16))) float smem[];
   const int tid = threadIdx.x, lane = tid & 63;
   const int wv = __builtin_amdgcn_readfirstlane(tid >> 6);
   const int strip = wv & 1, quarter = wv >> 1;
   const int F = a.F, Q = F / 4;
-  constexpr int Fp = 64 * NTQ;
-  const int Fz = zstride(F);
+  constexpr int Fp = 64 * NTQ, Fz = Fp + 4;  // s_Z row stride: 16-B rows, conflict-free MFMA-layout accesses
+  constexpr int Kr = 4 * KS;
   const int blk = (int)blockIdx.x;
   const int64_t m0 = (int64_t)blk * kRB;  // position in the block order (U's rows)
-  // LDS: s_Z [kRB][F + 4] | s_S [nhub][F] (phase 3: s_red [NP][3][2][64][4])
-  //      | s_W2 [F][P] | s_bias [F] | s_rec.  R8 (F 200, 50 hubs, P 8): 75 KB,
-  // two workgroups per CU, so one block's loads overlap another's MFMA and item
-  // loop.  Every global operand is loaded in the one round of loads that opens
-  // the kernel (LDS-DMA, or W1[Kc] and U straight into MFMA operand registers):
-  // a global load behind an LDS-read index costs a full memory round trip
-  // under load (~1-2 us each, measured), so nothing after the first wait
-  // touches global memory except the stores.
+  // LDS: region1 = s_B [Kr][F] + bpad zeros (phase 1), then s_Z [kRB][Fz]
+  //      | s_S [nhub][F] | s_W2 [F][P] | s_bias [F] | s_rec | s_red [NP][3][2][64][4]
+  // Every global operand is staged here in the one round of loads that opens the
+  // kernel: a global load behind an LDS-read index costs a full memory round trip
+  // under load (~1-2 us each, measured), so nothing after the first wait touches
+  // global memory except the stores.
+  const int r1 = region1_floats<KS>(F, NTQ);
+  float* s_B = smem;
   float* s_Z = smem;
-  float* s_S = smem + kRB * Fz;
-  float* s_red = s_S;
-  const int sr = a.nhub * F > sred_floats(NP) ? a.nhub * F : sred_floats(NP);
-  float* s_W2 = s_S + sr;
+  float* s_S = smem + r1;
+  float* s_W2 = s_S + a.nhub * F;
   float* s_bias = s_W2 + ((F * a.P + 3) & ~3);
   int32_t* s_rec = reinterpret_cast<int32_t*>(s_bias + F);
+  float* s_red = reinterpret_cast<float*>(s_rec + a.rec_words);
 
   // ---- 0. loads, all issued before the first wait: zeros first (no LDS-DMA in
-  //      flight yet), then LDS-DMA of the block's record, S_T, W2 and b1; the
-  //      W1[Kc] and U fragments straight into registers
+  //      flight yet), then LDS-DMA of W1[Kc] (flat) and the block's record, the
+  //      U fragments straight into registers
+  for (int e = a.Kc * F + tid; e < Kr * F + bpad(F, NTQ); e += kThreads) s_B[e] = 0.f;
   if (!a.epi.bias)
     for (int e = tid; e < F; e += kThreads) s_bias[e] = 0.f;
   {
+    const int n4 = a.Kc * Q;  // float4 pieces of W1[k0 .. k0 + Kc) (rows of F floats, ldw == F)
+    const float* wsrc = a.W + (int64_t)a.k0 * a.ldw;
+    for (int e0 = wv * 64; e0 < n4; e0 += kThreads)
+      if (e0 + lane < n4) lds_dma16(wsrc + 4 * (e0 + lane), s_B + 4 * e0);
     const int32_t* rec = a.rec + (int64_t)blk * a.rec_words;
     for (int e0 = wv * 64; e0 < a.rec_words / 4; e0 += kThreads)
       if (e0 + lane < a.rec_words / 4) lds_dma16(rec + 4 * (e0 + lane), s_rec + 4 * e0);
@@ -118,20 +125,6 @@ hubfactor_gc1_kernel(FactorArgs a) {
     if (a.epi.bias)
       for (int e0 = wv * 64; e0 < Q; e0 += kThreads)
         if (e0 + lane < Q) lds_dma16(a.epi.bias + 4 * (e0 + lane), s_bias + 4 * e0);
-  }
-  // W1[k0 + 4 s + (lane >> 4)][c0 + 16 i]: this wave's B fragments (rows past
-  // Kc and columns past F zero)
-  const int c0 = quarter * NTQ * 16 + (lane & 15);
-  float bf[KS][NTQ];
-  {
-    const float* wsrc = a.W + (int64_t)a.k0 * a.ldw + c0;
-#pragma unroll
-    for (int s = 0; s < KS; ++s)
-#pragma unroll
-      for (int i = 0; i < NTQ; ++i) {
-        const int k = 4 * s + (lane >> 4);
-        bf[s][i] = (k < a.Kc && c0 + 16 * i < F) ? wsrc[(int64_t)k * a.ldw + 16 * i] : 0.f;
-      }
   }
   float af[KS];
   {
@@ -148,18 +141,24 @@ hubfactor_gc1_kernel(FactorArgs a) {
   f32x4 acc[NTQ];
 #pragma unroll
   for (int i = 0; i < NTQ; ++i) acc[i] = f32x4{0.f, 0.f, 0.f, 0.f};
+  const int c0 = quarter * NTQ * 16 + (lane & 15);
 #pragma unroll
-  for (int s = 0; s < KS; ++s)
+  for (int s = 0; s < KS; ++s) {
+    const float* br = s_B + (4 * s + (lane >> 4)) * F + c0;
+    float bf[NTQ];
 #pragma unroll
-    for (int i = 0; i < NTQ; ++i) acc[i] = __builtin_amdgcn_mfma_f32_16x16x4f32(af[s], bf[s][i], acc[i], 0, 0, 0);
+    for (int i = 0; i < NTQ; ++i) bf[i] = br[i * 16];
+#pragma unroll
+    for (int i = 0; i < NTQ; ++i) acc[i] = __builtin_amdgcn_mfma_f32_16x16x4f32(af[s], bf[i], acc[i], 0, 0, 0);
+  }
+  __syncthreads();  // s_B is overwritten by s_Z below
   stamp(a.epi, 1);
   // C/D map of the 16x16 f32 MFMA: reg r -> row (lane >> 4) * 4 + r, col lane & 15
-  // (the n-tiles' columns past F are not kept)
 #pragma unroll
   for (int i = 0; i < NTQ; ++i)
 #pragma unroll
     for (int r = 0; r < 4; ++r)
-      if (c0 + 16 * i < F) s_Z[(16 * strip + (lane >> 4) * 4 + r) * Fz + c0 + i * 16] = acc[i][r];
+      s_Z[(16 * strip + (lane >> 4) * 4 + r) * Fz + c0 - (lane & 15) + i * 16 + (lane & 15)] = acc[i][r];
   __syncthreads();
 
   // ---- 2. row-major epilogue, 16 threads per row, NTQ float4 columns each
@@ -172,9 +171,7 @@ hubfactor_gc1_kernel(FactorArgs a) {
     const int64_t row = s_rec[kRecRow + r];  // output row (-1 past M)
     float4 z[NTQ];
 #pragma unroll
-    for (int u = 0; u < NTQ; ++u)
-      z[u] = c16 + 16 * u < Q ? *reinterpret_cast<const float4*>(s_Z + r * Fz + 4 * (c16 + 16 * u))
-                              : make_float4(0.f, 0.f, 0.f, 0.f);
+    for (int u = 0; u < NTQ; ++u) z[u] = *reinterpret_cast<const float4*>(s_Z + r * Fz + 4 * (c16 + 16 * u));
     // one item at a time: batching the items' loads (4 per round, selects past
     // the row) measured slower, 2.28 against 2.12 us per block (LDS throughput,
     // not the item chain, bounds this loop; profiles/r03_factor.md)
@@ -223,10 +220,7 @@ hubfactor_gc1_kernel(FactorArgs a) {
     constexpr int kq = Fp / 16;  // k-steps per quarter
     float av[kq];
 #pragma unroll
-    for (int j = 0; j < kq; ++j) {
-      const int k = 4 * (quarter * kq + j) + (lane >> 4);
-      av[j] = k < F ? s_Z[(16 * strip + (lane & 15)) * Fz + k] : 0.f;
-    }
+    for (int j = 0; j < kq; ++j) av[j] = s_Z[(16 * strip + (lane & 15)) * Fz + 4 * (quarter * kq + j) + (lane >> 4)];
 #pragma unroll
     for (int t = 0; t < NP; ++t) {
       float bw[kq];
@@ -294,9 +288,9 @@ extern "C" int gcnk_debug_poison_lds(uint32_t word, void* stream) {
 static int pick_np(int32_t P) { return P <= 16 ? 1 : 2; }
 
 static int64_t hubfactor_lds_bytes(int32_t F, int32_t Kc, int32_t nhub, int32_t rec_words, int32_t P) {
-  (void)Kc;
-  const int64_t sr = std::max<int64_t>((int64_t)nhub * F, sred_floats(pick_np(P)));
-  return 4 * ((int64_t)kRB * zstride(F) + sr + (((int64_t)F * P + 3) & ~3LL) + F + rec_words);
+  const int64_t Fz = 64 * pick_ntq(F) + 4, Kr = 4 * pick_ks(Kc);
+  const int64_t r1 = std::max<int64_t>(Kr * F + bpad(F, pick_ntq(F)), (int64_t)kRB * Fz);
+  return 4 * (r1 + (int64_t)nhub * F + (((int64_t)F * P + 3) & ~3LL) + F + rec_words + pick_np(P) * 3 * 2 * 64 * 4);
 }
 
 extern "C" int64_t gcnk_hubfactor_lds_bytes(int32_t F, int32_t Kc, int32_t nhub, int32_t rec_words, int32_t P) {

@@ -31,6 +31,9 @@ constexpr int kTileF = kRows * kCols;
 constexpr int kKB = 16;          // k per block (4 MFMA steps)
 constexpr int kWaves = 4;
 constexpr int kNB = 4;          // k-blocks per wave loaded together
+// arrival counters kCntStride words (256 B) apart: agent-scope atomics resolve
+// past the per-XCD L2s, and a few hundred of them on one line serialise
+constexpr int kCntStride = 64;
 
 struct HubXW {
   const float* X;  // [H x >= roundup4(K)] zero past K
@@ -41,7 +44,7 @@ struct HubXW {
   int64_t ldo;
   float* part1;    // [S][T] tiles
   float* part2;    // [NG][T] tiles
-  int32_t* cnt;    // [T][NG] group counters, then [T] final counters
+  int32_t* cnt;    // [T][NG] group counters, then [T] final counters, kCntStride words apart
   int32_t H, K, F, T, S, Ks, G, NG;
 };
 
@@ -138,8 +141,8 @@ __global__ void __launch_bounds__(256) hub_xw_kernel(HubXW a) {
 #pragma unroll
     for (int u = 1; u < kWaves; ++u) add4(v[j], s_red[u][e]);
   }
-  int32_t* cnt1 = a.cnt + t * a.NG;
-  int32_t* cnt2 = a.cnt + a.T * a.NG + t;
+  int32_t* cnt1 = a.cnt + (int64_t)t * a.NG * kCntStride;          // + g * kCntStride
+  int32_t* cnt2 = a.cnt + ((int64_t)a.T * a.NG + t) * kCntStride;
   if (a.S > 1) {
     // level 1: publish this slab's tile; the group's last arriver sums the group's
     float* p1 = a.part1 + (int64_t)t * kTileF;  // slot (s, t) at p1 + s * T * kTileF
@@ -149,10 +152,10 @@ __global__ void __launch_bounds__(256) hub_xw_kernel(HubXW a) {
     const int g = s / a.G, g0 = g * a.G, gn = min(a.S, g0 + a.G) - g0;
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // this wave's partial stores have completed
     __syncthreads();
-    if (tid == 0) s_flag = __hip_atomic_fetch_add(cnt1 + g, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == gn - 1;
+    if (tid == 0) s_flag = __hip_atomic_fetch_add(cnt1 + g * kCntStride, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == gn - 1;
     __syncthreads();
     if (!s_flag) return;
-    if (tid == 0) __hip_atomic_store(cnt1 + g, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    if (tid == 0) __hip_atomic_store(cnt1 + g * kCntStride, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     float4 gs[2] = {make_float4(0.f, 0.f, 0.f, 0.f), make_float4(0.f, 0.f, 0.f, 0.f)};
     for (int u = 0; u < gn; ++u)
 #pragma unroll
@@ -222,7 +225,7 @@ extern "C" int64_t gcnk_hub_xw_workspace_bytes(int32_t H, int32_t K, int32_t F) 
   if (H <= 0 || H > kRows || K <= 0 || F <= 0) return GCNK_EARG;
   const Shape sh = hub_xw_shape(K, F);
   const int64_t tiles = (int64_t)(sh.S + sh.NG) * sh.T * kTileF * 4;
-  return tiles + (int64_t)sh.T * (sh.NG + 1) * 4;
+  return tiles + (int64_t)sh.T * (sh.NG + 1) * kCntStride * 4;
 }
 
 extern "C" int gcnk_hub_xw_f32(int32_t H, int32_t K, int32_t F, const float* X, int64_t ldx, const float* W,

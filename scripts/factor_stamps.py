@@ -19,16 +19,20 @@ def main():
     from graph_convolutional_networks_for_text_classification_amd.sparse import as_csr
     dev = torch.device("cuda", 0)
     lib = _lib.load()
-    r8 = datasets.load_r8_fixture(os.path.join(ROOT, "tests", "golden", "r8_graph.npz"))
+    if os.environ.get("GCNK_STAMP_GRAPH") == "20ng":     # BASELINE config 3's shape: 70 hubs, 20 classes
+        r8 = datasets.doc_topic_graph(18846, 70, 20, seed=0)
+    else:
+        r8 = datasets.load_r8_fixture(os.path.join(ROOT, "tests", "golden", "r8_graph.npz"))
     A, X = r8["adj"].to(dev), r8["features"].to(dev)
     f = factor.get(as_csr(A), ops.Operand(X))
+    print(json.dumps({"M": f.M, "H": f.H, "Kc": f.Kc, "rec_words": f.rec_words, "nblk": f.nblk}), flush=True)
     W1s = [torch.randn(r8["nfeat"], 200, device=dev) * 0.05 for _ in range(8)]
-    W2 = torch.randn(200, 8, device=dev) * 0.1
+    W2 = torch.randn(200, r8["nclass"], device=dev) * 0.1
     b1 = torch.randn(200, device=dev) * 0.1
     for W1 in W1s:
         ops.hubfactor_gc1(f, W1, b1, W2, store_h1=False)
     torch.cuda.synchronize()
-    buf = torch.zeros(4 * 4096, dtype=torch.int64, device=dev)
+    buf = torch.zeros(4 * 8192, dtype=torch.int64, device=dev)
     for rep in range(4):
         S = f.hub_times(W1s[rep + 1])
         torch.cuda.synchronize()

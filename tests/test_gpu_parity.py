@@ -495,7 +495,7 @@ def test_trained_model_labels_bit_exact_on_every_row(r8, trained_golden):
     bound against the reference would demand reproducing its rounding
     sequence; instead the HIP forward must be at least as close to the
     float64 truth as the reference is, and within TRAINED_LOGIT_TOL of the
-    reference's logits in absolute terms (observed on MI355X: 2.7e-4, printed
+    reference's logits in absolute terms (observed on MI355X: 1.83e-4, printed
     below; the reference's own distance to float64 is 1.9e-4)."""
     import scipy.sparse as ssp
     m = GCN(nfeat=r8["nfeat"], nhid=200, nclass=r8["nclass"], dropout=0.5).to(DEV)
@@ -1290,6 +1290,7 @@ def test_device_factor_build_is_bitwise_the_host_build(r8, case):
         A, X = g["adj"], g["features"]
     a = as_csr(A.to(DEV))
     xop = ops.Operand(X.to(DEV))
+    Xd = X.to_dense() if X.is_sparse else X      # (a dense-enough sparse X becomes a dense operand)
     d = factor.build(a, xop)
     torch.cuda.synchronize()
     h = factor_host.build(a, xop)
@@ -1306,13 +1307,13 @@ def test_device_factor_build_is_bitwise_the_host_build(r8, case):
         assert np.array_equal(d.x_hub.colind.cpu().numpy(), h.x_hub_colind)
         assert np.array_equal(d.x_hub.val.cpu().numpy().view(np.int32), h.x_hub_val.view(np.int32))
     else:
-        assert torch.equal(d.x_hub_dense.cpu(), X[torch.from_numpy(h.hubs)])
+        assert torch.equal(d.x_hub_dense.cpu(), Xd[torch.from_numpy(h.hubs)])
     if d.x_hub_pad is not None:      # the hub_xw operand: X's hub rows, zero past K
         xp = d.x_hub_pad.cpu()
         assert xp.shape[1] % 4 == 0 and not bool(xp[:, d.K:].any())
         ref = torch.from_numpy(h.x_hub_rowptr) if xop.csr is not None else None
         want = (torch.sparse_csr_tensor(ref, torch.from_numpy(h.x_hub_colind).long(), torch.from_numpy(h.x_hub_val),
-                                        (d.H, d.K)).to_dense() if ref is not None else X[torch.from_numpy(h.hubs)])
+                                        (d.H, d.K)).to_dense() if ref is not None else Xd[torch.from_numpy(h.hubs)])
         assert torch.equal(xp[:, :d.K], want)
 
 
@@ -1342,5 +1343,5 @@ def test_hub_xw_against_float64(H, K, F):
     _close(a, ref, atol=2e-6 * np.sqrt(K) * max(1.0, np.abs(ref).max()))
     assert torch.equal(a, b)
     T = (F + 31) // 32
-    cw = (nb % (T * 64 * 32 * 4)) // 4     # the trailing T * (NG + 1) counter words (after whole 64 x 32 tiles)
-    assert cw > 0 and not bool(ws.view(torch.int32)[-cw:].any())   # every counter re-armed
+    # the last T x 64 words hold the T final counters (64 words apart) and never-written pad
+    assert not bool(ws.view(torch.int32)[-(T * 64):].any())   # every final counter re-armed

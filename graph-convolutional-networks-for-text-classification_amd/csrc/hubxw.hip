@@ -111,9 +111,11 @@ __global__ void __launch_bounds__(256) hub_xw_kernel(HubXW a) {
         wb[nb][j][1] = (k < k_end && colok1) ? wr[16] : 0.f;
       }
     }
-    // (X values past k_end -- only at K, inside the zero pad -- meet W zeros)
+    // (X values past k_end -- only at K, inside the zero pad -- meet W zeros;
+    // blocks wholly past k_end skip their MFMAs, a wave-uniform test)
 #pragma unroll
-    for (int nb = 0; nb < kNB; ++nb)
+    for (int nb = 0; nb < kNB; ++nb) {
+      if (kb0 + kKB * kWaves * nb >= k_end) break;
 #pragma unroll
       for (int j = 0; j < 4; ++j)
 #pragma unroll
@@ -122,6 +124,7 @@ __global__ void __launch_bounds__(256) hub_xw_kernel(HubXW a) {
           acc[r][0] = __builtin_amdgcn_mfma_f32_16x16x4f32(av, wb[nb][j][0], acc[r][0], 0, 0, 0);
           acc[r][1] = __builtin_amdgcn_mfma_f32_16x16x4f32(av, wb[nb][j][1], acc[r][1], 0, 0, 0);
         }
+    }
   }
   // C map of the 16x16 f32 MFMA: reg q -> row 4 * (lane >> 4) + q, col lane & 15.
   // Into LDS as the 64 x 32 row-major tile of this wave.

@@ -77,6 +77,11 @@ constexpr int kMaxSeg = 64;             // segments per heavy row (bounds the la
 #ifndef GCNK_ROW_SC1
 #define GCNK_ROW_SC1 0
 #endif
+// Nontemporal (streaming) output stores of the row kernel's finished rows
+// (scripts/micro/ns_micro.hip: a cold 12.4 MB copy 4.35 -> 3.25 us with them)
+#ifndef GCNK_ROW_NT
+#define GCNK_ROW_NT 0
+#endif
 #ifndef GCNK_LIGHT_RPW
 #define GCNK_LIGHT_RPW 2
 #endif
@@ -507,6 +512,12 @@ __device__ __forceinline__ void wave_group_sum(T& acc) {
   }
 }
 
+__device__ __forceinline__ void store_nt(float* p, const float4& v) {
+  typedef float f4a __attribute__((ext_vector_type(4), aligned(16)));
+  __builtin_nontemporal_store(f4a{v.x, v.y, v.z, v.w}, reinterpret_cast<f4a*>(p));
+}
+__device__ __forceinline__ void store_nt(float* p, const float& v) { __builtin_nontemporal_store(v, p); }
+
 // Epilogue + store (+ fused projection) of one finished row by lane group
 // q == 0 of the calling lanes.
 template <int LPR, int VEC, int NP>
@@ -523,6 +534,8 @@ __device__ __forceinline__ void finish_row(const typename Vec<VEC>::T& acc, int3
     if (off < ((int64_t)1 << 29)) store_coherent_v(C, off, h);  // C: the kernel argument (uniform)
     else V::store(C + off, h);
   }
+#elif GCNK_ROW_NT
+  if (colok && store_main) store_nt(C + (int64_t)r * ldc + colv, h);
 #else
   if (colok && store_main) V::store(C + (int64_t)r * ldc + colv, h);
 #endif

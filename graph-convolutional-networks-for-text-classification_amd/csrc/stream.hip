@@ -1,9 +1,10 @@
 // Streaming floor for measurements (bench.py "roofline_rocprof.copy"): dst = src
-// for n floats, float4 grid-stride, 1024 x 256 threads.  It moves exactly the
-// north-star SpMM's dense bytes (read B once, write C once) with no CSR and no
-// gathers, so its cold duration is the ceiling any single launch over those
-// bytes can reach (MI355X: 4.2-4.4 us for R8's 2 x 6.18 MB, 37-39 % of 8 TB/s,
-// scripts/micro/ns_micro.hip).  Not on the GCN path.
+// for n floats, float4 grid-stride, 1024 x 256 threads, nontemporal stores.  It
+// moves exactly the north-star SpMM's dense bytes (read B once, write C once)
+// with no CSR and no gathers, so its cold duration is the ceiling any single
+// launch over those bytes can reach (MI355X, R8's 2 x 6.18 MB, cold,
+// scripts/micro/ns_micro.hip: 4.35 us with plain stores, 3.25 us with
+// nontemporal ones = 50 % of 8 TB/s).  Not on the GCN path.
 #include "gcnk_common.h"
 
 namespace gcnk {
@@ -11,7 +12,11 @@ namespace {
 
 __global__ void __launch_bounds__(256) stream_copy_kernel(const float4* __restrict__ src, float4* __restrict__ dst,
                                                           int64_t n4) {
-  for (int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x; i < n4; i += (int64_t)gridDim.x * 256) dst[i] = src[i];
+  typedef float f4a __attribute__((ext_vector_type(4), aligned(16)));
+  for (int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x; i < n4; i += (int64_t)gridDim.x * 256) {
+    const float4 v = src[i];
+    __builtin_nontemporal_store(f4a{v.x, v.y, v.z, v.w}, reinterpret_cast<f4a*>(dst + i));
+  }
 }
 
 __global__ void __launch_bounds__(256) stream_copy_tail_kernel(const float* __restrict__ src, float* __restrict__ dst,

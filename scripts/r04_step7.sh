@@ -12,3 +12,7 @@ timeout -k 10 300 python -u -m pytest tests/test_gpu_parity.py -m gpu -p no:cach
 tail -3 gpurun_out/r04/pytest_c.log
 timeout -k 10 300 python -u scripts/eager_fwd_profile.py > gpurun_out/r04/eager2.log 2>&1; echo "eager rc=$?"
 grep -E "eager" gpurun_out/r04/eager2.log
+timeout -k 10 300 python -u scripts/hub_probe.py --variants row,copy --widths 200 --reps 200 > gpurun_out/r04/probe_prod.log 2>&1; echo "prod rc=$?"
+grep "^{" gpurun_out/r04/probe_prod.log | cut -c1-250
+GCNK_LIB=$PWD/_variants/libgcnk_rownt.so timeout -k 10 300 python -u scripts/hub_probe.py --variants row,light,topic --widths 200 --reps 200 > gpurun_out/r04/probe_nt.log 2>&1; echo "nt rc=$?"
+grep "^{" gpurun_out/r04/probe_nt.log | cut -c1-250

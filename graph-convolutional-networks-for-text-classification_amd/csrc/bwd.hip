@@ -14,19 +14,15 @@
 // two-pass column sums (profiles/r03_train_breakdown.json: 48 us of 85 us of
 // the step's gcnk kernels).
 //
-// One launch (gcn_bwd2_kernel): one workgroup per run of rows x a 256-column
+// Kernel 1 (gcn_bwd2_kernel): one workgroup per run of rows x a 256-column
 // slice.  Lane (rl, cu): column unit cu (VEC columns), rows rl, rl + RL, ...
 // The lane's first batch of H1 rows is loaded before the rows' gS2 (and G)
-// values are staged in LDS, so the two loads share one latency; each lane
-// keeps its columns' W2 rows in registers, writes gZ1 and accumulates its
-// columns' gW2 / gb1 terms in row order; the RL row lanes are then summed
-// through LDS in lane order and the workgroup's partial is published.  The
-// partials are summed in the same launch by two levels of last-arriver
-// hand-offs (groups of ~sqrt(workgroups) in workgroup order, then the groups
-// in order; the hand-off form of csrc/spmm.hip's heavy rows: coherent stores
-// and loads, each storing wave drained before one lane's agent-scope add).
-// Round 3 ran a second reduce launch (4.9 us in the R8 training step).  Fixed
-// order everywhere: bitwise reproducible.
+// values are staged in LDS once (the two loads share one latency); each lane keeps its
+// columns' W2 rows in registers, writes gZ1 and accumulates its columns' gW2 /
+// gb1 terms in row order; the RL row lanes are then summed through LDS in
+// lane order and the workgroup's partial goes to the workspace.
+// Kernel 2 (gcn_bwd2_reduce_kernel): every output sums the workgroups'
+// partials in workgroup order.  Fixed order everywhere: bitwise reproducible.
 #include "gcnk_common.h"
 
 #include <algorithm>
@@ -39,9 +35,6 @@ constexpr int kBwdCols = 256;      // columns per workgroup slice
 constexpr int kBwdRowsMax = 256;   // rows per workgroup (LDS staging of gS2 / G)
 constexpr int kBwdBatch = 8;       // rows per lane whose H1 loads are in flight together
 constexpr int kBwdTarget = 256;    // workgroups per slice (one per CU)
-// arrival counters kCntStride words (256 B) apart: agent-scope atomics resolve
-// past the per-XCD L2s, and a few hundred of them on one line serialise
-constexpr int kCntStride = 64;
 
 template <int VEC>
 struct VecIO;
@@ -80,19 +73,8 @@ struct Bwd2Args {
   float scale;
   float* Z; int64_t ldz;
   float* part; int64_t part_ld;   // per workgroup row: gW2 [N*P] | gb1 [N] | gb2 [P]
-  float* part2;                   // per group row, the same layout
-  int32_t* cnt;                   // [slices][ngroups] group counters, then [slices] final counters
-  float* gW; float* gb1; float* gb2;
   int32_t rpb;                    // rows per workgroup
-  int32_t grp, ngroups;           // workgroups per group, groups
 };
-
-__device__ __forceinline__ void st_coh(float* p, float v) {
-  __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-}
-__device__ __forceinline__ float ld_coh(const float* p) {
-  return __hip_atomic_load(const_cast<float*>(p), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-}
 
 template <int VEC, int PM>
 __global__ void __launch_bounds__(kBwdBlock) gcn_bwd2_kernel(Bwd2Args a) {
@@ -203,70 +185,57 @@ __global__ void __launch_bounds__(kBwdBlock) gcn_bwd2_kernel(Bwd2Args a) {
     for (int l = 0; l < RL; ++l) s += s_red[(l * CT + u) * KE + k];
     if (col >= a.N) continue;
     if (p < PM) {
-      if (p < a.P) st_coh(prow + col * a.P + p, s);
+      if (p < a.P) prow[col * a.P + p] = s;
     } else {
-      st_coh(prow + (int64_t)a.N * a.P + col, s);
+      prow[(int64_t)a.N * a.P + col] = s;
     }
   }
   if (with_g && tid < a.P) {  // gb2: the G rows, in row order
     float s = 0.f;
     for (int rr = 0; rr < nr; ++rr) s += s_gg[rr * PM + tid];
-    st_coh(prow + (int64_t)a.N * a.P + a.N + tid, s);
+    prow[(int64_t)a.N * a.P + a.N + tid] = s;
   }
+}
 
-  // ---- the slice's partials summed in workgroup order, in two levels
-  __shared__ int s_flag;
-  const int32_t nblk = (int32_t)gridDim.x;
-  const int32_t g = (int32_t)blockIdx.x / a.grp, g0 = g * a.grp, gn = min(nblk, g0 + a.grp) - g0;
-  int32_t* cnt1 = a.cnt + (int64_t)blockIdx.y * a.ngroups * kCntStride;   // + g * kCntStride
-  int32_t* cnt2 = a.cnt + ((int64_t)gridDim.y * a.ngroups + blockIdx.y) * kCntStride;
-  // this slice's entries: gW2 rows of its columns, their gb1, gb2 on slice 0
-  const int64_t ncol = min<int64_t>((int64_t)CT * VEC, (int64_t)a.N - (int64_t)cu0 * VEC);
-  const int64_t nw = ncol * a.P, ne = nw + ncol + (with_g ? a.P : 0);
-  auto entry = [&](int64_t i) -> int64_t {  // slice entry i -> offset in a partial row
-    if (i < nw) return (int64_t)cu0 * VEC * a.P + i;
-    if (i < nw + ncol) return (int64_t)a.N * a.P + (int64_t)cu0 * VEC + (i - nw);
-    return (int64_t)a.N * a.P + a.N + (i - nw - ncol);
-  };
-  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // this wave's partial stores have completed
-  __syncthreads();
-  if (tid == 0) s_flag = __hip_atomic_fetch_add(cnt1 + g * kCntStride, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == gn - 1;
-  __syncthreads();
-  if (!s_flag) return;
-  if (tid == 0) __hip_atomic_store(cnt1 + g * kCntStride, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-  const bool single = a.ngroups == 1;
-  float* grow = a.part2 + (int64_t)g * a.part_ld;
-  for (int64_t i = tid; i < ne; i += kBwdBlock) {
-    const int64_t o = entry(i);
-    float s = 0.f;
-    for (int32_t b = g0; b < g0 + gn; ++b) s += ld_coh(a.part + (int64_t)b * a.part_ld + o);
-    if (single) {
-      if (i < nw) { if (a.gW) a.gW[o] = s; }
-      else if (i < nw + ncol) { if (a.gb1) a.gb1[o - (int64_t)a.N * a.P] = s; }
-      else if (a.gb2) a.gb2[o - (int64_t)a.N * a.P - a.N] = s;
-    } else {
-      st_coh(grow + o, s);
+// out[e] = sum over workgroups of part[b][e], b in order: 16 entries x 16
+// workgroup lanes per block, each lane summing workgroups l, l + 16, ... (16
+// loads in flight), then the 16 lanes in order through LDS.
+__global__ void __launch_bounds__(256) gcn_bwd2_reduce_kernel(const float* __restrict__ part, int64_t part_ld,
+                                                              int32_t nblk, int32_t N, int32_t P, int32_t with_g,
+                                                              float* __restrict__ gW, float* __restrict__ gb1,
+                                                              float* __restrict__ gb2) {
+  __shared__ float s[16][17];
+  const int el = threadIdx.x & 15, bl = threadIdx.x >> 4;
+  const int64_t E = (int64_t)N * P + N + (with_g ? P : 0);
+  const int64_t e = (int64_t)blockIdx.x * 16 + el;
+  float acc = 0.f;
+  if (e < E) {
+    for (int32_t b0 = bl; b0 < nblk; b0 += 16 * 16) {
+      float v[16];
+#pragma unroll
+      for (int j = 0; j < 16; ++j) v[j] = b0 + 16 * j < nblk ? part[(int64_t)(b0 + 16 * j) * part_ld + e] : 0.f;
+#pragma unroll
+      for (int j = 0; j < 16; ++j)
+        if (b0 + 16 * j < nblk) acc += v[j];
     }
   }
-  if (single) return;
-  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  s[bl][el] = acc;
   __syncthreads();
-  if (tid == 0) s_flag = __hip_atomic_fetch_add(cnt2, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == a.ngroups - 1;
-  __syncthreads();
-  if (!s_flag) return;
-  if (tid == 0) __hip_atomic_store(cnt2, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-  for (int64_t i = tid; i < ne; i += kBwdBlock) {
-    const int64_t o = entry(i);
-    float s = 0.f;
-    for (int32_t q = 0; q < a.ngroups; ++q) s += ld_coh(a.part2 + (int64_t)q * a.part_ld + o);
-    if (i < nw) { if (a.gW) a.gW[o] = s; }
-    else if (i < nw + ncol) { if (a.gb1) a.gb1[o - (int64_t)a.N * a.P] = s; }
-    else if (a.gb2) a.gb2[o - (int64_t)a.N * a.P - a.N] = s;
+  if (bl != 0 || e >= E) return;
+  float t = s[0][el];
+  for (int q = 1; q < 16; ++q) t += s[q][el];
+  const int64_t NP = (int64_t)N * P;
+  if (e < NP) {
+    if (gW) gW[e] = t;
+  } else if (e < NP + N) {
+    if (gb1) gb1[e - NP] = t;
+  } else if (gb2) {
+    gb2[e - NP - N] = t;
   }
 }
 
 struct Bwd2Geom {
-  int vec, pm, slices, nblk, rpb, grp, ngroups;
+  int vec, pm, slices, nblk, rpb;
   int64_t part_ld;
 };
 
@@ -279,15 +248,7 @@ bool bwd2_geometry(int32_t M, int32_t N, int32_t P, bool vec4_ok, bool vec2_ok, 
   g.rpb = (int)std::min<int64_t>(kBwdRowsMax, std::max<int64_t>(1, ((int64_t)M + kBwdTarget - 1) / kBwdTarget));
   g.nblk = (int)(((int64_t)M + g.rpb - 1) / g.rpb);
   g.part_ld = (((int64_t)N * P + N + P) + 3) & ~3LL;
-  g.grp = 1;
-  while ((int64_t)g.grp * g.grp < g.nblk) ++g.grp;
-  g.ngroups = (g.nblk + g.grp - 1) / g.grp;
   return true;
-}
-
-// partials | group partials | counters (slices x (ngroups + 1), kCntStride words apart)
-int64_t bwd2_ws_bytes(const Bwd2Geom& g) {
-  return ((int64_t)g.nblk + g.ngroups) * g.part_ld * 4 + (int64_t)g.slices * (g.ngroups + 1) * kCntStride * 4 + 256;
 }
 
 }  // namespace
@@ -298,10 +259,7 @@ using namespace gcnk;
 extern "C" int64_t gcnk_gcn_bwd2_workspace_bytes(int32_t M, int32_t N, int32_t P) {
   Bwd2Geom g;
   if (!bwd2_geometry(M, N, P, true, true, g)) return 0;
-  // the most slices any alignment can pick (VEC = 1): counters for all of them
-  Bwd2Geom g1;
-  bwd2_geometry(M, N, P, false, false, g1);
-  return std::max(bwd2_ws_bytes(g), bwd2_ws_bytes(g1));
+  return (int64_t)g.nblk * g.part_ld * 4;
 }
 
 extern "C" int gcnk_gcn_bwd2_f32(const float* H, int64_t ldh, const float* gS, int64_t ldgs, const float* W,
@@ -328,18 +286,12 @@ extern "C" int gcnk_gcn_bwd2_f32(const float* H, int64_t ldh, const float* gS, i
   const bool v2 = N % 2 == 0 && ldh % 2 == 0 && ldz % 2 == 0 && ((uintptr_t)H & 7u) == 0 && ((uintptr_t)Z & 7u) == 0;
   Bwd2Geom g;
   bwd2_geometry(M, N, P, v4, v2, g);
-  const int64_t need = bwd2_ws_bytes(g);
+  const int64_t need = (int64_t)g.nblk * g.part_ld * 4;
   if (!workspace || workspace_bytes < need) {
     set_error("gcnk_gcn_bwd2_f32: workspace %lld B < %lld B", (long long)workspace_bytes, (long long)need);
     return GCNK_EARG;
   }
-  float* part = (float*)workspace;
-  float* part2 = part + (int64_t)g.nblk * g.part_ld;
-  // counters at the END of the caller's workspace (a fixed place whatever the geometry)
-  int32_t* cnt = reinterpret_cast<int32_t*>((char*)workspace + (workspace_bytes & ~255LL)) -
-                 (int64_t)g.slices * (g.ngroups + 1) * kCntStride;
-  Bwd2Args a{H, ldh, gS, ldgs, W, ldw, G, ldg, M, N, P, scale, Z, ldz, part, g.part_ld, part2, cnt,
-             gW, gb1, G ? gb2 : nullptr, g.rpb, g.grp, g.ngroups};
+  Bwd2Args a{H, ldh, gS, ldgs, W, ldw, G, ldg, M, N, P, scale, Z, ldz, (float*)workspace, g.part_ld, g.rpb};
   hipStream_t s = (hipStream_t)stream;
   const dim3 grid((unsigned)g.nblk, (unsigned)g.slices);
 #define GCNK_BWD2(V_, PM_) hipLaunchKernelGGL((gcn_bwd2_kernel<V_, PM_>), grid, dim3(kBwdBlock), 0, s, a)
@@ -356,5 +308,10 @@ extern "C" int gcnk_gcn_bwd2_f32(const float* H, int64_t ldh, const float* gS, i
     else GCNK_BWD2(1, 32);
   }
 #undef GCNK_BWD2
-  return launch_check("gcn_bwd2_kernel");
+  int rc = launch_check("gcn_bwd2_kernel");
+  if (rc) return rc;
+  const int64_t E = (int64_t)N * P + N + (G ? P : 0);
+  hipLaunchKernelGGL(gcn_bwd2_reduce_kernel, dim3((unsigned)((E + 15) / 16)), dim3(256), 0, s,
+                     (const float*)workspace, g.part_ld, g.nblk, N, P, G ? 1 : 0, gW, gb1, gb2);
+  return launch_check("gcn_bwd2_reduce_kernel");
 }

@@ -20,6 +20,8 @@
 //    last adder reading only after its add returned.
 #include "gcnk_common.h"
 
+#include <algorithm>
+
 namespace gcnk {
 namespace {
 
@@ -34,6 +36,7 @@ constexpr int kNB = 4;          // k-blocks per wave loaded together
 // arrival counters kCntStride words (256 B) apart: agent-scope atomics resolve
 // past the per-XCD L2s, and a few hundred of them on one line serialise
 constexpr int kCntStride = 64;
+constexpr int kMaxG = 8;        // partials per hand-off level (loaded together): S <= 64
 
 struct HubXW {
   const float* X;  // [H x >= roundup4(K)] zero past K
@@ -159,10 +162,21 @@ __global__ void __launch_bounds__(256) hub_xw_kernel(HubXW a) {
     __syncthreads();
     if (!s_flag) return;
     if (tid == 0) __hip_atomic_store(cnt1 + g * kCntStride, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    // every partial of the group loaded before the first add (one latency), then summed in order
     float4 gs[2] = {make_float4(0.f, 0.f, 0.f, 0.f), make_float4(0.f, 0.f, 0.f, 0.f)};
-    for (int u = 0; u < gn; ++u)
+    {
+      float4 pv[kMaxG][2];
 #pragma unroll
-      for (int j = 0; j < 2; ++j) add4(gs[j], ld_sc1(uni(p1 + (g0 + u) * slot_ld), 4 * (tid + 256 * j)));
+      for (int u = 0; u < kMaxG; ++u)
+#pragma unroll
+        for (int j = 0; j < 2; ++j)
+          pv[u][j] = u < gn ? ld_sc1(uni(p1 + (g0 + u) * slot_ld), 4 * (tid + 256 * j)) : make_float4(0.f, 0.f, 0.f, 0.f);
+#pragma unroll
+      for (int u = 0; u < kMaxG; ++u)
+#pragma unroll
+        for (int j = 0; j < 2; ++j)
+          if (u < gn) add4(gs[j], pv[u][j]);
+    }
     if (a.NG > 1) {
       // level 2: publish the group sum; the last group sums the groups in order
       float* p2 = a.part2 + (int64_t)t * kTileF;
@@ -176,9 +190,17 @@ __global__ void __launch_bounds__(256) hub_xw_kernel(HubXW a) {
       if (tid == 0) __hip_atomic_store(cnt2, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 #pragma unroll
       for (int j = 0; j < 2; ++j) gs[j] = make_float4(0.f, 0.f, 0.f, 0.f);
-      for (int u = 0; u < a.NG; ++u)
+      float4 pv[kMaxG][2];
 #pragma unroll
-        for (int j = 0; j < 2; ++j) add4(gs[j], ld_sc1(uni(p2 + u * slot_ld), 4 * (tid + 256 * j)));
+      for (int u = 0; u < kMaxG; ++u)
+#pragma unroll
+        for (int j = 0; j < 2; ++j)
+          pv[u][j] = u < a.NG ? ld_sc1(uni(p2 + u * slot_ld), 4 * (tid + 256 * j)) : make_float4(0.f, 0.f, 0.f, 0.f);
+#pragma unroll
+      for (int u = 0; u < kMaxG; ++u)
+#pragma unroll
+        for (int j = 0; j < 2; ++j)
+          if (u < a.NG) add4(gs[j], pv[u][j]);
     }
     v[0] = gs[0];
     v[1] = gs[1];
@@ -203,17 +225,17 @@ struct Shape {
 Shape hub_xw_shape(int32_t K, int32_t F) {
   Shape sh;
   sh.T = (F + kCols - 1) / kCols;
-  // about 256 workgroups (one per CU), S a multiple of 8 (whole XCD rounds);
-  // more slabs where a slab would need two load rounds per wave
+  // about 256 workgroups (one per CU), S a multiple of 8 (whole XCD rounds),
+  // at most kMaxG^2 slabs (two hand-off levels of at most kMaxG partials)
   int S = (256 + sh.T - 1) / sh.T;
-  S = (S + 7) / 8 * 8;
-  while ((K + S - 1) / S > kKB * kWaves * kNB && S < 1024) S += 8;
+  S = std::min((S + 7) / 8 * 8, kMaxG * kMaxG);
   int Ks = ((K + S - 1) / S + kKB - 1) / kKB * kKB;
   if (Ks < kKB * kWaves) Ks = kKB * kWaves;
   sh.Ks = Ks;
   sh.S = (K + Ks - 1) / Ks;
   int G = 1;
   while (G * G < sh.S) ++G;
+  if (G > kMaxG) G = kMaxG;
   sh.G = G;
   sh.NG = (sh.S + G - 1) / G;
   return sh;

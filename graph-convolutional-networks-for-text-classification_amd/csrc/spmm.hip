@@ -77,10 +77,14 @@ constexpr int kMaxSeg = 64;             // segments per heavy row (bounds the la
 #ifndef GCNK_ROW_SC1
 #define GCNK_ROW_SC1 0
 #endif
-// Nontemporal (streaming) output stores of the row kernel's finished rows
-// (scripts/micro/ns_micro.hip: a cold 12.4 MB copy 4.35 -> 3.25 us with them)
+// Nontemporal (streaming) output stores of the row kernel's finished rows: the
+// launch leaves no dirty output lines in the XCD L2s for the end-of-kernel
+// write-back.  R8 A-hat S1, F = 200, cold (HIP events per call,
+// gpurun_out/r04/probe_nt.log): 9.46 -> 8.16 us, document rows alone 8.16 ->
+// 6.95, topic rows alone 9.05 -> 7.78 (a cold 12.4 MB copy: 4.35 -> 3.25 us,
+// scripts/micro/ns_micro.hip).
 #ifndef GCNK_ROW_NT
-#define GCNK_ROW_NT 0
+#define GCNK_ROW_NT 1
 #endif
 #ifndef GCNK_LIGHT_RPW
 #define GCNK_LIGHT_RPW 2

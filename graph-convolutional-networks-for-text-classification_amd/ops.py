@@ -313,9 +313,9 @@ _BWD2_WS = {}
 
 
 def _bwd2_workspace(M, N, P, dev):
-    """gcnk_gcn_bwd2_f32's workspace for torch's current stream: zeroed once
-    (its trailing counter words must be zero on entry; every launch leaves
-    them zero), then reused by every call of that shape on that stream."""
+    """gcnk_gcn_bwd2_f32's workspace for torch's current stream, allocated once
+    and reused by every call of that shape on that stream (no allocation on
+    the eager backward's path)."""
     key = (M, N, P, dev.index, torch.cuda.current_stream(dev).cuda_stream)
     hit = _BWD2_WS.get(key)
     if hit is None:

@@ -219,8 +219,8 @@ class BackwardRecord:
         keep += [gS2, gZ1, gS1]
         s.gS2, s.gZ1, s.gS1 = gS2.data_ptr(), gZ1.data_ptr(), gS1.data_ptr()
         wsb = int(lib.gcnk_gcn_bwd2_workspace_bytes(M, F, P))
-        if wsb > 0:   # zeroed once: its trailing counter words must be zero on entry
-            w = torch.zeros((wsb + 3) // 4, dtype=torch.float32, device=device)
+        if wsb > 0:
+            w = torch.empty((wsb + 3) // 4, dtype=torch.float32, device=device)
             keep.append(w)
             s.bwd2_ws, s.bwd2_ws_bytes = w.data_ptr(), wsb
         self.s, self.keep, self.M, self.F, self.P, self.x_cols = s, keep, M, F, P, cols

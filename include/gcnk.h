@@ -233,10 +233,7 @@ int gcnk_colsum_f32(const float* X, int64_t ldx, int32_t M, int32_t N, float* ou
  * H = gc1's output after ReLU + dropout [M x N], gS = A^T G [M x P], W = W2
  * [N x P].  gW / gb1 / gb2 are nullable (not stored).  P <= 32 (else
  * GCNK_EUNSUP).  Two launches; sums in a fixed order (bitwise reproducible).
- * Workspace: gcnk_gcn_bwd2_workspace_bytes(M, N, P); the partials are summed
- * in the same launch by last-arriver hand-offs whose counter words sit at the
- * END of the workspace: zero them (e.g. the whole workspace) before its first
- * use; every launch leaves them zero (ABI 9; one workspace per stream).
+ * Workspace: gcnk_gcn_bwd2_workspace_bytes(M, N, P).
  * ------------------------------------------------------------------------- */
 int64_t gcnk_gcn_bwd2_workspace_bytes(int32_t M, int32_t N, int32_t P);
 int gcnk_gcn_bwd2_f32(const float* H, int64_t ldh, const float* gS, int64_t ldgs, const float* W, int64_t ldw,

@@ -3,7 +3,7 @@
 cd "${GRAFT_REPO_ROOT:-/root/repo}" || exit 2
 export TMPDIR=/tmp
 mkdir -p gpurun_out/r04
-timeout -k 10 200 python -u scripts/factor_probe.py --graphs r8 > gpurun_out/r04/factor_probe3.log 2>&1; echo "probe rc=$?"
+timeout -k 10 200 python -u scripts/factor_probe.py > gpurun_out/r04/factor_probe3.log 2>&1; echo "probe rc=$?"
 grep "^{" gpurun_out/r04/factor_probe3.log
 GCNK_FACTOR_XHUB=spmm timeout -k 10 200 python -u scripts/factor_probe.py --graphs r8 > gpurun_out/r04/factor_probe3s.log 2>&1; echo "probe spmm rc=$?"
 grep "forward" gpurun_out/r04/factor_probe3s.log

@@ -1084,8 +1084,8 @@ def test_factored_gc1_matches_spmm_path(r8, mode):
                                    err_msg=k)
 
 
-@pytest.mark.parametrize("F,P", [(52, 3), (200, 20), (36, 32)])
-def test_factored_gc1_kernel_against_float64(F, P):
+@pytest.mark.parametrize("F,P,ndoc", [(52, 3, 2000), (200, 20, 2000), (36, 32, 2000), (200, 20, 12000)])
+def test_factored_gc1_kernel_against_float64(F, P, ndoc):
     """gcnk_hubfactor_gc1_f32 alone on a synthetic doc-topic graph with hub x
     hub nonzeros, F not a multiple of 16 (and F < 64, where the n-tiles past F
     read the zero pad after W1[Kc]), P of one and two MFMA n-tiles, H1 stored:
@@ -1098,11 +1098,12 @@ def test_factored_gc1_kernel_against_float64(F, P):
     import scipy.sparse as ssp
     from graph_convolutional_networks_for_text_classification_amd import factor, ops
     from graph_convolutional_networks_for_text_classification_amd.sparse import as_csr
-    g = datasets.doc_topic_graph(2000, 40, 5, seed=4, tt_prob=0.3)
+    g = datasets.doc_topic_graph(ndoc, 40, 5, seed=4, tt_prob=0.3)
     A, X = g["adj"].to(DEV), g["features"].to(DEV)
     xop = ops.Operand(X)
     f = factor.get(as_csr(A), xop)
     assert f is not None
+    # 12,000 documents: more 32-row blocks (376) than CUs -- the persistent kernel
     assert not np.array_equal(f.perm.numpy(), np.arange(f.M))   # the hub rows moved
     rng = np.random.default_rng(3)
     W1 = torch.from_numpy(rng.standard_normal((g["nfeat"], F)).astype(np.float32)).to(DEV)

@@ -335,6 +335,7 @@ hubfactor_gc1_persist_kernel(FactorArgs a) {
     }
     __builtin_amdgcn_s_waitcnt(0x0F70);  // vmcnt(0): this wave's DMA and fragment loads have landed
     __syncthreads();
+    stamp(a.epi, 0);   // (stamps build: the workgroup's last block)
 
     // ---- 1. Z = U W1[Kc] for this wave's strip and column quarter
     f32x4 acc[NTQ];
@@ -350,6 +351,7 @@ hubfactor_gc1_persist_kernel(FactorArgs a) {
       for (int r = 0; r < 4; ++r)
         if (c0 + 16 * i < F) s_Z[(16 * strip + (lane >> 4) * 4 + r) * Fz + c0 + i * 16] = acc[i][r];
     __syncthreads();
+    stamp(a.epi, 1);
 
     // ---- 2. + A_H S_T, + b1, ReLU, dropout (as the kernel above)
     {
@@ -395,6 +397,7 @@ hubfactor_gc1_persist_kernel(FactorArgs a) {
       }
     }
     __syncthreads();
+    stamp(a.epi, 2);
 
     // ---- 3. S2 = H1 W2 (as the kernel above)
     f32x4 pc[NP];
@@ -444,6 +447,7 @@ hubfactor_gc1_persist_kernel(FactorArgs a) {
       }
     }
     __syncthreads();  // s_rec / s_Z / s_red are rewritten by the next block
+    stamp(a.epi, 3);
   }
 }
 

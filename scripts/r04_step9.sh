@@ -11,3 +11,5 @@ import sys, json
 for l in sys.stdin:
     d = json.loads(l); print('$v', d['variant'], d['ipc'], d['cold_us'], d['max_err'] < 1e-5, d['deterministic'])"
 done
+GCNK_STAMP_GRAPH=20ng GCNK_LIB=$PWD/_variants/libgcnk_stamps.so timeout -k 10 120 python -u scripts/factor_stamps.py > gpurun_out/r04/factorstamps20p.log 2>&1; echo "factorstamps20 rc=$?"
+grep "^{" gpurun_out/r04/factorstamps20p.log | cut -c1-1500

@@ -126,8 +126,6 @@ SIGNATURES = {
     "gcnk_gcn_forward_f32": (ctypes.c_int, [_vp, _vp, _vp, _vp, _vp, _vp, _i64, _vp, _i64, _i32, _vp, _i64, _f32,
                                             _f32, _u64, _u64, _vp, _vp]),
     "gcnk_gcn_fwd_layout": (_i32, [_vp, _i32]),
-    "gcnk_hub_xw_workspace_bytes": (_i64, [_i32, _i32, _i32]),
-    "gcnk_hub_xw_f32": (ctypes.c_int, [_i32, _i32, _i32, _vp, _i64, _vp, _i64, _vp, _i64, _vp, _i64, _vp]),
     "gcnk_factor_u_f32": (ctypes.c_int, [_vp, _vp, _vp, _i32, _vp, _vp, _vp, _i64, _i32, _vp, _i64, _i32, _vp]),
     "gcnk_factor_records": (ctypes.c_int, [_vp, _vp, _vp, _i32, _vp, _vp, _vp, _i32, _vp, _vp]),
     "gcnk_gcn_backward_f32": (ctypes.c_int, [_vp, _vp, _vp, _i64, _vp, _f32, _vp, _vp, _vp, _vp, _vp]),

@@ -24,9 +24,6 @@ int spmm_ref(const gcnk_plan_ref& p, const float* B, int64_t ldb, int32_t F, flo
 
 // S1 = X W1 (sparse X through its plan, dense X on the MFMA GEMM)
 int first_product(const gcnk_gcn_fwd& r, const float* W1, void* stream) {
-  if (r.x_hubxw)
-    return gcnk_hub_xw_f32(r.x_rows, r.x_cols, r.F, r.x_dense, r.ldx, W1, r.F, r.s1, r.lds1, r.gemm_ws,
-                           r.gemm_ws_bytes, stream);
   if (r.x.plan)
     return spmm_ref(r.x, W1, r.F, r.F, r.s1, r.lds1, nullptr, GCNK_EPI_NONE, nullptr, 0, 1.f, 1.f, 0, 0, nullptr,
                     stream);

@@ -29,12 +29,12 @@ import torch
 from .sparse import CSR
 
 MAX_HUBS = 128    # hub rows staged in LDS (S_T [hubs x F]; the kernel checks the LDS budget)
-# X[hubs] W1: "hubxw" (default, up to 64 hubs) -- one launch of
-# csrc/hubxw.hip over a zero-padded dense copy of X's hub rows; "spmm" -- the
-# SpMM tile plan on their CSR plus its slab reduce (R8 6.8 + 4.9 us, round 3);
-# "gemm" -- the split-K MFMA GEMM on a dense copy (9.5 + 4.9 us)
-XHUB = os.environ.get("GCNK_FACTOR_XHUB", "hubxw")
-HUBXW_MAX_HUBS = 64   # csrc/hubxw.hip: one 64-row MFMA tile of hub rows
+# X[hubs] W1: "spmm" (default) -- the SpMM tile plan on their CSR plus its slab
+# reduce (R8 9.8 us per call, two launches); "gemm" -- the split-K MFMA GEMM on
+# a dense copy (9.5 + 4.9 us, round 3).  A one-launch split-K MFMA kernel with
+# two levels of last-arriver slab sums measured 12.1 us (round 4, DESIGN §5:
+# each coherent hand-off is a ~2 us memory round trip) and was removed.
+XHUB = os.environ.get("GCNK_FACTOR_XHUB", "spmm")
 MAX_KC = 128      # X's light-row column range (U's width)
 ROWS_PER_BLOCK = 32   # csrc/factor.hip kRB
 # record words before the items: 33 row offsets | 3 pad | 32 row ids (-1 past
@@ -52,29 +52,11 @@ class HubFactor:
     """The (A-hat, X)-fixed operands of the factored gc1, resident on the device."""
 
     __slots__ = ("M", "H", "K", "hubs", "k0", "Kc", "U", "perm", "rec", "rec_words", "nblk", "x_hub",
-                 "x_hub_dense", "x_hub_pad", "_ws", "_src")
-
-    @property
-    def use_hubxw(self):
-        return self.x_hub_pad is not None
-
-    def hubxw_workspace(self, F, device):
-        """gcnk_hub_xw_f32's workspace for width F on torch's current stream
-        (its counter words zeroed once here; every launch leaves them zero)."""
-        from . import _lib
-        key = (F, torch.cuda.current_stream(device).cuda_stream)
-        ws = self._ws.get(key)
-        if ws is None:
-            nb = int(_lib.load().gcnk_hub_xw_workspace_bytes(self.H, self.K, F))
-            _lib.check(nb if nb < 0 else 0, "gcnk_hub_xw_workspace_bytes")
-            ws = self._ws[key] = torch.zeros((nb + 3) // 4, dtype=torch.float32, device=device)
-        return ws
+                 "x_hub_dense", "_src")
 
     def hub_times(self, W):
         """S_T = X[hubs] @ W  (the hub rows of reference layer.py:102)."""
-        from .ops import gemm, hub_xw, spmm
-        if self.use_hubxw:
-            return hub_xw(self.x_hub_pad, self.K, W, self.hubxw_workspace(W.shape[1], W.device))
+        from .ops import gemm, spmm
         if self.x_hub is not None and (XHUB != "gemm" or self.x_hub_dense is None):
             return spmm(self.x_hub, W)
         return gemm(self.x_hub_dense, W)
@@ -175,7 +157,6 @@ def build(adj, xop):
     f.nblk = nblk
     f.M, f.H, f.k0, f.Kc = M, H, k0, Kc
     f.K = xop.shape[1]
-    f._ws = {}
     f.hubs = hubs.to(torch.int64)
     f.perm = torch.from_numpy(perm.astype(np.int64))            # host: tests and tools
     f.U, f.rec, f.rec_words = U, rec, rec_words
@@ -198,17 +179,6 @@ def build(adj, xop):
     else:
         f.x_hub = None
         f.x_hub_dense = xop.dense.index_select(0, f.hubs).contiguous()
-    # the zero-padded dense copy gcnk_hub_xw_f32 reads (rows 16-B aligned)
-    f.x_hub_pad = None
-    Kp = (f.K + 3) // 4 * 4
-    if XHUB == "hubxw" and H <= HUBXW_MAX_HUBS and H * Kp * 4 <= 64 << 20:
-        d = torch.zeros((H, Kp), dtype=torch.float32, device=dev)
-        if xop.csr is not None:
-            d[torch.repeat_interleave(torch.arange(H, device=dev), lens, output_size=tot), x.colind[idx].long()] = \
-                x.val[idx]
-        else:
-            d[:, :f.K] = f.x_hub_dense
-        f.x_hub_pad = d
     if int(overflow.item()) != 0:
         raise RuntimeError("factor.build: A_H records overflowed their sized length (internal error)")
     return f

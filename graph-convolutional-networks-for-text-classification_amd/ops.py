@@ -277,24 +277,6 @@ def gemm(A, B, transA=False, transB=False, bias=None, epilogue=_lib.GEMM_EPI_NON
     return out
 
 
-def hub_xw(Xh, K, W, workspace):
-    """S_T = X_hubs @ W in one launch (gcnk_hub_xw_f32, csrc/hubxw.hip): the hub
-    rows of ``th.spmm(infeatn, W)`` (reference layer.py:102) for the factored
-    gc1.  Xh: X's hub rows, dense, zero-padded to a multiple of 4 columns;
-    workspace: factor.HubFactor.hubxw_workspace (counters zero on entry)."""
-    W = _dense_f32(W, "W")
-    H, F = Xh.shape[0], W.shape[1]
-    if W.shape[0] != K or Xh.shape[1] < K:
-        raise RuntimeError(f"hub_xw shape mismatch: X_hubs {tuple(Xh.shape)} (K={K}) @ W {tuple(W.shape)}")
-    out = torch.empty((H, F), dtype=torch.float32, device=W.device)
-    lib = _lib.load()
-    with torch.cuda.device(W.device):
-        rc = lib.gcnk_hub_xw_f32(H, K, F, _ptr(Xh), Xh.stride(0), _ptr(W), W.stride(0), _ptr(out), F,
-                                 _ptr(workspace), 4 * workspace.numel(), _stream(W.device))
-    _lib.check(rc, "gcnk_hub_xw_f32")
-    return out
-
-
 def colsum(X):
     """out[n] = sum_m X[m, n] — the bias gradient (autograd of layer.py:110)."""
     X = _dense_f32(X, "X")

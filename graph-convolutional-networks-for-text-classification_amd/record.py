@@ -34,7 +34,7 @@ class GcnFwd(_c.Structure):
     """gcnk_gcn_fwd (include/gcnk.h)."""
     _fields_ = [("kind", _c.c_int32), ("M", _c.c_int32), ("F", _c.c_int32), ("P", _c.c_int32),
                 ("x_rows", _c.c_int32), ("x_cols", _c.c_int32), ("x", PlanRef),
-                ("x_dense", _c.c_void_p), ("ldx", _c.c_int64), ("x_split_k", _c.c_int32), ("x_hubxw", _c.c_int32),
+                ("x_dense", _c.c_void_p), ("ldx", _c.c_int64), ("x_split_k", _c.c_int32), ("pad0_", _c.c_int32),
                 ("gemm_ws", _c.c_void_p), ("gemm_ws_bytes", _c.c_int64), ("s1", _c.c_void_p), ("lds1", _c.c_int64),
                 ("Kc", _c.c_int32), ("nhub", _c.c_int32), ("k0", _c.c_int32), ("rec_words", _c.c_int32),
                 ("U", _c.c_void_p), ("ldu", _c.c_int64), ("rec", _c.c_void_p),
@@ -102,15 +102,7 @@ class ForwardRecord:
             s.Kc, s.nhub, s.k0, s.rec_words = fac.Kc, fac.H, fac.k0, fac.rec_words
             s.U, s.ldu, s.rec = fac.U.data_ptr(), fac.U.stride(0), fac.rec.data_ptr()
             keep += [fac.U, fac.rec]
-            if fac.use_hubxw:   # one launch of gcnk_hub_xw_f32 (its workspace as gemm_ws)
-                x_csr, x_dense = None, None
-                rows, cols = fac.H, fac.K
-                s.x_hubxw = 1
-                s.x_dense, s.ldx = fac.x_hub_pad.data_ptr(), fac.x_hub_pad.stride(0)
-                ws = fac.hubxw_workspace(F, device)
-                s.gemm_ws, s.gemm_ws_bytes = ws.data_ptr(), 4 * ws.numel()
-                keep += [fac.x_hub_pad, ws]
-            elif fac.x_hub is not None and (factor.XHUB != "gemm" or fac.x_hub_dense is None):
+            if fac.x_hub is not None and (factor.XHUB != "gemm" or fac.x_hub_dense is None):
                 x_csr, x_dense = fac.x_hub, None
             else:
                 x_csr, x_dense = None, fac.x_hub_dense
@@ -137,7 +129,7 @@ class ForwardRecord:
             xp = x_csr.plan(ops.default_ipc(x_csr, F, 0), int(lib.gcnk_spmm_groups(F, 0)), DENSE_THRESHOLD)
             _fill_plan(s.x, xp, F, 0, device, keep)
             keep.append(xp)
-        elif x_dense is not None:
+        else:
             rows, cols = x_dense.shape
             s.x_dense, s.ldx = x_dense.data_ptr(), x_dense.stride(0)
             keep.append(x_dense)

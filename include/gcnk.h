@@ -269,18 +269,6 @@ int gcnk_hubfactor_gc1_f32(int32_t M, int32_t F, int32_t Kc, int32_t nhub, int32
                            uint64_t offset, const uint64_t* rng_base, const float* W2, int64_t ldw2, float* H,
                            int64_t ldh, float* C2, int64_t ldc2, void* stream);
 
-/* S_T = X_hubs W (the hub rows of gc1's support, layer.py:102, for the
- * factored gc1) in ONE launch (csrc/hubxw.hip): X_hubs dense [H x K], H <= 64,
- * ldx >= K rounded up to 4 with zeros in [K, ldx), 16-B aligned rows; W
- * [K x F] (ldw); S [H x F] (lds).  K is split over ~256 workgroups; their
- * partial tiles are summed by two levels of last-arriver hand-offs in a fixed
- * order (bitwise reproducible).  Workspace: gcnk_hub_xw_workspace_bytes, 16-B
- * aligned; its trailing counter words must be zero before the first launch and
- * every launch leaves them zero (one workspace per stream). */
-int64_t gcnk_hub_xw_workspace_bytes(int32_t H, int32_t K, int32_t F);
-int gcnk_hub_xw_f32(int32_t H, int32_t K, int32_t F, const float* X, int64_t ldx, const float* W, int64_t ldw,
-                    float* S, int64_t lds, void* workspace, int64_t workspace_bytes, void* stream);
-
 /* The hub factorisation's (A-hat, X)-fixed operands, built on the device once
  * per operand pair (csrc/factor_build.hip; factor.py drives it, the host
  * restatement is oracle/factor_host.py):
@@ -311,8 +299,7 @@ int gcnk_factor_records(const int32_t* rowptr, const int32_t* colind, const floa
  * issues the launches the per-op entry points above issue, in the same order
  * and with the same arguments (results are bitwise those of the per-op path).
  *
- *   GCNK_FWD_FACTORED   S_T = X_hubs W1 (x plan, dense GEMM, or with x_hubxw the
- *                       one-launch gcnk_hub_xw_f32; x_rows = nhub);
+ *   GCNK_FWD_FACTORED   S_T = X_hubs W1 (x plan or dense GEMM, x_rows = nhub);
  *                       (H1, S2) = gcnk_hubfactor_gc1_f32; out = A-hat S2 + b2
  *   GCNK_FWD_SPMM_PROJ  S1 = X W1; (H1, S2) = gcnk_spmm_proj_f32(aF); out = A-hat S2 + b2
  *   GCNK_FWD_SPMM_GEMM  S1 = X W1; H1 = epi(A-hat S1 + b1) (aF); S2 = H1 W2; out = A-hat S2 + b2
@@ -346,7 +333,7 @@ typedef struct gcnk_gcn_fwd {
   const float* x_dense;        /* ... or dense [x_rows x x_cols] (ldx) on the MFMA GEMM */
   int64_t ldx;
   int32_t x_split_k;
-  int32_t x_hubxw;             /* ABI 9: 1 -> S_T = gcnk_hub_xw_f32(x_dense, workspace gemm_ws) */
+  int32_t pad0_;
   float* gemm_ws;              /* GEMM split-K workspace (first product and H1 W2) */
   int64_t gemm_ws_bytes;
   float* s1;                   /* S1 = X W1, or S_T = X_hubs W1 [x_rows x F] */

@@ -1,5 +1,5 @@
 """Per-op timing of the factored forward (warm, hipGraph of back-to-back
-launches, HIP events per call): X_hubs W1 (hub_xw kernel / tile SpMM),
+launches, HIP events per call): X_hubs W1 (tile SpMM or GEMM),
 hubfactor_gc1, A-hat S2, and the whole record forward, on R8 and the
 20ng-shaped graph.  One JSON line per (graph, op).  Run it under
 GCNK_LIB=<variant .so> to compare kernel builds.
@@ -50,10 +50,6 @@ def main():
                 line("no factor", float("nan"))
                 continue
             S_T = f.hub_times(W1).contiguous()
-            if f.use_hubxw:
-                ws = f.hubxw_workspace(W1.shape[1], dev)
-                line("X_hubs W1 (hub_xw)", time_graph([lambda: ops.hub_xw(f.x_hub_pad, f.K, W1, ws)], args.reps),
-                     H=f.H, K=f.K)
             if f.x_hub is not None:
                 line("X_hubs W1 (tile spmm)", time_graph([lambda: ops.spmm(f.x_hub, W1)], args.reps))
             if f.x_hub_dense is not None:

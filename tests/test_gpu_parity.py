@@ -1307,40 +1307,3 @@ def test_device_factor_build_is_bitwise_the_host_build(r8, case):
         assert np.array_equal(d.x_hub.val.cpu().numpy().view(np.int32), h.x_hub_val.view(np.int32))
     else:
         assert torch.equal(d.x_hub_dense.cpu(), Xd[torch.from_numpy(h.hubs)])
-    if d.x_hub_pad is not None:      # the hub_xw operand: X's hub rows, zero past K
-        xp = d.x_hub_pad.cpu()
-        assert xp.shape[1] % 4 == 0 and not bool(xp[:, d.K:].any())
-        ref = torch.from_numpy(h.x_hub_rowptr) if xop.csr is not None else None
-        want = (torch.sparse_csr_tensor(ref, torch.from_numpy(h.x_hub_colind).long(), torch.from_numpy(h.x_hub_val),
-                                        (d.H, d.K)).to_dense() if ref is not None else Xd[torch.from_numpy(h.hubs)])
-        assert torch.equal(xp[:, :d.K], want)
-
-
-@pytest.mark.parametrize("H,K,F", [(50, 7463, 200), (7, 100, 16), (64, 33, 8), (1, 5000, 200), (37, 1000, 37),
-                                   (64, 20000, 256), (20, 7463, 20)])
-def test_hub_xw_against_float64(H, K, F):
-    """gcnk_hub_xw_f32 (csrc/hubxw.hip, S_T = X_hubs W1 in one launch with
-    two-level last-arriver slab sums): against float64 at R8's shape (50 x
-    7,463 x 200), ragged H / K / F (partial row tiles, K not a multiple of 4 or
-    of the slab, F not a multiple of the 32-column tile), a single-slab K and a
-    many-slab K; two launches bitwise equal, and the counter words left zero."""
-    from graph_convolutional_networks_for_text_classification_amd import ops
-    rng = np.random.default_rng(H * 7 + K + F)
-    Kp = (K + 3) // 4 * 4
-    X = np.zeros((H, Kp), np.float32)
-    X[:, :K] = rng.random((H, K), dtype=np.float32) * (rng.random((H, K)) < 0.9)
-    W = rng.standard_normal((K, F)).astype(np.float32)
-    lib = _lib.load()
-    nb = int(lib.gcnk_hub_xw_workspace_bytes(H, K, F))
-    assert nb > 0
-    ws = torch.zeros((nb + 3) // 4, dtype=torch.float32, device=DEV)
-    Xd, Wd = torch.from_numpy(X).to(DEV), torch.from_numpy(W).to(DEV)
-    a = ops.hub_xw(Xd, K, Wd, ws)
-    b = ops.hub_xw(Xd, K, Wd, ws)
-    torch.cuda.synchronize()
-    ref = X[:, :K].astype(np.float64) @ W.astype(np.float64)
-    _close(a, ref, atol=2e-6 * np.sqrt(K) * max(1.0, np.abs(ref).max()))
-    assert torch.equal(a, b)
-    T = (F + 31) // 32
-    # the last T x 64 words hold the T final counters (64 words apart) and never-written pad
-    assert not bool(ws.view(torch.int32)[-(T * 64):].any())   # every final counter re-armed

@@ -521,7 +521,10 @@ static int launch_factor(const FactorArgs& a, int64_t nblk, int64_t lds_b, void*
         hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
     if (attr_p != hipSuccess) return hip_check(attr_p, "hubfactor_gc1_persist_kernel LDS attribute");
     const int64_t per_cu = lds_p <= 80 * 1024 ? 2 : 1;
-    const int64_t grid = std::min<int64_t>(nblk, per_cu * cus);
+#ifndef GCNK_PERSIST_WGS
+#define GCNK_PERSIST_WGS 0
+#endif
+    const int64_t grid = std::min<int64_t>(nblk, GCNK_PERSIST_WGS > 0 ? GCNK_PERSIST_WGS : per_cu * cus);
     hipLaunchKernelGGL((hubfactor_gc1_persist_kernel<KS, NTQ, NP>), dim3((unsigned)grid), dim3(kThreads),
                        (size_t)lds_p, reinterpret_cast<hipStream_t>(stream), a);
     return launch_check("hubfactor_gc1_persist_kernel");

@@ -291,6 +291,7 @@ hubfactor_gc1_persist_kernel(FactorArgs a) {
   float* s_red = s_bias + ((F + 3) & ~3);
   int32_t* s_rec = reinterpret_cast<int32_t*>(s_red + sred_floats_p(NP));
   const int nblk = (a.M + kRB - 1) / kRB;
+  stamp(a.epi, 0);   // (stamps build: 0 entry, 1 first block staged, 2 first block done, 3 exit)
 
   // ---- once per workgroup: S_T, W2, b1 (LDS-DMA) and the W1[Kc] fragments
   if (!a.epi.bias)
@@ -335,7 +336,7 @@ hubfactor_gc1_persist_kernel(FactorArgs a) {
     }
     __builtin_amdgcn_s_waitcnt(0x0F70);  // vmcnt(0): this wave's DMA and fragment loads have landed
     __syncthreads();
-    stamp(a.epi, 0);   // (stamps build: the workgroup's last block)
+    if (blk == (int)blockIdx.x) stamp(a.epi, 1);
 
     // ---- 1. Z = U W1[Kc] for this wave's strip and column quarter
     f32x4 acc[NTQ];
@@ -351,7 +352,6 @@ hubfactor_gc1_persist_kernel(FactorArgs a) {
       for (int r = 0; r < 4; ++r)
         if (c0 + 16 * i < F) s_Z[(16 * strip + (lane >> 4) * 4 + r) * Fz + c0 + i * 16] = acc[i][r];
     __syncthreads();
-    stamp(a.epi, 1);
 
     // ---- 2. + A_H S_T, + b1, ReLU, dropout (as the kernel above)
     {
@@ -397,7 +397,6 @@ hubfactor_gc1_persist_kernel(FactorArgs a) {
       }
     }
     __syncthreads();
-    stamp(a.epi, 2);
 
     // ---- 3. S2 = H1 W2 (as the kernel above)
     f32x4 pc[NP];
@@ -447,8 +446,9 @@ hubfactor_gc1_persist_kernel(FactorArgs a) {
       }
     }
     __syncthreads();  // s_rec / s_Z / s_red are rewritten by the next block
-    stamp(a.epi, 3);
+    if (blk == (int)blockIdx.x) stamp(a.epi, 2);
   }
+  stamp(a.epi, 3);
 }
 
 

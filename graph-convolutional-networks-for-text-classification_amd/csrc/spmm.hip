@@ -80,7 +80,7 @@ constexpr int kMaxSeg = 64;             // segments per heavy row (bounds the la
 // Nontemporal (streaming) output stores of the row kernel's finished rows: the
 // launch leaves no dirty output lines in the XCD L2s for the end-of-kernel
 // write-back.  R8 A-hat S1, F = 200, cold (HIP events per call,
-// gpurun_out/r04/probe_nt.log): 9.46 -> 8.16 us, document rows alone 8.16 ->
+// profiles/r04_probe_nt.log): 9.46 -> 8.16 us, document rows alone 8.16 ->
 // 6.95, topic rows alone 9.05 -> 7.78 (a cold 12.4 MB copy: 4.35 -> 3.25 us,
 // scripts/micro/ns_micro.hip).
 #ifndef GCNK_ROW_NT

@@ -283,17 +283,22 @@ hubfactor_gc1_persist_kernel(FactorArgs a) {
   const int F = a.F, Q = F / 4;
   constexpr int Fp = 64 * NTQ;
   const int Fz = zstride_p(F);
-  // LDS: s_Z [kRB][F + 4] | s_S [nhub][F] | s_W2 [F][P] | s_bias [F] | s_red | s_rec
-  float* s_Z = smem;
-  float* s_S = smem + kRB * Fz;
+  // LDS: s_S [nhub][F] | s_W2 [F][P] | s_bias [F] | region X, which first holds
+  // W1[Kc] (flat, read once into the B-fragment registers) and then
+  // s_Z [kRB][F + 4] | s_red | s_rec[2] (the current block's record and the next's)
+  float* s_S = smem;
   float* s_W2 = s_S + a.nhub * F;
   float* s_bias = s_W2 + ((F * a.P + 3) & ~3);
-  float* s_red = s_bias + ((F + 3) & ~3);
-  int32_t* s_rec = reinterpret_cast<int32_t*>(s_red + sred_floats_p(NP));
+  float* s_X = s_bias + ((F + 3) & ~3);
+  float* s_B = s_X;
+  float* s_Z = s_X;
+  float* s_red = s_Z + kRB * Fz;
+  int32_t* s_rec0 = reinterpret_cast<int32_t*>(s_red + sred_floats_p(NP));
   const int nblk = (a.M + kRB - 1) / kRB;
   stamp(a.epi, 0);   // (stamps build: 0 entry, 1 first block staged, 2 first block done, 3 exit)
 
-  // ---- once per workgroup: S_T, W2, b1 (LDS-DMA) and the W1[Kc] fragments
+  // ---- once per workgroup: S_T, W2, b1 and W1[Kc] by LDS-DMA, then W1's B
+  //      fragments into registers (a strip pair shares one copy of W1 in LDS)
   if (!a.epi.bias)
     for (int e = tid; e < F; e += kThreads) s_bias[e] = 0.f;
   {
@@ -306,36 +311,46 @@ hubfactor_gc1_persist_kernel(FactorArgs a) {
     if (a.epi.bias)
       for (int e0 = wv * 64; e0 < Q; e0 += kThreads)
         if (e0 + lane < Q) lds_dma16(a.epi.bias + 4 * (e0 + lane), s_bias + 4 * e0);
+    const int n4 = a.Kc * Q;  // W1[k0 .. k0 + Kc) flat (ldw == F)
+    const float* wsrc = a.W + (int64_t)a.k0 * a.ldw;
+    for (int e0 = wv * 64; e0 < n4; e0 += kThreads)
+      if (e0 + lane < n4) lds_dma16(wsrc + 4 * (e0 + lane), s_B + 4 * e0);
   }
+  __builtin_amdgcn_s_waitcnt(0x0F70);
+  __syncthreads();
   const int c0 = quarter * NTQ * 16 + (lane & 15);
   float bf[KS][NTQ];
-  {
-    const float* wsrc = a.W + (int64_t)a.k0 * a.ldw + c0;
 #pragma unroll
-    for (int s = 0; s < KS; ++s)
+  for (int s = 0; s < KS; ++s)
 #pragma unroll
-      for (int i = 0; i < NTQ; ++i) {
-        const int k = 4 * s + (lane >> 4);
-        bf[s][i] = (k < a.Kc && c0 + 16 * i < F) ? wsrc[(int64_t)k * a.ldw + 16 * i] : 0.f;
-      }
-  }
+    for (int i = 0; i < NTQ; ++i) {
+      const int k = 4 * s + (lane >> 4);
+      bf[s][i] = (k < a.Kc && c0 + 16 * i < F) ? s_B[k * F + c0 + 16 * i] : 0.f;
+    }
+  __syncthreads();  // region X now becomes s_Z / s_red / s_rec
 
-  for (int blk = (int)blockIdx.x; blk < nblk; blk += (int)gridDim.x) {
-    const int64_t m0 = (int64_t)blk * kRB;
-    {
-      const int32_t* rec = a.rec + (int64_t)blk * a.rec_words;
-      for (int e0 = wv * 64; e0 < a.rec_words / 4; e0 += kThreads)
-        if (e0 + lane < a.rec_words / 4) lds_dma16(rec + 4 * (e0 + lane), s_rec + 4 * e0);
-    }
-    float af[KS];
-    {
-      const int64_t row = m0 + 16 * strip + (lane & 15);
-      const float* up = a.U + row * a.ldu + (lane >> 4);
+  // a block's record (LDS-DMA into s_rec[buf]) and U fragments (registers)
+  auto fetch = [&](int blk, int buf, float (&afr)[KS]) {
+    int32_t* dst = s_rec0 + buf * a.rec_words;
+    const int32_t* rec = a.rec + (int64_t)blk * a.rec_words;
+    for (int e0 = wv * 64; e0 < a.rec_words / 4; e0 += kThreads)
+      if (e0 + lane < a.rec_words / 4) lds_dma16(rec + 4 * (e0 + lane), dst + 4 * e0);
+    const int64_t row = (int64_t)blk * kRB + 16 * strip + (lane & 15);
+    const float* up = a.U + row * a.ldu + (lane >> 4);
 #pragma unroll
-      for (int s = 0; s < KS; ++s) af[s] = (row < a.M && 4 * s + (lane >> 4) < a.Kc) ? up[4 * s] : 0.f;
-    }
-    __builtin_amdgcn_s_waitcnt(0x0F70);  // vmcnt(0): this wave's DMA and fragment loads have landed
+    for (int s = 0; s < KS; ++s) afr[s] = (row < a.M && 4 * s + (lane >> 4) < a.Kc) ? up[4 * s] : 0.f;
+  };
+  float af[KS], af_next[KS];
+  if ((int)blockIdx.x < nblk) fetch((int)blockIdx.x, 0, af);
+  int buf = 0;
+
+  for (int blk = (int)blockIdx.x; blk < nblk; blk += (int)gridDim.x, buf ^= 1) {
+    int32_t* s_rec = s_rec0 + buf * a.rec_words;
+    __builtin_amdgcn_s_waitcnt(0x0F70);  // vmcnt(0): this block's record and U fragments have landed
     __syncthreads();
+    // the next block's operands fly while this block computes
+    const int nxt = blk + (int)gridDim.x;
+    if (nxt < nblk) fetch(nxt, buf ^ 1, af_next);
     if (blk == (int)blockIdx.x) stamp(a.epi, 1);
 
     // ---- 1. Z = U W1[Kc] for this wave's strip and column quarter
@@ -445,8 +460,10 @@ hubfactor_gc1_persist_kernel(FactorArgs a) {
         }
       }
     }
-    __syncthreads();  // s_rec / s_Z / s_red are rewritten by the next block
+    __syncthreads();  // s_Z / s_red (and this s_rec) are rewritten by the next blocks
     if (blk == (int)blockIdx.x) stamp(a.epi, 2);
+#pragma unroll
+    for (int s2 = 0; s2 < KS; ++s2) af[s2] = af_next[s2];
   }
   stamp(a.epi, 3);
 }
@@ -489,9 +506,10 @@ extern "C" int64_t gcnk_hubfactor_lds_bytes(int32_t F, int32_t Kc, int32_t nhub,
   return hubfactor_lds_bytes(F, Kc, nhub, rec_words, P);
 }
 
-static int64_t persist_lds_bytes(int32_t F, int32_t nhub, int32_t rec_words, int32_t P) {
-  return 4 * ((int64_t)kRB * zstride_p(F) + (int64_t)nhub * F + (((int64_t)F * P + 3) & ~3LL) + ((F + 3) & ~3) +
-              sred_floats_p(pick_np(P)) + rec_words);
+static int64_t persist_lds_bytes(int32_t F, int32_t Kc, int32_t nhub, int32_t rec_words, int32_t P) {
+  const int64_t x = std::max<int64_t>((int64_t)Kc * F,
+                                      (int64_t)kRB * zstride_p(F) + sred_floats_p(pick_np(P)) + 2 * (int64_t)rec_words);
+  return 4 * ((int64_t)nhub * F + (((int64_t)F * P + 3) & ~3LL) + ((F + 3) & ~3) + x);
 }
 
 // CUs of the current device (cached per device id)
@@ -514,7 +532,7 @@ static int device_cus() {
 template <int KS, int NTQ, int NP>
 static int launch_factor(const FactorArgs& a, int64_t nblk, int64_t lds_b, void* stream) {
   const int cus = device_cus();
-  const int64_t lds_p = persist_lds_bytes(a.F, a.nhub, a.rec_words, a.P);
+  const int64_t lds_p = persist_lds_bytes(a.F, a.Kc, a.nhub, a.rec_words, a.P);
   if (nblk > cus && lds_p <= 160 * 1024) {
     static const hipError_t attr_p = hipFuncSetAttribute(
         reinterpret_cast<const void*>(&hubfactor_gc1_persist_kernel<KS, NTQ, NP>),

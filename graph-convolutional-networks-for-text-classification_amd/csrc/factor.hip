@@ -70,6 +70,25 @@ struct FactorArgs {
   Epi epi;
 };
 
+// Stage n float4s (dma16) or floats (dma4) of an operand every workgroup reads
+// (W1[Kc], S_T, W2) into LDS in 64-lane chunks, the workgroup's chunk order
+// rotated by `rot`: workgroups that start together then read different L2
+// channels instead of all marching over the same lines in lockstep.
+__device__ __forceinline__ void stage_shared16(const float* src, float* dst, int n4, int rot, int wv, int lane) {
+  const int nch = (n4 + 63) >> 6;
+  for (int j = wv; j < nch; j += kThreads / 64) {
+    const int c = (j + rot) % nch;
+    if ((c << 6) + lane < n4) lds_dma16(src + 4 * ((c << 6) + lane), dst + 4 * (c << 6));
+  }
+}
+__device__ __forceinline__ void stage_shared4(const float* src, float* dst, int n, int rot, int wv, int lane) {
+  const int nch = (n + 63) >> 6;
+  for (int j = wv; j < nch; j += kThreads / 64) {
+    const int c = (j + rot) % nch;
+    if ((c << 6) + lane < n) lds_dma4(src + (c << 6) + lane, dst + (c << 6));
+  }
+}
+
 template <int KS>
 __host__ __device__ constexpr int region1_floats(int F, int ntq) {
   return (4 * KS * F + bpad(F, ntq)) > kRB * (64 * ntq + 4) ? (4 * KS * F + bpad(F, ntq)) : kRB * (64 * ntq + 4);
@@ -109,19 +128,14 @@ hubfactor_gc1_kernel(FactorArgs a) {
   if (!a.epi.bias)
     for (int e = tid; e < F; e += kThreads) s_bias[e] = 0.f;
   {
+    const int rot = 7 * blk;  // (stage_shared*: chunk order rotated per workgroup)
     const int n4 = a.Kc * Q;  // float4 pieces of W1[k0 .. k0 + Kc) (rows of F floats, ldw == F)
-    const float* wsrc = a.W + (int64_t)a.k0 * a.ldw;
-    for (int e0 = wv * 64; e0 < n4; e0 += kThreads)
-      if (e0 + lane < n4) lds_dma16(wsrc + 4 * (e0 + lane), s_B + 4 * e0);
+    stage_shared16(a.W + (int64_t)a.k0 * a.ldw, s_B, n4, rot, wv, lane);
     const int32_t* rec = a.rec + (int64_t)blk * a.rec_words;
     for (int e0 = wv * 64; e0 < a.rec_words / 4; e0 += kThreads)
       if (e0 + lane < a.rec_words / 4) lds_dma16(rec + 4 * (e0 + lane), s_rec + 4 * e0);
-    const int s4 = a.nhub * Q;  // S_T [nhub x F] flat (lds == F)
-    for (int e0 = wv * 64; e0 < s4; e0 += kThreads)
-      if (e0 + lane < s4) lds_dma16(a.S + 4 * (e0 + lane), s_S + 4 * e0);
-    const int w1 = F * a.P;     // W2 [F x P] flat (ldw2 == P), dword pieces
-    for (int e0 = wv * 64; e0 < w1; e0 += kThreads)
-      if (e0 + lane < w1) lds_dma4(a.W2 + e0 + lane, s_W2 + e0);
+    stage_shared16(a.S, s_S, a.nhub * Q, rot, wv, lane);    // S_T [nhub x F] flat (lds == F)
+    stage_shared4(a.W2, s_W2, F * a.P, rot, wv, lane);      // W2 [F x P] flat (ldw2 == P)
     if (a.epi.bias)
       for (int e0 = wv * 64; e0 < Q; e0 += kThreads)
         if (e0 + lane < Q) lds_dma16(a.epi.bias + 4 * (e0 + lane), s_bias + 4 * e0);
@@ -283,17 +297,17 @@ hubfactor_gc1_persist_kernel(FactorArgs a) {
   const int F = a.F, Q = F / 4;
   constexpr int Fp = 64 * NTQ;
   const int Fz = zstride_p(F);
-  // LDS: s_S [nhub][F] | s_W2 [F][P] | s_bias [F] | region X, which first holds
-  // W1[Kc] (flat, read once into the B-fragment registers) and then
-  // s_Z [kRB][F + 4] | s_red | s_rec[2] (the current block's record and the next's)
+  // LDS: s_S [nhub][F] | s_W2 [F][P] | s_bias [F] | s_rec[2] (the current block's
+  // record and the next's) | region X, which first holds W1[Kc] (flat, read once
+  // into the B-fragment registers) and then s_Z [kRB][F + 4] | s_red
   float* s_S = smem;
   float* s_W2 = s_S + a.nhub * F;
   float* s_bias = s_W2 + ((F * a.P + 3) & ~3);
-  float* s_X = s_bias + ((F + 3) & ~3);
+  int32_t* s_rec0 = reinterpret_cast<int32_t*>(s_bias + ((F + 3) & ~3));
+  float* s_X = reinterpret_cast<float*>(s_rec0 + 2 * a.rec_words);
   float* s_B = s_X;
   float* s_Z = s_X;
   float* s_red = s_Z + kRB * Fz;
-  int32_t* s_rec0 = reinterpret_cast<int32_t*>(s_red + sred_floats_p(NP));
   const int nblk = (a.M + kRB - 1) / kRB;
   stamp(a.epi, 0);   // (stamps build: 0 entry, 1 first block staged, 2 first block done, 3 exit)
 
@@ -302,34 +316,16 @@ hubfactor_gc1_persist_kernel(FactorArgs a) {
   if (!a.epi.bias)
     for (int e = tid; e < F; e += kThreads) s_bias[e] = 0.f;
   {
-    const int s4 = a.nhub * Q;
-    for (int e0 = wv * 64; e0 < s4; e0 += kThreads)
-      if (e0 + lane < s4) lds_dma16(a.S + 4 * (e0 + lane), s_S + 4 * e0);
-    const int w1 = F * a.P;
-    for (int e0 = wv * 64; e0 < w1; e0 += kThreads)
-      if (e0 + lane < w1) lds_dma4(a.W2 + e0 + lane, s_W2 + e0);
+    const int rot = 7 * (int)blockIdx.x;
+    stage_shared16(a.S, s_S, a.nhub * Q, rot, wv, lane);
+    stage_shared4(a.W2, s_W2, F * a.P, rot, wv, lane);
     if (a.epi.bias)
       for (int e0 = wv * 64; e0 < Q; e0 += kThreads)
         if (e0 + lane < Q) lds_dma16(a.epi.bias + 4 * (e0 + lane), s_bias + 4 * e0);
-    const int n4 = a.Kc * Q;  // W1[k0 .. k0 + Kc) flat (ldw == F)
-    const float* wsrc = a.W + (int64_t)a.k0 * a.ldw;
-    for (int e0 = wv * 64; e0 < n4; e0 += kThreads)
-      if (e0 + lane < n4) lds_dma16(wsrc + 4 * (e0 + lane), s_B + 4 * e0);
+    stage_shared16(a.W + (int64_t)a.k0 * a.ldw, s_B, a.Kc * Q, rot, wv, lane);  // W1[k0 .. k0 + Kc) flat
   }
-  __builtin_amdgcn_s_waitcnt(0x0F70);
-  __syncthreads();
-  const int c0 = quarter * NTQ * 16 + (lane & 15);
-  float bf[KS][NTQ];
-#pragma unroll
-  for (int s = 0; s < KS; ++s)
-#pragma unroll
-    for (int i = 0; i < NTQ; ++i) {
-      const int k = 4 * s + (lane >> 4);
-      bf[s][i] = (k < a.Kc && c0 + 16 * i < F) ? s_B[k * F + c0 + 16 * i] : 0.f;
-    }
-  __syncthreads();  // region X now becomes s_Z / s_red / s_rec
-
-  // a block's record (LDS-DMA into s_rec[buf]) and U fragments (registers)
+  // a block's record (LDS-DMA into s_rec[buf]) and U fragments (registers);
+  // the first block's fly with the shared staging
   auto fetch = [&](int blk, int buf, float (&afr)[KS]) {
     int32_t* dst = s_rec0 + buf * a.rec_words;
     const int32_t* rec = a.rec + (int64_t)blk * a.rec_words;
@@ -343,6 +339,18 @@ hubfactor_gc1_persist_kernel(FactorArgs a) {
   float af[KS], af_next[KS];
   if ((int)blockIdx.x < nblk) fetch((int)blockIdx.x, 0, af);
   int buf = 0;
+  __builtin_amdgcn_s_waitcnt(0x0F70);
+  __syncthreads();
+  const int c0 = quarter * NTQ * 16 + (lane & 15);
+  float bf[KS][NTQ];
+#pragma unroll
+  for (int s = 0; s < KS; ++s)
+#pragma unroll
+    for (int i = 0; i < NTQ; ++i) {
+      const int k = 4 * s + (lane >> 4);
+      bf[s][i] = (k < a.Kc && c0 + 16 * i < F) ? s_B[k * F + c0 + 16 * i] : 0.f;
+    }
+  __syncthreads();  // region X now becomes s_Z / s_red
 
   for (int blk = (int)blockIdx.x; blk < nblk; blk += (int)gridDim.x, buf ^= 1) {
     int32_t* s_rec = s_rec0 + buf * a.rec_words;
@@ -507,9 +515,8 @@ extern "C" int64_t gcnk_hubfactor_lds_bytes(int32_t F, int32_t Kc, int32_t nhub,
 }
 
 static int64_t persist_lds_bytes(int32_t F, int32_t Kc, int32_t nhub, int32_t rec_words, int32_t P) {
-  const int64_t x = std::max<int64_t>((int64_t)Kc * F,
-                                      (int64_t)kRB * zstride_p(F) + sred_floats_p(pick_np(P)) + 2 * (int64_t)rec_words);
-  return 4 * ((int64_t)nhub * F + (((int64_t)F * P + 3) & ~3LL) + ((F + 3) & ~3) + x);
+  const int64_t x = std::max<int64_t>((int64_t)Kc * F, (int64_t)kRB * zstride_p(F) + sred_floats_p(pick_np(P)));
+  return 4 * ((int64_t)nhub * F + (((int64_t)F * P + 3) & ~3LL) + ((F + 3) & ~3) + 2 * (int64_t)rec_words + x);
 }
 
 // CUs of the current device (cached per device id)

@@ -70,25 +70,6 @@ struct FactorArgs {
   Epi epi;
 };
 
-// Stage n float4s (dma16) or floats (dma4) of an operand every workgroup reads
-// (W1[Kc], S_T, W2) into LDS in 64-lane chunks, the workgroup's chunk order
-// rotated by `rot`: workgroups that start together then read different L2
-// channels instead of all marching over the same lines in lockstep.
-__device__ __forceinline__ void stage_shared16(const float* src, float* dst, int n4, int rot, int wv, int lane) {
-  const int nch = (n4 + 63) >> 6;
-  for (int j = wv; j < nch; j += kThreads / 64) {
-    const int c = (j + rot) % nch;
-    if ((c << 6) + lane < n4) lds_dma16(src + 4 * ((c << 6) + lane), dst + 4 * (c << 6));
-  }
-}
-__device__ __forceinline__ void stage_shared4(const float* src, float* dst, int n, int rot, int wv, int lane) {
-  const int nch = (n + 63) >> 6;
-  for (int j = wv; j < nch; j += kThreads / 64) {
-    const int c = (j + rot) % nch;
-    if ((c << 6) + lane < n) lds_dma4(src + (c << 6) + lane, dst + (c << 6));
-  }
-}
-
 template <int KS>
 __host__ __device__ constexpr int region1_floats(int F, int ntq) {
   return (4 * KS * F + bpad(F, ntq)) > kRB * (64 * ntq + 4) ? (4 * KS * F + bpad(F, ntq)) : kRB * (64 * ntq + 4);
@@ -128,14 +109,19 @@ hubfactor_gc1_kernel(FactorArgs a) {
   if (!a.epi.bias)
     for (int e = tid; e < F; e += kThreads) s_bias[e] = 0.f;
   {
-    const int rot = 7 * blk;  // (stage_shared*: chunk order rotated per workgroup)
     const int n4 = a.Kc * Q;  // float4 pieces of W1[k0 .. k0 + Kc) (rows of F floats, ldw == F)
-    stage_shared16(a.W + (int64_t)a.k0 * a.ldw, s_B, n4, rot, wv, lane);
+    const float* wsrc = a.W + (int64_t)a.k0 * a.ldw;
+    for (int e0 = wv * 64; e0 < n4; e0 += kThreads)
+      if (e0 + lane < n4) lds_dma16(wsrc + 4 * (e0 + lane), s_B + 4 * e0);
     const int32_t* rec = a.rec + (int64_t)blk * a.rec_words;
     for (int e0 = wv * 64; e0 < a.rec_words / 4; e0 += kThreads)
       if (e0 + lane < a.rec_words / 4) lds_dma16(rec + 4 * (e0 + lane), s_rec + 4 * e0);
-    stage_shared16(a.S, s_S, a.nhub * Q, rot, wv, lane);    // S_T [nhub x F] flat (lds == F)
-    stage_shared4(a.W2, s_W2, F * a.P, rot, wv, lane);      // W2 [F x P] flat (ldw2 == P)
+    const int s4 = a.nhub * Q;  // S_T [nhub x F] flat (lds == F)
+    for (int e0 = wv * 64; e0 < s4; e0 += kThreads)
+      if (e0 + lane < s4) lds_dma16(a.S + 4 * (e0 + lane), s_S + 4 * e0);
+    const int w1 = F * a.P;     // W2 [F x P] flat (ldw2 == P), dword pieces
+    for (int e0 = wv * 64; e0 < w1; e0 += kThreads)
+      if (e0 + lane < w1) lds_dma4(a.W2 + e0 + lane, s_W2 + e0);
     if (a.epi.bias)
       for (int e0 = wv * 64; e0 < Q; e0 += kThreads)
         if (e0 + lane < Q) lds_dma16(a.epi.bias + 4 * (e0 + lane), s_bias + 4 * e0);
@@ -274,208 +260,6 @@ hubfactor_gc1_kernel(FactorArgs a) {
   stamp(a.epi, 3);
 }
 
-// ---------------------------------------------------------------------------
-// Persistent form for graphs with more 32-row blocks than the chip holds at
-// once (BASELINE config 3, the 20ng shape: 592 blocks, 152 KB of LDS each at
-// one workgroup per CU).  The kernel above restages W1[Kc], S_T and W2 for
-// every block: with all CUs staging at once each round of blocks spent ~5 us
-// of its ~12 us loading them (gpurun_out/r04/factorstamps20.log).  Here a
-// workgroup stages S_T, W2 and b1 into LDS and its W1[Kc] B fragments into
-// registers ONCE, then walks blocks blockIdx.x, + gridDim.x, ...: per block only
-// its record (LDS-DMA) and U fragments are loaded.  Same arithmetic, same
-// order per output element as the kernel above (bitwise equal results).
-__host__ __device__ constexpr int zstride_p(int F) { return F + 4; }
-__host__ __device__ constexpr int sred_floats_p(int np) { return np * 3 * 2 * 64 * 4; }
-
-template <int KS, int NTQ, int NP>
-__global__ void __launch_bounds__(kThreads)
-hubfactor_gc1_persist_kernel(FactorArgs a) {
-  extern __shared__ __attribute__((aligned(16))) float smem[];
-  const int tid = threadIdx.x, lane = tid & 63;
-  const int wv = __builtin_amdgcn_readfirstlane(tid >> 6);
-  const int strip = wv & 1, quarter = wv >> 1;
-  const int F = a.F, Q = F / 4;
-  constexpr int Fp = 64 * NTQ;
-  const int Fz = zstride_p(F);
-  // LDS: s_S [nhub][F] | s_W2 [F][P] | s_bias [F] | s_rec[2] (the current block's
-  // record and the next's) | region X, which first holds W1[Kc] (flat, read once
-  // into the B-fragment registers) and then s_Z [kRB][F + 4] | s_red
-  float* s_S = smem;
-  float* s_W2 = s_S + a.nhub * F;
-  float* s_bias = s_W2 + ((F * a.P + 3) & ~3);
-  int32_t* s_rec0 = reinterpret_cast<int32_t*>(s_bias + ((F + 3) & ~3));
-  float* s_X = reinterpret_cast<float*>(s_rec0 + 2 * a.rec_words);
-  float* s_B = s_X;
-  float* s_Z = s_X;
-  float* s_red = s_Z + kRB * Fz;
-  const int nblk = (a.M + kRB - 1) / kRB;
-  stamp(a.epi, 0);   // (stamps build: 0 entry, 1 first block staged, 2 first block done, 3 exit)
-
-  // ---- once per workgroup: S_T, W2, b1 and W1[Kc] by LDS-DMA, then W1's B
-  //      fragments into registers (a strip pair shares one copy of W1 in LDS)
-  if (!a.epi.bias)
-    for (int e = tid; e < F; e += kThreads) s_bias[e] = 0.f;
-  {
-    const int rot = 7 * (int)blockIdx.x;
-    stage_shared16(a.S, s_S, a.nhub * Q, rot, wv, lane);
-    stage_shared4(a.W2, s_W2, F * a.P, rot, wv, lane);
-    if (a.epi.bias)
-      for (int e0 = wv * 64; e0 < Q; e0 += kThreads)
-        if (e0 + lane < Q) lds_dma16(a.epi.bias + 4 * (e0 + lane), s_bias + 4 * e0);
-    stage_shared16(a.W + (int64_t)a.k0 * a.ldw, s_B, a.Kc * Q, rot, wv, lane);  // W1[k0 .. k0 + Kc) flat
-  }
-  // a block's record (LDS-DMA into s_rec[buf]) and U fragments (registers);
-  // the first block's fly with the shared staging
-  auto fetch = [&](int blk, int buf, float (&afr)[KS]) {
-    int32_t* dst = s_rec0 + buf * a.rec_words;
-    const int32_t* rec = a.rec + (int64_t)blk * a.rec_words;
-    for (int e0 = wv * 64; e0 < a.rec_words / 4; e0 += kThreads)
-      if (e0 + lane < a.rec_words / 4) lds_dma16(rec + 4 * (e0 + lane), dst + 4 * e0);
-    const int64_t row = (int64_t)blk * kRB + 16 * strip + (lane & 15);
-    const float* up = a.U + row * a.ldu + (lane >> 4);
-#pragma unroll
-    for (int s = 0; s < KS; ++s) afr[s] = (row < a.M && 4 * s + (lane >> 4) < a.Kc) ? up[4 * s] : 0.f;
-  };
-  float af[KS], af_next[KS];
-  if ((int)blockIdx.x < nblk) fetch((int)blockIdx.x, 0, af);
-  int buf = 0;
-  __builtin_amdgcn_s_waitcnt(0x0F70);
-  __syncthreads();
-  const int c0 = quarter * NTQ * 16 + (lane & 15);
-  float bf[KS][NTQ];
-#pragma unroll
-  for (int s = 0; s < KS; ++s)
-#pragma unroll
-    for (int i = 0; i < NTQ; ++i) {
-      const int k = 4 * s + (lane >> 4);
-      bf[s][i] = (k < a.Kc && c0 + 16 * i < F) ? s_B[k * F + c0 + 16 * i] : 0.f;
-    }
-  __syncthreads();  // region X now becomes s_Z / s_red
-
-  for (int blk = (int)blockIdx.x; blk < nblk; blk += (int)gridDim.x, buf ^= 1) {
-    int32_t* s_rec = s_rec0 + buf * a.rec_words;
-    __builtin_amdgcn_s_waitcnt(0x0F70);  // vmcnt(0): this block's record and U fragments have landed
-    __syncthreads();
-    // the next block's operands fly while this block computes
-    const int nxt = blk + (int)gridDim.x;
-    if (nxt < nblk) fetch(nxt, buf ^ 1, af_next);
-    if (blk == (int)blockIdx.x) stamp(a.epi, 1);
-
-    // ---- 1. Z = U W1[Kc] for this wave's strip and column quarter
-    f32x4 acc[NTQ];
-#pragma unroll
-    for (int i = 0; i < NTQ; ++i) acc[i] = f32x4{0.f, 0.f, 0.f, 0.f};
-#pragma unroll
-    for (int s = 0; s < KS; ++s)
-#pragma unroll
-      for (int i = 0; i < NTQ; ++i) acc[i] = __builtin_amdgcn_mfma_f32_16x16x4f32(af[s], bf[s][i], acc[i], 0, 0, 0);
-#pragma unroll
-    for (int i = 0; i < NTQ; ++i)
-#pragma unroll
-      for (int r = 0; r < 4; ++r)
-        if (c0 + 16 * i < F) s_Z[(16 * strip + (lane >> 4) * 4 + r) * Fz + c0 + i * 16] = acc[i][r];
-    __syncthreads();
-
-    // ---- 2. + A_H S_T, + b1, ReLU, dropout (as the kernel above)
-    {
-      const int r = tid >> 4, c16 = tid & 15;
-      const int64_t row = s_rec[kRecRow + r];
-      float4 z[NTQ];
-#pragma unroll
-      for (int u = 0; u < NTQ; ++u)
-        z[u] = c16 + 16 * u < Q ? *reinterpret_cast<const float4*>(s_Z + r * Fz + 4 * (c16 + 16 * u))
-                                : make_float4(0.f, 0.f, 0.f, 0.f);
-      const int2* it = reinterpret_cast<const int2*>(s_rec + kRecHead);
-      const int k1 = s_rec[r + 1];
-#pragma unroll 2
-      for (int k = s_rec[r]; k < k1; ++k) {
-        const int2 p = it[k];
-        const float v = __int_as_float(p.y);
-        const float* srow = s_S + p.x * F + 4 * c16;
-        float4 sv[NTQ];
-#pragma unroll
-        for (int u = 0; u < NTQ; ++u)
-          sv[u] = c16 + 16 * u < Q ? *reinterpret_cast<const float4*>(srow + 64 * u) : make_float4(0.f, 0.f, 0.f, 0.f);
-#pragma unroll
-        for (int u = 0; u < NTQ; ++u) Vec<4>::fma(z[u], v, sv[u]);
-      }
-      if (row >= 0) {
-        const bool plain = a.epi.code == GCNK_EPI_BIAS_RELU;
-#pragma unroll
-        for (int u = 0; u < NTQ; ++u) {
-          const int q = c16 + 16 * u;
-          if (q < Q) {
-            const float4 bv = *reinterpret_cast<const float4*>(s_bias + 4 * q);
-            float4 h;
-            if (plain) {
-              h.x = fmaxf(z[u].x + bv.x, 0.f); h.y = fmaxf(z[u].y + bv.y, 0.f);
-              h.z = fmaxf(z[u].z + bv.z, 0.f); h.w = fmaxf(z[u].w + bv.w, 0.f);
-            } else {
-              h = Vec<4>::epi(a.epi, z[u], bv, row, 4 * (int64_t)q);
-            }
-            if (a.H) Vec<4>::store(a.H + row * a.ldh + 4 * q, h);
-            *reinterpret_cast<float4*>(s_Z + r * Fz + 4 * q) = h;
-          }
-        }
-      }
-    }
-    __syncthreads();
-
-    // ---- 3. S2 = H1 W2 (as the kernel above)
-    f32x4 pc[NP];
-    {
-      const int n = lane & 15;
-      constexpr int kq = Fp / 16;
-      float av[kq];
-#pragma unroll
-      for (int j = 0; j < kq; ++j) {
-        const int k = 4 * (quarter * kq + j) + (lane >> 4);
-        av[j] = k < F ? s_Z[(16 * strip + (lane & 15)) * Fz + k] : 0.f;
-      }
-#pragma unroll
-      for (int t = 0; t < NP; ++t) {
-        float bw[kq];
-#pragma unroll
-        for (int j = 0; j < kq; ++j) {
-          const int k = 4 * (quarter * kq + j) + (lane >> 4);
-          bw[j] = (k < F && 16 * t + n < a.P) ? s_W2[k * a.P + 16 * t + n] : 0.f;
-        }
-        f32x4 p0 = f32x4{0.f, 0.f, 0.f, 0.f}, p1 = p0;
-#pragma unroll
-        for (int j = 0; j < kq; j += 2) {
-          p0 = __builtin_amdgcn_mfma_f32_16x16x4f32(av[j], bw[j], p0, 0, 0, 0);
-          p1 = __builtin_amdgcn_mfma_f32_16x16x4f32(av[j + 1], bw[j + 1], p1, 0, 0, 0);
-        }
-        pc[t] = p0 + p1;
-      }
-    }
-    if (quarter > 0)
-#pragma unroll
-      for (int t = 0; t < NP; ++t)
-        *reinterpret_cast<f32x4*>(s_red + (((t * 3 + quarter - 1) * 2 + strip) * 64 + lane) * 4) = pc[t];
-    __syncthreads();
-    if (quarter == 0) {
-#pragma unroll
-      for (int t = 0; t < NP; ++t) {
-#pragma unroll
-        for (int qq = 0; qq < 3; ++qq)
-          pc[t] += *reinterpret_cast<const f32x4*>(s_red + (((t * 3 + qq) * 2 + strip) * 64 + lane) * 4);
-        const int p = 16 * t + (lane & 15);
-#pragma unroll
-        for (int r = 0; r < 4; ++r) {
-          const int64_t row = s_rec[kRecRow + 16 * strip + (lane >> 4) * 4 + r];
-          if (row >= 0 && p < a.P) a.C2[row * a.ldc2 + p] = pc[t][r];
-        }
-      }
-    }
-    __syncthreads();  // s_Z / s_red (and this s_rec) are rewritten by the next blocks
-    if (blk == (int)blockIdx.x) stamp(a.epi, 2);
-#pragma unroll
-    for (int s2 = 0; s2 < KS; ++s2) af[s2] = af_next[s2];
-  }
-  stamp(a.epi, 3);
-}
-
 
 // Debug/test aid: every workgroup fills the whole 160 KiB of LDS with `word`.
 // LDS is not cleared between workgroups, so a kernel launched next on the same
@@ -514,46 +298,10 @@ extern "C" int64_t gcnk_hubfactor_lds_bytes(int32_t F, int32_t Kc, int32_t nhub,
   return hubfactor_lds_bytes(F, Kc, nhub, rec_words, P);
 }
 
-static int64_t persist_lds_bytes(int32_t F, int32_t Kc, int32_t nhub, int32_t rec_words, int32_t P) {
-  const int64_t x = std::max<int64_t>((int64_t)Kc * F, (int64_t)kRB * zstride_p(F) + sred_floats_p(pick_np(P)));
-  return 4 * ((int64_t)nhub * F + (((int64_t)F * P + 3) & ~3LL) + ((F + 3) & ~3) + 2 * (int64_t)rec_words + x);
-}
-
-// CUs of the current device (cached per device id)
-static int device_cus() {
-  static int cus[64] = {0};
-  int dev = 0;
-  if (hipGetDevice(&dev) != hipSuccess || dev < 0 || dev >= 64) return 256;
-  if (cus[dev] == 0) {
-    int n = 0;
-    if (hipDeviceGetAttribute(&n, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || n <= 0) n = 256;
-    cus[dev] = n;
-  }
-  return cus[dev];
-}
-
 // The dynamic-LDS limit is raised once per kernel instantiation (a driver call
-// per launch cost host time on every eager forward), then the launch.  More
-// blocks than one workgroup per CU: the persistent kernel (operands staged
-// once per workgroup), when its LDS fits.
+// per launch cost host time on every eager forward), then the launch.
 template <int KS, int NTQ, int NP>
 static int launch_factor(const FactorArgs& a, int64_t nblk, int64_t lds_b, void* stream) {
-  const int cus = device_cus();
-  const int64_t lds_p = persist_lds_bytes(a.F, a.Kc, a.nhub, a.rec_words, a.P);
-  if (nblk > cus && lds_p <= 160 * 1024) {
-    static const hipError_t attr_p = hipFuncSetAttribute(
-        reinterpret_cast<const void*>(&hubfactor_gc1_persist_kernel<KS, NTQ, NP>),
-        hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
-    if (attr_p != hipSuccess) return hip_check(attr_p, "hubfactor_gc1_persist_kernel LDS attribute");
-    const int64_t per_cu = lds_p <= 80 * 1024 ? 2 : 1;
-#ifndef GCNK_PERSIST_WGS
-#define GCNK_PERSIST_WGS 0
-#endif
-    const int64_t grid = std::min<int64_t>(nblk, GCNK_PERSIST_WGS > 0 ? GCNK_PERSIST_WGS : per_cu * cus);
-    hipLaunchKernelGGL((hubfactor_gc1_persist_kernel<KS, NTQ, NP>), dim3((unsigned)grid), dim3(kThreads),
-                       (size_t)lds_p, reinterpret_cast<hipStream_t>(stream), a);
-    return launch_check("hubfactor_gc1_persist_kernel");
-  }
   static const hipError_t attr = hipFuncSetAttribute(reinterpret_cast<const void*>(&hubfactor_gc1_kernel<KS, NTQ, NP>),
                                                      hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
   if (attr != hipSuccess) return hip_check(attr, "hubfactor_gc1_kernel LDS attribute");

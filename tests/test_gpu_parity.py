@@ -1103,7 +1103,7 @@ def test_factored_gc1_kernel_against_float64(F, P, ndoc):
     xop = ops.Operand(X)
     f = factor.get(as_csr(A), xop)
     assert f is not None
-    # 12,000 documents: more 32-row blocks (376) than CUs -- the persistent kernel
+    # 12,000 documents: more 32-row blocks (377) than CUs (several rounds of workgroups)
     assert not np.array_equal(f.perm.numpy(), np.arange(f.M))   # the hub rows moved
     rng = np.random.default_rng(3)
     W1 = torch.from_numpy(rng.standard_normal((g["nfeat"], F)).astype(np.float32)).to(DEV)

@@ -3,13 +3,11 @@
 cd "${GRAFT_REPO_ROOT:-/root/repo}" || exit 2
 export TMPDIR=/tmp
 mkdir -p gpurun_out/r04
-for v in product wb512 hu8 wb512hu8; do
+for v in product hu12w4 hu8w4; do
   lib=""; [ $v != product ] && lib="GCNK_LIB=$PWD/_variants/libgcnk_$v.so"
-  env $lib timeout -k 10 200 python -u scripts/hub_probe.py --variants row,topic --widths 200 --ipc 12,16,24,32 --reps 200 --mode cold > gpurun_out/r04/sweep_$v.log 2>&1; echo "$v rc=$?"
+  env $lib timeout -k 10 200 python -u scripts/hub_probe.py --variants row,topic --widths 200 --ipc 12,16 --reps 200 --mode cold > gpurun_out/r04/sweep_$v.log 2>&1; echo "$v rc=$?"
   grep "^{" gpurun_out/r04/sweep_$v.log | python3 -c "
 import sys, json
 for l in sys.stdin:
     d = json.loads(l); print('$v', d['variant'], d['ipc'], d['cold_us'], d['max_err'] < 1e-5, d['deterministic'])"
 done
-GCNK_STAMP_GRAPH=20ng GCNK_LIB=$PWD/_variants/libgcnk_stamps.so timeout -k 10 120 python -u scripts/factor_stamps.py > gpurun_out/r04/factorstamps20p.log 2>&1; echo "factorstamps20 rc=$?"
-grep "^{" gpurun_out/r04/factorstamps20p.log | cut -c1-1500

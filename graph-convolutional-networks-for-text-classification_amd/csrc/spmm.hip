@@ -109,14 +109,6 @@ constexpr int kRowU = GCNK_ROW_U;            // gathers in flight per lane for l
 // Not for 1-4 lanes (one-wave workgroups spread the light rows over the chip;
 // 256-thread ones measured 5.64 -> 6.14 us at F = 8).
 constexpr bool kNarrowWG = GCNK_NARROW_WG != 0;
-// Light-row windows (whole-wavefront plans): each light wavefront's rows and
-// items stored together as 64 int2 {row ids | counts | items}, read by one
-// vector load that depends on nothing -- the unit -> items -> gathers chain of
-// the light rows loses a dependent memory round trip.
-#ifndef GCNK_LIGHT_WIN
-#define GCNK_LIGHT_WIN 0
-#endif
-constexpr bool kLightWin = GCNK_LIGHT_WIN != 0;
 constexpr int kWaveBlock = GCNK_WAVE_BLOCK;  // workgroup size for whole-wavefront groups
 constexpr int kLightRPW = GCNK_LIGHT_RPW;    // light rows per wavefront with whole-wavefront groups
 constexpr int kLightMax64 = 64 / kLightRPW;  // their nonzero limit (kLightRPW rows' items fill one 64-lane load)
@@ -137,16 +129,14 @@ constexpr int kLightMax64 = 64 / kLightRPW;  // their nonzero limit (kLightRPW r
 //   diagonal float[64 * ntblk] in block order).
 struct Layout {
   int64_t M, nnz, nunits, nhunits, nheavy, nslots, ntile, nred, ntblk, has_diag;
-  int64_t items, units, heavy, lwin, nlw, tdesc, tcols, tfrag, red, trows, dval, total;
+  int64_t items, units, heavy, tdesc, tcols, tfrag, red, trows, dval, total;
   __host__ __device__ explicit Layout(const int32_t* h) {
     M = h[1]; nunits = h[5]; nhunits = h[6]; nheavy = h[7]; ntile = h[8]; nred = h[9]; ntblk = h[11];
     has_diag = h[12]; nnz = h[13]; nslots = h[14];
     items = 16;
     units = (items + 2 * nnz + 3) & ~3LL;
     heavy = units + 4 * nunits;
-    lwin = (heavy + 4 * nheavy + 3) & ~3LL;
-    nlw = (kLightWin && h[3] == 1) ? (nunits - nhunits) / kLightRPW : 0;  // light wavefronts (64-lane groups)
-    tdesc = lwin + 2 * 64 * nlw;
+    tdesc = (heavy + 4 * nheavy + 3) & ~3LL;
     tcols = tdesc + 4 * ntile;
     tfrag = (tcols + (int64_t)kKC * ntile + 3) & ~3LL;
     red = tfrag + (int64_t)kRB * kKC * ntile;
@@ -393,9 +383,6 @@ struct RowPlan {
   int32_t* cnt;        // per heavy row x column tile: arrival counters, in the caller's
                        // counter region (zero on entry, re-armed by each row's last arriver)
   int32_t nunits, nhunits;
-  const int2* lwin;    // light-row windows (kLightWin): per light wavefront 64 int2
-                       // {row 0, row 1} | {count 0, count 1} | items of row 0, then row 1
-  int32_t nlw;
 };
 
 // Partial slots are written and read with agent-coherent accesses (the sc1
@@ -612,35 +599,18 @@ spmm_row_kernel(RowPlan rp, int32_t nhb, const float* __restrict__ B, int64_t ld
       int4 un[R];
       int32_t nb[R + 1];  // item prefix offsets of the R rows (wave-uniform)
       nb[0] = 0;
-      const int lane = tid & 63;
-      int2 mine;
-      int32_t i0 = 0;     // lane of the wavefront's first item
-      if constexpr (kLightWin) {
-        // one load: rows, counts and items of the wavefront (no unit load before it)
-        const int32_t lw = (u0 - rp.nhunits) / R;
-        mine = lw < rp.nlw ? rp.lwin[(int64_t)lw * 64 + lane] : make_int2(-1, 0);
-        __builtin_amdgcn_s_waitcnt(0x0F70);  // vmcnt(0): the window has landed (see gather_rows_wave)
-        const int32_t rows[2] = {__builtin_amdgcn_readlane(mine.x, 0), __builtin_amdgcn_readlane(mine.y, 0)};
-        const int32_t cnts[2] = {__builtin_amdgcn_readlane(mine.x, 1), __builtin_amdgcn_readlane(mine.y, 1)};
 #pragma unroll
-        for (int r = 0; r < R; ++r) {
-          un[r] = make_int4(lw < rp.nlw ? rows[r] : -1, 0, 0, -1);
-          nb[r + 1] = nb[r] + (un[r].x >= 0 ? cnts[r] : 0);
-        }
-        i0 = 2;
-      } else {
-#pragma unroll
-        for (int r = 0; r < R; ++r) {
-          un[r] = u0 + r < rp.nunits ? rp.units[u0 + r] : make_int4(-1, 0, 0, -1);
-          nb[r + 1] = nb[r] + (un[r].x >= 0 ? un[r].z - un[r].y : 0);
-        }
-        int32_t k = -1;
-#pragma unroll
-        for (int r = 0; r < R; ++r)
-          if (lane >= nb[r] && lane < nb[r + 1]) k = un[r].y + lane - nb[r];
-        mine = k >= 0 ? rp.items[k] : make_int2(-1, 0);
+      for (int r = 0; r < R; ++r) {
+        un[r] = u0 + r < rp.nunits ? rp.units[u0 + r] : make_int4(-1, 0, 0, -1);
+        nb[r + 1] = nb[r] + (un[r].x >= 0 ? un[r].z - un[r].y : 0);
       }
       stamp(epi, 1);
+      const int lane = tid & 63;
+      int32_t k = -1;
+#pragma unroll
+      for (int r = 0; r < R; ++r)
+        if (lane >= nb[r] && lane < nb[r + 1]) k = un[r].y + lane - nb[r];
+      const int2 mine = k >= 0 ? rp.items[k] : make_int2(-1, 0);
       const uint32_t ldb4 = (uint32_t)ldb * 4u, col4 = colok ? (uint32_t)colv * 4u : 0u;
       const int64_t colc = colok ? colv : 0;  // idle lanes read inside the row (no branch around the load)
       T accs[R];
@@ -655,8 +625,8 @@ spmm_row_kernel(RowPlan rp, int32_t nhb, const float* __restrict__ B, int64_t ld
           g[j] = V::zero();
           a[j] = 0.f;
           if (j0 + j < cnt) {
-            const int32_t c = __builtin_amdgcn_readlane(mine.x, i0 + j0 + j);
-            a[j] = __int_as_float(__builtin_amdgcn_readlane(mine.y, i0 + j0 + j));
+            const int32_t c = __builtin_amdgcn_readlane(mine.x, j0 + j);
+            a[j] = __int_as_float(__builtin_amdgcn_readlane(mine.y, j0 + j));
             g[j] = load_row<VEC, O32>(B, ldb, ldb4, c, colc, col4);
           }
         }
@@ -1482,10 +1452,7 @@ int host_plan(const int32_t* rp, const int32_t* ci, const float* vv, int32_t M, 
   // light-row limit: 2 * ipc for whole-wavefront groups (two light rows share a
   // wavefront, at most kLightMax64 nonzeros each; a heavy row is walked by a
   // 4-wavefront workgroup), ipc otherwise
-  // (windows hold 62 items of a wavefront's kLightRPW rows)
-  const int64_t light_max = lpr == 64 ? std::min<int64_t>(std::min<int64_t>(2 * (int64_t)ipc, kLightMax64),
-                                                          kLightWin ? 62 / kLightRPW : kLightMax64)
-                                      : ipc;
+  const int64_t light_max = lpr == 64 ? std::min<int64_t>(2 * (int64_t)ipc, kLightMax64) : ipc;
   const int lpb = lpr == 64 ? sg * kLightRPW : sg;  // light units per workgroup
   // XCD classes.  Workgroups b and b + 8 land on one XCD (round-robin dispatch;
   // speed only, never correctness), so every unit of workgroup b is given
@@ -1638,22 +1605,6 @@ void classic_image(const HostPlan& hp, const int32_t* ci, const float* vv, int64
   };
   put(L.units, hp.units.data(), hp.units.size());
   put(L.heavy, hp.heavy.data(), hp.heavy.size());
-  // light-row windows: wavefront w's kLightRPW units, their counts and items
-  static_assert(!kLightWin || kLightRPW == 2, "light windows hold two rows per wavefront");
-  for (int64_t w = 0; w < L.nlw; ++w) {
-    const int64_t base = L.lwin + 2 * 64 * w;
-    int64_t n = 2;
-    for (int r = 0; r < kLightRPW; ++r) {
-      const int32_t* u = hp.units.data() + 4 * (L.nhunits + w * kLightRPW + r);
-      const int32_t cnt = u[0] >= 0 ? u[2] - u[1] : 0;
-      img[(size_t)(base + r)] = u[0];            // slot 0: {row 0, row 1}
-      img[(size_t)(base + 2 + r)] = cnt;         // slot 1: {count 0, count 1}
-      for (int32_t k = u[1]; u[0] >= 0 && k < u[2]; ++k, ++n) {
-        img[(size_t)(base + 2 * n)] = ci[k];
-        img[(size_t)(base + 2 * n + 1)] = vv ? __builtin_bit_cast(int32_t, vv[k]) : 0;
-      }
-    }
-  }
   put(L.tdesc, hp.tdesc.data(), hp.tdesc.size());
   put(L.tcols, hp.tcols.data(), hp.tcols.size());
   putf(L.tfrag, hp.tfrag);
@@ -1961,8 +1912,7 @@ static int spmm_impl(const void* plan, const int32_t* hdr, const float* B, int64
   // ---- remaining rows: row kernel (heavy rows finished in-launch)
   if (L.nunits > 0 && part != 1) {
     RowPlan rp{reinterpret_cast<const int2*>(p + L.items), reinterpret_cast<const int4*>(p + L.units),
-               reinterpret_cast<const int4*>(p + L.heavy), counters, (int32_t)L.nunits, (int32_t)L.nhunits,
-               reinterpret_cast<const int2*>(p + L.lwin), (int32_t)L.nlw};
+               reinterpret_cast<const int4*>(p + L.heavy), counters, (int32_t)L.nunits, (int32_t)L.nhunits};
     RowLaunch a{rp, K, B, ldb, F, C, ldc, e, workspace, part_ld, pa, s};
     if (proj) return pa.P <= 8 ? dispatch_rows_proj<8>(lpr, a) : dispatch_rows_proj<32>(lpr, a);
     return vec4 ? dispatch_rows<4>(lpr, a) : dispatch_rows<1>(lpr, a);

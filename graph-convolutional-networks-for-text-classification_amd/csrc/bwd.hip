@@ -47,6 +47,11 @@ struct VecIO<4> {
   static __device__ __forceinline__ void store(float* p, const float (&v)[4]) {
     *reinterpret_cast<float4*>(p) = make_float4(v[0], v[1], v[2], v[3]);
   }
+  // streaming store (gZ1: written once, read by the next launch)
+  static __device__ __forceinline__ void store_nt(float* p, const float (&v)[4]) {
+    typedef float f4a __attribute__((ext_vector_type(4), aligned(16)));
+    __builtin_nontemporal_store(f4a{v[0], v[1], v[2], v[3]}, reinterpret_cast<f4a*>(p));
+  }
 };
 template <>
 struct VecIO<2> {
@@ -57,11 +62,16 @@ struct VecIO<2> {
   static __device__ __forceinline__ void store(float* p, const float (&v)[2]) {
     *reinterpret_cast<float2*>(p) = make_float2(v[0], v[1]);
   }
+  static __device__ __forceinline__ void store_nt(float* p, const float (&v)[2]) {
+    __builtin_nontemporal_store(v[0], p);
+    __builtin_nontemporal_store(v[1], p + 1);
+  }
 };
 template <>
 struct VecIO<1> {
   static __device__ __forceinline__ void load(const float* p, float (&v)[1]) { v[0] = *p; }
   static __device__ __forceinline__ void store(float* p, const float (&v)[1]) { *p = v[0]; }
+  static __device__ __forceinline__ void store_nt(float* p, const float (&v)[1]) { __builtin_nontemporal_store(v[0], p); }
 };
 
 struct Bwd2Args {
@@ -161,7 +171,7 @@ __global__ void __launch_bounds__(kBwdBlock) gcn_bwd2_kernel(Bwd2Args a) {
 #pragma unroll
         for (int p = 0; p < PM; ++p) gw[v][p] = fmaf(h[j][v], g[p], gw[v][p]);
       }
-      VecIO<VEC>::store(a.Z + (int64_t)(r0 + rr) * a.ldz + c, z);
+      VecIO<VEC>::store_nt(a.Z + (int64_t)(r0 + rr) * a.ldz + c, z);
     }
   }
 

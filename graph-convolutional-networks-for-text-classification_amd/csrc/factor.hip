@@ -202,7 +202,10 @@ hubfactor_gc1_kernel(FactorArgs a) {
           } else {
             h = Vec<4>::epi(a.epi, z[u], bv, row, 4 * (int64_t)q);
           }
-          if (a.H) Vec<4>::store(a.H + row * a.ldh + 4 * q, h);
+          if (a.H) {  // H1 for the backward: streaming store (no dirty L2 lines at the kernel's end)
+            typedef float f4a __attribute__((ext_vector_type(4), aligned(16)));
+            __builtin_nontemporal_store(f4a{h.x, h.y, h.z, h.w}, reinterpret_cast<f4a*>(a.H + row * a.ldh + 4 * q));
+          }
           *reinterpret_cast<float4*>(s_Z + r * Fz + 4 * q) = h;
         }
       }

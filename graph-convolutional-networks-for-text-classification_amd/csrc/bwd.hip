@@ -84,6 +84,7 @@ struct Bwd2Args {
   float* Z; int64_t ldz;
   float* part; int64_t part_ld;   // per workgroup row: gW2 [N*P] | gb1 [N] | gb2 [P]
   int32_t rpb;                    // rows per workgroup
+  Epi stamps;                     // (debug timeline of a -DGCNK_STAMPS build only: .stamps)
 };
 
 template <int VEC, int PM>
@@ -104,6 +105,7 @@ __global__ void __launch_bounds__(kBwdBlock) gcn_bwd2_kernel(Bwd2Args a) {
   const int32_t nr = min(a.M - r0, a.rpb);
   const bool with_g = a.G != nullptr && blockIdx.y == 0;
   const bool colok = act && c < a.N;  // VEC columns all valid (N % VEC == 0 on the vector paths)
+  stamp(a.stamps, 0);   // (stamps build: 0 entry, 1 operands staged, 2 rows done, 3 partial stored)
 
   // the first batch's H1 rows: in flight together with the staging loads below
   float h[kBwdBatch][VEC];
@@ -136,6 +138,7 @@ __global__ void __launch_bounds__(kBwdBlock) gcn_bwd2_kernel(Bwd2Args a) {
     for (int p = 0; p < PM; ++p) gw[v][p] = 0.f;
   }
   __syncthreads();
+  stamp(a.stamps, 1);
 
   for (int32_t b0 = rl; b0 < nr; b0 += RL * kBwdBatch) {
     // the batch's H1 loads first (one latency; the first batch's are in flight
@@ -175,6 +178,7 @@ __global__ void __launch_bounds__(kBwdBlock) gcn_bwd2_kernel(Bwd2Args a) {
     }
   }
 
+  stamp(a.stamps, 2);
   // row lanes -> one partial per column, summed in lane order
   {
     float* mine = s_red + tid * KE;
@@ -205,6 +209,7 @@ __global__ void __launch_bounds__(kBwdBlock) gcn_bwd2_kernel(Bwd2Args a) {
     for (int rr = 0; rr < nr; ++rr) s += s_gg[rr * PM + tid];
     prow[(int64_t)a.N * a.P + a.N + tid] = s;
   }
+  stamp(a.stamps, 3);
 }
 
 // out[e] = sum over workgroups of part[b][e], b in order: 16 entries x 16
@@ -301,7 +306,8 @@ extern "C" int gcnk_gcn_bwd2_f32(const float* H, int64_t ldh, const float* gS, i
     set_error("gcnk_gcn_bwd2_f32: workspace %lld B < %lld B", (long long)workspace_bytes, (long long)need);
     return GCNK_EARG;
   }
-  Bwd2Args a{H, ldh, gS, ldgs, W, ldw, G, ldg, M, N, P, scale, Z, ldz, (float*)workspace, g.part_ld, g.rpb};
+  Bwd2Args a{H, ldh, gS, ldgs, W, ldw, G, ldg, M, N, P, scale, Z, ldz, (float*)workspace, g.part_ld, g.rpb, Epi{}};
+  a.stamps.stamps = debug_stamps();
   hipStream_t s = (hipStream_t)stream;
   const dim3 grid((unsigned)g.nblk, (unsigned)g.slices);
 #define GCNK_BWD2(V_, PM_) hipLaunchKernelGGL((gcn_bwd2_kernel<V_, PM_>), grid, dim3(kBwdBlock), 0, s, a)

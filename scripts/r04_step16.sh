@@ -1,0 +1,11 @@
+#!/bin/bash
+# round 4: streaming stores for H1 (hubfactor, training) and gZ1 (gcn_bwd2): training step and parity
+cd "${GRAFT_REPO_ROOT:-/root/repo}" || exit 2
+export TMPDIR=/tmp
+mkdir -p gpurun_out/r04
+timeout -k 10 300 python -u -m pytest tests/test_gpu_parity.py -m gpu -p no:cacheprovider -x -q --timeout 120 --timeout-method thread -k "bwd2 or factor or record or train or 20ng" > gpurun_out/r04/pytest_14.log 2>&1; echo "pytest rc=$?"; tail -2 gpurun_out/r04/pytest_14.log
+timeout -k 10 300 python -u scripts/bench_train.py --steps 50 --cpu-steps 0 > gpurun_out/r04/train_nt.log 2>&1; echo "train rc=$?"; grep "^{" gpurun_out/r04/train_nt.log | cut -c1-200
+timeout -k 10 300 python -u scripts/eager_fwd_profile.py > gpurun_out/r04/eager_nt.log 2>&1; echo "eager rc=$?"; grep -E "eager" gpurun_out/r04/eager_nt.log
+mkdir -p gpurun_out/r04
+GCNK_LIB=$PWD/_variants/libgcnk_stamps.so timeout -k 10 120 python -u scripts/bwd2_stamps.py > gpurun_out/r04/bwd2_stamps.log 2>&1; echo "stamps rc=$?"
+grep "^{" gpurun_out/r04/bwd2_stamps.log

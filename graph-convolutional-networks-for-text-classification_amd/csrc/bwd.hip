@@ -197,8 +197,16 @@ __global__ void __launch_bounds__(kBwdBlock) gcn_bwd2_kernel(Bwd2Args a) {
     const int u = e / KE, k = e % KE;
     const int v = k / (PM + 1), p = k % (PM + 1);
     const int64_t col = (int64_t)(cu0 + u) * VEC + v;
+    // the row lanes' values eight at a time (loads together), added in lane order
     float s = 0.f;
-    for (int l = 0; l < RL; ++l) s += s_red[(l * CT + u) * KE + k];
+    for (int l0 = 0; l0 < RL; l0 += 8) {
+      float rv[8];
+#pragma unroll
+      for (int j = 0; j < 8; ++j) rv[j] = l0 + j < RL ? s_red[((l0 + j) * CT + u) * KE + k] : 0.f;
+#pragma unroll
+      for (int j = 0; j < 8; ++j)
+        if (l0 + j < RL) s += rv[j];
+    }
     if (col >= a.N) continue;
     if (p < PM) {
       if (p < a.P) prow[col * a.P + p] = s;
@@ -206,9 +214,16 @@ __global__ void __launch_bounds__(kBwdBlock) gcn_bwd2_kernel(Bwd2Args a) {
       prow[(int64_t)a.N * a.P + col] = s;
     }
   }
-  if (with_g && tid < a.P) {  // gb2: the G rows, in row order
+  if (with_g && tid < a.P) {  // gb2: the G rows, in row order (eight LDS reads in flight)
     float s = 0.f;
-    for (int rr = 0; rr < nr; ++rr) s += s_gg[rr * PM + tid];
+    for (int r8 = 0; r8 < nr; r8 += 8) {
+      float gv[8];
+#pragma unroll
+      for (int j = 0; j < 8; ++j) gv[j] = r8 + j < nr ? s_gg[(r8 + j) * PM + tid] : 0.f;
+#pragma unroll
+      for (int j = 0; j < 8; ++j)
+        if (r8 + j < nr) s += gv[j];
+    }
     prow[(int64_t)a.N * a.P + a.N + tid] = s;
   }
   stamp(a.stamps, 3);

@@ -34,7 +34,10 @@ constexpr int kBwdBlock = 256;
 constexpr int kBwdCols = 256;      // columns per workgroup slice
 constexpr int kBwdRowsMax = 256;   // rows per workgroup (LDS staging of gS2 / G)
 constexpr int kBwdBatch = 8;       // rows per lane whose H1 loads are in flight together
-constexpr int kBwdTarget = 256;    // workgroups per slice (one per CU)
+#ifndef GCNK_BWD_TARGET
+#define GCNK_BWD_TARGET 256
+#endif
+constexpr int kBwdTarget = GCNK_BWD_TARGET;    // workgroups per slice (256: one per CU)
 
 template <int VEC>
 struct VecIO;

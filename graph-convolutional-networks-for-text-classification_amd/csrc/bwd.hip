@@ -120,21 +120,20 @@ __global__ void __launch_bounds__(kBwdBlock) gcn_bwd2_kernel(Bwd2Args a) {
 #pragma unroll
       for (int v = 0; v < VEC; ++v) h[j][v] = 0.f;
   }
-  // this lane's columns of W2 (rows of W2: W2[n, :]), issued before the staging
-  // below waits for its loads (one round of latency for all of them; the
-  // timeline showed two, profiles/r04_bwd2_stamps.log)
-  float w[VEC][PM];
-#pragma unroll
-  for (int v = 0; v < VEC; ++v)
-#pragma unroll
-    for (int p = 0; p < PM; ++p)
-      w[v][p] = (act && c + v < a.N && p < a.P) ? a.W[(c + v) * a.ldw + p] : 0.f;
   // gS2 (and G) rows of the workgroup -> LDS, padded to PM columns with zeros
   for (int i = tid; i < nr * PM; i += kBwdBlock) {
     const int rr = i / PM, p = i % PM;
     s_g[i] = p < a.P ? a.gS[(int64_t)(r0 + rr) * a.ldgs + p] : 0.f;
     if (with_g) s_gg[i] = p < a.P ? a.G[(int64_t)(r0 + rr) * a.ldg + p] : 0.f;
   }
+  // this lane's columns of W2 (rows of W2: W2[n, :]).  (Issued before the
+  // staging above instead: staging 2.7 -> 4.2 us, profiles/r04_bwd2_stamps_v2.log.)
+  float w[VEC][PM];
+#pragma unroll
+  for (int v = 0; v < VEC; ++v)
+#pragma unroll
+    for (int p = 0; p < PM; ++p)
+      w[v][p] = (act && c + v < a.N && p < a.P) ? a.W[(c + v) * a.ldw + p] : 0.f;
   float gw[VEC][PM], gb[VEC];
 #pragma unroll
   for (int v = 0; v < VEC; ++v) {

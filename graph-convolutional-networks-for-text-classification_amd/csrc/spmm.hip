@@ -74,15 +74,13 @@ constexpr int kMaxSeg = 64;             // segments per heavy row (bounds the la
 #ifndef GCNK_TILE_PHASES
 #define GCNK_TILE_PHASES 2
 #endif
-#ifndef GCNK_ROW_SC1
-#define GCNK_ROW_SC1 0
-#endif
 // Nontemporal (streaming) output stores of the row kernel's finished rows: the
 // launch leaves no dirty output lines in the XCD L2s for the end-of-kernel
 // write-back.  R8 A-hat S1, F = 200, cold (HIP events per call,
 // profiles/r04_probe_nt.log): 9.46 -> 8.16 us, document rows alone 8.16 ->
 // 6.95, topic rows alone 9.05 -> 7.78 (a cold 12.4 MB copy: 4.35 -> 3.25 us,
-// scripts/micro/ns_micro.hip).
+// scripts/micro/ns_micro.hip).  Write-through (sc1) stores measured 9.06 us
+// there (removed).
 #ifndef GCNK_ROW_NT
 #define GCNK_ROW_NT 1
 #endif
@@ -332,13 +330,7 @@ struct Proj {
 #pragma unroll
         for (int c = 0; c < NR; ++c)
           if (chan + c < pa.P) {
-#if GCNK_ROW_SC1
-            const int64_t off = row * pa.ldc2 + chan + c;
-            if (off < ((int64_t)1 << 29)) store_coherent_v(pa.C2, off, s[c]);  // C2: kernel argument (uniform)
-            else pa.C2[off] = s[c];
-#else
             pa.C2[row * pa.ldc2 + chan + c] = s[c];
-#endif
           }
       }
     }
@@ -532,13 +524,7 @@ __device__ __forceinline__ void finish_row(const typename Vec<VEC>::T& acc, int3
   using V = Vec<VEC>;
   using T = typename V::T;
   const T h = colok ? V::epi(epi, acc, bv, r, colv) : V::zero();
-#if GCNK_ROW_SC1
-  if (colok && store_main) {
-    const int64_t off = (int64_t)r * ldc + colv;
-    if (off < ((int64_t)1 << 29)) store_coherent_v(C, off, h);  // C: the kernel argument (uniform)
-    else V::store(C + off, h);
-  }
-#elif GCNK_ROW_NT
+#if GCNK_ROW_NT
   if (colok && store_main) store_nt(C + (int64_t)r * ldc + colv, h);
 #else
   if (colok && store_main) V::store(C + (int64_t)r * ldc + colv, h);

@@ -84,8 +84,13 @@ constexpr int kMaxSeg = 64;             // segments per heavy row (bounds the la
 #ifndef GCNK_ROW_NT
 #define GCNK_ROW_NT 1
 #endif
+// Light rows per wavefront (whole-wavefront groups).  Round 4, with the
+// nontemporal stores and the gather-wait fix, cold R8 A-hat F = 200
+// (profiles/r04_sweep2_*.log): one row per wavefront takes the document rows
+// alone from 6.95 to 5.27 us and the launch from 8.30 to 8.14 (the topic rows,
+// 7.76 alone, now bound it); two rows had measured even in round 1.
 #ifndef GCNK_LIGHT_RPW
-#define GCNK_LIGHT_RPW 2
+#define GCNK_LIGHT_RPW 1
 #endif
 #ifndef GCNK_HEAVY_U
 #define GCNK_HEAVY_U 4

@@ -92,8 +92,15 @@ constexpr int kMaxSeg = 64;             // segments per heavy row (bounds the la
 #ifndef GCNK_LIGHT_RPW
 #define GCNK_LIGHT_RPW 1
 #endif
+// Gathers in flight per lane in a heavy segment.  With one light row per
+// wavefront the kernel holds 6 under its 64-VGPR cap (8 spills 16 B/lane, 12
+// spills 148): a 12-item segment is two batches of 6 instead of three of 4.
+// Cold R8 A-hat F = 200 (scripts/r04_step19.sh, four runs each, the last in
+// profiles/r04_sweep3_*.log): 8.10-8.15 -> 7.90-7.97 us; R8 F = 8
+// unchanged (5.47-5.50), the 20ng-shaped graph at F = 200 12.6 -> 12.8
+// (profiles/r04_hu_*.log).
 #ifndef GCNK_HEAVY_U
-#define GCNK_HEAVY_U 4
+#define GCNK_HEAVY_U 6
 #endif
 #ifndef GCNK_WAVE_BLOCK
 #define GCNK_WAVE_BLOCK 256

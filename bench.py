@@ -292,8 +292,11 @@ def labelled_forward_kernels(save_dir, graph, a_csr, x, N, nfeat, nnz_a, nnz_x, 
     if fac is not None:
         # hub-factored gc1 (factor.py): X[hubs] W1 (tile SpMM or dense GEMM), then one
         # launch reading U [N x Kc], the A_H records, W1[Kc], S_T, W2 and writing S2
-        x_hub_nnz = fac.x_hub.nnz if fac.x_hub is not None else fac.H * nfeat
-        alg = {"X_hubs W1": spmm_bytes(fac.H, nfeat, x_hub_nnz, nhid),
+        if fac.x_hub_dense is not None:   # the small-M split-K GEMM on the dense hub rows
+            xw = 4 * (fac.H * nfeat + nfeat * nhid + fac.H * nhid)
+        else:
+            xw = spmm_bytes(fac.H, nfeat, fac.x_hub.nnz, nhid)
+        alg = {"X_hubs W1": xw,
                "A X W1 factored + H1 W2": (4 * fac.U.numel() + 4 * fac.rec.numel() + 4 * fac.Kc * nhid
                                             + 4 * fac.H * nhid + 4 * nhid * nclass + 4 * N * nclass),
                "A S2": alg["A S2"]}

@@ -303,6 +303,129 @@ gemm_shortk_kernel(int32_t M, int32_t N, int32_t K, const float* __restrict__ A,
   }
 }
 
+// Small-M, long-K split-K GEMM (NN; M <= 64, N % 4 == 0, lda % 4 == 0,
+// ldb % 4 == 0, A and B 16-B aligned): the slabs of C = A B for the hub rows
+// of a graph whose hub feature rows are dense -- X[hubs] W1 of the factored
+// gc1 (R8: [50 x 7463] x [7463 x 200], 7.5 MB of operands).  The generic tile
+// kernel runs it as 64 x 64 tiles x 64 k-slabs (13.7 us with its reduce) and
+// the tile SpMM on the CSR of those rows 9.8 us.  Here workgroup (s, y) owns
+// k chunk s (16 * KCH deep) and columns [112 y, 112 y + 112): it stages its B
+// chunk in LDS once (every load in flight with the A loads), wave w multiplies
+// rows [16 w, 16 w + 16) by it (7 accumulators over 4 * KCH k steps, the k
+// order inside a 16-deep block permuted alike for A and B as in the skinny
+// kernel) and writes slab s of [S][M][N]; gemm_slab_reduce4_kernel sums the
+// slabs in a fixed order.  Columns of A past K (its row padding up to lda)
+// are zeroed, never multiplied.
+template <int KCH>
+__global__ void __launch_bounds__(256)
+gemm_smallm_splitk_kernel(int32_t M, int32_t N, int32_t K, const float* __restrict__ A, int64_t lda,
+                          const float* __restrict__ B, int64_t ldb, float* __restrict__ slab) {
+  constexpr int NT = 7, BN = 16 * NT, LW = BN + 4, KP = 16 * KCH, NQ = BN / 4;
+  constexpr int PT = (KP * NQ + 255) / 256;
+  __shared__ __attribute__((aligned(16))) float s_B[KP * LW];
+  const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
+  const int r = lane & 15, q = lane >> 4;
+  const int64_t k0 = (int64_t)blockIdx.x * KP;
+  const int64_t n0 = (int64_t)blockIdx.y * BN;
+  const int64_t row = 16 * w + r;
+  const bool rok = row < M;
+  float4 a[KCH];
+#pragma unroll
+  for (int c = 0; c < KCH; ++c) {
+    const int64_t k = k0 + 16 * c + 4 * q;
+    const bool ok = rok && k < K;  // lda % 4 == 0 and lda >= K: the float4 is inside the row
+    a[c] = *reinterpret_cast<const float4*>(A + (ok ? row * lda + k : 0));
+    if (!ok) a[c] = make_float4(0.f, 0.f, 0.f, 0.f);
+  }
+  float4 v[PT];
+#pragma unroll
+  for (int p = 0; p < PT; ++p) {
+    const int e = tid + 256 * p;
+    const int64_t k = k0 + e / NQ;
+    const int64_t n = n0 + 4 * (e % NQ);
+    const bool ok = e < KP * NQ && k < K && n < N;  // N % 4 == 0
+    v[p] = *reinterpret_cast<const float4*>(B + (ok ? k * ldb + n : 0));
+    if (!ok) v[p] = make_float4(0.f, 0.f, 0.f, 0.f);
+  }
+#pragma unroll
+  for (int p = 0; p < PT; ++p) {
+    const int e = tid + 256 * p;
+    if (e < KP * NQ) *reinterpret_cast<float4*>(s_B + (e / NQ) * LW + 4 * (e % NQ)) = v[p];
+  }
+  __syncthreads();
+  if (16 * w >= M) return;  // no barrier below
+  f32x4 acc[NT];
+#pragma unroll
+  for (int t = 0; t < NT; ++t) acc[t] = f32x4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+  for (int c = 0; c < KCH; ++c) {
+    const int64_t k = k0 + 16 * c + 4 * q;
+    const float av[4] = {k + 0 < K ? a[c].x : 0.f, k + 1 < K ? a[c].y : 0.f, k + 2 < K ? a[c].z : 0.f,
+                         k + 3 < K ? a[c].w : 0.f};
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      const float* br = s_B + (16 * c + 4 * q + j) * LW + r;
+#pragma unroll
+      for (int t = 0; t < NT; ++t) acc[t] = __builtin_amdgcn_mfma_f32_16x16x4f32(av[j], br[16 * t], acc[t], 0, 0, 0);
+    }
+  }
+  // C/D map: reg jj -> row 4q + jj, column lane & 15
+  float* out = slab + (int64_t)blockIdx.x * M * N;
+#pragma unroll
+  for (int t = 0; t < NT; ++t) {
+    const int64_t n = n0 + 16 * t + r;
+#pragma unroll
+    for (int jj = 0; jj < 4; ++jj) {
+      const int64_t gm = 16 * w + 4 * q + jj;
+      if (gm < M && n < N) out[gm * N + n] = acc[t][jj];
+    }
+  }
+}
+
+// Sum S slabs [S][M][N] (M N % 4 == 0) into C: a workgroup owns 16 float4 of
+// the output; thread group g (16 of them) sums the slabs [g P, g P + P) of
+// them in slab order with all its loads in flight, and group 0 adds the 16
+// group sums in group order (a fixed order: bitwise reproducible), then
+// applies the epilogue.
+constexpr int kRedItems = 16, kRedGroups = 16, kRedBatch = 8;
+__global__ void __launch_bounds__(256)
+gemm_slab_reduce4_kernel(int32_t M, int32_t N, int32_t S, const float* __restrict__ slab, float* __restrict__ C,
+                         int64_t ldc, GemmEpi epi) {
+  __shared__ float4 s_part[kRedGroups][kRedItems];
+  const int i = threadIdx.x % kRedItems, g = threadIdx.x / kRedItems;
+  const int64_t total4 = (int64_t)M * N / 4;
+  const int64_t o = (int64_t)blockIdx.x * kRedItems + i;
+  const int per = (S + kRedGroups - 1) / kRedGroups;
+  const int s0 = g * per, s1 = min(S, s0 + per);
+  const float4* sl = reinterpret_cast<const float4*>(slab);
+  float4 acc = make_float4(0.f, 0.f, 0.f, 0.f);
+  if (o < total4) {
+    for (int sb = s0; sb < s1; sb += kRedBatch) {
+      float4 v[kRedBatch];
+#pragma unroll
+      for (int j = 0; j < kRedBatch; ++j) v[j] = sb + j < s1 ? sl[(int64_t)(sb + j) * total4 + o] : make_float4(0.f, 0.f, 0.f, 0.f);
+#pragma unroll
+      for (int j = 0; j < kRedBatch; ++j)
+        if (sb + j < s1) { acc.x += v[j].x; acc.y += v[j].y; acc.z += v[j].z; acc.w += v[j].w; }
+    }
+  }
+  s_part[g][i] = acc;
+  __syncthreads();
+  if (g != 0 || o >= total4) return;
+  float4 t = s_part[0][i];
+#pragma unroll
+  for (int gg = 1; gg < kRedGroups; ++gg) {
+    const float4 u = s_part[gg][i];
+    t.x += u.x; t.y += u.y; t.z += u.z; t.w += u.w;
+  }
+  const int64_t e = 4 * o, m = e / N, n = e % N;  // N % 4 == 0: one row
+  float* c = C + m * ldc + n;
+  c[0] = gemm_epi(epi, t.x, m, n + 0);
+  c[1] = gemm_epi(epi, t.y, m, n + 1);
+  c[2] = gemm_epi(epi, t.z, m, n + 2);
+  c[3] = gemm_epi(epi, t.w, m, n + 3);
+}
+
 // Sum split-K slabs in slab order, then apply the epilogue.
 __global__ void gemm_splitk_reduce_kernel(int32_t M, int32_t N, int32_t S, const float* __restrict__ slab,
                                           float* __restrict__ C, int64_t ldc, GemmEpi epi) {
@@ -477,6 +600,32 @@ extern "C" int gcnk_gemm_f32(int32_t transA, int32_t transB, int32_t M, int32_t 
     }
 #undef GCNK_SHORTK
     return launch_check("gemm_shortk_kernel");
+  }
+  // chunk = 16 KCH >= ceil(K / split_k): at most split_k slabs (the workspace);
+  // splits too few for 128-deep chunks take the generic kernel
+  const int64_t sm_want = (K + split_k - 1) / split_k;
+  const int sm_kch = sm_want <= 16 ? 1 : sm_want <= 32 ? 2 : sm_want <= 64 ? 4 : 8;
+  const int64_t sm_S = ((int64_t)K + 16 * sm_kch - 1) / (16 * sm_kch);
+  if (!ta && !tb && M <= 64 && K >= 512 && N % 4 == 0 && lda % 4 == 0 && ldb % 4 == 0 && aligned16(A) &&
+      aligned16(B) && split_k > 1 && sm_S <= split_k) {
+    const int kch = sm_kch;
+    const int32_t S = (int32_t)sm_S;
+    const dim3 grid((unsigned)S, (unsigned)((N + 111) / 112));
+#define GCNK_SMALLM(KCH_) \
+  hipLaunchKernelGGL((gemm_smallm_splitk_kernel<KCH_>), grid, dim3(256), 0, s, M, N, K, A, lda, B, ldb, workspace)
+    switch (kch) {
+      case 1: GCNK_SMALLM(1); break;
+      case 2: GCNK_SMALLM(2); break;
+      case 4: GCNK_SMALLM(4); break;
+      default: GCNK_SMALLM(8); break;
+    }
+#undef GCNK_SMALLM
+    int rc = launch_check("gemm_smallm_splitk_kernel");
+    if (rc) return rc;
+    const int64_t total4 = (int64_t)M * N / 4;
+    hipLaunchKernelGGL(gemm_slab_reduce4_kernel, dim3((unsigned)((total4 + kRedItems - 1) / kRedItems)),
+                       dim3(kRedItems * kRedGroups), 0, s, M, N, S, workspace, C, ldc, e);
+    return launch_check("gemm_slab_reduce4_kernel");
   }
   if (N <= 16) return launch_gemm<4, 1, 2, 1>(ta, tb, M, N, K, A, lda, B, ldb, C, ldc, e, split_k, workspace, s);
   return launch_gemm<2, 2, 2, 2>(ta, tb, M, N, K, A, lda, B, ldb, C, ldc, e, split_k, workspace, s);

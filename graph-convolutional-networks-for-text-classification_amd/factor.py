@@ -29,11 +29,14 @@ import torch
 from .sparse import CSR
 
 MAX_HUBS = 128    # hub rows staged in LDS (S_T [hubs x F]; the kernel checks the LDS budget)
-# X[hubs] W1: "spmm" (default) -- the SpMM tile plan on their CSR plus its slab
-# reduce (R8 9.8 us per call, two launches); "gemm" -- the split-K MFMA GEMM on
-# a dense copy (9.5 + 4.9 us, round 3).  A one-launch split-K MFMA kernel with
-# two levels of last-arriver slab sums measured 12.1 us (round 4, DESIGN §5:
-# each coherent hand-off is a ~2 us memory round trip) and was removed.
+# X[hubs] W1 (R8: 50 dense hub rows x 7463): "spmm" (default) -- the SpMM tile
+# plan on their CSR plus its slab reduce (9.8 us per call; 6.8 + 4.9 us in the
+# forward's trace); "gemm" -- a dense copy of the hub rows through the small-M
+# split-K MFMA GEMM (csrc/gemm.hip gemm_smallm_splitk_kernel + slab reduce:
+# 10.4 us per call, 7.7 + 4.7 in the trace, profiles/r04_smallm_*; the generic
+# tiled GEMM took 13.7).  A one-launch split-K kernel with two levels of
+# last-arriver slab sums measured 12.1 us (round 4, DESIGN §5: each coherent
+# hand-off is a ~2 us memory round trip) and was removed.
 XHUB = os.environ.get("GCNK_FACTOR_XHUB", "spmm")
 MAX_KC = 128      # X's light-row column range (U's width)
 ROWS_PER_BLOCK = 32   # csrc/factor.hip kRB
@@ -57,7 +60,7 @@ class HubFactor:
     def hub_times(self, W):
         """S_T = X[hubs] @ W  (the hub rows of reference layer.py:102)."""
         from .ops import gemm, spmm
-        if self.x_hub is not None and (XHUB != "gemm" or self.x_hub_dense is None):
+        if self.x_hub_dense is None:
             return spmm(self.x_hub, W)
         return gemm(self.x_hub_dense, W)
 
@@ -171,11 +174,14 @@ def build(adj, xop):
             torch.arange(tot, device=dev, dtype=torch.int64)
         f.x_hub = CSR(hrp.to(torch.int32), x.colind[idx], x.val[idx], (H, x.shape[1]))
         f.x_hub_dense = None
-        if XHUB == "gemm" and H * x.shape[1] * 4 <= 64 << 20:
-            d = torch.zeros((H, x.shape[1]), dtype=torch.float32, device=dev)
+        kx = x.shape[1]
+        fits = H * kx * 4 <= 64 << 20
+        if fits and XHUB == "gemm":
+            # rows padded to a multiple of 4 floats (the GEMM's float4 loads)
+            d = torch.zeros((H, (kx + 3) // 4 * 4), dtype=torch.float32, device=dev)
             d[torch.repeat_interleave(torch.arange(H, device=dev), lens, output_size=tot), x.colind[idx].long()] = \
                 x.val[idx]
-            f.x_hub_dense = d
+            f.x_hub_dense = d[:, :kx]
     else:
         f.x_hub = None
         f.x_hub_dense = xop.dense.index_select(0, f.hubs).contiguous()

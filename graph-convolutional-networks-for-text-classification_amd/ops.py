@@ -240,6 +240,9 @@ def default_split_k(M, N, K):
     """K-slabs for a GEMM: only long reductions with a small output (H^T g,
     K = nodes) are split; short ones (H1 W2, K = 200) stay whole so the skinny
     kernel takes them."""
+    if M <= 64 and K >= 512 and N % 4 == 0:
+        # the small-M split-K kernel (csrc/gemm.hip): 64-deep k chunks
+        return (K + 63) // 64
     tiles = ((M + 63) // 64) * ((N + 63) // 64)
     split_k = 1
     while K >= 1024 and split_k < 128 and tiles * split_k < 512 and K // (split_k * 2) >= 64:

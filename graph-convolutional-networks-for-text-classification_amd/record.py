@@ -102,7 +102,7 @@ class ForwardRecord:
             s.Kc, s.nhub, s.k0, s.rec_words = fac.Kc, fac.H, fac.k0, fac.rec_words
             s.U, s.ldu, s.rec = fac.U.data_ptr(), fac.U.stride(0), fac.rec.data_ptr()
             keep += [fac.U, fac.rec]
-            if fac.x_hub is not None and (factor.XHUB != "gemm" or fac.x_hub_dense is None):
+            if fac.x_hub_dense is None:
                 x_csr, x_dense = fac.x_hub, None
             else:
                 x_csr, x_dense = None, fac.x_hub_dense

@@ -1,5 +1,6 @@
 """Per-call time (hipGraph of back-to-back launches) of gcnk_gemm_f32 on a
-given shape; one JSON line.  python scripts/gemm_probe.py M N K"""
+given shape; one JSON line.  python scripts/gemm_probe.py M N K
+(GCNK_PROBE_SPLIT=<n> forces split_k)"""
 import json
 import os
 import sys
@@ -18,11 +19,12 @@ def main():
     dev = torch.device("cuda", 0)
     A = torch.randn(M, K, device=dev)
     B = torch.randn(K, N, device=dev)
-    C = ops.gemm(A, B)
+    split = int(os.environ.get("GCNK_PROBE_SPLIT", "0")) or None
+    C = ops.gemm(A, B, split_k=split)
     err = float((C - A.double() @ B.double()).abs().max())
-    us = time_graph([lambda: ops.gemm(A, B, out=C)], 100)
-    print(json.dumps({"M": M, "N": N, "K": K, "us": round(us, 3), "tflops": 2 * M * N * K / us / 1e6,
-                      "max_err": err}), flush=True)
+    us = time_graph([lambda: ops.gemm(A, B, out=C, split_k=split)], 100)
+    print(json.dumps({"M": M, "N": N, "K": K, "split_k": split, "us": round(us, 3),
+                      "tflops": 2 * M * N * K / us / 1e6, "max_err": err}), flush=True)
 
 
 if __name__ == "__main__":

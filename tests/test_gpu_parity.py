@@ -381,6 +381,27 @@ def test_gemm_mfma(ta, tb, shape):
     _close(got, ref, rtol=1e-5, atol=2e-6 * np.sqrt(K) * 4)
 
 
+@pytest.mark.parametrize("shape", [(50, 200, 7463), (64, 200, 8192), (1, 4, 512), (17, 116, 1000),
+                                   (63, 332, 4099)])
+@pytest.mark.parametrize("split", [None, 8, 117, 234, 600])
+def test_gemm_small_m_split_k(shape, split):
+    """The small-M long-K split-K kernel + its slab reduce (X[hubs] W1 of the
+    factored gc1: R8 [50 x 7463] x [7463 x 200]) against the float64 oracle, on
+    A rows padded to a multiple of 4 (garbage in the padding, never
+    multiplied), every k chunk size and ragged M, N, K; bitwise reproducible."""
+    M, N, K = shape
+    g = torch.Generator().manual_seed(M + N + K)
+    A = torch.randn(M, K, generator=g)
+    B = torch.randn(K, N, generator=g)
+    Ap = torch.full((M, (K + 3) // 4 * 4), float("nan"))
+    Ap[:, :K] = A
+    Ad = Ap.to(DEV)[:, :K]
+    assert Ad.stride(0) % 4 == 0
+    got = gemm(Ad, B.to(DEV), split_k=split)
+    _close(got, A.double().numpy() @ B.double().numpy(), rtol=1e-5, atol=2e-6 * np.sqrt(K) * 4)
+    assert torch.equal(got, gemm(Ad, B.to(DEV), split_k=split))
+
+
 def test_gemm_epilogues_and_split_k():
     g = torch.Generator().manual_seed(1)
     A = torch.randn(500, 96, generator=g)

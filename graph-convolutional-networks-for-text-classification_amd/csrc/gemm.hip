@@ -280,16 +280,28 @@ gemm_shortk_kernel(int32_t M, int32_t N, int32_t K, const float* __restrict__ A,
   f32x4 acc[NT];
 #pragma unroll
   for (int t = 0; t < NT; ++t) acc[t] = f32x4{0.f, 0.f, 0.f, 0.f};
+  // B fragments of chunk c + 1 are read from LDS while chunk c's MFMAs run
+  // (left to itself the compiler waited on each ds_read2 before its two MFMAs)
+  float bf[2][4][NT];
+  auto fetch = [&](int c, float (&b)[4][NT]) {
+#pragma unroll
+    for (int j = 0; j < 4; ++j)
+#pragma unroll
+      for (int t = 0; t < NT; ++t) b[j][t] = s_B[(16 * c + 4 * q + j) * LW + r + 16 * t];
+  };
+  fetch(0, bf[0]);
 #pragma unroll
   for (int c = 0; c < KCH; ++c) {
+    if (c + 1 < KCH) fetch(c + 1, bf[(c + 1) & 1]);
+    __builtin_amdgcn_sched_barrier(0);
     const bool ok = (aok >> c) & 1;
     const float av[4] = {ok ? a[c].x : 0.f, ok ? a[c].y : 0.f, ok ? a[c].z : 0.f, ok ? a[c].w : 0.f};
 #pragma unroll
-    for (int j = 0; j < 4; ++j) {
-      const float* br = s_B + (16 * c + 4 * q + j) * LW + r;
+    for (int j = 0; j < 4; ++j)
 #pragma unroll
-      for (int t = 0; t < NT; ++t) acc[t] = __builtin_amdgcn_mfma_f32_16x16x4f32(av[j], br[16 * t], acc[t], 0, 0, 0);
-    }
+      for (int t = 0; t < NT; ++t)
+        acc[t] = __builtin_amdgcn_mfma_f32_16x16x4f32(av[j], bf[c & 1][j][t], acc[t], 0, 0, 0);
+    __builtin_amdgcn_sched_barrier(0);
   }
   // C/D map: reg jj -> row 4q + jj, column lane & 15
 #pragma unroll
@@ -357,17 +369,29 @@ gemm_smallm_splitk_kernel(int32_t M, int32_t N, int32_t K, const float* __restri
   f32x4 acc[NT];
 #pragma unroll
   for (int t = 0; t < NT; ++t) acc[t] = f32x4{0.f, 0.f, 0.f, 0.f};
+  // B fragments of block c + 1 are read from LDS while block c's MFMAs run
+  // (left to itself the compiler waited on each ds_read2 before its two MFMAs)
+  float bf[2][4][NT];
+  auto fetch = [&](int c, float (&b)[4][NT]) {
+#pragma unroll
+    for (int j = 0; j < 4; ++j)
+#pragma unroll
+      for (int t = 0; t < NT; ++t) b[j][t] = s_B[(16 * c + 4 * q + j) * LW + r + 16 * t];
+  };
+  fetch(0, bf[0]);
 #pragma unroll
   for (int c = 0; c < KCH; ++c) {
+    if (c + 1 < KCH) fetch(c + 1, bf[(c + 1) & 1]);
+    __builtin_amdgcn_sched_barrier(0);
     const int64_t k = k0 + 16 * c + 4 * q;
     const float av[4] = {k + 0 < K ? a[c].x : 0.f, k + 1 < K ? a[c].y : 0.f, k + 2 < K ? a[c].z : 0.f,
                          k + 3 < K ? a[c].w : 0.f};
 #pragma unroll
-    for (int j = 0; j < 4; ++j) {
-      const float* br = s_B + (16 * c + 4 * q + j) * LW + r;
+    for (int j = 0; j < 4; ++j)
 #pragma unroll
-      for (int t = 0; t < NT; ++t) acc[t] = __builtin_amdgcn_mfma_f32_16x16x4f32(av[j], br[16 * t], acc[t], 0, 0, 0);
-    }
+      for (int t = 0; t < NT; ++t)
+        acc[t] = __builtin_amdgcn_mfma_f32_16x16x4f32(av[j], bf[c & 1][j][t], acc[t], 0, 0, 0);
+    __builtin_amdgcn_sched_barrier(0);
   }
   // C/D map: reg jj -> row 4q + jj, column lane & 15
   float* out = slab + (int64_t)blockIdx.x * M * N;

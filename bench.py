@@ -240,10 +240,8 @@ def rocprof_kernel_us(mode, kernels_like, save_dir=None, variant="row"):
 
 def _factored(a_csr, x):
     """The HubFactor the product forward uses for (A-hat, X), or None (SpMM path)."""
-    from graph_convolutional_networks_for_text_classification_amd import factor, ops
-    if not ops.FACTOR_GC1:
-        return None
-    return factor.get(a_csr, ops.Operand(x))
+    from graph_convolutional_networks_for_text_classification_amd import ops
+    return ops.factor_for(a_csr, ops.Operand(x))
 
 
 def forward_kernels(save_dir=None, graph="r8"):

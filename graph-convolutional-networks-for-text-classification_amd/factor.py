@@ -190,6 +190,23 @@ def build(adj, xop):
     return f
 
 
+_cus = {}
+
+
+def pays(f, device):
+    """Whether the factored gc1 is the faster forward for factor ``f``.  Its
+    workgroups (one per 32-row block, one per CU at R8's / 20ng's LDS) each
+    restage W1[Kc], S_T and W2, so it pays while the blocks fit one round over
+    the CUs: R8 (242 blocks on 256 CUs) 25.1-25.4 us per forward against 29.0
+    on the SpMM path; the 20ng shape (592 blocks) 50.9 against 49.0
+    (profiles/r04_fwd_path_*.log, record forward, hipGraph)."""
+    idx = torch.device(device).index or 0
+    n = _cus.get(idx)
+    if n is None:
+        n = _cus[idx] = torch.cuda.get_device_properties(idx).multi_processor_count
+    return f.nblk <= n
+
+
 def get(adj, xop):
     """The cached HubFactor of (adj, X), built on first use; None when the
     operands do not factor (the caller runs the generic SpMM path)."""

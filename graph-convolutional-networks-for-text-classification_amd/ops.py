@@ -189,10 +189,22 @@ def spmm_proj(a, B, W, bias=None, epilogue=_lib.EPI_NONE, mask=None, scale=1.0, 
     return H, C2
 
 
-# gc1 through the hub factorisation (factor.py, csrc/factor.hip) whenever the
-# (A-hat, X) pair has the doc-topic structure; GCNK_FACTOR_GC1=0 forces the
-# SpMM path (experiments, A/B timing).
-FACTOR_GC1 = os.environ.get("GCNK_FACTOR_GC1", "1") != "0"
+# gc1 through the hub factorisation (factor.py, csrc/factor.hip) when the
+# (A-hat, X) pair has the doc-topic structure and the factored launch is the
+# faster one (factor.pays); GCNK_FACTOR_GC1=1 takes it whenever the operands
+# factor, =0 never (experiments, A/B timing).
+_FACTOR_ENV = os.environ.get("GCNK_FACTOR_GC1", "auto")
+FACTOR_GC1 = "auto" if _FACTOR_ENV == "auto" else _FACTOR_ENV != "0"
+
+
+def factor_for(adj, xop):
+    """The HubFactor gc1 runs through for (adj, X), or None (the SpMM path)."""
+    if not FACTOR_GC1:
+        return None
+    f = factor.get(adj, xop)
+    if f is not None and FACTOR_GC1 == "auto" and not factor.pays(f, adj.device):
+        return None
+    return f
 
 
 def hubfactor_gc1(f, W1, b1, W2, epilogue=_lib.EPI_BIAS_RELU, mask=None, scale=1.0, keep_prob=1.0, seed=0,
@@ -523,7 +535,7 @@ class GCNFn(torch.autograd.Function):
             ctx.has_b1, ctx.has_b2 = b1 is not None, b2 is not None
             ctx.save_for_backward(W2, H1)
             return out
-        fac = factor.get(adj, xop) if FACTOR_GC1 else None
+        fac = factor_for(adj, xop)
         res = None
         if fac is not None:
             res = hubfactor_gc1(fac, W1, b1, W2, epilogue=epi, mask=mask, scale=scale, keep_prob=keep, seed=seed,

@@ -94,7 +94,7 @@ class ForwardRecord:
         s = GcnFwd()
         keep = []
         s.M, s.F, s.P = M, F, P
-        fac = factor.get(adj, xop) if ops.FACTOR_GC1 else None
+        fac = ops.factor_for(adj, xop)
         kind = None
         if fac is not None and P <= 32 and F % 4 == 0 and F <= 256 and \
                 int(lib.gcnk_hubfactor_lds_bytes(F, fac.Kc, fac.H, fac.rec_words, P)) <= 160 * 1024:

@@ -46,8 +46,8 @@ def main():
             print(json.dumps({"lib": tag, "graph": gname, "op": op, "us": round(us, 3), **kw}), flush=True)
 
         with torch.no_grad():
-            if f is None:
-                line("no factor", float("nan"))
+            if f is None or not ops.FACTOR_GC1:
+                line("forward (record, unfactored)", time_graph([lambda: m(x, adj)], args.reps))
                 continue
             S_T = f.hub_times(W1).contiguous()
             if f.x_hub is not None:

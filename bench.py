@@ -285,6 +285,7 @@ def labelled_forward_kernels(save_dir, graph, a_csr, x, N, nfeat, nnz_a, nnz_x, 
         "X W1": spmm_bytes(N, nfeat, nnz_x, nhid),
         "A S1": 4 * (N + 1) + 8 * nnz_a + 4 * N * nhid + 4 * N * nclass + 4 * nhid * nclass,
         "A S2": spmm_bytes(N, N, nnz_a, nclass),
+        "H1 W2": 4 * (N * nhid + nhid * nclass + N * nclass),   # unfused gc2 support (P > FUSE_MAX_P)
     }
     fac = _factored(a_csr, x)
     if fac is not None:
@@ -306,6 +307,8 @@ def labelled_forward_kernels(save_dir, graph, a_csr, x, N, nfeat, nnz_a, nnz_x, 
         elif "spmm_row_kernel" in name:
             key = "A S1" if na == 0 and fac is None else "A S2"
             na += 1
+        elif fac is None and na > 0:
+            key = "H1 W2"        # the skinny GEMM between the two aggregations
         else:
             key = "X W1" if fac is None else "X_hubs W1"
         ks.append({"kernel": name[:120], "us": k["us"], "op": key})

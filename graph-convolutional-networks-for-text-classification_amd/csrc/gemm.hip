@@ -227,24 +227,39 @@ gemm_skinny_ksplit_kernel(int32_t M, int32_t N, int32_t K, const float* __restri
 // rows 16-B aligned): C = epi(A B) for a dense gensim-style X W1 ([nodes x
 // 100] x [100 x 200]: the 20ng-shaped graph, R8 with 100-d features), where
 // the tiled kernel above spends its time in 7 barrier-separated k tiles of a
-// 64 x 64 tile.  One workgroup = 64 rows x 7 n-tiles (112 columns): its B
-// slice [K x 112] is staged in LDS ONCE (float4 copies, rows padded to 116
+// 64 x 64 tile.  One workgroup = 64 rows x NT n-tiles (16 NT columns): its B
+// slice [K x 16 NT] is staged in LDS ONCE (float4 copies, rows padded by 4
 // floats), all of it in flight with the A loads, and each wave multiplies its
 // 16 rows by it with no further barrier: lane l holds A[row l&15][16c +
 // 4(l>>4) .. +3] for every 16-deep k chunk c (the k order inside a chunk is
 // permuted the same way for A and B, as in the skinny kernel) and runs
-// 4 * KCH k-steps over 7 independent accumulators.
+// 4 * KCH k-steps over NT independent accumulators.
+// NT = 3 (48 columns, 23 KB of LDS, ~5 workgroups per CU) against round 3's 7
+// (112 columns, 52 KB, 3 per CU): [70 x 100] x [100 x 200] 8.1 -> 4.7 us,
+// [1000 x ..] 8.2 -> 4.9, the 20ng-shaped X W1 [18846 x ..] 18.2-18.6 ->
+// 16.4-16.5 (profiles/r04_shortk_nt.log).
+#ifndef GCNK_SHORTK_NT
+#define GCNK_SHORTK_NT 3
+#endif
+constexpr int kShortkNT = GCNK_SHORTK_NT;
 template <int KCH>
 __global__ void __launch_bounds__(256)
 gemm_shortk_kernel(int32_t M, int32_t N, int32_t K, const float* __restrict__ A, int64_t lda,
                    const float* __restrict__ B, int64_t ldb, float* __restrict__ C, int64_t ldc, GemmEpi epi) {
-  constexpr int NT = 7, BN = 16 * NT, LW = BN + 4, KP = 16 * KCH, NQ = BN / 4;
+  constexpr int NT = kShortkNT, BN = 16 * NT, LW = BN + 4, KP = 16 * KCH, NQ = BN / 4;
   constexpr int PT = (KP * NQ + 255) / 256;
   __shared__ __attribute__((aligned(16))) float s_B[KP * LW];
   const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
   const int r = lane & 15, q = lane >> 4;
-  const int64_t m0 = (int64_t)blockIdx.x * 64 + 16 * w;
-  const int64_t n0 = (int64_t)blockIdx.y * BN;
+  // XCD-aware order (1-D grid): workgroups b and b + 8 share an XCD, so the
+  // column tiles of one 64-row block run on one XCD -- its L2 serves their A
+  // rows and merges their parts of each C line before the write-back
+  const int nct = (N + BN - 1) / BN;
+  const int b = blockIdx.x, grp = b / (8 * nct), rem = b % (8 * nct);
+  const int64_t rb = (int64_t)grp * 8 + rem % 8;
+  if (rb * 64 >= M) return;  // tail of the last group of 8 row blocks (no barrier passed yet)
+  const int64_t m0 = rb * 64 + 16 * w;
+  const int64_t n0 = (int64_t)(rem / 8) * BN;
   const int64_t row = m0 + r;
   const bool rok = row < M;
   // every load of the workgroup is issued before the first LDS store; invalid
@@ -608,7 +623,8 @@ extern "C" int gcnk_gemm_f32(int32_t transA, int32_t transB, int32_t M, int32_t 
 #endif
   if (GCNK_GEMM_SHORTK && !ta && !tb && K > 0 && K <= 128 && K % 4 == 0 && N > 64 && N % 4 == 0 && lda % 4 == 0 &&
       ldb % 4 == 0 && aligned16(A) && aligned16(B) && split_k == 1) {
-    const dim3 grid((unsigned)(((int64_t)M + 63) / 64), (unsigned)((N + 111) / 112));
+    const int64_t nrb8 = ((int64_t)M + 64 * 8 - 1) / (64 * 8);  // groups of 8 row blocks
+    const dim3 grid((unsigned)(nrb8 * 8 * ((N + 16 * kShortkNT - 1) / (16 * kShortkNT))));
     const int kch = (K + 15) / 16;
 #define GCNK_SHORTK(KCH_) \
   hipLaunchKernelGGL((gemm_shortk_kernel<KCH_>), grid, dim3(256), 0, s, M, N, K, A, lda, B, ldb, C, ldc, e)

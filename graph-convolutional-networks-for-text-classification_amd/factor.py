@@ -197,9 +197,10 @@ def pays(f, device):
     """Whether the factored gc1 is the faster forward for factor ``f``.  Its
     workgroups (one per 32-row block, one per CU at R8's / 20ng's LDS) each
     restage W1[Kc], S_T and W2, so it pays while the blocks fit one round over
-    the CUs: R8 (242 blocks on 256 CUs) 25.1-25.4 us per forward against 29.0
-    on the SpMM path; the 20ng shape (592 blocks) 50.9 against 49.0
-    (profiles/r04_fwd_path_*.log, record forward, hipGraph)."""
+    the CUs: R8 (242 blocks on 256 CUs) 25.0-25.2 us per forward against
+    28.7-28.9 on the SpMM path; the 20ng shape (592 blocks) 47.4 against 47.2
+    (50.9 against 49.0 before this round's GEMM changes;
+    profiles/r04_fwd_path_*.log, record forward, hipGraph)."""
     idx = torch.device(device).index or 0
     n = _cus.get(idx)
     if n is None:

@@ -132,7 +132,7 @@ def _side_stream(device):
 # whose per-row projection costs more than the launch it saves (forward 106 us
 # fused vs 58 us unfused, profiles/r02_variants.log).
 FUSE_PROJECTION = os.environ.get("GCNK_FUSE_PROJECTION", "1") != "0"
-FUSE_MAX_P = 8
+FUSE_MAX_P = int(os.environ.get("GCNK_FUSE_MAX_P", "8"))
 # gc2's backward + gc1's ReLU/dropout backward in one pass over H1 (gcn_bwd2)
 FUSE_BACKWARD = os.environ.get("GCNK_FUSE_BACKWARD", "1") != "0"
 

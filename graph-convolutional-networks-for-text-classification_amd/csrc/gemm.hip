@@ -242,11 +242,11 @@ gemm_skinny_ksplit_kernel(int32_t M, int32_t N, int32_t K, const float* __restri
 #define GCNK_SHORTK_NT 3
 #endif
 constexpr int kShortkNT = GCNK_SHORTK_NT;
-template <int KCH>
+template <int KCH, int NT = kShortkNT>
 __global__ void __launch_bounds__(256)
 gemm_shortk_kernel(int32_t M, int32_t N, int32_t K, const float* __restrict__ A, int64_t lda,
                    const float* __restrict__ B, int64_t ldb, float* __restrict__ C, int64_t ldc, GemmEpi epi) {
-  constexpr int NT = kShortkNT, BN = 16 * NT, LW = BN + 4, KP = 16 * KCH, NQ = BN / 4;
+  constexpr int BN = 16 * NT, LW = BN + 4, KP = 16 * KCH, NQ = BN / 4;
   constexpr int PT = (KP * NQ + 255) / 256;
   __shared__ __attribute__((aligned(16))) float s_B[KP * LW];
   const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
@@ -596,6 +596,27 @@ extern "C" int gcnk_gemm_f32(int32_t transA, int32_t transB, int32_t M, int32_t 
   GemmEpi e{bias, R, ldr, scale, epilogue};
   hipStream_t s = (hipStream_t)stream;
   const bool ta = transA != 0, tb = transB != 0;
+#ifndef GCNK_GEMM_NARROW_SHORTK
+#define GCNK_GEMM_NARROW_SHORTK 1
+#endif
+  if (GCNK_GEMM_NARROW_SHORTK && !ta && !tb && M >= 16384 && N > 16 && N <= 32 && N % 4 == 0 && K > 128 &&
+      K <= 256 && K % 4 == 0 && lda % 4 == 0 && ldb % 4 == 0 && aligned16(A) && aligned16(B) && split_k == 1) {
+    // gc2's support H1 W2 at many rows ([nodes x 200] x [200 x classes]):
+    // 64-row workgroups, each wave one whole K chain per output (no cross-wave
+    // sum), W2's slice staged in LDS once per workgroup.  Against the skinny
+    // K-split kernel (profiles/r04_narrow.log): [18846 x 200] x [200 x 20] 8.9 ->
+    // 8.2 us, but [4000 x ..] 4.6 -> 5.5 and [7724 x 200] x [200 x 8] 3.5 -> 4.2:
+    // only past 16k rows and 16 columns
+    const int64_t nrb8 = ((int64_t)M + 64 * 8 - 1) / (64 * 8);
+    const dim3 grid((unsigned)(nrb8 * 8));
+#define GCNK_NARROW(KCH_, NT_) \
+  hipLaunchKernelGGL((gemm_shortk_kernel<KCH_, NT_>), grid, dim3(256), 0, s, M, N, K, A, lda, B, ldb, C, ldc, e)
+    if (K <= 208)  // N in (16, 32]: two n-tiles
+      GCNK_NARROW(13, 2);
+    else GCNK_NARROW(16, 2);
+#undef GCNK_NARROW
+    return launch_check("gemm_shortk_kernel");
+  }
   if (!ta && !tb && N <= 64 && K <= 1024 && lda % 4 == 0 && aligned16(A) && split_k == 1) {
     // 16 rows per workgroup, K split over its 4 waves (k blocks of 16 per wave),
     // every column tile of N from the same A registers

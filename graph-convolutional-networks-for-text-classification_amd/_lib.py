@@ -31,7 +31,7 @@ def _resolve_lib():
 
 
 LIB_PATH = _resolve_lib()
-ABI_VERSION = 9
+ABI_VERSION = 10
 
 # C-ABI return codes (gcnk.h)
 OK, EARG, EUNSUP, EHIP = 0, -1, -2, -3
@@ -121,6 +121,15 @@ SIGNATURES = {
         _f32, _u64, _u64, _vp,            # keep_prob, seed, offset, rng_base
         _vp, _i64, _vp, _i64, _vp, _i64,  # W2, ldw2, H, ldh, C2, ldc2
         _vp]),                            # stream
+    "gcnk_dense_gc1_f32": (ctypes.c_int, [
+        _i32, _i32, _i32, _i32,           # M, K, F, P
+        _vp, _i64, _vp, _i64,             # AX, ldax, W1, ldw1
+        _vp, _i32,                        # bias, epilogue
+        _vp, _i64, _f32,                  # drop_mask, ldm, drop_scale
+        _f32, _u64, _u64, _vp,            # keep_prob, seed, offset, rng_base
+        _vp, _i64, _vp, _i64, _vp, _i64,  # W2, ldw2, H, ldh, C2, ldc2
+        _vp]),                            # stream
+    "gcnk_aggregate_f32": (ctypes.c_int, [_vp, _vp, _vp, _i32, _vp, _i64, _i32, _vp, _i64, _i32, _vp]),
     # record (host struct gcnk_gcn_fwd), W1, b1, W2, b2, out, ldo, H1, ldh, epilogue, mask, ldm, scale,
     # keep_prob, seed, offset, rng_base, stream
     "gcnk_gcn_forward_f32": (ctypes.c_int, [_vp, _vp, _vp, _vp, _vp, _vp, _i64, _vp, _i64, _i32, _vp, _i64, _f32,

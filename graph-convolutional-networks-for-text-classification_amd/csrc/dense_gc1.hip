@@ -1,0 +1,259 @@
+// gc1 of a narrow-feature GCN from a cached aggregated operand (gfx950).
+//
+// Reference (layer.py:102,106,110,182,185 inside GCN.forward, layer.py:164-190,
+// and gc2's support layer.py:102):
+//   H1 = dropout(relu(A-hat (X W1) + b1)),   S2 = H1 W2
+// When X is dense and narrow (nfeat <= nhid: the gensim-shaped 100-d topic
+// features the README's R8 / 20ng numbers use, README.md:77,95), A-hat X is a
+// fixed [M x K] operand of the (A-hat, X) pair, built once (the float64 row sums
+// of csrc/factor_build.hip, rounded to fp32 once).  Then
+//   Z = (A-hat X) W1
+// is ONE short-K MFMA product per forward: the F-wide SpMM A-hat (X W1) and the
+// X W1 GEMM in front of it never run (the association differs from the
+// reference's A-hat (X W1) only in fp32 rounding, ~1e-6 relative).
+//
+// Persistent workgroups (one per CU, 4 waves, one per SIMD).  Wave w owns the
+// 16-column n-tiles t = w, w + 4, w + 8, ... of F; its W1 fragments (every
+// k-step x its n-tiles) and W2 fragments stay in registers for the whole
+// launch.  Per 16-row tile:
+//   1. Z_w = A_tile W1[:, cols_w] on v_mfma_f32_16x16x4_f32 (exact fp32 FMA
+//      chains; the next tile's A fragments are loaded under these MFMAs);
+//   2. + b1, ReLU, dropout (mask or hash: the SpMM's epilogue), H1 stored only
+//      when a backward needs it;
+//   3. H1[:, cols_w] W2[cols_w, :] on MFMA (the tile transposed to the A layout
+//      through wave-private LDS), the four waves' partials summed in LDS in a
+//      fixed order and stored as S2.
+// No atomics, no hand-off between workgroups: bitwise reproducible.
+#include "gcnk_common.h"
+
+#include <algorithm>
+
+namespace gcnk {
+namespace {
+
+typedef float f32x4 __attribute__((ext_vector_type(4)));
+
+constexpr int kWaves = 4;        // one per SIMD
+constexpr int kThreads = 64 * kWaves;
+constexpr int kNTQ = 4;          // n-tiles per wave: F <= 16 * 4 * kNTQ = 256
+constexpr int kHP = 64 + 4;      // wave-private H1 tile row stride (floats): 16 x (64 + 4)
+constexpr int kMaxP = 32;
+
+struct DenseArgs {
+  int32_t M, K, F, P;
+  const float* A; int64_t lda;     // A-hat X [M x >= K]
+  const float* W; int64_t ldw;     // W1 [K x F]
+  const float* W2; int64_t ldw2;   // [F x P]
+  float* H; int64_t ldh;           // nullable
+  float* C2; int64_t ldc2;         // S2 [M x P]
+  Epi epi;
+  int32_t ntiles;                  // ceil(M / 16)
+};
+
+// KS k-steps of 4 (K <= 4 KS; lane quadrant q of step s multiplies k = 4 s + q),
+// NP 16-column tiles of P
+template <int KS, int NP>
+__global__ void __launch_bounds__(kThreads)
+dense_gc1_kernel(DenseArgs a) {
+  __shared__ __attribute__((aligned(16))) float s_h[kWaves][16 * kHP];
+  __shared__ __attribute__((aligned(16))) float s_red[2][kWaves][NP][64 * 4];
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int w = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int c = lane & 15, q = lane >> 4;
+  const int F = a.F, K = a.K, P = a.P;
+  const int NT = (F + 15) / 16;
+  const int ntw = NT > w ? (NT - w + kWaves - 1) / kWaves : 0;  // this wave's n-tiles (wave-uniform)
+
+  // ---- registers for the whole launch: W1 fragments (k = 4 s + q, column
+  //      16 (w + 4 t) + c), W2 fragments of this wave's columns (local column
+  //      lc = 16 t + (lane's k within the step), 4 k-steps per n-tile), b1
+  float wf[KS][kNTQ];
+#pragma unroll
+  for (int s = 0; s < KS; ++s)
+#pragma unroll
+    for (int t = 0; t < kNTQ; ++t) {
+      const int k = 4 * s + q, col = 16 * (w + kWaves * t) + c;
+      wf[s][t] = (t < ntw && k < K && col < F) ? a.W[(int64_t)k * a.ldw + col] : 0.f;
+    }
+  // projection step (t, j): local columns 16 t + 4 j + q' for lane quadrant q'
+  float w2f[kNTQ][4][NP];
+#pragma unroll
+  for (int t = 0; t < kNTQ; ++t)
+#pragma unroll
+    for (int j = 0; j < 4; ++j)
+#pragma unroll
+      for (int p = 0; p < NP; ++p) {
+        const int col = 16 * (w + kWaves * t) + 4 * j + q, pc = 16 * p + c;
+        w2f[t][j][p] = (t < ntw && col < F && pc < P) ? a.W2[(int64_t)col * a.ldw2 + pc] : 0.f;
+      }
+  float bv[kNTQ];
+#pragma unroll
+  for (int t = 0; t < kNTQ; ++t) {
+    const int col = 16 * (w + kWaves * t) + c;
+    bv[t] = (a.epi.bias && t < ntw && col < F) ? a.epi.bias[col] : 0.f;
+  }
+  float* hw = s_h[w];
+
+  // A fragments of a tile: lane (row c, quadrant q) holds A[row][4 s + q]
+  auto load_a = [&](int tile, float (&af)[KS]) {
+    const int64_t row = (int64_t)tile * 16 + c;
+    const bool rok = tile < a.ntiles && row < a.M;
+    const float* ap = a.A + (rok ? row : 0) * a.lda + q;
+#pragma unroll
+    for (int s = 0; s < KS; ++s) af[s] = (rok && 4 * s + q < K) ? ap[4 * s] : 0.f;
+  };
+  // one 16-row tile: its MFMAs, epilogue and projection with `af`; the next
+  // tile's A fragments are loaded into `an` under the MFMAs (two named buffers,
+  // the tile loop unrolled by two: no runtime index into a register array)
+  auto tile_step = [&](int tile, int buf, float (&af)[KS], float (&an)[KS]) {
+    load_a(tile + gridDim.x, an);
+    // ---- 1. Z = A W1[:, cols_w]
+    f32x4 acc[kNTQ];
+#pragma unroll
+    for (int t = 0; t < kNTQ; ++t) acc[t] = f32x4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+    for (int s = 0; s < KS; ++s)
+#pragma unroll
+      for (int t = 0; t < kNTQ; ++t)
+        if (t < ntw) acc[t] = __builtin_amdgcn_mfma_f32_16x16x4f32(af[s], wf[s][t], acc[t], 0, 0, 0);
+    // ---- 2. epilogue (C/D map: reg r -> row 4 q + r, column c), H1 store,
+    //      tile into wave-private LDS
+    const int64_t row0 = (int64_t)tile * 16;
+    const bool plain = a.epi.code == GCNK_EPI_BIAS_RELU;
+#pragma unroll
+    for (int t = 0; t < kNTQ; ++t) {
+      if (t >= ntw) break;
+      const int64_t col = 16 * (w + kWaves * t) + c;
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const int64_t row = row0 + 4 * q + r;
+        float h;
+        if (plain) h = fmaxf(acc[t][r] + bv[t], 0.f);
+        else h = (row < a.M && col < F) ? apply_epi(a.epi, acc[t][r], bv[t], row, col) : 0.f;
+        if (a.H && row < a.M && col < F) __builtin_nontemporal_store(h, a.H + row * a.ldh + col);
+        hw[(4 * q + r) * kHP + 16 * t + c] = h;
+      }
+    }
+    // the wave's own LDS writes before its reads (other lanes' elements)
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+    // ---- 3. partial S2 = H1[:, cols_w] W2[cols_w, :]; A layout: lane (row c,
+    //      quadrant q) reads local columns 16 t + 4 j + q
+    f32x4 pacc[NP];
+#pragma unroll
+    for (int p = 0; p < NP; ++p) pacc[p] = f32x4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+    for (int t = 0; t < kNTQ; ++t) {
+      if (t >= ntw) break;
+      float ha[4];
+#pragma unroll
+      for (int j = 0; j < 4; ++j) ha[j] = hw[c * kHP + 16 * t + 4 * j + q];
+#pragma unroll
+      for (int j = 0; j < 4; ++j)
+#pragma unroll
+        for (int p = 0; p < NP; ++p) pacc[p] = __builtin_amdgcn_mfma_f32_16x16x4f32(ha[j], w2f[t][j][p], pacc[p], 0, 0, 0);
+    }
+#pragma unroll
+    for (int p = 0; p < NP; ++p) *reinterpret_cast<f32x4*>(&s_red[buf][w][p][4 * lane]) = pacc[p];
+    // (double-buffered by tile parity: wave 0 reads buffer `buf` before it
+    // reaches the next barrier, and buffer `buf` is written again only after it)
+    __syncthreads();
+    if (w == 0) {
+#pragma unroll
+      for (int p = 0; p < NP; ++p) {
+        f32x4 sum = *reinterpret_cast<const f32x4*>(&s_red[buf][0][p][4 * lane]);
+#pragma unroll
+        for (int v = 1; v < kWaves; ++v) sum += *reinterpret_cast<const f32x4*>(&s_red[buf][v][p][4 * lane]);
+        const int pc = 16 * p + c;
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          const int64_t row = row0 + 4 * q + r;
+          if (row < a.M && pc < P) a.C2[row * a.ldc2 + pc] = sum[r];
+        }
+      }
+    }
+    // the wave-private H1 tile is rewritten next tile after these reads (in
+    // order within the wave): no barrier needed
+    __builtin_amdgcn_wave_barrier();
+  };
+  float a0[KS], a1[KS];
+  load_a(blockIdx.x, a0);
+  for (int tile = blockIdx.x; tile < a.ntiles; tile += 2 * gridDim.x) {
+    tile_step(tile, 0, a0, a1);
+    if (tile + (int)gridDim.x >= a.ntiles) break;
+    tile_step(tile + gridDim.x, 1, a1, a0);
+  }
+}
+
+template <int KS>
+int launch_ks(const DenseArgs& a, int np, unsigned grid, hipStream_t s) {
+  if (np == 1)
+    hipLaunchKernelGGL((dense_gc1_kernel<KS, 1>), dim3(grid), dim3(kThreads), 0, s, a);
+  else
+    hipLaunchKernelGGL((dense_gc1_kernel<KS, 2>), dim3(grid), dim3(kThreads), 0, s, a);
+  return launch_check("dense_gc1_kernel");
+}
+
+}  // namespace
+}  // namespace gcnk
+
+using namespace gcnk;
+
+static int g_cus[64] = {0};
+
+extern "C" int gcnk_dense_gc1_f32(int32_t M, int32_t K, int32_t F, int32_t P, const float* AX, int64_t ldax,
+                                  const float* W1, int64_t ldw1, const float* bias, int32_t epilogue,
+                                  const uint8_t* drop_mask, int64_t ldm, float drop_scale, float keep_prob,
+                                  uint64_t seed, uint64_t offset, const uint64_t* rng_base, const float* W2,
+                                  int64_t ldw2, float* H, int64_t ldh, float* C2, int64_t ldc2, void* stream) {
+  if (M <= 0 || K <= 0 || F <= 0 || P <= 0 || !AX || !W1 || !W2 || !C2 || ldax < K || ldw1 < F || ldw2 < P ||
+      ldc2 < P || (H && ldh < F)) {
+    set_error("gcnk_dense_gc1_f32: bad sizes or null operand (M=%d K=%d F=%d P=%d)", M, K, F, P);
+    return GCNK_EARG;
+  }
+  if (K > 128 || F > 16 * kWaves * kNTQ || P > kMaxP) {
+    set_error("gcnk_dense_gc1_f32: unsupported shape (K=%d <= 128, F=%d <= 256, P=%d <= 32)", K, F, P);
+    return GCNK_EUNSUP;
+  }
+  if (epilogue != GCNK_EPI_BIAS_RELU && epilogue != GCNK_EPI_BIAS_RELU_DROP && epilogue != GCNK_EPI_BIAS_RELU_HASH) {
+    set_error("gcnk_dense_gc1_f32: epilogue %d is not a gc1 epilogue (bias + ReLU [+ dropout])", epilogue);
+    return GCNK_EARG;
+  }
+  if (epilogue == GCNK_EPI_BIAS_RELU_DROP && (!drop_mask || ldm < F)) {
+    set_error("gcnk_dense_gc1_f32: dropout epilogue needs a mask with ldm >= F");
+    return GCNK_EARG;
+  }
+  DenseArgs a;
+  a.M = M; a.K = K; a.F = F; a.P = P;
+  a.A = AX; a.lda = ldax; a.W = W1; a.ldw = ldw1; a.W2 = W2; a.ldw2 = ldw2;
+  a.H = H; a.ldh = ldh; a.C2 = C2; a.ldc2 = ldc2;
+  a.epi.bias = bias;
+  a.epi.mask = drop_mask;
+  a.epi.ldm = epilogue == GCNK_EPI_BIAS_RELU_HASH ? (ldm > 0 ? ldm : F) : ldm;
+  a.epi.scale = drop_scale;
+  a.epi.keep_prob = keep_prob;
+  a.epi.seed_lo = (uint32_t)seed;
+  a.epi.seed_hi = (uint32_t)(seed >> 32);
+  a.epi.offset = offset;
+  a.epi.rng_base = rng_base;
+  a.epi.code = epilogue;
+  a.epi.stamps = nullptr;
+  a.ntiles = (M + 15) / 16;
+  int dev = 0;
+  if (hipGetDevice(&dev) != hipSuccess || dev < 0) dev = 0;
+  int cus = dev < 64 ? g_cus[dev] : 0;
+  if (cus <= 0) {
+    if (hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || cus <= 0) cus = 256;
+    if (dev < 64) g_cus[dev] = cus;
+  }
+  const unsigned grid = (unsigned)std::min<int64_t>(a.ntiles, cus);
+  const int np = P <= 16 ? 1 : 2;
+  hipStream_t s = reinterpret_cast<hipStream_t>(stream);
+  const int ks = (K + 3) / 4;
+  if (ks <= 8) return launch_ks<8>(a, np, grid, s);
+  if (ks <= 13) return launch_ks<13>(a, np, grid, s);
+  if (ks <= 16) return launch_ks<16>(a, np, grid, s);
+  if (ks <= 25) return launch_ks<25>(a, np, grid, s);
+  return launch_ks<32>(a, np, grid, s);
+}

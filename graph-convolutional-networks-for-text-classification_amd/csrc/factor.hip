@@ -281,8 +281,8 @@ __global__ void __launch_bounds__(1024) lds_poison_kernel(uint32_t word) {
 using namespace gcnk;
 
 extern "C" int gcnk_debug_poison_lds(uint32_t word, void* stream) {
-  static const hipError_t attr = hipFuncSetAttribute(reinterpret_cast<const void*>(&lds_poison_kernel),
-                                                     hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
+  static std::atomic<uint64_t> done{0};
+  const hipError_t attr = dyn_lds_attr(done, reinterpret_cast<const void*>(&lds_poison_kernel), 160 * 1024);
   if (attr != hipSuccess) return hip_check(attr, "lds_poison_kernel LDS attribute");
   hipLaunchKernelGGL(lds_poison_kernel, dim3(1024), dim3(1024), 160 * 1024, reinterpret_cast<hipStream_t>(stream), word);
   return launch_check("lds_poison_kernel");
@@ -301,12 +301,13 @@ extern "C" int64_t gcnk_hubfactor_lds_bytes(int32_t F, int32_t Kc, int32_t nhub,
   return hubfactor_lds_bytes(F, Kc, nhub, rec_words, P);
 }
 
-// The dynamic-LDS limit is raised once per kernel instantiation (a driver call
-// per launch cost host time on every eager forward), then the launch.
+// The dynamic-LDS limit is raised once per kernel instantiation and device
+// (dyn_lds_attr), then the launch.
 template <int KS, int NTQ, int NP>
 static int launch_factor(const FactorArgs& a, int64_t nblk, int64_t lds_b, void* stream) {
-  static const hipError_t attr = hipFuncSetAttribute(reinterpret_cast<const void*>(&hubfactor_gc1_kernel<KS, NTQ, NP>),
-                                                     hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
+  static std::atomic<uint64_t> done{0};
+  const hipError_t attr =
+      dyn_lds_attr(done, reinterpret_cast<const void*>(&hubfactor_gc1_kernel<KS, NTQ, NP>), 160 * 1024);
   if (attr != hipSuccess) return hip_check(attr, "hubfactor_gc1_kernel LDS attribute");
   hipLaunchKernelGGL((hubfactor_gc1_kernel<KS, NTQ, NP>), dim3((unsigned)nblk), dim3(kThreads), (size_t)lds_b,
                      reinterpret_cast<hipStream_t>(stream), a);

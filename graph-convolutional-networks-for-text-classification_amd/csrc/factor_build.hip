@@ -42,7 +42,7 @@ __global__ void __launch_bounds__(256) factor_u_kernel(const int32_t* __restrict
   const int lane = threadIdx.x & 63;
   const int64_t p = (int64_t)blockIdx.x * kBuildRows + (threadIdx.x >> 6);
   if (p >= M) return;
-  const int r = perm[p];
+  const int r = perm ? perm[p] : (int)p;
   const int c0 = lane, c1 = lane + 64;
   const bool in0 = c0 < Kc, in1 = c1 < Kc;
   double acc0 = 0.0, acc1 = 0.0;
@@ -59,7 +59,7 @@ __global__ void __launch_bounds__(256) factor_u_kernel(const int32_t* __restrict
     }
 #pragma unroll
     for (int u = 0; u < 4; ++u) {
-      const bool light = hub_index[d[u]] < 0;
+      const bool light = !hub_index || hub_index[d[u]] < 0;
       const float* xr = Xl + (int64_t)d[u] * ldxl;
       x0[u] = light && in0 ? xr[c0] : 0.f;
       x1[u] = light && in1 ? xr[c1] : 0.f;
@@ -72,7 +72,7 @@ __global__ void __launch_bounds__(256) factor_u_kernel(const int32_t* __restrict
   }
   for (; j < end; ++j) {
     const int d = colind[j];
-    if (hub_index[d] >= 0) continue;
+    if (hub_index && hub_index[d] >= 0) continue;
     const double a = (double)val[j];
     const float* xr = Xl + (int64_t)d * ldxl;
     acc0 += a * (double)(in0 ? xr[c0] : 0.f);
@@ -168,6 +168,21 @@ extern "C" int gcnk_factor_u_f32(const int32_t* rowptr, const int32_t* colind, c
   const unsigned grid = (unsigned)(((int64_t)M + kBuildRows - 1) / kBuildRows);
   hipLaunchKernelGGL(factor_u_kernel, dim3(grid), dim3(64 * kBuildRows), 0, reinterpret_cast<hipStream_t>(stream),
                      rowptr, colind, val, M, hub_index, perm, Xl, ldxl, Kc, U, ldu, Kcp);
+  return launch_check("factor_u_kernel");
+}
+
+// A-hat X for the narrow-feature gc1 (csrc/dense_gc1.hip): every item of every
+// row, rows in order -- factor_u_kernel with no hub index and no permutation.
+extern "C" int gcnk_aggregate_f32(const int32_t* rowptr, const int32_t* colind, const float* val, int32_t M,
+                                  const float* X, int64_t ldx, int32_t K, float* out, int64_t ldo, int32_t Kp,
+                                  void* stream) {
+  if (M <= 0 || K <= 0 || Kp < K || Kp > 128 || ldo < Kp || ldx < K || !rowptr || !colind || !val || !X || !out) {
+    set_error("gcnk_aggregate_f32: bad sizes or null operand (M=%d K=%d Kp=%d)", M, K, Kp);
+    return GCNK_EARG;
+  }
+  const unsigned grid = (unsigned)(((int64_t)M + kBuildRows - 1) / kBuildRows);
+  hipLaunchKernelGGL(factor_u_kernel, dim3(grid), dim3(64 * kBuildRows), 0, reinterpret_cast<hipStream_t>(stream),
+                     rowptr, colind, val, M, nullptr, nullptr, X, ldx, K, out, ldo, Kp);
   return launch_check("factor_u_kernel");
 }
 

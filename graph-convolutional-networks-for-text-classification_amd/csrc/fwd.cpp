@@ -44,9 +44,10 @@ extern "C" int gcnk_gcn_forward_f32(const gcnk_gcn_fwd* rec, const float* W1, co
     return GCNK_EARG;
   }
   const gcnk_gcn_fwd& r = *rec;
-  if ((r.kind == GCNK_FWD_FACTORED && (!r.U || !r.rec)) ||
+  if ((r.kind == GCNK_FWD_FACTORED && (!r.U || !r.rec)) || (r.kind == GCNK_FWD_DENSE_AX && !r.U) ||
       ((r.kind == GCNK_FWD_SPMM_PROJ || r.kind == GCNK_FWD_SPMM_GEMM) && !r.aF.plan) ||
-      (r.kind == GCNK_FWD_SPMM_GEMM && !H1 && !r.h1_tmp) || (!r.x.plan && !r.x_dense)) {
+      (r.kind == GCNK_FWD_SPMM_GEMM && !H1 && !r.h1_tmp) ||
+      (r.kind != GCNK_FWD_DENSE_AX && !r.x.plan && !r.x_dense)) {
     set_error("gcnk_gcn_forward_f32: record kind %d is missing an operand (U / records / F-wide plan / H1 scratch / X)",
               r.kind);
     return GCNK_EARG;
@@ -59,16 +60,24 @@ extern "C" int gcnk_gcn_forward_f32(const gcnk_gcn_fwd* rec, const float* W1, co
                                   r.rec_words, b1, epilogue, drop_mask, ldm, drop_scale, keep_prob, seed, offset,
                                   rng_base, W2, r.P, H1, ldh, r.s2, r.lds2, stream);
       break;
+    case GCNK_FWD_DENSE_AX:
+      rc = gcnk_dense_gc1_f32(r.M, r.Kc, r.F, r.P, r.U, r.ldu, W1, r.F, b1, epilogue, drop_mask, ldm, drop_scale,
+                              keep_prob, seed, offset, rng_base, W2, r.P, H1, ldh, r.s2, r.lds2, stream);
+      break;
     case GCNK_FWD_SPMM_PROJ:
       if ((rc = first_product(r, W1, stream)) != GCNK_OK) return rc;
       rc = gcnk_spmm_proj_f32(r.aF.plan, r.aF.hdr, r.s1, r.lds1, r.F, H1, ldh, b1, epilogue, drop_mask, ldm, drop_scale,
                               keep_prob, seed, offset, rng_base, W2, r.P, r.P, r.s2, r.lds2, r.aF.workspace,
                               r.aF.workspace_bytes, r.aF.counters, r.aF.counter_bytes, r.aF.lanes_hint, stream);
-      break;
+      // outside the fused kernel's range (width, alignment of an operand): the
+      // same result from the SpMM into H1 (or the record's scratch) + the GEMM,
+      // as ops.spmm_proj does (nothing was launched by the refused call)
+      if (rc != GCNK_EUNSUP || (!H1 && !r.h1_tmp)) break;
+      [[fallthrough]];
     case GCNK_FWD_SPMM_GEMM: {
       float* h = H1 ? H1 : r.h1_tmp;
       const int64_t lh = H1 ? ldh : r.ld_h1_tmp;
-      if ((rc = first_product(r, W1, stream)) != GCNK_OK) return rc;
+      if (r.kind == GCNK_FWD_SPMM_GEMM && (rc = first_product(r, W1, stream)) != GCNK_OK) return rc;
       if ((rc = spmm_ref(r.aF, r.s1, r.lds1, r.F, h, lh, b1, epilogue, drop_mask, ldm, drop_scale, keep_prob, seed,
                          offset, rng_base, stream)) != GCNK_OK)
         return rc;
@@ -103,8 +112,10 @@ extern "C" int32_t gcnk_gcn_fwd_layout(int64_t* out, int32_t n) {
 extern "C" int gcnk_gcn_backward_f32(const gcnk_gcn_bwd* rec, const float* G, const float* H1, int64_t ldh,
                                      const float* W2, float scale, float* gW1, float* gb1, float* gW2, float* gb2,
                                      void* stream) {
+  const bool ax = (rec && (rec->flags & GCNK_BWD_AX_DIRECT));
   if (!rec || !G || !H1 || !W2 || rec->M <= 0 || rec->F <= 0 || rec->P <= 0 || ldh < rec->F || !rec->aTP.plan ||
-      !rec->gS2 || !rec->gZ1 || (gW1 && (!rec->aTF.plan || !rec->gS1 || (!rec->xT.plan && !rec->x_dense)))) {
+      !rec->gS2 || !rec->gZ1 ||
+      (gW1 && (ax ? !rec->x_dense : (!rec->aTF.plan || !rec->gS1 || (!rec->xT.plan && !rec->x_dense))))) {
     set_error("gcnk_gcn_backward_f32: null record/operand or incomplete record");
     return GCNK_EARG;
   }
@@ -119,6 +130,9 @@ extern "C" int gcnk_gcn_backward_f32(const gcnk_gcn_bwd* rec, const float* G, co
                               gW2, gb1, gb2, r.bwd2_ws, r.bwd2_ws_bytes, stream)) != GCNK_OK)
     return rc;
   if (!gW1) return GCNK_OK;
+  if (ax)  // gW1 = (A-hat X)^T gZ1: the DENSE_AX forward's Z1 = (A-hat X) W1
+    return gcnk_gemm_f32(1, 0, r.x_cols, r.F, r.x_rows, r.x_dense, r.ldx, r.gZ1, r.F, gW1, r.F, nullptr,
+                         GCNK_GEMM_EPI_NONE, nullptr, 0, 1.f, r.x_split_k, r.gemm_ws, r.gemm_ws_bytes, stream);
   // gS1 = A-hat^T gZ1, gW1 = X^T gS1  (autograd of layer.py:106, :102 in gc1)
   if ((rc = spmm_ref(r.aTF, r.gZ1, r.F, r.F, r.gS1, r.F, nullptr, GCNK_EPI_NONE, nullptr, 0, 1.f, 1.f, 0, 0, nullptr,
                      stream)) != GCNK_OK)

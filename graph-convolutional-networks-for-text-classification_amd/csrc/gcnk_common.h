@@ -6,6 +6,7 @@
 #include <cstdio>
 #include <cstdarg>
 #include <vector>
+#include <atomic>
 
 #include "../../include/gcnk.h"
 
@@ -27,6 +28,22 @@ inline int hip_check(hipError_t e, const char* what) {
 
 // Launch-error check right after a <<<>>> launch (never synchronises).
 inline int launch_check(const char* what) { return hip_check(hipGetLastError(), what); }
+
+// hipFuncSetAttribute(MaxDynamicSharedMemorySize) once per (kernel, device):
+// the attribute belongs to the device the launch runs on, so a process that
+// launches a kernel on several GPUs raises it on each (bit d of `done`, set
+// after the first successful call on device d; a driver call per launch would
+// cost host time on every eager forward).
+inline hipError_t dyn_lds_attr(std::atomic<uint64_t>& done, const void* fn, int bytes) {
+  int dev = 0;
+  hipError_t e = hipGetDevice(&dev);
+  if (e != hipSuccess) return e;
+  const uint64_t bit = dev >= 0 && dev < 64 ? (1ull << dev) : 0;
+  if (bit && (done.load(std::memory_order_acquire) & bit)) return hipSuccess;
+  e = hipFuncSetAttribute(fn, hipFuncAttributeMaxDynamicSharedMemorySize, bytes);
+  if (e == hipSuccess && bit) done.fetch_or(bit, std::memory_order_acq_rel);
+  return e;
+}
 
 inline bool aligned16(const void* p) { return (reinterpret_cast<uintptr_t>(p) & 15u) == 0; }
 

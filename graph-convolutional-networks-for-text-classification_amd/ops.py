@@ -248,11 +248,90 @@ def hubfactor_gc1(f, W1, b1, W2, epilogue=_lib.EPI_BIAS_RELU, mask=None, scale=1
     return H1, S2
 
 
-def default_split_k(M, N, K):
+# gc1 from a cached A-hat X (csrc/dense_gc1.hip) for a dense, narrow X (at most
+# DENSE_AX_MAX_K features: the gensim-shaped topic features of README.md:77,95):
+# one launch (A-hat X) W1 + b1, ReLU, dropout and gc2's H1 W2 instead of the
+# X W1 GEMM, the F-wide SpMM and the projection.  GCNK_DENSE_AX=0 turns it off
+# (A/B timing), =1 / auto (default) takes it wherever it applies.
+DENSE_AX = os.environ.get("GCNK_DENSE_AX", "auto") != "0"
+DENSE_AX_MAX_K = 128
+
+
+class DenseAX:
+    """A-hat X [M x K] (fp32, rows padded to a multiple of 4 floats), built once
+    per (A-hat, X) pair: float64 row sums in CSR order rounded once
+    (gcnk_aggregate_f32, the factored path's U kernel with every row light)."""
+
+    __slots__ = ("AX", "K", "_src")
+
+
+def dense_ax_for(adj, xop, F=None, P=None):
+    """The cached DenseAX of (adj, X) when the narrow-feature gc1 applies, else None."""
+    if not DENSE_AX or xop.dense is None:
+        return None
+    M, K = xop.shape
+    if adj.shape[0] != adj.shape[1] or adj.shape[1] != M or K > DENSE_AX_MAX_K or K == 0:
+        return None
+    if (F is not None and F > 256) or (P is not None and P > 32):
+        return None
+    src = xop.dense
+    key = (id(src), src.data_ptr(), src._version, adj.val.data_ptr(), adj.val._version)
+    cache = getattr(adj, "_dense_ax", None)
+    if cache is None:
+        cache = adj._dense_ax = {}
+    hit = cache.get(key)
+    if hit is not None:
+        return hit
+    if src.stride(1) != 1:
+        src = src.contiguous()
+    Kp = (K + 3) // 4 * 4
+    AX = torch.empty((adj.shape[0], Kp), dtype=torch.float32, device=adj.device)
+    with torch.cuda.device(adj.device):
+        _lib.check(_lib.load().gcnk_aggregate_f32(_ptr(adj.rowptr), _ptr(adj.colind), _ptr(adj.val), adj.shape[0],
+                                                  _ptr(src), src.stride(0), K, _ptr(AX), Kp, Kp,
+                                                  _stream(adj.device)), "gcnk_aggregate_f32")
+    d = DenseAX()
+    d.AX, d.K, d._src = AX, K, xop.dense   # (holds the operand: its id cannot be recycled while cached)
+    while len(cache) >= 4:
+        cache.pop(next(iter(cache)))
+    cache[key] = d
+    return d
+
+
+def dense_gc1(d, W1, b1, W2, epilogue=_lib.EPI_BIAS_RELU, mask=None, scale=1.0, keep_prob=1.0, seed=0, offset=0,
+              rng_base=None, store_h1=True):
+    """(H1, S2) of gc1 + gc2's support from A-hat X (DenseAX ``d``): one launch of
+    gcnk_dense_gc1_f32 -- H1 = drop(relu((A-hat X) W1 + b1)) (reference
+    layer.py:102,106,110,182,185) and S2 = H1 W2 (layer.py:102, gc2)."""
+    W1 = _dense_f32(W1, "gc1 weight")
+    W2 = _dense_f32(W2, "gc2 weight")
+    _check_rng_base(rng_base, W1.device)
+    M, F, P = d.AX.shape[0], W1.shape[1], W2.shape[1]
+    if W1.shape[0] != d.K or W2.shape[0] != F:
+        raise RuntimeError(f"dense_gc1 shape mismatch: A-hat X [{M} x {d.K}], W1 {tuple(W1.shape)}, "
+                           f"W2 {tuple(W2.shape)}")
+    H1 = torch.empty((M, F), dtype=torch.float32, device=W1.device) if store_h1 else None
+    S2 = torch.empty((M, P), dtype=torch.float32, device=W1.device)
+    if b1 is not None:
+        b1 = b1.contiguous()
+    if mask is not None:
+        mask = mask.contiguous()
+    with torch.cuda.device(W1.device):
+        rc = _lib.load().gcnk_dense_gc1_f32(
+            M, d.K, F, P, _ptr(d.AX), d.AX.stride(0), _ptr(W1), W1.stride(0), _ptr(b1), epilogue,
+            _ptr(mask), mask.stride(0) if mask is not None else 0, float(scale),
+            float(keep_prob), int(seed) & (2**64 - 1), int(offset) & (2**64 - 1), _ptr(rng_base),
+            _ptr(W2), W2.stride(0), _ptr(H1), F, _ptr(S2), P, _stream(W1.device))
+    _lib.check(rc, "gcnk_dense_gc1_f32")
+    return H1, S2
+
+
+def default_split_k(M, N, K, trans=False):
     """K-slabs for a GEMM: only long reductions with a small output (H^T g,
     K = nodes) are split; short ones (H1 W2, K = 200) stay whole so the skinny
-    kernel takes them."""
-    if M <= 64 and K >= 512 and N % 4 == 0:
+    kernel takes them.  ``trans``: an operand is transposed (the small-M
+    kernel, which takes one 64-deep chunk per slab, is NN only)."""
+    if M <= 64 and K >= 512 and N % 4 == 0 and not trans:
         # the small-M split-K kernel (csrc/gemm.hip): 64-deep k chunks
         return (K + 63) // 64
     tiles = ((M + 63) // 64) * ((N + 63) // 64)
@@ -277,7 +356,7 @@ def gemm(A, B, transA=False, transB=False, bias=None, epilogue=_lib.GEMM_EPI_NON
     if out is None:
         out = torch.empty((M, N), dtype=torch.float32, device=A.device)
     if split_k is None:
-        split_k = default_split_k(M, N, K)
+        split_k = default_split_k(M, N, K, trans=transA or transB)
     lib = _lib.load()
     wsb = lib.gcnk_gemm_workspace_bytes(M, N, K, split_k)
     ws = torch.empty((wsb + 3) // 4, dtype=torch.float32, device=A.device) if wsb > 0 else None
@@ -318,9 +397,15 @@ def _bwd2_workspace(M, N, P, dev):
     if hit is None:
         wsb = int(_lib.load().gcnk_gcn_bwd2_workspace_bytes(M, N, P))
         if len(_BWD2_WS) >= 32:
-            _BWD2_WS.pop(next(iter(_BWD2_WS)))
-        hit = _BWD2_WS[key] = (wsb, torch.zeros((wsb + 3) // 4, dtype=torch.float32, device=dev))
-    return hit
+            # (a workspace a captured graph launched with is never freed: the
+            # graph replays into it)
+            victim = next((k for k, v in _BWD2_WS.items() if not v[2]), None)
+            if victim is not None:
+                _BWD2_WS.pop(victim)
+        hit = _BWD2_WS[key] = [wsb, torch.zeros((wsb + 3) // 4, dtype=torch.float32, device=dev), False]
+    if torch.cuda.is_current_stream_capturing():
+        hit[2] = True
+    return hit[0], hit[1]
 
 
 def gcn_bwd2(H1, gS2, W2, G=None, scale=1.0, want_gw=True, want_gb1=True):
@@ -532,12 +617,17 @@ class GCNFn(torch.autograd.Function):
         if res is not None:
             out, H1 = res
             ctx.xop, ctx.adj, ctx.scale = xop, adj, float(scale)
+            ctx.dax = None
             ctx.has_b1, ctx.has_b2 = b1 is not None, b2 is not None
             ctx.save_for_backward(W2, H1)
             return out
-        fac = factor_for(adj, xop)
+        dax = dense_ax_for(adj, xop, W1.shape[1], W2.shape[1])
+        fac = factor_for(adj, xop) if dax is None else None
         res = None
-        if fac is not None:
+        if dax is not None:
+            res = dense_gc1(dax, W1, b1, W2, epilogue=epi, mask=mask, scale=scale, keep_prob=keep, seed=seed,
+                            offset=offset, rng_base=rng_base, store_h1=keep_h1)
+        elif fac is not None:
             res = hubfactor_gc1(fac, W1, b1, W2, epilogue=epi, mask=mask, scale=scale, keep_prob=keep, seed=seed,
                                 offset=offset, rng_base=rng_base, store_h1=keep_h1)
         out = None
@@ -555,6 +645,7 @@ class GCNFn(torch.autograd.Function):
         if out is None:
             out = spmm(adj, S2, bias=b2, epilogue=_lib.EPI_BIAS if b2 is not None else _lib.EPI_NONE)
         ctx.xop, ctx.adj, ctx.scale = xop, adj, float(scale)
+        ctx.dax = dax
         ctx.has_b1, ctx.has_b2 = b1 is not None, b2 is not None
         ctx.save_for_backward(W2, H1)
         return out
@@ -586,6 +677,9 @@ class GCNFn(torch.autograd.Function):
                 if ctx.has_b1 and need[1]:
                     gb1 = colsum(gZ1)
         if need[0]:
-            gS1 = spmm(adjT, gZ1)
-            gW1 = ctx.xop.t_times(gS1)
+            if ctx.dax is not None:   # Z1 = (A-hat X) W1  =>  gW1 = (A-hat X)^T gZ1
+                gW1 = gemm(ctx.dax.AX[:, :ctx.dax.K], gZ1, transA=True)
+            else:
+                gS1 = spmm(adjT, gZ1)
+                gW1 = ctx.xop.t_times(gS1)
         return gW1, gb1, gW2, gb2, None, None, None, None, None, None, None, None, None, None

@@ -45,14 +45,16 @@ class GcnFwd(_c.Structure):
 class GcnBwd(_c.Structure):
     """gcnk_gcn_bwd (include/gcnk.h)."""
     _fields_ = [("M", _c.c_int32), ("F", _c.c_int32), ("P", _c.c_int32), ("x_rows", _c.c_int32),
-                ("x_cols", _c.c_int32), ("x_split_k", _c.c_int32), ("aTP", PlanRef), ("aTF", PlanRef),
+                ("x_cols", _c.c_int32), ("x_split_k", _c.c_int32), ("flags", _c.c_int32), ("pad1_", _c.c_int32),
+                ("aTP", PlanRef), ("aTF", PlanRef),
                 ("xT", PlanRef), ("x_dense", _c.c_void_p), ("ldx", _c.c_int64), ("gemm_ws", _c.c_void_p),
                 ("gemm_ws_bytes", _c.c_int64), ("gS2", _c.c_void_p), ("gZ1", _c.c_void_p), ("gS1", _c.c_void_p),
                 ("bwd2_ws", _c.c_void_p), ("bwd2_ws_bytes", _c.c_int64)]
 
 
-FACTORED, SPMM_PROJ, SPMM_GEMM = 1, 2, 3
-KIND_NAMES = {FACTORED: "factored", SPMM_PROJ: "spmm+proj", SPMM_GEMM: "spmm+gemm"}
+FACTORED, SPMM_PROJ, SPMM_GEMM, DENSE_AX = 1, 2, 3, 4
+KIND_NAMES = {FACTORED: "factored", SPMM_PROJ: "spmm+proj", SPMM_GEMM: "spmm+gemm", DENSE_AX: "dense-ax"}
+BWD_AX_DIRECT = 1
 
 
 def layout_ok():
@@ -86,7 +88,7 @@ def _fill_plan(ref, plan, F, lanes, device, keep):
 class ForwardRecord:
     """One filled gcnk_gcn_fwd plus the tensors and plans it points into."""
 
-    __slots__ = ("s", "keep", "kind", "M", "F", "P", "src", "__weakref__")
+    __slots__ = ("s", "keep", "kind", "M", "F", "P", "src", "pinned", "__weakref__")
 
     def __init__(self, adj, xop, F, P, device):
         lib = _lib.load()
@@ -94,8 +96,24 @@ class ForwardRecord:
         s = GcnFwd()
         keep = []
         s.M, s.F, s.P = M, F, P
-        fac = ops.factor_for(adj, xop)
+        dax = ops.dense_ax_for(adj, xop, F, P)
+        fac = ops.factor_for(adj, xop) if dax is None else None
         kind = None
+        if dax is not None:
+            # gc1 from the cached A-hat X: no first product, no F-wide plan
+            kind = DENSE_AX
+            s.Kc, s.U, s.ldu = dax.K, dax.AX.data_ptr(), dax.AX.stride(0)
+            keep.append(dax.AX)
+            s2 = torch.empty((M, P), dtype=torch.float32, device=device)
+            keep.append(s2)
+            s.s2, s.lds2 = s2.data_ptr(), P
+            aP = adj.plan(ops.default_ipc(adj, P, 0), int(lib.gcnk_spmm_groups(P, 0)), DENSE_THRESHOLD)
+            _fill_plan(s.aP, aP, P, 0, device, keep)
+            keep.append(aP)
+            s.kind = kind
+            self.s, self.keep, self.kind, self.M, self.F, self.P = s, keep, kind, M, F, P
+            self.src = (adj, xop.dense)
+            return
         if fac is not None and P <= 32 and F % 4 == 0 and F <= 256 and \
                 int(lib.gcnk_hubfactor_lds_bytes(F, fac.Kc, fac.H, fac.rec_words, P)) <= 160 * 1024:
             kind = FACTORED
@@ -109,7 +127,7 @@ class ForwardRecord:
         else:
             x_csr, x_dense = xop.csr, xop.dense
             plan = None
-            if ops.FUSE_PROJECTION and P <= ops.FUSE_MAX_P:
+            if ops.FUSE_PROJECTION and P <= ops.FUSE_MAX_P and F % 4 == 0 and F <= 256:
                 lanes = 64
                 plan = adj.plan(ops.default_ipc(adj, F, lanes), int(lib.gcnk_spmm_groups(F, lanes)), DENSE_THRESHOLD)
                 # the fused projection runs on plans without dense tile blocks
@@ -118,9 +136,12 @@ class ForwardRecord:
                 lanes = 0
                 plan = adj.plan(ops.default_ipc(adj, F, lanes), int(lib.gcnk_spmm_groups(F, lanes)), DENSE_THRESHOLD)
                 kind = SPMM_GEMM
-                h = torch.empty((M, F), dtype=torch.float32, device=device)
-                keep.append(h)
-                s.h1_tmp, s.ld_h1_tmp = h.data_ptr(), F
+            # H1 scratch for an eval forward: the unfused path's intermediate, and
+            # the fused path's fallback where the library refuses the fusion (an
+            # operand it cannot take as float4, gcnk_gcn_forward_f32)
+            h = torch.empty((M, F), dtype=torch.float32, device=device)
+            keep.append(h)
+            s.h1_tmp, s.ld_h1_tmp = h.data_ptr(), F
             _fill_plan(s.aF, plan, F, lanes, device, keep)
             keep.append(plan)
         # the first product S1 = X W1 (factored: S_T = X_hubs W1)
@@ -174,7 +195,7 @@ class BackwardRecord:
     fused gcn_bwd2, A-hat^T gZ1, X^T gS1) with their plans, workspaces and
     scratch, issued by one ctypes call (bitwise the per-op backward)."""
 
-    __slots__ = ("s", "keep", "M", "F", "P", "x_cols", "src", "__weakref__")
+    __slots__ = ("s", "keep", "M", "F", "P", "x_cols", "src", "pinned", "__weakref__")
 
     def __init__(self, adj, xop, F, P, device):
         lib = _lib.load()
@@ -184,13 +205,25 @@ class BackwardRecord:
         s.M, s.F, s.P = M, F, P
         adjT = adj.t()
         keep.append(adjT)
-        for ref, width in ((s.aTP, P), (s.aTF, F)):
+        dax = ops.dense_ax_for(adj, xop, F, P)
+        for ref, width in ((s.aTP, P), (s.aTF, F)) if dax is None else ((s.aTP, P),):
             pl = adjT.plan(ops.default_ipc(adjT, width, 0), int(lib.gcnk_spmm_groups(width, 0)), DENSE_THRESHOLD)
             _fill_plan(ref, pl, width, 0, device, keep)
             keep.append(pl)
         rows, cols = xop.shape
         s.x_rows, s.x_cols = rows, cols
-        if xop.csr is not None:    # X^T gS1 = spmm(X^T, gS1)  (ops.XOperand.t_times)
+        if dax is not None:        # gW1 = (A-hat X)^T gZ1 (the DENSE_AX forward's association)
+            s.flags = BWD_AX_DIRECT
+            s.x_dense, s.ldx = dax.AX.data_ptr(), dax.AX.stride(0)
+            s.x_rows, s.x_cols = M, dax.K
+            s.x_split_k = ops.default_split_k(dax.K, F, M, trans=True)
+            keep.append(dax.AX)
+            gws = int(lib.gcnk_gemm_workspace_bytes(dax.K, F, M, s.x_split_k))
+            if gws > 0:
+                g = torch.empty((gws + 3) // 4, dtype=torch.float32, device=device)
+                keep.append(g)
+                s.gemm_ws, s.gemm_ws_bytes = g.data_ptr(), gws
+        elif xop.csr is not None:    # X^T gS1 = spmm(X^T, gS1)  (ops.XOperand.t_times)
             xT = xop.csr.t()
             pl = xT.plan(ops.default_ipc(xT, F, 0), int(lib.gcnk_spmm_groups(F, 0)), DENSE_THRESHOLD)
             _fill_plan(s.xT, pl, F, 0, device, keep)
@@ -198,7 +231,7 @@ class BackwardRecord:
         else:                      # gemm(X, gS1, transA=True)
             x = xop.dense
             s.x_dense, s.ldx = x.data_ptr(), x.stride(0)
-            s.x_split_k = ops.default_split_k(cols, F, rows)
+            s.x_split_k = ops.default_split_k(cols, F, rows, trans=True)
             keep.append(x)
             gws = int(lib.gcnk_gemm_workspace_bytes(cols, F, rows, s.x_split_k))
             if gws > 0:
@@ -207,9 +240,12 @@ class BackwardRecord:
                 s.gemm_ws, s.gemm_ws_bytes = g.data_ptr(), gws
         gS2 = torch.empty((M, P), dtype=torch.float32, device=device)
         gZ1 = torch.empty((M, F), dtype=torch.float32, device=device)
-        gS1 = torch.empty((rows, F), dtype=torch.float32, device=device)
-        keep += [gS2, gZ1, gS1]
-        s.gS2, s.gZ1, s.gS1 = gS2.data_ptr(), gZ1.data_ptr(), gS1.data_ptr()
+        keep += [gS2, gZ1]
+        s.gS2, s.gZ1 = gS2.data_ptr(), gZ1.data_ptr()
+        if dax is None:
+            gS1 = torch.empty((rows, F), dtype=torch.float32, device=device)
+            keep.append(gS1)
+            s.gS1 = gS1.data_ptr()
         wsb = int(lib.gcnk_gcn_bwd2_workspace_bytes(M, F, P))
         if wsb > 0:
             w = torch.empty((wsb + 3) // 4, dtype=torch.float32, device=device)
@@ -249,24 +285,46 @@ def get(adj, xop, F, P, device):
 
 
 def _get(adj, xop, F, P, device, cls, tag):
+    """A record's launches bake in raw pointers to its scratch buffers, so a
+    record is rebuilt when either operand's values change in place (the
+    factored operands and plans are derived from them) and a record that was
+    used while a hipGraph was being captured is never evicted: the graph keeps
+    replaying into its buffers.  A record's scratch (S1, S2, H1) is shared by
+    every launch on its stream; a graph captured on that stream replays into
+    it, so two graphs of the same record must not replay concurrently."""
     stream = torch.cuda.current_stream(device).cuda_stream
     src = xop.csr if xop.csr is not None else xop.dense
-    key = (tag, id(src), F, P, stream, ops.FACTOR_GC1, ops.FUSE_PROJECTION)
+    key = (tag, id(src), F, P, stream, ops.FACTOR_GC1, ops.FUSE_PROJECTION, ops.DENSE_AX)
     recs = getattr(adj, "_records", None)
     if recs is None:
         with _lock:
             recs = getattr(adj, "_records", None)
             if recs is None:
                 recs = adj._records = {}
+    capturing = torch.cuda.is_current_stream_capturing()
+    ver = (_version(src), _version(adj))
     hit = recs.get(key)
-    if hit is not None and hit[0] is src and _version(src) == hit[1]:
+    if hit is not None and hit[0] is src and ver == hit[1]:
+        if capturing:
+            hit[2].pinned = True
         return hit[2], stream
     with _lock:
         rec = cls(adj, xop, F, P, device)
+        rec.pinned = capturing
+        old = recs.get(key)
+        if old is not None and old[2].pinned:
+            _PINNED.append(old[2])   # replaced (operands changed) but still referenced by a graph
         while len(recs) >= 8:
-            recs.pop(next(iter(recs)))
-        recs[key] = (src, _version(src), rec)
+            victim = next((k for k, v in recs.items() if not v[2].pinned), None)
+            if victim is None:
+                break
+            recs.pop(victim)
+        recs[key] = (src, ver, rec)
         return rec, stream
+
+
+# records displaced from a cache while a captured graph still points into them
+_PINNED = []
 
 
 def _version(src):

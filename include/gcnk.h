@@ -50,7 +50,7 @@
 extern "C" {
 #endif
 
-#define GCNK_ABI_VERSION 9
+#define GCNK_ABI_VERSION 10
 
 #define GCNK_OK 0
 #define GCNK_EARG (-1)
@@ -269,6 +269,27 @@ int gcnk_hubfactor_gc1_f32(int32_t M, int32_t F, int32_t Kc, int32_t nhub, int32
                            uint64_t offset, const uint64_t* rng_base, const float* W2, int64_t ldw2, float* H,
                            int64_t ldh, float* C2, int64_t ldc2, void* stream);
 
+/* ---------------------------------------------------------------------------
+ * Narrow-feature gc1 (csrc/dense_gc1.hip; GCN.forward layer.py:164-190 through
+ * layer.py:102,106,110,182,185 and gc2's support layer.py:102) for a dense X
+ * with at most 128 features (the gensim-shaped topic features, README.md:77,95):
+ * with AX = A-hat X [M x K] (ldax >= K, gcnk_aggregate_f32, built once per
+ * (A-hat, X) pair),
+ *   H[r, n]  = epilogue((AX W1)[r, n] + bias[n])   (GCNK_EPI_BIAS_RELU[_DROP|_HASH])
+ *   C2[r, p] = sum_n H[r, n] W2[n, p]
+ * in one launch (fp32 MFMA, fixed-order sums).  H nullable (not stored).
+ * K <= 128, F <= 256, P <= 32 (GCNK_EUNSUP otherwise).  The association
+ * (A-hat X) W1 differs from the reference's A-hat (X W1) in fp32 rounding only.
+ *   gcnk_aggregate_f32: out[r, c] = fp32( sum over row r's items in CSR order,
+ *   in float64, of val * X[col, c] ), c < K; 0 for K <= c < Kp <= 128.
+ * ------------------------------------------------------------------------- */
+int gcnk_dense_gc1_f32(int32_t M, int32_t K, int32_t F, int32_t P, const float* AX, int64_t ldax, const float* W1,
+                       int64_t ldw1, const float* bias, int32_t epilogue, const uint8_t* drop_mask, int64_t ldm,
+                       float drop_scale, float keep_prob, uint64_t seed, uint64_t offset, const uint64_t* rng_base,
+                       const float* W2, int64_t ldw2, float* H, int64_t ldh, float* C2, int64_t ldc2, void* stream);
+int gcnk_aggregate_f32(const int32_t* rowptr, const int32_t* colind, const float* val, int32_t M, const float* X,
+                       int64_t ldx, int32_t K, float* out, int64_t ldo, int32_t Kp, void* stream);
+
 /* The hub factorisation's (A-hat, X)-fixed operands, built on the device once
  * per operand pair (csrc/factor_build.hip; factor.py drives it, the host
  * restatement is oracle/factor_host.py):
@@ -303,6 +324,8 @@ int gcnk_factor_records(const int32_t* rowptr, const int32_t* colind, const floa
  *                       (H1, S2) = gcnk_hubfactor_gc1_f32; out = A-hat S2 + b2
  *   GCNK_FWD_SPMM_PROJ  S1 = X W1; (H1, S2) = gcnk_spmm_proj_f32(aF); out = A-hat S2 + b2
  *   GCNK_FWD_SPMM_GEMM  S1 = X W1; H1 = epi(A-hat S1 + b1) (aF); S2 = H1 W2; out = A-hat S2 + b2
+ *   GCNK_FWD_DENSE_AX   (H1, S2) = gcnk_dense_gc1_f32(U = A-hat X [M x Kc], ldu); out = A-hat S2 + b2
+ *                       (no first product: x, s1 unused)
  *
  * gc2's aggregation uses the plan aP with GCNK_EPI_BIAS (GCNK_EPI_NONE when b2
  * is NULL).  W1 [x_cols x F] and W2 [F x P] contiguous; H1 (ldh) is stored
@@ -324,6 +347,7 @@ typedef struct gcnk_plan_ref {
 #define GCNK_FWD_FACTORED 1
 #define GCNK_FWD_SPMM_PROJ 2
 #define GCNK_FWD_SPMM_GEMM 3
+#define GCNK_FWD_DENSE_AX 4
 
 typedef struct gcnk_gcn_fwd {
   int32_t kind;
@@ -338,7 +362,7 @@ typedef struct gcnk_gcn_fwd {
   int64_t gemm_ws_bytes;
   float* s1;                   /* S1 = X W1, or S_T = X_hubs W1 [x_rows x F] */
   int64_t lds1;
-  int32_t Kc, nhub, k0, rec_words;   /* factored gc1 (gcnk_hubfactor_gc1_f32) */
+  int32_t Kc, nhub, k0, rec_words;   /* factored gc1 (gcnk_hubfactor_gc1_f32); DENSE_AX: Kc = K */
   const float* U;
   int64_t ldu;
   const int32_t* rec;
@@ -364,11 +388,16 @@ int gcnk_gcn_forward_f32(const gcnk_gcn_fwd* rec,
  *   gS1 = A-hat^T gZ1; gW1 = X^T gS1         (aTF; X^T's plan xT, or the MFMA
  *                                             GEMM on dense X with x_split_k)
  * G = dlogits [M x P] (contiguous), H1 [M x F] (ldh), W2 [F x P].  gW1, gb1,
- * gW2, gb2 are nullable (not computed); gb2 needs G's column sums only. */
+ * gW2, gb2 are nullable (not computed); gb2 needs G's column sums only.
+ * flags & GCNK_BWD_AX_DIRECT: x_dense holds A-hat X (the DENSE_AX forward) and
+ * gW1 = (A-hat X)^T gZ1 directly (no gS1, no aTF plan). */
+#define GCNK_BWD_AX_DIRECT 1
 typedef struct gcnk_gcn_bwd {
   int32_t M, F, P;             /* rows of A-hat, nhid, nclass */
   int32_t x_rows, x_cols;      /* X [x_rows x x_cols]: gW1 is [x_cols x F] */
   int32_t x_split_k;           /* dense X: K-slabs of X^T gS1 */
+  int32_t flags;               /* GCNK_BWD_* */
+  int32_t pad1_;
   gcnk_plan_ref aTP, aTF;      /* A-hat^T at widths P and F */
   gcnk_plan_ref xT;            /* sparse X: X^T's plan at width F (xT.plan != NULL) ... */
   const float* x_dense;        /* ... or dense X (ldx) */

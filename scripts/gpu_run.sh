@@ -1,0 +1,63 @@
+#!/bin/bash
+# One parameterised GPU-box driver (round 5 on; replaces the per-step rNN_stepK.sh
+# scripts): every step runs under its own time limit, output goes to
+# gpurun_out/<tag>/, and the first failing step ends the call.
+#
+# usage: scripts/gpu_run.sh <tag> <step> [<step> ...]
+#   micro:<binary>[:<args>]   prebuilt scripts/micro/<binary> on the R8 A-hat (NS_ONLY, PROF honoured)
+#   test:<pytest -k expr>     GPU tests matching the expression (-m gpu)
+#   tests                     the whole GPU suite
+#   bench[:<args>]            python bench.py <args> (default --steps 200 --warmup 20) -> bench.json
+#   prof:<script>[:<args>]    rocprofv3 --kernel-trace --stats over python scripts/<script> -> <script>_stats/
+#   py:<script>[:<args>]      python scripts/<script> <args> -> <script>.log
+# Steps' outputs are summarised in profiles/ by hand (profiles/INDEX.md).
+cd "${GRAFT_REPO_ROOT:-/root/repo}" || exit 2
+export TMPDIR=/tmp
+tag="$1"; shift
+out="gpurun_out/$tag"
+mkdir -p "$out"
+for step in "$@"; do
+  kind="${step%%:*}"; rest="${step#*:}"; [ "$rest" = "$step" ] && rest=""
+  echo "=== $step" | tee -a "$out/steps.log"
+  case "$kind" in
+    micro)
+      bin="${rest%%:*}"; args="${rest#*:}"; [ "$args" = "$rest" ] && args=""
+      python3 scripts/micro/dump_r8.py /tmp/r8_adj.bin > /dev/null || exit 3
+      timeout -k 10 240 "scripts/micro/$bin" /tmp/r8_adj.bin $args > "$out/$bin.log" 2>&1
+      rc=$?; tail -n 80 "$out/$bin.log"; [ $rc -eq 0 ] || { echo "rc=$rc"; exit 3; }
+      if [ -n "$PROF" ]; then
+        timeout -k 10 240 rocprofv3 --kernel-trace --stats --output-format csv -d "$out/${bin}_prof" -o kt -- \
+          "scripts/micro/$bin" /tmp/r8_adj.bin $args > "$out/${bin}_prof.log" 2>&1 || { echo "prof rc=$?"; exit 3; }
+      fi ;;
+    test)
+      timeout -k 10 900 python -u -m pytest tests -m gpu -x -q --timeout 300 --timeout-method thread -k "$rest" \
+        > "$out/pytest_$(echo "$rest" | tr -c 'A-Za-z0-9_' '_' | cut -c1-40).log" 2>&1
+      rc=$?; tail -n 25 "$out"/pytest_*.log | tail -n 25; [ $rc -eq 0 ] || { echo "rc=$rc"; exit 3; } ;;
+    tests)
+      timeout -k 10 1000 python -u -m pytest tests -m gpu -x -q --timeout 300 --timeout-method thread \
+        > "$out/pytest_gpu.log" 2>&1
+      rc=$?; tail -n 15 "$out/pytest_gpu.log"; [ $rc -eq 0 ] || { echo "rc=$rc"; exit 3; } ;;
+    bench)
+      args="${rest:---steps 200 --warmup 20}"
+      timeout -k 10 900 python -u bench.py $args --rocprof-dir "$out/bench_prof" > "$out/bench.json" 2> "$out/bench.err"
+      rc=$?; tail -c 3000 "$out/bench.json"; [ $rc -eq 0 ] || { echo "rc=$rc"; tail -n 20 "$out/bench.err"; exit 3; } ;;
+    prof)
+      s="${rest%%:*}"; args="${rest#*:}"; [ "$args" = "$rest" ] && args=""
+      timeout -k 10 400 rocprofv3 --kernel-trace --stats --output-format csv -d "$out/${s%.py}_stats" -o kt -- \
+        python3 "scripts/$s" $args > "$out/${s%.py}_prof.log" 2>&1
+      rc=$?; tail -n 30 "$out/${s%.py}_prof.log"; [ $rc -eq 0 ] || { echo "rc=$rc"; exit 3; }
+      python3 - "$out/${s%.py}_stats" <<'PY'
+import csv, glob, sys
+for f in glob.glob(f"{sys.argv[1]}/**/*kernel_stats.csv", recursive=True):
+    for r in csv.DictReader(open(f)):
+        print(f"  {r['Name'][:100]:100s} calls {r['Calls']:>6s} avg {float(r['AverageNs'])/1e3:8.2f} us")
+PY
+      ;;
+    py)
+      s="${rest%%:*}"; args="${rest#*:}"; [ "$args" = "$rest" ] && args=""
+      timeout -k 10 600 python3 -u "scripts/$s" $args > "$out/${s%.py}.log" 2>&1
+      rc=$?; tail -n 60 "$out/${s%.py}.log"; [ $rc -eq 0 ] || { echo "rc=$rc"; exit 3; } ;;
+    *) echo "unknown step $step"; exit 2 ;;
+  esac
+done
+echo "=== all steps done"

@@ -1,0 +1,585 @@
+// Standalone microbenchmark: schedules for the hub (topic) rows of the north-star op
+// (R8 A-hat x S1, F = 200, bias + ReLU), measured against the product's
+// segment + last-arriver combine.  Not the product library: it decides what
+// moves into csrc/spmm.hip.
+//
+//  * light rows: as scripts/micro/ns_micro.hip (one wave per row, its items in
+//    one window load, gathers, nontemporal store).
+//  * hub rows, "seg": the product schedule -- 48-item segments cut at XCD
+//    column-class boundaries, one 4-wave workgroup each, partials handed off
+//    (sc1) to the last arriver.
+//  * hub rows, "slice": one workgroup per (hub row, SL-float4 column slice).
+//    All its waves walk the row's WHOLE item list (lane = item group x column
+//    of the slice), the groups meet by an xor butterfly, the waves in LDS, and
+//    wave 0 stores the slice.  No partial store, no counter, no coherent
+//    reload.  Slice s runs on XCD s % 8 (workgroup b -> XCD b % 8), so each
+//    XCD's L2 serves one column slice of B.  With a row pitch that is a
+//    multiple of 32 floats a 32-float slice is one 128-B line per item.
+//   build: hipcc -O3 --offload-arch=gfx950 -std=c++17 slice_micro.hip -o slice_micro
+//   run:   python scripts/micro/dump_r8.py /tmp/r8_adj.bin && ./slice_micro /tmp/r8_adj.bin
+#include <hip/hip_runtime.h>
+
+#include <algorithm>
+#include <cmath>
+#include <cstdio>
+#include <cstdlib>
+#include <cstring>
+#include <functional>
+#include <string>
+#include <vector>
+
+#define CHECK(x)                                                                         \
+  do {                                                                                   \
+    hipError_t e_ = (x);                                                                 \
+    if (e_ != hipSuccess) {                                                              \
+      fprintf(stderr, "%s:%d %s: %s\n", __FILE__, __LINE__, #x, hipGetErrorString(e_)); \
+      exit(2);                                                                           \
+    }                                                                                    \
+  } while (0)
+
+constexpr int NX = 8;         // XCD classes
+constexpr int WIN = 64;       // off-diagonal items per light wave
+constexpr int kColBits = 27;  // window item col field; row-in-wave above it
+
+typedef float f32v4 __attribute__((ext_vector_type(4)));
+__device__ __forceinline__ __amdgpu_buffer_rsrc_t rsrc(const void* base) {
+  return __builtin_amdgcn_make_buffer_rsrc(const_cast<void*>(base), (short)0, 0x7fffffff, 0x00020000);
+}
+__device__ __forceinline__ void st_sc1(const void* base, int off_bytes, const float4& v) {
+  const f32v4 x = {v.x, v.y, v.z, v.w};
+  __builtin_amdgcn_raw_buffer_store_b128(x, rsrc(base), off_bytes, 0, 16);
+}
+__device__ __forceinline__ float4 ld_sc1(const void* base, int off_bytes) {
+  const f32v4 x = __builtin_amdgcn_raw_buffer_load_b128(rsrc(base), off_bytes, 0, 16);
+  return make_float4(x.x, x.y, x.z, x.w);
+}
+__device__ __forceinline__ void fma4(float4& a, float s, const float4& b) {
+  a.x = fmaf(s, b.x, a.x); a.y = fmaf(s, b.y, a.y); a.z = fmaf(s, b.z, a.z); a.w = fmaf(s, b.w, a.w);
+}
+__device__ __forceinline__ void add4(float4& a, const float4& b) { a.x += b.x; a.y += b.y; a.z += b.z; a.w += b.w; }
+__device__ __forceinline__ float4 relu_bias(float4 a, float4 b) {
+  a.x = fmaxf(a.x + b.x, 0.f); a.y = fmaxf(a.y + b.y, 0.f); a.z = fmaxf(a.z + b.z, 0.f); a.w = fmaxf(a.w + b.w, 0.f);
+  return a;
+}
+__device__ __forceinline__ int rl(int v, int i) { return __builtin_amdgcn_readlane(v, i); }
+__device__ __forceinline__ void store_nt(float4* C, int64_t idx, const float4& v) {
+  const f32v4 x = {v.x, v.y, v.z, v.w};
+  __builtin_nontemporal_store(x, reinterpret_cast<f32v4*>(C + idx));
+}
+
+template <int OFF>
+__device__ __forceinline__ float xor_lane(float v) {
+  if constexpr (OFF < 32)
+    return __int_as_float(__builtin_amdgcn_ds_swizzle(__float_as_int(v), (OFF << 10) | 0x1F));
+  else
+    return __shfl_xor(v, OFF, 64);
+}
+template <int OFF>
+__device__ __forceinline__ void xor_sum_from(float4& a) {
+  if constexpr (OFF < 64) {
+    a.x += xor_lane<OFF>(a.x); a.y += xor_lane<OFF>(a.y); a.z += xor_lane<OFF>(a.z); a.w += xor_lane<OFF>(a.w);
+    xor_sum_from<OFF * 2>(a);
+  }
+}
+
+struct Args {
+  const float4* B; float4* C; const float4* bias;
+  int M, Q, P4;            // Q float4 columns (F / 4), P4 = row pitch of B and C in float4
+  int rpc;                 // light: rows per class
+  const int2* win;         // [M / RPW][WIN] {col | k << kColBits, val}
+  const int2* rowinfo;     // [M] {diag bits, 1 light / 0 hub}
+  const int4* units;       // heavy units
+  const int2* items;       // CSR items {col, val bits}
+  const int4* heavy; float4* part; int* ctr;   // seg: {row, first slot, nseg, 0}
+  int nhb;
+  unsigned long long* stamps;
+};
+
+__device__ __forceinline__ void stamp(const Args& a, int k) {
+  if (a.stamps && threadIdx.x == 0) a.stamps[4 * blockIdx.x + k] = __builtin_amdgcn_s_memrealtime();
+}
+
+// ---------------------------------------------------------------------------
+// light role (ns_micro's): wave (b, wv) -> rows row0 .. row0 + RPW - 1
+template <int WPB, int RPW, int U>
+__device__ void light_role(const Args& a, int b) {
+  const int lane = threadIdx.x & 63;
+  const int wv = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  constexpr int RB = WPB * RPW;
+  const int c = b % NX, k = b / NX;
+  const int row0 = c * a.rpc + k * RB + wv * RPW;  // wave-uniform
+  if (row0 >= a.M) return;
+  const int col = lane < a.Q ? lane : 0;
+  float4 self[RPW];
+#pragma unroll
+  for (int r = 0; r < RPW; ++r) {
+    const int row = row0 + r;
+    self[r] = row < a.M ? a.B[(int64_t)row * a.P4 + col] : make_float4(0.f, 0.f, 0.f, 0.f);
+  }
+  const int2 it = a.win[(int64_t)(row0 / RPW) * WIN + lane];
+  const int2 ri = (lane < RPW && row0 + lane < a.M) ? a.rowinfo[row0 + lane] : make_int2(0, 0);
+  const float4 bv = a.bias[col];
+  const int kr = it.x >= 0 ? (int)((unsigned)it.x >> kColBits) : RPW;
+  int nb[RPW + 1];
+  nb[0] = 0;
+#pragma unroll
+  for (int r = 0; r < RPW; ++r) nb[r + 1] = nb[r] + __builtin_popcountll(__ballot(kr == r));
+  const int cnt = nb[RPW];
+  float4 acc[RPW];
+#pragma unroll
+  for (int r = 0; r < RPW; ++r) {
+    const float d = __int_as_float(rl(ri.x, r));
+    acc[r] = make_float4(d * self[r].x, d * self[r].y, d * self[r].z, d * self[r].w);
+  }
+  for (int j0 = 0; j0 < cnt; j0 += U) {
+    float4 g[U];
+    float w[U];
+#pragma unroll
+    for (int j = 0; j < U; ++j) {
+      g[j] = make_float4(0.f, 0.f, 0.f, 0.f);
+      w[j] = 0.f;
+      if (j0 + j < cnt) {
+        const int cc = rl(it.x, j0 + j) & ((1 << kColBits) - 1);
+        w[j] = __int_as_float(rl(it.y, j0 + j));
+        g[j] = a.B[(int64_t)cc * a.P4 + col];
+      }
+    }
+#pragma unroll
+    for (int j = 0; j < U; ++j)
+#pragma unroll
+      for (int r = 0; r < RPW; ++r)
+        if (j0 + j >= nb[r] && j0 + j < nb[r + 1]) fma4(acc[r], w[j], g[j]);
+  }
+#pragma unroll
+  for (int r = 0; r < RPW; ++r)
+    if (rl(ri.y, r) && lane < a.Q) store_nt(a.C, (int64_t)(row0 + r) * a.P4 + lane, relu_bias(acc[r], bv));
+}
+
+// ---------------------------------------------------------------------------
+// seg role: the product's heavy schedule (one piece per workgroup, last-arriver combine)
+template <int WPB, int UH>
+__device__ void seg_role(const Args& a, int u) {
+  __shared__ float4 s_red[WPB][64];
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int wv = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int4 un = a.units[u];
+  if (un.x < 0) return;
+  const int col = lane < a.Q ? lane : 0;
+  const float4 bv = a.bias[col];
+  const int kb = un.y + wv, e = un.z;
+  const int k = kb + WPB * lane;
+  const int2 mine = k < e ? a.items[k] : make_int2(0, 0);
+  __builtin_amdgcn_s_waitcnt(0x0F70);
+  const int cnt = e > kb ? min(64, (e - kb + WPB - 1) / WPB) : 0;
+  float4 acc = make_float4(0.f, 0.f, 0.f, 0.f);
+  for (int j0 = 0; j0 < cnt; j0 += UH) {
+    float4 g[UH];
+    float w[UH];
+#pragma unroll
+    for (int j = 0; j < UH; ++j) {
+      g[j] = make_float4(0.f, 0.f, 0.f, 0.f);
+      w[j] = 0.f;
+      if (j0 + j < cnt) {
+        w[j] = __int_as_float(rl(mine.y, j0 + j));
+        g[j] = a.B[(int64_t)rl(mine.x, j0 + j) * a.P4 + col];
+      }
+    }
+#pragma unroll
+    for (int j = 0; j < UH; ++j) fma4(acc, w[j], g[j]);
+  }
+  if (wv > 0) s_red[wv][lane] = acc;
+  __syncthreads();
+  if (wv > 0) return;
+#pragma unroll
+  for (int v = 1; v < WPB; ++v) add4(acc, s_red[v][lane]);
+  if (un.w < 0) {
+    if (lane < a.Q) store_nt(a.C, (int64_t)un.x * a.P4 + lane, relu_bias(acc, bv));
+    return;
+  }
+  const int hid = un.w >> 6, seg = un.w & 63;
+  const int4 hv = a.heavy[hid];
+  const float4* p0 = a.part + (int64_t)hv.y * a.Q;
+  if (lane < a.Q) st_sc1(p0, (seg * a.Q + lane) * 16, acc);
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  int arrived = 0;
+  if (lane == 0) arrived = __hip_atomic_fetch_add(a.ctr + hid, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  if (__builtin_amdgcn_readfirstlane(arrived) != hv.z - 1) return;
+  float4 sum = make_float4(0.f, 0.f, 0.f, 0.f);
+  for (int s0 = 0; s0 < hv.z; s0 += 16) {
+    float4 pv[16];
+#pragma unroll
+    for (int j = 0; j < 16; ++j) pv[j] = s0 + j < hv.z ? ld_sc1(p0, ((s0 + j) * a.Q + col) * 16) : make_float4(0.f, 0.f, 0.f, 0.f);
+#pragma unroll
+    for (int j = 0; j < 16; ++j) add4(sum, pv[j]);
+  }
+  if (lane < a.Q) store_nt(a.C, (int64_t)hv.x * a.P4 + lane, relu_bias(sum, bv));
+  if (lane == 0) __hip_atomic_store(a.ctr + hid, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+
+// ---------------------------------------------------------------------------
+// slice role: unit {row, nz begin, nz end, slice}; SL float4 columns per slice,
+// G = 64 / SL item groups per wave; the WG's WPB * G groups take items
+// begin + grp, begin + grp + S, ... (S = WPB * G), U per batch, the next
+// batch's item words loaded under the current batch's gathers.
+template <int WPB, int SL, int U>
+__device__ void slice_role(const Args& a, int u) {
+  constexpr int G = 64 / SL;
+  constexpr int S = WPB * G;
+  __shared__ float4 s_red[WPB][SL];
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int wv = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int4 un = a.units[u];
+  if (un.x < 0) return;  // padding (workgroup-uniform)
+  const int g = lane / SL, c = lane % SL;
+  const int col = un.w * SL + c;
+  const bool colok = col < a.Q;
+  const int colc = colok ? col : 0;
+  const int e = un.z;
+  int k = un.y + wv * G + g;
+  float4 acc = make_float4(0.f, 0.f, 0.f, 0.f);
+  int2 it[U];
+#pragma unroll
+  for (int j = 0; j < U; ++j) it[j] = k + S * j < e ? a.items[k + S * j] : make_int2(0, 0);
+  for (; k < e; k += S * U) {
+    float4 gv[U];
+#pragma unroll
+    for (int j = 0; j < U; ++j) gv[j] = a.B[(int64_t)it[j].x * a.P4 + colc];  // padding: row 0, weight 0
+    float w[U];
+#pragma unroll
+    for (int j = 0; j < U; ++j) w[j] = __int_as_float(it[j].y);
+    const int kn = k + S * U;
+#pragma unroll
+    for (int j = 0; j < U; ++j) it[j] = kn + S * j < e ? a.items[kn + S * j] : make_int2(0, 0);
+#pragma unroll
+    for (int j = 0; j < U; ++j) fma4(acc, w[j], gv[j]);
+  }
+  xor_sum_from<SL>(acc);  // the wave's G groups (every lane of column c ends with the same sum)
+  if (g == 0) s_red[wv][c] = acc;
+  __syncthreads();
+  if (wv == 0 && lane < SL) {
+    float4 sum = s_red[0][c];
+#pragma unroll
+    for (int v = 1; v < WPB; ++v) add4(sum, s_red[v][c]);
+    if (colok) store_nt(a.C, (int64_t)un.x * a.P4 + col, relu_bias(sum, a.bias[col]));
+  }
+}
+
+template <int WPB, int RPW, int U, int UH>
+__global__ void __launch_bounds__(WPB * 64) seg_kernel(Args a) {
+  stamp(a, 0);
+  const int b = blockIdx.x;
+  if (b < a.nhb) seg_role<WPB, UH>(a, b);
+  else light_role<WPB, RPW, U>(a, b - a.nhb);
+  stamp(a, 3);
+}
+template <int WPB, int RPW, int U, int SL, int US>
+__global__ void __launch_bounds__(WPB * 64) slice_kernel(Args a) {
+  stamp(a, 0);
+  const int b = blockIdx.x;
+  if (b < a.nhb) slice_role<WPB, SL, US>(a, b);
+  else light_role<WPB, RPW, U>(a, b - a.nhb);
+  stamp(a, 3);
+}
+__global__ void copy_nt(const float4* __restrict__ a, float4* __restrict__ b, int n) {
+  for (int i = blockIdx.x * blockDim.x + threadIdx.x; i < n; i += gridDim.x * blockDim.x) store_nt(b, i, a[i]);
+}
+
+// ---------------------------------------------------------------------------
+struct Csr {
+  int M = 0, nnz = 0;
+  std::vector<int> rp, ci;
+  std::vector<float> v;
+};
+static Csr read_csr(const char* path) {
+  Csr c;
+  FILE* f = fopen(path, "rb");
+  if (!f) { perror(path); exit(2); }
+  int hdr[2];
+  if (fread(hdr, 4, 2, f) != 2) exit(2);
+  c.M = hdr[0]; c.nnz = hdr[1];
+  c.rp.resize(c.M + 1); c.ci.resize(c.nnz); c.v.resize(c.nnz);
+  if (fread(c.rp.data(), 4, c.M + 1, f) != (size_t)c.M + 1) exit(2);
+  if (fread(c.ci.data(), 4, c.nnz, f) != (size_t)c.nnz) exit(2);
+  if (fread(c.v.data(), 4, c.nnz, f) != (size_t)c.nnz) exit(2);
+  fclose(f);
+  return c;
+}
+
+struct Plan {
+  std::string name;
+  int WPB, RPW, rpc, nlwg, nhb;
+  std::vector<int2> win, rowinfo, items;
+  std::vector<int4> units, heavy;
+  int nslots = 0, nheavy = 0;
+};
+
+static void light_part(const Csr& A, const std::vector<char>& hub, Plan& P) {
+  const int M = A.M, RB = P.WPB * P.RPW;
+  P.rpc = ((M + NX - 1) / NX + RB - 1) / RB * RB;
+  P.nlwg = NX * (P.rpc / RB);
+  const int nwave = (NX * P.rpc) / P.RPW;
+  P.win.assign((size_t)nwave * WIN, make_int2(-1, 0));
+  P.rowinfo.assign(M, make_int2(0, 0));
+  for (int w = 0; w < nwave; ++w) {
+    int n = 0;
+    for (int k = 0; k < P.RPW; ++k) {
+      const int r = w * P.RPW + k;
+      if (r >= M || hub[r]) continue;
+      float d = 0.f;
+      for (int q = A.rp[r]; q < A.rp[r + 1]; ++q) {
+        if (A.ci[q] == r) { d += A.v[q]; continue; }
+        if (n >= WIN) { fprintf(stderr, "light window overflow at wave %d\n", w); exit(2); }
+        P.win[(size_t)w * WIN + n++] = make_int2(A.ci[q] | (k << kColBits), __builtin_bit_cast(int, A.v[q]));
+      }
+      P.rowinfo[r] = make_int2(__builtin_bit_cast(int, d), 1);
+    }
+  }
+  P.items.resize(A.nnz);
+  for (int i = 0; i < A.nnz; ++i) P.items[i] = make_int2(A.ci[i], __builtin_bit_cast(int, A.v[i]));
+}
+
+// product-like segments (cut at column-class boundaries and every SEG items)
+static Plan seg_plan(const Csr& A, const std::vector<char>& hub, int WPB, int RPW, int SEG) {
+  Plan P{};
+  P.WPB = WPB; P.RPW = RPW;
+  light_part(A, hub, P);
+  std::vector<std::vector<int4>> q(NX);
+  auto cls = [&](int c) { return std::min(NX - 1, c / P.rpc); };
+  for (int r = 0; r < A.M; ++r) {
+    if (!hub[r]) continue;
+    const int b = A.rp[r], e = A.rp[r + 1];
+    std::vector<int4> segs;
+    int s = b;
+    while (s < e) {
+      const int c = cls(A.ci[s]);
+      int t = s;
+      while (t < e && cls(A.ci[t]) == c && t - s < SEG) ++t;
+      segs.push_back(make_int4(r, s, t, c));
+      s = t;
+    }
+    const int nseg = (int)segs.size();
+    const int hid = P.nheavy;
+    if (nseg > 1) {
+      P.heavy.push_back(make_int4(r, P.nslots, nseg, 0));
+      P.nslots += nseg;
+      ++P.nheavy;
+    }
+    for (int i = 0; i < nseg; ++i) q[segs[i].w].push_back(make_int4(r, segs[i].y, segs[i].z, nseg > 1 ? hid * 64 + i : -1));
+    if (nseg > 64) { fprintf(stderr, "too many segments\n"); exit(2); }
+  }
+  size_t rounds = 0;
+  for (auto& x : q) rounds = std::max(rounds, x.size());
+  for (size_t k = 0; k < rounds; ++k)
+    for (int c = 0; c < NX; ++c) P.units.push_back(k < q[c].size() ? q[c][k] : make_int4(-1, 0, 0, -1));
+  P.nhb = (int)P.units.size();
+  char nm[96];
+  snprintf(nm, sizeof nm, "seg WPB%d SEG%d", WPB, SEG);
+  P.name = nm;
+  return P;
+}
+
+// slices: every hub row x ceil(Q / SL) slices; slice s on XCD s % 8, longest rows first
+static Plan slice_plan(const Csr& A, const std::vector<char>& hub, int WPB, int RPW, int SL, int Q) {
+  Plan P{};
+  P.WPB = WPB; P.RPW = RPW;
+  light_part(A, hub, P);
+  std::vector<int> rows;
+  for (int r = 0; r < A.M; ++r) if (hub[r]) rows.push_back(r);
+  std::sort(rows.begin(), rows.end(), [&](int x, int y) { return A.rp[x + 1] - A.rp[x] > A.rp[y + 1] - A.rp[y]; });
+  const int ns = (Q + SL - 1) / SL;
+  std::vector<std::vector<int4>> q(NX);
+  for (int r : rows)
+    for (int s = 0; s < ns; ++s) q[s % NX].push_back(make_int4(r, A.rp[r], A.rp[r + 1], s));
+  size_t rounds = 0;
+  for (auto& x : q) rounds = std::max(rounds, x.size());
+  for (size_t k = 0; k < rounds; ++k)
+    for (int c = 0; c < NX; ++c) P.units.push_back(k < q[c].size() ? q[c][k] : make_int4(-1, 0, 0, 0));
+  P.nhb = (int)P.units.size();
+  char nm[96];
+  snprintf(nm, sizeof nm, "slice WPB%d SL%d", WPB, SL);
+  P.name = nm;
+  return P;
+}
+
+template <typename T>
+static T* upload(const std::vector<T>& h) {
+  T* d;
+  CHECK(hipMalloc(&d, std::max<size_t>(1, h.size()) * sizeof(T)));
+  if (!h.empty()) CHECK(hipMemcpy(d, h.data(), h.size() * sizeof(T), hipMemcpyHostToDevice));
+  return d;
+}
+
+struct Built {
+  Plan P;
+  int2 *win, *rowinfo, *items;
+  int4 *units, *heavy;
+  float4* part;
+  int* ctr;
+};
+static Built build(Plan P, int Q) {
+  Built b;
+  b.P = std::move(P);
+  b.win = upload(b.P.win); b.rowinfo = upload(b.P.rowinfo); b.items = upload(b.P.items);
+  b.units = upload(b.P.units); b.heavy = upload(b.P.heavy);
+  CHECK(hipMalloc(&b.part, (size_t)std::max(1, b.P.nslots) * Q * 16));
+  CHECK(hipMalloc(&b.ctr, (size_t)std::max(1, b.P.nheavy) * 4));
+  CHECK(hipMemset(b.ctr, 0, (size_t)std::max(1, b.P.nheavy) * 4));
+  printf("{\"plan\": \"%s\", \"light_wg\": %d, \"heavy_wg\": %d, \"slots\": %d}\n", b.P.name.c_str(), b.P.nlwg, b.P.nhb,
+         b.P.nslots);
+  return b;
+}
+
+int main(int argc, char** argv) {
+  const char* path = argc > 1 ? argv[1] : "/tmp/r8_adj.bin";
+  const Csr A = read_csr(path);
+  const int F = 200, Q = F / 4, M = A.M;
+  std::vector<char> hub(M);
+  for (int r = 0; r < M; ++r) hub[r] = A.rp[r + 1] - A.rp[r] >= 64;
+  const int pitches[2] = {50, 56};  // row pitch in float4: 200 floats, 224 floats (896 B = 7 lines)
+  const size_t matmax = (size_t)M * 56 * 4;
+  const int nsets = std::max(2, (int)(320e6 / (8.0 * (size_t)M * F)) + 1);
+  std::vector<float*> Bs(nsets), Cs(nsets);
+  std::vector<float> hbias(F);
+  srand(1);
+  for (auto& x : hbias) x = (rand() / (float)RAND_MAX - 0.5f) * 0.1f;
+  std::vector<float> hB0((size_t)M * F);
+  for (auto& x : hB0) x = rand() / (float)RAND_MAX - 0.5f;
+  for (int s = 0; s < nsets; ++s) {
+    CHECK(hipMalloc(&Bs[s], matmax * 4));
+    CHECK(hipMalloc(&Cs[s], matmax * 4));
+  }
+  std::vector<double> ref((size_t)M * F);
+  for (int r = 0; r < M; ++r)
+    for (int f = 0; f < F; ++f) {
+      double acc = 0;
+      for (int k = A.rp[r]; k < A.rp[r + 1]; ++k) acc += (double)A.v[k] * hB0[(size_t)A.ci[k] * F + f];
+      ref[(size_t)r * F + f] = std::max(0.0, acc + hbias[f]);
+    }
+  float* d_bias = upload(hbias);
+  unsigned long long* d_st;
+  CHECK(hipMalloc(&d_st, (size_t)65536 * 32));
+  hipStream_t st;
+  CHECK(hipStreamCreate(&st));
+
+  std::vector<Built> plans;
+  plans.push_back(build(seg_plan(A, hub, 4, 1, 48), Q));     // 0
+  plans.push_back(build(slice_plan(A, hub, 4, 1, 8, Q), Q));  // 1
+  plans.push_back(build(slice_plan(A, hub, 8, 1, 8, Q), Q));  // 2
+  plans.push_back(build(slice_plan(A, hub, 16, 1, 8, Q), Q)); // 3
+  plans.push_back(build(slice_plan(A, hub, 16, 1, 4, Q), Q)); // 4
+  plans.push_back(build(slice_plan(A, hub, 16, 1, 16, Q), Q));// 5
+  plans.push_back(build(slice_plan(A, hub, 8, 1, 4, Q), Q));  // 6
+
+  int P4 = 50;
+  auto args = [&](const Built& b, int s, int nhb) {
+    Args a{};
+    a.B = reinterpret_cast<const float4*>(Bs[s]); a.C = reinterpret_cast<float4*>(Cs[s]);
+    a.bias = reinterpret_cast<const float4*>(d_bias);
+    a.M = M; a.Q = Q; a.P4 = P4; a.rpc = b.P.rpc; a.win = b.win; a.rowinfo = b.rowinfo;
+    a.units = b.units; a.heavy = b.heavy; a.items = b.items; a.part = b.part; a.ctr = b.ctr; a.nhb = nhb;
+    return a;
+  };
+  struct Variant { std::string name; std::function<void(int, unsigned long long*)> run; int check; int grid; };
+  std::vector<Variant> vs;
+  // which: 0 all rows, 1 light rows only, 2 hub rows only
+  auto add = [&](const std::string& name, int pi, int which, auto kern) {
+    const Built& b = plans[pi];
+    const int grid = which == 0 ? b.P.nhb + b.P.nlwg : which == 1 ? b.P.nlwg : b.P.nhb;
+    const int check = which == 0 ? 3 : which;
+    vs.push_back({name + (which == 0 ? " all" : which == 1 ? " light" : " hub"),
+                  [&, pi, which, kern, grid](int s, unsigned long long* stp) {
+                    Args a = args(plans[pi], s, which == 1 ? 0 : plans[pi].P.nhb);
+                    a.stamps = stp;
+                    hipLaunchKernelGGL(kern, dim3(grid), dim3(plans[pi].P.WPB * 64), 0, st, a);
+                  },
+                  check, grid});
+  };
+  vs.push_back({"copy_nt", [&](int s, unsigned long long*) {
+                  hipLaunchKernelGGL(copy_nt, dim3(1024), dim3(256), 0, st, (const float4*)Bs[s], (float4*)Cs[s], M * P4);
+                }, 0, 0});
+  for (int which = 2; which >= 0; --which) {
+    add("seg WPB4 SEG48 UH6", 0, which, (seg_kernel<4, 1, 8, 6>));
+    add("slice WPB4 SL8 U8", 1, which, (slice_kernel<4, 1, 8, 8, 8>));
+    add("slice WPB8 SL8 U8", 2, which, (slice_kernel<8, 1, 8, 8, 8>));
+    add("slice WPB16 SL8 U8", 3, which, (slice_kernel<16, 1, 8, 8, 8>));
+    add("slice WPB16 SL8 U4", 3, which, (slice_kernel<16, 1, 8, 8, 4>));
+    add("slice WPB16 SL4 U8", 4, which, (slice_kernel<16, 1, 8, 4, 8>));
+    add("slice WPB16 SL16 U8", 5, which, (slice_kernel<16, 1, 8, 16, 8>));
+    add("slice WPB8 SL4 U8", 6, which, (slice_kernel<8, 1, 8, 4, 8>));
+  }
+
+  const char* only = getenv("NS_ONLY");
+  auto pct = [](std::vector<double> x, double q) { std::sort(x.begin(), x.end()); return x.empty() ? 0.0 : x[(size_t)(q * (x.size() - 1))]; };
+  std::vector<float> out(matmax);
+  for (int pi = 0; pi < 2; ++pi) {
+    P4 = pitches[pi];
+    // B sets with this pitch (padding columns hold garbage that must never be read into C)
+    std::vector<float> hB((size_t)M * P4 * 4, 1e30f);
+    for (int r = 0; r < M; ++r) memcpy(&hB[(size_t)r * P4 * 4], &hB0[(size_t)r * F], F * 4);
+    for (int s = 0; s < nsets; ++s) CHECK(hipMemcpy(Bs[s], hB.data(), hB.size() * 4, hipMemcpyHostToDevice));
+    for (auto& V : vs) {
+      if (only && !strstr(V.name.c_str(), only)) continue;
+      CHECK(hipMemset(Cs[0], 0, matmax * 4));
+      V.run(0, nullptr);
+      CHECK(hipStreamSynchronize(st));
+      CHECK(hipGetLastError());
+      double maxerr = 0;
+      if (V.check) {
+        CHECK(hipMemcpy(out.data(), Cs[0], (size_t)M * P4 * 16, hipMemcpyDeviceToHost));
+        for (int r = 0; r < M; ++r) {
+          if ((hub[r] && !(V.check & 2)) || (!hub[r] && !(V.check & 1))) continue;
+          for (int f = 0; f < F; ++f) {
+            const double e = std::fabs(out[(size_t)r * P4 * 4 + f] - ref[(size_t)r * F + f]) / (1.0 + std::fabs(ref[(size_t)r * F + f]));
+            maxerr = std::max(maxerr, std::isfinite(e) ? e : 1e30);
+          }
+        }
+      }
+      double us[2];
+      for (int mode = 0; mode < 2; ++mode) {
+        const int reps = mode == 0 ? std::max(1, 200 / nsets) : 1;
+        const int per = mode == 0 ? nsets : 200;
+        hipGraph_t gr;
+        hipGraphExec_t ge;
+        CHECK(hipStreamBeginCapture(st, hipStreamCaptureModeGlobal));
+        for (int r = 0; r < reps; ++r)
+          for (int s = 0; s < per; ++s) V.run(mode == 0 ? s : 0, nullptr);
+        CHECK(hipStreamEndCapture(st, &gr));
+        CHECK(hipGraphInstantiate(&ge, gr, nullptr, nullptr, 0));
+        CHECK(hipGraphLaunch(ge, st));
+        CHECK(hipStreamSynchronize(st));
+        hipEvent_t e0, e1;
+        CHECK(hipEventCreate(&e0));
+        CHECK(hipEventCreate(&e1));
+        CHECK(hipEventRecord(e0, st));
+        CHECK(hipGraphLaunch(ge, st));
+        CHECK(hipEventRecord(e1, st));
+        CHECK(hipEventSynchronize(e1));
+        float ms = 0;
+        CHECK(hipEventElapsedTime(&ms, e0, e1));
+        us[mode] = ms * 1e3 / (reps * per);
+        CHECK(hipGraphExecDestroy(ge));
+        CHECK(hipGraphDestroy(gr));
+      }
+      printf("{\"pitch\": %d, \"variant\": \"%s\", \"cold_us\": %.3f, \"warm_us\": %.3f, \"frac_cold\": %.3f, \"maxerr\": %.3g",
+             P4 * 4, V.name.c_str(), us[0], us[1], 12.94234e6 / (us[0] * 1e-6) / 8e12, maxerr);
+      if (V.grid > 0) {  // one stamped launch on a cold set
+        CHECK(hipMemset(d_st, 0, (size_t)V.grid * 32));
+        V.run(nsets - 1, d_st);
+        CHECK(hipStreamSynchronize(st));
+        std::vector<unsigned long long> hs((size_t)4 * V.grid);
+        CHECK(hipMemcpy(hs.data(), d_st, hs.size() * 8, hipMemcpyDeviceToHost));
+        unsigned long long t0 = ~0ull;
+        for (int b = 0; b < V.grid; ++b) if (hs[4 * b]) t0 = std::min(t0, hs[4 * b]);
+        for (int k : {0, 3}) {
+          std::vector<double> x;
+          for (int b = 0; b < V.grid; ++b)
+            if (hs[4 * b + k]) x.push_back((hs[4 * b + k] - t0) / 100.0);
+          printf(", \"ph%d\": [%.2f, %.2f, %.2f]", k, pct(x, 0.1), pct(x, 0.5), pct(x, 1.0));
+        }
+      }
+      printf("}\n");
+      fflush(stdout);
+    }
+  }
+  return 0;
+}

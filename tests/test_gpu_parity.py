@@ -695,19 +695,22 @@ def test_r8_training_accuracy_parity(r8, golden_meta, seed):
 def test_gcn_20ng_shaped_forward_matches_oracle(mode, monkeypatch):
     """BASELINE config 3: 20ng-shaped doc-topic graph (18,846 docs, 70 topics,
     nclass 20, gensim-shaped nfeat 100 -> dense X).  The default forward takes
-    the hub-factored first layer (70 hubs, Kc = 70, P = 20: the 18-k-step,
-    two-n-tile gcnk_hubfactor_gc1_f32): eval logits vs the oracle's
-    reference-equivalent forward on the same tensors; logits and every
-    gradient of a train-mode step (device dropout) vs the SpMM path
-    (ops.FACTOR_GC1 = False)."""
+    the narrow-feature first layer (ops.dense_ax_for: the cached A-hat X, one
+    gcnk_dense_gc1_f32 launch); eval logits of every path vs the oracle's
+    reference-equivalent forward on the same tensors; logits and every gradient
+    of a train-mode step (device dropout) of the dense-AX path and of the
+    hub-factored path (70 hubs, Kc = 70, P = 20) vs the SpMM path."""
     from graph_convolutional_networks_for_text_classification_amd import factor, ops, record
     from graph_convolutional_networks_for_text_classification_amd.sparse import as_csr
     g = datasets.doc_topic_graph(18846, 70, 20, seed=0)
     X, A = g["features"].to(DEV), g["adj"].to(DEV)
     f = factor.get(as_csr(A), ops.Operand(X))
     assert f is not None and f.H == 70 and f.Kc == 70
-    outs = {}
-    for fac in (True, False):
+    outs, want = {}, None
+    paths = {"dense_ax": (True, False, record.DENSE_AX), "factored": (False, True, record.FACTORED),
+             "spmm": (False, False, record.SPMM_GEMM)}
+    for name, (dax, fac, kind) in paths.items():
+        monkeypatch.setattr(ops, "DENSE_AX", dax)
         monkeypatch.setattr(ops, "FACTOR_GC1", fac)
         torch.manual_seed(11)
         m = GCN(nfeat=g["nfeat"], nhid=200, nclass=20, dropout=0.5,
@@ -716,26 +719,29 @@ def test_gcn_20ng_shaped_forward_matches_oracle(mode, monkeypatch):
         if mode == "eval":
             with torch.no_grad():
                 got = m(X, A)
-            outs[fac] = (got.cpu().numpy(), {})
-            if fac:
-                kinds = {r[2].kind for r in as_csr(A)._records.values() if r[2] is not None}
-                assert record.FACTORED in kinds, "config 3 takes the factored first layer"
+            outs[name] = (got.cpu().numpy(), {})
+            kinds = {r[2].kind for k, r in as_csr(A)._records.items()
+                     if isinstance(r[2], record.ForwardRecord) and k[5] == ops.FACTOR_GC1 and k[7] == ops.DENSE_AX}
+            assert kind in kinds, (name, kinds)
+            if want is None:
                 ref = gcn_ref.RefGCN(nfeat=g["nfeat"], nhid=200, nclass=20, dropout=0.5).eval()
                 ref.load_state_dict({k: v.cpu() for k, v in m.state_dict().items()})
                 with torch.no_grad():
                     want = ref(g["features"], g["adj"]).numpy()
-                assert np.abs(outs[fac][0] - want).max() <= LOGIT_TOL
-                _labels_check(outs[fac][0], want)
+            assert np.abs(outs[name][0] - want).max() <= LOGIT_TOL, name
+            _labels_check(outs[name][0], want)
         else:
             lg = m(X, A)
             lg.square().sum().backward()
-            outs[fac] = (lg.detach().cpu().numpy(), {k: p.grad.cpu().numpy() for k, p in m.named_parameters()})
-    (la, ga), (lb, gb) = outs[True], outs[False]
-    scale = max(1.0, float(np.abs(lb).max()))
-    assert np.abs(la - lb).max() <= 1e-5 * scale, float(np.abs(la - lb).max())
-    for k in ga:
-        np.testing.assert_allclose(ga[k], gb[k], rtol=1e-4, atol=1e-5 * max(1.0, float(np.abs(gb[k]).max())),
-                                   err_msg=k)
+            outs[name] = (lg.detach().cpu().numpy(), {k: p.grad.cpu().numpy() for k, p in m.named_parameters()})
+    lb, gb = outs["spmm"]
+    for name in ("dense_ax", "factored"):
+        la, ga = outs[name]
+        scale = max(1.0, float(np.abs(lb).max()))
+        assert np.abs(la - lb).max() <= 1e-5 * scale, (name, float(np.abs(la - lb).max()))
+        for k in ga:
+            np.testing.assert_allclose(ga[k], gb[k], rtol=1e-4, atol=1e-5 * max(1.0, float(np.abs(gb[k]).max())),
+                                       err_msg=f"{name} {k}")
 
 
 @pytest.fixture(scope="module")
@@ -1186,8 +1192,8 @@ def test_factored_forward_hub_rows_first_ragged(mode):
     assert f is not None and f.hubs.cpu().tolist() == list(range(37)) and f.M % 32 != 0
     outs = {}
     for fac in (True, False):
-        saved = ops.FACTOR_GC1
-        ops.FACTOR_GC1 = fac
+        saved, saved_ax = ops.FACTOR_GC1, ops.DENSE_AX
+        ops.FACTOR_GC1, ops.DENSE_AX = fac, False    # (the dense X would otherwise take the dense-AX gc1)
         try:
             torch.manual_seed(5)
             m = GCN(nfeat=g["nfeat"], nhid=200, nclass=g["nclass"], dropout=0.5,
@@ -1197,7 +1203,116 @@ def test_factored_forward_hub_rows_first_ragged(mode):
             lg.square().sum().backward()
             outs[fac] = (lg.detach().cpu().numpy(), {k: p.grad.cpu().numpy() for k, p in m.named_parameters()})
         finally:
-            ops.FACTOR_GC1 = saved
+            ops.FACTOR_GC1, ops.DENSE_AX = saved, saved_ax
+    (la, ga), (lb, gb) = outs[True], outs[False]
+    scale = max(1.0, float(np.abs(lb).max()))
+    assert np.abs(la - lb).max() <= 1e-5 * scale, float(np.abs(la - lb).max())
+    for k in ga:
+        np.testing.assert_allclose(ga[k], gb[k], rtol=1e-4, atol=1e-5 * max(1.0, float(np.abs(gb[k]).max())),
+                                   err_msg=k)
+
+
+# ------------------------------------------------------------------------------ narrow-feature gc1 (A-hat X cached)
+
+def _gensim_r8_x(r8):
+    """The gensim-shaped 100-d R8 X: documents' LDA
+    theta in columns 0-49, topics N(0,1) 100-d, rows L2-normalised."""
+    ndoc, ntopic = r8["ndoc"], r8["ntopic"]
+    X = np.zeros((r8["nodes"], 100), np.float32)
+    X[:ndoc, :ntopic] = r8["features_dense"][:ndoc, :ntopic]
+    X[ndoc:] = np.random.default_rng(0).standard_normal((ntopic, 100))
+    X /= np.maximum(np.linalg.norm(X, axis=1, keepdims=True), 1e-12)
+    return X
+
+
+@pytest.mark.parametrize("K,F,P,M", [(100, 200, 20, 18916), (100, 200, 8, 7724), (7, 8, 3, 1000),
+                                     (50, 52, 32, 777), (128, 256, 17, 2049), (64, 100, 16, 33), (13, 200, 1, 16)])
+def test_dense_gc1_kernel_against_float64(K, F, P, M):
+    """gcnk_dense_gc1_f32 alone: H1 = relu(AX W1 + b1) and S2 = H1 W2 against
+    float64 for K of 1-32 k-steps (K not a multiple of 4 included), F not a
+    multiple of 16, P of one and two MFMA n-tiles, M ragged (a partial last
+    16-row tile) and below / above the CU count in tiles; H1 stored or not
+    (S2 bitwise the same); the dropout-mask epilogue against the same mask in
+    float64; the launch bitwise reproducible."""
+    import ctypes
+    rng = np.random.default_rng(K * 1000 + F + P)
+    AX = rng.standard_normal((M, (K + 3) // 4 * 4)).astype(np.float32)
+    AX[:, K:] = 0.0
+    W1 = rng.standard_normal((K, F)).astype(np.float32)
+    W2 = rng.standard_normal((F, P)).astype(np.float32)
+    b1 = rng.standard_normal(F).astype(np.float32)
+    mask = (rng.random((M, F)) < 0.5).astype(np.uint8)
+    t = {k: torch.from_numpy(v).to(DEV) for k, v in dict(AX=AX, W1=W1, W2=W2, b1=b1, mask=mask).items()}
+    lib = _lib.load()
+    stream = ctypes.c_void_p(torch.cuda.current_stream().cuda_stream)
+    p = lambda x: ctypes.c_void_p(x.data_ptr()) if x is not None else None
+
+    def launch(epi, store_h1=True, m=None, scale=1.0):
+        H1 = torch.full((M, F), float("nan"), device=DEV) if store_h1 else None
+        S2 = torch.full((M, P), float("nan"), device=DEV)
+        _lib.check(lib.gcnk_dense_gc1_f32(M, K, F, P, p(t["AX"]), t["AX"].stride(0), p(t["W1"]), F, p(t["b1"]), epi,
+                                          p(m), F if m is not None else 0, scale, 0.5, 0, 0, None, p(t["W2"]), P,
+                                          p(H1), F, p(S2), P, stream), "gcnk_dense_gc1_f32")
+        return H1, S2
+    Z = AX[:, :K].astype(np.float64) @ W1.astype(np.float64) + b1
+    want = np.maximum(Z, 0.0)
+    H1, S2 = launch(_lib.EPI_BIAS_RELU)
+    tol = 2e-5 * max(1.0, np.abs(want).max())
+    _close(H1, want, atol=tol)
+    _close(S2, H1.cpu().double().numpy() @ W2.astype(np.float64), atol=tol * max(1.0, np.abs(W2).sum(0).max()))
+    H1b, S2b = launch(_lib.EPI_BIAS_RELU, store_h1=False)
+    assert H1b is None and torch.equal(S2b, S2)
+    H1c, S2c = launch(_lib.EPI_BIAS_RELU)
+    assert torch.equal(H1c, H1) and torch.equal(S2c, S2)
+    Hd, Sd = launch(_lib.EPI_BIAS_RELU_DROP, m=t["mask"], scale=2.0)
+    _close(Hd, want * mask * 2.0, atol=2 * tol)
+    _close(Sd, Hd.cpu().double().numpy() @ W2.astype(np.float64), atol=2 * tol * max(1.0, np.abs(W2).sum(0).max()))
+    with pytest.raises(RuntimeError):   # an epilogue without the ReLU is not gc1's
+        launch(_lib.EPI_BIAS)
+
+
+@pytest.mark.parametrize("mode", ["eval", "train_mask", "train_hash"])
+@pytest.mark.parametrize("graph", ["r8_gensim", "ragged"])
+def test_dense_ax_forward_backward_matches_spmm_path(r8, mode, graph, monkeypatch):
+    """GCN.forward / backward through the narrow-feature gc1 (the cached
+    A-hat X, gcnk_dense_gc1_f32; backward gW1 = (A-hat X)^T gZ1) against the
+    SpMM path (X W1, then A-hat S1, layer.py:102,106) with the same weights and
+    dropout masks: logits within fp32 reassociation error, every gradient to
+    1e-4; the eval logits also against the oracle (reference ATen calls) to
+    1e-4.  On R8 with the gensim-shaped X and on a ragged synthetic doc-topic
+    graph (M = 1,038) whose X is dense."""
+    from graph_convolutional_networks_for_text_classification_amd import ops, record
+    from graph_convolutional_networks_for_text_classification_amd.sparse import as_csr
+    if graph == "r8_gensim":
+        Xn, A_cpu, nclass = _gensim_r8_x(r8), r8["adj"], r8["nclass"]
+    else:
+        g = datasets.doc_topic_graph(1001, 37, 5, seed=11)
+        Xn, A_cpu, nclass = g["features_dense"], g["adj"], g["nclass"]
+    Xs = datasets.dense_to_coo(Xn)
+    X, A = Xs.to(DEV), A_cpu.to(DEV)
+    assert ops.dense_ax_for(as_csr(A), ops.Operand(X), 200, nclass) is not None
+    outs = {}
+    for dax in (True, False):
+        monkeypatch.setattr(ops, "DENSE_AX", dax)
+        monkeypatch.setattr(ops, "FACTOR_GC1", False)
+        torch.manual_seed(123)
+        m = GCN(nfeat=Xn.shape[1], nhid=200, nclass=nclass, dropout=0.5,
+                dropout_rng="device" if mode == "train_hash" else "cpu").to(DEV)
+        m.train(mode != "eval")
+        torch.manual_seed(9)
+        lg = m(X, A)
+        if dax:
+            kinds = {r[2].kind for r in as_csr(A)._records.values() if isinstance(r[2], record.ForwardRecord)}
+            assert record.DENSE_AX in kinds, kinds
+        if mode == "eval":
+            assert torch.equal(lg, m(X, A))
+            ref = gcn_ref.RefGCN(nfeat=Xn.shape[1], nhid=200, nclass=nclass, dropout=0.5).eval()
+            ref.load_state_dict({k: v.cpu() for k, v in m.state_dict().items()})
+            with torch.no_grad():
+                want = ref(Xs, A_cpu).numpy()
+            assert np.abs(lg.detach().cpu().numpy() - want).max() <= LOGIT_TOL
+        lg.square().sum().backward()
+        outs[dax] = (lg.detach().cpu().numpy(), {k: p.grad.cpu().numpy() for k, p in m.named_parameters()})
     (la, ga), (lb, gb) = outs[True], outs[False]
     scale = max(1.0, float(np.abs(lb).max()))
     assert np.abs(la - lb).max() <= 1e-5 * scale, float(np.abs(la - lb).max())
@@ -1208,7 +1323,7 @@ def test_factored_forward_hub_rows_first_ragged(mode):
 
 # ------------------------------------------------------------------------------ whole-forward launch record
 
-@pytest.mark.parametrize("path", ["factored", "spmm_proj", "spmm_gemm", "dense_factored", "dense_spmm"])
+@pytest.mark.parametrize("path", ["factored", "spmm_proj", "spmm_gemm", "dense_factored", "dense_spmm", "dense_ax"])
 @pytest.mark.parametrize("mode", ["eval", "train_mask", "train_hash"])
 def test_forward_record_is_bitwise_the_per_op_path(r8, path, mode, monkeypatch):
     """gcnk_gcn_forward_f32 / gcnk_gcn_backward_f32 (record.py: the whole
@@ -1220,6 +1335,7 @@ def test_forward_record_is_bitwise_the_per_op_path(r8, path, mode, monkeypatch):
     from graph_convolutional_networks_for_text_classification_amd import ops, record
     monkeypatch.setattr(ops, "FACTOR_GC1", path in ("factored", "dense_factored"))
     monkeypatch.setattr(ops, "FUSE_PROJECTION", path != "spmm_gemm")
+    monkeypatch.setattr(ops, "DENSE_AX", path == "dense_ax")
     A = r8["adj"].to(DEV)
     if path.startswith("dense"):       # the gensim-shaped 100-d X (dense copy, MFMA GEMM)
         ndoc, ntopic = r8["ndoc"], r8["ntopic"]
@@ -1255,7 +1371,7 @@ def test_forward_record_is_bitwise_the_per_op_path(r8, path, mode, monkeypatch):
     # the training modes' backward went through gcnk_gcn_backward_f32
     assert (mode != "eval") == any(isinstance(r, record.BackwardRecord) for r in recs)
     want = {"factored": record.FACTORED, "dense_factored": record.FACTORED, "spmm_proj": record.SPMM_PROJ,
-            "spmm_gemm": record.SPMM_GEMM}.get(path)
+            "spmm_gemm": record.SPMM_GEMM, "dense_ax": record.DENSE_AX}.get(path)
     if want is not None:
         assert want in kinds, kinds
 

@@ -276,50 +276,66 @@ def forward_kernels(save_dir=None, graph="r8"):
         shutil.rmtree(tmp, ignore_errors=True)
 
 
+def forward_path(a_csr, x, nhid, nclass):
+    """The record kind the product forward takes for (A-hat, X): "dense-ax"
+    (ops.dense_ax_for), "factored" (ops.factor_for), "spmm+proj" or "spmm+gemm"."""
+    from graph_convolutional_networks_for_text_classification_amd import ops
+    xop = ops.Operand(x)
+    if ops.dense_ax_for(a_csr, xop, nhid, nclass) is not None:
+        return "dense-ax"
+    if ops.factor_for(a_csr, xop) is not None:
+        return "factored"
+    fused = ops.FUSE_PROJECTION and nclass <= ops.FUSE_MAX_P and nhid % 4 == 0 and nhid <= 256
+    return "spmm+proj" if fused else "spmm+gemm"
+
+
 def labelled_forward_kernels(save_dir, graph, a_csr, x, N, nfeat, nnz_a, nnz_x, nhid, nclass):
     """forward_kernels() with each launch labelled by the op it belongs to and
-    that op's algorithmic bytes (SURVEY §8(d) formula) and fraction."""
+    that op's algorithmic bytes (SURVEY §8(d) formulas: every operand read once,
+    every output written once) and fraction of the HBM peak."""
     trace, trace_src = forward_kernels(save_dir, graph)
     if trace is None or not trace.get("kernels"):
         return {"error": trace_src}
     from graph_convolutional_networks_for_text_classification_amd import ops
     dense_x = ops.Operand(x).dense is not None
-    # gc2's support fused into the gc1 aggregation (record.ForwardRecord's SPMM_PROJ
-    # rule): the aggregation writes S2 [N x nclass]; unfused it writes H1 [N x nhid]
-    # and the skinny GEMM reads it back
-    fused = ops.FUSE_PROJECTION and nclass <= ops.FUSE_MAX_P and nhid % 4 == 0 and nhid <= 256
-    alg = {   # algorithmic bytes of each launch of the eval forward
-        # dense X (gensim-shaped): the GEMM's operands once; sparse X: the CSR SpMM formula
-        "X W1": 4 * (N * nfeat + nfeat * nhid + N * nhid) if dense_x else spmm_bytes(N, nfeat, nnz_x, nhid),
-        "A S1": (4 * (N + 1) + 8 * nnz_a + 4 * N * nhid + 4 * N * nclass + 4 * nhid * nclass) if fused
-        else spmm_bytes(N, N, nnz_a, nhid),
-        "A S2": spmm_bytes(N, N, nnz_a, nclass),
-        "H1 W2": 4 * (N * nhid + nhid * nclass + N * nclass),   # unfused gc2 support
-    }
-    fac = _factored(a_csr, x)
-    if fac is not None:
-        # hub-factored gc1 (factor.py): X[hubs] W1 (tile SpMM or dense GEMM), then one
-        # launch reading U [N x Kc], the A_H records, W1[Kc], S_T, W2 and writing S2
-        if fac.x_hub_dense is not None:   # the small-M split-K GEMM on the dense hub rows
-            xw = 4 * (fac.H * nfeat + nfeat * nhid + fac.H * nhid)
-        else:
-            xw = spmm_bytes(fac.H, nfeat, fac.x_hub.nnz, nhid)
+    path = forward_path(a_csr, x, nhid, nclass)
+    a_s2 = spmm_bytes(N, N, nnz_a, nclass)
+    if path == "dense-ax":
+        # one launch: A-hat X [N x nfeat] (cached), W1, b1, W2 read; S2 written
+        alg = {"AX W1 + H1 W2": 4 * (N * nfeat + nfeat * nhid + nhid + nhid * nclass + N * nclass), "A S2": a_s2}
+    elif path == "factored":
+        fac = _factored(a_csr, x)
+        # X[hubs] W1 (dense hub rows on the one-pass small-M GEMM, or their CSR),
+        # then one launch reading U [N x Kc], the A_H records, W1[Kc], S_T, W2, writing S2
+        xw = 4 * (fac.H * nfeat + nfeat * nhid + fac.H * nhid) if fac.x_hub_dense is not None \
+            else spmm_bytes(fac.H, nfeat, fac.x_hub.nnz, nhid)
         alg = {"X_hubs W1": xw,
                "A X W1 factored + H1 W2": (4 * fac.U.numel() + 4 * fac.rec.numel() + 4 * fac.Kc * nhid
                                             + 4 * fac.H * nhid + 4 * nhid * nclass + 4 * N * nclass),
-               "A S2": alg["A S2"]}
+               "A S2": a_s2}
+    else:
+        fused = path == "spmm+proj"
+        alg = {   # dense X (gensim-shaped): the GEMM's operands once; sparse X: the CSR SpMM formula
+            "X W1": 4 * (N * nfeat + nfeat * nhid + N * nhid) if dense_x else spmm_bytes(N, nfeat, nnz_x, nhid),
+            # gc2's support fused into the gc1 aggregation: it writes S2 [N x nclass];
+            # unfused it writes H1 [N x nhid] and the skinny GEMM reads it back
+            "A S1": (4 * (N + 1) + 8 * nnz_a + 4 * N * nhid + 4 * N * nclass + 4 * nhid * nclass) if fused
+            else spmm_bytes(N, N, nnz_a, nhid),
+            "A S2": a_s2,
+            "H1 W2": 4 * (N * nhid + nhid * nclass + N * nclass)}
     ks, na = [], 0
-    for k in trace["kernels"]:   # the A-hat launches are the row kernels, X W1 the rest
+    for k in trace["kernels"]:   # launch order: the A-hat launches are the row kernels
         name = k["kernel"]
-        if "hubfactor" in name:
-            key = "A X W1 factored + H1 W2"
+        if path == "dense-ax":
+            key = "A S2" if "spmm_row_kernel" in name else "AX W1 + H1 W2"
+        elif path == "factored":
+            key = ("A X W1 factored + H1 W2" if ("hubfactor" in name or "dense_gc1" in name)
+                   else "A S2" if "spmm_row_kernel" in name else "X_hubs W1")
         elif "spmm_row_kernel" in name:
-            key = "A S1" if na == 0 and fac is None else "A S2"
+            key = "A S1" if na == 0 else "A S2"
             na += 1
-        elif fac is None and na > 0:
-            key = "H1 W2"        # the skinny GEMM between the two aggregations
         else:
-            key = "X W1" if fac is None else "X_hubs W1"
+            key = "H1 W2" if na > 0 else "X W1"   # (the skinny GEMM sits between the two aggregations)
         ks.append({"kernel": name[:120], "us": k["us"], "op": key})
     for key, nb in alg.items():   # per op: its launches' summed duration against its bytes
         us = sum(e["us"] for e in ks if e["op"] == key)
@@ -331,8 +347,7 @@ def labelled_forward_kernels(save_dir, graph, a_csr, x, N, nfeat, nnz_a, nnz_x, 
     for e in ks:
         per_op.setdefault(e["op"], {"op_us": e.get("op_us"), "algorithmic_bytes": e.get("algorithmic_bytes"),
                                     "frac": e.get("frac"), "kernels": []})["kernels"].append(e["kernel"][:60])
-    return {"source": trace_src, "path": "factored" if fac is not None else ("spmm+proj" if fused else "spmm+gemm"),
-            "x_operand": "dense" if dense_x else "csr",
+    return {"source": trace_src, "path": path, "x_operand": "dense" if dense_x else "csr",
             "forward_span_us": trace["forward_span_us_median"], "kernels": ks, "ops": per_op}
 
 
@@ -457,6 +472,27 @@ def setup_legs(r8, dev, nhid=200):
     finally:
         ops.FACTOR_GC1 = saved
     return out
+
+
+def dense_ax_build_ms(a_csr, x, nhid, nclass):
+    """Fresh builds of the narrow-feature path's one-time operand A-hat X
+    (ops.dense_ax_for: gcnk_aggregate_f32, float64 row sums rounded once):
+    {"first_ms", "ms"} as factor_build_ms; None where the path does not apply."""
+    import torch
+    from graph_convolutional_networks_for_text_classification_amd import ops
+    xop = ops.Operand(x)
+    ts = []
+    for _ in range(4):
+        if hasattr(a_csr, "_dense_ax"):
+            a_csr._dense_ax.clear()
+        torch.cuda.synchronize()
+        t0 = time.perf_counter()
+        d = ops.dense_ax_for(a_csr, xop, nhid, nclass)
+        torch.cuda.synchronize()
+        ts.append((time.perf_counter() - t0) * 1e3)
+        if d is None:
+            return None
+    return {"first_ms": round(ts[0], 3), "ms": round(sorted(ts[1:])[1], 3)}
 
 
 def sharded_config5(dev, world, rank, datasets, ops, F=4096, reps=3):
@@ -827,6 +863,7 @@ def main():
         fk20 = None if args.no_rocprof else labelled_forward_kernels(
             args.rocprof_dir, "20ng", ac20, x20, ac20.shape[0], g20["nfeat"], ac20.nnz, as_csr(x20).nnz, 200, 20)
         fb20 = factor_build_ms(ac20, x20)
+        dab20 = dense_ax_build_ms(ac20, x20, 200, 20)
         M20 = ac20.shape[0]
         bb = torch.randn(200, device=dev)
         nsets = max(2, -(-int(1.25 * MALL_BYTES) // (2 * 4 * M20 * 200)))
@@ -844,7 +881,8 @@ def main():
             "spmm_F200_frac_cold": nb / (c * 1e-6) / 1e9 / HBM_PEAK_GBS,
             "spmm_F200_frac_warm": nb / (w * 1e-6) / 1e9 / HBM_PEAK_GBS,
             "spmm_F200_gflops_cold": 2 * ac20.nnz * 200 / (c * 1e-6) / 1e9,
-            "path": fk20.get("path") if fk20 else None, "factor_build_ms": fb20, "forward_kernels": fk20}
+            "path": forward_path(ac20, x20, 200, 20), "factor_build_ms": fb20, "dense_ax_build_ms": dab20,
+            "forward_kernels": fk20}
         del m20, a20, x20, ac20
         torch.cuda.empty_cache()
         from graph_convolutional_networks_for_text_classification_amd.sparse import CSR
@@ -930,7 +968,7 @@ def main():
         "config": {"workload": "R8 GCN forward (eval), hidden 200, 8 classes, nfeat 7463",
                    "nodes": N, "adj_nnz": nnz_a, "x_nnz": nnz_x, "graph": not args.no_graph,
                    "forwards_per_graph": per,
-                   "path": "factored" if fb_r8 is not None and _factored(a_csr, x) is not None else "spmm",
+                   "path": forward_path(a_csr, x, nhid, nclass),
                    "factor_build_ms": fb_r8,
                    "parallelism": f"replicas{world}" if world > 1 else "single"},
         "roofline": roof,

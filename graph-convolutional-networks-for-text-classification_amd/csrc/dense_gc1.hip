@@ -39,24 +39,36 @@ constexpr int kNTQ = 4;          // n-tiles per wave: F <= 16 * 4 * kNTQ = 256
 constexpr int kHP = 64 + 4;      // wave-private H1 tile row stride (floats): 16 x (64 + 4)
 constexpr int kMaxP = 32;
 
+// hub mode (the factored gc1, csrc/factor.hip's record layout): U's rows are
+// positions of the block order; per 32-position block a record of rec_words
+// int32: 33 block-relative item offsets, 3 pad, 32 output row ids (-1 past M),
+// then items int2 {hub index, value bits}
+constexpr int kRecRow = 36, kRecHead = 68;
+
 struct DenseArgs {
   int32_t M, K, F, P;
-  const float* A; int64_t lda;     // A-hat X [M x >= K]
-  const float* W; int64_t ldw;     // W1 [K x F]
+  const float* A; int64_t lda;     // A-hat X [M x >= K] (hub mode: U in block order)
+  const float* W; int64_t ldw;     // W1 [K x F] (hub mode: W1's rows k0 ..)
   const float* W2; int64_t ldw2;   // [F x P]
   float* H; int64_t ldh;           // nullable
   float* C2; int64_t ldc2;         // S2 [M x P]
   Epi epi;
   int32_t ntiles;                  // ceil(M / 16)
+  // hub mode: Z += A_H S_T
+  const float* S; int64_t lds;     // S_T [nhub x F]
+  int32_t nhub;
+  const int32_t* rec; int32_t rec_words;
 };
 
 // KS k-steps of 4 (K <= 4 KS; lane quadrant q of step s multiplies k = 4 s + q),
-// NP 16-column tiles of P
-template <int KS, int NP>
+// NP 16-column tiles of P; HUB: the factored gc1 (S_T staged in LDS once, the
+// tile's block record staged per tile, one tile ahead)
+template <int KS, int NP, bool HUB>
 __global__ void __launch_bounds__(kThreads)
 dense_gc1_kernel(DenseArgs a) {
   __shared__ __attribute__((aligned(16))) float s_h[kWaves][16 * kHP];
   __shared__ __attribute__((aligned(16))) float s_red[2][kWaves][NP][64 * 4];
+  extern __shared__ __attribute__((aligned(16))) float s_dyn[];   // HUB: s_S [nhub x F] | s_rec [2][rec_words]
   const int tid = threadIdx.x, lane = tid & 63;
   const int w = __builtin_amdgcn_readfirstlane(tid >> 6);
   const int c = lane & 15, q = lane >> 4;
@@ -93,6 +105,43 @@ dense_gc1_kernel(DenseArgs a) {
     bv[t] = (a.epi.bias && t < ntw && col < F) ? a.epi.bias[col] : 0.f;
   }
   float* hw = s_h[w];
+  float* s_S = s_dyn;
+  int32_t* s_rec = reinterpret_cast<int32_t*>(s_dyn + (HUB ? a.nhub * F : 0));
+  const int rw = HUB ? a.rec_words : 0;
+  // HUB: the block record of a tile (block tile / 2) into registers, then LDS
+  constexpr int kRecPer = 4;   // record words per thread (rec_words <= 1024, checked on the host)
+  auto load_rec = [&](int tile, int32_t (&rv)[kRecPer]) {
+    if constexpr (HUB) {
+      const int32_t* rb = a.rec + (int64_t)(tile / 2) * rw;
+#pragma unroll
+      for (int i = 0; i < kRecPer; ++i) {
+        const int e = tid + kThreads * i;
+        rv[i] = (tile < a.ntiles && e < rw) ? rb[e] : 0;
+      }
+    }
+  };
+  auto put_rec = [&](int buf, const int32_t (&rv)[kRecPer]) {
+    if constexpr (HUB) {
+#pragma unroll
+      for (int i = 0; i < kRecPer; ++i) {
+        const int e = tid + kThreads * i;
+        if (e < rw) s_rec[buf * rw + e] = rv[i];
+      }
+    }
+  };
+  if constexpr (HUB) {
+    // S_T once per workgroup (float4 pieces: F % 4 == 0, lds % 4 == 0, checked on the host)
+    const int n4 = a.nhub * (F / 4);
+    for (int e = tid; e < n4; e += kThreads) {
+      const int hrow = e / (F / 4), c4 = e % (F / 4);
+      *reinterpret_cast<float4*>(s_S + hrow * F + 4 * c4) =
+          *reinterpret_cast<const float4*>(a.S + (int64_t)hrow * a.lds + 4 * c4);
+    }
+    int32_t rv[kRecPer];
+    load_rec(blockIdx.x, rv);
+    put_rec(0, rv);
+    __syncthreads();
+  }
 
   // A fragments of a tile: lane (row c, quadrant q) holds A[row][4 s + q]
   auto load_a = [&](int tile, float (&af)[KS]) {
@@ -107,6 +156,8 @@ dense_gc1_kernel(DenseArgs a) {
   // the tile loop unrolled by two: no runtime index into a register array)
   auto tile_step = [&](int tile, int buf, float (&af)[KS], float (&an)[KS]) {
     load_a(tile + gridDim.x, an);
+    int32_t rv[kRecPer];
+    load_rec(tile + gridDim.x, rv);
     // ---- 1. Z = A W1[:, cols_w]
     f32x4 acc[kNTQ];
 #pragma unroll
@@ -120,13 +171,35 @@ dense_gc1_kernel(DenseArgs a) {
     //      tile into wave-private LDS
     const int64_t row0 = (int64_t)tile * 16;
     const bool plain = a.epi.code == GCNK_EPI_BIAS_RELU;
+    int64_t orow[4];   // output rows of this lane's 4 tile rows
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+      if constexpr (HUB) {
+        const int pb = 16 * (tile & 1) + 4 * q + r;   // position within the 32-row block
+        const int32_t* rb = s_rec + buf * rw;
+        const int32_t id = rb[kRecRow + pb];
+        orow[r] = id >= 0 ? id : a.M;                 // -1 (past M): never stored
+        // + A_H S_T: the row's hub items in CSR order
+        const int2* it = reinterpret_cast<const int2*>(rb + kRecHead);
+        for (int k = rb[pb]; k < rb[pb + 1]; ++k) {
+          const int2 p2 = it[k];
+          const float v = __int_as_float(p2.y);
+          const float* srow = s_S + p2.x * F + 16 * w + c;
+#pragma unroll
+          for (int t = 0; t < kNTQ; ++t)   // (columns past F: no read past the hub's row)
+            if (t < ntw && 16 * (w + kWaves * t) + c < F) acc[t][r] = fmaf(v, srow[16 * kWaves * t], acc[t][r]);
+        }
+      } else {
+        orow[r] = row0 + 4 * q + r;
+      }
+    }
 #pragma unroll
     for (int t = 0; t < kNTQ; ++t) {
       if (t >= ntw) break;
       const int64_t col = 16 * (w + kWaves * t) + c;
 #pragma unroll
       for (int r = 0; r < 4; ++r) {
-        const int64_t row = row0 + 4 * q + r;
+        const int64_t row = orow[r];
         float h;
         if (plain) h = fmaxf(acc[t][r] + bv[t], 0.f);
         else h = (row < a.M && col < F) ? apply_epi(a.epi, acc[t][r], bv[t], row, col) : 0.f;
@@ -156,6 +229,7 @@ dense_gc1_kernel(DenseArgs a) {
     }
 #pragma unroll
     for (int p = 0; p < NP; ++p) *reinterpret_cast<f32x4*>(&s_red[buf][w][p][4 * lane]) = pacc[p];
+    put_rec(buf ^ 1, rv);   // the next tile's record (its readers passed the previous barrier)
     // (double-buffered by tile parity: wave 0 reads buffer `buf` before it
     // reaches the next barrier, and buffer `buf` is written again only after it)
     __syncthreads();
@@ -168,7 +242,7 @@ dense_gc1_kernel(DenseArgs a) {
         const int pc = 16 * p + c;
 #pragma unroll
         for (int r = 0; r < 4; ++r) {
-          const int64_t row = row0 + 4 * q + r;
+          const int64_t row = orow[r];
           if (row < a.M && pc < P) a.C2[row * a.ldc2 + pc] = sum[r];
         }
       }
@@ -186,21 +260,95 @@ dense_gc1_kernel(DenseArgs a) {
   }
 }
 
-template <int KS>
-int launch_ks(const DenseArgs& a, int np, unsigned grid, hipStream_t s) {
+template <int KS, bool HUB>
+int launch_ks(const DenseArgs& a, int np, unsigned grid, size_t dyn, hipStream_t s) {
+  if (dyn > 64 * 1024) {   // dynamic LDS past the default limit: raised once per device
+    static std::atomic<uint64_t> done1{0}, done2{0};
+    const hipError_t e = np == 1 ? dyn_lds_attr(done1, reinterpret_cast<const void*>(&dense_gc1_kernel<KS, 1, HUB>), 160 * 1024)
+                                 : dyn_lds_attr(done2, reinterpret_cast<const void*>(&dense_gc1_kernel<KS, 2, HUB>), 160 * 1024);
+    if (e != hipSuccess) return hip_check(e, "dense_gc1_kernel LDS attribute");
+  }
   if (np == 1)
-    hipLaunchKernelGGL((dense_gc1_kernel<KS, 1>), dim3(grid), dim3(kThreads), 0, s, a);
+    hipLaunchKernelGGL((dense_gc1_kernel<KS, 1, HUB>), dim3(grid), dim3(kThreads), dyn, s, a);
   else
-    hipLaunchKernelGGL((dense_gc1_kernel<KS, 2>), dim3(grid), dim3(kThreads), 0, s, a);
+    hipLaunchKernelGGL((dense_gc1_kernel<KS, 2, HUB>), dim3(grid), dim3(kThreads), dyn, s, a);
   return launch_check("dense_gc1_kernel");
 }
+
+int cu_count() {
+  static int cus[64] = {0};
+  int dev = 0;
+  if (hipGetDevice(&dev) != hipSuccess || dev < 0) dev = 0;
+  int n = dev < 64 ? cus[dev] : 0;
+  if (n <= 0) {
+    if (hipDeviceGetAttribute(&n, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || n <= 0) n = 256;
+    if (dev < 64) cus[dev] = n;
+  }
+  return n;
+}
+
+template <bool HUB>
+int launch(const DenseArgs& a, hipStream_t s) {
+  // persistent: one workgroup per CU (4 waves, one per SIMD, up to 512 registers each)
+  const unsigned grid = (unsigned)std::min<int64_t>(a.ntiles, cu_count());
+  const int np = a.P <= 16 ? 1 : 2;
+  const size_t dyn = HUB ? (size_t)4 * ((size_t)a.nhub * a.F + 2 * (size_t)a.rec_words) : 0;
+  const int ks = (a.K + 3) / 4;
+  if (ks <= 8) return launch_ks<8, HUB>(a, np, grid, dyn, s);
+  if (ks <= 13) return launch_ks<13, HUB>(a, np, grid, dyn, s);
+  if (ks <= 16) return launch_ks<16, HUB>(a, np, grid, dyn, s);
+  if (ks <= 25) return launch_ks<25, HUB>(a, np, grid, dyn, s);
+  return launch_ks<32, HUB>(a, np, grid, dyn, s);
+}
+
+// the epilogue fields shared by both entry points
+Epi make_epi(const float* bias, int32_t epilogue, const uint8_t* mask, int64_t ldm, int32_t F, float scale, float keep,
+             uint64_t seed, uint64_t offset, const uint64_t* rng_base) {
+  Epi e;
+  e.bias = bias;
+  e.mask = mask;
+  e.ldm = epilogue == GCNK_EPI_BIAS_RELU_HASH ? (ldm > 0 ? ldm : F) : ldm;
+  e.scale = scale;
+  e.keep_prob = keep;
+  e.seed_lo = (uint32_t)seed;
+  e.seed_hi = (uint32_t)(seed >> 32);
+  e.offset = offset;
+  e.rng_base = rng_base;
+  e.code = epilogue;
+  e.stamps = nullptr;
+  return e;
+}
+
+}  // namespace
+
+// The factored gc1 (gcnk_hubfactor_gc1_f32, csrc/factor.hip) on this kernel:
+// GCNK_EUNSUP where its shape or LDS does not fit (the caller falls back).
+int hubfactor_persistent(int32_t M, int32_t F, int32_t Kc, int32_t nhub, int32_t P, const float* U, int64_t ldu,
+                         const float* W, int64_t ldw, int32_t k0, const float* S, int64_t lds, const int32_t* rec,
+                         int32_t rec_words, const float* bias, int32_t epilogue, const uint8_t* mask, int64_t ldm,
+                         float scale, float keep, uint64_t seed, uint64_t offset, const uint64_t* rng_base,
+                         const float* W2, int64_t ldw2, float* H, int64_t ldh, float* C2, int64_t ldc2, void* stream) {
+  const size_t lds_bytes = (size_t)4 * ((size_t)nhub * F + 2 * (size_t)rec_words) + sizeof(float) * (size_t)kWaves * 16 * kHP +
+                           sizeof(float) * 2 * kWaves * 2 * 64 * 4;
+  if (Kc > 128 || F > 16 * kWaves * kNTQ || F % 4 || lds % 4 || ((uintptr_t)S & 15) || P > kMaxP ||
+      rec_words > kThreads * 4 || lds_bytes > 160 * 1024)
+    return GCNK_EUNSUP;
+  DenseArgs a{};
+  a.M = M; a.K = Kc; a.F = F; a.P = P;
+  a.A = U; a.lda = ldu; a.W = W + (int64_t)k0 * ldw; a.ldw = ldw; a.W2 = W2; a.ldw2 = ldw2;
+  a.H = H; a.ldh = ldh; a.C2 = C2; a.ldc2 = ldc2;
+  a.epi = make_epi(bias, epilogue, mask, ldm, F, scale, keep, seed, offset, rng_base);
+  a.ntiles = 2 * ((M + 31) / 32);
+  a.S = S; a.lds = lds; a.nhub = nhub; a.rec = rec; a.rec_words = rec_words;
+  return launch<true>(a, reinterpret_cast<hipStream_t>(stream));
+}
+
+namespace {
 
 }  // namespace
 }  // namespace gcnk
 
 using namespace gcnk;
-
-static int g_cus[64] = {0};
 
 extern "C" int gcnk_dense_gc1_f32(int32_t M, int32_t K, int32_t F, int32_t P, const float* AX, int64_t ldax,
                                   const float* W1, int64_t ldw1, const float* bias, int32_t epilogue,
@@ -224,36 +372,11 @@ extern "C" int gcnk_dense_gc1_f32(int32_t M, int32_t K, int32_t F, int32_t P, co
     set_error("gcnk_dense_gc1_f32: dropout epilogue needs a mask with ldm >= F");
     return GCNK_EARG;
   }
-  DenseArgs a;
+  DenseArgs a{};
   a.M = M; a.K = K; a.F = F; a.P = P;
   a.A = AX; a.lda = ldax; a.W = W1; a.ldw = ldw1; a.W2 = W2; a.ldw2 = ldw2;
   a.H = H; a.ldh = ldh; a.C2 = C2; a.ldc2 = ldc2;
-  a.epi.bias = bias;
-  a.epi.mask = drop_mask;
-  a.epi.ldm = epilogue == GCNK_EPI_BIAS_RELU_HASH ? (ldm > 0 ? ldm : F) : ldm;
-  a.epi.scale = drop_scale;
-  a.epi.keep_prob = keep_prob;
-  a.epi.seed_lo = (uint32_t)seed;
-  a.epi.seed_hi = (uint32_t)(seed >> 32);
-  a.epi.offset = offset;
-  a.epi.rng_base = rng_base;
-  a.epi.code = epilogue;
-  a.epi.stamps = nullptr;
+  a.epi = make_epi(bias, epilogue, drop_mask, ldm, F, drop_scale, keep_prob, seed, offset, rng_base);
   a.ntiles = (M + 15) / 16;
-  int dev = 0;
-  if (hipGetDevice(&dev) != hipSuccess || dev < 0) dev = 0;
-  int cus = dev < 64 ? g_cus[dev] : 0;
-  if (cus <= 0) {
-    if (hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || cus <= 0) cus = 256;
-    if (dev < 64) g_cus[dev] = cus;
-  }
-  const unsigned grid = (unsigned)std::min<int64_t>(a.ntiles, cus);
-  const int np = P <= 16 ? 1 : 2;
-  hipStream_t s = reinterpret_cast<hipStream_t>(stream);
-  const int ks = (K + 3) / 4;
-  if (ks <= 8) return launch_ks<8>(a, np, grid, s);
-  if (ks <= 13) return launch_ks<13>(a, np, grid, s);
-  if (ks <= 16) return launch_ks<16>(a, np, grid, s);
-  if (ks <= 25) return launch_ks<25>(a, np, grid, s);
-  return launch_ks<32>(a, np, grid, s);
+  return launch<false>(a, reinterpret_cast<hipStream_t>(stream));
 }

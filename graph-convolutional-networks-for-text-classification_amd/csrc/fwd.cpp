@@ -27,6 +27,9 @@ int first_product(const gcnk_gcn_fwd& r, const float* W1, void* stream) {
   if (r.x.plan)
     return spmm_ref(r.x, W1, r.F, r.F, r.s1, r.lds1, nullptr, GCNK_EPI_NONE, nullptr, 0, 1.f, 1.f, 0, 0, nullptr,
                     stream);
+  if (r.x_ctr)
+    return gcnk_gemm_smallm_f32(r.x_rows, r.F, r.x_cols, r.x_dense, r.ldx, W1, r.F, r.s1, r.lds1, r.gemm_ws,
+                                r.gemm_ws_bytes, r.x_ctr, r.x_ctr_bytes, stream);
   return gcnk_gemm_f32(0, 0, r.x_rows, r.F, r.x_cols, r.x_dense, r.ldx, W1, r.F, r.s1, r.lds1, nullptr,
                        GCNK_GEMM_EPI_NONE, nullptr, 0, 1.f, r.x_split_k, r.gemm_ws, r.gemm_ws_bytes, stream);
 }
@@ -102,7 +105,7 @@ extern "C" int32_t gcnk_gcn_fwd_layout(int64_t* out, int32_t n) {
                        (int64_t)offsetof(gcnk_gcn_fwd, aF), (int64_t)offsetof(gcnk_gcn_fwd, aP),
                        (int64_t)offsetof(gcnk_gcn_fwd, ld_h1_tmp), (int64_t)offsetof(gcnk_plan_ref, lanes_hint),
                        (int64_t)sizeof(gcnk_gcn_bwd), (int64_t)offsetof(gcnk_gcn_bwd, xT),
-                       (int64_t)offsetof(gcnk_gcn_bwd, bwd2_ws_bytes)};
+                       (int64_t)offsetof(gcnk_gcn_bwd, bwd2_ws_bytes), (int64_t)offsetof(gcnk_gcn_fwd, x_ctr)};
   const int32_t m = (int32_t)(sizeof(v) / sizeof(v[0]));
   for (int32_t i = 0; i < n && i < m; ++i) out[i] = v[i];
   return m;

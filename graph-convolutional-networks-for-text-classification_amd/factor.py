@@ -37,7 +37,10 @@ MAX_HUBS = 128    # hub rows staged in LDS (S_T [hubs x F]; the kernel checks th
 # tiled GEMM took 13.7).  A one-launch split-K kernel with two levels of
 # last-arriver slab sums measured 12.1 us (round 4, DESIGN §5: each coherent
 # hand-off is a ~2 us memory round trip) and was removed.
-XHUB = os.environ.get("GCNK_FACTOR_XHUB", "spmm")
+# "onepass" (default, round 5): a dense copy of the hub rows through the
+# one-launch small-M GEMM (csrc/smallm.hip: ~20 K ranges x 16-column tiles,
+# each tile's partials summed by its last workgroup) -- no slab-reduce launch.
+XHUB = os.environ.get("GCNK_FACTOR_XHUB", "onepass")
 MAX_KC = 128      # X's light-row column range (U's width)
 ROWS_PER_BLOCK = 32   # csrc/factor.hip kRB
 # record words before the items: 33 row offsets | 3 pad | 32 row ids (-1 past
@@ -57,11 +60,18 @@ class HubFactor:
     __slots__ = ("M", "H", "K", "hubs", "k0", "Kc", "U", "perm", "rec", "rec_words", "nblk", "x_hub",
                  "x_hub_dense", "_src")
 
+    def onepass(self):
+        """X_hubs W1 runs on the one-launch small-M GEMM (gcnk_gemm_smallm_f32)."""
+        return XHUB == "onepass" and self.x_hub_dense is not None and self.H <= 64 and \
+            self.x_hub_dense.stride(0) % 4 == 0
+
     def hub_times(self, W):
         """S_T = X[hubs] @ W  (the hub rows of reference layer.py:102)."""
-        from .ops import gemm, spmm
+        from .ops import gemm, gemm_smallm, spmm
         if self.x_hub_dense is None:
             return spmm(self.x_hub, W)
+        if self.onepass():
+            return gemm_smallm(self.x_hub_dense, W)
         return gemm(self.x_hub_dense, W)
 
 
@@ -176,7 +186,7 @@ def build(adj, xop):
         f.x_hub_dense = None
         kx = x.shape[1]
         fits = H * kx * 4 <= 64 << 20
-        if fits and XHUB == "gemm":
+        if fits and XHUB in ("gemm", "onepass"):
             # rows padded to a multiple of 4 floats (the GEMM's float4 loads)
             d = torch.zeros((H, (kx + 3) // 4 * 4), dtype=torch.float32, device=dev)
             d[torch.repeat_interleave(torch.arange(H, device=dev), lens, output_size=tot), x.colind[idx].long()] = \
@@ -184,7 +194,10 @@ def build(adj, xop):
             f.x_hub_dense = d[:, :kx]
     else:
         f.x_hub = None
-        f.x_hub_dense = xop.dense.index_select(0, f.hubs).contiguous()
+        kx = xop.shape[1]
+        d = torch.zeros((H, (kx + 3) // 4 * 4), dtype=torch.float32, device=dev)   # rows padded to 4 floats
+        d[:, :kx] = xop.dense.index_select(0, f.hubs)
+        f.x_hub_dense = d[:, :kx]
     if int(overflow.item()) != 0:
         raise RuntimeError("factor.build: A_H records overflowed their sized length (internal error)")
     return f

@@ -326,6 +326,45 @@ def dense_gc1(d, W1, b1, W2, epilogue=_lib.EPI_BIAS_RELU, mask=None, scale=1.0, 
     return H1, S2
 
 
+_SMALLM_SCRATCH = {}
+
+
+def _smallm_scratch(M, N, K, dev):
+    """(workspace, zeroed counter region) of gcnk_gemm_smallm_f32 for torch's
+    current stream: concurrent calls on different streams never share a
+    counter region; a captured graph keeps using the ones it was captured with
+    (never freed)."""
+    key = (M, N, K, dev.index, torch.cuda.current_stream(dev).cuda_stream)
+    hit = _SMALLM_SCRATCH.get(key)
+    if hit is None:
+        lib = _lib.load()
+        wsb, cb = int(lib.gcnk_gemm_smallm_workspace_bytes(M, N, K)), int(lib.gcnk_gemm_smallm_counter_bytes(N))
+        hit = _SMALLM_SCRATCH[key] = (torch.empty((wsb + 3) // 4, dtype=torch.float32, device=dev), wsb,
+                                      torch.zeros((cb + 3) // 4, dtype=torch.int32, device=dev), cb)
+    return hit
+
+
+def gemm_smallm(A, B, out=None):
+    """C = A @ B for A [M x K] with M <= 64 (the dense hub rows of X times W1,
+    reference layer.py:102 on the topic rows) in one launch
+    (gcnk_gemm_smallm_f32).  A's rows must be padded to a multiple of 4 floats
+    (stride(0) % 4 == 0) and 16-B aligned."""
+    A = _dense_f32(A, "A")
+    B = _dense_f32(B, "B")
+    M, K = A.shape
+    if B.shape[0] != K:
+        raise RuntimeError(f"gemm_smallm shape mismatch: {tuple(A.shape)} @ {tuple(B.shape)}")
+    N = B.shape[1]
+    if out is None:
+        out = torch.empty((M, N), dtype=torch.float32, device=A.device)
+    ws, wsb, ctr, cb = _smallm_scratch(M, N, K, A.device)
+    with torch.cuda.device(A.device):
+        rc = _lib.load().gcnk_gemm_smallm_f32(M, N, K, _ptr(A), A.stride(0), _ptr(B), B.stride(0), _ptr(out),
+                                              out.stride(0), _ptr(ws), wsb, _ptr(ctr), cb, _stream(A.device))
+    _lib.check(rc, "gcnk_gemm_smallm_f32")
+    return out
+
+
 def default_split_k(M, N, K, trans=False):
     """K-slabs for a GEMM: only long reductions with a small output (H^T g,
     K = nodes) are split; short ones (H1 W2, K = 200) stay whole so the skinny

@@ -39,7 +39,8 @@ class GcnFwd(_c.Structure):
                 ("Kc", _c.c_int32), ("nhub", _c.c_int32), ("k0", _c.c_int32), ("rec_words", _c.c_int32),
                 ("U", _c.c_void_p), ("ldu", _c.c_int64), ("rec", _c.c_void_p),
                 ("aF", PlanRef), ("aP", PlanRef), ("s2", _c.c_void_p), ("lds2", _c.c_int64),
-                ("h1_tmp", _c.c_void_p), ("ld_h1_tmp", _c.c_int64)]
+                ("h1_tmp", _c.c_void_p), ("ld_h1_tmp", _c.c_int64), ("x_ctr", _c.c_void_p),
+                ("x_ctr_bytes", _c.c_int64)]
 
 
 class GcnBwd(_c.Structure):
@@ -59,12 +60,12 @@ BWD_AX_DIRECT = 1
 
 def layout_ok():
     """The ctypes mirrors match the library's struct layout (gcnk_gcn_fwd_layout)."""
-    buf = (_c.c_int64 * 11)()
-    n = _lib.load().gcnk_gcn_fwd_layout(buf, 11)
+    buf = (_c.c_int64 * 12)()
+    n = _lib.load().gcnk_gcn_fwd_layout(buf, 12)
     want = [_c.sizeof(PlanRef), _c.sizeof(GcnFwd), GcnFwd.x.offset, GcnFwd.U.offset, GcnFwd.aF.offset,
             GcnFwd.aP.offset, GcnFwd.ld_h1_tmp.offset, PlanRef.lanes_hint.offset, _c.sizeof(GcnBwd),
-            GcnBwd.xT.offset, GcnBwd.bwd2_ws_bytes.offset]
-    return n == 11 and list(buf) == want
+            GcnBwd.xT.offset, GcnBwd.bwd2_ws_bytes.offset, GcnFwd.x_ctr.offset]
+    return n == 12 and list(buf) == want
 
 
 def _fill_plan(ref, plan, F, lanes, device, keep):
@@ -156,8 +157,19 @@ class ForwardRecord:
             keep.append(x_dense)
             s.x_split_k = ops.default_split_k(rows, F, cols)
         s.x_rows, s.x_cols = rows, cols
-        # GEMM workspace: split-K slabs of X W1 (dense X); H1 W2 runs unsplit
-        gws = int(lib.gcnk_gemm_workspace_bytes(rows, F, cols, s.x_split_k)) if x_dense is not None else 0
+        onepass = kind == FACTORED and fac.onepass()
+        if onepass:   # S_T = X_hubs W1 on the one-launch small-M GEMM: its counter region
+            cb = int(lib.gcnk_gemm_smallm_counter_bytes(F))
+            ctr = torch.zeros((cb + 3) // 4, dtype=torch.int32, device=device)
+            keep.append(ctr)
+            s.x_ctr, s.x_ctr_bytes = ctr.data_ptr(), cb
+        # GEMM workspace: split-K slabs of X W1 (dense X) or the small-M GEMM's
+        # partials; H1 W2 runs unsplit
+        gws = 0
+        if onepass:
+            gws = int(lib.gcnk_gemm_smallm_workspace_bytes(rows, F, cols))
+        elif x_dense is not None:
+            gws = int(lib.gcnk_gemm_workspace_bytes(rows, F, cols, s.x_split_k))
         if gws > 0:
             g = torch.empty((gws + 3) // 4, dtype=torch.float32, device=device)
             keep.append(g)

@@ -290,6 +290,22 @@ int gcnk_dense_gc1_f32(int32_t M, int32_t K, int32_t F, int32_t P, const float* 
 int gcnk_aggregate_f32(const int32_t* rowptr, const int32_t* colind, const float* val, int32_t M, const float* X,
                        int64_t ldx, int32_t K, float* out, int64_t ldo, int32_t Kp, void* stream);
 
+/* ---------------------------------------------------------------------------
+ * Small-M, long-K GEMM in one launch (csrc/smallm.hip): C = A B with A
+ * [M x K] dense, M <= 64 (lda % 4 == 0, A and B 16-B aligned, ldb % 4 == 0) --
+ * the hub rows of X times W1 (layer.py:102 on the topic rows) for the
+ * factored gc1.  K split into ~20 ranges x 16-column tiles; each tile's
+ * partials (workspace: gcnk_gemm_smallm_workspace_bytes) are summed in range
+ * order by the tile's last workgroup (arrival counters: a caller region of
+ * gcnk_gemm_smallm_counter_bytes, zero on entry, left zero on return;
+ * concurrent calls need regions of their own).  Bitwise reproducible.
+ * ------------------------------------------------------------------------- */
+int64_t gcnk_gemm_smallm_workspace_bytes(int32_t M, int32_t N, int32_t K);
+int64_t gcnk_gemm_smallm_counter_bytes(int32_t N);
+int gcnk_gemm_smallm_f32(int32_t M, int32_t N, int32_t K, const float* A, int64_t lda, const float* B, int64_t ldb,
+                         float* C, int64_t ldc, float* workspace, int64_t workspace_bytes, int32_t* counters,
+                         int64_t counter_bytes, void* stream);
+
 /* The hub factorisation's (A-hat, X)-fixed operands, built on the device once
  * per operand pair (csrc/factor_build.hip; factor.py drives it, the host
  * restatement is oracle/factor_host.py):
@@ -372,6 +388,8 @@ typedef struct gcnk_gcn_fwd {
   int64_t lds2;
   float* h1_tmp;               /* SPMM_GEMM scratch H1 when H1 == NULL */
   int64_t ld_h1_tmp;
+  int32_t* x_ctr;              /* non-NULL: the first product on the one-pass small-M GEMM */
+  int64_t x_ctr_bytes;         /* (gcnk_gemm_smallm_f32; gemm_ws its workspace), zeroed once */
 } gcnk_gcn_fwd;
 
 int gcnk_gcn_forward_f32(const gcnk_gcn_fwd* rec,
@@ -416,8 +434,8 @@ int gcnk_gcn_backward_f32(const gcnk_gcn_bwd* rec, const float* G, const float* 
 
 /* Layout of the record structs for bindings that mirror them: writes up to n
  * of {sizeof plan_ref, sizeof gcn_fwd, offsetof x, U, aF, aP, ld_h1_tmp,
- * plan_ref.lanes_hint, sizeof gcn_bwd, gcn_bwd.xT, gcn_bwd.bwd2_ws_bytes} to
- * out and returns how many exist. */
+ * plan_ref.lanes_hint, sizeof gcn_bwd, gcn_bwd.xT, gcn_bwd.bwd2_ws_bytes,
+ * gcn_fwd.x_ctr} to out and returns how many exist. */
 int32_t gcnk_gcn_fwd_layout(int64_t* out, int32_t n);
 
 /* ---------------------------------------------------------------------------

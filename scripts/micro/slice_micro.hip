@@ -231,7 +231,7 @@ __device__ void slice_role(const Args& a, int u) {
   const int4 un = a.units[u];
   if (un.x < 0) return;  // padding (workgroup-uniform)
   const int g = lane / SL, c = lane % SL;
-  const int col = un.w * SL + c;
+  const int col = (un.w & 0xffff) * SL + c;
   const bool colok = col < a.Q;
   const int colc = colok ? col : 0;
   const int e = un.z;
@@ -262,6 +262,22 @@ __device__ void slice_role(const Args& a, int u) {
     for (int v = 1; v < WPB; ++v) add4(sum, s_red[v][c]);
     if (colok) store_nt(a.C, (int64_t)un.x * a.P4 + col, relu_bias(sum, a.bias[col]));
   }
+}
+
+// mixed slices: unit.w = slice | (slice width in float4 << 16): rows longer than
+// the split threshold take half-line slices (SL 4), the rest line slices (SL 8)
+template <int WPB, int RPW, int U, int US>
+__global__ void __launch_bounds__(WPB * 64) mixed_kernel(Args a) {
+  stamp(a, 0);
+  const int b = blockIdx.x;
+  if (b < a.nhb) {
+    const int sw = __builtin_amdgcn_readfirstlane(a.units[b].w >> 16);
+    if (sw == 4) slice_role<WPB, 4, US>(a, b);
+    else slice_role<WPB, 8, US>(a, b);
+  } else {
+    light_role<WPB, RPW, U>(a, b - a.nhb);
+  }
+  stamp(a, 3);
 }
 
 template <int WPB, int RPW, int U, int UH>
@@ -401,6 +417,35 @@ static Plan slice_plan(const Csr& A, const std::vector<char>& hub, int WPB, int 
   return P;
 }
 
+// rows with more than `split` items in half-line slices (SL 4, both halves of a
+// line on one XCD), the rest in line slices (SL 8); longest first
+static Plan mixed_plan(const Csr& A, const std::vector<char>& hub, int WPB, int RPW, int Q, int split) {
+  Plan P{};
+  P.WPB = WPB; P.RPW = RPW;
+  light_part(A, hub, P);
+  std::vector<int> rows;
+  for (int r = 0; r < A.M; ++r) if (hub[r]) rows.push_back(r);
+  std::sort(rows.begin(), rows.end(), [&](int x, int y) { return A.rp[x + 1] - A.rp[x] > A.rp[y + 1] - A.rp[y]; });
+  std::vector<std::vector<int4>> q(NX);
+  for (int r : rows) {
+    const int n = A.rp[r + 1] - A.rp[r];
+    const int sl = n > split ? 4 : 8, ns = (Q + sl - 1) / sl;
+    for (int s = 0; s < ns; ++s) {
+      const int x = sl == 4 ? (s / 2) % NX : s % NX;
+      q[x].push_back(make_int4(r, A.rp[r], A.rp[r + 1], s | (sl << 16)));
+    }
+  }
+  size_t rounds = 0;
+  for (auto& x : q) rounds = std::max(rounds, x.size());
+  for (size_t k = 0; k < rounds; ++k)
+    for (int c = 0; c < NX; ++c) P.units.push_back(k < q[c].size() ? q[c][k] : make_int4(-1, 0, 0, 8 << 16));
+  P.nhb = (int)P.units.size();
+  char nm[96];
+  snprintf(nm, sizeof nm, "mixed WPB%d split%d", WPB, split);
+  P.name = nm;
+  return P;
+}
+
 template <typename T>
 static T* upload(const std::vector<T>& h) {
   T* d;
@@ -469,6 +514,9 @@ int main(int argc, char** argv) {
   plans.push_back(build(slice_plan(A, hub, 16, 1, 4, Q), Q)); // 4
   plans.push_back(build(slice_plan(A, hub, 16, 1, 16, Q), Q));// 5
   plans.push_back(build(slice_plan(A, hub, 8, 1, 4, Q), Q));  // 6
+  plans.push_back(build(mixed_plan(A, hub, 16, 1, Q, 900), Q));  // 7
+  plans.push_back(build(mixed_plan(A, hub, 16, 1, Q, 500), Q));  // 8
+  plans.push_back(build(mixed_plan(A, hub, 8, 1, Q, 500), Q));  // 9
 
   int P4 = 50;
   auto args = [&](const Built& b, int s, int nhb) {
@@ -506,6 +554,9 @@ int main(int argc, char** argv) {
     add("slice WPB16 SL4 U8", 4, which, (slice_kernel<16, 1, 8, 4, 8>));
     add("slice WPB16 SL16 U8", 5, which, (slice_kernel<16, 1, 8, 16, 8>));
     add("slice WPB8 SL4 U8", 6, which, (slice_kernel<8, 1, 8, 4, 8>));
+    add("mixed WPB16 split900", 7, which, (mixed_kernel<16, 1, 8, 8>));
+    add("mixed WPB16 split500", 8, which, (mixed_kernel<16, 1, 8, 8>));
+    add("mixed WPB8 split500", 9, which, (mixed_kernel<8, 1, 8, 8>));
   }
 
   const char* only = getenv("NS_ONLY");

@@ -402,6 +402,38 @@ def test_gemm_small_m_split_k(shape, split):
     assert torch.equal(got, gemm(Ad, B.to(DEV), split_k=split))
 
 
+@pytest.mark.parametrize("shape", [(50, 200, 7463), (64, 200, 8192), (1, 4, 512), (17, 116, 1000), (64, 13, 100),
+                                   (50, 8, 7463), (33, 200, 30000)])
+def test_gemm_small_m_one_pass(shape):
+    """gcnk_gemm_smallm_f32 (one launch: K ranges x 16-column tiles, each tile's
+    partials summed in range order by its last workgroup) against float64:
+    M <= 64 incl. 1, N not a multiple of 16, K not a multiple of 4 (rows padded
+    to 4 floats), a K needing 32-chunk ranges; bitwise reproducible from call
+    to call and on a second stream (own counter region); the counter region is
+    left zeroed (re-armed by each tile's last workgroup)."""
+    from graph_convolutional_networks_for_text_classification_amd import ops
+    M, N, K = shape
+    rng = np.random.default_rng(M + N + K)
+    Kp = (K + 3) // 4 * 4
+    Ab = torch.zeros((M, Kp), dtype=torch.float32)
+    Ab[:, :K] = torch.from_numpy(rng.standard_normal((M, K)).astype(np.float32))
+    A = Ab.to(DEV)[:, :K]
+    B = torch.from_numpy(rng.standard_normal((K, N)).astype(np.float32)).to(DEV)
+    C = ops.gemm_smallm(A, B)
+    want = A.cpu().double().numpy() @ B.cpu().double().numpy()
+    _close(C, want, rtol=1e-5, atol=1e-5 * np.sqrt(K))
+    assert torch.equal(ops.gemm_smallm(A, B), C)
+    side = torch.cuda.Stream()
+    side.wait_stream(torch.cuda.current_stream())
+    with torch.cuda.stream(side):
+        C2 = ops.gemm_smallm(A, B)
+    torch.cuda.current_stream().wait_stream(side)
+    assert torch.equal(C2, C)
+    torch.cuda.synchronize()
+    for key, (_, _, ctr, _) in ops._SMALLM_SCRATCH.items():
+        assert int(ctr.abs().sum()) == 0, key
+
+
 def test_gemm_epilogues_and_split_k():
     g = torch.Generator().manual_seed(1)
     A = torch.randn(500, 96, generator=g)

@@ -4,7 +4,7 @@
 //    row-major (trainer.py:226-238) -- which ATen re-coalesces on every call;
 //    here they are converted once: stable radix sort of (row * K + col), runs
 //    of equal keys summed in input order (what ATen's coalesce computes), row
-//    counts (integer atomics: exact) and a scan into row pointers;
+//    pointers as the lower bounds of each row in the sorted output;
 //  * CSR transpose (stable), for the A^T / X^T operands of the autograd
 //    products (the backward of th.spmm(adj, support) / th.spmm(X, W) at
 //    layer.py:102,106 needs sparse^T g).
@@ -78,11 +78,14 @@ __global__ void run_heads_kernel(const uint64_t* __restrict__ keys, int64_t nnz,
 }
 
 // at each run head: the run's values summed in input order (the sort is stable),
-// written at the run's rank (pos = inclusive scan of heads), and the row counted
+// written at the run's rank (pos = inclusive scan of heads), with the run's row
+// in orow[rank] (the output rows are then sorted: the row pointers are their
+// lower bounds, no per-nonzero counting -- round 4 counted rows with one integer
+// atomic per run, 7,463 of them on each of R8 X's 50 dense topic rows: 2.2 ms)
 __global__ void run_sum_kernel(const uint64_t* __restrict__ keys, const int32_t* __restrict__ idx,
                                const int32_t* __restrict__ pos, const float* __restrict__ vals, int64_t nnz,
                                int32_t K, int32_t* __restrict__ colind, float* __restrict__ val,
-                               int32_t* __restrict__ cnt) {
+                               int32_t* __restrict__ orow) {
   const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
   if (i >= nnz || (i > 0 && keys[i] == keys[i - 1])) return;
   const uint64_t k = keys[i];
@@ -91,7 +94,22 @@ __global__ void run_sum_kernel(const uint64_t* __restrict__ keys, const int32_t*
   const int32_t o = pos[i] - 1;
   colind[o] = (int32_t)(k % (uint64_t)K);
   val[o] = v;
-  atomicAdd(&cnt[k / (uint64_t)K], 1);
+  orow[o] = (int32_t)(k / (uint64_t)K);
+}
+
+// rowptr[r] = first output position whose row >= r, over the n = pos[nnz - 1]
+// unique entries (orow sorted ascending)
+__global__ void row_bounds_kernel(const int32_t* __restrict__ orow, const int32_t* __restrict__ pos, int64_t nnz,
+                                  int32_t M, int32_t* __restrict__ rowptr) {
+  const int64_t r = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (r > M) return;
+  int64_t lo = 0, hi = pos[nnz - 1];
+  while (lo < hi) {
+    const int64_t mid = (lo + hi) >> 1;
+    if (orow[mid] < r) lo = mid + 1;
+    else hi = mid;
+  }
+  rowptr[r] = (int32_t)lo;
 }
 
 __global__ void poison_kernel(const int32_t* __restrict__ bad, int32_t M, int32_t* __restrict__ rowptr) {
@@ -228,8 +246,8 @@ extern "C" int gcnk_coo_to_csr(const int64_t* rows, const int64_t* cols, const f
   void* tmp = w + L.tmp;
   size_t tb = L.tmp_bytes;
   const unsigned nb = (unsigned)((nnz + 255) / 256);
-  int rc = hip_check(hipMemsetAsync(cnt, 0, ((size_t)M + 1) * 4, s), "coo_to_csr counts");
-  if (!rc) rc = hip_check(hipMemsetAsync(bad, 0, 4, s), "coo_to_csr flag");
+  (void)cnt;
+  int rc = hip_check(hipMemsetAsync(bad, 0, 4, s), "coo_to_csr flag");
   if (rc) return rc;
   hipLaunchKernelGGL(coo_keys_kernel, dim3(nb), dim3(256), 0, s, rows, cols, nnz, M, K, keys_in, idx_in, bad);
   if ((rc = launch_check("coo_keys_kernel"))) return rc;
@@ -242,12 +260,13 @@ extern "C" int gcnk_coo_to_csr(const int64_t* rows, const int64_t* cols, const f
   tb = L.tmp_bytes;
   rc = hip_check(hipcub::DeviceScan::InclusiveSum(tmp, tb, head, pos, (int)nnz, s), "coo_to_csr scan");
   if (rc) return rc;
+  // (head is free once scanned: it receives the output rows)
   hipLaunchKernelGGL(run_sum_kernel, dim3(nb), dim3(256), 0, s, keys_out, idx_out, pos, vals, nnz, K, colind, val,
-                     cnt);
+                     head);
   if ((rc = launch_check("run_sum_kernel"))) return rc;
-  tb = L.tmp_bytes;
-  rc = hip_check(hipcub::DeviceScan::ExclusiveSum(tmp, tb, cnt, rowptr, M + 1, s), "coo_to_csr row scan");
-  if (rc) return rc;
+  hipLaunchKernelGGL(row_bounds_kernel, dim3((unsigned)(((int64_t)M + 1 + 255) / 256)), dim3(256), 0, s, head, pos,
+                     nnz, M, rowptr);
+  if ((rc = launch_check("row_bounds_kernel"))) return rc;
   hipLaunchKernelGGL(poison_kernel, dim3(1), dim3(1), 0, s, bad, M, rowptr);
   return launch_check("poison_kernel");
 }

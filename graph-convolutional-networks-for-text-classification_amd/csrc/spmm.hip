@@ -119,6 +119,13 @@ constexpr int kRowU = GCNK_ROW_U;            // gathers in flight per lane for l
 // Not for 1-4 lanes (one-wave workgroups spread the light rows over the chip;
 // 256-thread ones measured 5.64 -> 6.14 us at F = 8).
 constexpr bool kNarrowWG = GCNK_NARROW_WG != 0;
+// smallest group width (lanes) that takes 256-thread workgroups with
+// workgroup-wide heavy segments (experiment knob; narrower groups run one-wave
+// workgroups)
+#ifndef GCNK_NARROW_MIN_LPR
+#define GCNK_NARROW_MIN_LPR 8
+#endif
+constexpr int kNarrowMin = GCNK_NARROW_MIN_LPR;
 constexpr int kWaveBlock = GCNK_WAVE_BLOCK;  // workgroup size for whole-wavefront groups
 constexpr int kLightRPW = GCNK_LIGHT_RPW;    // light rows per wavefront with whole-wavefront groups
 constexpr int kLightMax64 = 64 / kLightRPW;  // their nonzero limit (kLightRPW rows' items fill one 64-lane load)
@@ -662,7 +669,7 @@ spmm_row_kernel(RowPlan rp, int32_t nhb, const float* __restrict__ B, int64_t ld
   //      unit per workgroup, its WPB wavefronts interleaving the nonzeros and
   //      meeting in LDS.  Either way GS = SW * (LPR == 64 ? WPB : 1) groups
   //      share the segment and every sum has a fixed order.
-  constexpr bool WG = WPB > 1 && (LPR == 64 || (kNarrowWG && LPR >= 8));
+  constexpr bool WG = WPB > 1 && (LPR == 64 || (kNarrowWG && LPR >= kNarrowMin));
   constexpr int GS = WG ? SW * WPB : SW;
   __shared__ T s_red[WG ? WPB : 1][64];
   __shared__ int32_t s_last;
@@ -1119,7 +1126,7 @@ inline int choose_lpr(int32_t F, int lanes_hint) {
 }
 
 // Narrow groups use one-wave workgroups so a light launch still spans the chip.
-inline int choose_block(int lpr) { return lpr == 64 ? kWaveBlock : lpr >= 8 ? 256 : 64; }
+inline int choose_block(int lpr) { return lpr == 64 ? kWaveBlock : lpr >= kNarrowMin ? 256 : 64; }
 
 struct RowLaunch {
   RowPlan rp;
@@ -1141,7 +1148,7 @@ int launch_rows(const RowLaunch& a) {
   constexpr int SG = BLOCK / LPR, WPB = BLOCK / 64;
   constexpr int LPB = LPR == 64 ? SG * kLightRPW : SG;  // light units per workgroup
   // heavy segments: one per workgroup for whole-wavefront groups, else one per wavefront
-  const int64_t nhb = (LPR == 64 || (kNarrowWG && LPR >= 8 && WPB > 1)) ? (int64_t)a.rp.nhunits
+  const int64_t nhb = (LPR == 64 || (kNarrowWG && LPR >= kNarrowMin && WPB > 1)) ? (int64_t)a.rp.nhunits
                                                             : ((int64_t)a.rp.nhunits + WPB - 1) / WPB;
   const int64_t nlb = ((int64_t)a.rp.nunits - a.rp.nhunits + LPB - 1) / LPB;
   if (nhb + nlb == 0) return GCNK_OK;
@@ -1183,9 +1190,9 @@ int launch_rows(const RowLaunch& a) {
 template <int VEC>
 int dispatch_rows(int lpr, const RowLaunch& a) {
   switch (lpr) {
-    case 1: return launch_rows<64, 1, VEC, kRowU, 0>(a);
-    case 2: return launch_rows<64, 2, VEC, kRowU, 0>(a);
-    case 4: return launch_rows<64, 4, VEC, kRowU, 0>(a);
+    case 1: return launch_rows<kNarrowMin <= 1 ? 256 : 64, 1, VEC, kRowU, 0>(a);
+    case 2: return launch_rows<kNarrowMin <= 2 ? 256 : 64, 2, VEC, kRowU, 0>(a);
+    case 4: return launch_rows<kNarrowMin <= 4 ? 256 : 64, 4, VEC, kRowU, 0>(a);
     case 8: return launch_rows<256, 8, VEC, kRowU, 0>(a);
     case 16: return launch_rows<256, 16, VEC, kRowU, 0>(a);
     case 32: return launch_rows<256, 32, VEC, kRowU, 0>(a);
@@ -1444,7 +1451,7 @@ int host_plan(const int32_t* rp, const int32_t* ci, const float* vv, int32_t M, 
   }
   const int lpr = 64 / groups;
   const int block = choose_block(lpr), wpb = block / 64, sg = block / lpr;
-  const bool wg_heavy = lpr == 64 || (kNarrowWG && lpr >= 8 && wpb > 1);  // a heavy segment spans the workgroup
+  const bool wg_heavy = lpr == 64 || (kNarrowWG && lpr >= kNarrowMin && wpb > 1);  // a heavy segment spans the workgroup
   const int hpb = wg_heavy ? 1 : wpb;                            // heavy units per workgroup
   const int64_t seg = (int64_t)ipc * (lpr == 64 ? wpb : groups * (wg_heavy ? wpb : 1));  // nonzeros per segment
   // light-row limit: 2 * ipc for whole-wavefront groups (two light rows share a

@@ -10,6 +10,7 @@
 #   bench[:<args>]            python bench.py <args> (default --steps 200 --warmup 20) -> bench.json
 #   prof:<script>[:<args>]    rocprofv3 --kernel-trace --stats over python scripts/<script> -> <script>_stats/
 #   py:<script>[:<args>]      python scripts/<script> <args> -> <script>.log
+#   vpy:<variant>:<script>[:<args>]  the same on _variants/libgcnk_<variant>.so
 # Steps' outputs are summarised in profiles/ by hand (profiles/INDEX.md).
 cd "${GRAFT_REPO_ROOT:-/root/repo}" || exit 2
 export TMPDIR=/tmp
@@ -57,6 +58,11 @@ PY
       s="${rest%%:*}"; args="${rest#*:}"; [ "$args" = "$rest" ] && args=""
       timeout -k 10 600 python3 -u "scripts/$s" $args > "$out/${s%.py}.log" 2>&1
       rc=$?; tail -n 60 "$out/${s%.py}.log"; [ $rc -eq 0 ] || { echo "rc=$rc"; exit 3; } ;;
+    vpy)   # vpy:<variant name>:<script>[:<args>]: the script on _variants/libgcnk_<variant>.so
+      v="${rest%%:*}"; rest2="${rest#*:}"
+      s="${rest2%%:*}"; args="${rest2#*:}"; [ "$args" = "$rest2" ] && args=""
+      GCNK_LIB="_variants/libgcnk_$v.so" timeout -k 10 600 python3 -u "scripts/$s" $args > "$out/${s%.py}_$v.log" 2>&1
+      rc=$?; tail -n 60 "$out/${s%.py}_$v.log"; [ $rc -eq 0 ] || { echo "rc=$rc"; exit 3; } ;;
     *) echo "unknown step $step"; exit 2 ;;
   esac
 done

@@ -418,7 +418,10 @@ def test_gemm_small_m_one_pass(shape):
     Ab = torch.zeros((M, Kp), dtype=torch.float32)
     Ab[:, :K] = torch.from_numpy(rng.standard_normal((M, K)).astype(np.float32))
     A = Ab.to(DEV)[:, :K]
-    B = torch.from_numpy(rng.standard_normal((K, N)).astype(np.float32)).to(DEV)
+    Np = (N + 3) // 4 * 4                    # (B's rows padded to 4 floats, as the kernel requires)
+    Bb = torch.zeros((K, Np), dtype=torch.float32)
+    Bb[:, :N] = torch.from_numpy(rng.standard_normal((K, N)).astype(np.float32))
+    B = Bb.to(DEV)[:, :N]
     C = ops.gemm_smallm(A, B)
     want = A.cpu().double().numpy() @ B.cpu().double().numpy()
     _close(C, want, rtol=1e-5, atol=1e-5 * np.sqrt(K))

@@ -131,8 +131,8 @@ SIGNATURES = {
         _vp]),                            # stream
     "gcnk_gemm_smallm_workspace_bytes": (_i64, [_i32, _i32, _i32]),
     "gcnk_gemm_smallm_counter_bytes": (_i64, [_i32]),
-    "gcnk_gemm_smallm_f32": (ctypes.c_int, [_i32, _i32, _i32, _vp, _i64, _vp, _i64, _vp, _i64, _vp, _i64, _vp, _i64,
-                                            _vp]),
+    "gcnk_gemm_smallm_f32": (ctypes.c_int, [_i32, _i32, _i32, _vp, _i64, _vp, _i64, _vp, _i64, _i32, _vp, _i64, _vp,
+                                            _i64, _vp]),
     "gcnk_aggregate_f32": (ctypes.c_int, [_vp, _vp, _vp, _i32, _vp, _i64, _i32, _vp, _i64, _i32, _vp]),
     # record (host struct gcnk_gcn_fwd), W1, b1, W2, b2, out, ldo, H1, ldh, epilogue, mask, ldm, scale,
     # keep_prob, seed, offset, rng_base, stream

@@ -1,4 +1,4 @@
-// Small-M, long-K GEMM in ONE launch (gfx950): C = A B for the dense hub rows
+// Small-M, long-K GEMM in ONE launch (gfx950): C = A B (or C += A B) for the dense hub rows
 // of X -- S_T = X[hubs] W1 of the factored gc1 (reference layer.py:102 on the
 // topic rows; R8: [50 x 7463] x [7463 x 200], 7.5 MB of operands, read once
 // per forward because W1 changes every step).
@@ -43,7 +43,7 @@ template <int KCH>
 __global__ void __launch_bounds__(256)
 gemm_smallm_onepass_kernel(int32_t M, int32_t N, int32_t K, int32_t nsplit, const float* __restrict__ A, int64_t lda,
                            const float* __restrict__ B, int64_t ldb, float* __restrict__ C, int64_t ldc,
-                           float* __restrict__ part, int32_t* __restrict__ ctr) {
+                           int32_t accumulate, float* __restrict__ part, int32_t* __restrict__ ctr) {
   constexpr int KR = 16 * KCH;
   constexpr int LS = KR + 4;   // s_Bt row stride (floats): 16-B reads of 4 consecutive k, banks spread
   __shared__ __attribute__((aligned(16))) float s_Bt[kCT * LS];
@@ -154,7 +154,7 @@ gemm_smallm_onepass_kernel(int32_t M, int32_t N, int32_t K, int32_t nsplit, cons
 #pragma unroll
   for (int r = 0; r < 4; ++r) {
     const int64_t m = 16 * w + 4 * q + r;
-    if (m < M && n < N) C[m * ldc + n] = sum[r];
+    if (m < M && n < N) C[m * ldc + n] = accumulate ? C[m * ldc + n] + sum[r] : sum[r];
   }
   if (tid == 0) __hip_atomic_store(ctr + t, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);   // re-armed
 }
@@ -184,8 +184,8 @@ extern "C" int64_t gcnk_gemm_smallm_counter_bytes(int32_t N) {
 }
 
 extern "C" int gcnk_gemm_smallm_f32(int32_t M, int32_t N, int32_t K, const float* A, int64_t lda, const float* B,
-                                   int64_t ldb, float* C, int64_t ldc, float* workspace, int64_t workspace_bytes,
-                                   int32_t* counters, int64_t counter_bytes, void* stream) {
+                                   int64_t ldb, float* C, int64_t ldc, int32_t accumulate, float* workspace,
+                                   int64_t workspace_bytes, int32_t* counters, int64_t counter_bytes, void* stream) {
   if (M <= 0 || N <= 0 || K <= 0 || !A || !B || !C || lda < K || ldb < N || ldc < N) {
     set_error("gcnk_gemm_smallm_f32: bad sizes or null operand (M=%d N=%d K=%d)", M, N, K);
     return GCNK_EARG;
@@ -207,7 +207,7 @@ extern "C" int gcnk_gemm_smallm_f32(int32_t M, int32_t N, int32_t K, const float
   hipStream_t s = reinterpret_cast<hipStream_t>(stream);
 #define GCNK_SMALLM(KCH_)                                                                                     \
   hipLaunchKernelGGL((gemm_smallm_onepass_kernel<KCH_>), grid, dim3(256), 0, s, M, N, K, nsplit, A, lda, B, ldb, C, \
-                     ldc, workspace, counters)
+                     ldc, accumulate, workspace, counters)
   switch (kch) {
     case 4: GCNK_SMALLM(4); break;
     case 8: GCNK_SMALLM(8); break;

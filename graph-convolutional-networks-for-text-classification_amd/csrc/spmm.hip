@@ -126,6 +126,13 @@ constexpr bool kNarrowWG = GCNK_NARROW_WG != 0;
 #define GCNK_NARROW_MIN_LPR 8
 #endif
 constexpr int kNarrowMin = GCNK_NARROW_MIN_LPR;
+// Heavy segments of whole-wavefront plans keep a padded copy of their items
+// (segment u's at u * segp, col -1 past its end), so a heavy workgroup loads
+// its items at an address it knows from its index, in flight with its unit
+// word -- no unit -> items dependency before the gathers.
+#ifndef GCNK_HEAVY_DIRECT
+#define GCNK_HEAVY_DIRECT 1
+#endif
 constexpr int kWaveBlock = GCNK_WAVE_BLOCK;  // workgroup size for whole-wavefront groups
 constexpr int kLightRPW = GCNK_LIGHT_RPW;    // light rows per wavefront with whole-wavefront groups
 constexpr int kLightMax64 = 64 / kLightRPW;  // their nonzero limit (kLightRPW rows' items fill one 64-lane load)
@@ -134,7 +141,7 @@ constexpr int kLightMax64 = 64 / kLightRPW;  // their nonzero limit (kLightRPW r
 // Plan layout (int32 words).  Header (16 words, see gcnk.h):
 //   0 magic  1 M  2 K  3 lane groups per wavefront (64 / LPR)  4 ipc (light-row limit)
 //   5 nunits  6 nhunits (heavy region, padded)  7 nheavy (rows of > 1 segment)
-//   8 ntile (chunks)  9 nred  10 nslabs  11 ntblk (tile blocks)  12 has_diag  13 nnz
+//   8 ntile (chunks)  9 nred  10 nslabs  11 ntblk (tile blocks)  12 has_diag | segp << 1  13 nnz
 //   14 nslots (partial slots)  15 nsingle (chunk items of single-chunk blocks, listed first)
 // Body: items int2[nnz] {col, value bits} in CSR order | units int4[nunits]
 //   {row (-1: empty), nz begin, nz end, heavy row * 64 + segment or -1}: the
@@ -143,13 +150,14 @@ constexpr int kLightMax64 = 64 / kLightRPW;  // their nonzero limit (kLightRPW r
 //   {row, first partial slot, nseg, 0} | tile part (descriptors,
 //   condensed columns, A fragments, reduce rows int4[64 * nred] {row (-1:
 //   none), first slab, slabs, diagonal value bits}, row lists, extracted
-//   diagonal float[64 * ntblk] in block order).
+//   diagonal float[64 * ntblk] in block order) | (segp > 0) the heavy units'
+//   items, padded: int2[nhunits][segp], col -1 past a unit's end.
 struct Layout {
-  int64_t M, nnz, nunits, nhunits, nheavy, nslots, ntile, nred, ntblk, has_diag;
-  int64_t items, units, heavy, tdesc, tcols, tfrag, red, trows, dval, total;
+  int64_t M, nnz, nunits, nhunits, nheavy, nslots, ntile, nred, ntblk, has_diag, segp;
+  int64_t items, units, heavy, tdesc, tcols, tfrag, red, trows, dval, hitems, total;
   __host__ __device__ explicit Layout(const int32_t* h) {
     M = h[1]; nunits = h[5]; nhunits = h[6]; nheavy = h[7]; ntile = h[8]; nred = h[9]; ntblk = h[11];
-    has_diag = h[12]; nnz = h[13]; nslots = h[14];
+    has_diag = h[12] & 1; segp = (uint32_t)h[12] >> 1; nnz = h[13]; nslots = h[14];
     items = 16;
     units = (items + 2 * nnz + 3) & ~3LL;
     heavy = units + 4 * nunits;
@@ -159,7 +167,8 @@ struct Layout {
     red = tfrag + (int64_t)kRB * kKC * ntile;
     trows = red + 4 * nred * kRB;
     dval = trows + (int64_t)kRB * ntblk;
-    total = dval + (has_diag ? (int64_t)kRB * ntblk : 0);
+    hitems = (dval + (has_diag ? (int64_t)kRB * ntblk : 0) + 3) & ~3LL;
+    total = hitems + 2 * nhunits * segp;   // padded heavy items int2[nhunits][segp]
   }
 };
 
@@ -394,6 +403,8 @@ struct RowPlan {
   int32_t* cnt;        // per heavy row x column tile: arrival counters, in the caller's
                        // counter region (zero on entry, re-armed by each row's last arriver)
   int32_t nunits, nhunits;
+  const int2* hitems;  // heavy units' items, padded to segp each (null: none)
+  int32_t segp;
 };
 
 // Partial slots are written and read with agent-coherent accesses (the sc1
@@ -512,6 +523,45 @@ __device__ __forceinline__ void gather_rows_wave(const int2* __restrict__ items,
       for (int j = 0; j < U; ++j)
         if (j0 + j < cnt) V::fma(acc, a[j], g[j]);
     }
+  }
+}
+
+// gather_rows_wave over a heavy unit's padded item copy (its items at
+// hi[0 .. segp), col -1 past the end): the item load's address is known from
+// the unit index alone, so it flies with the unit word's load.
+template <int VEC, int U, int S, bool O32>
+__device__ __forceinline__ void gather_rows_wave_direct(const int2* __restrict__ hi, int32_t segp, int q,
+                                                        const float* __restrict__ B, int64_t ldb, int64_t colv,
+                                                        bool colok, typename Vec<VEC>::T& acc) {
+  using V = Vec<VEC>;
+  using T = typename V::T;
+  const int lane = threadIdx.x & 63;
+  const uint32_t ldb4 = (uint32_t)ldb * 4u, col4 = colok ? (uint32_t)colv * 4u : 0u;
+  const int64_t colc = colok ? colv : 0;
+  for (int32_t base = q; base < segp; base += 64 * S) {
+    const int32_t k = base + S * lane;
+    const int2 mine = k < segp ? hi[k] : make_int2(-1, 0);
+    __builtin_amdgcn_s_waitcnt(0x0F70);  // vmcnt(0): the item words (and the unit word) have landed
+    // the segment's items are packed at the front: the valid lanes are a prefix
+    const int32_t cnt = __builtin_popcountll(__ballot(mine.x >= 0));  // wave-uniform
+    for (int32_t j0 = 0; j0 < cnt; j0 += U) {
+      T g[U];
+      float a[U];
+#pragma unroll
+      for (int j = 0; j < U; ++j) {
+        g[j] = V::zero();
+        a[j] = 0.f;
+        if (j0 + j < cnt) {
+          const int32_t c = __builtin_amdgcn_readlane(mine.x, j0 + j);
+          a[j] = __int_as_float(__builtin_amdgcn_readlane(mine.y, j0 + j));
+          g[j] = load_row<VEC, O32>(B, ldb, ldb4, c, colc, col4);
+        }
+      }
+#pragma unroll
+      for (int j = 0; j < U; ++j)
+        if (j0 + j < cnt) V::fma(acc, a[j], g[j]);
+    }
+    if (cnt < 64) break;
   }
 }
 
@@ -679,10 +729,17 @@ spmm_row_kernel(RowPlan rp, int32_t nhb, const float* __restrict__ B, int64_t ld
   const int32_t u = WG ? (int32_t)blockIdx.x : __builtin_amdgcn_readfirstlane((int32_t)blockIdx.x * WPB + w);
   if (u >= rp.nhunits) return;  // WG: uniform over the workgroup
   const int4 un = rp.units[u];
-  if (un.x < 0) return;           // padding of the XCD-class layout
-  stamp(epi, 1);
-  if constexpr (LPR == 64) gather_rows_wave<VEC, kHeavyU, GS, O32>(rp.items, un.y, un.z, q, B, ldb, colv, colok, acc);
-  else gather_rows<VEC, U, GS, O32>(rp.items, un.y, un.z, q, B, ldb, colv, colok, acc);
+  if (LPR == 64 && GCNK_HEAVY_DIRECT && rp.segp > 0) {
+    // the unit word and the padded items load together (a padding unit's items are all -1)
+    gather_rows_wave_direct<VEC, kHeavyU, GS, O32>(rp.hitems + (int64_t)u * rp.segp, rp.segp, q, B, ldb, colv, colok,
+                                                   acc);
+    if (un.x < 0) return;           // padding of the XCD-class layout (workgroup-uniform)
+  } else {
+    if (un.x < 0) return;           // padding of the XCD-class layout
+    stamp(epi, 1);
+    if constexpr (LPR == 64) gather_rows_wave<VEC, kHeavyU, GS, O32>(rp.items, un.y, un.z, q, B, ldb, colv, colok, acc);
+    else gather_rows<VEC, U, GS, O32>(rp.items, un.y, un.z, q, B, ldb, colv, colok, acc);
+  }
   wave_group_sum<LPR>(acc);  // the wave's SW groups (no-op at LPR = 64)
   if constexpr (WG) {
     if (w > 0) s_red[w][lane] = acc;
@@ -1582,6 +1639,15 @@ int host_plan(const int32_t* rp, const int32_t* ci, const float* vv, int32_t M, 
     }
   layout(hq, hpb);
   const int64_t nh = (int64_t)hp.units.size() / 4;
+  // padded item copies of the heavy units (whole-wavefront groups): stride = the
+  // longest unit, rounded up to 4 items
+  int64_t segp = 0;
+  if (GCNK_HEAVY_DIRECT && lpr == 64)
+    for (int64_t u = 0; u < nh; ++u)
+      if (hp.units[(size_t)(4 * u)] >= 0)
+        segp = std::max<int64_t>(segp, (int64_t)hp.units[(size_t)(4 * u + 2)] - hp.units[(size_t)(4 * u + 1)]);
+  segp = (segp + 3) & ~3LL;
+  if (segp > (1 << 29) || 2 * nh * segp >= (int64_t)INT32_MAX) segp = 0;   // (never for real plans: keep the old path)
   layout(lq, lpb);
   const int64_t nunits = (int64_t)hp.units.size() / 4;
   if (nunits >= (int64_t)INT32_MAX || nslots >= (int64_t)INT32_MAX || nheavy >= (1 << 25)) {
@@ -1590,7 +1656,8 @@ int host_plan(const int32_t* rp, const int32_t* ci, const float* vv, int32_t M, 
     return GCNK_EUNSUP;
   }
   const int32_t h[16] = {kMagic, M,     K,      groups, ipc,  (int32_t)nunits, (int32_t)nh, nheavy,
-                         ntile,  nred, nslabs, ntblk,  any_diag ? 1 : 0, (int32_t)nnz, (int32_t)nslots, nsingle};
+                         ntile,  nred, nslabs, ntblk,  (any_diag ? 1 : 0) | (int32_t)(segp << 1), (int32_t)nnz,
+                         (int32_t)nslots, nsingle};
   std::copy(h, h + 16, hp.hdr);
   return GCNK_OK;
 }
@@ -1616,6 +1683,15 @@ void classic_image(const HostPlan& hp, const int32_t* ci, const float* vv, int64
   put(L.red, hp.red.data(), hp.red.size());
   put(L.trows, hp.trows.data(), hp.trows.size());
   putf(L.dval, hp.dval);
+  for (int64_t u = 0; u < L.nhunits && L.segp > 0; ++u) {
+    const int32_t r = hp.units[(size_t)(4 * u)], b = hp.units[(size_t)(4 * u + 1)], e = hp.units[(size_t)(4 * u + 2)];
+    for (int64_t i = 0; i < L.segp; ++i) {
+      const size_t o = (size_t)(L.hitems + 2 * (u * L.segp + i));
+      const bool in = r >= 0 && b + i < e;
+      img[o] = in ? ci[b + i] : -1;
+      img[o + 1] = in && vv ? __builtin_bit_cast(int32_t, vv[b + i]) : 0;
+    }
+  }
 }
 
 // The row-unit + tile plan image for host CSR arrays.
@@ -1917,7 +1993,8 @@ static int spmm_impl(const void* plan, const int32_t* hdr, const float* B, int64
   // ---- remaining rows: row kernel (heavy rows finished in-launch)
   if (L.nunits > 0 && part != 1) {
     RowPlan rp{reinterpret_cast<const int2*>(p + L.items), reinterpret_cast<const int4*>(p + L.units),
-               reinterpret_cast<const int4*>(p + L.heavy), counters, (int32_t)L.nunits, (int32_t)L.nhunits};
+               reinterpret_cast<const int4*>(p + L.heavy), counters, (int32_t)L.nunits, (int32_t)L.nhunits,
+               L.segp > 0 ? reinterpret_cast<const int2*>(p + L.hitems) : nullptr, (int32_t)L.segp};
     RowLaunch a{rp, K, B, ldb, F, C, ldc, e, workspace, part_ld, pa, s};
     if (proj) return pa.P <= 8 ? dispatch_rows_proj<8>(lpr, a) : dispatch_rows_proj<32>(lpr, a);
     return vec4 ? dispatch_rows<4>(lpr, a) : dispatch_rows<1>(lpr, a);

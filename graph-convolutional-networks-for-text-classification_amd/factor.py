@@ -58,7 +58,64 @@ class HubFactor:
     """The (A-hat, X)-fixed operands of the factored gc1, resident on the device."""
 
     __slots__ = ("M", "H", "K", "hubs", "k0", "Kc", "U", "perm", "rec", "rec_words", "nblk", "x_hub",
-                 "x_hub_dense", "_src")
+                 "x_hub_dense", "_src", "_bwd")
+
+    def backward_operands(self, adj):
+        """(UT, aT_hub, x_hubT, Hp) for the factored gW1 (built on first use):
+
+            gW1 = X^T A-hat^T gZ1 = U~^T gZ1 + X_hubs^T (A_H^T gZ1)
+
+        (A-hat X = U~ + A_H X_hubs, U~ = U placed in X's columns k0 .. k0 + Kc).
+        UT [Kc x Mp]: U in row order, transposed, rows padded to 4 floats;
+        aT_hub: the CSR of A-hat^T's hub rows (A_H^T); x_hubT [K x Hp]: X's hub
+        rows transposed, Hp = H rounded up to 4, zero past H."""
+        b = getattr(self, "_bwd", None)
+        if b is not None:
+            return b
+        dev = self.U.device
+        M, H = self.M, self.H
+        Mp, Hp = (M + 3) // 4 * 4, (H + 3) // 4 * 4
+        inv = torch.empty(M, dtype=torch.int64)
+        inv[self.perm] = torch.arange(M)
+        UT = torch.zeros((self.Kc, Mp), dtype=torch.float32, device=dev)
+        UT[:, :M] = self.U[inv.to(dev), :self.Kc].t()
+        aT = adj.t()
+        rp = aT.rowptr.long()
+        lens = rp[self.hubs + 1] - rp[self.hubs]
+        hrp = torch.zeros(H + 1, dtype=torch.int64, device=dev)
+        hrp[1:] = torch.cumsum(lens, 0)
+        tot = int(hrp[-1])
+        idx = torch.repeat_interleave(rp[self.hubs] - hrp[:-1], lens, output_size=tot) + \
+            torch.arange(tot, device=dev, dtype=torch.int64)
+        aT_hub = CSR(hrp.to(torch.int32), aT.colind[idx], aT.val[idx], (H, M))
+        if self.x_hub_dense is not None:
+            xd = self.x_hub_dense
+        else:
+            xd = torch.zeros((H, self.K), dtype=torch.float32, device=dev)
+            xrp = self.x_hub.rowptr.long()
+            rows = torch.repeat_interleave(torch.arange(H, device=dev), xrp[1:] - xrp[:-1],
+                                           output_size=self.x_hub.nnz)
+            xd.index_put_((rows, self.x_hub.colind.long()), self.x_hub.val, accumulate=True)
+        x_hubT = torch.zeros((self.K, Hp), dtype=torch.float32, device=dev)
+        x_hubT[:, :H] = xd.t()
+        self._bwd = b = (UT, aT_hub, x_hubT, Hp)
+        return b
+
+    def grad_w1(self, adj, gZ1, out=None):
+        """gW1 [K x F] of the factored gc1 from gZ1 = dL/d(A-hat X W1)  (the
+        autograd of reference layer.py:102,106 in gc1): A_H^T gZ1 on the SpMM
+        (the hub rows of A-hat^T), X_hubs^T times it on the short-K GEMM, then
+        U^T gZ1 added into rows k0 .. k0 + Kc on the one-pass small-M GEMM."""
+        from .ops import gemm, gemm_smallm, spmm
+        UT, aT_hub, x_hubT, Hp = self.backward_operands(adj)
+        F = gZ1.shape[1]
+        Y = torch.zeros((Hp, F), dtype=torch.float32, device=gZ1.device)
+        spmm(aT_hub, gZ1, out=Y[:self.H])
+        gW1 = gemm(x_hubT, Y, out=out)
+        for c0 in range(0, self.Kc, 64):
+            c1 = min(self.Kc, c0 + 64)
+            gemm_smallm(UT[c0:c1], gZ1, out=gW1[self.k0 + c0:self.k0 + c1], accumulate=True)
+        return gW1
 
     def onepass(self):
         """X_hubs W1 runs on the one-launch small-M GEMM (gcnk_gemm_smallm_f32)."""

@@ -344,11 +344,11 @@ def _smallm_scratch(M, N, K, dev):
     return hit
 
 
-def gemm_smallm(A, B, out=None):
-    """C = A @ B for A [M x K] with M <= 64 (the dense hub rows of X times W1,
-    reference layer.py:102 on the topic rows) in one launch
-    (gcnk_gemm_smallm_f32).  A's rows must be padded to a multiple of 4 floats
-    (stride(0) % 4 == 0) and 16-B aligned."""
+def gemm_smallm(A, B, out=None, accumulate=False):
+    """C = A @ B (``accumulate``: out += A @ B) for A [M x K] with M <= 64 (the
+    dense hub rows of X times W1, reference layer.py:102 on the topic rows) in
+    one launch (gcnk_gemm_smallm_f32).  A's and B's rows must be padded to a
+    multiple of 4 floats (stride(0) % 4 == 0) and 16-B aligned."""
     A = _dense_f32(A, "A")
     B = _dense_f32(B, "B")
     M, K = A.shape
@@ -360,7 +360,8 @@ def gemm_smallm(A, B, out=None):
     ws, wsb, ctr, cb = _smallm_scratch(M, N, K, A.device)
     with torch.cuda.device(A.device):
         rc = _lib.load().gcnk_gemm_smallm_f32(M, N, K, _ptr(A), A.stride(0), _ptr(B), B.stride(0), _ptr(out),
-                                              out.stride(0), _ptr(ws), wsb, _ptr(ctr), cb, _stream(A.device))
+                                              out.stride(0), int(bool(accumulate)), _ptr(ws), wsb, _ptr(ctr), cb,
+                                              _stream(A.device))
     _lib.check(rc, "gcnk_gemm_smallm_f32")
     return out
 
@@ -574,6 +575,12 @@ class GraphConvFn(torch.autograd.Function):
         return gW, gb, gx, None, None
 
 
+# The factored forward's gW1 through the factor (factor.HubFactor.grad_w1:
+# A_H^T gZ1, X_hubs^T on the short-K GEMM, U^T gZ1 on the small-M GEMM) instead of
+# A-hat^T gZ1 at F then X^T gS1; GCNK_FACTOR_BWD=0 keeps the latter (A/B timing).
+FACTOR_BWD = os.environ.get("GCNK_FACTOR_BWD", "1") != "0"
+
+
 # The whole forward from one C call (record.py, gcnk_gcn_forward_f32) wherever
 # a record applies; GCNK_FORWARD_RECORD=0 issues it op by op (A/B timing).
 USE_RECORD = os.environ.get("GCNK_FORWARD_RECORD", "1") != "0"
@@ -656,7 +663,7 @@ class GCNFn(torch.autograd.Function):
         if res is not None:
             out, H1 = res
             ctx.xop, ctx.adj, ctx.scale = xop, adj, float(scale)
-            ctx.dax = None
+            ctx.dax = ctx.fac = None
             ctx.has_b1, ctx.has_b2 = b1 is not None, b2 is not None
             ctx.save_for_backward(W2, H1)
             return out
@@ -685,6 +692,7 @@ class GCNFn(torch.autograd.Function):
             out = spmm(adj, S2, bias=b2, epilogue=_lib.EPI_BIAS if b2 is not None else _lib.EPI_NONE)
         ctx.xop, ctx.adj, ctx.scale = xop, adj, float(scale)
         ctx.dax = dax
+        ctx.fac = fac if (dax is None and res is not None) else None
         ctx.has_b1, ctx.has_b2 = b1 is not None, b2 is not None
         ctx.save_for_backward(W2, H1)
         return out
@@ -718,6 +726,8 @@ class GCNFn(torch.autograd.Function):
         if need[0]:
             if ctx.dax is not None:   # Z1 = (A-hat X) W1  =>  gW1 = (A-hat X)^T gZ1
                 gW1 = gemm(ctx.dax.AX[:, :ctx.dax.K], gZ1, transA=True)
+            elif ctx.fac is not None and FACTOR_BWD:   # A-hat X = U~ + A_H X_hubs (factor.py)
+                gW1 = ctx.fac.grad_w1(ctx.adj, gZ1.contiguous())
             else:
                 gS1 = spmm(adjT, gZ1)
                 gW1 = ctx.xop.t_times(gS1)

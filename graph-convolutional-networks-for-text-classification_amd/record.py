@@ -50,22 +50,27 @@ class GcnBwd(_c.Structure):
                 ("aTP", PlanRef), ("aTF", PlanRef),
                 ("xT", PlanRef), ("x_dense", _c.c_void_p), ("ldx", _c.c_int64), ("gemm_ws", _c.c_void_p),
                 ("gemm_ws_bytes", _c.c_int64), ("gS2", _c.c_void_p), ("gZ1", _c.c_void_p), ("gS1", _c.c_void_p),
-                ("bwd2_ws", _c.c_void_p), ("bwd2_ws_bytes", _c.c_int64)]
+                ("bwd2_ws", _c.c_void_p), ("bwd2_ws_bytes", _c.c_int64), ("aTH", PlanRef), ("x_hubT", _c.c_void_p),
+                ("ld_xhT", _c.c_int64), ("nhub", _c.c_int32), ("nhub_p", _c.c_int32), ("Kc", _c.c_int32),
+                ("k0", _c.c_int32), ("UT", _c.c_void_p), ("ldut", _c.c_int64), ("y", _c.c_void_p),
+                ("sm_ws", _c.c_void_p), ("sm_ws_bytes", _c.c_int64), ("sm_ctr", _c.c_void_p),
+                ("sm_ctr_bytes", _c.c_int64)]
 
 
 FACTORED, SPMM_PROJ, SPMM_GEMM, DENSE_AX = 1, 2, 3, 4
 KIND_NAMES = {FACTORED: "factored", SPMM_PROJ: "spmm+proj", SPMM_GEMM: "spmm+gemm", DENSE_AX: "dense-ax"}
-BWD_AX_DIRECT = 1
+BWD_AX_DIRECT, BWD_FACTORED = 1, 2
 
 
 def layout_ok():
     """The ctypes mirrors match the library's struct layout (gcnk_gcn_fwd_layout)."""
-    buf = (_c.c_int64 * 12)()
-    n = _lib.load().gcnk_gcn_fwd_layout(buf, 12)
+    buf = (_c.c_int64 * 14)()
+    n = _lib.load().gcnk_gcn_fwd_layout(buf, 14)
     want = [_c.sizeof(PlanRef), _c.sizeof(GcnFwd), GcnFwd.x.offset, GcnFwd.U.offset, GcnFwd.aF.offset,
             GcnFwd.aP.offset, GcnFwd.ld_h1_tmp.offset, PlanRef.lanes_hint.offset, _c.sizeof(GcnBwd),
-            GcnBwd.xT.offset, GcnBwd.bwd2_ws_bytes.offset, GcnFwd.x_ctr.offset]
-    return n == 12 and list(buf) == want
+            GcnBwd.xT.offset, GcnBwd.bwd2_ws_bytes.offset, GcnFwd.x_ctr.offset, GcnBwd.aTH.offset,
+            GcnBwd.sm_ctr_bytes.offset]
+    return n == 14 and list(buf) == want
 
 
 def _fill_plan(ref, plan, F, lanes, device, keep):
@@ -218,13 +223,31 @@ class BackwardRecord:
         adjT = adj.t()
         keep.append(adjT)
         dax = ops.dense_ax_for(adj, xop, F, P)
-        for ref, width in ((s.aTP, P), (s.aTF, F)) if dax is None else ((s.aTP, P),):
+        fac = ops.factor_for(adj, xop) if dax is None and ops.FACTOR_BWD else None
+        if fac is not None and not (P <= 32 and F % 4 == 0 and F <= 256):   # (the factored forward's range)
+            fac = None
+        for ref, width in ((s.aTP, P), (s.aTF, F)) if dax is None and fac is None else ((s.aTP, P),):
             pl = adjT.plan(ops.default_ipc(adjT, width, 0), int(lib.gcnk_spmm_groups(width, 0)), DENSE_THRESHOLD)
             _fill_plan(ref, pl, width, 0, device, keep)
             keep.append(pl)
         rows, cols = xop.shape
         s.x_rows, s.x_cols = rows, cols
-        if dax is not None:        # gW1 = (A-hat X)^T gZ1 (the DENSE_AX forward's association)
+        if fac is not None:        # gW1 = X_hubs^T (A_H^T gZ1) + U~^T gZ1 (factor.HubFactor.grad_w1)
+            UT, aT_hub, x_hubT, Hp = fac.backward_operands(adj)
+            s.flags = BWD_FACTORED
+            pl = aT_hub.plan(ops.default_ipc(aT_hub, F, 0), int(lib.gcnk_spmm_groups(F, 0)), DENSE_THRESHOLD)
+            _fill_plan(s.aTH, pl, F, 0, device, keep)
+            y = torch.zeros((Hp, F), dtype=torch.float32, device=device)
+            cb = int(lib.gcnk_gemm_smallm_counter_bytes(F))
+            ctr = torch.zeros((cb + 3) // 4, dtype=torch.int32, device=device)
+            wsb = int(lib.gcnk_gemm_smallm_workspace_bytes(min(64, fac.Kc), F, M))
+            ws = torch.empty((wsb + 3) // 4, dtype=torch.float32, device=device)
+            keep += [pl, aT_hub, UT, x_hubT, y, ctr, ws]
+            s.x_hubT, s.ld_xhT, s.nhub, s.nhub_p, s.Kc, s.k0 = x_hubT.data_ptr(), x_hubT.stride(0), fac.H, Hp, \
+                fac.Kc, fac.k0
+            s.UT, s.ldut, s.y = UT.data_ptr(), UT.stride(0), y.data_ptr()
+            s.sm_ws, s.sm_ws_bytes, s.sm_ctr, s.sm_ctr_bytes = ws.data_ptr(), wsb, ctr.data_ptr(), cb
+        elif dax is not None:        # gW1 = (A-hat X)^T gZ1 (the DENSE_AX forward's association)
             s.flags = BWD_AX_DIRECT
             s.x_dense, s.ldx = dax.AX.data_ptr(), dax.AX.stride(0)
             s.x_rows, s.x_cols = M, dax.K
@@ -254,7 +277,7 @@ class BackwardRecord:
         gZ1 = torch.empty((M, F), dtype=torch.float32, device=device)
         keep += [gS2, gZ1]
         s.gS2, s.gZ1 = gS2.data_ptr(), gZ1.data_ptr()
-        if dax is None:
+        if dax is None and fac is None:
             gS1 = torch.empty((rows, F), dtype=torch.float32, device=device)
             keep.append(gS1)
             s.gS1 = gS1.data_ptr()

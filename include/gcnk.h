@@ -292,7 +292,8 @@ int gcnk_aggregate_f32(const int32_t* rowptr, const int32_t* colind, const float
 
 /* ---------------------------------------------------------------------------
  * Small-M, long-K GEMM in one launch (csrc/smallm.hip): C = A B with A
- * [M x K] dense, M <= 64 (lda % 4 == 0, A and B 16-B aligned, ldb % 4 == 0) --
+ * [M x K] dense, M <= 64 (lda % 4 == 0, A and B 16-B aligned, ldb % 4 == 0); accumulate != 0:
+ * C += A B (the backward's gW1 rows of the factored operand U) --
  * the hub rows of X times W1 (layer.py:102 on the topic rows) for the
  * factored gc1.  K split into ~20 ranges x 16-column tiles; each tile's
  * partials (workspace: gcnk_gemm_smallm_workspace_bytes) are summed in range
@@ -303,8 +304,8 @@ int gcnk_aggregate_f32(const int32_t* rowptr, const int32_t* colind, const float
 int64_t gcnk_gemm_smallm_workspace_bytes(int32_t M, int32_t N, int32_t K);
 int64_t gcnk_gemm_smallm_counter_bytes(int32_t N);
 int gcnk_gemm_smallm_f32(int32_t M, int32_t N, int32_t K, const float* A, int64_t lda, const float* B, int64_t ldb,
-                         float* C, int64_t ldc, float* workspace, int64_t workspace_bytes, int32_t* counters,
-                         int64_t counter_bytes, void* stream);
+                         float* C, int64_t ldc, int32_t accumulate, float* workspace, int64_t workspace_bytes,
+                         int32_t* counters, int64_t counter_bytes, void* stream);
 
 /* The hub factorisation's (A-hat, X)-fixed operands, built on the device once
  * per operand pair (csrc/factor_build.hip; factor.py drives it, the host
@@ -408,8 +409,14 @@ int gcnk_gcn_forward_f32(const gcnk_gcn_fwd* rec,
  * G = dlogits [M x P] (contiguous), H1 [M x F] (ldh), W2 [F x P].  gW1, gb1,
  * gW2, gb2 are nullable (not computed); gb2 needs G's column sums only.
  * flags & GCNK_BWD_AX_DIRECT: x_dense holds A-hat X (the DENSE_AX forward) and
- * gW1 = (A-hat X)^T gZ1 directly (no gS1, no aTF plan). */
+ * gW1 = (A-hat X)^T gZ1 directly (no gS1, no aTF plan).
+ * flags & GCNK_BWD_FACTORED (the FACTORED forward, A-hat X = U~ + A_H X_hubs):
+ *   y = A_H^T gZ1 (aTH: A-hat^T's hub rows at width F), gW1 = X_hubs^T y
+ *   (x_hubT [x_cols x nhub_p], the short-K GEMM), then rows k0 .. k0 + Kc of
+ *   gW1 += U^T gZ1 (UT [Kc x >= M], gcnk_gemm_smallm_f32 with its workspace and
+ *   counter region) -- no gS1, no aTF plan, no X^T plan. */
 #define GCNK_BWD_AX_DIRECT 1
+#define GCNK_BWD_FACTORED 2
 typedef struct gcnk_gcn_bwd {
   int32_t M, F, P;             /* rows of A-hat, nhid, nclass */
   int32_t x_rows, x_cols;      /* X [x_rows x x_cols]: gW1 is [x_cols x F] */
@@ -427,6 +434,17 @@ typedef struct gcnk_gcn_bwd {
   float* gS1;                  /* scratch [M x F] */
   void* bwd2_ws;               /* gcnk_gcn_bwd2_workspace_bytes(M, F, P) */
   int64_t bwd2_ws_bytes;
+  gcnk_plan_ref aTH;           /* GCNK_BWD_FACTORED operands (above) */
+  const float* x_hubT;
+  int64_t ld_xhT;
+  int32_t nhub, nhub_p, Kc, k0;
+  const float* UT;
+  int64_t ldut;
+  float* y;                    /* [nhub_p x F], rows nhub .. nhub_p zero */
+  float* sm_ws;
+  int64_t sm_ws_bytes;
+  int32_t* sm_ctr;
+  int64_t sm_ctr_bytes;
 } gcnk_gcn_bwd;
 
 int gcnk_gcn_backward_f32(const gcnk_gcn_bwd* rec, const float* G, const float* H1, int64_t ldh, const float* W2,
@@ -435,7 +453,7 @@ int gcnk_gcn_backward_f32(const gcnk_gcn_bwd* rec, const float* G, const float* 
 /* Layout of the record structs for bindings that mirror them: writes up to n
  * of {sizeof plan_ref, sizeof gcn_fwd, offsetof x, U, aF, aP, ld_h1_tmp,
  * plan_ref.lanes_hint, sizeof gcn_bwd, gcn_bwd.xT, gcn_bwd.bwd2_ws_bytes,
- * gcn_fwd.x_ctr} to out and returns how many exist. */
+ * gcn_fwd.x_ctr, gcn_bwd.aTH, gcn_bwd.sm_ctr_bytes} to out and returns how many exist. */
 int32_t gcnk_gcn_fwd_layout(int64_t* out, int32_t n);
 
 /* ---------------------------------------------------------------------------

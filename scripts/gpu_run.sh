@@ -23,30 +23,30 @@ for step in "$@"; do
   case "$kind" in
     micro)
       bin="${rest%%:*}"; args="${rest#*:}"; [ "$args" = "$rest" ] && args=""
-      python3 scripts/micro/dump_r8.py /tmp/r8_adj.bin > /dev/null || exit 3
+      python3 scripts/micro/dump_r8.py /tmp/r8_adj.bin > /dev/null || exit 1
       timeout -k 10 240 "scripts/micro/$bin" /tmp/r8_adj.bin $args > "$out/$bin.log" 2>&1
-      rc=$?; tail -n 80 "$out/$bin.log"; [ $rc -eq 0 ] || { echo "rc=$rc"; exit 3; }
+      rc=$?; tail -n 80 "$out/$bin.log"; [ $rc -eq 0 ] || { echo "rc=$rc"; exit 1; }
       if [ -n "$PROF" ]; then
         timeout -k 10 240 rocprofv3 --kernel-trace --stats --output-format csv -d "$out/${bin}_prof" -o kt -- \
-          "scripts/micro/$bin" /tmp/r8_adj.bin $args > "$out/${bin}_prof.log" 2>&1 || { echo "prof rc=$?"; exit 3; }
+          "scripts/micro/$bin" /tmp/r8_adj.bin $args > "$out/${bin}_prof.log" 2>&1 || { echo "prof rc=$?"; exit 1; }
       fi ;;
     test)
       timeout -k 10 900 python -u -m pytest tests -m gpu -x -q --timeout 300 --timeout-method thread -k "$rest" \
         > "$out/pytest_$(echo "$rest" | tr -c 'A-Za-z0-9_' '_' | cut -c1-40).log" 2>&1
-      rc=$?; tail -n 25 "$out"/pytest_*.log | tail -n 25; [ $rc -eq 0 ] || { echo "rc=$rc"; exit 3; } ;;
+      rc=$?; tail -n 25 "$out"/pytest_*.log | tail -n 25; [ $rc -eq 0 ] || { echo "rc=$rc"; exit 1; } ;;
     tests)
       timeout -k 10 1000 python -u -m pytest tests -m gpu -x -q --timeout 300 --timeout-method thread \
         > "$out/pytest_gpu.log" 2>&1
-      rc=$?; tail -n 15 "$out/pytest_gpu.log"; [ $rc -eq 0 ] || { echo "rc=$rc"; exit 3; } ;;
+      rc=$?; tail -n 15 "$out/pytest_gpu.log"; [ $rc -eq 0 ] || { echo "rc=$rc"; exit 1; } ;;
     bench)
       args="${rest:---steps 200 --warmup 20}"
       timeout -k 10 900 python -u bench.py $args --rocprof-dir "$out/bench_prof" > "$out/bench.json" 2> "$out/bench.err"
-      rc=$?; tail -c 3000 "$out/bench.json"; [ $rc -eq 0 ] || { echo "rc=$rc"; tail -n 20 "$out/bench.err"; exit 3; } ;;
+      rc=$?; tail -c 3000 "$out/bench.json"; [ $rc -eq 0 ] || { echo "rc=$rc"; tail -n 20 "$out/bench.err"; exit 1; } ;;
     prof)
       s="${rest%%:*}"; args="${rest#*:}"; [ "$args" = "$rest" ] && args=""
       timeout -k 10 400 rocprofv3 --kernel-trace --stats --output-format csv -d "$out/${s%.py}_stats" -o kt -- \
         python3 "scripts/$s" $args > "$out/${s%.py}_prof.log" 2>&1
-      rc=$?; tail -n 30 "$out/${s%.py}_prof.log"; [ $rc -eq 0 ] || { echo "rc=$rc"; exit 3; }
+      rc=$?; tail -n 30 "$out/${s%.py}_prof.log"; [ $rc -eq 0 ] || { echo "rc=$rc"; exit 1; }
       python3 - "$out/${s%.py}_stats" <<'PY'
 import csv, glob, sys
 for f in glob.glob(f"{sys.argv[1]}/**/*kernel_stats.csv", recursive=True):
@@ -57,12 +57,12 @@ PY
     py)
       s="${rest%%:*}"; args="${rest#*:}"; [ "$args" = "$rest" ] && args=""
       timeout -k 10 600 python3 -u "scripts/$s" $args > "$out/${s%.py}.log" 2>&1
-      rc=$?; tail -n 60 "$out/${s%.py}.log"; [ $rc -eq 0 ] || { echo "rc=$rc"; exit 3; } ;;
+      rc=$?; tail -n 60 "$out/${s%.py}.log"; [ $rc -eq 0 ] || { echo "rc=$rc"; exit 1; } ;;
     vpy)   # vpy:<variant name>:<script>[:<args>]: the script on _variants/libgcnk_<variant>.so
       v="${rest%%:*}"; rest2="${rest#*:}"
       s="${rest2%%:*}"; args="${rest2#*:}"; [ "$args" = "$rest2" ] && args=""
       GCNK_LIB="_variants/libgcnk_$v.so" timeout -k 10 600 python3 -u "scripts/$s" $args > "$out/${s%.py}_$v.log" 2>&1
-      rc=$?; tail -n 60 "$out/${s%.py}_$v.log"; [ $rc -eq 0 ] || { echo "rc=$rc"; exit 3; } ;;
+      rc=$?; tail -n 60 "$out/${s%.py}_$v.log"; [ $rc -eq 0 ] || { echo "rc=$rc"; exit 1; } ;;
     *) echo "unknown step $step"; exit 2 ;;
   esac
 done

@@ -36,6 +36,19 @@ def _close(got, ref, rtol=1e-5, atol=1e-5):
     assert np.all(err <= bound), f"max err {err.max():.3e} (bound at worst {bound.flat[np.argmax(err - bound)]:.3e})"
 
 
+def _grads_close(got, want, name, rtol=1e-4, kink_frac=1e-3):
+    """Gradients of two fp32 associations of the same forward (e.g. (A-hat X) W1
+    against A-hat (X W1)): every element within rtol (atol 1e-5 of the largest),
+    except where an element of Z1 that sits within rounding of 0 took the other
+    side of the ReLU in one of them (its whole gZ1 entry then differs, and so do
+    the gW1 / gb1 terms it feeds): at most `kink_frac` of the elements (or 2),
+    each still within 1e-2 relative / 10x the absolute bound."""
+    atol = 1e-5 * max(1.0, float(np.abs(want).max()))
+    bad = np.abs(got - want) > atol + rtol * np.abs(want)
+    assert bad.sum() <= max(2, kink_frac * bad.size), f"{name}: {int(bad.sum())} of {bad.size} elements off"
+    np.testing.assert_allclose(got, want, rtol=1e-2, atol=10 * atol, err_msg=name)
+
+
 def _random_csr(M, K, nnz, rng, heavy_rows=(), heavy_deg=0, empty_frac=0.0):
     rows = rng.integers(0, M, nnz)
     if empty_frac > 0:
@@ -70,7 +83,7 @@ def test_spmm_r8_adjacency(r8, F):
     got_t = spmm(a, B.to(DEV), dense=0.05)
     _close(got_t, ref)
     hdr = [p for k, p in a._plans.items() if abs(k[2]) == 0.05][0].header
-    assert hdr[8] > 0 and hdr[12] == 1, "R8 document rows: MFMA tiles over the topic columns + diagonal"
+    assert hdr[8] > 0 and (hdr[12] & 1) == 1, "R8 document rows: MFMA tiles over the topic columns + diagonal"
 
 
 @pytest.mark.parametrize("F", [1, 3, 7, 8, 16, 64, 100, 200, 256, 257, 1000, 4096])
@@ -145,7 +158,7 @@ def test_spmm_hybrid_dense_blocks(F, M):
     _close(got, csr_ref.spmm_epilogue(acc, bias, relu=True, mask=mask, scale=1.5), atol=2e-5 * np.sqrt(K))
     hdr = list(a._plans.values())[0].header
     assert hdr[8] > 0 and hdr[9] > 0, "dense blocks (single and multi-chunk) expected on the tile path"
-    assert hdr[12] == (1 if M == K else 0), "diagonal entries of a square operand's tile rows are kept aside"
+    assert (hdr[12] & 1) == (1 if M == K else 0), "diagonal entries of a square operand's tile rows are kept aside"
     # tile path disabled: the row kernel alone gives the same product
     got2 = spmm(a, torch.from_numpy(B).to(DEV), dense=2.0)
     _close(got2, acc, atol=2e-5 * np.sqrt(K))
@@ -775,8 +788,7 @@ def test_gcn_20ng_shaped_forward_matches_oracle(mode, monkeypatch):
         scale = max(1.0, float(np.abs(lb).max()))
         assert np.abs(la - lb).max() <= 1e-5 * scale, (name, float(np.abs(la - lb).max()))
         for k in ga:
-            np.testing.assert_allclose(ga[k], gb[k], rtol=1e-4, atol=1e-5 * max(1.0, float(np.abs(gb[k]).max())),
-                                       err_msg=f"{name} {k}")
+            _grads_close(ga[k], gb[k], f"{name} {k}")
 
 
 @pytest.fixture(scope="module")
@@ -1142,8 +1154,7 @@ def test_factored_gc1_matches_spmm_path(r8, mode):
     scale = max(1.0, float(np.abs(lb).max()))
     assert np.abs(la - lb).max() <= 1e-5 * scale, float(np.abs(la - lb).max())
     for k in ga:
-        np.testing.assert_allclose(ga[k], gb[k], rtol=1e-4, atol=1e-5 * max(1.0, float(np.abs(gb[k]).max())),
-                                   err_msg=k)
+        _grads_close(ga[k], gb[k], k)
 
 
 @pytest.mark.parametrize("F,P,ndoc", [(52, 3, 2000), (200, 20, 2000), (36, 32, 2000), (200, 20, 12000)])
@@ -1243,8 +1254,7 @@ def test_factored_forward_hub_rows_first_ragged(mode):
     scale = max(1.0, float(np.abs(lb).max()))
     assert np.abs(la - lb).max() <= 1e-5 * scale, float(np.abs(la - lb).max())
     for k in ga:
-        np.testing.assert_allclose(ga[k], gb[k], rtol=1e-4, atol=1e-5 * max(1.0, float(np.abs(gb[k]).max())),
-                                   err_msg=k)
+        _grads_close(ga[k], gb[k], k)
 
 
 # ------------------------------------------------------------------------------ narrow-feature gc1 (A-hat X cached)
@@ -1352,8 +1362,7 @@ def test_dense_ax_forward_backward_matches_spmm_path(r8, mode, graph, monkeypatc
     scale = max(1.0, float(np.abs(lb).max()))
     assert np.abs(la - lb).max() <= 1e-5 * scale, float(np.abs(la - lb).max())
     for k in ga:
-        np.testing.assert_allclose(ga[k], gb[k], rtol=1e-4, atol=1e-5 * max(1.0, float(np.abs(gb[k]).max())),
-                                   err_msg=k)
+        _grads_close(ga[k], gb[k], k)
 
 
 # ------------------------------------------------------------------------------ whole-forward launch record

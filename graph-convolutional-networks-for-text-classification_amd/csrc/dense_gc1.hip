@@ -12,12 +12,17 @@
 // X W1 GEMM in front of it never run (the association differs from the
 // reference's A-hat (X W1) only in fp32 rounding, ~1e-6 relative).
 //
-// Persistent workgroups (one per CU, 4 waves, one per SIMD).  Wave w owns the
-// 16-column n-tiles t = w, w + 4, w + 8, ... of F; its W1 fragments (every
-// k-step x its n-tiles) and W2 fragments stay in registers for the whole
-// launch.  Per 16-row tile:
+// Persistent workgroups (two per CU in dense mode, so one wave's MFMAs overlap
+// the other's epilogue on each SIMD; one per CU in hub mode, whose S_T fills the
+// LDS).  4 waves each; wave w owns the 16-column n-tiles t = w, w + 4, w + 8, ...
+// of F; its W1 fragments (every k-step x its n-tiles) and W2 fragments stay in
+// registers for the whole launch.  Per 16-row tile:
+//   0. the A tile [16 x K] is staged in LDS by the whole workgroup with
+//      coalesced loads, one tile ahead (round 5's first version had every wave
+//      load its own fragments straight from global memory -- 16 rows x 4 B per
+//      instruction, four waves fetching the same tile -- and ran 4x slower);
 //   1. Z_w = A_tile W1[:, cols_w] on v_mfma_f32_16x16x4_f32 (exact fp32 FMA
-//      chains; the next tile's A fragments are loaded under these MFMAs);
+//      chains);
 //   2. + b1, ReLU, dropout (mask or hash: the SpMM's epilogue), H1 stored only
 //      when a backward needs it;
 //   3. H1[:, cols_w] W2[cols_w, :] on MFMA (the tile transposed to the A layout
@@ -38,6 +43,11 @@ constexpr int kThreads = 64 * kWaves;
 constexpr int kNTQ = 4;          // n-tiles per wave: F <= 16 * 4 * kNTQ = 256
 constexpr int kHP = 64 + 4;      // wave-private H1 tile row stride (floats): 16 x (64 + 4)
 constexpr int kMaxP = 32;
+// experiment knob (variant builds only): 1 no W1 MFMAs, 2 no projection MFMAs,
+// 3 no A loads, 4 no S2 reduction / stores
+#ifndef GCNK_DG_EXP
+#define GCNK_DG_EXP 0
+#endif
 
 // hub mode (the factored gc1, csrc/factor.hip's record layout): U's rows are
 // positions of the block order; per 32-position block a record of rec_words
@@ -63,9 +73,16 @@ struct DenseArgs {
 // KS k-steps of 4 (K <= 4 KS; lane quadrant q of step s multiplies k = 4 s + q),
 // NP 16-column tiles of P; HUB: the factored gc1 (S_T staged in LDS once, the
 // tile's block record staged per tile, one tile ahead)
+// A-tile row stride: >= 4 KS and = 4 (mod 64), so lane (row c, quadrant q)
+// reading k = 4 s + q hits bank 4 c + q: conflict-free
+constexpr int a_stride(int ks) { return 64 * ((4 * ks - 4 + 63) / 64) + 4; }
+
 template <int KS, int NP, bool HUB>
-__global__ void __launch_bounds__(kThreads)
+__global__ void __launch_bounds__(kThreads, HUB ? 1 : 2)
 dense_gc1_kernel(DenseArgs a) {
+  constexpr int KP = a_stride(KS);
+  constexpr int kAPer = (16 * 4 * KS + kThreads - 1) / kThreads;   // A-tile elements per thread
+  __shared__ __attribute__((aligned(16))) float s_A[2][16 * KP];
   __shared__ __attribute__((aligned(16))) float s_h[kWaves][16 * kHP];
   __shared__ __attribute__((aligned(16))) float s_red[2][kWaves][NP][64 * 4];
   extern __shared__ __attribute__((aligned(16))) float s_dyn[];   // HUB: s_S [nhub x F] | s_rec [2][rec_words]
@@ -137,61 +154,93 @@ dense_gc1_kernel(DenseArgs a) {
       *reinterpret_cast<float4*>(s_S + hrow * F + 4 * c4) =
           *reinterpret_cast<const float4*>(a.S + (int64_t)hrow * a.lds + 4 * c4);
     }
-    int32_t rv[kRecPer];
-    load_rec(blockIdx.x, rv);
-    put_rec(0, rv);
+  }
+  // the A tile [16 x 4 KS] (zero past K and M): thread element e -> row e / (4 KS),
+  // k e % (4 KS) -- consecutive threads, consecutive k: coalesced
+  auto load_a = [&](int tile, float (&av)[kAPer]) {
+#pragma unroll
+    for (int i = 0; i < kAPer; ++i) {
+      const int e = tid + kThreads * i, r = e / (4 * KS), k = e % (4 * KS);
+      const int64_t row = (int64_t)tile * 16 + r;
+      av[i] = (GCNK_DG_EXP != 3 && e < 16 * 4 * KS && tile < a.ntiles && row < a.M && k < K) ? a.A[row * a.lda + k] : 0.f;
+    }
+  };
+  auto put_a = [&](int buf, const float (&av)[kAPer]) {
+#pragma unroll
+    for (int i = 0; i < kAPer; ++i) {
+      const int e = tid + kThreads * i;
+      if (e < 16 * 4 * KS) s_A[buf][(e / (4 * KS)) * KP + e % (4 * KS)] = av[i];
+    }
+  };
+  {
+    float av[kAPer];
+    load_a(blockIdx.x, av);
+    put_a(0, av);
+    if constexpr (HUB) {
+      int32_t rv[kRecPer];
+      load_rec(blockIdx.x, rv);
+      put_rec(0, rv);
+    }
     __syncthreads();
   }
 
-  // A fragments of a tile: lane (row c, quadrant q) holds A[row][4 s + q]
-  auto load_a = [&](int tile, float (&af)[KS]) {
-    const int64_t row = (int64_t)tile * 16 + c;
-    const bool rok = tile < a.ntiles && row < a.M;
-    const float* ap = a.A + (rok ? row : 0) * a.lda + q;
-#pragma unroll
-    for (int s = 0; s < KS; ++s) af[s] = (rok && 4 * s + q < K) ? ap[4 * s] : 0.f;
-  };
-  // one 16-row tile: its MFMAs, epilogue and projection with `af`; the next
-  // tile's A fragments are loaded into `an` under the MFMAs (two named buffers,
-  // the tile loop unrolled by two: no runtime index into a register array)
-  auto tile_step = [&](int tile, int buf, float (&af)[KS], float (&an)[KS]) {
-    load_a(tile + gridDim.x, an);
+  // one 16-row tile from LDS buffer `buf`; the next tile's A (and record) are
+  // loaded under its MFMAs and written to buffer buf ^ 1 before the barrier
+  auto tile_step = [&](int tile, int buf) {
+    float av[kAPer];
+    load_a(tile + gridDim.x, av);
     int32_t rv[kRecPer];
     load_rec(tile + gridDim.x, rv);
-    // ---- 1. Z = A W1[:, cols_w]
+    // ---- 1. Z = A W1[:, cols_w]; lane (row c, quadrant q) reads A[c][4 s + q]
+    const float* sa = &s_A[buf][c * KP + q];
     f32x4 acc[kNTQ];
 #pragma unroll
     for (int t = 0; t < kNTQ; ++t) acc[t] = f32x4{0.f, 0.f, 0.f, 0.f};
 #pragma unroll
-    for (int s = 0; s < KS; ++s)
+    for (int s = 0; s < (GCNK_DG_EXP == 1 ? 0 : KS); ++s) {
+      const float af = sa[4 * s];
 #pragma unroll
       for (int t = 0; t < kNTQ; ++t)
-        if (t < ntw) acc[t] = __builtin_amdgcn_mfma_f32_16x16x4f32(af[s], wf[s][t], acc[t], 0, 0, 0);
+        if (t < ntw) acc[t] = __builtin_amdgcn_mfma_f32_16x16x4f32(af, wf[s][t], acc[t], 0, 0, 0);
+    }
     // ---- 2. epilogue (C/D map: reg r -> row 4 q + r, column c), H1 store,
     //      tile into wave-private LDS
     const int64_t row0 = (int64_t)tile * 16;
     const bool plain = a.epi.code == GCNK_EPI_BIAS_RELU;
     int64_t orow[4];   // output rows of this lane's 4 tile rows
+    if constexpr (HUB) {
+      const int32_t* rb = s_rec + buf * rw;
+      const int2* it = reinterpret_cast<const int2*>(rb + kRecHead);
+      int beg[4], len[4], most = 0;
 #pragma unroll
-    for (int r = 0; r < 4; ++r) {
-      if constexpr (HUB) {
+      for (int r = 0; r < 4; ++r) {
         const int pb = 16 * (tile & 1) + 4 * q + r;   // position within the 32-row block
-        const int32_t* rb = s_rec + buf * rw;
         const int32_t id = rb[kRecRow + pb];
         orow[r] = id >= 0 ? id : a.M;                 // -1 (past M): never stored
-        // + A_H S_T: the row's hub items in CSR order
-        const int2* it = reinterpret_cast<const int2*>(rb + kRecHead);
-        for (int k = rb[pb]; k < rb[pb + 1]; ++k) {
-          const int2 p2 = it[k];
-          const float v = __int_as_float(p2.y);
-          const float* srow = s_S + p2.x * F + 16 * w + c;
-#pragma unroll
-          for (int t = 0; t < kNTQ; ++t)   // (columns past F: no read past the hub's row)
-            if (t < ntw && 16 * (w + kWaves * t) + c < F) acc[t][r] = fmaf(v, srow[16 * kWaves * t], acc[t][r]);
-        }
-      } else {
-        orow[r] = row0 + 4 * q + r;
+        beg[r] = rb[pb];
+        len[r] = rb[pb + 1] - rb[pb];
+        most = max(most, len[r]);
       }
+      // + A_H S_T: each row's hub items in CSR order, the lane's four rows
+      // advanced together (four independent FMA chains per LDS round trip)
+      for (int j = 0; j < most; ++j) {
+        float v[4];
+        const float* srow[4];
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          const int2 p2 = j < len[r] ? it[beg[r] + j] : int2{0, 0};   // (pad: + 0 x S_T[0])
+          v[r] = __int_as_float(p2.y);
+          srow[r] = s_S + p2.x * F + 16 * w + c;
+        }
+#pragma unroll
+        for (int t = 0; t < kNTQ; ++t)   // (columns past F: no read past the hub's row)
+          if (t < ntw && 16 * (w + kWaves * t) + c < F)
+#pragma unroll
+            for (int r = 0; r < 4; ++r) acc[t][r] = fmaf(v[r], srow[r][16 * kWaves * t], acc[t][r]);
+      }
+    } else {
+#pragma unroll
+      for (int r = 0; r < 4; ++r) orow[r] = row0 + 4 * q + r;
     }
 #pragma unroll
     for (int t = 0; t < kNTQ; ++t) {
@@ -225,15 +274,18 @@ dense_gc1_kernel(DenseArgs a) {
 #pragma unroll
       for (int j = 0; j < 4; ++j)
 #pragma unroll
-        for (int p = 0; p < NP; ++p) pacc[p] = __builtin_amdgcn_mfma_f32_16x16x4f32(ha[j], w2f[t][j][p], pacc[p], 0, 0, 0);
+        for (int p = 0; p < NP; ++p)
+          if (GCNK_DG_EXP == 2) pacc[p][j] += ha[j] * w2f[t][j][p];
+          else pacc[p] = __builtin_amdgcn_mfma_f32_16x16x4f32(ha[j], w2f[t][j][p], pacc[p], 0, 0, 0);
     }
 #pragma unroll
     for (int p = 0; p < NP; ++p) *reinterpret_cast<f32x4*>(&s_red[buf][w][p][4 * lane]) = pacc[p];
-    put_rec(buf ^ 1, rv);   // the next tile's record (its readers passed the previous barrier)
+    put_a(buf ^ 1, av);     // the next tile's A and record (their readers passed the previous barrier)
+    put_rec(buf ^ 1, rv);
     // (double-buffered by tile parity: wave 0 reads buffer `buf` before it
     // reaches the next barrier, and buffer `buf` is written again only after it)
     __syncthreads();
-    if (w == 0) {
+    if (w == 0 && GCNK_DG_EXP != 4) {
 #pragma unroll
       for (int p = 0; p < NP; ++p) {
         f32x4 sum = *reinterpret_cast<const f32x4*>(&s_red[buf][0][p][4 * lane]);
@@ -251,13 +303,8 @@ dense_gc1_kernel(DenseArgs a) {
     // order within the wave): no barrier needed
     __builtin_amdgcn_wave_barrier();
   };
-  float a0[KS], a1[KS];
-  load_a(blockIdx.x, a0);
-  for (int tile = blockIdx.x; tile < a.ntiles; tile += 2 * gridDim.x) {
-    tile_step(tile, 0, a0, a1);
-    if (tile + (int)gridDim.x >= a.ntiles) break;
-    tile_step(tile + gridDim.x, 1, a1, a0);
-  }
+  int buf = 0;
+  for (int tile = blockIdx.x; tile < a.ntiles; tile += gridDim.x, buf ^= 1) tile_step(tile, buf);
 }
 
 template <int KS, bool HUB>
@@ -289,8 +336,9 @@ int cu_count() {
 
 template <bool HUB>
 int launch(const DenseArgs& a, hipStream_t s) {
-  // persistent: one workgroup per CU (4 waves, one per SIMD, up to 512 registers each)
-  const unsigned grid = (unsigned)std::min<int64_t>(a.ntiles, cu_count());
+  // persistent: 4 waves per workgroup, two workgroups per CU in dense mode (<= 256
+  // registers a wave), one in hub mode (S_T fills the LDS)
+  const unsigned grid = (unsigned)std::min<int64_t>(a.ntiles, (HUB ? 1 : 2) * cu_count());
   const int np = a.P <= 16 ? 1 : 2;
   const size_t dyn = HUB ? (size_t)4 * ((size_t)a.nhub * a.F + 2 * (size_t)a.rec_words) : 0;
   const int ks = (a.K + 3) / 4;
@@ -329,7 +377,7 @@ int hubfactor_persistent(int32_t M, int32_t F, int32_t Kc, int32_t nhub, int32_t
                          float scale, float keep, uint64_t seed, uint64_t offset, const uint64_t* rng_base,
                          const float* W2, int64_t ldw2, float* H, int64_t ldh, float* C2, int64_t ldc2, void* stream) {
   const size_t lds_bytes = (size_t)4 * ((size_t)nhub * F + 2 * (size_t)rec_words) + sizeof(float) * (size_t)kWaves * 16 * kHP +
-                           sizeof(float) * 2 * kWaves * 2 * 64 * 4;
+                           sizeof(float) * 2 * kWaves * 2 * 64 * 4 + sizeof(float) * 2 * 16 * a_stride(32);
   if (Kc > 128 || F > 16 * kWaves * kNTQ || F % 4 || lds % 4 || ((uintptr_t)S & 15) || P > kMaxP ||
       rec_words > kThreads * 4 || lds_bytes > 160 * 1024)
     return GCNK_EUNSUP;

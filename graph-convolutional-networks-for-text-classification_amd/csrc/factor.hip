@@ -30,6 +30,8 @@
 // No atomics, no hand-off between workgroups: bitwise reproducible.
 #include "gcnk_common.h"
 
+#include <cstring>
+
 #include <algorithm>
 #include <cstdlib>
 
@@ -347,14 +349,12 @@ extern "C" int gcnk_hubfactor_gc1_f32(int32_t M, int32_t F, int32_t Kc, int32_t 
               (long long)lds_b, F, Kc, nhub);
     return GCNK_EUNSUP;
   }
-  // round 5: the persistent kernel (csrc/dense_gc1.hip: W1[Kc] fragments held in
-  // registers for the whole launch, S_T staged once per CU instead of once per
-  // 32-row block); GCNK_HUBFACTOR_LEGACY=1 keeps this file's per-block kernel
-  static const bool legacy = [] {
-    const char* v = getenv("GCNK_HUBFACTOR_LEGACY");
-    return v && v[0] == '1';
-  }();
-  if (!legacy) {
+  // round 5: GCNK_HUBFACTOR=persistent takes the persistent kernel
+  // (csrc/dense_gc1.hip: W1[Kc] fragments held in registers for the whole
+  // launch, S_T staged once per CU instead of once per 32-row block); read per
+  // call (a hipGraph keeps the choice made at capture)
+  const char* hv = getenv("GCNK_HUBFACTOR");
+  if (hv && strcmp(hv, "persistent") == 0) {
     const int rc = hubfactor_persistent(M, F, Kc, nhub, P, U, ldu, W, ldw, k0, S, lds, rec, rec_words, bias, epilogue,
                                         drop_mask, ldm, drop_scale, keep_prob, seed, offset, rng_base, W2, ldw2, H,
                                         ldh, C2, ldc2, stream);

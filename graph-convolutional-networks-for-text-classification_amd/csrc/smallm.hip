@@ -37,6 +37,10 @@ __device__ __forceinline__ const float* uniform_ptr(const float* p) {
   return reinterpret_cast<const float*>(((uint64_t)hi << 32) | lo);
 }
 constexpr int kSc1 = 16;   // cache-policy aux bit sc1 (write-through / coherent past the XCD L2)
+// experiment knob (variant builds only): 1 no hand-off, 2 no A loads, 3 no B loads, 4 no MFMA
+#ifndef GCNK_SMALLM_EXP
+#define GCNK_SMALLM_EXP 0
+#endif
 
 // KCH 16-deep chunks per K range (kSplitDepth = 16 KCH)
 template <int KCH>
@@ -63,7 +67,7 @@ gemm_smallm_onepass_kernel(int32_t M, int32_t N, int32_t K, int32_t nsplit, cons
   for (int p = 0; p < PB; ++p) {
     const int e = tid + 256 * p;             // piece e: k = e / 4, columns 4 (e % 4) ..
     const int64_t k = k0 + e / 4, n = n0 + 4 * (e % 4);
-    const bool ok = e < KR * 4 && k < K && n + 3 < N;
+    const bool ok = e < KR * 4 && k < K && n + 3 < N && GCNK_SMALLM_EXP != 3;
     bv[p] = ok ? *reinterpret_cast<const float4*>(B + k * ldb + n) : make_float4(0.f, 0.f, 0.f, 0.f);
     if (e < KR * 4 && k < K && !ok && n < N) {   // a partial float4 at the right edge
       float tmp[4] = {0.f, 0.f, 0.f, 0.f};
@@ -77,7 +81,7 @@ gemm_smallm_onepass_kernel(int32_t M, int32_t N, int32_t K, int32_t nsplit, cons
 #pragma unroll
   for (int ch = 0; ch < KCH; ++ch) {
     const int64_t k = k0 + 16 * ch + 4 * q;
-    const bool ok = rok && k < K;   // lda % 4 == 0 and lda >= K rounded up to 4: the float4 lies in the row
+    const bool ok = rok && k < K && GCNK_SMALLM_EXP != 2;   // lda % 4 == 0 and lda >= K rounded up to 4: the float4 lies in the row
     a[ch] = ok ? *reinterpret_cast<const float4*>(A + row * lda + k) : make_float4(0.f, 0.f, 0.f, 0.f);
     if (ok && k + 3 >= K) {          // zero the pad columns past K
       if (k + 1 >= K) a[ch].y = 0.f;
@@ -103,7 +107,7 @@ gemm_smallm_onepass_kernel(int32_t M, int32_t N, int32_t K, int32_t nsplit, cons
   f32x4 acc0 = f32x4{0.f, 0.f, 0.f, 0.f}, acc1 = acc0;
   const float* bcol = s_Bt + c * LS + 4 * q;
 #pragma unroll
-  for (int ch = 0; ch < KCH; ++ch) {
+  for (int ch = 0; ch < (GCNK_SMALLM_EXP == 4 ? 0 : KCH); ++ch) {
     const float4 b4 = *reinterpret_cast<const float4*>(bcol + 16 * ch);
     f32x4& acc = (ch & 1) ? acc1 : acc0;
     acc = __builtin_amdgcn_mfma_f32_16x16x4f32(a[ch].x, b4.x, acc, 0, 0, 0);
@@ -111,7 +115,14 @@ gemm_smallm_onepass_kernel(int32_t M, int32_t N, int32_t K, int32_t nsplit, cons
     acc = __builtin_amdgcn_mfma_f32_16x16x4f32(a[ch].z, b4.z, acc, 0, 0, 0);
     acc = __builtin_amdgcn_mfma_f32_16x16x4f32(a[ch].w, b4.w, acc, 0, 0, 0);
   }
-  const f32x4 pv = acc0 + acc1;
+  f32x4 pv = acc0 + acc1;
+  if (GCNK_SMALLM_EXP == 4) pv += f32x4{a[KCH - 1].x, a[0].y, bcol[0], bcol[KR - 1]};
+  if (GCNK_SMALLM_EXP == 1) {
+    float* pt1 = part + ((int64_t)t * nsplit + s) * (kRows * kCT);
+#pragma unroll
+    for (int r = 0; r < 4; ++r) pt1[(16 * w + 4 * q + r) * kCT + c] = pv[r];
+    return;
+  }
   // ---- publish this K range's partial [64 x 16] (C/D map: reg r -> row 4 q + r,
   //      column c), sc1 stores; every wave drained before the arrival
   float* pt = part + ((int64_t)t * nsplit + s) * (kRows * kCT);
@@ -130,41 +141,38 @@ gemm_smallm_onepass_kernel(int32_t M, int32_t N, int32_t K, int32_t nsplit, cons
   }
   __syncthreads();
   if (!s_last) return;
-  // ---- the last arriver: the tile's partials in split order (sc1 loads), C
+  // ---- the last arriver: the tile's partials in split order (sc1 loads), C.
+  //      Thread (row tid / 4, columns 4 (tid % 4) ..): one 16-B load per split,
+  //      ALL of them in flight at once (one memory latency, not one per batch:
+  //      batches of 8 took ~1 us each past the L2s)
   const float* base = uniform_ptr(part + (int64_t)t * nsplit * (kRows * kCT));
-  float sum[4] = {0.f, 0.f, 0.f, 0.f};
-  constexpr int U = 8;
-  for (int s0 = 0; s0 < nsplit; s0 += U) {
-    float v[U][4];
+  const int rr = tid >> 2, c4 = 4 * (tid & 3);
+  constexpr int kMaxSplit = 32;   // (pick_kch keeps nsplit <= 32 for K <= 16384)
+  f32v4 v[kMaxSplit];
 #pragma unroll
-    for (int j = 0; j < U; ++j)
+  for (int j = 0; j < kMaxSplit; ++j)
+    if (j < nsplit) v[j] = __builtin_amdgcn_raw_buffer_load_b128(rsrc(base), (int)(((j * kRows + rr) * kCT + c4) * 4), 0, kSc1);
+  f32v4 sum = {0.f, 0.f, 0.f, 0.f};
 #pragma unroll
-      for (int r = 0; r < 4; ++r)
-        v[j][r] = s0 + j < nsplit
-                      ? __uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(
-                            rsrc(base), (int)((((s0 + j) * kRows + 16 * w + 4 * q + r) * kCT + c) * 4), 0, kSc1))
-                      : 0.f;
+  for (int j = 0; j < kMaxSplit; ++j)
+    if (j < nsplit) sum += v[j];
+  if (rr < M) {
 #pragma unroll
-    for (int j = 0; j < U; ++j)
-      if (s0 + j < nsplit)
-#pragma unroll
-        for (int r = 0; r < 4; ++r) sum[r] += v[j][r];
-  }
-  const int64_t n = n0 + c;
-#pragma unroll
-  for (int r = 0; r < 4; ++r) {
-    const int64_t m = 16 * w + 4 * q + r;
-    if (m < M && n < N) C[m * ldc + n] = accumulate ? C[m * ldc + n] + sum[r] : sum[r];
+    for (int i = 0; i < 4; ++i) {
+      const int64_t n = n0 + c4 + i;
+      if (n < N) C[rr * ldc + n] = accumulate ? C[rr * ldc + n] + sum[i] : sum[i];
+    }
   }
   if (tid == 0) __hip_atomic_store(ctr + t, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);   // re-armed
 }
 
 // K range depth (16 KCH) for a K: ~20 ranges for R8's 7463 (the last arriver
-// then reads 20 x 4 KB), never below 64
+// then reads 20 x 4 KB), never below 64, never more than 32 ranges
 int pick_kch(int32_t K) {
   const int want = (K + 20 * 16 - 1) / (20 * 16);
   return want <= 4 ? 4 : want <= 8 ? 8 : want <= 16 ? 16 : want <= 24 ? 24 : 32;
 }
+int64_t nsplit_for(int32_t K) { return (K + 16 * pick_kch(K) - 1) / (16 * pick_kch(K)); }
 
 }  // namespace
 }  // namespace gcnk
@@ -190,7 +198,7 @@ extern "C" int gcnk_gemm_smallm_f32(int32_t M, int32_t N, int32_t K, const float
     set_error("gcnk_gemm_smallm_f32: bad sizes or null operand (M=%d N=%d K=%d)", M, N, K);
     return GCNK_EARG;
   }
-  if (M > kRows || lda % 4 || !aligned16(A) || ldb % 4 || !aligned16(B)) {
+  if (M > kRows || lda % 4 || !aligned16(A) || ldb % 4 || !aligned16(B) || nsplit_for(K) > 32) {
     set_error("gcnk_gemm_smallm_f32: unsupported (M=%d <= 64, lda %% 4, ldb %% 4, 16-B aligned A and B)", M);
     return GCNK_EUNSUP;
   }

@@ -116,14 +116,15 @@ constexpr int kRowU = GCNK_ROW_U;            // gathers in flight per lane for l
 // Lane groups of 8-32 lanes (256-thread workgroups): a heavy segment spans the
 // whole 4-wavefront workgroup (4x the nonzeros per segment, 4x fewer partials)
 // instead of one wavefront.  R8 A-hat at F = 64: 7.30 -> 6.69 us, F = 32 even.
-// Not for 1-4 lanes (one-wave workgroups spread the light rows over the chip;
-// 256-thread ones measured 5.64 -> 6.14 us at F = 8).
+// Round 1-4 kept 1-4 lanes on one-wave workgroups (256-thread ones measured
+// 5.64 -> 6.14 us at F = 8); with round 5's padded heavy items the 256-thread
+// ones win from 2 lanes on (kNarrowMin below: F = 8 5.41 -> 4.73 us).
 constexpr bool kNarrowWG = GCNK_NARROW_WG != 0;
 // smallest group width (lanes) that takes 256-thread workgroups with
 // workgroup-wide heavy segments (experiment knob; narrower groups run one-wave
 // workgroups)
 #ifndef GCNK_NARROW_MIN_LPR
-#define GCNK_NARROW_MIN_LPR 8
+#define GCNK_NARROW_MIN_LPR 2
 #endif
 constexpr int kNarrowMin = GCNK_NARROW_MIN_LPR;
 // Heavy segments of whole-wavefront plans keep a padded copy of their items
@@ -1775,7 +1776,12 @@ extern "C" int32_t gcnk_spmm_default_ipc(int32_t M, int64_t nnz, int32_t F, int3
   // (profiles/r01_variants.log): R8 (69k nnz) ipc 12 8.67 us, 16 8.95, 20 9.24,
   // 24 9.72; 20ng-shaped (175k) 12 17.9, 16 17.0, 20 16.4, 24 16.2, 32 16.4;
   // 1M/20M F = 256: 16 and 32 both 3.37 ms.
-  if (choose_lpr(F, lanes_hint) != 64) return 8;
+  // 2-lane groups with workgroup-wide heavy segments (LPR >= kNarrowMin): 16
+  // (round 5, after the padded heavy items: R8 F = 8 4.73 us vs 5.41 with
+  // one-wave workgroups at ipc 8, profiles/r05_hub_probe_nw2.log).
+  const int lpr = choose_lpr(F, lanes_hint);
+  // (F = 16, 4 lanes: 8 stays best, 5.52 vs 6.13 us, profiles/r05_hub_probe_nw.log)
+  if (lpr != 64) return kNarrowWG && lpr >= kNarrowMin && lpr == 2 ? 16 : 8;
   int64_t ipc = (nnz / 5760 + 2) / 4 * 4;
   return (int32_t)std::min<int64_t>(32, std::max<int64_t>(12, ipc));
 }

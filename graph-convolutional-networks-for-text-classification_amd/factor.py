@@ -37,10 +37,10 @@ MAX_HUBS = 128    # hub rows staged in LDS (S_T [hubs x F]; the kernel checks th
 # tiled GEMM took 13.7).  A one-launch split-K kernel with two levels of
 # last-arriver slab sums measured 12.1 us (round 4, DESIGN §5: each coherent
 # hand-off is a ~2 us memory round trip) and was removed.
-# "onepass" (default, round 5): a dense copy of the hub rows through the
+# "onepass" (round 5): a dense copy of the hub rows through the
 # one-launch small-M GEMM (csrc/smallm.hip: ~20 K ranges x 16-column tiles,
 # each tile's partials summed by its last workgroup) -- no slab-reduce launch.
-XHUB = os.environ.get("GCNK_FACTOR_XHUB", "onepass")
+XHUB = os.environ.get("GCNK_FACTOR_XHUB", "spmm")
 MAX_KC = 128      # X's light-row column range (U's width)
 ROWS_PER_BLOCK = 32   # csrc/factor.hip kRB
 # record words before the items: 33 row offsets | 3 pad | 32 row ids (-1 past

@@ -11,13 +11,17 @@
 #   prof:<script>[:<args>]    rocprofv3 --kernel-trace --stats over python scripts/<script> -> <script>_stats/
 #   py:<script>[:<args>]      python scripts/<script> <args> -> <script>.log
 #   vpy:<variant>:<script>[:<args>]  the same on _variants/libgcnk_<variant>.so
+#   env:<NAME>=<value>        export for the following steps (env:<NAME>= unsets)
+# prof/py/vpy outputs carry the step number (several runs of one script per call)
 # Steps' outputs are summarised in profiles/ by hand (profiles/INDEX.md).
 cd "${GRAFT_REPO_ROOT:-/root/repo}" || exit 2
 export TMPDIR=/tmp
 tag="$1"; shift
 out="gpurun_out/$tag"
 mkdir -p "$out"
+n=0
 for step in "$@"; do
+  n=$((n + 1))
   kind="${step%%:*}"; rest="${step#*:}"; [ "$rest" = "$step" ] && rest=""
   echo "=== $step" | tee -a "$out/steps.log"
   case "$kind" in
@@ -44,10 +48,10 @@ for step in "$@"; do
       rc=$?; tail -c 3000 "$out/bench.json"; [ $rc -eq 0 ] || { echo "rc=$rc"; tail -n 20 "$out/bench.err"; exit 1; } ;;
     prof)
       s="${rest%%:*}"; args="${rest#*:}"; [ "$args" = "$rest" ] && args=""
-      timeout -k 10 400 rocprofv3 --kernel-trace --stats --output-format csv -d "$out/${s%.py}_stats" -o kt -- \
-        python3 "scripts/$s" $args > "$out/${s%.py}_prof.log" 2>&1
-      rc=$?; tail -n 30 "$out/${s%.py}_prof.log"; [ $rc -eq 0 ] || { echo "rc=$rc"; exit 1; }
-      python3 - "$out/${s%.py}_stats" <<'PY'
+      timeout -k 10 400 rocprofv3 --kernel-trace --stats --output-format csv -d "$out/${s%.py}_stats$n" -o kt -- \
+        python3 "scripts/$s" $args > "$out/${s%.py}_prof$n.log" 2>&1
+      rc=$?; tail -n 30 "$out/${s%.py}_prof$n.log"; [ $rc -eq 0 ] || { echo "rc=$rc"; exit 1; }
+      python3 - "$out/${s%.py}_stats$n" <<'PY'
 import csv, glob, sys
 for f in glob.glob(f"{sys.argv[1]}/**/*kernel_stats.csv", recursive=True):
     for r in csv.DictReader(open(f)):
@@ -56,13 +60,16 @@ PY
       ;;
     py)
       s="${rest%%:*}"; args="${rest#*:}"; [ "$args" = "$rest" ] && args=""
-      timeout -k 10 600 python3 -u "scripts/$s" $args > "$out/${s%.py}.log" 2>&1
-      rc=$?; tail -n 60 "$out/${s%.py}.log"; [ $rc -eq 0 ] || { echo "rc=$rc"; exit 1; } ;;
+      timeout -k 10 600 python3 -u "scripts/$s" $args > "$out/${s%.py}$n.log" 2>&1
+      rc=$?; tail -n 60 "$out/${s%.py}$n.log"; [ $rc -eq 0 ] || { echo "rc=$rc"; exit 1; } ;;
     vpy)   # vpy:<variant name>:<script>[:<args>]: the script on _variants/libgcnk_<variant>.so
       v="${rest%%:*}"; rest2="${rest#*:}"
       s="${rest2%%:*}"; args="${rest2#*:}"; [ "$args" = "$rest2" ] && args=""
-      GCNK_LIB="_variants/libgcnk_$v.so" timeout -k 10 600 python3 -u "scripts/$s" $args > "$out/${s%.py}_$v.log" 2>&1
-      rc=$?; tail -n 60 "$out/${s%.py}_$v.log"; [ $rc -eq 0 ] || { echo "rc=$rc"; exit 1; } ;;
+      GCNK_LIB="_variants/libgcnk_$v.so" timeout -k 10 600 python3 -u "scripts/$s" $args > "$out/${s%.py}_$v$n.log" 2>&1
+      rc=$?; tail -n 60 "$out/${s%.py}_$v$n.log"; [ $rc -eq 0 ] || { echo "rc=$rc"; exit 1; } ;;
+    env)
+      name="${rest%%=*}"; val="${rest#*=}"
+      if [ -n "$val" ]; then export "$name=$val"; else unset "$name"; fi ;;
     *) echo "unknown step $step"; exit 2 ;;
   esac
 done

@@ -94,11 +94,13 @@ def test_plan_and_workspace_sizes():
     assert lib.gcnk_spmm_workspace_bytes(h, 198) == 8192 + 3 * 64 * 208 * 4
     assert lib.gcnk_gemm_workspace_bytes(200, 8, 7724, 4) == 4 * 200 * 8 * 4
     assert lib.gcnk_colsum_workspace_bytes(7724, 200) == ((7724 + 63) // 64) * 200 * 4
-    # heavy-segment size follows the operand at 64 lanes (R8 12, 20ng-shaped 32), 8 for narrow groups
+    # heavy-segment size follows the operand at 64 lanes (R8 12, 20ng-shaped 32); narrow groups:
+    # 16 with workgroup-wide heavy segments (2+ lanes, round 5), 8 for 1-lane groups
     assert lib.gcnk_spmm_default_ipc(7724, 69130, 200, 0) == 12
     assert lib.gcnk_spmm_default_ipc(18916, 174674, 200, 0) == 32
     assert lib.gcnk_spmm_default_ipc(1000000, 19999805, 256, 0) == 32
-    assert lib.gcnk_spmm_default_ipc(7724, 69130, 8, 0) == 8
+    assert lib.gcnk_spmm_default_ipc(7724, 69130, 8, 0) == 16
+    assert lib.gcnk_spmm_default_ipc(7724, 69130, 4, 0) == 8
 
 
 def test_product_path_refuses_cpu_tensors(r8):

@@ -1157,8 +1157,9 @@ def test_factored_gc1_matches_spmm_path(r8, mode):
         _grads_close(ga[k], gb[k], k)
 
 
+@pytest.mark.parametrize("kernel", ["legacy", "persistent"])
 @pytest.mark.parametrize("F,P,ndoc", [(52, 3, 2000), (200, 20, 2000), (36, 32, 2000), (200, 20, 12000)])
-def test_factored_gc1_kernel_against_float64(F, P, ndoc):
+def test_factored_gc1_kernel_against_float64(F, P, ndoc, kernel, monkeypatch):
     """gcnk_hubfactor_gc1_f32 alone on a synthetic doc-topic graph with hub x
     hub nonzeros, F not a multiple of 16 (and F < 64, where the n-tiles past F
     read the zero pad after W1[Kc]), P of one and two MFMA n-tiles, H1 stored:
@@ -1166,10 +1167,13 @@ def test_factored_gc1_kernel_against_float64(F, P, ndoc):
     ones), rows written through the block order's row ids (hub rows spread over
     the blocks, factor.py).  Every launch follows one that filled all LDS with
     NaN bits (gcnk_debug_poison_lds): a read of LDS the kernel did not write
-    would surface as NaN."""
+    would surface as NaN.  Both kernels: csrc/factor.hip's per-block one and
+    the persistent one of csrc/dense_gc1.hip (GCNK_HUBFACTOR=persistent, read
+    per launch)."""
     import ctypes
     import scipy.sparse as ssp
     from graph_convolutional_networks_for_text_classification_amd import factor, ops
+    monkeypatch.setenv("GCNK_HUBFACTOR", kernel)
     from graph_convolutional_networks_for_text_classification_amd.sparse import as_csr
     g = datasets.doc_topic_graph(ndoc, 40, 5, seed=4, tt_prob=0.3)
     A, X = g["adj"].to(DEV), g["features"].to(DEV)

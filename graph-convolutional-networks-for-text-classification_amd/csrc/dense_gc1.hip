@@ -14,9 +14,13 @@
 //
 // Persistent workgroups (two per CU in dense mode, so one wave's MFMAs overlap
 // the other's epilogue on each SIMD; one per CU in hub mode, whose S_T fills the
-// LDS).  4 waves each; wave w owns the 16-column n-tiles t = w, w + 4, w + 8, ...
-// of F; its W1 fragments (every k-step x its n-tiles) and W2 fragments stay in
-// registers for the whole launch.  Per 16-row tile:
+// LDS).  4 waves each; wave w owns the 64 columns 64 w .. 64 w + 63 of F as four
+// MFMA n-tiles INTERLEAVED by lane: n-tile t, lane column c is physical column
+// 64 w + 4 c + t, so a lane's four n-tiles are four consecutive columns and every
+// W1 row piece, b1, S_T row piece and H1 piece it touches is one 16-B access
+// (the n-tile-major mapping took 100 4-B W1 loads a wave, 4 rows x 64 B each --
+// with 512 workgroups re-reading W1 that was half of the launch).  The W1 and W2
+// fragments stay in registers for the whole launch.  Per 16-row tile:
 //   0. the A tile [16 x K] is staged in LDS by the whole workgroup with
 //      coalesced loads, one tile ahead (round 5's first version had every wave
 //      load its own fragments straight from global memory -- 16 rows x 4 B per
@@ -44,7 +48,8 @@ constexpr int kNTQ = 4;          // n-tiles per wave: F <= 16 * 4 * kNTQ = 256
 constexpr int kHP = 64 + 4;      // wave-private H1 tile row stride (floats): 16 x (64 + 4)
 constexpr int kMaxP = 32;
 // experiment knob (variant builds only): 1 no W1 MFMAs, 2 no projection MFMAs,
-// 3 no A loads, 4 no S2 reduction / stores
+// 3 no A loads, 4 no S2 reduction / stores, 5 no W1 / W2 fragment loads,
+// 6 W1 fragments loaded in a per-workgroup rotated row order (wrong values: timing only)
 #ifndef GCNK_DG_EXP
 #define GCNK_DG_EXP 0
 #endif
@@ -90,21 +95,25 @@ dense_gc1_kernel(DenseArgs a) {
   const int w = __builtin_amdgcn_readfirstlane(tid >> 6);
   const int c = lane & 15, q = lane >> 4;
   const int F = a.F, K = a.K, P = a.P;
-  const int NT = (F + 15) / 16;
-  const int ntw = NT > w ? (NT - w + kWaves - 1) / kWaves : 0;  // this wave's n-tiles (wave-uniform)
+  const int col0 = 64 * w + 4 * c;   // this lane's four physical columns col0 + t (n-tile t)
+  const bool cok = col0 < F;         // (F % 4 == 0, checked on the host: all four or none)
 
-  // ---- registers for the whole launch: W1 fragments (k = 4 s + q, column
-  //      16 (w + 4 t) + c), W2 fragments of this wave's columns (local column
-  //      lc = 16 t + (lane's k within the step), 4 k-steps per n-tile), b1
+  // ---- registers for the whole launch: W1 fragments (k = 4 s + q, columns
+  //      col0 + t: one 16-B load per k-step), W2 fragments of this wave's
+  //      columns (local column lc = 16 t + 4 j + q of step (t, j) is physical
+  //      column 64 w + lc), b1.  All in flight at once (staging them through LDS
+  //      in rounds -- a barrier per 16 W1 rows -- measured 2x slower: eleven
+  //      dependent memory round trips)
+  stamp(a.epi, 0);
   float wf[KS][kNTQ];
 #pragma unroll
-  for (int s = 0; s < KS; ++s)
-#pragma unroll
-    for (int t = 0; t < kNTQ; ++t) {
-      const int k = 4 * s + q, col = 16 * (w + kWaves * t) + c;
-      wf[s][t] = (t < ntw && k < K && col < F) ? a.W[(int64_t)k * a.ldw + col] : 0.f;
-    }
-  // projection step (t, j): local columns 16 t + 4 j + q' for lane quadrant q'
+  for (int s = 0; s < KS; ++s) {
+    const int k = GCNK_DG_EXP == 6 ? (4 * s + q + 4 * (int)(blockIdx.x % KS)) % (4 * KS) : 4 * s + q;
+    float4 v = make_float4(0.f, 0.f, 0.f, 0.f);
+    if (GCNK_DG_EXP == 5) v = make_float4(1e-3f, 1e-3f, 1e-3f, 1e-3f);
+    else if (cok && k < K) v = *reinterpret_cast<const float4*>(a.W + (int64_t)k * a.ldw + col0);
+    wf[s][0] = v.x; wf[s][1] = v.y; wf[s][2] = v.z; wf[s][3] = v.w;
+  }
   float w2f[kNTQ][4][NP];
 #pragma unroll
   for (int t = 0; t < kNTQ; ++t)
@@ -112,15 +121,21 @@ dense_gc1_kernel(DenseArgs a) {
     for (int j = 0; j < 4; ++j)
 #pragma unroll
       for (int p = 0; p < NP; ++p) {
-        const int col = 16 * (w + kWaves * t) + 4 * j + q, pc = 16 * p + c;
-        w2f[t][j][p] = (t < ntw && col < F && pc < P) ? a.W2[(int64_t)col * a.ldw2 + pc] : 0.f;
+        const int col = 64 * w + 16 * t + 4 * j + q, pc = 16 * p + c;
+        w2f[t][j][p] = (GCNK_DG_EXP != 5 && col < F && pc < P) ? a.W2[(int64_t)col * a.ldw2 + pc]
+                                                             : (GCNK_DG_EXP == 5 ? 1e-3f : 0.f);
       }
   float bv[kNTQ];
-#pragma unroll
-  for (int t = 0; t < kNTQ; ++t) {
-    const int col = 16 * (w + kWaves * t) + c;
-    bv[t] = (a.epi.bias && t < ntw && col < F) ? a.epi.bias[col] : 0.f;
+  {
+    float4 v = make_float4(0.f, 0.f, 0.f, 0.f);
+    if (a.epi.bias && cok) v = *reinterpret_cast<const float4*>(a.epi.bias + col0);
+    bv[0] = v.x; bv[1] = v.y; bv[2] = v.z; bv[3] = v.w;
   }
+#ifdef GCNK_STAMPS
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  __syncthreads();
+  stamp(a.epi, 1);
+#endif
   float* hw = s_h[w];
   float* s_S = s_dyn;
   int32_t* s_rec = reinterpret_cast<int32_t*>(s_dyn + (HUB ? a.nhub * F : 0));
@@ -162,7 +177,10 @@ dense_gc1_kernel(DenseArgs a) {
     for (int i = 0; i < kAPer; ++i) {
       const int e = tid + kThreads * i, r = e / (4 * KS), k = e % (4 * KS);
       const int64_t row = (int64_t)tile * 16 + r;
-      av[i] = (GCNK_DG_EXP != 3 && e < 16 * 4 * KS && tile < a.ntiles && row < a.M && k < K) ? a.A[row * a.lda + k] : 0.f;
+      // (the address clamped into A, the value selected: no branch per load)
+      const int64_t rc = row < a.M ? row : a.M - 1;
+      const float v = a.A[rc * a.lda + (k < K ? k : K - 1)];
+      av[i] = (GCNK_DG_EXP != 3 && e < 16 * 4 * KS && tile < a.ntiles && row < a.M && k < K) ? v : 0.f;
     }
   };
   auto put_a = [&](int buf, const float (&av)[kAPer]) {
@@ -192,17 +210,21 @@ dense_gc1_kernel(DenseArgs a) {
     int32_t rv[kRecPer];
     load_rec(tile + gridDim.x, rv);
     // ---- 1. Z = A W1[:, cols_w]; lane (row c, quadrant q) reads A[c][4 s + q]
+    //      All KS fragments read before the MFMAs (one LDS wait), and every
+    //      wave issues kNTQ MFMAs per k-step: an absent n-tile's W1 fragments
+    //      are zero (a branch per MFMA broke the back-to-back issue and put an
+    //      LDS wait on every k-step)
     const float* sa = &s_A[buf][c * KP + q];
+    float af[KS];
+#pragma unroll
+    for (int s = 0; s < KS; ++s) af[s] = sa[4 * s];
     f32x4 acc[kNTQ];
 #pragma unroll
     for (int t = 0; t < kNTQ; ++t) acc[t] = f32x4{0.f, 0.f, 0.f, 0.f};
 #pragma unroll
-    for (int s = 0; s < (GCNK_DG_EXP == 1 ? 0 : KS); ++s) {
-      const float af = sa[4 * s];
+    for (int s = 0; s < (GCNK_DG_EXP == 1 ? 0 : KS); ++s)
 #pragma unroll
-      for (int t = 0; t < kNTQ; ++t)
-        if (t < ntw) acc[t] = __builtin_amdgcn_mfma_f32_16x16x4f32(af, wf[s][t], acc[t], 0, 0, 0);
-    }
+      for (int t = 0; t < kNTQ; ++t) acc[t] = __builtin_amdgcn_mfma_f32_16x16x4f32(af[s], wf[s][t], acc[t], 0, 0, 0);
     // ---- 2. epilogue (C/D map: reg r -> row 4 q + r, column c), H1 store,
     //      tile into wave-private LDS
     const int64_t row0 = (int64_t)tile * 16;
@@ -230,31 +252,36 @@ dense_gc1_kernel(DenseArgs a) {
         for (int r = 0; r < 4; ++r) {
           const int2 p2 = j < len[r] ? it[beg[r] + j] : int2{0, 0};   // (pad: + 0 x S_T[0])
           v[r] = __int_as_float(p2.y);
-          srow[r] = s_S + p2.x * F + 16 * w + c;
+          srow[r] = s_S + p2.x * F + col0;
         }
+        if (cok) {   // (columns past F: no read past the hub's row)
 #pragma unroll
-        for (int t = 0; t < kNTQ; ++t)   // (columns past F: no read past the hub's row)
-          if (t < ntw && 16 * (w + kWaves * t) + c < F)
-#pragma unroll
-            for (int r = 0; r < 4; ++r) acc[t][r] = fmaf(v[r], srow[r][16 * kWaves * t], acc[t][r]);
+          for (int r = 0; r < 4; ++r) {
+            const float4 sv = *reinterpret_cast<const float4*>(srow[r]);
+            acc[0][r] = fmaf(v[r], sv.x, acc[0][r]);
+            acc[1][r] = fmaf(v[r], sv.y, acc[1][r]);
+            acc[2][r] = fmaf(v[r], sv.z, acc[2][r]);
+            acc[3][r] = fmaf(v[r], sv.w, acc[3][r]);
+          }
+        }
       }
     } else {
 #pragma unroll
       for (int r = 0; r < 4; ++r) orow[r] = row0 + 4 * q + r;
     }
+    //      (columns past F: acc and b1 zero, h = 0 written)
 #pragma unroll
-    for (int t = 0; t < kNTQ; ++t) {
-      if (t >= ntw) break;
-      const int64_t col = 16 * (w + kWaves * t) + c;
+    for (int r = 0; r < 4; ++r) {
+      const int64_t row = orow[r];
+      float h[kNTQ];
 #pragma unroll
-      for (int r = 0; r < 4; ++r) {
-        const int64_t row = orow[r];
-        float h;
-        if (plain) h = fmaxf(acc[t][r] + bv[t], 0.f);
-        else h = (row < a.M && col < F) ? apply_epi(a.epi, acc[t][r], bv[t], row, col) : 0.f;
-        if (a.H && row < a.M && col < F) __builtin_nontemporal_store(h, a.H + row * a.ldh + col);
-        hw[(4 * q + r) * kHP + 16 * t + c] = h;
+      for (int t = 0; t < kNTQ; ++t) {
+        if (plain) h[t] = fmaxf(acc[t][r] + bv[t], 0.f);
+        else h[t] = (row < a.M && cok) ? apply_epi(a.epi, acc[t][r], bv[t], row, col0 + t) : 0.f;
       }
+      const f32x4 h4 = {h[0], h[1], h[2], h[3]};
+      if (a.H && row < a.M && cok) __builtin_nontemporal_store(h4, reinterpret_cast<f32x4*>(a.H + row * a.ldh + col0));
+      *reinterpret_cast<f32x4*>(&hw[(4 * q + r) * kHP + 4 * c]) = h4;
     }
     // the wave's own LDS writes before its reads (other lanes' elements)
     __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
@@ -266,8 +293,7 @@ dense_gc1_kernel(DenseArgs a) {
 #pragma unroll
     for (int p = 0; p < NP; ++p) pacc[p] = f32x4{0.f, 0.f, 0.f, 0.f};
 #pragma unroll
-    for (int t = 0; t < kNTQ; ++t) {
-      if (t >= ntw) break;
+    for (int t = 0; t < kNTQ; ++t) {   // (absent n-tiles: zero H1 x zero W2, no branch)
       float ha[4];
 #pragma unroll
       for (int j = 0; j < 4; ++j) ha[j] = hw[c * kHP + 16 * t + 4 * j + q];
@@ -280,23 +306,36 @@ dense_gc1_kernel(DenseArgs a) {
     }
 #pragma unroll
     for (int p = 0; p < NP; ++p) *reinterpret_cast<f32x4*>(&s_red[buf][w][p][4 * lane]) = pacc[p];
+    // output rows of this thread's S2 elements (e = tid + 256 i: tile row e / (16 NP),
+    // column e % (16 NP)), read before the barrier (the record buffer `buf` is
+    // rewritten by the next tile before ITS barrier)
+    int64_t rrow[NP];
+#pragma unroll
+    for (int i = 0; i < NP; ++i) {
+      const int tr = (tid + kThreads * i) / (16 * NP);
+      if constexpr (HUB) {
+        const int32_t id = s_rec[buf * rw + kRecRow + 16 * (tile & 1) + tr];
+        rrow[i] = id >= 0 ? id : a.M;
+      } else {
+        rrow[i] = row0 + tr;
+      }
+    }
     put_a(buf ^ 1, av);     // the next tile's A and record (their readers passed the previous barrier)
     put_rec(buf ^ 1, rv);
     // (double-buffered by tile parity: wave 0 reads buffer `buf` before it
     // reaches the next barrier, and buffer `buf` is written again only after it)
     __syncthreads();
-    if (w == 0 && GCNK_DG_EXP != 4) {
+    // the four waves' partials summed in wave order by the whole workgroup
+    // (partial (row 4 q + r, column 16 p + c) at s_red[.][w][p][4 (16 q + c) + r])
+    if (GCNK_DG_EXP != 4) {
 #pragma unroll
-      for (int p = 0; p < NP; ++p) {
-        f32x4 sum = *reinterpret_cast<const f32x4*>(&s_red[buf][0][p][4 * lane]);
+      for (int i = 0; i < NP; ++i) {
+        const int e = tid + kThreads * i, tr = e / (16 * NP), col = e % (16 * NP);
+        const int p = col >> 4, cc = col & 15, idx = 4 * (16 * (tr >> 2) + cc) + (tr & 3);
+        float sum = s_red[buf][0][p][idx];
 #pragma unroll
-        for (int v = 1; v < kWaves; ++v) sum += *reinterpret_cast<const f32x4*>(&s_red[buf][v][p][4 * lane]);
-        const int pc = 16 * p + c;
-#pragma unroll
-        for (int r = 0; r < 4; ++r) {
-          const int64_t row = orow[r];
-          if (row < a.M && pc < P) a.C2[row * a.ldc2 + pc] = sum[r];
-        }
+        for (int v = 1; v < kWaves; ++v) sum += s_red[buf][v][p][idx];
+        if (rrow[i] < a.M && col < P) a.C2[rrow[i] * a.ldc2 + col] = sum;
       }
     }
     // the wave-private H1 tile is rewritten next tile after these reads (in
@@ -304,7 +343,11 @@ dense_gc1_kernel(DenseArgs a) {
     __builtin_amdgcn_wave_barrier();
   };
   int buf = 0;
-  for (int tile = blockIdx.x; tile < a.ntiles; tile += gridDim.x, buf ^= 1) tile_step(tile, buf);
+  for (int tile = blockIdx.x; tile < a.ntiles; tile += gridDim.x, buf ^= 1) {
+    tile_step(tile, buf);
+    if (tile == (int)blockIdx.x) stamp(a.epi, 2);
+  }
+  stamp(a.epi, 3);
 }
 
 template <int KS, bool HUB>
@@ -363,7 +406,7 @@ Epi make_epi(const float* bias, int32_t epilogue, const uint8_t* mask, int64_t l
   e.offset = offset;
   e.rng_base = rng_base;
   e.code = epilogue;
-  e.stamps = nullptr;
+  e.stamps = debug_stamps();
   return e;
 }
 
@@ -378,7 +421,8 @@ int hubfactor_persistent(int32_t M, int32_t F, int32_t Kc, int32_t nhub, int32_t
                          const float* W2, int64_t ldw2, float* H, int64_t ldh, float* C2, int64_t ldc2, void* stream) {
   const size_t lds_bytes = (size_t)4 * ((size_t)nhub * F + 2 * (size_t)rec_words) + sizeof(float) * (size_t)kWaves * 16 * kHP +
                            sizeof(float) * 2 * kWaves * 2 * 64 * 4 + sizeof(float) * 2 * 16 * a_stride(32);
-  if (Kc > 128 || F > 16 * kWaves * kNTQ || F % 4 || lds % 4 || ((uintptr_t)S & 15) || P > kMaxP ||
+  if (Kc > 128 || F > 16 * kWaves * kNTQ || F % 4 || lds % 4 || ((uintptr_t)S & 15) || P > kMaxP || ldw % 4 ||
+      ((uintptr_t)(W + (int64_t)k0 * ldw) & 15) || (bias && ((uintptr_t)bias & 15)) || (H && (ldh % 4 || ((uintptr_t)H & 15))) ||
       rec_words > kThreads * 4 || lds_bytes > 160 * 1024)
     return GCNK_EUNSUP;
   DenseArgs a{};
@@ -408,8 +452,10 @@ extern "C" int gcnk_dense_gc1_f32(int32_t M, int32_t K, int32_t F, int32_t P, co
     set_error("gcnk_dense_gc1_f32: bad sizes or null operand (M=%d K=%d F=%d P=%d)", M, K, F, P);
     return GCNK_EARG;
   }
-  if (K > 128 || F > 16 * kWaves * kNTQ || P > kMaxP) {
-    set_error("gcnk_dense_gc1_f32: unsupported shape (K=%d <= 128, F=%d <= 256, P=%d <= 32)", K, F, P);
+  if (K > 128 || F > 16 * kWaves * kNTQ || F % 4 || P > kMaxP || ldw1 % 4 || !aligned16(W1) ||
+      (bias && !aligned16(bias)) || (H && (ldh % 4 || !aligned16(H)))) {
+    set_error("gcnk_dense_gc1_f32: unsupported shape (K=%d <= 128, F=%d <= 256 and %% 4, P=%d <= 32, "
+              "16-B aligned W1 / b1 / H1 rows)", K, F, P);
     return GCNK_EUNSUP;
   }
   if (epilogue != GCNK_EPI_BIAS_RELU && epilogue != GCNK_EPI_BIAS_RELU_DROP && epilogue != GCNK_EPI_BIAS_RELU_HASH) {

@@ -27,6 +27,7 @@ typedef float f32v4 __attribute__((ext_vector_type(4)));
 
 constexpr int kRows = 64;                    // M <= 64 (4 waves x 16 rows)
 constexpr int kCT = 16;                      // columns per tile (one MFMA n-tile)
+constexpr int kMaxSplits = 48;               // K ranges per column tile (the last arriver's loads in flight)
 
 __device__ __forceinline__ __amdgpu_buffer_rsrc_t rsrc(const void* base_uniform) {
   return __builtin_amdgcn_make_buffer_rsrc(const_cast<void*>(base_uniform), (short)0, 0x7fffffff, 0x00020000);
@@ -102,20 +103,27 @@ gemm_smallm_onepass_kernel(int32_t M, int32_t N, int32_t K, int32_t nsplit, cons
   }
   __syncthreads();
   // ---- MFMA: k order inside a 16-deep chunk permuted alike for A and B (lane
-  //      quadrant q, step j multiplies k = 16 ch + 4 q + j); two accumulators
-  //      (even / odd chunks) so the dependent-MFMA latency is hidden
-  f32x4 acc0 = f32x4{0.f, 0.f, 0.f, 0.f}, acc1 = acc0;
+  //      quadrant q, step j multiplies k = 16 ch + 4 q + j); four accumulators
+  //      (one per step j: independent chains, so the 40-cycle dependent latency
+  //      of v_mfma_f32_16x16x4_f32 hides under its 32-cycle issue), summed in a
+  //      fixed order
+  f32x4 acc[4];
+#pragma unroll
+  for (int j = 0; j < 4; ++j) acc[j] = f32x4{0.f, 0.f, 0.f, 0.f};
   const float* bcol = s_Bt + c * LS + 4 * q;
+  // every chunk's B fragments read before the MFMAs (one LDS wait, not one per chunk)
+  float4 bf[KCH];
+#pragma unroll
+  for (int ch = 0; ch < KCH; ++ch) bf[ch] = *reinterpret_cast<const float4*>(bcol + 16 * ch);
 #pragma unroll
   for (int ch = 0; ch < (GCNK_SMALLM_EXP == 4 ? 0 : KCH); ++ch) {
-    const float4 b4 = *reinterpret_cast<const float4*>(bcol + 16 * ch);
-    f32x4& acc = (ch & 1) ? acc1 : acc0;
-    acc = __builtin_amdgcn_mfma_f32_16x16x4f32(a[ch].x, b4.x, acc, 0, 0, 0);
-    acc = __builtin_amdgcn_mfma_f32_16x16x4f32(a[ch].y, b4.y, acc, 0, 0, 0);
-    acc = __builtin_amdgcn_mfma_f32_16x16x4f32(a[ch].z, b4.z, acc, 0, 0, 0);
-    acc = __builtin_amdgcn_mfma_f32_16x16x4f32(a[ch].w, b4.w, acc, 0, 0, 0);
+    const float4 b4 = bf[ch];
+    acc[0] = __builtin_amdgcn_mfma_f32_16x16x4f32(a[ch].x, b4.x, acc[0], 0, 0, 0);
+    acc[1] = __builtin_amdgcn_mfma_f32_16x16x4f32(a[ch].y, b4.y, acc[1], 0, 0, 0);
+    acc[2] = __builtin_amdgcn_mfma_f32_16x16x4f32(a[ch].z, b4.z, acc[2], 0, 0, 0);
+    acc[3] = __builtin_amdgcn_mfma_f32_16x16x4f32(a[ch].w, b4.w, acc[3], 0, 0, 0);
   }
-  f32x4 pv = acc0 + acc1;
+  f32x4 pv = (acc[0] + acc[1]) + (acc[2] + acc[3]);
   if (GCNK_SMALLM_EXP == 4) pv += f32x4{a[KCH - 1].x, a[0].y, bcol[0], bcol[KR - 1]};
   if (GCNK_SMALLM_EXP == 1) {
     float* pt1 = part + ((int64_t)t * nsplit + s) * (kRows * kCT);
@@ -147,7 +155,7 @@ gemm_smallm_onepass_kernel(int32_t M, int32_t N, int32_t K, int32_t nsplit, cons
   //      batches of 8 took ~1 us each past the L2s)
   const float* base = uniform_ptr(part + (int64_t)t * nsplit * (kRows * kCT));
   const int rr = tid >> 2, c4 = 4 * (tid & 3);
-  constexpr int kMaxSplit = 32;   // (pick_kch keeps nsplit <= 32 for K <= 16384)
+  constexpr int kMaxSplit = kMaxSplits;
   f32v4 v[kMaxSplit];
 #pragma unroll
   for (int j = 0; j < kMaxSplit; ++j)
@@ -166,11 +174,22 @@ gemm_smallm_onepass_kernel(int32_t M, int32_t N, int32_t K, int32_t nsplit, cons
   if (tid == 0) __hip_atomic_store(ctr + t, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);   // re-armed
 }
 
-// K range depth (16 KCH) for a K: ~20 ranges for R8's 7463 (the last arriver
-// then reads 20 x 4 KB), never below 64, never more than 32 ranges
+// K range depth (16 KCH) for a K: about kTargetSplits ranges (GCNK_SMALLM_SPLITS
+// overrides it for probes), never below 64 deep, never more than kMaxSplits
+int target_splits() {
+  static const int t = [] {
+    const char* v = getenv("GCNK_SMALLM_SPLITS");
+    const int n = v ? atoi(v) : 0;
+    return n > 0 && n <= kMaxSplits ? n : 20;
+  }();
+  return t;
+}
 int pick_kch(int32_t K) {
-  const int want = (K + 20 * 16 - 1) / (20 * 16);
-  return want <= 4 ? 4 : want <= 8 ? 8 : want <= 16 ? 16 : want <= 24 ? 24 : 32;
+  const int want = (int)((K + 16LL * target_splits() - 1) / (16LL * target_splits()));
+  static const int opts[] = {4, 6, 8, 12, 16, 24, 32};
+  for (int o : opts)
+    if (want <= o && (K + 16LL * o - 1) / (16LL * o) <= kMaxSplits) return o;
+  return 32;
 }
 int64_t nsplit_for(int32_t K) { return (K + 16 * pick_kch(K) - 1) / (16 * pick_kch(K)); }
 
@@ -198,7 +217,7 @@ extern "C" int gcnk_gemm_smallm_f32(int32_t M, int32_t N, int32_t K, const float
     set_error("gcnk_gemm_smallm_f32: bad sizes or null operand (M=%d N=%d K=%d)", M, N, K);
     return GCNK_EARG;
   }
-  if (M > kRows || lda % 4 || !aligned16(A) || ldb % 4 || !aligned16(B) || nsplit_for(K) > 32) {
+  if (M > kRows || lda % 4 || !aligned16(A) || ldb % 4 || !aligned16(B) || nsplit_for(K) > kMaxSplits) {
     set_error("gcnk_gemm_smallm_f32: unsupported (M=%d <= 64, lda %% 4, ldb %% 4, 16-B aligned A and B)", M);
     return GCNK_EUNSUP;
   }
@@ -218,7 +237,9 @@ extern "C" int gcnk_gemm_smallm_f32(int32_t M, int32_t N, int32_t K, const float
                      ldc, accumulate, workspace, counters)
   switch (kch) {
     case 4: GCNK_SMALLM(4); break;
+    case 6: GCNK_SMALLM(6); break;
     case 8: GCNK_SMALLM(8); break;
+    case 12: GCNK_SMALLM(12); break;
     case 16: GCNK_SMALLM(16); break;
     case 24: GCNK_SMALLM(24); break;
     default: GCNK_SMALLM(32); break;

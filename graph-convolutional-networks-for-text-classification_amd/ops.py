@@ -272,7 +272,7 @@ def dense_ax_for(adj, xop, F=None, P=None):
     M, K = xop.shape
     if adj.shape[0] != adj.shape[1] or adj.shape[1] != M or K > DENSE_AX_MAX_K or K == 0:
         return None
-    if (F is not None and F > 256) or (P is not None and P > 32):
+    if (F is not None and (F > 256 or F % 4)) or (P is not None and P > 32):   # (csrc/dense_gc1.hip's range)
         return None
     src = xop.dense
     key = (id(src), src.data_ptr(), src._version, adj.val.data_ptr(), adj.val._version)

@@ -12,6 +12,8 @@
 #   py:<script>[:<args>]      python scripts/<script> <args> -> <script>.log
 #   vpy:<variant>:<script>[:<args>]  the same on _variants/libgcnk_<variant>.so
 #   env:<NAME>=<value>        export for the following steps (env:<NAME>= unsets)
+#   pmc:<c1,c2,..>:<script>[:<args>]  one rocprofv3 --pmc pass (counters comma-separated,
+#                             within one pass's slots) over python scripts/<script> -> pmc<n>/
 # prof/py/vpy outputs carry the step number (several runs of one script per call)
 # Steps' outputs are summarised in profiles/ by hand (profiles/INDEX.md).
 cd "${GRAFT_REPO_ROOT:-/root/repo}" || exit 2
@@ -67,6 +69,12 @@ PY
       s="${rest2%%:*}"; args="${rest2#*:}"; [ "$args" = "$rest2" ] && args=""
       GCNK_LIB="_variants/libgcnk_$v.so" timeout -k 10 600 python3 -u "scripts/$s" $args > "$out/${s%.py}_$v$n.log" 2>&1
       rc=$?; tail -n 60 "$out/${s%.py}_$v$n.log"; [ $rc -eq 0 ] || { echo "rc=$rc"; exit 1; } ;;
+    pmc)
+      ctrs="${rest%%:*}"; rest2="${rest#*:}"
+      s="${rest2%%:*}"; args="${rest2#*:}"; [ "$args" = "$rest2" ] && args=""
+      timeout -s KILL 120 rocprofv3 --pmc ${ctrs//,/ } --output-format csv -d "$out/pmc$n" -o pmc -- \
+        python3 "scripts/$s" $args > "$out/pmc$n.log" 2>&1
+      rc=$?; tail -n 5 "$out/pmc$n.log"; [ $rc -eq 0 ] || { echo "rc=$rc"; exit 1; } ;;
     env)
       name="${rest%%=*}"; val="${rest#*=}"
       if [ -n "$val" ]; then export "$name=$val"; else unset "$name"; fi ;;

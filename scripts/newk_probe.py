@@ -21,6 +21,7 @@ sys.path.insert(0, os.path.join(ROOT, "scripts"))
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--reps", type=int, default=200)
+    ap.add_argument("--ops", default="smallm,dense20,dense8", help="subset of smallm,dense20,dense8")
     args = ap.parse_args()
     import torch
     import gcn_amd  # noqa: F401
@@ -34,24 +35,35 @@ def main():
     def line(op, us, **kw):
         print(json.dumps({"lib": tag, "op": op, "us": round(us, 3), **kw}), flush=True)
 
+    ops_sel = set(args.ops.split(","))
     # X_hubs W1
+    if "smallm" in ops_sel:
+        smallm(torch, ops, time_graph, g, dev, line, args.reps)
+    dense(torch, _lib, lib, time_graph, g, dev, line, args.reps, ops_sel)
+
+
+def smallm(torch, ops, time_graph, g, dev, line, reps):
     A = torch.zeros((50, 7464)).normal_(generator=g).to(dev)
     B = torch.zeros((7463, 200)).normal_(generator=g).to(dev)
     Av = A[:, :7463]
     C = ops.gemm_smallm(Av, B)
     err = float((C.cpu().double() - Av.cpu().double() @ B.cpu().double()).abs().max())
-    line("gemm_smallm 50x200x7463", time_graph([lambda: ops.gemm_smallm(Av, B, out=C)], args.reps), max_err=err)
+    line("gemm_smallm 50x200x7463", time_graph([lambda: ops.gemm_smallm(Av, B, out=C)], reps), max_err=err)
 
-    stream = ctypes.c_void_p(torch.cuda.current_stream().cuda_stream)
+
+def dense(torch, _lib, lib, time_graph, g, dev, line, reps, ops_sel):
     p = lambda t: ctypes.c_void_p(t.data_ptr())
-    for M, K, F, P in ((18916, 100, 200, 20), (7724, 100, 200, 8)):
+    for name, (M, K, F, P) in (("dense20", (18916, 100, 200, 20)), ("dense8", (7724, 100, 200, 8))):
+        if name not in ops_sel:
+            continue
         AX = torch.zeros((M, K)).normal_(generator=g).to(dev)
         W1 = (torch.zeros((K, F)).normal_(generator=g) * 0.1).to(dev)
         W2 = (torch.zeros((F, P)).normal_(generator=g) * 0.1).to(dev)
         b1 = torch.zeros(F).normal_(generator=g).to(dev)
         S2 = torch.empty((M, P), device=dev)
 
-        def run():
+        def run():   # (the stream inside: a hipGraph capture runs on a side stream)
+            stream = ctypes.c_void_p(torch.cuda.current_stream().cuda_stream)
             _lib.check(lib.gcnk_dense_gc1_f32(M, K, F, P, p(AX), K, p(W1), F, p(b1), _lib.EPI_BIAS_RELU, None, 0,
                                               1.0, 1.0, 0, 0, None, p(W2), P, None, 0, p(S2), P, stream),
                        "gcnk_dense_gc1_f32")
@@ -59,7 +71,7 @@ def main():
         torch.cuda.synchronize()
         want = torch.relu(AX.cpu().double() @ W1.cpu().double() + b1.cpu().double()) @ W2.cpu().double()
         err = float((S2.cpu().double() - want).abs().max())
-        line(f"dense_gc1 M{M} K{K} F{F} P{P}", time_graph([run], args.reps), max_err=err)
+        line(f"dense_gc1 M{M} K{K} F{F} P{P}", time_graph([run], reps), max_err=err)
 
 
 if __name__ == "__main__":

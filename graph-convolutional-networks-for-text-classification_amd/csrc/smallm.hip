@@ -155,15 +155,17 @@ gemm_smallm_onepass_kernel(int32_t M, int32_t N, int32_t K, int32_t nsplit, cons
   //      batches of 8 took ~1 us each past the L2s)
   const float* base = uniform_ptr(part + (int64_t)t * nsplit * (kRows * kCT));
   const int rr = tid >> 2, c4 = 4 * (tid & 3);
-  constexpr int kMaxSplit = kMaxSplits;
-  f32v4 v[kMaxSplit];
-#pragma unroll
-  for (int j = 0; j < kMaxSplit; ++j)
-    if (j < nsplit) v[j] = __builtin_amdgcn_raw_buffer_load_b128(rsrc(base), (int)(((j * kRows + rr) * kCT + c4) * 4), 0, kSc1);
   f32v4 sum = {0.f, 0.f, 0.f, 0.f};
+  for (int j0 = 0; j0 < nsplit; j0 += kMaxSplits) {   // (one batch unless K > 16 x 32 x kMaxSplits)
+    f32v4 v[kMaxSplits];
 #pragma unroll
-  for (int j = 0; j < kMaxSplit; ++j)
-    if (j < nsplit) sum += v[j];
+    for (int j = 0; j < kMaxSplits; ++j)
+      if (j0 + j < nsplit)
+        v[j] = __builtin_amdgcn_raw_buffer_load_b128(rsrc(base), (int)((((j0 + j) * kRows + rr) * kCT + c4) * 4), 0, kSc1);
+#pragma unroll
+    for (int j = 0; j < kMaxSplits; ++j)
+      if (j0 + j < nsplit) sum += v[j];
+  }
   if (rr < M) {
 #pragma unroll
     for (int i = 0; i < 4; ++i) {
@@ -175,7 +177,8 @@ gemm_smallm_onepass_kernel(int32_t M, int32_t N, int32_t K, int32_t nsplit, cons
 }
 
 // K range depth (16 KCH) for a K: about kTargetSplits ranges (GCNK_SMALLM_SPLITS
-// overrides it for probes), never below 64 deep, never more than kMaxSplits
+// overrides it for probes), never below 64 deep; past 32 x 16 x kMaxSplits the
+// last arriver sums the partials in batches of kMaxSplits
 int target_splits() {
   static const int t = [] {
     const char* v = getenv("GCNK_SMALLM_SPLITS");
@@ -217,7 +220,7 @@ extern "C" int gcnk_gemm_smallm_f32(int32_t M, int32_t N, int32_t K, const float
     set_error("gcnk_gemm_smallm_f32: bad sizes or null operand (M=%d N=%d K=%d)", M, N, K);
     return GCNK_EARG;
   }
-  if (M > kRows || lda % 4 || !aligned16(A) || ldb % 4 || !aligned16(B) || nsplit_for(K) > kMaxSplits) {
+  if (M > kRows || lda % 4 || !aligned16(A) || ldb % 4 || !aligned16(B) || nsplit_for(K) * kRows * kCT * 4 > INT32_MAX / 2) {
     set_error("gcnk_gemm_smallm_f32: unsupported (M=%d <= 64, lda %% 4, ldb %% 4, 16-B aligned A and B)", M);
     return GCNK_EUNSUP;
   }

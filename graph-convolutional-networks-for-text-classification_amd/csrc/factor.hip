@@ -65,13 +65,17 @@ struct FactorArgs {
   int32_t M, F, Kc, nhub, P;
   const float* U; int64_t ldu;          // [M x >= Kc], rows in block order
   const float* W; int64_t ldw; int32_t k0;  // W1 rows k0 .. k0 + Kc - 1 (ldw == F: staged flat)
-  const float* S; int64_t lds;          // [nhub x F]
+  const float* S; int64_t lds;          // [nhub x F], or nslab K-slabs of it (S_T = their sum in slab order)
+  int32_t nslab; int64_t slab_stride;   // (csrc/kslab.hip; slabs past the first summed after the DMA wait)
   const int32_t* rec; int32_t rec_words;  // per 32-row block: off[33] | pad | row ids | items int2 {hub, val}
   const float* W2; int64_t ldw2;        // [F x P]
   float* H; int64_t ldh;                // nullable
   float* C2; int64_t ldc2;              // [M x P]
   Epi epi;
 };
+
+// float4 registers per thread for S_T's K-slabs past the first
+constexpr int kSlabRegs = 16;
 
 template <int KS>
 __host__ __device__ constexpr int region1_floats(int F, int ntq) {
@@ -119,7 +123,7 @@ hubfactor_gc1_kernel(FactorArgs a) {
     const int32_t* rec = a.rec + (int64_t)blk * a.rec_words;
     for (int e0 = wv * 64; e0 < a.rec_words / 4; e0 += kThreads)
       if (e0 + lane < a.rec_words / 4) lds_dma16(rec + 4 * (e0 + lane), s_rec + 4 * e0);
-    const int s4 = a.nhub * Q;  // S_T [nhub x F] flat (lds == F)
+    const int s4 = a.nhub * Q;  // S_T [nhub x F] flat (lds == F): its first K-slab
     for (int e0 = wv * 64; e0 < s4; e0 += kThreads)
       if (e0 + lane < s4) lds_dma16(a.S + 4 * (e0 + lane), s_S + 4 * e0);
     const int w1 = F * a.P;     // W2 [F x P] flat (ldw2 == P), dword pieces
@@ -128,6 +132,18 @@ hubfactor_gc1_kernel(FactorArgs a) {
     if (a.epi.bias)
       for (int e0 = wv * 64; e0 < Q; e0 += kThreads)
         if (e0 + lane < Q) lds_dma16(a.epi.bias + 4 * (e0 + lane), s_bias + 4 * e0);
+  }
+  // S_T's further K-slabs (csrc/kslab.hip) into registers in the same round of
+  // loads: slot i holds slab 1 + i / per, piece i % per (piece p = float4
+  // tid + 512 p of the flat [nhub x F]); the host keeps (nslab - 1) per <= kSlabRegs
+  const int per = (a.nhub * Q + kThreads - 1) / kThreads;
+  float4 sv[kSlabRegs];
+#pragma unroll
+  for (int i = 0; i < kSlabRegs; ++i) {
+    const int j = 1 + i / per, e = tid + kThreads * (i % per);
+    sv[i] = (j < a.nslab && e < a.nhub * Q)
+                ? *reinterpret_cast<const float4*>(a.S + j * a.slab_stride + 4 * (int64_t)e)
+                : make_float4(0.f, 0.f, 0.f, 0.f);
   }
   float af[KS];
   {
@@ -138,6 +154,20 @@ hubfactor_gc1_kernel(FactorArgs a) {
   }
   __builtin_amdgcn_s_waitcnt(0x0F70);  // vmcnt(0): this wave's DMA and fragment loads have landed
   __syncthreads();
+  // S_T = ((slab 0 + slab 1) + slab 2) + slab 3, each thread on its own pieces
+  // (slots in slab order); phase 2 reads s_S only after the barriers below
+  if (a.nslab > 1) {
+#pragma unroll
+    for (int i = 0; i < kSlabRegs; ++i) {
+      const int j = 1 + i / per, e = tid + kThreads * (i % per);
+      if (j < a.nslab && e < a.nhub * Q) {
+        float4* d = reinterpret_cast<float4*>(s_S + 4 * e);
+        float4 v = *d;
+        v.x += sv[i].x; v.y += sv[i].y; v.z += sv[i].z; v.w += sv[i].w;
+        *d = v;
+      }
+    }
+  }
   stamp(a.epi, 0);
 
   // ---- 1. Z = U W1[Kc] for this wave's strip and column quarter
@@ -317,13 +347,23 @@ static int launch_factor(const FactorArgs& a, int64_t nblk, int64_t lds_b, void*
   return launch_check("hubfactor_gc1_kernel");
 }
 
-extern "C" int gcnk_hubfactor_gc1_f32(int32_t M, int32_t F, int32_t Kc, int32_t nhub, int32_t P, const float* U,
-                                      int64_t ldu, const float* W, int64_t ldw, int32_t k0, const float* S,
-                                      int64_t lds, const int32_t* rec, int32_t rec_words, const float* bias,
-                                      int32_t epilogue, const uint8_t* drop_mask, int64_t ldm, float drop_scale,
-                                      float keep_prob, uint64_t seed, uint64_t offset, const uint64_t* rng_base,
-                                      const float* W2, int64_t ldw2, float* H, int64_t ldh, float* C2,
-                                      int64_t ldc2, void* stream) {
+extern "C" int gcnk_hubfactor_gc1_slabs_f32(int32_t M, int32_t F, int32_t Kc, int32_t nhub, int32_t P,
+                                            const float* U, int64_t ldu, const float* W, int64_t ldw, int32_t k0,
+                                            const float* S, int64_t lds, int32_t nslab, int64_t slab_stride,
+                                            const int32_t* rec, int32_t rec_words, const float* bias,
+                                            int32_t epilogue, const uint8_t* drop_mask, int64_t ldm,
+                                            float drop_scale, float keep_prob, uint64_t seed, uint64_t offset,
+                                            const uint64_t* rng_base, const float* W2, int64_t ldw2, float* H,
+                                            int64_t ldh, float* C2, int64_t ldc2, void* stream) {
+  if (nslab < 1 || nslab > 4 || (nslab > 1 && slab_stride < (int64_t)nhub * lds)) {
+    set_error("gcnk_hubfactor_gc1_f32: bad K-slab count %d or stride %lld", nslab, (long long)slab_stride);
+    return GCNK_EARG;
+  }
+  if (nslab > 1 && ((int64_t)(nslab - 1) * (((int64_t)nhub * (F / 4) + kThreads - 1) / kThreads) > kSlabRegs ||
+                    slab_stride % 4)) {
+    set_error("gcnk_hubfactor_gc1_f32: %d K-slabs of %d x %d exceed the staging registers", nslab, nhub, F);
+    return GCNK_EUNSUP;
+  }
   if (M <= 0 || F <= 0 || Kc <= 0 || nhub <= 0 || P <= 0 || !U || !W || !S || !rec || !W2 || !C2 || k0 < 0) {
     set_error("gcnk_hubfactor_gc1_f32: bad sizes or null operand (M=%d F=%d Kc=%d hubs=%d P=%d)", M, F, Kc, nhub, P);
     return GCNK_EARG;
@@ -354,7 +394,7 @@ extern "C" int gcnk_hubfactor_gc1_f32(int32_t M, int32_t F, int32_t Kc, int32_t 
   // launch, S_T staged once per CU instead of once per 32-row block); read per
   // call (a hipGraph keeps the choice made at capture)
   const char* hv = getenv("GCNK_HUBFACTOR");
-  if (hv && strcmp(hv, "persistent") == 0) {
+  if (nslab == 1 && hv && strcmp(hv, "persistent") == 0) {
     const int rc = hubfactor_persistent(M, F, Kc, nhub, P, U, ldu, W, ldw, k0, S, lds, rec, rec_words, bias, epilogue,
                                         drop_mask, ldm, drop_scale, keep_prob, seed, offset, rng_base, W2, ldw2, H,
                                         ldh, C2, ldc2, stream);
@@ -364,6 +404,7 @@ extern "C" int gcnk_hubfactor_gc1_f32(int32_t M, int32_t F, int32_t Kc, int32_t 
   a.M = M; a.F = F; a.Kc = Kc; a.nhub = nhub; a.P = P;
   a.U = U; a.ldu = ldu; a.W = W; a.ldw = ldw; a.k0 = k0;
   a.S = S; a.lds = lds; a.rec = rec; a.rec_words = rec_words;
+  a.nslab = nslab; a.slab_stride = slab_stride;
   a.W2 = W2; a.ldw2 = ldw2; a.H = H; a.ldh = ldh; a.C2 = C2; a.ldc2 = ldc2;
   Epi& e = a.epi;
   e.bias = bias; e.mask = drop_mask; e.scale = drop_scale; e.keep_prob = keep_prob;
@@ -383,4 +424,16 @@ extern "C" int gcnk_hubfactor_gc1_f32(int32_t M, int32_t F, int32_t Kc, int32_t 
 #undef GCNK_FACTOR_CASE
   set_error("gcnk_hubfactor_gc1_f32: no kernel for Kc=%d F=%d", Kc, F);
   return GCNK_EUNSUP;
+}
+
+extern "C" int gcnk_hubfactor_gc1_f32(int32_t M, int32_t F, int32_t Kc, int32_t nhub, int32_t P, const float* U,
+                                      int64_t ldu, const float* W, int64_t ldw, int32_t k0, const float* S,
+                                      int64_t lds, const int32_t* rec, int32_t rec_words, const float* bias,
+                                      int32_t epilogue, const uint8_t* drop_mask, int64_t ldm, float drop_scale,
+                                      float keep_prob, uint64_t seed, uint64_t offset, const uint64_t* rng_base,
+                                      const float* W2, int64_t ldw2, float* H, int64_t ldh, float* C2,
+                                      int64_t ldc2, void* stream) {
+  return gcnk_hubfactor_gc1_slabs_f32(M, F, Kc, nhub, P, U, ldu, W, ldw, k0, S, lds, 1, 0, rec, rec_words, bias,
+                                      epilogue, drop_mask, ldm, drop_scale, keep_prob, seed, offset, rng_base, W2,
+                                      ldw2, H, ldh, C2, ldc2, stream);
 }

@@ -24,6 +24,9 @@ int spmm_ref(const gcnk_plan_ref& p, const float* B, int64_t ldb, int32_t F, flo
 
 // S1 = X W1 (sparse X through its plan, dense X on the MFMA GEMM)
 int first_product(const gcnk_gcn_fwd& r, const float* W1, void* stream) {
+  if (r.s1_slabs > 1 && r.x_dense)   // S_T as K-slabs, summed by the factored gc1
+    return gcnk_gemm_kslabs_f32(r.x_rows, r.F, r.x_cols, r.x_dense, r.ldx, W1, r.F, r.s1_slabs, r.s1, r.lds1,
+                                r.s1_slab_stride, stream);
   if (r.x.plan)
     return spmm_ref(r.x, W1, r.F, r.F, r.s1, r.lds1, nullptr, GCNK_EPI_NONE, nullptr, 0, 1.f, 1.f, 0, 0, nullptr,
                     stream);
@@ -60,9 +63,10 @@ extern "C" int gcnk_gcn_forward_f32(const gcnk_gcn_fwd* rec, const float* W1, co
   switch (r.kind) {
     case GCNK_FWD_FACTORED:
       if ((rc = first_product(r, W1, stream)) != GCNK_OK) return rc;
-      rc = gcnk_hubfactor_gc1_f32(r.M, r.F, r.Kc, r.nhub, r.P, r.U, r.ldu, W1, r.F, r.k0, r.s1, r.lds1, r.rec,
-                                  r.rec_words, b1, epilogue, drop_mask, ldm, drop_scale, keep_prob, seed, offset,
-                                  rng_base, W2, r.P, H1, ldh, r.s2, r.lds2, stream);
+      rc = gcnk_hubfactor_gc1_slabs_f32(r.M, r.F, r.Kc, r.nhub, r.P, r.U, r.ldu, W1, r.F, r.k0, r.s1, r.lds1,
+                                        (r.s1_slabs > 1 && r.x_dense) ? r.s1_slabs : 1, r.s1_slab_stride, r.rec,
+                                        r.rec_words, b1, epilogue, drop_mask, ldm, drop_scale, keep_prob, seed,
+                                        offset, rng_base, W2, r.P, H1, ldh, r.s2, r.lds2, stream);
       break;
     case GCNK_FWD_DENSE_AX:
       rc = gcnk_dense_gc1_f32(r.M, r.Kc, r.F, r.P, r.U, r.ldu, W1, r.F, b1, epilogue, drop_mask, ldm, drop_scale,
@@ -107,7 +111,8 @@ extern "C" int32_t gcnk_gcn_fwd_layout(int64_t* out, int32_t n) {
                        (int64_t)offsetof(gcnk_gcn_fwd, ld_h1_tmp), (int64_t)offsetof(gcnk_plan_ref, lanes_hint),
                        (int64_t)sizeof(gcnk_gcn_bwd), (int64_t)offsetof(gcnk_gcn_bwd, xT),
                        (int64_t)offsetof(gcnk_gcn_bwd, bwd2_ws_bytes), (int64_t)offsetof(gcnk_gcn_fwd, x_ctr),
-                       (int64_t)offsetof(gcnk_gcn_bwd, aTH), (int64_t)offsetof(gcnk_gcn_bwd, sm_ctr_bytes)};
+                       (int64_t)offsetof(gcnk_gcn_bwd, aTH), (int64_t)offsetof(gcnk_gcn_bwd, sm_ctr_bytes),
+                       (int64_t)offsetof(gcnk_gcn_fwd, s1_slabs), (int64_t)offsetof(gcnk_gcn_fwd, s1_slab_stride)};
   const int32_t m = (int32_t)(sizeof(v) / sizeof(v[0]));
   for (int32_t i = 0; i < n && i < m; ++i) out[i] = v[i];
   return m;

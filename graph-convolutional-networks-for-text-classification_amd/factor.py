@@ -37,10 +37,17 @@ MAX_HUBS = 128    # hub rows staged in LDS (S_T [hubs x F]; the kernel checks th
 # tiled GEMM took 13.7).  A one-launch split-K kernel with two levels of
 # last-arriver slab sums measured 12.1 us (round 4, DESIGN §5: each coherent
 # hand-off is a ~2 us memory round trip) and was removed.
-# "onepass" (round 5): a dense copy of the hub rows through the
-# one-launch small-M GEMM (csrc/smallm.hip: ~20 K ranges x 16-column tiles,
-# each tile's partials summed by its last workgroup) -- no slab-reduce launch.
+# "slabs" (round 5): a dense copy of the hub rows through gcnk_gemm_kslabs_f32
+# into SLABS K-slabs (csrc/kslab.hip), summed by the factored gc1 while it
+# stages S_T -- no reduction launch, no hand-off.  Measured slower on R8: the
+# 4-deep slabs leave 238 KB of loads per workgroup (11.9 us) and the factored gc1
+# slows 9.9 -> 13.2 us staging 4 slabs (profiles/r05_fwdtrace_r8_slabs_*).
+# "onepass" (round 5): a dense copy of the hub rows through the one-launch
+# small-M GEMM (csrc/smallm.hip: ~20 K ranges x 16-column tiles, each tile's
+# partials summed by its last workgroup) -- no slab-reduce launch, but measured
+# slower: 12.2 us, ~4 us of it the coherent hand-off (profiles/r05_smallm_*).
 XHUB = os.environ.get("GCNK_FACTOR_XHUB", "spmm")
+SLABS = int(os.environ.get("GCNK_FACTOR_SLABS", "4"))
 MAX_KC = 128      # X's light-row column range (U's width)
 ROWS_PER_BLOCK = 32   # csrc/factor.hip kRB
 # record words before the items: 33 row offsets | 3 pad | 32 row ids (-1 past
@@ -121,6 +128,35 @@ class HubFactor:
         """X_hubs W1 runs on the one-launch small-M GEMM (gcnk_gemm_smallm_f32)."""
         return XHUB == "onepass" and self.x_hub_dense is not None and self.H <= 64 and \
             self.x_hub_dense.stride(0) % 4 == 0
+
+    def slabs(self, F):
+        """K-slabs of S_T = X_hubs W1 (gcnk_gemm_kslabs_f32, summed by
+        gcnk_hubfactor_gc1_slabs_f32) at width F; 1 = one whole S_T.  Bounded by
+        the kernel's staging registers: (slabs - 1) ceil(H F / 2048) <= 16."""
+        if XHUB != "slabs" or self.x_hub_dense is None or self.x_hub_dense.stride(0) % 4:
+            return 1
+        per = (self.H * (F // 4) + 511) // 512
+        n = max(1, min(SLABS, 4, 1 + 16 // max(1, per)))
+        kx = self.x_hub_dense.shape[1]
+        while n > 1 and ((kx + 15) // 16 + n - 1) // n > 24 * 8:   # the kernel's chunks per slab
+            n -= 1
+        return n if n > 1 and ((kx + 15) // 16 + n - 1) // n <= 24 * 8 else 1
+
+    def hub_slabs(self, W):
+        """(S, nslab): S_T = X[hubs] @ W as nslab K-slabs stacked [nslab H x F]
+        (gcnk_gemm_kslabs_f32), or the whole S_T with nslab 1."""
+        n = self.slabs(W.shape[1])
+        if n == 1:
+            return self.hub_times(W).contiguous(), 1
+        from . import _lib
+        H, F = self.H, W.shape[1]
+        S = torch.empty((n * H, F), dtype=torch.float32, device=W.device)
+        xd = self.x_hub_dense
+        with torch.cuda.device(W.device):
+            _lib.check(_lib.load().gcnk_gemm_kslabs_f32(
+                H, F, xd.shape[1], xd.data_ptr(), xd.stride(0), W.data_ptr(), W.stride(0), n, S.data_ptr(), F, H * F,
+                torch.cuda.current_stream(W.device).cuda_stream), "gcnk_gemm_kslabs_f32")
+        return S, n
 
     def hub_times(self, W):
         """S_T = X[hubs] @ W  (the hub rows of reference layer.py:102)."""
@@ -243,7 +279,7 @@ def build(adj, xop):
         f.x_hub_dense = None
         kx = x.shape[1]
         fits = H * kx * 4 <= 64 << 20
-        if fits and XHUB in ("gemm", "onepass"):
+        if fits and XHUB in ("gemm", "onepass", "slabs"):
             # rows padded to a multiple of 4 floats (the GEMM's float4 loads)
             d = torch.zeros((H, (kx + 3) // 4 * 4), dtype=torch.float32, device=dev)
             d[torch.repeat_interleave(torch.arange(H, device=dev), lens, output_size=tot), x.colind[idx].long()] = \

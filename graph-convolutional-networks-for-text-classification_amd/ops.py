@@ -210,8 +210,9 @@ def factor_for(adj, xop):
 def hubfactor_gc1(f, W1, b1, W2, epilogue=_lib.EPI_BIAS_RELU, mask=None, scale=1.0, keep_prob=1.0, seed=0,
                   offset=0, rng_base=None, store_h1=True, S=None):
     """(H1, S2) of gc1 + gc2's support through the hub factorisation ``f``
-    (factor.HubFactor): S_T = X[hubs] W1 (layer.py:102, the tile GEMM), then
-    one launch of gcnk_hubfactor_gc1_f32 -- H1 = drop(relu(A-hat X W1 + b1))
+    (factor.HubFactor): S_T = X[hubs] W1 (layer.py:102; K-slabs on
+    gcnk_gemm_kslabs_f32 where factor.slabs allows), then one launch of
+    gcnk_hubfactor_gc1_slabs_f32 (the slabs summed while staging S_T) -- H1 = drop(relu(A-hat X W1 + b1))
     (layer.py:106,110,182,185) and S2 = H1 W2 (layer.py:102, gc2).  Returns
     None when the shapes are outside the kernel's range (the caller takes the
     SpMM path).  ``S``: S_T already computed (timing probes)."""
@@ -228,7 +229,7 @@ def hubfactor_gc1(f, W1, b1, W2, epilogue=_lib.EPI_BIAS_RELU, mask=None, scale=1
     lib = _lib.load()
     if int(lib.gcnk_hubfactor_lds_bytes(F, f.Kc, f.H, f.rec_words, P)) > 160 * 1024:
         return None
-    S = f.hub_times(W1).contiguous() if S is None else S
+    S, nslab = f.hub_slabs(W1) if S is None else (S, 1)
     H1 = torch.empty((M, F), dtype=torch.float32, device=W1.device) if store_h1 else None
     S2 = torch.empty((M, P), dtype=torch.float32, device=W1.device)
     if b1 is not None:
@@ -236,15 +237,15 @@ def hubfactor_gc1(f, W1, b1, W2, epilogue=_lib.EPI_BIAS_RELU, mask=None, scale=1
     if mask is not None:
         mask = mask.contiguous()
     with torch.cuda.device(W1.device):
-        rc = lib.gcnk_hubfactor_gc1_f32(
+        rc = lib.gcnk_hubfactor_gc1_slabs_f32(
             M, F, f.Kc, f.H, P, _ptr(f.U), f.U.stride(0), _ptr(W1), W1.stride(0), f.k0, _ptr(S), S.stride(0),
-            _ptr(f.rec), f.rec_words, _ptr(b1), epilogue,
+            nslab, f.H * S.stride(0), _ptr(f.rec), f.rec_words, _ptr(b1), epilogue,
             _ptr(mask), mask.stride(0) if mask is not None else 0, float(scale),
             float(keep_prob), int(seed) & (2**64 - 1), int(offset) & (2**64 - 1), _ptr(rng_base),
             _ptr(W2), W2.stride(0), _ptr(H1), F, _ptr(S2), P, _stream(W1.device))
     if rc == _lib.EUNSUP:
         return None
-    _lib.check(rc, "gcnk_hubfactor_gc1_f32")
+    _lib.check(rc, "gcnk_hubfactor_gc1_slabs_f32")
     return H1, S2
 
 

@@ -40,7 +40,8 @@ class GcnFwd(_c.Structure):
                 ("U", _c.c_void_p), ("ldu", _c.c_int64), ("rec", _c.c_void_p),
                 ("aF", PlanRef), ("aP", PlanRef), ("s2", _c.c_void_p), ("lds2", _c.c_int64),
                 ("h1_tmp", _c.c_void_p), ("ld_h1_tmp", _c.c_int64), ("x_ctr", _c.c_void_p),
-                ("x_ctr_bytes", _c.c_int64)]
+                ("x_ctr_bytes", _c.c_int64), ("s1_slabs", _c.c_int32), ("pad2_", _c.c_int32),
+                ("s1_slab_stride", _c.c_int64)]
 
 
 class GcnBwd(_c.Structure):
@@ -64,13 +65,13 @@ BWD_AX_DIRECT, BWD_FACTORED = 1, 2
 
 def layout_ok():
     """The ctypes mirrors match the library's struct layout (gcnk_gcn_fwd_layout)."""
-    buf = (_c.c_int64 * 14)()
-    n = _lib.load().gcnk_gcn_fwd_layout(buf, 14)
+    buf = (_c.c_int64 * 16)()
+    n = _lib.load().gcnk_gcn_fwd_layout(buf, 16)
     want = [_c.sizeof(PlanRef), _c.sizeof(GcnFwd), GcnFwd.x.offset, GcnFwd.U.offset, GcnFwd.aF.offset,
             GcnFwd.aP.offset, GcnFwd.ld_h1_tmp.offset, PlanRef.lanes_hint.offset, _c.sizeof(GcnBwd),
             GcnBwd.xT.offset, GcnBwd.bwd2_ws_bytes.offset, GcnFwd.x_ctr.offset, GcnBwd.aTH.offset,
-            GcnBwd.sm_ctr_bytes.offset]
-    return n == 14 and list(buf) == want
+            GcnBwd.sm_ctr_bytes.offset, GcnFwd.s1_slabs.offset, GcnFwd.s1_slab_stride.offset]
+    return n == 16 and list(buf) == want
 
 
 def _fill_plan(ref, plan, F, lanes, device, keep):
@@ -179,7 +180,12 @@ class ForwardRecord:
             g = torch.empty((gws + 3) // 4, dtype=torch.float32, device=device)
             keep.append(g)
             s.gemm_ws, s.gemm_ws_bytes = g.data_ptr(), gws
-        s1 = torch.empty((rows, F), dtype=torch.float32, device=device)
+        # factored with dense X_hubs: S_T as K-slabs that the factored gc1 sums
+        # while staging it (gcnk_gemm_kslabs_f32; no reduction launch)
+        nslab = fac.slabs(F) if kind == FACTORED and not onepass else 1
+        s1 = torch.empty((nslab * rows, F), dtype=torch.float32, device=device)
+        if nslab > 1:
+            s.s1_slabs, s.s1_slab_stride = nslab, rows * F
         s2 = torch.empty((M, P), dtype=torch.float32, device=device)
         keep += [s1, s2]
         s.s1, s.lds1, s.s2, s.lds2 = s1.data_ptr(), F, s2.data_ptr(), P

@@ -50,7 +50,7 @@
 extern "C" {
 #endif
 
-#define GCNK_ABI_VERSION 10
+#define GCNK_ABI_VERSION 11
 
 #define GCNK_OK 0
 #define GCNK_EARG (-1)
@@ -268,6 +268,26 @@ int gcnk_hubfactor_gc1_f32(int32_t M, int32_t F, int32_t Kc, int32_t nhub, int32
                            const uint8_t* drop_mask, int64_t ldm, float drop_scale, float keep_prob, uint64_t seed,
                            uint64_t offset, const uint64_t* rng_base, const float* W2, int64_t ldw2, float* H,
                            int64_t ldh, float* C2, int64_t ldc2, void* stream);
+/* The same with S_T given as nslab (1-4) K-slabs S + s slab_stride, s < nslab
+ * (gcnk_gemm_kslabs_f32), summed in slab order while the kernel stages S_T:
+ * S_T = ((S_0 + S_1) + S_2) + S_3.  GCNK_EUNSUP when (nslab - 1) x
+ * ceil(nhub F / 2048) > 16 (the staging registers); nslab == 1 is
+ * gcnk_hubfactor_gc1_f32. */
+int gcnk_hubfactor_gc1_slabs_f32(int32_t M, int32_t F, int32_t Kc, int32_t nhub, int32_t P, const float* U,
+                                 int64_t ldu, const float* W, int64_t ldw, int32_t k0, const float* S, int64_t lds,
+                                 int32_t nslab, int64_t slab_stride, const int32_t* rec, int32_t rec_words,
+                                 const float* bias, int32_t epilogue, const uint8_t* drop_mask, int64_t ldm,
+                                 float drop_scale, float keep_prob, uint64_t seed, uint64_t offset,
+                                 const uint64_t* rng_base, const float* W2, int64_t ldw2, float* H, int64_t ldh,
+                                 float* C2, int64_t ldc2, void* stream);
+/* S_T's K-slabs for the above (csrc/kslab.hip; X_hubs W1, reference layer.py:102
+ * on the topic rows): C + s slab_stride = A[:, K_s] B[K_s, :] for s < nslab
+ * (1-4), K cut into 16-deep chunks and slab s owning chunks [s cps, (s+1) cps),
+ * cps = ceil(ceil(K / 16) / nslab).  No reduction launch and no hand-off: the
+ * consumer sums the slabs.  A: 16-B aligned rows (lda % 4 == 0).  Fixed-order
+ * sums: bitwise reproducible.  GCNK_EUNSUP past K = 3072 nslab. */
+int gcnk_gemm_kslabs_f32(int32_t M, int32_t N, int32_t K, const float* A, int64_t lda, const float* B, int64_t ldb,
+                         int32_t nslab, float* C, int64_t ldc, int64_t slab_stride, void* stream);
 
 /* ---------------------------------------------------------------------------
  * Narrow-feature gc1 (csrc/dense_gc1.hip; GCN.forward layer.py:164-190 through
@@ -391,6 +411,10 @@ typedef struct gcnk_gcn_fwd {
   int64_t ld_h1_tmp;
   int32_t* x_ctr;              /* non-NULL: the first product on the one-pass small-M GEMM */
   int64_t x_ctr_bytes;         /* (gcnk_gemm_smallm_f32; gemm_ws its workspace), zeroed once */
+  int32_t s1_slabs;            /* FACTORED, dense X_hubs: > 1 -> S_T as that many K-slabs (ABI 11) */
+  int32_t pad2_;
+  int64_t s1_slab_stride;      /* floats between the slabs in s1 (gcnk_gemm_kslabs_f32 ->
+                                  gcnk_hubfactor_gc1_slabs_f32) */
 } gcnk_gcn_fwd;
 
 int gcnk_gcn_forward_f32(const gcnk_gcn_fwd* rec,

@@ -49,6 +49,13 @@ def smallm(torch, ops, time_graph, g, dev, line, reps):
     C = ops.gemm_smallm(Av, B)
     err = float((C.cpu().double() - Av.cpu().double() @ B.cpu().double()).abs().max())
     line("gemm_smallm 50x200x7463", time_graph([lambda: ops.gemm_smallm(Av, B, out=C)], reps), max_err=err)
+    # the library GEMMs on the same product (reference points: rocBLAS / hipBLASLt through torch.mm)
+    Ac = Av.contiguous()
+    C2 = torch.mm(Ac, B)
+    line("torch.mm 50x200x7463 (library)", time_graph([lambda: torch.mm(Ac, B, out=C2)], reps),
+         max_err=float((C2.cpu().double() - Av.cpu().double() @ B.cpu().double()).abs().max()))
+    C3 = ops.gemm(Av, B)
+    line("ops.gemm 50x200x7463 (tiled MFMA)", time_graph([lambda: ops.gemm(Av, B, out=C3)], reps))
 
 
 def dense(torch, _lib, lib, time_graph, g, dev, line, reps, ops_sel):

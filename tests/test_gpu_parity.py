@@ -415,6 +415,44 @@ def test_gemm_small_m_split_k(shape, split):
     assert torch.equal(got, gemm(Ad, B.to(DEV), split_k=split))
 
 
+@pytest.mark.parametrize("shape,nslab", [((50, 200, 7463), 4), ((64, 200, 8192), 4), ((1, 4, 100), 1),
+                                         ((17, 116, 1000), 3), ((50, 8, 7463), 3), ((50, 8, 3000), 2),
+                                         ((33, 20, 12000), 4),
+                                         ((70, 200, 100), 3)])
+def test_gemm_kslabs(shape, nslab):
+    """gcnk_gemm_kslabs_f32 (csrc/kslab.hip): slab s = A[:, K_s] B[K_s, :] for
+    the documented 16-deep chunk ranges (cps = ceil(ceil(K / 16) / nslab)), each
+    against float64 (K ragged against 16, N against 16, M against 16, A rows
+    padded to 4 floats); bitwise reproducible; too deep a K is refused."""
+    import ctypes
+    M, N, K = shape
+    rng = np.random.default_rng(M + N + K)
+    Ap = torch.from_numpy(rng.standard_normal((M, (K + 3) // 4 * 4)).astype(np.float32))
+    A = Ap[:, :K]
+    B = torch.from_numpy(rng.standard_normal((K, N)).astype(np.float32))
+    Ad, Bd = Ap.to(DEV)[:, :K], B.to(DEV)
+    lib = _lib.load()
+    stream = ctypes.c_void_p(torch.cuda.current_stream().cuda_stream)
+
+    def run():
+        C = torch.full((nslab * M, N), float("nan"), device=DEV)
+        _lib.check(lib.gcnk_gemm_kslabs_f32(M, N, K, Ad.data_ptr(), Ad.stride(0), Bd.data_ptr(), N, nslab,
+                                            C.data_ptr(), N, M * N, stream), "gcnk_gemm_kslabs_f32")
+        return C
+    C = run()
+    cps = ((K + 15) // 16 + nslab - 1) // nslab
+    for sl in range(nslab):
+        k0, k1 = min(K, 16 * cps * sl), min(K, 16 * cps * (sl + 1))
+        want = A[:, k0:k1].double().numpy() @ B[k0:k1].double().numpy()
+        _close(C[sl * M:(sl + 1) * M], want, rtol=1e-5, atol=2e-6 * np.sqrt(max(1, k1 - k0)) * 4)
+    assert torch.equal(run(), C)
+    C2 = torch.empty((4 * 64, 200), device=DEV)
+    A2 = torch.zeros((64, 30000), device=DEV)
+    B2 = torch.zeros((30000, 200), device=DEV)
+    assert lib.gcnk_gemm_kslabs_f32(64, 200, 30000, A2.data_ptr(), 30000, B2.data_ptr(), 200, 4, C2.data_ptr(), 200,
+                                    64 * 200, stream) == _lib.EUNSUP
+
+
 @pytest.mark.parametrize("shape", [(50, 200, 7463), (64, 200, 8192), (1, 4, 512), (17, 116, 1000), (64, 13, 100),
                                    (50, 8, 7463), (33, 200, 30000)])
 def test_gemm_small_m_one_pass(shape):
@@ -1157,7 +1195,7 @@ def test_factored_gc1_matches_spmm_path(r8, mode):
         _grads_close(ga[k], gb[k], k)
 
 
-@pytest.mark.parametrize("kernel", ["legacy", "persistent"])
+@pytest.mark.parametrize("kernel", ["legacy", "persistent", "slabs"])
 @pytest.mark.parametrize("F,P,ndoc", [(52, 3, 2000), (200, 20, 2000), (36, 32, 2000), (200, 20, 12000)])
 def test_factored_gc1_kernel_against_float64(F, P, ndoc, kernel, monkeypatch):
     """gcnk_hubfactor_gc1_f32 alone on a synthetic doc-topic graph with hub x
@@ -1169,11 +1207,12 @@ def test_factored_gc1_kernel_against_float64(F, P, ndoc, kernel, monkeypatch):
     NaN bits (gcnk_debug_poison_lds): a read of LDS the kernel did not write
     would surface as NaN.  Both kernels: csrc/factor.hip's per-block one and
     the persistent one of csrc/dense_gc1.hip (GCNK_HUBFACTOR=persistent, read
-    per launch)."""
+    per launch); and S_T given as K-slabs (gcnk_gemm_kslabs_f32 ->
+    gcnk_hubfactor_gc1_slabs_f32, the slabs summed while staging)."""
     import ctypes
     import scipy.sparse as ssp
     from graph_convolutional_networks_for_text_classification_amd import factor, ops
-    monkeypatch.setenv("GCNK_HUBFACTOR", kernel)
+    monkeypatch.setenv("GCNK_HUBFACTOR", "legacy" if kernel == "slabs" else kernel)
     from graph_convolutional_networks_for_text_classification_amd.sparse import as_csr
     g = datasets.doc_topic_graph(ndoc, 40, 5, seed=4, tt_prob=0.3)
     A, X = g["adj"].to(DEV), g["features"].to(DEV)
@@ -1193,18 +1232,23 @@ def test_factored_gc1_kernel_against_float64(F, P, ndoc, kernel, monkeypatch):
     Z = Ad @ (Xd @ W1.cpu().double().numpy())
     lib = _lib.load()
 
-    S_T = f.hub_times(W1).contiguous()
+    if kernel == "slabs":
+        S_T, nslab = f.hub_slabs(W1)
+        assert nslab > 1
+    else:
+        S_T, nslab = f.hub_times(W1).contiguous(), 1
     stream = ctypes.c_void_p(torch.cuda.current_stream().cuda_stream)
 
     def launch(epi, store_h1=True):
-        """gcnk_hubfactor_gc1_f32 right after an LDS poison launch (as ops.hubfactor_gc1 calls it)."""
+        """gcnk_hubfactor_gc1_slabs_f32 right after an LDS poison launch (as ops.hubfactor_gc1 calls it)."""
         H1 = torch.empty((f.M, F), device=DEV) if store_h1 else None
         S2 = torch.empty((f.M, P), device=DEV)
         _lib.check(lib.gcnk_debug_poison_lds(0xFFFFFFFF, stream), "gcnk_debug_poison_lds")
         p = lambda t: ctypes.c_void_p(t.data_ptr()) if t is not None else None
-        _lib.check(lib.gcnk_hubfactor_gc1_f32(
-            f.M, F, f.Kc, f.H, P, p(f.U), f.U.stride(0), p(W1), F, f.k0, p(S_T), F, p(f.rec), f.rec_words, p(b1), epi,
-            None, 0, 1.0, 1.0, 0, 0, None, p(W2), P, p(H1), F, p(S2), P, stream), "gcnk_hubfactor_gc1_f32")
+        _lib.check(lib.gcnk_hubfactor_gc1_slabs_f32(
+            f.M, F, f.Kc, f.H, P, p(f.U), f.U.stride(0), p(W1), F, f.k0, p(S_T), F, nslab, f.H * F, p(f.rec),
+            f.rec_words, p(b1), epi, None, 0, 1.0, 1.0, 0, 0, None, p(W2), P, p(H1), F, p(S2), P, stream),
+            "gcnk_hubfactor_gc1_slabs_f32")
         return H1, S2
     for epi in (_lib.EPI_NONE, _lib.EPI_BIAS, _lib.EPI_BIAS_RELU):
         H1, S2 = launch(epi)
@@ -1216,8 +1260,12 @@ def test_factored_gc1_kernel_against_float64(F, P, ndoc, kernel, monkeypatch):
         _close(S2, H1.cpu().double().numpy() @ W2.cpu().double().numpy(), atol=2e-5 * max(1.0, np.abs(want).max()))
     H1b, S2b = launch(_lib.EPI_BIAS_RELU, store_h1=False)
     assert H1b is None and torch.equal(S2b, S2)
-    H1c, S2c = ops.hubfactor_gc1(f, W1, b1, W2, epilogue=_lib.EPI_BIAS_RELU)   # the op wrapper: same bits
-    assert torch.equal(H1c, H1) and torch.equal(S2c, S2)
+    if kernel != "persistent":   # (the op wrapper takes factor.slabs' choice: the slab path by default)
+        H1c, S2c = ops.hubfactor_gc1(f, W1, b1, W2, epilogue=_lib.EPI_BIAS_RELU)
+        if (kernel == "slabs") == (f.slabs(F) > 1):   # same S_T form: same bits
+            assert torch.equal(H1c, H1) and torch.equal(S2c, S2)
+        else:
+            _close(H1c, H1.cpu().double().numpy(), atol=2e-5 * max(1.0, float(np.abs(want).max())))
 
 
 @pytest.mark.parametrize("mode", ["eval", "train_hash"])

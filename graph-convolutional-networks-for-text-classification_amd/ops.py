@@ -578,8 +578,12 @@ class GraphConvFn(torch.autograd.Function):
 
 # The factored forward's gW1 through the factor (factor.HubFactor.grad_w1:
 # A_H^T gZ1, X_hubs^T on the short-K GEMM, U^T gZ1 on the small-M GEMM) instead of
-# A-hat^T gZ1 at F then X^T gS1; GCNK_FACTOR_BWD=0 keeps the latter (A/B timing).
-FACTOR_BWD = os.environ.get("GCNK_FACTOR_BWD", "1") != "0"
+# A-hat^T gZ1 at F then X^T gS1.  Off by default (GCNK_FACTOR_BWD=1 turns it on):
+# in R8's replayed training step it took 8.1 + 7.3 + 14.8 = 30.2 us against
+# 8.5 + 9.4 + 4.9 = 22.8 for the latter (profiles/r05_train_trace.json) -- U^T gZ1
+# is the same [50 x 7724] x [7724 x 200] long-K product as X_hubs W1, with no
+# faster kernel for it.
+FACTOR_BWD = os.environ.get("GCNK_FACTOR_BWD", "0") == "1"
 
 
 # The whole forward from one C call (record.py, gcnk_gcn_forward_f32) wherever

@@ -335,7 +335,8 @@ def _get(adj, xop, F, P, device, cls, tag):
     it, so two graphs of the same record must not replay concurrently."""
     stream = torch.cuda.current_stream(device).cuda_stream
     src = xop.csr if xop.csr is not None else xop.dense
-    key = (tag, id(src), F, P, stream, ops.FACTOR_GC1, ops.FUSE_PROJECTION, ops.DENSE_AX)
+    key = (tag, id(src), F, P, stream, ops.FACTOR_GC1, ops.FUSE_PROJECTION, ops.DENSE_AX, ops.FACTOR_BWD,
+           factor.XHUB)
     recs = getattr(adj, "_records", None)
     if recs is None:
         with _lock:

@@ -1157,15 +1157,19 @@ def test_tile_path_repeat_streams_and_graph_replay_are_exact(r8, dense, monkeypa
 
 # ------------------------------------------------------------------------------ hub-factored gc1
 
+@pytest.mark.parametrize("factor_bwd", [False, True])
 @pytest.mark.parametrize("mode", ["eval", "train_mask", "train_hash"])
-def test_factored_gc1_matches_spmm_path(r8, mode):
+def test_factored_gc1_matches_spmm_path(r8, mode, factor_bwd, monkeypatch):
     """GCN.forward through the hub factorisation (factor.py + gcnk_hubfactor_gc1_f32:
     A-hat X W1 as U W1[Kc] + A_H (X_hubs W1)) against the SpMM path
     (ops.FACTOR_GC1 = False: X W1 then A-hat S1, layer.py:102,106) on R8 with
     the same weights and the same dropout masks: logits and every gradient
     within fp32 reassociation error; H1 kept for the backward only when
-    needed; the factored launch bitwise reproducible."""
+    needed; the factored launch bitwise reproducible.  The backward both ways:
+    gW1 through A-hat^T gZ1 and X^T gS1, and through the factor (ops.FACTOR_BWD:
+    A_H^T gZ1, X_hubs^T, U^T gZ1)."""
     from graph_convolutional_networks_for_text_classification_amd import factor, ops
+    monkeypatch.setattr(ops, "FACTOR_BWD", factor_bwd)
     X, A = r8["features"].to(DEV), r8["adj"].to(DEV)
     from graph_convolutional_networks_for_text_classification_amd.sparse import as_csr
     f = factor.get(as_csr(A), ops.Operand(X))
@@ -1213,6 +1217,8 @@ def test_factored_gc1_kernel_against_float64(F, P, ndoc, kernel, monkeypatch):
     import scipy.sparse as ssp
     from graph_convolutional_networks_for_text_classification_amd import factor, ops
     monkeypatch.setenv("GCNK_HUBFACTOR", "legacy" if kernel == "slabs" else kernel)
+    if kernel == "slabs":   # (the factor built below keeps a dense copy of X's hub rows)
+        monkeypatch.setattr(factor, "XHUB", "slabs")
     from graph_convolutional_networks_for_text_classification_amd.sparse import as_csr
     g = datasets.doc_topic_graph(ndoc, 40, 5, seed=4, tt_prob=0.3)
     A, X = g["adj"].to(DEV), g["features"].to(DEV)

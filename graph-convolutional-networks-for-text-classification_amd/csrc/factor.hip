@@ -82,7 +82,10 @@ __host__ __device__ constexpr int region1_floats(int F, int ntq) {
   return (4 * KS * F + bpad(F, ntq)) > kRB * (64 * ntq + 4) ? (4 * KS * F + bpad(F, ntq)) : kRB * (64 * ntq + 4);
 }
 
-template <int KS, int NTQ, int NP>
+// SLB: S_T arrives as K-slabs (a separate instantiation: the staging registers
+// of the slab path cost the one-slab kernel ~1.2 us at R8's shape when they
+// were merely present, 64 -> 102 VGPRs)
+template <int KS, int NTQ, int NP, bool SLB>
 __global__ void __launch_bounds__(kThreads)
 hubfactor_gc1_kernel(FactorArgs a) {
   extern __shared__ __attribute__((aligned(16))) float smem[];
@@ -137,11 +140,12 @@ hubfactor_gc1_kernel(FactorArgs a) {
   // loads: slot i holds slab 1 + i / per, piece i % per (piece p = float4
   // tid + 512 p of the flat [nhub x F]); the host keeps (nslab - 1) per <= kSlabRegs
   const int per = (a.nhub * Q + kThreads - 1) / kThreads;
-  float4 sv[kSlabRegs];
+  constexpr int kSR = SLB ? kSlabRegs : 1;
+  float4 sv[kSR];
 #pragma unroll
-  for (int i = 0; i < kSlabRegs; ++i) {
+  for (int i = 0; i < kSR; ++i) {
     const int j = 1 + i / per, e = tid + kThreads * (i % per);
-    sv[i] = (j < a.nslab && e < a.nhub * Q)
+    sv[i] = (SLB && j < a.nslab && e < a.nhub * Q)
                 ? *reinterpret_cast<const float4*>(a.S + j * a.slab_stride + 4 * (int64_t)e)
                 : make_float4(0.f, 0.f, 0.f, 0.f);
   }
@@ -156,9 +160,9 @@ hubfactor_gc1_kernel(FactorArgs a) {
   __syncthreads();
   // S_T = ((slab 0 + slab 1) + slab 2) + slab 3, each thread on its own pieces
   // (slots in slab order); phase 2 reads s_S only after the barriers below
-  if (a.nslab > 1) {
+  if (SLB && a.nslab > 1) {
 #pragma unroll
-    for (int i = 0; i < kSlabRegs; ++i) {
+    for (int i = 0; i < kSR; ++i) {
       const int j = 1 + i / per, e = tid + kThreads * (i % per);
       if (j < a.nslab && e < a.nhub * Q) {
         float4* d = reinterpret_cast<float4*>(s_S + 4 * e);
@@ -336,15 +340,21 @@ extern "C" int64_t gcnk_hubfactor_lds_bytes(int32_t F, int32_t Kc, int32_t nhub,
 
 // The dynamic-LDS limit is raised once per kernel instantiation and device
 // (dyn_lds_attr), then the launch.
-template <int KS, int NTQ, int NP>
-static int launch_factor(const FactorArgs& a, int64_t nblk, int64_t lds_b, void* stream) {
+template <int KS, int NTQ, int NP, bool SLB>
+static int launch_factor_s(const FactorArgs& a, int64_t nblk, int64_t lds_b, void* stream) {
   static std::atomic<uint64_t> done{0};
   const hipError_t attr =
-      dyn_lds_attr(done, reinterpret_cast<const void*>(&hubfactor_gc1_kernel<KS, NTQ, NP>), 160 * 1024);
+      dyn_lds_attr(done, reinterpret_cast<const void*>(&hubfactor_gc1_kernel<KS, NTQ, NP, SLB>), 160 * 1024);
   if (attr != hipSuccess) return hip_check(attr, "hubfactor_gc1_kernel LDS attribute");
-  hipLaunchKernelGGL((hubfactor_gc1_kernel<KS, NTQ, NP>), dim3((unsigned)nblk), dim3(kThreads), (size_t)lds_b,
+  hipLaunchKernelGGL((hubfactor_gc1_kernel<KS, NTQ, NP, SLB>), dim3((unsigned)nblk), dim3(kThreads), (size_t)lds_b,
                      reinterpret_cast<hipStream_t>(stream), a);
   return launch_check("hubfactor_gc1_kernel");
+}
+
+template <int KS, int NTQ, int NP>
+static int launch_factor(const FactorArgs& a, int64_t nblk, int64_t lds_b, void* stream) {
+  return a.nslab > 1 ? launch_factor_s<KS, NTQ, NP, true>(a, nblk, lds_b, stream)
+                     : launch_factor_s<KS, NTQ, NP, false>(a, nblk, lds_b, stream);
 }
 
 extern "C" int gcnk_hubfactor_gc1_slabs_f32(int32_t M, int32_t F, int32_t Kc, int32_t nhub, int32_t P,

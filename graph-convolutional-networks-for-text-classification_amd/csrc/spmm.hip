@@ -66,7 +66,8 @@ constexpr int kMaxSeg = 64;             // segments per heavy row (bounds the la
 // VGPRs, 4 waves/SIMD); 512-thread workgroups (8 waves per heavy segment): 10.7.
 // Write-through (sc1) output stores: the launch leaves no dirty output lines
 // in the XCD L2s for the kernel boundary to write back (R8 X W1: tile kernel
-// 13.2 -> 11.4 us in the forward, forward 36.4 -> 34.7 us).
+// 13.2 -> 11.4 us in the forward, forward 36.4 -> 34.7 us).  2: nontemporal
+// stores instead (experiment).
 #ifndef GCNK_TILE_SC1
 #define GCNK_TILE_SC1 1
 #endif
@@ -1068,7 +1069,9 @@ __device__ __forceinline__ void tile_body(int32_t bx, const int4* __restrict__ t
         v = make_float4(o[0], o[1], o[2], o[3]);
       }
     }
-#if GCNK_TILE_SC1
+#if GCNK_TILE_SC1 == 2   // (experiment: nontemporal stores)
+    store_nt(dst, v);
+#elif GCNK_TILE_SC1
     {
       const float* base = uniform_ptr(single ? C : slabs);
       const int64_t off = dst - base;

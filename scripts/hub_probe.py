@@ -81,6 +81,7 @@ def main():
     ap.add_argument("--widths", default="200,8")
     ap.add_argument("--graph", default="r8", choices=["r8", "20ng"])
     ap.add_argument("--ipc", default="", help="comma list of light-row limits to sweep (default: the library's)")
+    ap.add_argument("--lanes", default="0", help="comma list of lanes-per-row hints to sweep (0: the library's)")
     ap.add_argument("--mode", default="both", choices=["warm", "cold", "both"],
                     help="which timing graphs to run (one mode alone for a rocprofv3 kernel average)")
     args = ap.parse_args()
@@ -101,7 +102,10 @@ def main():
         Bs = [torch.from_numpy(Bh).to(dev) for _ in range(nsets)]
         Cs = [torch.empty(M, F, device=dev) for _ in range(nsets)]
         ipcs = [int(v) for v in args.ipc.split(",")] if args.ipc else [None]
-        for name, ipc in ((n, i) for n in args.variants.split(",") for i in (ipcs if n != "copy" else [None])):
+        lanes_l = [int(v) for v in args.lanes.split(",")]
+        for name, ipc, lanes in ((n, i, ln) for n in args.variants.split(",")
+                                 for i in (ipcs if n != "copy" else [None])
+                                 for ln in (lanes_l if n != "copy" else [0])):
             if name == "copy":
                 # the streaming floor of the same bytes: one float4 copy C = B
                 # (reads B once, writes C once: the op's compulsory traffic minus the CSR)
@@ -124,22 +128,23 @@ def main():
                 vref = csr_ref.spmm_epilogue(csr_ref.spmm_csr(srp, sci, sv, Bh), bias.cpu().numpy(), relu=True)
             else:
                 vref = ref
-            out = ops.spmm(a, Bs[0], bias=bias, epilogue=_lib.EPI_BIAS_RELU, ipc=ipc)
+            out = ops.spmm(a, Bs[0], bias=bias, epilogue=_lib.EPI_BIAS_RELU, ipc=ipc, lanes=lanes)
             torch.cuda.synchronize()
             err = float(np.abs(out.cpu().numpy().astype(np.float64) - vref).max())
-            again = ops.spmm(a, Bs[0], bias=bias, epilogue=_lib.EPI_BIAS_RELU, ipc=ipc)
+            again = ops.spmm(a, Bs[0], bias=bias, epilogue=_lib.EPI_BIAS_RELU, ipc=ipc, lanes=lanes)
             det = bool(torch.equal(out, again))
             plan = list(a._plans.values())[-1]
             warm = cold = float("nan")
             if args.mode in ("warm", "both"):
                 warm = time_graph([lambda: ops.spmm(a, Bs[0], bias=bias, epilogue=_lib.EPI_BIAS_RELU, out=Cs[0],
-                                                    ipc=ipc)], args.reps)
-            fns = [(lambda i=i: ops.spmm(a, Bs[i], bias=bias, epilogue=_lib.EPI_BIAS_RELU, out=Cs[i], ipc=ipc))
+                                                    ipc=ipc, lanes=lanes)], args.reps)
+            fns = [(lambda i=i: ops.spmm(a, Bs[i], bias=bias, epilogue=_lib.EPI_BIAS_RELU, out=Cs[i], ipc=ipc,
+                                         lanes=lanes))
                    for i in range(nsets)]
             if args.mode in ("cold", "both"):
                 cold = time_graph(fns, max(1, args.reps // nsets))
             vbytes = spmm_bytes(M, M, a.nnz, F)
-            print(json.dumps({"graph": args.graph, "F": F, "variant": name, "ipc": ipc, "nnz": a.nnz,
+            print(json.dumps({"graph": args.graph, "F": F, "variant": name, "ipc": ipc, "lanes": lanes, "nnz": a.nnz,
                               "hdr": plan.header, "max_err": err, "deterministic": det,
                               "warm_us": round(warm, 3), "cold_us": round(cold, 3),
                               "warm_frac": vbytes / (warm * 1e-6) / 8e12, "cold_frac": vbytes / (cold * 1e-6) / 8e12,

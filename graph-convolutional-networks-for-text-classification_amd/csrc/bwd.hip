@@ -38,6 +38,17 @@ constexpr int kBwdBatch = 8;       // rows per lane whose H1 loads are in flight
 #define GCNK_BWD_TARGET 256
 #endif
 constexpr int kBwdTarget = GCNK_BWD_TARGET;    // workgroups per slice (256: one per CU)
+// gZ1 store policy (experiment knob): 1 nontemporal, 0 plain, 2 sc1 write-through,
+// 3 none (timing only: gZ1 not written)
+#ifndef GCNK_BWD2_STAMPV   // stamps-build timeline variant (2: around the lane sum)
+#define GCNK_BWD2_STAMPV 1
+#endif
+#ifndef GCNK_BWD2_PEXP     // experiment: 1 no partial stores, 2 no gb2 loop, 3 no partial loop
+#define GCNK_BWD2_PEXP 0
+#endif
+#ifndef GCNK_BWD2_ZST
+#define GCNK_BWD2_ZST 1
+#endif
 
 template <int VEC>
 struct VecIO;
@@ -128,12 +139,25 @@ __global__ void __launch_bounds__(kBwdBlock) gcn_bwd2_kernel(Bwd2Args a) {
   }
   // this lane's columns of W2 (rows of W2: W2[n, :]).  (Issued before the
   // staging above instead: staging 2.7 -> 4.2 us, profiles/r04_bwd2_stamps_v2.log.)
+  // (W2 rows are ldw apart; with ldw == P == PM a lane's VEC rows are one run
+  // of VEC PM floats: 16-B loads instead of VEC PM 4-B loads 32 lanes apart)
   float w[VEC][PM];
+  if (a.ldw == PM && a.P == PM && (reinterpret_cast<uintptr_t>(a.W) & 15) == 0) {
 #pragma unroll
-  for (int v = 0; v < VEC; ++v)
+    for (int v = 0; v < VEC; ++v)
 #pragma unroll
-    for (int p = 0; p < PM; ++p)
-      w[v][p] = (act && c + v < a.N && p < a.P) ? a.W[(c + v) * a.ldw + p] : 0.f;
+      for (int p = 0; p < PM; p += 4) {
+        float4 q = make_float4(0.f, 0.f, 0.f, 0.f);
+        if (act && c + v < a.N) q = *reinterpret_cast<const float4*>(a.W + (c + v) * a.ldw + p);
+        w[v][p] = q.x; w[v][p + 1] = q.y; w[v][p + 2] = q.z; w[v][p + 3] = q.w;
+      }
+  } else {
+#pragma unroll
+    for (int v = 0; v < VEC; ++v)
+#pragma unroll
+      for (int p = 0; p < PM; ++p)
+        w[v][p] = (act && c + v < a.N && p < a.P) ? a.W[(c + v) * a.ldw + p] : 0.f;
+  }
   float gw[VEC][PM], gb[VEC];
 #pragma unroll
   for (int v = 0; v < VEC; ++v) {
@@ -142,7 +166,9 @@ __global__ void __launch_bounds__(kBwdBlock) gcn_bwd2_kernel(Bwd2Args a) {
     for (int p = 0; p < PM; ++p) gw[v][p] = 0.f;
   }
   __syncthreads();
+#if GCNK_BWD2_STAMPV != 2
   stamp(a.stamps, 1);
+#endif
 
   for (int32_t b0 = rl; b0 < nr; b0 += RL * kBwdBatch) {
     // the batch's H1 loads first (one latency; the first batch's are in flight
@@ -178,11 +204,21 @@ __global__ void __launch_bounds__(kBwdBlock) gcn_bwd2_kernel(Bwd2Args a) {
 #pragma unroll
         for (int p = 0; p < PM; ++p) gw[v][p] = fmaf(h[j][v], g[p], gw[v][p]);
       }
-      VecIO<VEC>::store_nt(a.Z + (int64_t)(r0 + rr) * a.ldz + c, z);
+      if (GCNK_BWD2_ZST == 1) VecIO<VEC>::store_nt(a.Z + (int64_t)(r0 + rr) * a.ldz + c, z);
+      else if (GCNK_BWD2_ZST == 0) VecIO<VEC>::store(a.Z + (int64_t)(r0 + rr) * a.ldz + c, z);
+      else if (GCNK_BWD2_ZST == 3) { if (z[0] == 1234.5f) a.Z[0] = z[VEC - 1]; }
+      else
+#pragma unroll
+        for (int v = 0; v < VEC; ++v)
+          __hip_atomic_store(a.Z + (int64_t)(r0 + rr) * a.ldz + c + v, z[v], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
     }
   }
 
+#if GCNK_BWD2_STAMPV == 2
+  stamp(a.stamps, 1);   // (variant timeline: 1 rows done, 2 after the lane-sum barrier, 3 partial stored)
+#else
   stamp(a.stamps, 2);
+#endif
   // row lanes -> one partial per column, summed in lane order
   {
     float* mine = s_red + tid * KE;
@@ -194,37 +230,42 @@ __global__ void __launch_bounds__(kBwdBlock) gcn_bwd2_kernel(Bwd2Args a) {
     }
   }
   __syncthreads();
+#if GCNK_BWD2_STAMPV == 2
+  stamp(a.stamps, 2);
+#endif
   float* prow = a.part + (int64_t)blockIdx.x * a.part_ld;
-  for (int e = tid; e < CT * KE; e += kBwdBlock) {
+  for (int e = tid; e < (GCNK_BWD2_PEXP == 3 ? 0 : CT * KE); e += kBwdBlock) {
     const int u = e / KE, k = e % KE;
     const int v = k / (PM + 1), p = k % (PM + 1);
     const int64_t col = (int64_t)(cu0 + u) * VEC + v;
     // the row lanes' values eight at a time (loads together), added in lane order
     float s = 0.f;
+    // (clamped reads and selected adds: no branch per read, all eight in flight
+    // behind one wait -- the guarded form compiled to a branch per read and took
+    // ~2 us at R8's shape)
     for (int l0 = 0; l0 < RL; l0 += 8) {
       float rv[8];
 #pragma unroll
-      for (int j = 0; j < 8; ++j) rv[j] = l0 + j < RL ? s_red[((l0 + j) * CT + u) * KE + k] : 0.f;
+      for (int j = 0; j < 8; ++j) rv[j] = s_red[(min(l0 + j, RL - 1) * CT + u) * KE + k];
 #pragma unroll
-      for (int j = 0; j < 8; ++j)
-        if (l0 + j < RL) s += rv[j];
+      for (int j = 0; j < 8; ++j) s = l0 + j < RL ? s + rv[j] : s;
     }
     if (col >= a.N) continue;
+    if (GCNK_BWD2_PEXP == 1) { if (s == 1234.5f) prow[0] = s; continue; }
     if (p < PM) {
       if (p < a.P) prow[col * a.P + p] = s;
     } else {
       prow[(int64_t)a.N * a.P + col] = s;
     }
   }
-  if (with_g && tid < a.P) {  // gb2: the G rows, in row order (eight LDS reads in flight)
+  if (GCNK_BWD2_PEXP != 2 && with_g && tid < a.P) {  // gb2: the G rows, in row order (eight LDS reads in flight)
     float s = 0.f;
-    for (int r8 = 0; r8 < nr; r8 += 8) {
-      float gv[8];
+    for (int r8 = 0; r8 < nr; r8 += 16) {
+      float gv[16];
 #pragma unroll
-      for (int j = 0; j < 8; ++j) gv[j] = r8 + j < nr ? s_gg[(r8 + j) * PM + tid] : 0.f;
+      for (int j = 0; j < 16; ++j) gv[j] = s_gg[min(r8 + j, nr - 1) * PM + tid];
 #pragma unroll
-      for (int j = 0; j < 8; ++j)
-        if (r8 + j < nr) s += gv[j];
+      for (int j = 0; j < 16; ++j) s = r8 + j < nr ? s + gv[j] : s;
     }
     prow[(int64_t)a.N * a.P + a.N + tid] = s;
   }

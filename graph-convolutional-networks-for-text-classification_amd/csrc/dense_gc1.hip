@@ -85,6 +85,7 @@ constexpr int a_stride(int ks) { return 64 * ((4 * ks - 4 + 63) / 64) + 4; }
 template <int KS, int NP, bool HUB>
 __global__ void __launch_bounds__(kThreads, HUB ? 1 : 2)
 dense_gc1_kernel(DenseArgs a) {
+  resolve_rng(a.epi);
   constexpr int KP = a_stride(KS);
   constexpr int kAPer = (16 * 4 * KS + kThreads - 1) / kThreads;   // A-tile elements per thread
   __shared__ __attribute__((aligned(16))) float s_A[2][16 * KP];

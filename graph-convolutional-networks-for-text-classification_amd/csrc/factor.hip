@@ -88,6 +88,7 @@ __host__ __device__ constexpr int region1_floats(int F, int ntq) {
 template <int KS, int NTQ, int NP, bool SLB>
 __global__ void __launch_bounds__(kThreads)
 hubfactor_gc1_kernel(FactorArgs a) {
+  resolve_rng(a.epi);
   extern __shared__ __attribute__((aligned(16))) float smem[];
   const int tid = threadIdx.x, lane = tid & 63;
   const int wv = __builtin_amdgcn_readfirstlane(tid >> 6);

@@ -116,6 +116,17 @@ __device__ __forceinline__ float apply_epi(const Epi& e, float acc, float b, int
   return u < e.keep_prob ? v * e.scale : 0.0f;
 }
 
+// A hash-dropout epilogue's device stream offset (*rng_base), read ONCE at a
+// kernel's entry and folded into offset: apply_epi reading it per element put a
+// dependent global load in front of every kept / dropped decision (behind the
+// epilogue's own stores, so the compiler could not reuse it).
+__device__ __forceinline__ void resolve_rng(Epi& e) {
+  if (e.code == GCNK_EPI_BIAS_RELU_HASH && e.rng_base) {
+    e.offset += *e.rng_base;
+    e.rng_base = nullptr;
+  }
+}
+
 // Column vectors of a lane: VEC = 4 (float4, 16-B accesses) or 1 (scalar).
 template <int VEC>
 struct Vec;

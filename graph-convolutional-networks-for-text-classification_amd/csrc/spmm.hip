@@ -617,6 +617,7 @@ __global__ void __launch_bounds__(BLOCK) __attribute__((amdgpu_waves_per_eu(LPR 
 spmm_row_kernel(RowPlan rp, int32_t nhb, const float* __restrict__ B, int64_t ldb, int32_t F,
                 float* __restrict__ C, int64_t ldc, Epi epi, float* __restrict__ part, int64_t part_ld,
                 ProjArgs pa) {
+  resolve_rng(epi);
   using V = Vec<VEC>;
   using T = typename V::T;
   constexpr int SG = BLOCK / LPR;  // lane groups per workgroup
@@ -1091,6 +1092,7 @@ spmm_tile_kernel(const int4* __restrict__ tdesc, const int32_t* __restrict__ tco
                  const int32_t* __restrict__ trows, const float* __restrict__ dval, int32_t F,
                  const float* __restrict__ B, int64_t ldb, float* __restrict__ C, int64_t ldc, Epi epi,
                  float* __restrict__ slabs, int64_t slab_ld, int32_t item0, int32_t nitems, int32_t nslices) {
+  resolve_rng(epi);
   tile_body<VEC4, NT, DIAG>((int32_t)blockIdx.x, tdesc, tcols, tfrag, trows, dval, F, B, ldb, C, ldc, epi, slabs,
                             slab_ld, item0, nitems, nslices);
 }
@@ -1162,6 +1164,7 @@ __device__ __forceinline__ void reduce_body(int32_t bx, int32_t by, int32_t bz, 
 __global__ void __launch_bounds__(256)
 spmm_tile_reduce_kernel(const int4* __restrict__ red, int32_t F, const float* __restrict__ slabs, int64_t slab_ld,
                         const float* __restrict__ B, int64_t ldb, float* __restrict__ C, int64_t ldc, Epi epi) {
+  resolve_rng(epi);
   reduce_body((int32_t)blockIdx.x, (int32_t)blockIdx.y, (int32_t)blockIdx.z, red, F, slabs, slab_ld, B, ldb, C, ldc,
               epi);
 }

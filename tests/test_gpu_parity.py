@@ -704,6 +704,47 @@ def test_gcn_gensim_shaped_r8_forward_backward(r8):
                                    atol=1e-4 * max(1.0, float(q.grad.abs().max())), err_msg=k)
 
 
+@pytest.mark.parametrize("nhid", [50, 36, 300])
+@pytest.mark.parametrize("gensim", [False, True])
+def test_gcn_hidden_widths_outside_the_fused_kernels(r8, nhid, gensim):
+    """GCN widths the fused / factored / narrow-feature kernels refuse (nhid % 4
+    != 0 -- no 16-B rows -- or nhid > 256): the forward record falls back to the
+    SpMM + GEMM launches (a record must never pick a kernel that then
+    refuses), on R8's X and on the gensim-shaped 100-d X.  Eval logits and a
+    train-mode step's gradients (reference CPU dropout stream) against the
+    oracle's torch-CPU restatement of layer.py."""
+    if gensim:
+        X = _gensim_r8_x(r8)
+        Xs = datasets.dense_to_coo(X)
+        nfeat = 100
+    else:
+        Xs, nfeat = r8["features"], r8["nfeat"]
+    torch.manual_seed(nhid)
+    m = GCN(nfeat=nfeat, nhid=nhid, nclass=r8["nclass"], dropout=0.5).to(DEV)
+    ref = gcn_ref.RefGCN(nfeat=nfeat, nhid=nhid, nclass=r8["nclass"], dropout=0.5)
+    ref.load_state_dict({k: v.cpu() for k, v in m.state_dict().items()})
+    m.eval()
+    ref.eval()
+    with torch.no_grad():
+        lg = m(Xs.to(DEV), r8["adj"].to(DEV)).cpu().numpy()
+        again = m(Xs.to(DEV), r8["adj"].to(DEV)).cpu().numpy()
+        want = ref(Xs, r8["adj"]).numpy()
+    assert np.abs(lg - want).max() <= LOGIT_TOL * max(1.0, float(np.abs(want).max()))
+    assert np.array_equal(lg, again)
+    m.train()
+    ref.train()
+    torch.manual_seed(11)
+    out = m(Xs.to(DEV), r8["adj"].to(DEV))
+    torch.manual_seed(11)
+    out_ref = ref(Xs, r8["adj"])
+    assert float((out.detach().cpu() - out_ref.detach()).abs().max()) <= \
+        LOGIT_TOL * max(1.0, float(out_ref.detach().abs().max()))
+    out.square().sum().backward()
+    out_ref.square().sum().backward()
+    for (k, p), (_, q) in zip(m.named_parameters(), ref.named_parameters()):
+        _grads_close(p.grad.cpu().numpy(), q.grad.numpy(), k)
+
+
 def test_gcn_dense_features_path(r8, golden_logits):
     """Dense infeatn (th.spmm falls through to mm) -> MFMA GEMM path."""
     torch.manual_seed(0)

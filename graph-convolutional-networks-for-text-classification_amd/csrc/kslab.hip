@@ -27,7 +27,7 @@ typedef float f32x4 __attribute__((ext_vector_type(4)));
 
 constexpr int kWaves = 8;
 constexpr int kThreads = 64 * kWaves;
-constexpr int kMaxSlabs = 4;
+constexpr int kMaxSlabs = 64;   // (gcnk_hubfactor_gc1_slabs_f32 sums at most 4 of them)
 
 template <int CPW>
 __global__ void __launch_bounds__(kThreads)

@@ -282,7 +282,7 @@ int gcnk_hubfactor_gc1_slabs_f32(int32_t M, int32_t F, int32_t Kc, int32_t nhub,
                                  float* C2, int64_t ldc2, void* stream);
 /* S_T's K-slabs for the above (csrc/kslab.hip; X_hubs W1, reference layer.py:102
  * on the topic rows): C + s slab_stride = A[:, K_s] B[K_s, :] for s < nslab
- * (1-4), K cut into 16-deep chunks and slab s owning chunks [s cps, (s+1) cps),
+ * (1-64; the factored gc1 sums at most 4), K cut into 16-deep chunks and slab s owning chunks [s cps, (s+1) cps),
  * cps = ceil(ceil(K / 16) / nslab).  No reduction launch and no hand-off: the
  * consumer sums the slabs.  A: 16-B aligned rows (lda % 4 == 0).  Fixed-order
  * sums: bitwise reproducible.  GCNK_EUNSUP past K = 3072 nslab. */

@@ -63,6 +63,7 @@ ROOT = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, ROOT)
 
 HBM_PEAK_GBS = 8000.0   # MI355X HBM3E spec (MI355X_MICROARCH.md)
+FP32_MFMA_PEAK_TFLOPS = 157.3   # dense fp32-input MFMA (= the fp32 vector rate), MI355X_MICROARCH.md
 MALL_BYTES = 256 * 1024 * 1024
 
 
@@ -300,9 +301,11 @@ def labelled_forward_kernels(save_dir, graph, a_csr, x, N, nfeat, nnz_a, nnz_x, 
     dense_x = ops.Operand(x).dense is not None
     path = forward_path(a_csr, x, nhid, nclass)
     a_s2 = spmm_bytes(N, N, nnz_a, nclass)
+    flops = {}   # the MFMA-bound ops' useful fp32 FLOPs (fraction of the fp32 MFMA peak beside the HBM one)
     if path == "dense-ax":
         # one launch: A-hat X [N x nfeat] (cached), W1, b1, W2 read; S2 written
         alg = {"AX W1 + H1 W2": 4 * (N * nfeat + nfeat * nhid + nhid + nhid * nclass + N * nclass), "A S2": a_s2}
+        flops = {"AX W1 + H1 W2": 2 * N * (nfeat * nhid + nhid * nclass)}
     elif path == "factored":
         fac = _factored(a_csr, x)
         # X[hubs] W1 (dense hub rows on the one-pass small-M GEMM, or their CSR),
@@ -313,6 +316,9 @@ def labelled_forward_kernels(save_dir, graph, a_csr, x, N, nfeat, nnz_a, nnz_x, 
                "A X W1 factored + H1 W2": (4 * fac.U.numel() + 4 * fac.rec.numel() + 4 * fac.Kc * nhid
                                             + 4 * fac.H * nhid + 4 * nhid * nclass + 4 * N * nclass),
                "A S2": a_s2}
+        flops = {"X_hubs W1": 2 * fac.H * nfeat * nhid,
+                 "A X W1 factored + H1 W2": 2 * N * (fac.Kc * nhid + nhid * nclass)
+                 + 2 * nhid * (fac.rec.numel() - 68 * fac.nblk) // 2}   # (+ the A_H items: 2 words each)
     else:
         fused = path == "spmm+proj"
         alg = {   # dense X (gensim-shaped): the GEMM's operands once; sparse X: the CSR SpMM formula
@@ -343,10 +349,14 @@ def labelled_forward_kernels(save_dir, graph, a_csr, x, N, nfeat, nnz_a, nnz_x, 
             if e["op"] == key:
                 e.update({"op_us": round(us, 3), "algorithmic_bytes": nb,
                           "frac": nb / (us * 1e-6) / 1e9 / HBM_PEAK_GBS if us > 0 else None})
+                if key in flops and us > 0:
+                    e.update({"flops": flops[key], "tflops": flops[key] / (us * 1e-6) / 1e12,
+                              "mfma_frac": flops[key] / (us * 1e-6) / 1e12 / FP32_MFMA_PEAK_TFLOPS})
     per_op = {}
     for e in ks:
         per_op.setdefault(e["op"], {"op_us": e.get("op_us"), "algorithmic_bytes": e.get("algorithmic_bytes"),
-                                    "frac": e.get("frac"), "kernels": []})["kernels"].append(e["kernel"][:60])
+                                    "frac": e.get("frac"), "tflops": e.get("tflops"), "mfma_frac": e.get("mfma_frac"),
+                                    "kernels": []})["kernels"].append(e["kernel"][:60])
     return {"source": trace_src, "path": path, "x_operand": "dense" if dense_x else "csr",
             "forward_span_us": trace["forward_span_us_median"], "kernels": ks, "ops": per_op}
 

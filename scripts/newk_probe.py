@@ -21,7 +21,7 @@ sys.path.insert(0, os.path.join(ROOT, "scripts"))
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--reps", type=int, default=200)
-    ap.add_argument("--ops", default="smallm,dense20,dense8", help="subset of smallm,dense20,dense8")
+    ap.add_argument("--ops", default="smallm,dense20,dense8", help="subset of smallm,dense20,dense8,densem (M sweep at K 100, F 200, P 20)")
     args = ap.parse_args()
     import torch
     import gcn_amd  # noqa: F401
@@ -60,7 +60,9 @@ def smallm(torch, ops, time_graph, g, dev, line, reps):
 
 def dense(torch, _lib, lib, time_graph, g, dev, line, reps, ops_sel):
     p = lambda t: ctypes.c_void_p(t.data_ptr())
-    for name, (M, K, F, P) in (("dense20", (18916, 100, 200, 20)), ("dense8", (7724, 100, 200, 8))):
+    cases = [("dense20", (18916, 100, 200, 20)), ("dense8", (7724, 100, 200, 8))]
+    cases += [("densem", (m, 100, 200, 20)) for m in (8192, 16384, 16400, 18916, 24576)]
+    for name, (M, K, F, P) in cases:
         if name not in ops_sel:
             continue
         AX = torch.zeros((M, K)).normal_(generator=g).to(dev)

@@ -74,6 +74,12 @@ struct FactorArgs {
   Epi epi;
 };
 
+// 1 (default): the item loop skips the last column slot where it lies past F
+// (R8: hubfactor_gc1 10.09 -> 9.78 us, profiles/r05_factor_lastu.log)
+#ifndef GCNK_FACTOR_LASTU
+#define GCNK_FACTOR_LASTU 1
+#endif
+
 // float4 registers per thread for S_T's K-slabs past the first
 constexpr int kSlabRegs = 16;
 
@@ -222,7 +228,14 @@ hubfactor_gc1_kernel(FactorArgs a) {
       const float* srow = s_S + p.x * F + 4 * c16;
       float4 sv[NTQ];
 #pragma unroll
-      for (int u = 0; u < NTQ; ++u) sv[u] = *reinterpret_cast<const float4*>(srow + 64 * u);
+      for (int u = 0; u < NTQ; ++u) {
+#if GCNK_FACTOR_LASTU
+        // the last column slot only where it lies inside F (R8: 2 of 16 lanes):
+        // inactive lanes move no LDS bytes, and this loop is LDS-bandwidth-bound
+        if (u == NTQ - 1 && c16 + 16 * u >= Q) { sv[u] = make_float4(0.f, 0.f, 0.f, 0.f); continue; }
+#endif
+        sv[u] = *reinterpret_cast<const float4*>(srow + 64 * u);
+      }
 #pragma unroll
       for (int u = 0; u < NTQ; ++u) Vec<4>::fma(z[u], v, sv[u]);
     }

@@ -80,6 +80,12 @@ struct FactorArgs {
 #define GCNK_FACTOR_LASTU 1
 #endif
 
+// experiment knob (variant builds only): 1 no W1[Kc] DMA, U loads or U W1 MFMAs,
+// 2 no U W1 MFMAs (wrong values: timing only; profiles/r05_factor_zp_ab.log)
+#ifndef GCNK_FACTOR_EXP
+#define GCNK_FACTOR_EXP 0
+#endif
+
 // float4 registers per thread for S_T's K-slabs past the first
 constexpr int kSlabRegs = 16;
 
@@ -128,7 +134,7 @@ hubfactor_gc1_kernel(FactorArgs a) {
   {
     const int n4 = a.Kc * Q;  // float4 pieces of W1[k0 .. k0 + Kc) (rows of F floats, ldw == F)
     const float* wsrc = a.W + (int64_t)a.k0 * a.ldw;
-    for (int e0 = wv * 64; e0 < n4; e0 += kThreads)
+    for (int e0 = wv * 64; e0 < (GCNK_FACTOR_EXP == 1 ? 0 : n4); e0 += kThreads)
       if (e0 + lane < n4) lds_dma16(wsrc + 4 * (e0 + lane), s_B + 4 * e0);
     const int32_t* rec = a.rec + (int64_t)blk * a.rec_words;
     for (int e0 = wv * 64; e0 < a.rec_words / 4; e0 += kThreads)
@@ -161,7 +167,8 @@ hubfactor_gc1_kernel(FactorArgs a) {
     const int64_t row = m0 + 16 * strip + (lane & 15);
     const float* up = a.U + row * a.ldu + (lane >> 4);
 #pragma unroll
-    for (int s = 0; s < KS; ++s) af[s] = (row < a.M && 4 * s + (lane >> 4) < a.Kc) ? up[4 * s] : 0.f;
+    for (int s = 0; s < KS; ++s)
+      af[s] = (GCNK_FACTOR_EXP != 1 && row < a.M && 4 * s + (lane >> 4) < a.Kc) ? up[4 * s] : 0.f;
   }
   __builtin_amdgcn_s_waitcnt(0x0F70);  // vmcnt(0): this wave's DMA and fragment loads have landed
   __syncthreads();
@@ -187,7 +194,7 @@ hubfactor_gc1_kernel(FactorArgs a) {
   for (int i = 0; i < NTQ; ++i) acc[i] = f32x4{0.f, 0.f, 0.f, 0.f};
   const int c0 = quarter * NTQ * 16 + (lane & 15);
 #pragma unroll
-  for (int s = 0; s < KS; ++s) {
+  for (int s = 0; s < (GCNK_FACTOR_EXP ? 0 : KS); ++s) {
     const float* br = s_B + (4 * s + (lane >> 4)) * F + c0;
     float bf[NTQ];
 #pragma unroll

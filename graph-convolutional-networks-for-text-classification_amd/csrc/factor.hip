@@ -69,6 +69,7 @@ struct FactorArgs {
   int32_t nslab; int64_t slab_stride;   // (csrc/kslab.hip; slabs past the first summed after the DMA wait)
   const int32_t* rec; int32_t rec_words;  // per 32-row block: off[33] | pad | row ids | items int2 {hub, val}
   const float* W2; int64_t ldw2;        // [F x P]
+  int32_t u_lds;                        // 1: the block's U rows staged in LDS by 16-B DMA (ldu % 4 == 0, aligned)
   float* H; int64_t ldh;                // nullable
   float* C2; int64_t ldc2;              // [M x P]
   Epi epi;
@@ -81,9 +82,14 @@ struct FactorArgs {
 #endif
 
 // experiment knob (variant builds only): 1 no W1[Kc] DMA, U loads or U W1 MFMAs,
-// 2 no U W1 MFMAs (wrong values: timing only; profiles/r05_factor_zp_ab.log)
+// 2 no U W1 MFMAs, 3 no U loads (wrong values: timing only; profiles/r05_factor_zp_ab.log)
 #ifndef GCNK_FACTOR_EXP
 #define GCNK_FACTOR_EXP 0
+#endif
+
+// 1 (default): U's rows staged in LDS by DMA where the block's LDS allows
+#ifndef GCNK_FACTOR_ULDS
+#define GCNK_FACTOR_ULDS 1
 #endif
 
 // float4 registers per thread for S_T's K-slabs past the first
@@ -124,6 +130,10 @@ hubfactor_gc1_kernel(FactorArgs a) {
   float* s_bias = s_W2 + ((F * a.P + 3) & ~3);
   int32_t* s_rec = reinterpret_cast<int32_t*>(s_bias + F);
   float* s_red = reinterpret_cast<float*>(s_rec + a.rec_words);
+  // u_lds: U's 32 rows [kRB][KPU] after s_red; row stride = 4 (mod 64), so lane
+  // (row c, quadrant q) reading k = 4 s + q hits bank 4 c + q (conflict-free)
+  constexpr int KPU = 64 * ((4 * KS - 4 + 63) / 64) + 4;
+  float* s_U = s_red + NP * 3 * 2 * 64 * 4;
 
   // ---- 0. loads, all issued before the first wait: zeros first (no LDS-DMA in
   //      flight yet), then LDS-DMA of W1[Kc] (flat) and the block's record, the
@@ -148,6 +158,12 @@ hubfactor_gc1_kernel(FactorArgs a) {
     if (a.epi.bias)
       for (int e0 = wv * 64; e0 < Q; e0 += kThreads)
         if (e0 + lane < Q) lds_dma16(a.epi.bias + 4 * (e0 + lane), s_bias + 4 * e0);
+    // U's rows by 16-B DMA (the per-lane fragment loads -- 16 rows x 16 B per
+    // instruction -- cost ~1.1 us of the block: profiles/r05_factor_zp_ab.log);
+    // one instruction per row, pieces covering Kc (inside the row: ldu % 4 == 0)
+    if (a.u_lds && GCNK_FACTOR_EXP != 1)
+      for (int r = wv; r < kRB; r += kThreads / 64)
+        if (m0 + r < a.M && 4 * lane < a.Kc) lds_dma16(a.U + (m0 + r) * a.ldu + 4 * lane, s_U + r * KPU);
   }
   // S_T's further K-slabs (csrc/kslab.hip) into registers in the same round of
   // loads: slot i holds slab 1 + i / per, piece i % per (piece p = float4
@@ -163,15 +179,24 @@ hubfactor_gc1_kernel(FactorArgs a) {
                 : make_float4(0.f, 0.f, 0.f, 0.f);
   }
   float af[KS];
-  {
-    const int64_t row = m0 + 16 * strip + (lane & 15);
-    const float* up = a.U + row * a.ldu + (lane >> 4);
+  const int64_t urow = m0 + 16 * strip + (lane & 15);
+  if (!a.u_lds) {
+    const float* up = a.U + urow * a.ldu + (lane >> 4);
 #pragma unroll
     for (int s = 0; s < KS; ++s)
-      af[s] = (GCNK_FACTOR_EXP != 1 && row < a.M && 4 * s + (lane >> 4) < a.Kc) ? up[4 * s] : 0.f;
+      af[s] = GCNK_FACTOR_EXP == 3 ? 1e-3f
+              : (GCNK_FACTOR_EXP != 1 && urow < a.M && 4 * s + (lane >> 4) < a.Kc) ? up[4 * s] : 0.f;
   }
   __builtin_amdgcn_s_waitcnt(0x0F70);  // vmcnt(0): this wave's DMA and fragment loads have landed
   __syncthreads();
+  if (a.u_lds) {   // (cells past Kc or past M were not written: selected away)
+    const float* su = s_U + (16 * strip + (lane & 15)) * KPU + (lane >> 4);
+#pragma unroll
+    for (int s = 0; s < KS; ++s) {
+      const float v = su[4 * s];
+      af[s] = (GCNK_FACTOR_EXP != 1 && urow < a.M && 4 * s + (lane >> 4) < a.Kc) ? v : 0.f;
+    }
+  }
   // S_T = ((slab 0 + slab 1) + slab 2) + slab 3, each thread on its own pieces
   // (slots in slab order); phase 2 reads s_S only after the barriers below
   if (SLB && a.nslab > 1) {
@@ -194,7 +219,7 @@ hubfactor_gc1_kernel(FactorArgs a) {
   for (int i = 0; i < NTQ; ++i) acc[i] = f32x4{0.f, 0.f, 0.f, 0.f};
   const int c0 = quarter * NTQ * 16 + (lane & 15);
 #pragma unroll
-  for (int s = 0; s < (GCNK_FACTOR_EXP ? 0 : KS); ++s) {
+  for (int s = 0; s < (GCNK_FACTOR_EXP == 1 || GCNK_FACTOR_EXP == 2 ? 0 : KS); ++s) {
     const float* br = s_B + (4 * s + (lane >> 4)) * F + c0;
     float bf[NTQ];
 #pragma unroll
@@ -354,6 +379,12 @@ static int64_t hubfactor_lds_bytes(int32_t F, int32_t Kc, int32_t nhub, int32_t 
   return 4 * (r1 + (int64_t)nhub * F + (((int64_t)F * P + 3) & ~3LL) + F + rec_words + pick_np(P) * 3 * 2 * 64 * 4);
 }
 
+// U's staged rows (u_lds): kRB rows of 4 KS floats at a stride of 4 (mod 64)
+static int64_t hubfactor_u_bytes(int32_t Kc) {
+  const int64_t ks = pick_ks(Kc);
+  return 4 * (int64_t)kRB * (64 * ((4 * ks - 4 + 63) / 64) + 4);
+}
+
 extern "C" int64_t gcnk_hubfactor_lds_bytes(int32_t F, int32_t Kc, int32_t nhub, int32_t rec_words, int32_t P) {
   if (F <= 0 || Kc <= 0 || nhub <= 0 || rec_words < kRecHead || P <= 0 || P > kProjMax) return GCNK_EARG;
   return hubfactor_lds_bytes(F, Kc, nhub, rec_words, P);
@@ -433,6 +464,9 @@ extern "C" int gcnk_hubfactor_gc1_slabs_f32(int32_t M, int32_t F, int32_t Kc, in
   }
   FactorArgs a;
   a.M = M; a.F = F; a.Kc = Kc; a.nhub = nhub; a.P = P;
+  // U's rows through LDS where they fit (R8: 95 + 8.7 KB; the 20ng-shaped 70
+  // topic-weight columns at 152 KB take the direct loads)
+  a.u_lds = GCNK_FACTOR_ULDS && ldu % 4 == 0 && aligned16(U) && lds_b + hubfactor_u_bytes(Kc) <= 160 * 1024;
   a.U = U; a.ldu = ldu; a.W = W; a.ldw = ldw; a.k0 = k0;
   a.S = S; a.lds = lds; a.rec = rec; a.rec_words = rec_words;
   a.nslab = nslab; a.slab_stride = slab_stride;
@@ -444,10 +478,11 @@ extern "C" int gcnk_hubfactor_gc1_slabs_f32(int32_t M, int32_t F, int32_t Kc, in
   e.ldm = epilogue == GCNK_EPI_BIAS_RELU_HASH ? (ldm > 0 ? ldm : F) : ldm;
   const int64_t nblk = ((int64_t)M + kRB - 1) / kRB;
   const int ks = pick_ks(Kc), ntq = pick_ntq(F), np = pick_np(P);
+  const int64_t lds_l = lds_b + (a.u_lds ? hubfactor_u_bytes(Kc) : 0);
 #define GCNK_FACTOR_CASE(KS_, NTQ_)                                                   \
   if (ks == KS_ && ntq == NTQ_)                                                       \
-    return np == 1 ? launch_factor<KS_, NTQ_, 1>(a, nblk, lds_b, stream)              \
-                   : launch_factor<KS_, NTQ_, 2>(a, nblk, lds_b, stream);
+    return np == 1 ? launch_factor<KS_, NTQ_, 1>(a, nblk, lds_l, stream)              \
+                   : launch_factor<KS_, NTQ_, 2>(a, nblk, lds_l, stream);
   GCNK_FACTOR_CASE(13, 2) GCNK_FACTOR_CASE(13, 3) GCNK_FACTOR_CASE(13, 4)
   GCNK_FACTOR_CASE(18, 2) GCNK_FACTOR_CASE(18, 3) GCNK_FACTOR_CASE(18, 4)
   GCNK_FACTOR_CASE(25, 2) GCNK_FACTOR_CASE(25, 3) GCNK_FACTOR_CASE(25, 4)

@@ -141,29 +141,35 @@ hubfactor_gc1_kernel(FactorArgs a) {
   for (int e = a.Kc * F + tid; e < Kr * F + bpad(F, NTQ); e += kThreads) s_B[e] = 0.f;
   if (!a.epi.bias)
     for (int e = tid; e < F; e += kThreads) s_bias[e] = 0.f;
+  // (splitting these loads by wave role -- waves 0-3 phase 1's operands, the
+  // first barrier waiting only for those -- measured 9.28 against 9.35 us:
+  // profiles/r05_factor_ulds_ab.log; not kept)
+  const int gw = wv, gstride = kThreads;
   {
     const int n4 = a.Kc * Q;  // float4 pieces of W1[k0 .. k0 + Kc) (rows of F floats, ldw == F)
     const float* wsrc = a.W + (int64_t)a.k0 * a.ldw;
-    for (int e0 = wv * 64; e0 < (GCNK_FACTOR_EXP == 1 ? 0 : n4); e0 += kThreads)
+    for (int e0 = gw * 64; e0 < (GCNK_FACTOR_EXP == 1 ? 0 : n4); e0 += gstride)
       if (e0 + lane < n4) lds_dma16(wsrc + 4 * (e0 + lane), s_B + 4 * e0);
-    const int32_t* rec = a.rec + (int64_t)blk * a.rec_words;
-    for (int e0 = wv * 64; e0 < a.rec_words / 4; e0 += kThreads)
-      if (e0 + lane < a.rec_words / 4) lds_dma16(rec + 4 * (e0 + lane), s_rec + 4 * e0);
-    const int s4 = a.nhub * Q;  // S_T [nhub x F] flat (lds == F): its first K-slab
-    for (int e0 = wv * 64; e0 < s4; e0 += kThreads)
-      if (e0 + lane < s4) lds_dma16(a.S + 4 * (e0 + lane), s_S + 4 * e0);
-    const int w1 = F * a.P;     // W2 [F x P] flat (ldw2 == P), dword pieces
-    for (int e0 = wv * 64; e0 < w1; e0 += kThreads)
-      if (e0 + lane < w1) lds_dma4(a.W2 + e0 + lane, s_W2 + e0);
-    if (a.epi.bias)
-      for (int e0 = wv * 64; e0 < Q; e0 += kThreads)
-        if (e0 + lane < Q) lds_dma16(a.epi.bias + 4 * (e0 + lane), s_bias + 4 * e0);
     // U's rows by 16-B DMA (the per-lane fragment loads -- 16 rows x 16 B per
-    // instruction -- cost ~1.1 us of the block: profiles/r05_factor_zp_ab.log);
+    // instruction -- cost ~1.1 us of the block: profiles/r05_factor_ulds_ab.log);
     // one instruction per row, pieces covering Kc (inside the row: ldu % 4 == 0)
     if (a.u_lds && GCNK_FACTOR_EXP != 1)
-      for (int r = wv; r < kRB; r += kThreads / 64)
+      for (int r = gw; r < kRB; r += gstride / 64)
         if (m0 + r < a.M && 4 * lane < a.Kc) lds_dma16(a.U + (m0 + r) * a.ldu + 4 * lane, s_U + r * KPU);
+    {
+      const int32_t* rec = a.rec + (int64_t)blk * a.rec_words;
+      for (int e0 = gw * 64; e0 < a.rec_words / 4; e0 += gstride)
+        if (e0 + lane < a.rec_words / 4) lds_dma16(rec + 4 * (e0 + lane), s_rec + 4 * e0);
+      const int s4 = a.nhub * Q;  // S_T [nhub x F] flat (lds == F): its first K-slab
+      for (int e0 = gw * 64; e0 < s4; e0 += gstride)
+        if (e0 + lane < s4) lds_dma16(a.S + 4 * (e0 + lane), s_S + 4 * e0);
+      const int w1 = F * a.P;     // W2 [F x P] flat (ldw2 == P), dword pieces
+      for (int e0 = gw * 64; e0 < w1; e0 += gstride)
+        if (e0 + lane < w1) lds_dma4(a.W2 + e0 + lane, s_W2 + e0);
+      if (a.epi.bias)
+        for (int e0 = gw * 64; e0 < Q; e0 += gstride)
+          if (e0 + lane < Q) lds_dma16(a.epi.bias + 4 * (e0 + lane), s_bias + 4 * e0);
+    }
   }
   // S_T's further K-slabs (csrc/kslab.hip) into registers in the same round of
   // loads: slot i holds slab 1 + i / per, piece i % per (piece p = float4
@@ -193,8 +199,10 @@ hubfactor_gc1_kernel(FactorArgs a) {
     const float* su = s_U + (16 * strip + (lane & 15)) * KPU + (lane >> 4);
 #pragma unroll
     for (int s = 0; s < KS; ++s) {
-      const float v = su[4 * s];
-      af[s] = (GCNK_FACTOR_EXP != 1 && urow < a.M && 4 * s + (lane >> 4) < a.Kc) ? v : 0.f;
+      // bit mask, not a select: a select let the compiler sink each read into a
+      // branch with its own LDS wait (13 round trips)
+      const bool ok = GCNK_FACTOR_EXP != 1 && urow < a.M && 4 * s + (lane >> 4) < a.Kc;
+      af[s] = __int_as_float(__float_as_int(su[4 * s]) & (ok ? -1 : 0));
     }
   }
   // S_T = ((slab 0 + slab 1) + slab 2) + slab 3, each thread on its own pieces

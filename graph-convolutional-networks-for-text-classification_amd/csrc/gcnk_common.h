@@ -110,9 +110,12 @@ __device__ __forceinline__ float apply_epi(const Epi& e, float acc, float b, int
   v = v > 0.0f ? v : 0.0f;
   if (e.code == GCNK_EPI_BIAS_RELU) return v;
   if (e.code == GCNK_EPI_BIAS_RELU_DROP) return e.mask[row * e.ldm + col] ? v * e.scale : 0.0f;
-  // GCNK_EPI_BIAS_RELU_HASH
-  const uint64_t base = e.rng_base ? *e.rng_base : 0;
-  const float u = hash_uniform(e.seed_lo, e.seed_hi, base + e.offset + (uint64_t)(row * e.ldm + col));
+  // GCNK_EPI_BIAS_RELU_HASH: the device offset *rng_base was folded into offset
+  // at the kernel's entry (resolve_rng, every kernel with an Epi calls it).  Not
+  // read here: even guarded by rng_base != null, the read left an s_waitcnt
+  // vmcnt(0) on every element's path (the compiler cannot see resolve_rng
+  // nulled the pointer), serialising the epilogue's H1 stores behind it
+  const float u = hash_uniform(e.seed_lo, e.seed_hi, e.offset + (uint64_t)(row * e.ldm + col));
   return u < e.keep_prob ? v * e.scale : 0.0f;
 }
 

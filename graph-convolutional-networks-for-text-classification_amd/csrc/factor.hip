@@ -21,7 +21,8 @@
 // One workgroup = 32 rows (512 threads, 8 waves: 2 row strips x 4 quarters of the
 // F columns):
 //   0. every operand of the block in one round of loads: W1[Kc] and S_T into LDS,
-//      the block's U fragments into registers, its A_H record and W2 into LDS;
+//      the block's U rows into LDS (16-B DMA; or its U fragments into registers),
+//      its A_H record and W2 into LDS;
 //   1. Z_strip = U_strip W1[Kc] on v_mfma_f32_16x16x4_f32 (exact fp32 FMA chains);
 //   2. Z through LDS to row-major; + A_H S_T, + b1, ReLU, dropout (mask or hash,
 //      the row kernel's epilogue); H1 stored only when a backward needs it;
@@ -136,40 +137,38 @@ hubfactor_gc1_kernel(FactorArgs a) {
   float* s_U = s_red + NP * 3 * 2 * 64 * 4;
 
   // ---- 0. loads, all issued before the first wait: zeros first (no LDS-DMA in
-  //      flight yet), then LDS-DMA of W1[Kc] (flat) and the block's record, the
-  //      U fragments straight into registers
+  //      flight yet), then LDS-DMA of W1[Kc] (flat), U's rows (u_lds; else the
+  //      U fragments straight into registers below), the block's record, S_T,
+  //      W2 and b1
   for (int e = a.Kc * F + tid; e < Kr * F + bpad(F, NTQ); e += kThreads) s_B[e] = 0.f;
   if (!a.epi.bias)
     for (int e = tid; e < F; e += kThreads) s_bias[e] = 0.f;
   // (splitting these loads by wave role -- waves 0-3 phase 1's operands, the
   // first barrier waiting only for those -- measured 9.28 against 9.35 us:
   // profiles/r05_factor_ulds_ab.log; not kept)
-  const int gw = wv, gstride = kThreads;
   {
     const int n4 = a.Kc * Q;  // float4 pieces of W1[k0 .. k0 + Kc) (rows of F floats, ldw == F)
     const float* wsrc = a.W + (int64_t)a.k0 * a.ldw;
-    for (int e0 = gw * 64; e0 < (GCNK_FACTOR_EXP == 1 ? 0 : n4); e0 += gstride)
+    for (int e0 = wv * 64; e0 < (GCNK_FACTOR_EXP == 1 ? 0 : n4); e0 += kThreads)
       if (e0 + lane < n4) lds_dma16(wsrc + 4 * (e0 + lane), s_B + 4 * e0);
     // U's rows by 16-B DMA (the per-lane fragment loads -- 16 rows x 16 B per
     // instruction -- cost ~1.1 us of the block: profiles/r05_factor_ulds_ab.log);
     // one instruction per row, pieces covering Kc (inside the row: ldu % 4 == 0)
     if (a.u_lds && GCNK_FACTOR_EXP != 1)
-      for (int r = gw; r < kRB; r += gstride / 64)
+      for (int r = wv; r < kRB; r += kThreads / 64)
         if (m0 + r < a.M && 4 * lane < a.Kc) lds_dma16(a.U + (m0 + r) * a.ldu + 4 * lane, s_U + r * KPU);
-    {
-      const int32_t* rec = a.rec + (int64_t)blk * a.rec_words;
-      for (int e0 = gw * 64; e0 < a.rec_words / 4; e0 += gstride)
-        if (e0 + lane < a.rec_words / 4) lds_dma16(rec + 4 * (e0 + lane), s_rec + 4 * e0);
-      const int s4 = a.nhub * Q;  // S_T [nhub x F] flat (lds == F): its first K-slab
-      for (int e0 = gw * 64; e0 < s4; e0 += gstride)
-        if (e0 + lane < s4) lds_dma16(a.S + 4 * (e0 + lane), s_S + 4 * e0);
-      const int w1 = F * a.P;     // W2 [F x P] flat (ldw2 == P), dword pieces
-      for (int e0 = gw * 64; e0 < w1; e0 += gstride)
-        if (e0 + lane < w1) lds_dma4(a.W2 + e0 + lane, s_W2 + e0);
-      if (a.epi.bias)
-        for (int e0 = gw * 64; e0 < Q; e0 += gstride)
-          if (e0 + lane < Q) lds_dma16(a.epi.bias + 4 * (e0 + lane), s_bias + 4 * e0);
-    }
+    const int32_t* rec = a.rec + (int64_t)blk * a.rec_words;
+    for (int e0 = wv * 64; e0 < a.rec_words / 4; e0 += kThreads)
+      if (e0 + lane < a.rec_words / 4) lds_dma16(rec + 4 * (e0 + lane), s_rec + 4 * e0);
+    const int s4 = a.nhub * Q;  // S_T [nhub x F] flat (lds == F): its first K-slab
+    for (int e0 = wv * 64; e0 < s4; e0 += kThreads)
+      if (e0 + lane < s4) lds_dma16(a.S + 4 * (e0 + lane), s_S + 4 * e0);
+    const int w1 = F * a.P;     // W2 [F x P] flat (ldw2 == P), dword pieces
+    for (int e0 = wv * 64; e0 < w1; e0 += kThreads)
+      if (e0 + lane < w1) lds_dma4(a.W2 + e0 + lane, s_W2 + e0);
+    if (a.epi.bias)
+      for (int e0 = wv * 64; e0 < Q; e0 += kThreads)
+        if (e0 + lane < Q) lds_dma16(a.epi.bias + 4 * (e0 + lane), s_bias + 4 * e0);
   }
   // S_T's further K-slabs (csrc/kslab.hip) into registers in the same round of
   // loads: slot i holds slab 1 + i / per, piece i % per (piece p = float4

@@ -44,8 +44,20 @@ physical core with one bound OpenMP thread each, with nproc and the CPU model; "
 "gpu_stock" stock PyTorch-ROCm torch.sparse.mm (hipSPARSE) on the device.
 
 configs: BASELINE configs 3 (20ng-shaped doc-topic graph, hidden 200, 20
-classes, gensim-shaped X) and 4 (uniform 1M nodes / 20M edges, F = 256) as
-extra keys (edges/s, GFLOP/s, algorithmic fraction), bounded time.
+classes, gensim-shaped X) and 4 (uniform 1M nodes / 20M edges, F = 256), plus
+config 4's power-law variant (R-MAT(0.57, 0.19, 0.19), 2^20 nodes, 20M edges
+drawn) as extra keys: edges/s, GFLOP/s, the algorithmic
+fraction, and for the 1M-node graphs the gather-rate fraction (nnz F 4 B of
+row pieces over the guide's 5.5 TB/s random-row gather rate).  Each carries the
+north_star's baselines beside it: "cpu_baseline" (the reference's th.spmm on
+its COO layout, utils.py:196-203 -- the oracle's forward for config 3 -- at the
+job's thread share and at 1 thread, >= 30 calls on config 3, 3 on config 4),
+"cpu_stock_csr" (torch CSR sparse.mm, MKL) and "gpu_stock" (torch.sparse.mm on
+the device, hipSPARSE).
+
+setup_ms.first_forward_breakdown: scripts/first_forward.py in fresh child
+processes -- the first forward's one-time costs step by step (library load,
+first launch, COO -> CSR, hub factor, launch record, first launches).
 """
 import argparse
 import csv
@@ -83,6 +95,8 @@ def parse():
     ap.add_argument("--kernel-reps", type=int, default=200, help="launches per op-timing graph")
     ap.add_argument("--no-pmc", action="store_true", help="skip the live rocprofv3 --pmc traffic passes")
     ap.add_argument("--no-configs", action="store_true", help="skip BASELINE configs 3 and 4")
+    ap.add_argument("--no-rmat", action="store_true", help="skip config 4's R-MAT (power-law) variant")
+    ap.add_argument("--rmat-cpu", action="store_true", help="also time the CPU legs on the R-MAT graph")
     ap.add_argument("--no-train", action="store_true", help="skip the training-step and setup legs")
     ap.add_argument("--no-rocprof", action="store_true", help="skip the child rocprofv3 kernel-trace runs")
     ap.add_argument("--rocprof-dir", default=None, help="keep the child kernel-trace summaries here")
@@ -158,6 +172,162 @@ def timed_cpu(fn, budget_s):
         fn()
         n += 1
     return (time.perf_counter() - t0) / n, n
+
+
+def timed_cpu_n(fn, n, warm=0):
+    """Median seconds per call of fn over exactly n timed calls (after `warm`
+    untimed ones), and every call's time: the CPU legs of the big configs,
+    where one call takes seconds."""
+    for _ in range(warm):
+        fn()
+    ts = []
+    for _ in range(n):
+        t0 = time.perf_counter()
+        fn()
+        ts.append(time.perf_counter() - t0)
+    return sorted(ts)[len(ts) // 2], [round(t, 4) for t in ts]
+
+
+# The random-row gather rate MI355X_MICROARCH.md measures for whole rows of a
+# buffer far larger than the Infinity Cache, gathered into registers: 5.5-5.6
+# TB/s for 1,152-B rows, 5.7-5.8 TB/s for 2,304-B rows (guide line 357).  A
+# uniform-random SpMM at F = 256 gathers one 1 KB row piece of B per nonzero, so
+# its bound is that rate, not the HBM peak against algorithmic bytes.
+GATHER_RATE_GBS = 5550.0
+
+
+def spmm_cpu_legs(rp, ci, v, shape, F, threads, iters, seed=0):
+    """The synthetic configs' CPU and stock-GPU lines (BASELINE.md
+    §3; north_star: "alongside the reference's scipy/torch.sparse CPU path timed on
+    the same box's host cores"): C = A B for one [K x F] B of this config,
+      cpu_baseline  the reference's call, th.spmm on the COO tensor laid out as
+                    utils.py:196-203 hands it (column-major, uncoalesced:
+                    datasets.reference_coo; layer.py:106), at the job's thread
+                    share and at 1 thread;
+      cpu_stock_csr torch CPU sparse.mm on a CSR tensor (MKL), same two thread counts;
+    each the median of `iters` timed calls (plus one untimed call for the CSR
+    leg), with the host's CPU model and nproc."""
+    import torch
+    from graph_convolutional_networks_for_text_classification_amd import datasets
+    M, K = shape
+    nnz = int(ci.numel())
+    g = torch.Generator().manual_seed(seed)
+    B = torch.randn(K, F, generator=g)
+    coo = datasets.reference_coo(rp, ci, v, shape)
+    csr = torch.sparse_csr_tensor(rp.cpu().long(), ci.cpu().long(), v.cpu(), shape)
+    saved = torch.get_num_threads()
+    out = {"cpu_baseline": {}, "cpu_stock_csr": {}}
+    try:
+        for th in sorted({threads, 1}, reverse=True):
+            torch.set_num_threads(th)
+            t, runs = timed_cpu_n(lambda: torch.spmm(coo, B), iters)
+            out["cpu_baseline"][f"threads_{th}"] = {"s_per_spmm": round(t, 4), "runs_s": runs,
+                                                     "edges_per_s": nnz / t, "gflops": 2 * nnz * F / t / 1e9}
+            t, runs = timed_cpu_n(lambda: torch.sparse.mm(csr, B), iters, warm=1)
+            out["cpu_stock_csr"][f"threads_{th}"] = {"s_per_spmm": round(t, 4), "runs_s": runs,
+                                                      "edges_per_s": nnz / t, "gflops": 2 * nnz * F / t / 1e9}
+    finally:
+        torch.set_num_threads(saved)
+    out["cpu_baseline"].update({"kind": "port", "unit": "edges/s", "cores": threads, "iterations": iters,
+                                "value": out["cpu_baseline"][f"threads_{threads}"]["edges_per_s"],
+                                "impl": "th.spmm on the reference-layout COO tensor (utils.py:196-203, "
+                                        "layer.py:106), torch CPU", **cpu_info()})
+    out["cpu_stock_csr"].update({"unit": "edges/s", "cores": threads, "iterations": iters,
+                                 "value": out["cpu_stock_csr"][f"threads_{threads}"]["edges_per_s"],
+                                 "impl": "torch CPU sparse.mm on a CSR tensor (MKL)"})
+    return out
+
+
+def gpu_stock_spmm(rp, ci, v, shape, B, iters=5):
+    """Stock PyTorch-ROCm: torch.sparse.mm on a device CSR tensor (hipSPARSE),
+    the same product; HIP events, best of `iters` after one untimed call."""
+    import torch
+    nnz = int(ci.numel())
+    a = torch.sparse_csr_tensor(rp.long(), ci.long(), v, shape, device=B.device)
+    torch.sparse.mm(a, B)
+    torch.cuda.synchronize()
+    best = None
+    for _ in range(iters):
+        e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        e0.record()
+        torch.sparse.mm(a, B)
+        e1.record()
+        e1.synchronize()
+        ms = e0.elapsed_time(e1)
+        best = ms if best is None else min(best, ms)
+    F = B.shape[1]
+    del a
+    return {"ms_spmm": round(best, 4), "edges_per_s": nnz / (best * 1e-3), "gflops": 2 * nnz * F / (best * 1e-3) / 1e9,
+            "unit": "edges/s", "value": nnz / (best * 1e-3),
+            "impl": "PyTorch-ROCm torch.sparse.mm on a device CSR tensor (hipSPARSE), best of %d" % iters}
+
+
+def big_spmm_config(name, rp, ci, v, n, F, dev, ops, cpu_threads, cpu_iters, build_s):
+    """One 1M-node synthetic config at width F on this GPU: the product path
+    (ops.spmm, plan built untimed), best of 5 HIP-event timings, edges/s, GFLOP/s,
+    the algorithmic-roofline fraction and the gather-rate fraction (nnz F 4 B of
+    row pieces over the guide's random-row gather rate), the heaviest row, then
+    the stock-GPU and CPU lines of the same product."""
+    import torch
+    from graph_convolutional_networks_for_text_classification_amd.sparse import CSR
+    big = CSR(rp, ci, v, (n, n))
+    g = torch.Generator(device=dev).manual_seed(7)
+    Bb = torch.randn(n, F, device=dev, generator=g)
+    Cb = torch.empty(n, F, device=dev)
+    t0 = time.time()
+    ops.spmm(big, Bb, out=Cb)
+    torch.cuda.synchronize()
+    plan_s = time.time() - t0
+    best = None
+    for _ in range(5):
+        e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        e0.record()
+        ops.spmm(big, Bb, out=Cb)
+        e1.record()
+        e1.synchronize()
+        ms = e0.elapsed_time(e1)
+        best = ms if best is None else min(best, ms)
+    nb = spmm_bytes(n, n, big.nnz, F)
+    gathered = 4 * big.nnz * F
+    deg = rp[1:] - rp[:-1]
+    res = {"nodes": n, "nnz": big.nnz, "F": F, "max_row_nnz": int(deg.max()), "ms_spmm": round(best, 4),
+           "edges_per_s": big.nnz / (best * 1e-3), "gflops": 2 * big.nnz * F / (best * 1e-3) / 1e9,
+           "frac": nb / (best * 1e-3) / 1e9 / HBM_PEAK_GBS, "algorithmic_bytes": nb,
+           "gather_bytes": gathered, "gather_gbs": gathered / (best * 1e-3) / 1e9,
+           "gather_frac": gathered / (best * 1e-3) / 1e9 / GATHER_RATE_GBS,
+           "gather_rate_ref": "MI355X_MICROARCH.md: 5.5-5.6 TB/s random 1,152-B rows gathered into registers "
+                              "(%.0f GB/s used)" % GATHER_RATE_GBS,
+           "graph_build_s": round(build_s, 1), "plan_build_s": round(plan_s, 2),
+           "note": "B (%.1f GB) and C exceed the 256 MB Infinity Cache: every launch is cold" % (4 * n * F / 1e9)}
+    hdr = big.plan(ops.default_ipc(big, F), int(ops._lib.load().gcnk_spmm_groups(F, 0))).header
+    res["plan"] = {"ipc": hdr[4], "row_units": hdr[5], "heavy_segments": hdr[6], "multi_segment_rows": hdr[7],
+                   "partial_slots": hdr[14]}
+    try:
+        res["gpu_stock"] = gpu_stock_spmm(rp, ci, v, (n, n), Bb)
+    except RuntimeError as e:   # reported, never fatal to the bench line
+        res["gpu_stock"] = {"error": str(e)[:300]}
+    del big, Bb, Cb
+    torch.cuda.empty_cache()
+    if cpu_iters > 0:
+        res.update(spmm_cpu_legs(rp.cpu(), ci.cpu(), v.cpu(), (n, n), F, cpu_threads, cpu_iters))
+    return res
+
+
+def first_forward_breakdown():
+    """scripts/first_forward.py in a fresh child process: the first R8 forward's
+    one-time costs step by step (library load, first launch, COO -> CSR, hub
+    factor, launch record / plans, the first launches), and the same first
+    forward as one step (--direct) in another fresh process."""
+    out = {}
+    for key, extra in (("steps", []), ("direct", ["--direct"])):
+        try:
+            r = subprocess.run([sys.executable, os.path.join(ROOT, "scripts", "first_forward.py")] + extra, cwd=ROOT,
+                               stdout=subprocess.PIPE, stderr=subprocess.STDOUT, timeout=300)
+            line = [ln for ln in r.stdout.decode(errors="replace").splitlines() if ln.startswith("{")]
+            out[key] = json.loads(line[-1]) if r.returncode == 0 and line else {"error": f"rc={r.returncode}"}
+        except (OSError, subprocess.SubprocessError, ValueError) as e:
+            out[key] = {"error": str(e)[:200]}
+    return out
 
 
 def pmc_traffic(op, kernels_like, detail=None):
@@ -636,6 +806,86 @@ def pinned_cpu_leg(state_dict, sample_s):
         shutil.rmtree(tmp, ignore_errors=True)
 
 
+def config3_baselines(g20, m20, a20, x20, ac20, sample_s):
+    """BASELINE config 3 (the 20ng-shaped doc-topic graph) beside the product:
+    the reference's forward on the host CPU (the oracle issuing layer.py's
+    th.spmm calls on the same COO tensors, layer.py:102,106) at the job's thread
+    share and at 1 thread, the same forward through torch CPU CSR sparse.mm
+    (MKL), and through stock PyTorch-ROCm torch.sparse.mm (hipSPARSE) on the
+    device; plus the north-star-shaped op alone (A-hat S at F = 200) on the
+    reference's COO path.  >= 30 timed calls each (bounded by sample_s)."""
+    import torch
+    from oracle import gcn_ref
+    threads = int(os.environ.get("OMP_NUM_THREADS", str(min(16, os.cpu_count() or 1))))
+    nnz = ac20.nnz
+    ref = gcn_ref.RefGCN(nfeat=g20["nfeat"], nhid=200, nclass=20, dropout=0.5).eval()
+    ref.load_state_dict({k: v.cpu() for k, v in m20.state_dict().items()})
+    xc, adc = g20["features"], g20["adj"]
+    W1, b1, W2, b2 = (p.detach() for p in (m20.gc1.weight, m20.gc1.bias, m20.gc2.weight, m20.gc2.bias))
+    Wc1, bc1, Wc2, bc2 = (p.cpu() for p in (W1, b1, W2, b2))
+    xs, as_ = xc.coalesce().to_sparse_csr(), adc.coalesce().to_sparse_csr()
+    S = torch.randn(adc.shape[0], 200, generator=torch.Generator().manual_seed(3))
+    saved = torch.get_num_threads()
+    fwd, csr, op = {}, {}, {}
+
+    def budgeted(fn):
+        fn()
+        n, t0, ts = 0, time.perf_counter(), []
+        while n < 30 or time.perf_counter() - t0 < sample_s / 4:
+            t1 = time.perf_counter()
+            fn()
+            ts.append(time.perf_counter() - t1)
+            n += 1
+            if time.perf_counter() - t0 > 4 * sample_s and n >= 30:
+                break
+        return sorted(ts)[len(ts) // 2], n
+    try:
+        with torch.no_grad():
+            for th in sorted({threads, 1}, reverse=True):
+                torch.set_num_threads(th)
+                t, n = budgeted(lambda: ref(xc, adc))
+                fwd[f"threads_{th}"] = {"ms_per_forward": round(t * 1e3, 3), "forwards": n,
+                                        "edges_per_s": 2 * nnz / t}
+
+                def csr_forward():
+                    h = torch.relu(torch.sparse.mm(as_, torch.sparse.mm(xs, Wc1)) + bc1)
+                    return torch.sparse.mm(as_, h @ Wc2) + bc2
+                t, n = budgeted(csr_forward)
+                csr[f"threads_{th}"] = {"ms_per_forward": round(t * 1e3, 3), "forwards": n,
+                                        "edges_per_s": 2 * nnz / t}
+                t, n = budgeted(lambda: torch.spmm(adc, S))
+                op[f"threads_{th}"] = {"ms": round(t * 1e3, 3), "calls": n, "edges_per_s": nnz / t,
+                                       "gflops": 2 * nnz * 200 / t / 1e9}
+    finally:
+        torch.set_num_threads(saved)
+    xg, ag = x20.coalesce().to_sparse_csr(), a20.coalesce().to_sparse_csr()
+
+    def stock_forward():
+        with torch.no_grad():
+            h = torch.relu(torch.sparse.mm(ag, torch.sparse.mm(xg, W1)) + b1)
+            return torch.sparse.mm(ag, h @ W2) + b2
+    stock_forward()
+    torch.cuda.synchronize()
+    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    e0.record()
+    for _ in range(30):
+        stock_forward()
+    e1.record()
+    e1.synchronize()
+    tg = e0.elapsed_time(e1) / 30 * 1e-3
+    return {
+        "cpu_baseline": {"value": fwd[f"threads_{threads}"]["edges_per_s"], "unit": "edges/s", "cores": threads,
+                         "kind": "port", "ms_per_forward": fwd[f"threads_{threads}"]["ms_per_forward"],
+                         "sample": "20ng-shaped eval forwards of the oracle (torch-CPU th.spmm on the reference COO "
+                                   "tensors, layer.py:102,106), median", **fwd, **cpu_info(),
+                         "spmm_F200_reference_coo": op},
+        "cpu_stock_csr": {"value": csr[f"threads_{threads}"]["edges_per_s"], "unit": "edges/s", "cores": threads,
+                          "ms_per_forward": csr[f"threads_{threads}"]["ms_per_forward"],
+                          "impl": "torch CPU sparse.mm on CSR tensors (MKL), same forward", **csr},
+        "gpu_stock": {"value": 2 * nnz / tg, "unit": "edges/s", "ms_per_forward": round(tg * 1e3, 4),
+                      "impl": "PyTorch-ROCm torch.sparse.mm on CSR tensors (hipSPARSE), eager, same forward"}}
+
+
 def main():
     args = parse()
     if "WORLD_SIZE" not in os.environ and args.gpus > 1:
@@ -861,6 +1111,7 @@ def main():
         train = train_step_legs(r8, dev)
         setup = setup_legs(r8, dev)
         setup["first_forward_fresh_process_ms"] = round(first_forward_ms, 3)
+        setup["first_forward_breakdown"] = first_forward_breakdown()
 
     # ---- BASELINE configs 3 and 4 (bounded)
     configs = None
@@ -881,6 +1132,10 @@ def main():
             args.rocprof_dir, "20ng", ac20, x20, ac20.shape[0], g20["nfeat"], ac20.nnz, as_csr(x20).nnz, 200, 20)
         fb20 = factor_build_ms(ac20, x20)
         dab20 = dense_ax_build_ms(ac20, x20, 200, 20)
+        # the same forward on the reference's CPU path and on stock PyTorch-ROCm
+        legs20 = {}
+        if args.cpu_sample_s > 0:
+            legs20 = config3_baselines(g20, m20, a20, x20, ac20, args.cpu_sample_s)
         M20 = ac20.shape[0]
         bb = torch.randn(200, device=dev)
         nsets = max(2, -(-int(1.25 * MALL_BYTES) // (2 * 4 * M20 * 200)))
@@ -899,36 +1154,27 @@ def main():
             "spmm_F200_frac_warm": nb / (w * 1e-6) / 1e9 / HBM_PEAK_GBS,
             "spmm_F200_gflops_cold": 2 * ac20.nnz * 200 / (c * 1e-6) / 1e9,
             "path": forward_path(ac20, x20, 200, 20), "factor_build_ms": fb20, "dense_ax_build_ms": dab20,
-            "forward_kernels": fk20}
+            "forward_kernels": fk20, **legs20}
         del m20, a20, x20, ac20
         torch.cuda.empty_cache()
-        from graph_convolutional_networks_for_text_classification_amd.sparse import CSR
+        threads = int(os.environ.get("OMP_NUM_THREADS", str(min(16, os.cpu_count() or 1))))
+        cpu_iters = 3 if args.cpu_sample_s > 0 else 0
         tb = time.time()
         rp, ci, v = datasets.uniform_random_csr(1_000_000, 20_000_000, seed=0, device=dev)
-        big = CSR(rp, ci, v, (1_000_000, 1_000_000))
-        Fb = 256
-        Bb = torch.randn(1_000_000, Fb, device=dev)
-        Cb = torch.empty(1_000_000, Fb, device=dev)
-        ops.spmm(big, Bb, out=Cb)
-        torch.cuda.synchronize()
-        build_s = time.time() - tb
-        e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
-        best = None
-        for _ in range(5):
-            e0.record()
-            ops.spmm(big, Bb, out=Cb)
-            e1.record()
-            e1.synchronize()
-            ms = e0.elapsed_time(e1)
-            best = ms if best is None else min(best, ms)
-        nb = spmm_bytes(1_000_000, 1_000_000, big.nnz, Fb)
-        configs["uniform_1M_20M_F256"] = {
-            "nnz": big.nnz, "ms_spmm": round(best, 4), "edges_per_s": big.nnz / (best * 1e-3),
-            "gflops": 2 * big.nnz * Fb / (best * 1e-3) / 1e9,
-            "frac": nb / (best * 1e-3) / 1e9 / HBM_PEAK_GBS, "setup_s": round(build_s, 1),
-            "note": "B (1 GB) and C exceed the 256 MB Infinity Cache: every launch is cold"}
-        del big, Bb, Cb, rp, ci, v
+        configs["uniform_1M_20M_F256"] = big_spmm_config("uniform", rp, ci, v, 1_000_000, 256, dev, ops, threads,
+                                                         cpu_iters, time.time() - tb)
+        del rp, ci, v
         torch.cuda.empty_cache()
+        if not args.no_rmat:
+            # SURVEY §8(d) row 4's power-law variant, reported separately: R-MAT(0.57,
+            # 0.19, 0.19), 2^20 nodes, 20M edges drawn (rows of up to ~45k nonzeros)
+            tb = time.time()
+            rp, ci, v = datasets.rmat_csr(20, 20_000_000, seed=0, device=dev)
+            configs["rmat_1M_20M_F256"] = big_spmm_config("rmat", rp, ci, v, 1 << 20, 256, dev, ops, threads,
+                                                          cpu_iters if args.rmat_cpu else 0, time.time() - tb)
+            configs["rmat_1M_20M_F256"]["generator"] = "datasets.rmat_csr(20, 20_000_000, a=0.57, b=0.19, c=0.19, seed=0)"
+            del rp, ci, v
+            torch.cuda.empty_cache()
 
     # ---- BASELINE config 5 (N > 1): 1M nodes / 20M edges, F = 4096 feature
     #      columns sharded over the ranks (parallel.ColumnShardedSpMM: local

@@ -31,7 +31,7 @@ def _resolve_lib():
 
 
 LIB_PATH = _resolve_lib()
-ABI_VERSION = 11
+ABI_VERSION = 12
 
 # C-ABI return codes (gcnk.h)
 OK, EARG, EUNSUP, EHIP = 0, -1, -2, -3
@@ -121,17 +121,6 @@ SIGNATURES = {
         _f32, _u64, _u64, _vp,            # keep_prob, seed, offset, rng_base
         _vp, _i64, _vp, _i64, _vp, _i64,  # W2, ldw2, H, ldh, C2, ldc2
         _vp]),                            # stream
-    "gcnk_hubfactor_gc1_slabs_f32": (ctypes.c_int, [
-        _i32, _i32, _i32, _i32, _i32,     # M, F, Kc, nhub, P
-        _vp, _i64, _vp, _i64, _i32,       # U, ldu, W, ldw, k0
-        _vp, _i64, _i32, _i64,            # S, lds, nslab, slab_stride
-        _vp, _i32,                        # rec, rec_words
-        _vp, _i32,                        # bias, epilogue
-        _vp, _i64, _f32,                  # drop_mask, ldm, drop_scale
-        _f32, _u64, _u64, _vp,            # keep_prob, seed, offset, rng_base
-        _vp, _i64, _vp, _i64, _vp, _i64,  # W2, ldw2, H, ldh, C2, ldc2
-        _vp]),                            # stream
-    "gcnk_gemm_kslabs_f32": (ctypes.c_int, [_i32, _i32, _i32, _vp, _i64, _vp, _i64, _i32, _vp, _i64, _i64, _vp]),
     "gcnk_dense_gc1_f32": (ctypes.c_int, [
         _i32, _i32, _i32, _i32,           # M, K, F, P
         _vp, _i64, _vp, _i64,             # AX, ldax, W1, ldw1
@@ -140,10 +129,6 @@ SIGNATURES = {
         _f32, _u64, _u64, _vp,            # keep_prob, seed, offset, rng_base
         _vp, _i64, _vp, _i64, _vp, _i64,  # W2, ldw2, H, ldh, C2, ldc2
         _vp]),                            # stream
-    "gcnk_gemm_smallm_workspace_bytes": (_i64, [_i32, _i32, _i32]),
-    "gcnk_gemm_smallm_counter_bytes": (_i64, [_i32]),
-    "gcnk_gemm_smallm_f32": (ctypes.c_int, [_i32, _i32, _i32, _vp, _i64, _vp, _i64, _vp, _i64, _i32, _vp, _i64, _vp,
-                                            _i64, _vp]),
     "gcnk_aggregate_f32": (ctypes.c_int, [_vp, _vp, _vp, _i32, _vp, _i64, _i32, _vp, _i64, _i32, _vp]),
     # record (host struct gcnk_gcn_fwd), W1, b1, W2, b2, out, ldo, H1, ldh, epilogue, mask, ldm, scale,
     # keep_prob, seed, offset, rng_base, stream

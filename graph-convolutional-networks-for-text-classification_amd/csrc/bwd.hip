@@ -38,16 +38,8 @@ constexpr int kBwdBatch = 8;       // rows per lane whose H1 loads are in flight
 #define GCNK_BWD_TARGET 256
 #endif
 constexpr int kBwdTarget = GCNK_BWD_TARGET;    // workgroups per slice (256: one per CU)
-// gZ1 store policy (experiment knob): 1 nontemporal, 0 plain, 2 sc1 write-through,
-// 3 none (timing only: gZ1 not written)
 #ifndef GCNK_BWD2_STAMPV   // stamps-build timeline variant (2: around the lane sum)
 #define GCNK_BWD2_STAMPV 1
-#endif
-#ifndef GCNK_BWD2_PEXP     // experiment: 1 no partial stores, 2 no gb2 loop, 3 no partial loop
-#define GCNK_BWD2_PEXP 0
-#endif
-#ifndef GCNK_BWD2_ZST
-#define GCNK_BWD2_ZST 1
 #endif
 
 template <int VEC>
@@ -204,13 +196,8 @@ __global__ void __launch_bounds__(kBwdBlock) gcn_bwd2_kernel(Bwd2Args a) {
 #pragma unroll
         for (int p = 0; p < PM; ++p) gw[v][p] = fmaf(h[j][v], g[p], gw[v][p]);
       }
-      if (GCNK_BWD2_ZST == 1) VecIO<VEC>::store_nt(a.Z + (int64_t)(r0 + rr) * a.ldz + c, z);
-      else if (GCNK_BWD2_ZST == 0) VecIO<VEC>::store(a.Z + (int64_t)(r0 + rr) * a.ldz + c, z);
-      else if (GCNK_BWD2_ZST == 3) { if (z[0] == 1234.5f) a.Z[0] = z[VEC - 1]; }
-      else
-#pragma unroll
-        for (int v = 0; v < VEC; ++v)
-          __hip_atomic_store(a.Z + (int64_t)(r0 + rr) * a.ldz + c + v, z[v], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+      // gZ1 streamed out (nontemporal: no dirty L2 lines left at the kernel's end)
+      VecIO<VEC>::store_nt(a.Z + (int64_t)(r0 + rr) * a.ldz + c, z);
     }
   }
 
@@ -234,7 +221,7 @@ __global__ void __launch_bounds__(kBwdBlock) gcn_bwd2_kernel(Bwd2Args a) {
   stamp(a.stamps, 2);
 #endif
   float* prow = a.part + (int64_t)blockIdx.x * a.part_ld;
-  for (int e = tid; e < (GCNK_BWD2_PEXP == 3 ? 0 : CT * KE); e += kBwdBlock) {
+  for (int e = tid; e < CT * KE; e += kBwdBlock) {
     const int u = e / KE, k = e % KE;
     const int v = k / (PM + 1), p = k % (PM + 1);
     const int64_t col = (int64_t)(cu0 + u) * VEC + v;
@@ -251,14 +238,13 @@ __global__ void __launch_bounds__(kBwdBlock) gcn_bwd2_kernel(Bwd2Args a) {
       for (int j = 0; j < 8; ++j) s = l0 + j < RL ? s + rv[j] : s;
     }
     if (col >= a.N) continue;
-    if (GCNK_BWD2_PEXP == 1) { if (s == 1234.5f) prow[0] = s; continue; }
     if (p < PM) {
       if (p < a.P) prow[col * a.P + p] = s;
     } else {
       prow[(int64_t)a.N * a.P + col] = s;
     }
   }
-  if (GCNK_BWD2_PEXP != 2 && with_g && tid < a.P) {  // gb2: the G rows, in row order (eight LDS reads in flight)
+  if (with_g && tid < a.P) {  // gb2: the G rows, in row order (eight LDS reads in flight)
     float s = 0.f;
     for (int r8 = 0; r8 < nr; r8 += 16) {
       float gv[16];

@@ -12,12 +12,11 @@
 // X W1 GEMM in front of it never run (the association differs from the
 // reference's A-hat (X W1) only in fp32 rounding, ~1e-6 relative).
 //
-// Persistent workgroups (two per CU in dense mode, so one wave's MFMAs overlap
-// the other's epilogue on each SIMD; one per CU in hub mode, whose S_T fills the
-// LDS).  4 waves each; wave w owns the 64 columns 64 w .. 64 w + 63 of F as four
+// Persistent workgroups (two per CU, so one wave's MFMAs overlap the other's
+// epilogue on each SIMD).  4 waves each; wave w owns the 64 columns 64 w .. 64 w + 63 of F as four
 // MFMA n-tiles INTERLEAVED by lane: n-tile t, lane column c is physical column
 // 64 w + 4 c + t, so a lane's four n-tiles are four consecutive columns and every
-// W1 row piece, b1, S_T row piece and H1 piece it touches is one 16-B access
+// W1 row piece, b1 and H1 piece it touches is one 16-B access
 // (the n-tile-major mapping took 100 4-B W1 loads a wave, 4 rows x 64 B each --
 // with 512 workgroups re-reading W1 that was half of the launch).  The W1 and W2
 // fragments stay in registers for the whole launch.  Per 16-row tile:
@@ -47,43 +46,25 @@ constexpr int kThreads = 64 * kWaves;
 constexpr int kNTQ = 4;          // n-tiles per wave: F <= 16 * 4 * kNTQ = 256
 constexpr int kHP = 64 + 4;      // wave-private H1 tile row stride (floats): 16 x (64 + 4)
 constexpr int kMaxP = 32;
-// experiment knob (variant builds only): 1 no W1 MFMAs, 2 no projection MFMAs,
-// 3 no A loads, 4 no S2 reduction / stores, 5 no W1 / W2 fragment loads,
-// 6 W1 fragments loaded in a per-workgroup rotated row order (wrong values: timing only)
-#ifndef GCNK_DG_EXP
-#define GCNK_DG_EXP 0
-#endif
-
-// hub mode (the factored gc1, csrc/factor.hip's record layout): U's rows are
-// positions of the block order; per 32-position block a record of rec_words
-// int32: 33 block-relative item offsets, 3 pad, 32 output row ids (-1 past M),
-// then items int2 {hub index, value bits}
-constexpr int kRecRow = 36, kRecHead = 68;
-
 struct DenseArgs {
   int32_t M, K, F, P;
-  const float* A; int64_t lda;     // A-hat X [M x >= K] (hub mode: U in block order)
-  const float* W; int64_t ldw;     // W1 [K x F] (hub mode: W1's rows k0 ..)
+  const float* A; int64_t lda;     // A-hat X [M x >= K]
+  const float* W; int64_t ldw;     // W1 [K x F]
   const float* W2; int64_t ldw2;   // [F x P]
   float* H; int64_t ldh;           // nullable
   float* C2; int64_t ldc2;         // S2 [M x P]
   Epi epi;
   int32_t ntiles;                  // ceil(M / 16)
-  // hub mode: Z += A_H S_T
-  const float* S; int64_t lds;     // S_T [nhub x F]
-  int32_t nhub;
-  const int32_t* rec; int32_t rec_words;
 };
 
 // KS k-steps of 4 (K <= 4 KS; lane quadrant q of step s multiplies k = 4 s + q),
-// NP 16-column tiles of P; HUB: the factored gc1 (S_T staged in LDS once, the
-// tile's block record staged per tile, one tile ahead)
+// NP 16-column tiles of P
 // A-tile row stride: >= 4 KS and = 4 (mod 64), so lane (row c, quadrant q)
 // reading k = 4 s + q hits bank 4 c + q: conflict-free
 constexpr int a_stride(int ks) { return 64 * ((4 * ks - 4 + 63) / 64) + 4; }
 
-template <int KS, int NP, bool HUB>
-__global__ void __launch_bounds__(kThreads, HUB ? 1 : 2)
+template <int KS, int NP>
+__global__ void __launch_bounds__(kThreads, 2)
 dense_gc1_kernel(DenseArgs a) {
   resolve_rng(a.epi);
   constexpr int KP = a_stride(KS);
@@ -91,7 +72,6 @@ dense_gc1_kernel(DenseArgs a) {
   __shared__ __attribute__((aligned(16))) float s_A[2][16 * KP];
   __shared__ __attribute__((aligned(16))) float s_h[kWaves][16 * kHP];
   __shared__ __attribute__((aligned(16))) float s_red[2][kWaves][NP][64 * 4];
-  extern __shared__ __attribute__((aligned(16))) float s_dyn[];   // HUB: s_S [nhub x F] | s_rec [2][rec_words]
   const int tid = threadIdx.x, lane = tid & 63;
   const int w = __builtin_amdgcn_readfirstlane(tid >> 6);
   const int c = lane & 15, q = lane >> 4;
@@ -109,10 +89,9 @@ dense_gc1_kernel(DenseArgs a) {
   float wf[KS][kNTQ];
 #pragma unroll
   for (int s = 0; s < KS; ++s) {
-    const int k = GCNK_DG_EXP == 6 ? (4 * s + q + 4 * (int)(blockIdx.x % KS)) % (4 * KS) : 4 * s + q;
+    const int k = 4 * s + q;
     float4 v = make_float4(0.f, 0.f, 0.f, 0.f);
-    if (GCNK_DG_EXP == 5) v = make_float4(1e-3f, 1e-3f, 1e-3f, 1e-3f);
-    else if (cok && k < K) v = *reinterpret_cast<const float4*>(a.W + (int64_t)k * a.ldw + col0);
+    if (cok && k < K) v = *reinterpret_cast<const float4*>(a.W + (int64_t)k * a.ldw + col0);
     wf[s][0] = v.x; wf[s][1] = v.y; wf[s][2] = v.z; wf[s][3] = v.w;
   }
   float w2f[kNTQ][4][NP];
@@ -123,8 +102,7 @@ dense_gc1_kernel(DenseArgs a) {
 #pragma unroll
       for (int p = 0; p < NP; ++p) {
         const int col = 64 * w + 16 * t + 4 * j + q, pc = 16 * p + c;
-        w2f[t][j][p] = (GCNK_DG_EXP != 5 && col < F && pc < P) ? a.W2[(int64_t)col * a.ldw2 + pc]
-                                                             : (GCNK_DG_EXP == 5 ? 1e-3f : 0.f);
+        w2f[t][j][p] = (col < F && pc < P) ? a.W2[(int64_t)col * a.ldw2 + pc] : 0.f;
       }
   float bv[kNTQ];
   {
@@ -138,39 +116,6 @@ dense_gc1_kernel(DenseArgs a) {
   stamp(a.epi, 1);
 #endif
   float* hw = s_h[w];
-  float* s_S = s_dyn;
-  int32_t* s_rec = reinterpret_cast<int32_t*>(s_dyn + (HUB ? a.nhub * F : 0));
-  const int rw = HUB ? a.rec_words : 0;
-  // HUB: the block record of a tile (block tile / 2) into registers, then LDS
-  constexpr int kRecPer = 4;   // record words per thread (rec_words <= 1024, checked on the host)
-  auto load_rec = [&](int tile, int32_t (&rv)[kRecPer]) {
-    if constexpr (HUB) {
-      const int32_t* rb = a.rec + (int64_t)(tile / 2) * rw;
-#pragma unroll
-      for (int i = 0; i < kRecPer; ++i) {
-        const int e = tid + kThreads * i;
-        rv[i] = (tile < a.ntiles && e < rw) ? rb[e] : 0;
-      }
-    }
-  };
-  auto put_rec = [&](int buf, const int32_t (&rv)[kRecPer]) {
-    if constexpr (HUB) {
-#pragma unroll
-      for (int i = 0; i < kRecPer; ++i) {
-        const int e = tid + kThreads * i;
-        if (e < rw) s_rec[buf * rw + e] = rv[i];
-      }
-    }
-  };
-  if constexpr (HUB) {
-    // S_T once per workgroup (float4 pieces: F % 4 == 0, lds % 4 == 0, checked on the host)
-    const int n4 = a.nhub * (F / 4);
-    for (int e = tid; e < n4; e += kThreads) {
-      const int hrow = e / (F / 4), c4 = e % (F / 4);
-      *reinterpret_cast<float4*>(s_S + hrow * F + 4 * c4) =
-          *reinterpret_cast<const float4*>(a.S + (int64_t)hrow * a.lds + 4 * c4);
-    }
-  }
   // the A tile [16 x 4 KS] (zero past K and M): thread element e -> row e / (4 KS),
   // k e % (4 KS) -- consecutive threads, consecutive k: coalesced
   auto load_a = [&](int tile, float (&av)[kAPer]) {
@@ -181,7 +126,7 @@ dense_gc1_kernel(DenseArgs a) {
       // (the address clamped into A, the value selected: no branch per load)
       const int64_t rc = row < a.M ? row : a.M - 1;
       const float v = a.A[rc * a.lda + (k < K ? k : K - 1)];
-      av[i] = (GCNK_DG_EXP != 3 && e < 16 * 4 * KS && tile < a.ntiles && row < a.M && k < K) ? v : 0.f;
+      av[i] = (e < 16 * 4 * KS && tile < a.ntiles && row < a.M && k < K) ? v : 0.f;
     }
   };
   auto put_a = [&](int buf, const float (&av)[kAPer]) {
@@ -195,21 +140,14 @@ dense_gc1_kernel(DenseArgs a) {
     float av[kAPer];
     load_a(blockIdx.x, av);
     put_a(0, av);
-    if constexpr (HUB) {
-      int32_t rv[kRecPer];
-      load_rec(blockIdx.x, rv);
-      put_rec(0, rv);
-    }
     __syncthreads();
   }
 
-  // one 16-row tile from LDS buffer `buf`; the next tile's A (and record) are
-  // loaded under its MFMAs and written to buffer buf ^ 1 before the barrier
+  // one 16-row tile from LDS buffer `buf`; the next tile's A is loaded under
+  // its MFMAs and written to buffer buf ^ 1 before the barrier
   auto tile_step = [&](int tile, int buf) {
     float av[kAPer];
     load_a(tile + gridDim.x, av);
-    int32_t rv[kRecPer];
-    load_rec(tile + gridDim.x, rv);
     // ---- 1. Z = A W1[:, cols_w]; lane (row c, quadrant q) reads A[c][4 s + q]
     //      All KS fragments read before the MFMAs (one LDS wait), and every
     //      wave issues kNTQ MFMAs per k-step: an absent n-tile's W1 fragments
@@ -223,57 +161,17 @@ dense_gc1_kernel(DenseArgs a) {
 #pragma unroll
     for (int t = 0; t < kNTQ; ++t) acc[t] = f32x4{0.f, 0.f, 0.f, 0.f};
 #pragma unroll
-    for (int s = 0; s < (GCNK_DG_EXP == 1 ? 0 : KS); ++s)
+    for (int s = 0; s < KS; ++s)
 #pragma unroll
       for (int t = 0; t < kNTQ; ++t) acc[t] = __builtin_amdgcn_mfma_f32_16x16x4f32(af[s], wf[s][t], acc[t], 0, 0, 0);
     // ---- 2. epilogue (C/D map: reg r -> row 4 q + r, column c), H1 store,
     //      tile into wave-private LDS
     const int64_t row0 = (int64_t)tile * 16;
     const bool plain = a.epi.code == GCNK_EPI_BIAS_RELU;
-    int64_t orow[4];   // output rows of this lane's 4 tile rows
-    if constexpr (HUB) {
-      const int32_t* rb = s_rec + buf * rw;
-      const int2* it = reinterpret_cast<const int2*>(rb + kRecHead);
-      int beg[4], len[4], most = 0;
-#pragma unroll
-      for (int r = 0; r < 4; ++r) {
-        const int pb = 16 * (tile & 1) + 4 * q + r;   // position within the 32-row block
-        const int32_t id = rb[kRecRow + pb];
-        orow[r] = id >= 0 ? id : a.M;                 // -1 (past M): never stored
-        beg[r] = rb[pb];
-        len[r] = rb[pb + 1] - rb[pb];
-        most = max(most, len[r]);
-      }
-      // + A_H S_T: each row's hub items in CSR order, the lane's four rows
-      // advanced together (four independent FMA chains per LDS round trip)
-      for (int j = 0; j < most; ++j) {
-        float v[4];
-        const float* srow[4];
-#pragma unroll
-        for (int r = 0; r < 4; ++r) {
-          const int2 p2 = j < len[r] ? it[beg[r] + j] : int2{0, 0};   // (pad: + 0 x S_T[0])
-          v[r] = __int_as_float(p2.y);
-          srow[r] = s_S + p2.x * F + col0;
-        }
-        if (cok) {   // (columns past F: no read past the hub's row)
-#pragma unroll
-          for (int r = 0; r < 4; ++r) {
-            const float4 sv = *reinterpret_cast<const float4*>(srow[r]);
-            acc[0][r] = fmaf(v[r], sv.x, acc[0][r]);
-            acc[1][r] = fmaf(v[r], sv.y, acc[1][r]);
-            acc[2][r] = fmaf(v[r], sv.z, acc[2][r]);
-            acc[3][r] = fmaf(v[r], sv.w, acc[3][r]);
-          }
-        }
-      }
-    } else {
-#pragma unroll
-      for (int r = 0; r < 4; ++r) orow[r] = row0 + 4 * q + r;
-    }
     //      (columns past F: acc and b1 zero, h = 0 written)
 #pragma unroll
     for (int r = 0; r < 4; ++r) {
-      const int64_t row = orow[r];
+      const int64_t row = row0 + 4 * q + r;
       float h[kNTQ];
 #pragma unroll
       for (int t = 0; t < kNTQ; ++t) {
@@ -302,42 +200,24 @@ dense_gc1_kernel(DenseArgs a) {
       for (int j = 0; j < 4; ++j)
 #pragma unroll
         for (int p = 0; p < NP; ++p)
-          if (GCNK_DG_EXP == 2) pacc[p][j] += ha[j] * w2f[t][j][p];
-          else pacc[p] = __builtin_amdgcn_mfma_f32_16x16x4f32(ha[j], w2f[t][j][p], pacc[p], 0, 0, 0);
+          pacc[p] = __builtin_amdgcn_mfma_f32_16x16x4f32(ha[j], w2f[t][j][p], pacc[p], 0, 0, 0);
     }
 #pragma unroll
     for (int p = 0; p < NP; ++p) *reinterpret_cast<f32x4*>(&s_red[buf][w][p][4 * lane]) = pacc[p];
-    // output rows of this thread's S2 elements (e = tid + 256 i: tile row e / (16 NP),
-    // column e % (16 NP)), read before the barrier (the record buffer `buf` is
-    // rewritten by the next tile before ITS barrier)
-    int64_t rrow[NP];
-#pragma unroll
-    for (int i = 0; i < NP; ++i) {
-      const int tr = (tid + kThreads * i) / (16 * NP);
-      if constexpr (HUB) {
-        const int32_t id = s_rec[buf * rw + kRecRow + 16 * (tile & 1) + tr];
-        rrow[i] = id >= 0 ? id : a.M;
-      } else {
-        rrow[i] = row0 + tr;
-      }
-    }
-    put_a(buf ^ 1, av);     // the next tile's A and record (their readers passed the previous barrier)
-    put_rec(buf ^ 1, rv);
+    put_a(buf ^ 1, av);     // the next tile's A (its readers passed the previous barrier)
     // (double-buffered by tile parity: wave 0 reads buffer `buf` before it
     // reaches the next barrier, and buffer `buf` is written again only after it)
     __syncthreads();
     // the four waves' partials summed in wave order by the whole workgroup
     // (partial (row 4 q + r, column 16 p + c) at s_red[.][w][p][4 (16 q + c) + r])
-    if (GCNK_DG_EXP != 4) {
 #pragma unroll
-      for (int i = 0; i < NP; ++i) {
-        const int e = tid + kThreads * i, tr = e / (16 * NP), col = e % (16 * NP);
-        const int p = col >> 4, cc = col & 15, idx = 4 * (16 * (tr >> 2) + cc) + (tr & 3);
-        float sum = s_red[buf][0][p][idx];
+    for (int i = 0; i < NP; ++i) {
+      const int e = tid + kThreads * i, tr = e / (16 * NP), col = e % (16 * NP);
+      const int p = col >> 4, cc = col & 15, idx = 4 * (16 * (tr >> 2) + cc) + (tr & 3);
+      float sum = s_red[buf][0][p][idx];
 #pragma unroll
-        for (int v = 1; v < kWaves; ++v) sum += s_red[buf][v][p][idx];
-        if (rrow[i] < a.M && col < P) a.C2[rrow[i] * a.ldc2 + col] = sum;
-      }
+      for (int v = 1; v < kWaves; ++v) sum += s_red[buf][v][p][idx];
+      if (row0 + tr < a.M && col < P) a.C2[(row0 + tr) * a.ldc2 + col] = sum;
     }
     // the wave-private H1 tile is rewritten next tile after these reads (in
     // order within the wave): no barrier needed
@@ -351,18 +231,12 @@ dense_gc1_kernel(DenseArgs a) {
   stamp(a.epi, 3);
 }
 
-template <int KS, bool HUB>
-int launch_ks(const DenseArgs& a, int np, unsigned grid, size_t dyn, hipStream_t s) {
-  if (dyn > 64 * 1024) {   // dynamic LDS past the default limit: raised once per device
-    static std::atomic<uint64_t> done1{0}, done2{0};
-    const hipError_t e = np == 1 ? dyn_lds_attr(done1, reinterpret_cast<const void*>(&dense_gc1_kernel<KS, 1, HUB>), 160 * 1024)
-                                 : dyn_lds_attr(done2, reinterpret_cast<const void*>(&dense_gc1_kernel<KS, 2, HUB>), 160 * 1024);
-    if (e != hipSuccess) return hip_check(e, "dense_gc1_kernel LDS attribute");
-  }
+template <int KS>
+int launch_ks(const DenseArgs& a, int np, unsigned grid, hipStream_t s) {
   if (np == 1)
-    hipLaunchKernelGGL((dense_gc1_kernel<KS, 1, HUB>), dim3(grid), dim3(kThreads), dyn, s, a);
+    hipLaunchKernelGGL((dense_gc1_kernel<KS, 1>), dim3(grid), dim3(kThreads), 0, s, a);
   else
-    hipLaunchKernelGGL((dense_gc1_kernel<KS, 2, HUB>), dim3(grid), dim3(kThreads), dyn, s, a);
+    hipLaunchKernelGGL((dense_gc1_kernel<KS, 2>), dim3(grid), dim3(kThreads), 0, s, a);
   return launch_check("dense_gc1_kernel");
 }
 
@@ -378,22 +252,19 @@ int cu_count() {
   return n;
 }
 
-template <bool HUB>
 int launch(const DenseArgs& a, hipStream_t s) {
-  // persistent: 4 waves per workgroup, two workgroups per CU in dense mode (<= 256
-  // registers a wave), one in hub mode (S_T fills the LDS)
-  const unsigned grid = (unsigned)std::min<int64_t>(a.ntiles, (HUB ? 1 : 2) * cu_count());
+  // persistent: 4 waves per workgroup, two workgroups per CU (<= 256 registers a wave)
+  const unsigned grid = (unsigned)std::min<int64_t>(a.ntiles, 2 * cu_count());
   const int np = a.P <= 16 ? 1 : 2;
-  const size_t dyn = HUB ? (size_t)4 * ((size_t)a.nhub * a.F + 2 * (size_t)a.rec_words) : 0;
   const int ks = (a.K + 3) / 4;
-  if (ks <= 8) return launch_ks<8, HUB>(a, np, grid, dyn, s);
-  if (ks <= 13) return launch_ks<13, HUB>(a, np, grid, dyn, s);
-  if (ks <= 16) return launch_ks<16, HUB>(a, np, grid, dyn, s);
-  if (ks <= 25) return launch_ks<25, HUB>(a, np, grid, dyn, s);
-  return launch_ks<32, HUB>(a, np, grid, dyn, s);
+  if (ks <= 8) return launch_ks<8>(a, np, grid, s);
+  if (ks <= 13) return launch_ks<13>(a, np, grid, s);
+  if (ks <= 16) return launch_ks<16>(a, np, grid, s);
+  if (ks <= 25) return launch_ks<25>(a, np, grid, s);
+  return launch_ks<32>(a, np, grid, s);
 }
 
-// the epilogue fields shared by both entry points
+// the epilogue fields of the entry point
 Epi make_epi(const float* bias, int32_t epilogue, const uint8_t* mask, int64_t ldm, int32_t F, float scale, float keep,
              uint64_t seed, uint64_t offset, const uint64_t* rng_base) {
   Epi e;
@@ -410,33 +281,6 @@ Epi make_epi(const float* bias, int32_t epilogue, const uint8_t* mask, int64_t l
   e.stamps = debug_stamps();
   return e;
 }
-
-}  // namespace
-
-// The factored gc1 (gcnk_hubfactor_gc1_f32, csrc/factor.hip) on this kernel:
-// GCNK_EUNSUP where its shape or LDS does not fit (the caller falls back).
-int hubfactor_persistent(int32_t M, int32_t F, int32_t Kc, int32_t nhub, int32_t P, const float* U, int64_t ldu,
-                         const float* W, int64_t ldw, int32_t k0, const float* S, int64_t lds, const int32_t* rec,
-                         int32_t rec_words, const float* bias, int32_t epilogue, const uint8_t* mask, int64_t ldm,
-                         float scale, float keep, uint64_t seed, uint64_t offset, const uint64_t* rng_base,
-                         const float* W2, int64_t ldw2, float* H, int64_t ldh, float* C2, int64_t ldc2, void* stream) {
-  const size_t lds_bytes = (size_t)4 * ((size_t)nhub * F + 2 * (size_t)rec_words) + sizeof(float) * (size_t)kWaves * 16 * kHP +
-                           sizeof(float) * 2 * kWaves * 2 * 64 * 4 + sizeof(float) * 2 * 16 * a_stride(32);
-  if (Kc > 128 || F > 16 * kWaves * kNTQ || F % 4 || lds % 4 || ((uintptr_t)S & 15) || P > kMaxP || ldw % 4 ||
-      ((uintptr_t)(W + (int64_t)k0 * ldw) & 15) || (bias && ((uintptr_t)bias & 15)) || (H && (ldh % 4 || ((uintptr_t)H & 15))) ||
-      rec_words > kThreads * 4 || lds_bytes > 160 * 1024)
-    return GCNK_EUNSUP;
-  DenseArgs a{};
-  a.M = M; a.K = Kc; a.F = F; a.P = P;
-  a.A = U; a.lda = ldu; a.W = W + (int64_t)k0 * ldw; a.ldw = ldw; a.W2 = W2; a.ldw2 = ldw2;
-  a.H = H; a.ldh = ldh; a.C2 = C2; a.ldc2 = ldc2;
-  a.epi = make_epi(bias, epilogue, mask, ldm, F, scale, keep, seed, offset, rng_base);
-  a.ntiles = 2 * ((M + 31) / 32);
-  a.S = S; a.lds = lds; a.nhub = nhub; a.rec = rec; a.rec_words = rec_words;
-  return launch<true>(a, reinterpret_cast<hipStream_t>(stream));
-}
-
-namespace {
 
 }  // namespace
 }  // namespace gcnk
@@ -473,5 +317,5 @@ extern "C" int gcnk_dense_gc1_f32(int32_t M, int32_t K, int32_t F, int32_t P, co
   a.H = H; a.ldh = ldh; a.C2 = C2; a.ldc2 = ldc2;
   a.epi = make_epi(bias, epilogue, drop_mask, ldm, F, drop_scale, keep_prob, seed, offset, rng_base);
   a.ntiles = (M + 15) / 16;
-  return launch<false>(a, reinterpret_cast<hipStream_t>(stream));
+  return launch(a, reinterpret_cast<hipStream_t>(stream));
 }

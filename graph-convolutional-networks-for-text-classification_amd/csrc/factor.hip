@@ -31,10 +31,8 @@
 // No atomics, no hand-off between workgroups: bitwise reproducible.
 #include "gcnk_common.h"
 
-#include <cstring>
 
 #include <algorithm>
-#include <cstdlib>
 
 namespace gcnk {
 namespace {
@@ -66,8 +64,7 @@ struct FactorArgs {
   int32_t M, F, Kc, nhub, P;
   const float* U; int64_t ldu;          // [M x >= Kc], rows in block order
   const float* W; int64_t ldw; int32_t k0;  // W1 rows k0 .. k0 + Kc - 1 (ldw == F: staged flat)
-  const float* S; int64_t lds;          // [nhub x F], or nslab K-slabs of it (S_T = their sum in slab order)
-  int32_t nslab; int64_t slab_stride;   // (csrc/kslab.hip; slabs past the first summed after the DMA wait)
+  const float* S; int64_t lds;          // S_T [nhub x F]
   const int32_t* rec; int32_t rec_words;  // per 32-row block: off[33] | pad | row ids | items int2 {hub, val}
   const float* W2; int64_t ldw2;        // [F x P]
   int32_t u_lds;                        // 1: the block's U rows staged in LDS by 16-B DMA (ldu % 4 == 0, aligned)
@@ -82,29 +79,17 @@ struct FactorArgs {
 #define GCNK_FACTOR_LASTU 1
 #endif
 
-// experiment knob (variant builds only): 1 no W1[Kc] DMA, U loads or U W1 MFMAs,
-// 2 no U W1 MFMAs, 3 no U loads (wrong values: timing only; profiles/r05_factor_zp_ab.log)
-#ifndef GCNK_FACTOR_EXP
-#define GCNK_FACTOR_EXP 0
-#endif
-
 // 1 (default): U's rows staged in LDS by DMA where the block's LDS allows
 #ifndef GCNK_FACTOR_ULDS
 #define GCNK_FACTOR_ULDS 1
 #endif
-
-// float4 registers per thread for S_T's K-slabs past the first
-constexpr int kSlabRegs = 16;
 
 template <int KS>
 __host__ __device__ constexpr int region1_floats(int F, int ntq) {
   return (4 * KS * F + bpad(F, ntq)) > kRB * (64 * ntq + 4) ? (4 * KS * F + bpad(F, ntq)) : kRB * (64 * ntq + 4);
 }
 
-// SLB: S_T arrives as K-slabs (a separate instantiation: the staging registers
-// of the slab path cost the one-slab kernel ~1.2 us at R8's shape when they
-// were merely present, 64 -> 102 VGPRs)
-template <int KS, int NTQ, int NP, bool SLB>
+template <int KS, int NTQ, int NP>
 __global__ void __launch_bounds__(kThreads)
 hubfactor_gc1_kernel(FactorArgs a) {
   resolve_rng(a.epi);
@@ -149,18 +134,18 @@ hubfactor_gc1_kernel(FactorArgs a) {
   {
     const int n4 = a.Kc * Q;  // float4 pieces of W1[k0 .. k0 + Kc) (rows of F floats, ldw == F)
     const float* wsrc = a.W + (int64_t)a.k0 * a.ldw;
-    for (int e0 = wv * 64; e0 < (GCNK_FACTOR_EXP == 1 ? 0 : n4); e0 += kThreads)
+    for (int e0 = wv * 64; e0 < n4; e0 += kThreads)
       if (e0 + lane < n4) lds_dma16(wsrc + 4 * (e0 + lane), s_B + 4 * e0);
     // U's rows by 16-B DMA (the per-lane fragment loads -- 16 rows x 16 B per
     // instruction -- cost ~1.1 us of the block: profiles/r05_factor_ulds_ab.log);
     // one instruction per row, pieces covering Kc (inside the row: ldu % 4 == 0)
-    if (a.u_lds && GCNK_FACTOR_EXP != 1)
+    if (a.u_lds)
       for (int r = wv; r < kRB; r += kThreads / 64)
         if (m0 + r < a.M && 4 * lane < a.Kc) lds_dma16(a.U + (m0 + r) * a.ldu + 4 * lane, s_U + r * KPU);
     const int32_t* rec = a.rec + (int64_t)blk * a.rec_words;
     for (int e0 = wv * 64; e0 < a.rec_words / 4; e0 += kThreads)
       if (e0 + lane < a.rec_words / 4) lds_dma16(rec + 4 * (e0 + lane), s_rec + 4 * e0);
-    const int s4 = a.nhub * Q;  // S_T [nhub x F] flat (lds == F): its first K-slab
+    const int s4 = a.nhub * Q;  // S_T [nhub x F] flat (lds == F)
     for (int e0 = wv * 64; e0 < s4; e0 += kThreads)
       if (e0 + lane < s4) lds_dma16(a.S + 4 * (e0 + lane), s_S + 4 * e0);
     const int w1 = F * a.P;     // W2 [F x P] flat (ldw2 == P), dword pieces
@@ -170,27 +155,13 @@ hubfactor_gc1_kernel(FactorArgs a) {
       for (int e0 = wv * 64; e0 < Q; e0 += kThreads)
         if (e0 + lane < Q) lds_dma16(a.epi.bias + 4 * (e0 + lane), s_bias + 4 * e0);
   }
-  // S_T's further K-slabs (csrc/kslab.hip) into registers in the same round of
-  // loads: slot i holds slab 1 + i / per, piece i % per (piece p = float4
-  // tid + 512 p of the flat [nhub x F]); the host keeps (nslab - 1) per <= kSlabRegs
-  const int per = (a.nhub * Q + kThreads - 1) / kThreads;
-  constexpr int kSR = SLB ? kSlabRegs : 1;
-  float4 sv[kSR];
-#pragma unroll
-  for (int i = 0; i < kSR; ++i) {
-    const int j = 1 + i / per, e = tid + kThreads * (i % per);
-    sv[i] = (SLB && j < a.nslab && e < a.nhub * Q)
-                ? *reinterpret_cast<const float4*>(a.S + j * a.slab_stride + 4 * (int64_t)e)
-                : make_float4(0.f, 0.f, 0.f, 0.f);
-  }
   float af[KS];
   const int64_t urow = m0 + 16 * strip + (lane & 15);
   if (!a.u_lds) {
     const float* up = a.U + urow * a.ldu + (lane >> 4);
 #pragma unroll
     for (int s = 0; s < KS; ++s)
-      af[s] = GCNK_FACTOR_EXP == 3 ? 1e-3f
-              : (GCNK_FACTOR_EXP != 1 && urow < a.M && 4 * s + (lane >> 4) < a.Kc) ? up[4 * s] : 0.f;
+      af[s] = (urow < a.M && 4 * s + (lane >> 4) < a.Kc) ? up[4 * s] : 0.f;
   }
   __builtin_amdgcn_s_waitcnt(0x0F70);  // vmcnt(0): this wave's DMA and fragment loads have landed
   __syncthreads();
@@ -200,22 +171,8 @@ hubfactor_gc1_kernel(FactorArgs a) {
     for (int s = 0; s < KS; ++s) {
       // bit mask, not a select: a select let the compiler sink each read into a
       // branch with its own LDS wait (13 round trips)
-      const bool ok = GCNK_FACTOR_EXP != 1 && urow < a.M && 4 * s + (lane >> 4) < a.Kc;
+      const bool ok = urow < a.M && 4 * s + (lane >> 4) < a.Kc;
       af[s] = __int_as_float(__float_as_int(su[4 * s]) & (ok ? -1 : 0));
-    }
-  }
-  // S_T = ((slab 0 + slab 1) + slab 2) + slab 3, each thread on its own pieces
-  // (slots in slab order); phase 2 reads s_S only after the barriers below
-  if (SLB && a.nslab > 1) {
-#pragma unroll
-    for (int i = 0; i < kSR; ++i) {
-      const int j = 1 + i / per, e = tid + kThreads * (i % per);
-      if (j < a.nslab && e < a.nhub * Q) {
-        float4* d = reinterpret_cast<float4*>(s_S + 4 * e);
-        float4 v = *d;
-        v.x += sv[i].x; v.y += sv[i].y; v.z += sv[i].z; v.w += sv[i].w;
-        *d = v;
-      }
     }
   }
   stamp(a.epi, 0);
@@ -226,7 +183,7 @@ hubfactor_gc1_kernel(FactorArgs a) {
   for (int i = 0; i < NTQ; ++i) acc[i] = f32x4{0.f, 0.f, 0.f, 0.f};
   const int c0 = quarter * NTQ * 16 + (lane & 15);
 #pragma unroll
-  for (int s = 0; s < (GCNK_FACTOR_EXP == 1 || GCNK_FACTOR_EXP == 2 ? 0 : KS); ++s) {
+  for (int s = 0; s < KS; ++s) {
     const float* br = s_B + (4 * s + (lane >> 4)) * F + c0;
     float bf[NTQ];
 #pragma unroll
@@ -399,40 +356,24 @@ extern "C" int64_t gcnk_hubfactor_lds_bytes(int32_t F, int32_t Kc, int32_t nhub,
 
 // The dynamic-LDS limit is raised once per kernel instantiation and device
 // (dyn_lds_attr), then the launch.
-template <int KS, int NTQ, int NP, bool SLB>
-static int launch_factor_s(const FactorArgs& a, int64_t nblk, int64_t lds_b, void* stream) {
+template <int KS, int NTQ, int NP>
+static int launch_factor(const FactorArgs& a, int64_t nblk, int64_t lds_b, void* stream) {
   static std::atomic<uint64_t> done{0};
   const hipError_t attr =
-      dyn_lds_attr(done, reinterpret_cast<const void*>(&hubfactor_gc1_kernel<KS, NTQ, NP, SLB>), 160 * 1024);
+      dyn_lds_attr(done, reinterpret_cast<const void*>(&hubfactor_gc1_kernel<KS, NTQ, NP>), 160 * 1024);
   if (attr != hipSuccess) return hip_check(attr, "hubfactor_gc1_kernel LDS attribute");
-  hipLaunchKernelGGL((hubfactor_gc1_kernel<KS, NTQ, NP, SLB>), dim3((unsigned)nblk), dim3(kThreads), (size_t)lds_b,
+  hipLaunchKernelGGL((hubfactor_gc1_kernel<KS, NTQ, NP>), dim3((unsigned)nblk), dim3(kThreads), (size_t)lds_b,
                      reinterpret_cast<hipStream_t>(stream), a);
   return launch_check("hubfactor_gc1_kernel");
 }
 
-template <int KS, int NTQ, int NP>
-static int launch_factor(const FactorArgs& a, int64_t nblk, int64_t lds_b, void* stream) {
-  return a.nslab > 1 ? launch_factor_s<KS, NTQ, NP, true>(a, nblk, lds_b, stream)
-                     : launch_factor_s<KS, NTQ, NP, false>(a, nblk, lds_b, stream);
-}
-
-extern "C" int gcnk_hubfactor_gc1_slabs_f32(int32_t M, int32_t F, int32_t Kc, int32_t nhub, int32_t P,
-                                            const float* U, int64_t ldu, const float* W, int64_t ldw, int32_t k0,
-                                            const float* S, int64_t lds, int32_t nslab, int64_t slab_stride,
-                                            const int32_t* rec, int32_t rec_words, const float* bias,
-                                            int32_t epilogue, const uint8_t* drop_mask, int64_t ldm,
-                                            float drop_scale, float keep_prob, uint64_t seed, uint64_t offset,
-                                            const uint64_t* rng_base, const float* W2, int64_t ldw2, float* H,
-                                            int64_t ldh, float* C2, int64_t ldc2, void* stream) {
-  if (nslab < 1 || nslab > 4 || (nslab > 1 && slab_stride < (int64_t)nhub * lds)) {
-    set_error("gcnk_hubfactor_gc1_f32: bad K-slab count %d or stride %lld", nslab, (long long)slab_stride);
-    return GCNK_EARG;
-  }
-  if (nslab > 1 && ((int64_t)(nslab - 1) * (((int64_t)nhub * (F / 4) + kThreads - 1) / kThreads) > kSlabRegs ||
-                    slab_stride % 4)) {
-    set_error("gcnk_hubfactor_gc1_f32: %d K-slabs of %d x %d exceed the staging registers", nslab, nhub, F);
-    return GCNK_EUNSUP;
-  }
+extern "C" int gcnk_hubfactor_gc1_f32(int32_t M, int32_t F, int32_t Kc, int32_t nhub, int32_t P, const float* U,
+                                      int64_t ldu, const float* W, int64_t ldw, int32_t k0, const float* S,
+                                      int64_t lds, const int32_t* rec, int32_t rec_words, const float* bias,
+                                      int32_t epilogue, const uint8_t* drop_mask, int64_t ldm, float drop_scale,
+                                      float keep_prob, uint64_t seed, uint64_t offset, const uint64_t* rng_base,
+                                      const float* W2, int64_t ldw2, float* H, int64_t ldh, float* C2,
+                                      int64_t ldc2, void* stream) {
   if (M <= 0 || F <= 0 || Kc <= 0 || nhub <= 0 || P <= 0 || !U || !W || !S || !rec || !W2 || !C2 || k0 < 0) {
     set_error("gcnk_hubfactor_gc1_f32: bad sizes or null operand (M=%d F=%d Kc=%d hubs=%d P=%d)", M, F, Kc, nhub, P);
     return GCNK_EARG;
@@ -458,17 +399,6 @@ extern "C" int gcnk_hubfactor_gc1_slabs_f32(int32_t M, int32_t F, int32_t Kc, in
               (long long)lds_b, F, Kc, nhub);
     return GCNK_EUNSUP;
   }
-  // round 5: GCNK_HUBFACTOR=persistent takes the persistent kernel
-  // (csrc/dense_gc1.hip: W1[Kc] fragments held in registers for the whole
-  // launch, S_T staged once per CU instead of once per 32-row block); read per
-  // call (a hipGraph keeps the choice made at capture)
-  const char* hv = getenv("GCNK_HUBFACTOR");
-  if (nslab == 1 && hv && strcmp(hv, "persistent") == 0) {
-    const int rc = hubfactor_persistent(M, F, Kc, nhub, P, U, ldu, W, ldw, k0, S, lds, rec, rec_words, bias, epilogue,
-                                        drop_mask, ldm, drop_scale, keep_prob, seed, offset, rng_base, W2, ldw2, H,
-                                        ldh, C2, ldc2, stream);
-    if (rc != GCNK_EUNSUP) return rc;
-  }
   FactorArgs a;
   a.M = M; a.F = F; a.Kc = Kc; a.nhub = nhub; a.P = P;
   // U's rows through LDS where they fit (R8: 95 + 8.7 KB; the 20ng-shaped 70
@@ -476,7 +406,6 @@ extern "C" int gcnk_hubfactor_gc1_slabs_f32(int32_t M, int32_t F, int32_t Kc, in
   a.u_lds = GCNK_FACTOR_ULDS && ldu % 4 == 0 && aligned16(U) && lds_b + hubfactor_u_bytes(Kc) <= 160 * 1024;
   a.U = U; a.ldu = ldu; a.W = W; a.ldw = ldw; a.k0 = k0;
   a.S = S; a.lds = lds; a.rec = rec; a.rec_words = rec_words;
-  a.nslab = nslab; a.slab_stride = slab_stride;
   a.W2 = W2; a.ldw2 = ldw2; a.H = H; a.ldh = ldh; a.C2 = C2; a.ldc2 = ldc2;
   Epi& e = a.epi;
   e.bias = bias; e.mask = drop_mask; e.scale = drop_scale; e.keep_prob = keep_prob;
@@ -497,16 +426,4 @@ extern "C" int gcnk_hubfactor_gc1_slabs_f32(int32_t M, int32_t F, int32_t Kc, in
 #undef GCNK_FACTOR_CASE
   set_error("gcnk_hubfactor_gc1_f32: no kernel for Kc=%d F=%d", Kc, F);
   return GCNK_EUNSUP;
-}
-
-extern "C" int gcnk_hubfactor_gc1_f32(int32_t M, int32_t F, int32_t Kc, int32_t nhub, int32_t P, const float* U,
-                                      int64_t ldu, const float* W, int64_t ldw, int32_t k0, const float* S,
-                                      int64_t lds, const int32_t* rec, int32_t rec_words, const float* bias,
-                                      int32_t epilogue, const uint8_t* drop_mask, int64_t ldm, float drop_scale,
-                                      float keep_prob, uint64_t seed, uint64_t offset, const uint64_t* rng_base,
-                                      const float* W2, int64_t ldw2, float* H, int64_t ldh, float* C2,
-                                      int64_t ldc2, void* stream) {
-  return gcnk_hubfactor_gc1_slabs_f32(M, F, Kc, nhub, P, U, ldu, W, ldw, k0, S, lds, 1, 0, rec, rec_words, bias,
-                                      epilogue, drop_mask, ldm, drop_scale, keep_prob, seed, offset, rng_base, W2,
-                                      ldw2, H, ldh, C2, ldc2, stream);
 }

@@ -24,15 +24,9 @@ int spmm_ref(const gcnk_plan_ref& p, const float* B, int64_t ldb, int32_t F, flo
 
 // S1 = X W1 (sparse X through its plan, dense X on the MFMA GEMM)
 int first_product(const gcnk_gcn_fwd& r, const float* W1, void* stream) {
-  if (r.s1_slabs > 1 && r.x_dense)   // S_T as K-slabs, summed by the factored gc1
-    return gcnk_gemm_kslabs_f32(r.x_rows, r.F, r.x_cols, r.x_dense, r.ldx, W1, r.F, r.s1_slabs, r.s1, r.lds1,
-                                r.s1_slab_stride, stream);
   if (r.x.plan)
     return spmm_ref(r.x, W1, r.F, r.F, r.s1, r.lds1, nullptr, GCNK_EPI_NONE, nullptr, 0, 1.f, 1.f, 0, 0, nullptr,
                     stream);
-  if (r.x_ctr)
-    return gcnk_gemm_smallm_f32(r.x_rows, r.F, r.x_cols, r.x_dense, r.ldx, W1, r.F, r.s1, r.lds1, 0, r.gemm_ws,
-                                r.gemm_ws_bytes, r.x_ctr, r.x_ctr_bytes, stream);
   return gcnk_gemm_f32(0, 0, r.x_rows, r.F, r.x_cols, r.x_dense, r.ldx, W1, r.F, r.s1, r.lds1, nullptr,
                        GCNK_GEMM_EPI_NONE, nullptr, 0, 1.f, r.x_split_k, r.gemm_ws, r.gemm_ws_bytes, stream);
 }
@@ -63,10 +57,9 @@ extern "C" int gcnk_gcn_forward_f32(const gcnk_gcn_fwd* rec, const float* W1, co
   switch (r.kind) {
     case GCNK_FWD_FACTORED:
       if ((rc = first_product(r, W1, stream)) != GCNK_OK) return rc;
-      rc = gcnk_hubfactor_gc1_slabs_f32(r.M, r.F, r.Kc, r.nhub, r.P, r.U, r.ldu, W1, r.F, r.k0, r.s1, r.lds1,
-                                        (r.s1_slabs > 1 && r.x_dense) ? r.s1_slabs : 1, r.s1_slab_stride, r.rec,
-                                        r.rec_words, b1, epilogue, drop_mask, ldm, drop_scale, keep_prob, seed,
-                                        offset, rng_base, W2, r.P, H1, ldh, r.s2, r.lds2, stream);
+      rc = gcnk_hubfactor_gc1_f32(r.M, r.F, r.Kc, r.nhub, r.P, r.U, r.ldu, W1, r.F, r.k0, r.s1, r.lds1, r.rec,
+                                  r.rec_words, b1, epilogue, drop_mask, ldm, drop_scale, keep_prob, seed, offset,
+                                  rng_base, W2, r.P, H1, ldh, r.s2, r.lds2, stream);
       break;
     case GCNK_FWD_DENSE_AX:
       rc = gcnk_dense_gc1_f32(r.M, r.Kc, r.F, r.P, r.U, r.ldu, W1, r.F, b1, epilogue, drop_mask, ldm, drop_scale,
@@ -110,9 +103,7 @@ extern "C" int32_t gcnk_gcn_fwd_layout(int64_t* out, int32_t n) {
                        (int64_t)offsetof(gcnk_gcn_fwd, aF), (int64_t)offsetof(gcnk_gcn_fwd, aP),
                        (int64_t)offsetof(gcnk_gcn_fwd, ld_h1_tmp), (int64_t)offsetof(gcnk_plan_ref, lanes_hint),
                        (int64_t)sizeof(gcnk_gcn_bwd), (int64_t)offsetof(gcnk_gcn_bwd, xT),
-                       (int64_t)offsetof(gcnk_gcn_bwd, bwd2_ws_bytes), (int64_t)offsetof(gcnk_gcn_fwd, x_ctr),
-                       (int64_t)offsetof(gcnk_gcn_bwd, aTH), (int64_t)offsetof(gcnk_gcn_bwd, sm_ctr_bytes),
-                       (int64_t)offsetof(gcnk_gcn_fwd, s1_slabs), (int64_t)offsetof(gcnk_gcn_fwd, s1_slab_stride)};
+                       (int64_t)offsetof(gcnk_gcn_bwd, bwd2_ws_bytes)};
   const int32_t m = (int32_t)(sizeof(v) / sizeof(v[0]));
   for (int32_t i = 0; i < n && i < m; ++i) out[i] = v[i];
   return m;
@@ -123,12 +114,9 @@ extern "C" int gcnk_gcn_backward_f32(const gcnk_gcn_bwd* rec, const float* G, co
                                      const float* W2, float scale, float* gW1, float* gb1, float* gW2, float* gb2,
                                      void* stream) {
   const bool ax = (rec && (rec->flags & GCNK_BWD_AX_DIRECT));
-  const bool fac = (rec && (rec->flags & GCNK_BWD_FACTORED));
   if (!rec || !G || !H1 || !W2 || rec->M <= 0 || rec->F <= 0 || rec->P <= 0 || ldh < rec->F || !rec->aTP.plan ||
       !rec->gS2 || !rec->gZ1 ||
-      (gW1 && (ax    ? !rec->x_dense
-               : fac ? (!rec->aTH.plan || !rec->x_hubT || !rec->UT || !rec->y || !rec->sm_ctr || rec->Kc <= 0)
-                     : (!rec->aTF.plan || !rec->gS1 || (!rec->xT.plan && !rec->x_dense))))) {
+      (gW1 && (ax ? !rec->x_dense : (!rec->aTF.plan || !rec->gS1 || (!rec->xT.plan && !rec->x_dense))))) {
     set_error("gcnk_gcn_backward_f32: null record/operand or incomplete record");
     return GCNK_EARG;
   }
@@ -146,22 +134,6 @@ extern "C" int gcnk_gcn_backward_f32(const gcnk_gcn_bwd* rec, const float* G, co
   if (ax)  // gW1 = (A-hat X)^T gZ1: the DENSE_AX forward's Z1 = (A-hat X) W1
     return gcnk_gemm_f32(1, 0, r.x_cols, r.F, r.x_rows, r.x_dense, r.ldx, r.gZ1, r.F, gW1, r.F, nullptr,
                          GCNK_GEMM_EPI_NONE, nullptr, 0, 1.f, r.x_split_k, r.gemm_ws, r.gemm_ws_bytes, stream);
-  if (fac) {  // gW1 = X_hubs^T (A_H^T gZ1) + U~^T gZ1 (factor.HubFactor.grad_w1)
-    if ((rc = spmm_ref(r.aTH, r.gZ1, r.F, r.F, r.y, r.F, nullptr, GCNK_EPI_NONE, nullptr, 0, 1.f, 1.f, 0, 0, nullptr,
-                       stream)) != GCNK_OK)
-      return rc;
-    if ((rc = gcnk_gemm_f32(0, 0, r.x_cols, r.F, r.nhub_p, r.x_hubT, r.ld_xhT, r.y, r.F, gW1, r.F, nullptr,
-                            GCNK_GEMM_EPI_NONE, nullptr, 0, 1.f, 1, nullptr, 0, stream)) != GCNK_OK)
-      return rc;
-    for (int32_t c0 = 0; c0 < r.Kc; c0 += 64) {
-      const int32_t rows = r.Kc - c0 < 64 ? r.Kc - c0 : 64;
-      if ((rc = gcnk_gemm_smallm_f32(rows, r.F, r.M, r.UT + (int64_t)c0 * r.ldut, r.ldut, r.gZ1, r.F,
-                                     gW1 + (int64_t)(r.k0 + c0) * r.F, r.F, 1, r.sm_ws, r.sm_ws_bytes, r.sm_ctr,
-                                     r.sm_ctr_bytes, stream)) != GCNK_OK)
-        return rc;
-    }
-    return GCNK_OK;
-  }
   // gS1 = A-hat^T gZ1, gW1 = X^T gS1  (autograd of layer.py:106, :102 in gc1)
   if ((rc = spmm_ref(r.aTF, r.gZ1, r.F, r.F, r.gS1, r.F, nullptr, GCNK_EPI_NONE, nullptr, 0, 1.f, 1.f, 0, 0, nullptr,
                      stream)) != GCNK_OK)

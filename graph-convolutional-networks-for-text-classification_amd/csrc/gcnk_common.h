@@ -47,15 +47,6 @@ inline hipError_t dyn_lds_attr(std::atomic<uint64_t>& done, const void* fn, int 
 
 inline bool aligned16(const void* p) { return (reinterpret_cast<uintptr_t>(p) & 15u) == 0; }
 
-// The factored gc1 on the persistent register-resident kernel (csrc/dense_gc1.hip);
-// GCNK_EUNSUP where it does not apply (gcnk_hubfactor_gc1_f32 then runs its
-// per-block kernel, csrc/factor.hip).
-int hubfactor_persistent(int32_t M, int32_t F, int32_t Kc, int32_t nhub, int32_t P, const float* U, int64_t ldu,
-                         const float* W, int64_t ldw, int32_t k0, const float* S, int64_t lds, const int32_t* rec,
-                         int32_t rec_words, const float* bias, int32_t epilogue, const uint8_t* mask, int64_t ldm,
-                         float scale, float keep, uint64_t seed, uint64_t offset, const uint64_t* rng_base,
-                         const float* W2, int64_t ldw2, float* H, int64_t ldh, float* C2, int64_t ldc2, void* stream);
-
 // ----------------------------------------------------------------------------
 // Epilogue parameters for SpMM (row-complete elements).
 struct Epi {

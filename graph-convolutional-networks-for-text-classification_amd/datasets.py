@@ -120,6 +120,52 @@ def uniform_random_csr(n, nnz, seed=0, device="cpu"):
     return rowptr.to(torch.int32).to(device), idx[1].to(torch.int32).to(device), t.values().to(device)
 
 
+def rmat_csr(scale, nnz, a=0.57, b=0.19, c=0.19, seed=0, device="cpu", permute=True):
+    """Power-law variant of BASELINE config 4 (R-MAT(0.57,
+    0.19, 0.19), reported separately): 2^scale nodes, ``nnz`` edges drawn by
+    recursive quadrant choice (probabilities a, b, c, 1 - a - b - c per level,
+    torch.Generator(seed)), node ids relabelled by a seeded permutation (as
+    Graph500 does, so degree is not correlated with id), values U[0, 1),
+    duplicates summed (coalesce) -> (rowptr, colind, val) int32/fp32.  At
+    scale 20 / 20M edges the largest row holds ~10^5 nonzeros: the heavy-row
+    case a uniform graph never has."""
+    n = 1 << scale
+    g = torch.Generator().manual_seed(seed)
+    rows = torch.zeros(nnz, dtype=torch.int64)
+    cols = torch.zeros(nnz, dtype=torch.int64)
+    for _ in range(scale):
+        r = torch.rand(nnz, generator=g)
+        rbit = (r >= a + b).to(torch.int64)
+        cbit = (((r >= a) & (r < a + b)) | (r >= a + b + c)).to(torch.int64)
+        rows.mul_(2).add_(rbit)
+        cols.mul_(2).add_(cbit)
+        del r, rbit, cbit
+    if permute:
+        p = torch.randperm(n, generator=g)
+        rows, cols = p[rows], p[cols]
+    vals = torch.rand(nnz, generator=g)
+    t = torch.sparse_coo_tensor(torch.stack([rows, cols]), vals, (n, n)).coalesce()
+    del rows, cols, vals
+    idx = t.indices()
+    rowptr = torch.zeros(n + 1, dtype=torch.int64)
+    rowptr[1:] = torch.cumsum(torch.bincount(idx[0], minlength=n), 0)
+    return rowptr.to(torch.int32).to(device), idx[1].to(torch.int32).to(device), t.values().to(device)
+
+
+def reference_coo(rowptr, colind, val, shape):
+    """The torch sparse COO the reference would hand th.spmm for this matrix
+    (utils.py:196-203: ``sparse_mx.tocoo()`` of the normalised matrix, which
+    comes out of normalize_adj's transpose in COLUMN-major order, int64
+    indices, fp32 values, not flagged coalesced) -- the CPU baseline's input
+    for the synthetic configs."""
+    rp = torch.as_tensor(rowptr).to("cpu", torch.int64)
+    ci = torch.as_tensor(colind).to("cpu", torch.int64)
+    v = torch.as_tensor(val).to("cpu", torch.float32)
+    rows = torch.repeat_interleave(torch.arange(shape[0], dtype=torch.int64), rp[1:] - rp[:-1])
+    order = torch.argsort(ci * shape[0] + rows, stable=True)
+    return torch.sparse_coo_tensor(torch.stack([rows[order], ci[order]]), v[order], shape)
+
+
 def load_edgelist(path, device=None):
     """The graph file the reference's builder writes (build_graph.py:199,
     "u v weight" lines) -> the symmetric float32 adjacency A that

@@ -20,7 +20,6 @@ dropout + the gc2 projection H1 W2), and the hub rows' 600-term gather sums
 of the SpMM never run.  The association differs from A (X W1) only in fp32
 rounding (checked against the reference's goldens to 1e-4, tests/).
 """
-import os
 import threading
 
 import numpy as np
@@ -29,25 +28,17 @@ import torch
 from .sparse import CSR
 
 MAX_HUBS = 128    # hub rows staged in LDS (S_T [hubs x F]; the kernel checks the LDS budget)
-# X[hubs] W1 (R8: 50 dense hub rows x 7463): "spmm" (default) -- the SpMM tile
-# plan on their CSR plus its slab reduce (9.8 us per call; 6.8 + 4.9 us in the
-# forward's trace); "gemm" -- a dense copy of the hub rows through the small-M
-# split-K MFMA GEMM (csrc/gemm.hip gemm_smallm_splitk_kernel + slab reduce:
-# 10.4 us per call, 7.7 + 4.7 in the trace, profiles/r04_smallm_*; the generic
-# tiled GEMM took 13.7).  A one-launch split-K kernel with two levels of
-# last-arriver slab sums measured 12.1 us (round 4, DESIGN §5: each coherent
-# hand-off is a ~2 us memory round trip) and was removed.
-# "slabs" (round 5): a dense copy of the hub rows through gcnk_gemm_kslabs_f32
-# into SLABS K-slabs (csrc/kslab.hip), summed by the factored gc1 while it
-# stages S_T -- no reduction launch, no hand-off.  Measured slower on R8: the
-# 4-deep slabs leave 238 KB of loads per workgroup (11.9 us) and the factored gc1
-# slows 9.9 -> 13.2 us staging 4 slabs (profiles/r05_fwdtrace_r8_slabs_*).
-# "onepass" (round 5): a dense copy of the hub rows through the one-launch
-# small-M GEMM (csrc/smallm.hip: ~20 K ranges x 16-column tiles, each tile's
-# partials summed by its last workgroup) -- no slab-reduce launch, but measured
-# slower: 12.2 us, ~4 us of it the coherent hand-off (profiles/r05_smallm_*).
-XHUB = os.environ.get("GCNK_FACTOR_XHUB", "spmm")
-SLABS = int(os.environ.get("GCNK_FACTOR_SLABS", "4"))
+# X[hubs] W1 (R8: 50 dense hub rows x 7463): the SpMM tile plan on their CSR
+# plus its slab reduce (9.8 us per call; 6.8 + 4.9 us in the forward's trace);
+# dense X's hub rows: the MFMA GEMM (gcnk_gemm_f32, small-M split-K).  Measured
+# and removed (DESIGN.md keeps the numbers): a dense copy of the sparse hub rows
+# through the small-M split-K GEMM (10.4 us per call, profiles/r04_smallm_*), a
+# one-launch split-K kernel with two levels of last-arriver slab sums (12.1 us,
+# round 4), <= 4 K-slabs summed by the factored gc1 while it stages S_T (slab
+# GEMM 11.9 us + factored gc1 9.9 -> 13.2 us, profiles/r05_fwdtrace_r8_slabs_*;
+# kslab.hip, ABI 11) and a one-launch small-M GEMM whose tiles' last workgroups
+# sum the partials (12.2 us, ~4 of it the coherent hand-off,
+# profiles/r05_smallm_*; smallm.hip, ABI 11).
 MAX_KC = 128      # X's light-row column range (U's width)
 ROWS_PER_BLOCK = 32   # csrc/factor.hip kRB
 # record words before the items: 33 row offsets | 3 pad | 32 row ids (-1 past
@@ -65,106 +56,13 @@ class HubFactor:
     """The (A-hat, X)-fixed operands of the factored gc1, resident on the device."""
 
     __slots__ = ("M", "H", "K", "hubs", "k0", "Kc", "U", "perm", "rec", "rec_words", "nblk", "x_hub",
-                 "x_hub_dense", "_src", "_bwd")
-
-    def backward_operands(self, adj):
-        """(UT, aT_hub, x_hubT, Hp) for the factored gW1 (built on first use):
-
-            gW1 = X^T A-hat^T gZ1 = U~^T gZ1 + X_hubs^T (A_H^T gZ1)
-
-        (A-hat X = U~ + A_H X_hubs, U~ = U placed in X's columns k0 .. k0 + Kc).
-        UT [Kc x Mp]: U in row order, transposed, rows padded to 4 floats;
-        aT_hub: the CSR of A-hat^T's hub rows (A_H^T); x_hubT [K x Hp]: X's hub
-        rows transposed, Hp = H rounded up to 4, zero past H."""
-        b = getattr(self, "_bwd", None)
-        if b is not None:
-            return b
-        dev = self.U.device
-        M, H = self.M, self.H
-        Mp, Hp = (M + 3) // 4 * 4, (H + 3) // 4 * 4
-        inv = torch.empty(M, dtype=torch.int64)
-        inv[self.perm] = torch.arange(M)
-        UT = torch.zeros((self.Kc, Mp), dtype=torch.float32, device=dev)
-        UT[:, :M] = self.U[inv.to(dev), :self.Kc].t()
-        aT = adj.t()
-        rp = aT.rowptr.long()
-        lens = rp[self.hubs + 1] - rp[self.hubs]
-        hrp = torch.zeros(H + 1, dtype=torch.int64, device=dev)
-        hrp[1:] = torch.cumsum(lens, 0)
-        tot = int(hrp[-1])
-        idx = torch.repeat_interleave(rp[self.hubs] - hrp[:-1], lens, output_size=tot) + \
-            torch.arange(tot, device=dev, dtype=torch.int64)
-        aT_hub = CSR(hrp.to(torch.int32), aT.colind[idx], aT.val[idx], (H, M))
-        if self.x_hub_dense is not None:
-            xd = self.x_hub_dense
-        else:
-            xd = torch.zeros((H, self.K), dtype=torch.float32, device=dev)
-            xrp = self.x_hub.rowptr.long()
-            rows = torch.repeat_interleave(torch.arange(H, device=dev), xrp[1:] - xrp[:-1],
-                                           output_size=self.x_hub.nnz)
-            xd.index_put_((rows, self.x_hub.colind.long()), self.x_hub.val, accumulate=True)
-        x_hubT = torch.zeros((self.K, Hp), dtype=torch.float32, device=dev)
-        x_hubT[:, :H] = xd.t()
-        self._bwd = b = (UT, aT_hub, x_hubT, Hp)
-        return b
-
-    def grad_w1(self, adj, gZ1, out=None):
-        """gW1 [K x F] of the factored gc1 from gZ1 = dL/d(A-hat X W1)  (the
-        autograd of reference layer.py:102,106 in gc1): A_H^T gZ1 on the SpMM
-        (the hub rows of A-hat^T), X_hubs^T times it on the short-K GEMM, then
-        U^T gZ1 added into rows k0 .. k0 + Kc on the one-pass small-M GEMM."""
-        from .ops import gemm, gemm_smallm, spmm
-        UT, aT_hub, x_hubT, Hp = self.backward_operands(adj)
-        F = gZ1.shape[1]
-        Y = torch.zeros((Hp, F), dtype=torch.float32, device=gZ1.device)
-        spmm(aT_hub, gZ1, out=Y[:self.H])
-        gW1 = gemm(x_hubT, Y, out=out)
-        for c0 in range(0, self.Kc, 64):
-            c1 = min(self.Kc, c0 + 64)
-            gemm_smallm(UT[c0:c1], gZ1, out=gW1[self.k0 + c0:self.k0 + c1], accumulate=True)
-        return gW1
-
-    def onepass(self):
-        """X_hubs W1 runs on the one-launch small-M GEMM (gcnk_gemm_smallm_f32)."""
-        return XHUB == "onepass" and self.x_hub_dense is not None and self.H <= 64 and \
-            self.x_hub_dense.stride(0) % 4 == 0
-
-    def slabs(self, F):
-        """K-slabs of S_T = X_hubs W1 (gcnk_gemm_kslabs_f32, summed by
-        gcnk_hubfactor_gc1_slabs_f32) at width F; 1 = one whole S_T.  Bounded by
-        the kernel's staging registers: (slabs - 1) ceil(H F / 2048) <= 16."""
-        if XHUB != "slabs" or self.x_hub_dense is None or self.x_hub_dense.stride(0) % 4:
-            return 1
-        per = (self.H * (F // 4) + 511) // 512
-        n = max(1, min(SLABS, 4, 1 + 16 // max(1, per)))
-        kx = self.x_hub_dense.shape[1]
-        while n > 1 and ((kx + 15) // 16 + n - 1) // n > 24 * 8:   # the kernel's chunks per slab
-            n -= 1
-        return n if n > 1 and ((kx + 15) // 16 + n - 1) // n <= 24 * 8 else 1
-
-    def hub_slabs(self, W):
-        """(S, nslab): S_T = X[hubs] @ W as nslab K-slabs stacked [nslab H x F]
-        (gcnk_gemm_kslabs_f32), or the whole S_T with nslab 1."""
-        n = self.slabs(W.shape[1])
-        if n == 1:
-            return self.hub_times(W).contiguous(), 1
-        from . import _lib
-        H, F = self.H, W.shape[1]
-        S = torch.empty((n * H, F), dtype=torch.float32, device=W.device)
-        xd = self.x_hub_dense
-        with torch.cuda.device(W.device):
-            _lib.check(_lib.load().gcnk_gemm_kslabs_f32(
-                H, F, xd.shape[1], xd.data_ptr(), xd.stride(0), W.data_ptr(), W.stride(0), n, S.data_ptr(), F, H * F,
-                torch.cuda.current_stream(W.device).cuda_stream), "gcnk_gemm_kslabs_f32")
-        return S, n
+                 "x_hub_dense", "_src")
 
     def hub_times(self, W):
         """S_T = X[hubs] @ W  (the hub rows of reference layer.py:102)."""
-        from .ops import gemm, gemm_smallm, spmm
+        from .ops import gemm, spmm
         if self.x_hub_dense is None:
             return spmm(self.x_hub, W)
-        if self.onepass():
-            return gemm_smallm(self.x_hub_dense, W)
         return gemm(self.x_hub_dense, W)
 
 
@@ -277,14 +175,6 @@ def build(adj, xop):
             torch.arange(tot, device=dev, dtype=torch.int64)
         f.x_hub = CSR(hrp.to(torch.int32), x.colind[idx], x.val[idx], (H, x.shape[1]))
         f.x_hub_dense = None
-        kx = x.shape[1]
-        fits = H * kx * 4 <= 64 << 20
-        if fits and XHUB in ("gemm", "onepass", "slabs"):
-            # rows padded to a multiple of 4 floats (the GEMM's float4 loads)
-            d = torch.zeros((H, (kx + 3) // 4 * 4), dtype=torch.float32, device=dev)
-            d[torch.repeat_interleave(torch.arange(H, device=dev), lens, output_size=tot), x.colind[idx].long()] = \
-                x.val[idx]
-            f.x_hub_dense = d[:, :kx]
     else:
         f.x_hub = None
         kx = xop.shape[1]

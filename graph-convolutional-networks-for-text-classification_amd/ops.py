@@ -210,9 +210,8 @@ def factor_for(adj, xop):
 def hubfactor_gc1(f, W1, b1, W2, epilogue=_lib.EPI_BIAS_RELU, mask=None, scale=1.0, keep_prob=1.0, seed=0,
                   offset=0, rng_base=None, store_h1=True, S=None):
     """(H1, S2) of gc1 + gc2's support through the hub factorisation ``f``
-    (factor.HubFactor): S_T = X[hubs] W1 (layer.py:102; K-slabs on
-    gcnk_gemm_kslabs_f32 where factor.slabs allows), then one launch of
-    gcnk_hubfactor_gc1_slabs_f32 (the slabs summed while staging S_T) -- H1 = drop(relu(A-hat X W1 + b1))
+    (factor.HubFactor): S_T = X[hubs] W1 (layer.py:102), then one launch of
+    gcnk_hubfactor_gc1_f32 -- H1 = drop(relu(A-hat X W1 + b1))
     (layer.py:106,110,182,185) and S2 = H1 W2 (layer.py:102, gc2).  Returns
     None when the shapes are outside the kernel's range (the caller takes the
     SpMM path).  ``S``: S_T already computed (timing probes)."""
@@ -229,7 +228,8 @@ def hubfactor_gc1(f, W1, b1, W2, epilogue=_lib.EPI_BIAS_RELU, mask=None, scale=1
     lib = _lib.load()
     if int(lib.gcnk_hubfactor_lds_bytes(F, f.Kc, f.H, f.rec_words, P)) > 160 * 1024:
         return None
-    S, nslab = f.hub_slabs(W1) if S is None else (S, 1)
+    if S is None:
+        S = f.hub_times(W1).contiguous()
     H1 = torch.empty((M, F), dtype=torch.float32, device=W1.device) if store_h1 else None
     S2 = torch.empty((M, P), dtype=torch.float32, device=W1.device)
     if b1 is not None:
@@ -237,15 +237,15 @@ def hubfactor_gc1(f, W1, b1, W2, epilogue=_lib.EPI_BIAS_RELU, mask=None, scale=1
     if mask is not None:
         mask = mask.contiguous()
     with torch.cuda.device(W1.device):
-        rc = lib.gcnk_hubfactor_gc1_slabs_f32(
+        rc = lib.gcnk_hubfactor_gc1_f32(
             M, F, f.Kc, f.H, P, _ptr(f.U), f.U.stride(0), _ptr(W1), W1.stride(0), f.k0, _ptr(S), S.stride(0),
-            nslab, f.H * S.stride(0), _ptr(f.rec), f.rec_words, _ptr(b1), epilogue,
+            _ptr(f.rec), f.rec_words, _ptr(b1), epilogue,
             _ptr(mask), mask.stride(0) if mask is not None else 0, float(scale),
             float(keep_prob), int(seed) & (2**64 - 1), int(offset) & (2**64 - 1), _ptr(rng_base),
             _ptr(W2), W2.stride(0), _ptr(H1), F, _ptr(S2), P, _stream(W1.device))
     if rc == _lib.EUNSUP:
         return None
-    _lib.check(rc, "gcnk_hubfactor_gc1_slabs_f32")
+    _lib.check(rc, "gcnk_hubfactor_gc1_f32")
     return H1, S2
 
 
@@ -303,7 +303,9 @@ def dense_gc1(d, W1, b1, W2, epilogue=_lib.EPI_BIAS_RELU, mask=None, scale=1.0, 
               rng_base=None, store_h1=True):
     """(H1, S2) of gc1 + gc2's support from A-hat X (DenseAX ``d``): one launch of
     gcnk_dense_gc1_f32 -- H1 = drop(relu((A-hat X) W1 + b1)) (reference
-    layer.py:102,106,110,182,185) and S2 = H1 W2 (layer.py:102, gc2)."""
+    layer.py:102,106,110,182,185) and S2 = H1 W2 (layer.py:102, gc2).  None
+    where the kernel refuses the operands (GCNK_EUNSUP: rows of W1 / b1 / H1
+    that are not 16-B aligned): the caller then takes the SpMM path."""
     W1 = _dense_f32(W1, "gc1 weight")
     W2 = _dense_f32(W2, "gc2 weight")
     _check_rng_base(rng_base, W1.device)
@@ -323,48 +325,10 @@ def dense_gc1(d, W1, b1, W2, epilogue=_lib.EPI_BIAS_RELU, mask=None, scale=1.0, 
             _ptr(mask), mask.stride(0) if mask is not None else 0, float(scale),
             float(keep_prob), int(seed) & (2**64 - 1), int(offset) & (2**64 - 1), _ptr(rng_base),
             _ptr(W2), W2.stride(0), _ptr(H1), F, _ptr(S2), P, _stream(W1.device))
+    if rc == _lib.EUNSUP:
+        return None
     _lib.check(rc, "gcnk_dense_gc1_f32")
     return H1, S2
-
-
-_SMALLM_SCRATCH = {}
-
-
-def _smallm_scratch(M, N, K, dev):
-    """(workspace, zeroed counter region) of gcnk_gemm_smallm_f32 for torch's
-    current stream: concurrent calls on different streams never share a
-    counter region; a captured graph keeps using the ones it was captured with
-    (never freed)."""
-    key = (M, N, K, dev.index, torch.cuda.current_stream(dev).cuda_stream)
-    hit = _SMALLM_SCRATCH.get(key)
-    if hit is None:
-        lib = _lib.load()
-        wsb, cb = int(lib.gcnk_gemm_smallm_workspace_bytes(M, N, K)), int(lib.gcnk_gemm_smallm_counter_bytes(N))
-        hit = _SMALLM_SCRATCH[key] = (torch.empty((wsb + 3) // 4, dtype=torch.float32, device=dev), wsb,
-                                      torch.zeros((cb + 3) // 4, dtype=torch.int32, device=dev), cb)
-    return hit
-
-
-def gemm_smallm(A, B, out=None, accumulate=False):
-    """C = A @ B (``accumulate``: out += A @ B) for A [M x K] with M <= 64 (the
-    dense hub rows of X times W1, reference layer.py:102 on the topic rows) in
-    one launch (gcnk_gemm_smallm_f32).  A's and B's rows must be padded to a
-    multiple of 4 floats (stride(0) % 4 == 0) and 16-B aligned."""
-    A = _dense_f32(A, "A")
-    B = _dense_f32(B, "B")
-    M, K = A.shape
-    if B.shape[0] != K:
-        raise RuntimeError(f"gemm_smallm shape mismatch: {tuple(A.shape)} @ {tuple(B.shape)}")
-    N = B.shape[1]
-    if out is None:
-        out = torch.empty((M, N), dtype=torch.float32, device=A.device)
-    ws, wsb, ctr, cb = _smallm_scratch(M, N, K, A.device)
-    with torch.cuda.device(A.device):
-        rc = _lib.load().gcnk_gemm_smallm_f32(M, N, K, _ptr(A), A.stride(0), _ptr(B), B.stride(0), _ptr(out),
-                                              out.stride(0), int(bool(accumulate)), _ptr(ws), wsb, _ptr(ctr), cb,
-                                              _stream(A.device))
-    _lib.check(rc, "gcnk_gemm_smallm_f32")
-    return out
 
 
 def default_split_k(M, N, K, trans=False):
@@ -576,14 +540,10 @@ class GraphConvFn(torch.autograd.Function):
         return gW, gb, gx, None, None
 
 
-# The factored forward's gW1 through the factor (factor.HubFactor.grad_w1:
-# A_H^T gZ1, X_hubs^T on the short-K GEMM, U^T gZ1 on the small-M GEMM) instead of
-# A-hat^T gZ1 at F then X^T gS1.  Off by default (GCNK_FACTOR_BWD=1 turns it on):
-# in R8's replayed training step it took 8.1 + 7.3 + 14.8 = 30.2 us against
-# 8.5 + 9.4 + 4.9 = 22.8 for the latter (profiles/r05_train_trace.json) -- U^T gZ1
-# is the same [50 x 7724] x [7724 x 200] long-K product as X_hubs W1, with no
-# faster kernel for it.
-FACTOR_BWD = os.environ.get("GCNK_FACTOR_BWD", "0") == "1"
+# (ABI 11 also had the factored forward's gW1 through the factor -- A_H^T gZ1,
+# X_hubs^T on the short-K GEMM, U^T gZ1 on a one-pass small-M GEMM: 30.2 us in
+# R8's replayed step against 22.8 for A-hat^T gZ1 + X^T gS1,
+# profiles/r05_train_trace.json -- removed in ABI 12.)
 
 
 # The whole forward from one C call (record.py, gcnk_gcn_forward_f32) wherever
@@ -621,6 +581,8 @@ def record_forward(W1, b1, W2, b2, xop, adj, epi, mask, scale, keep, seed, offse
     rec, stream = record.get(adj, xop, F, P, dev)
     if rec is None:
         return None
+    if rec.kind == record.DENSE_AX and not all(t is None or t.data_ptr() % 16 == 0 for t in (W1, b1)):
+        return None   # (gcnk_dense_gc1_f32 takes 16-B aligned W1 / b1 rows: the per-op path falls back)
     return rec.run(W1, b1, W2, b2, epi, mask, float(scale), float(keep), int(seed), int(offset), rng_base,
                    keep_h1, stream)
 
@@ -731,8 +693,6 @@ class GCNFn(torch.autograd.Function):
         if need[0]:
             if ctx.dax is not None:   # Z1 = (A-hat X) W1  =>  gW1 = (A-hat X)^T gZ1
                 gW1 = gemm(ctx.dax.AX[:, :ctx.dax.K], gZ1, transA=True)
-            elif ctx.fac is not None and FACTOR_BWD:   # A-hat X = U~ + A_H X_hubs (factor.py)
-                gW1 = ctx.fac.grad_w1(ctx.adj, gZ1.contiguous())
             else:
                 gS1 = spmm(adjT, gZ1)
                 gW1 = ctx.xop.t_times(gS1)

@@ -39,9 +39,7 @@ class GcnFwd(_c.Structure):
                 ("Kc", _c.c_int32), ("nhub", _c.c_int32), ("k0", _c.c_int32), ("rec_words", _c.c_int32),
                 ("U", _c.c_void_p), ("ldu", _c.c_int64), ("rec", _c.c_void_p),
                 ("aF", PlanRef), ("aP", PlanRef), ("s2", _c.c_void_p), ("lds2", _c.c_int64),
-                ("h1_tmp", _c.c_void_p), ("ld_h1_tmp", _c.c_int64), ("x_ctr", _c.c_void_p),
-                ("x_ctr_bytes", _c.c_int64), ("s1_slabs", _c.c_int32), ("pad2_", _c.c_int32),
-                ("s1_slab_stride", _c.c_int64)]
+                ("h1_tmp", _c.c_void_p), ("ld_h1_tmp", _c.c_int64)]
 
 
 class GcnBwd(_c.Structure):
@@ -51,16 +49,12 @@ class GcnBwd(_c.Structure):
                 ("aTP", PlanRef), ("aTF", PlanRef),
                 ("xT", PlanRef), ("x_dense", _c.c_void_p), ("ldx", _c.c_int64), ("gemm_ws", _c.c_void_p),
                 ("gemm_ws_bytes", _c.c_int64), ("gS2", _c.c_void_p), ("gZ1", _c.c_void_p), ("gS1", _c.c_void_p),
-                ("bwd2_ws", _c.c_void_p), ("bwd2_ws_bytes", _c.c_int64), ("aTH", PlanRef), ("x_hubT", _c.c_void_p),
-                ("ld_xhT", _c.c_int64), ("nhub", _c.c_int32), ("nhub_p", _c.c_int32), ("Kc", _c.c_int32),
-                ("k0", _c.c_int32), ("UT", _c.c_void_p), ("ldut", _c.c_int64), ("y", _c.c_void_p),
-                ("sm_ws", _c.c_void_p), ("sm_ws_bytes", _c.c_int64), ("sm_ctr", _c.c_void_p),
-                ("sm_ctr_bytes", _c.c_int64)]
+                ("bwd2_ws", _c.c_void_p), ("bwd2_ws_bytes", _c.c_int64)]
 
 
 FACTORED, SPMM_PROJ, SPMM_GEMM, DENSE_AX = 1, 2, 3, 4
 KIND_NAMES = {FACTORED: "factored", SPMM_PROJ: "spmm+proj", SPMM_GEMM: "spmm+gemm", DENSE_AX: "dense-ax"}
-BWD_AX_DIRECT, BWD_FACTORED = 1, 2
+BWD_AX_DIRECT = 1
 
 
 def layout_ok():
@@ -69,9 +63,8 @@ def layout_ok():
     n = _lib.load().gcnk_gcn_fwd_layout(buf, 16)
     want = [_c.sizeof(PlanRef), _c.sizeof(GcnFwd), GcnFwd.x.offset, GcnFwd.U.offset, GcnFwd.aF.offset,
             GcnFwd.aP.offset, GcnFwd.ld_h1_tmp.offset, PlanRef.lanes_hint.offset, _c.sizeof(GcnBwd),
-            GcnBwd.xT.offset, GcnBwd.bwd2_ws_bytes.offset, GcnFwd.x_ctr.offset, GcnBwd.aTH.offset,
-            GcnBwd.sm_ctr_bytes.offset, GcnFwd.s1_slabs.offset, GcnFwd.s1_slab_stride.offset]
-    return n == 16 and list(buf) == want
+            GcnBwd.xT.offset, GcnBwd.bwd2_ws_bytes.offset]
+    return n == len(want) and list(buf)[:n] == want
 
 
 def _fill_plan(ref, plan, F, lanes, device, keep):
@@ -163,29 +156,15 @@ class ForwardRecord:
             keep.append(x_dense)
             s.x_split_k = ops.default_split_k(rows, F, cols)
         s.x_rows, s.x_cols = rows, cols
-        onepass = kind == FACTORED and fac.onepass()
-        if onepass:   # S_T = X_hubs W1 on the one-launch small-M GEMM: its counter region
-            cb = int(lib.gcnk_gemm_smallm_counter_bytes(F))
-            ctr = torch.zeros((cb + 3) // 4, dtype=torch.int32, device=device)
-            keep.append(ctr)
-            s.x_ctr, s.x_ctr_bytes = ctr.data_ptr(), cb
-        # GEMM workspace: split-K slabs of X W1 (dense X) or the small-M GEMM's
-        # partials; H1 W2 runs unsplit
+        # GEMM workspace: split-K slabs of X W1 (dense X); H1 W2 runs unsplit
         gws = 0
-        if onepass:
-            gws = int(lib.gcnk_gemm_smallm_workspace_bytes(rows, F, cols))
-        elif x_dense is not None:
+        if x_dense is not None:
             gws = int(lib.gcnk_gemm_workspace_bytes(rows, F, cols, s.x_split_k))
         if gws > 0:
             g = torch.empty((gws + 3) // 4, dtype=torch.float32, device=device)
             keep.append(g)
             s.gemm_ws, s.gemm_ws_bytes = g.data_ptr(), gws
-        # factored with dense X_hubs: S_T as K-slabs that the factored gc1 sums
-        # while staging it (gcnk_gemm_kslabs_f32; no reduction launch)
-        nslab = fac.slabs(F) if kind == FACTORED and not onepass else 1
-        s1 = torch.empty((nslab * rows, F), dtype=torch.float32, device=device)
-        if nslab > 1:
-            s.s1_slabs, s.s1_slab_stride = nslab, rows * F
+        s1 = torch.empty((rows, F), dtype=torch.float32, device=device)
         s2 = torch.empty((M, P), dtype=torch.float32, device=device)
         keep += [s1, s2]
         s.s1, s.lds1, s.s2, s.lds2 = s1.data_ptr(), F, s2.data_ptr(), P
@@ -229,31 +208,13 @@ class BackwardRecord:
         adjT = adj.t()
         keep.append(adjT)
         dax = ops.dense_ax_for(adj, xop, F, P)
-        fac = ops.factor_for(adj, xop) if dax is None and ops.FACTOR_BWD else None
-        if fac is not None and not (P <= 32 and F % 4 == 0 and F <= 256):   # (the factored forward's range)
-            fac = None
-        for ref, width in ((s.aTP, P), (s.aTF, F)) if dax is None and fac is None else ((s.aTP, P),):
+        for ref, width in ((s.aTP, P), (s.aTF, F)) if dax is None else ((s.aTP, P),):
             pl = adjT.plan(ops.default_ipc(adjT, width, 0), int(lib.gcnk_spmm_groups(width, 0)), DENSE_THRESHOLD)
             _fill_plan(ref, pl, width, 0, device, keep)
             keep.append(pl)
         rows, cols = xop.shape
         s.x_rows, s.x_cols = rows, cols
-        if fac is not None:        # gW1 = X_hubs^T (A_H^T gZ1) + U~^T gZ1 (factor.HubFactor.grad_w1)
-            UT, aT_hub, x_hubT, Hp = fac.backward_operands(adj)
-            s.flags = BWD_FACTORED
-            pl = aT_hub.plan(ops.default_ipc(aT_hub, F, 0), int(lib.gcnk_spmm_groups(F, 0)), DENSE_THRESHOLD)
-            _fill_plan(s.aTH, pl, F, 0, device, keep)
-            y = torch.zeros((Hp, F), dtype=torch.float32, device=device)
-            cb = int(lib.gcnk_gemm_smallm_counter_bytes(F))
-            ctr = torch.zeros((cb + 3) // 4, dtype=torch.int32, device=device)
-            wsb = int(lib.gcnk_gemm_smallm_workspace_bytes(min(64, fac.Kc), F, M))
-            ws = torch.empty((wsb + 3) // 4, dtype=torch.float32, device=device)
-            keep += [pl, aT_hub, UT, x_hubT, y, ctr, ws]
-            s.x_hubT, s.ld_xhT, s.nhub, s.nhub_p, s.Kc, s.k0 = x_hubT.data_ptr(), x_hubT.stride(0), fac.H, Hp, \
-                fac.Kc, fac.k0
-            s.UT, s.ldut, s.y = UT.data_ptr(), UT.stride(0), y.data_ptr()
-            s.sm_ws, s.sm_ws_bytes, s.sm_ctr, s.sm_ctr_bytes = ws.data_ptr(), wsb, ctr.data_ptr(), cb
-        elif dax is not None:        # gW1 = (A-hat X)^T gZ1 (the DENSE_AX forward's association)
+        if dax is not None:        # gW1 = (A-hat X)^T gZ1 (the DENSE_AX forward's association)
             s.flags = BWD_AX_DIRECT
             s.x_dense, s.ldx = dax.AX.data_ptr(), dax.AX.stride(0)
             s.x_rows, s.x_cols = M, dax.K
@@ -283,7 +244,7 @@ class BackwardRecord:
         gZ1 = torch.empty((M, F), dtype=torch.float32, device=device)
         keep += [gS2, gZ1]
         s.gS2, s.gZ1 = gS2.data_ptr(), gZ1.data_ptr()
-        if dax is None and fac is None:
+        if dax is None:
             gS1 = torch.empty((rows, F), dtype=torch.float32, device=device)
             keep.append(gS1)
             s.gS1 = gS1.data_ptr()
@@ -335,8 +296,7 @@ def _get(adj, xop, F, P, device, cls, tag):
     it, so two graphs of the same record must not replay concurrently."""
     stream = torch.cuda.current_stream(device).cuda_stream
     src = xop.csr if xop.csr is not None else xop.dense
-    key = (tag, id(src), F, P, stream, ops.FACTOR_GC1, ops.FUSE_PROJECTION, ops.DENSE_AX, ops.FACTOR_BWD,
-           factor.XHUB)
+    key = (tag, id(src), F, P, stream, ops.FACTOR_GC1, ops.FUSE_PROJECTION, ops.DENSE_AX)
     recs = getattr(adj, "_records", None)
     if recs is None:
         with _lock:

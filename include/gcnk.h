@@ -50,7 +50,7 @@
 extern "C" {
 #endif
 
-#define GCNK_ABI_VERSION 11
+#define GCNK_ABI_VERSION 12
 
 #define GCNK_OK 0
 #define GCNK_EARG (-1)
@@ -268,27 +268,6 @@ int gcnk_hubfactor_gc1_f32(int32_t M, int32_t F, int32_t Kc, int32_t nhub, int32
                            const uint8_t* drop_mask, int64_t ldm, float drop_scale, float keep_prob, uint64_t seed,
                            uint64_t offset, const uint64_t* rng_base, const float* W2, int64_t ldw2, float* H,
                            int64_t ldh, float* C2, int64_t ldc2, void* stream);
-/* The same with S_T given as nslab (1-4) K-slabs S + s slab_stride, s < nslab
- * (gcnk_gemm_kslabs_f32), summed in slab order while the kernel stages S_T:
- * S_T = ((S_0 + S_1) + S_2) + S_3.  GCNK_EUNSUP when (nslab - 1) x
- * ceil(nhub F / 2048) > 16 (the staging registers); nslab == 1 is
- * gcnk_hubfactor_gc1_f32. */
-int gcnk_hubfactor_gc1_slabs_f32(int32_t M, int32_t F, int32_t Kc, int32_t nhub, int32_t P, const float* U,
-                                 int64_t ldu, const float* W, int64_t ldw, int32_t k0, const float* S, int64_t lds,
-                                 int32_t nslab, int64_t slab_stride, const int32_t* rec, int32_t rec_words,
-                                 const float* bias, int32_t epilogue, const uint8_t* drop_mask, int64_t ldm,
-                                 float drop_scale, float keep_prob, uint64_t seed, uint64_t offset,
-                                 const uint64_t* rng_base, const float* W2, int64_t ldw2, float* H, int64_t ldh,
-                                 float* C2, int64_t ldc2, void* stream);
-/* S_T's K-slabs for the above (csrc/kslab.hip; X_hubs W1, reference layer.py:102
- * on the topic rows): C + s slab_stride = A[:, K_s] B[K_s, :] for s < nslab
- * (1-64; the factored gc1 sums at most 4), K cut into 16-deep chunks and slab s owning chunks [s cps, (s+1) cps),
- * cps = ceil(ceil(K / 16) / nslab).  No reduction launch and no hand-off: the
- * consumer sums the slabs.  A: 16-B aligned rows (lda % 4 == 0).  Fixed-order
- * sums: bitwise reproducible.  GCNK_EUNSUP past K = 3072 nslab. */
-int gcnk_gemm_kslabs_f32(int32_t M, int32_t N, int32_t K, const float* A, int64_t lda, const float* B, int64_t ldb,
-                         int32_t nslab, float* C, int64_t ldc, int64_t slab_stride, void* stream);
-
 /* ---------------------------------------------------------------------------
  * Narrow-feature gc1 (csrc/dense_gc1.hip; GCN.forward layer.py:164-190 through
  * layer.py:102,106,110,182,185 and gc2's support layer.py:102) for a dense X
@@ -309,23 +288,6 @@ int gcnk_dense_gc1_f32(int32_t M, int32_t K, int32_t F, int32_t P, const float* 
                        const float* W2, int64_t ldw2, float* H, int64_t ldh, float* C2, int64_t ldc2, void* stream);
 int gcnk_aggregate_f32(const int32_t* rowptr, const int32_t* colind, const float* val, int32_t M, const float* X,
                        int64_t ldx, int32_t K, float* out, int64_t ldo, int32_t Kp, void* stream);
-
-/* ---------------------------------------------------------------------------
- * Small-M, long-K GEMM in one launch (csrc/smallm.hip): C = A B with A
- * [M x K] dense, M <= 64 (lda % 4 == 0, A and B 16-B aligned, ldb % 4 == 0); accumulate != 0:
- * C += A B (the backward's gW1 rows of the factored operand U) --
- * the hub rows of X times W1 (layer.py:102 on the topic rows) for the
- * factored gc1.  K split into ~20 ranges x 16-column tiles; each tile's
- * partials (workspace: gcnk_gemm_smallm_workspace_bytes) are summed in range
- * order by the tile's last workgroup (arrival counters: a caller region of
- * gcnk_gemm_smallm_counter_bytes, zero on entry, left zero on return;
- * concurrent calls need regions of their own).  Bitwise reproducible.
- * ------------------------------------------------------------------------- */
-int64_t gcnk_gemm_smallm_workspace_bytes(int32_t M, int32_t N, int32_t K);
-int64_t gcnk_gemm_smallm_counter_bytes(int32_t N);
-int gcnk_gemm_smallm_f32(int32_t M, int32_t N, int32_t K, const float* A, int64_t lda, const float* B, int64_t ldb,
-                         float* C, int64_t ldc, int32_t accumulate, float* workspace, int64_t workspace_bytes,
-                         int32_t* counters, int64_t counter_bytes, void* stream);
 
 /* The hub factorisation's (A-hat, X)-fixed operands, built on the device once
  * per operand pair (csrc/factor_build.hip; factor.py drives it, the host
@@ -409,12 +371,6 @@ typedef struct gcnk_gcn_fwd {
   int64_t lds2;
   float* h1_tmp;               /* SPMM_GEMM scratch H1 when H1 == NULL */
   int64_t ld_h1_tmp;
-  int32_t* x_ctr;              /* non-NULL: the first product on the one-pass small-M GEMM */
-  int64_t x_ctr_bytes;         /* (gcnk_gemm_smallm_f32; gemm_ws its workspace), zeroed once */
-  int32_t s1_slabs;            /* FACTORED, dense X_hubs: > 1 -> S_T as that many K-slabs (ABI 11) */
-  int32_t pad2_;
-  int64_t s1_slab_stride;      /* floats between the slabs in s1 (gcnk_gemm_kslabs_f32 ->
-                                  gcnk_hubfactor_gc1_slabs_f32) */
 } gcnk_gcn_fwd;
 
 int gcnk_gcn_forward_f32(const gcnk_gcn_fwd* rec,
@@ -434,13 +390,9 @@ int gcnk_gcn_forward_f32(const gcnk_gcn_fwd* rec,
  * gW2, gb2 are nullable (not computed); gb2 needs G's column sums only.
  * flags & GCNK_BWD_AX_DIRECT: x_dense holds A-hat X (the DENSE_AX forward) and
  * gW1 = (A-hat X)^T gZ1 directly (no gS1, no aTF plan).
- * flags & GCNK_BWD_FACTORED (the FACTORED forward, A-hat X = U~ + A_H X_hubs):
- *   y = A_H^T gZ1 (aTH: A-hat^T's hub rows at width F), gW1 = X_hubs^T y
- *   (x_hubT [x_cols x nhub_p], the short-K GEMM), then rows k0 .. k0 + Kc of
- *   gW1 += U^T gZ1 (UT [Kc x >= M], gcnk_gemm_smallm_f32 with its workspace and
- *   counter region) -- no gS1, no aTF plan, no X^T plan. */
+ * (ABI 11's GCNK_BWD_FACTORED -- gW1 through the hub factor -- measured slower
+ * than A-hat^T gZ1 + X^T gS1 in the step and was removed in ABI 12.) */
 #define GCNK_BWD_AX_DIRECT 1
-#define GCNK_BWD_FACTORED 2
 typedef struct gcnk_gcn_bwd {
   int32_t M, F, P;             /* rows of A-hat, nhid, nclass */
   int32_t x_rows, x_cols;      /* X [x_rows x x_cols]: gW1 is [x_cols x F] */
@@ -458,17 +410,6 @@ typedef struct gcnk_gcn_bwd {
   float* gS1;                  /* scratch [M x F] */
   void* bwd2_ws;               /* gcnk_gcn_bwd2_workspace_bytes(M, F, P) */
   int64_t bwd2_ws_bytes;
-  gcnk_plan_ref aTH;           /* GCNK_BWD_FACTORED operands (above) */
-  const float* x_hubT;
-  int64_t ld_xhT;
-  int32_t nhub, nhub_p, Kc, k0;
-  const float* UT;
-  int64_t ldut;
-  float* y;                    /* [nhub_p x F], rows nhub .. nhub_p zero */
-  float* sm_ws;
-  int64_t sm_ws_bytes;
-  int32_t* sm_ctr;
-  int64_t sm_ctr_bytes;
 } gcnk_gcn_bwd;
 
 int gcnk_gcn_backward_f32(const gcnk_gcn_bwd* rec, const float* G, const float* H1, int64_t ldh, const float* W2,
@@ -476,8 +417,8 @@ int gcnk_gcn_backward_f32(const gcnk_gcn_bwd* rec, const float* G, const float* 
 
 /* Layout of the record structs for bindings that mirror them: writes up to n
  * of {sizeof plan_ref, sizeof gcn_fwd, offsetof x, U, aF, aP, ld_h1_tmp,
- * plan_ref.lanes_hint, sizeof gcn_bwd, gcn_bwd.xT, gcn_bwd.bwd2_ws_bytes,
- * gcn_fwd.x_ctr, gcn_bwd.aTH, gcn_bwd.sm_ctr_bytes} to out and returns how many exist. */
+ * plan_ref.lanes_hint, sizeof gcn_bwd, gcn_bwd.xT, gcn_bwd.bwd2_ws_bytes} to
+ * out and returns how many exist. */
 int32_t gcnk_gcn_fwd_layout(int64_t* out, int32_t n);
 
 /* ---------------------------------------------------------------------------

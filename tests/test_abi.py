@@ -39,7 +39,7 @@ def _hdr(M=10, K=10, groups=1, ipc=32, nslots=0, nslabs=0):
 
 def test_abi_version_and_error_text():
     lib = _lib.load()
-    assert lib.gcnk_abi_version() == _lib.ABI_VERSION == 11
+    assert lib.gcnk_abi_version() == _lib.ABI_VERSION == 12
     rc = lib.gcnk_spmm_csr_f32(None, None, None, 0, 8, None, 0, None, 0, None, 0,
                                1.0, 1.0, 0, 0, None, None, 0, None, 0, 0, None)
     assert rc == _lib.EARG

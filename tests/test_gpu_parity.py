@@ -97,6 +97,44 @@ def test_spmm_widths_with_heavy_and_empty_rows(F):
     _close(got, csr_ref.spmm_csr(rp, ci, v, B), rtol=1e-5, atol=2e-5 * np.sqrt(2500))
 
 
+@pytest.fixture(scope="module")
+def rmat17():
+    """A power-law graph (SURVEY §8(d) row 4's R-MAT(0.57, 0.19, 0.19), scale 17:
+    131,072 nodes, 2.6M edges drawn; its heaviest rows hold ~10^4 nonzeros,
+    far beyond 64 segments of ipc) as host CSR arrays."""
+    rp, ci, v = datasets.rmat_csr(17, 2_621_440, seed=5)
+    return rp.numpy(), ci.numpy(), v.numpy()
+
+
+@pytest.mark.parametrize("F", [8, 64, 256])
+def test_spmm_power_law_rows_and_linearity(rmat17, F):
+    """The SpMM on the R-MAT graph: its 16 heaviest rows, every empty-row kind
+    and 400 random rows against the float64 oracle (csr_ref.spmm_csr on the
+    sampled rows), the whole product linear (A (B1 + 2 B2) = A B1 + 2 A B2
+    to fp32 reassociation), bitwise reproducible."""
+    rp, ci, v = rmat17
+    n = len(rp) - 1
+    deg = np.diff(rp)
+    assert deg.max() > 64 * 32, deg.max()   # a row past 64 segments of the largest ipc
+    a = from_arrays(rp, ci, v, (n, n), DEV)
+    rng = np.random.default_rng(F)
+    B1 = torch.from_numpy(rng.standard_normal((n, F)).astype(np.float32)).to(DEV)
+    B2 = torch.from_numpy(rng.standard_normal((n, F)).astype(np.float32)).to(DEV)
+    C1 = spmm(a, B1)
+    rows = np.unique(np.concatenate([np.argsort(deg)[-16:], rng.choice(n, 400, replace=False),
+                                     np.flatnonzero(deg == 0)[:8]]))
+    sub_rp = np.concatenate([[0], np.cumsum(deg[rows])])
+    sub_ci = np.concatenate([ci[rp[r]:rp[r + 1]] for r in rows])
+    sub_v = np.concatenate([v[rp[r]:rp[r + 1]] for r in rows])
+    want = csr_ref.spmm_csr(sub_rp, sub_ci, sub_v, B1.cpu().numpy())
+    _close(C1[torch.from_numpy(rows).to(DEV)], want, rtol=1e-5, atol=2e-5 * np.sqrt(deg.max()))
+    lin = spmm(a, B1 + 2 * B2)
+    both = C1 + 2 * spmm(a, B2)
+    scale = float(both.abs().max())
+    assert float((lin - both).abs().max()) <= 1e-5 * max(1.0, scale) * np.sqrt(deg.max() / 100)
+    assert torch.equal(spmm(a, B1), C1)
+
+
 @pytest.mark.parametrize("ipc", [4, 8, 12, 16, 32, 64])
 @pytest.mark.parametrize("lanes", [0, 16, 32])
 def test_spmm_schedule_variants(ipc, lanes):
@@ -413,79 +451,6 @@ def test_gemm_small_m_split_k(shape, split):
     got = gemm(Ad, B.to(DEV), split_k=split)
     _close(got, A.double().numpy() @ B.double().numpy(), rtol=1e-5, atol=2e-6 * np.sqrt(K) * 4)
     assert torch.equal(got, gemm(Ad, B.to(DEV), split_k=split))
-
-
-@pytest.mark.parametrize("shape,nslab", [((50, 200, 7463), 4), ((64, 200, 8192), 4), ((1, 4, 100), 1),
-                                         ((17, 116, 1000), 3), ((50, 8, 7463), 3), ((50, 8, 3000), 2),
-                                         ((33, 20, 12000), 4),
-                                         ((70, 200, 100), 3)])
-def test_gemm_kslabs(shape, nslab):
-    """gcnk_gemm_kslabs_f32 (csrc/kslab.hip): slab s = A[:, K_s] B[K_s, :] for
-    the documented 16-deep chunk ranges (cps = ceil(ceil(K / 16) / nslab)), each
-    against float64 (K ragged against 16, N against 16, M against 16, A rows
-    padded to 4 floats); bitwise reproducible; too deep a K is refused."""
-    import ctypes
-    M, N, K = shape
-    rng = np.random.default_rng(M + N + K)
-    Ap = torch.from_numpy(rng.standard_normal((M, (K + 3) // 4 * 4)).astype(np.float32))
-    A = Ap[:, :K]
-    B = torch.from_numpy(rng.standard_normal((K, N)).astype(np.float32))
-    Ad, Bd = Ap.to(DEV)[:, :K], B.to(DEV)
-    lib = _lib.load()
-    stream = ctypes.c_void_p(torch.cuda.current_stream().cuda_stream)
-
-    def run():
-        C = torch.full((nslab * M, N), float("nan"), device=DEV)
-        _lib.check(lib.gcnk_gemm_kslabs_f32(M, N, K, Ad.data_ptr(), Ad.stride(0), Bd.data_ptr(), N, nslab,
-                                            C.data_ptr(), N, M * N, stream), "gcnk_gemm_kslabs_f32")
-        return C
-    C = run()
-    cps = ((K + 15) // 16 + nslab - 1) // nslab
-    for sl in range(nslab):
-        k0, k1 = min(K, 16 * cps * sl), min(K, 16 * cps * (sl + 1))
-        want = A[:, k0:k1].double().numpy() @ B[k0:k1].double().numpy()
-        _close(C[sl * M:(sl + 1) * M], want, rtol=1e-5, atol=2e-6 * np.sqrt(max(1, k1 - k0)) * 4)
-    assert torch.equal(run(), C)
-    C2 = torch.empty((4 * 64, 200), device=DEV)
-    A2 = torch.zeros((64, 30000), device=DEV)
-    B2 = torch.zeros((30000, 200), device=DEV)
-    assert lib.gcnk_gemm_kslabs_f32(64, 200, 30000, A2.data_ptr(), 30000, B2.data_ptr(), 200, 4, C2.data_ptr(), 200,
-                                    64 * 200, stream) == _lib.EUNSUP
-
-
-@pytest.mark.parametrize("shape", [(50, 200, 7463), (64, 200, 8192), (1, 4, 512), (17, 116, 1000), (64, 13, 100),
-                                   (50, 8, 7463), (33, 200, 30000)])
-def test_gemm_small_m_one_pass(shape):
-    """gcnk_gemm_smallm_f32 (one launch: K ranges x 16-column tiles, each tile's
-    partials summed in range order by its last workgroup) against float64:
-    M <= 64 incl. 1, N not a multiple of 16, K not a multiple of 4 (rows padded
-    to 4 floats), a K needing 32-chunk ranges; bitwise reproducible from call
-    to call and on a second stream (own counter region); the counter region is
-    left zeroed (re-armed by each tile's last workgroup)."""
-    from graph_convolutional_networks_for_text_classification_amd import ops
-    M, N, K = shape
-    rng = np.random.default_rng(M + N + K)
-    Kp = (K + 3) // 4 * 4
-    Ab = torch.zeros((M, Kp), dtype=torch.float32)
-    Ab[:, :K] = torch.from_numpy(rng.standard_normal((M, K)).astype(np.float32))
-    A = Ab.to(DEV)[:, :K]
-    Np = (N + 3) // 4 * 4                    # (B's rows padded to 4 floats, as the kernel requires)
-    Bb = torch.zeros((K, Np), dtype=torch.float32)
-    Bb[:, :N] = torch.from_numpy(rng.standard_normal((K, N)).astype(np.float32))
-    B = Bb.to(DEV)[:, :N]
-    C = ops.gemm_smallm(A, B)
-    want = A.cpu().double().numpy() @ B.cpu().double().numpy()
-    _close(C, want, rtol=1e-5, atol=1e-5 * np.sqrt(K))
-    assert torch.equal(ops.gemm_smallm(A, B), C)
-    side = torch.cuda.Stream()
-    side.wait_stream(torch.cuda.current_stream())
-    with torch.cuda.stream(side):
-        C2 = ops.gemm_smallm(A, B)
-    torch.cuda.current_stream().wait_stream(side)
-    assert torch.equal(C2, C)
-    torch.cuda.synchronize()
-    for key, (_, _, ctr, _) in ops._SMALLM_SCRATCH.items():
-        assert int(ctr.abs().sum()) == 0, key
 
 
 def test_gemm_epilogues_and_split_k():
@@ -1198,19 +1163,15 @@ def test_tile_path_repeat_streams_and_graph_replay_are_exact(r8, dense, monkeypa
 
 # ------------------------------------------------------------------------------ hub-factored gc1
 
-@pytest.mark.parametrize("factor_bwd", [False, True])
 @pytest.mark.parametrize("mode", ["eval", "train_mask", "train_hash"])
-def test_factored_gc1_matches_spmm_path(r8, mode, factor_bwd, monkeypatch):
+def test_factored_gc1_matches_spmm_path(r8, mode):
     """GCN.forward through the hub factorisation (factor.py + gcnk_hubfactor_gc1_f32:
     A-hat X W1 as U W1[Kc] + A_H (X_hubs W1)) against the SpMM path
     (ops.FACTOR_GC1 = False: X W1 then A-hat S1, layer.py:102,106) on R8 with
     the same weights and the same dropout masks: logits and every gradient
     within fp32 reassociation error; H1 kept for the backward only when
-    needed; the factored launch bitwise reproducible.  The backward both ways:
-    gW1 through A-hat^T gZ1 and X^T gS1, and through the factor (ops.FACTOR_BWD:
-    A_H^T gZ1, X_hubs^T, U^T gZ1)."""
+    needed; the factored launch bitwise reproducible."""
     from graph_convolutional_networks_for_text_classification_amd import factor, ops
-    monkeypatch.setattr(ops, "FACTOR_BWD", factor_bwd)
     X, A = r8["features"].to(DEV), r8["adj"].to(DEV)
     from graph_convolutional_networks_for_text_classification_amd.sparse import as_csr
     f = factor.get(as_csr(A), ops.Operand(X))
@@ -1240,9 +1201,8 @@ def test_factored_gc1_matches_spmm_path(r8, mode, factor_bwd, monkeypatch):
         _grads_close(ga[k], gb[k], k)
 
 
-@pytest.mark.parametrize("kernel", ["legacy", "persistent", "slabs"])
 @pytest.mark.parametrize("F,P,ndoc", [(52, 3, 2000), (200, 20, 2000), (36, 32, 2000), (200, 20, 12000)])
-def test_factored_gc1_kernel_against_float64(F, P, ndoc, kernel, monkeypatch):
+def test_factored_gc1_kernel_against_float64(F, P, ndoc):
     """gcnk_hubfactor_gc1_f32 alone on a synthetic doc-topic graph with hub x
     hub nonzeros, F not a multiple of 16 (and F < 64, where the n-tiles past F
     read the zero pad after W1[Kc]), P of one and two MFMA n-tiles, H1 stored:
@@ -1250,16 +1210,10 @@ def test_factored_gc1_kernel_against_float64(F, P, ndoc, kernel, monkeypatch):
     ones), rows written through the block order's row ids (hub rows spread over
     the blocks, factor.py).  Every launch follows one that filled all LDS with
     NaN bits (gcnk_debug_poison_lds): a read of LDS the kernel did not write
-    would surface as NaN.  Both kernels: csrc/factor.hip's per-block one and
-    the persistent one of csrc/dense_gc1.hip (GCNK_HUBFACTOR=persistent, read
-    per launch); and S_T given as K-slabs (gcnk_gemm_kslabs_f32 ->
-    gcnk_hubfactor_gc1_slabs_f32, the slabs summed while staging)."""
+    would surface as NaN."""
     import ctypes
     import scipy.sparse as ssp
     from graph_convolutional_networks_for_text_classification_amd import factor, ops
-    monkeypatch.setenv("GCNK_HUBFACTOR", "legacy" if kernel == "slabs" else kernel)
-    if kernel == "slabs":   # (the factor built below keeps a dense copy of X's hub rows)
-        monkeypatch.setattr(factor, "XHUB", "slabs")
     from graph_convolutional_networks_for_text_classification_amd.sparse import as_csr
     g = datasets.doc_topic_graph(ndoc, 40, 5, seed=4, tt_prob=0.3)
     A, X = g["adj"].to(DEV), g["features"].to(DEV)
@@ -1279,23 +1233,19 @@ def test_factored_gc1_kernel_against_float64(F, P, ndoc, kernel, monkeypatch):
     Z = Ad @ (Xd @ W1.cpu().double().numpy())
     lib = _lib.load()
 
-    if kernel == "slabs":
-        S_T, nslab = f.hub_slabs(W1)
-        assert nslab > 1
-    else:
-        S_T, nslab = f.hub_times(W1).contiguous(), 1
+    S_T = f.hub_times(W1).contiguous()
     stream = ctypes.c_void_p(torch.cuda.current_stream().cuda_stream)
 
     def launch(epi, store_h1=True):
-        """gcnk_hubfactor_gc1_slabs_f32 right after an LDS poison launch (as ops.hubfactor_gc1 calls it)."""
+        """gcnk_hubfactor_gc1_f32 right after an LDS poison launch (as ops.hubfactor_gc1 calls it)."""
         H1 = torch.empty((f.M, F), device=DEV) if store_h1 else None
         S2 = torch.empty((f.M, P), device=DEV)
         _lib.check(lib.gcnk_debug_poison_lds(0xFFFFFFFF, stream), "gcnk_debug_poison_lds")
         p = lambda t: ctypes.c_void_p(t.data_ptr()) if t is not None else None
-        _lib.check(lib.gcnk_hubfactor_gc1_slabs_f32(
-            f.M, F, f.Kc, f.H, P, p(f.U), f.U.stride(0), p(W1), F, f.k0, p(S_T), F, nslab, f.H * F, p(f.rec),
+        _lib.check(lib.gcnk_hubfactor_gc1_f32(
+            f.M, F, f.Kc, f.H, P, p(f.U), f.U.stride(0), p(W1), F, f.k0, p(S_T), F, p(f.rec),
             f.rec_words, p(b1), epi, None, 0, 1.0, 1.0, 0, 0, None, p(W2), P, p(H1), F, p(S2), P, stream),
-            "gcnk_hubfactor_gc1_slabs_f32")
+            "gcnk_hubfactor_gc1_f32")
         return H1, S2
     for epi in (_lib.EPI_NONE, _lib.EPI_BIAS, _lib.EPI_BIAS_RELU):
         H1, S2 = launch(epi)
@@ -1307,12 +1257,8 @@ def test_factored_gc1_kernel_against_float64(F, P, ndoc, kernel, monkeypatch):
         _close(S2, H1.cpu().double().numpy() @ W2.cpu().double().numpy(), atol=2e-5 * max(1.0, np.abs(want).max()))
     H1b, S2b = launch(_lib.EPI_BIAS_RELU, store_h1=False)
     assert H1b is None and torch.equal(S2b, S2)
-    if kernel != "persistent":   # (the op wrapper takes factor.slabs' choice: the slab path by default)
-        H1c, S2c = ops.hubfactor_gc1(f, W1, b1, W2, epilogue=_lib.EPI_BIAS_RELU)
-        if (kernel == "slabs") == (f.slabs(F) > 1):   # same S_T form: same bits
-            assert torch.equal(H1c, H1) and torch.equal(S2c, S2)
-        else:
-            _close(H1c, H1.cpu().double().numpy(), atol=2e-5 * max(1.0, float(np.abs(want).max())))
+    H1c, S2c = ops.hubfactor_gc1(f, W1, b1, W2, epilogue=_lib.EPI_BIAS_RELU)   # (the op wrapper: same bits)
+    assert torch.equal(H1c, H1) and torch.equal(S2c, S2)
 
 
 @pytest.mark.parametrize("mode", ["eval", "train_hash"])
@@ -1462,6 +1408,31 @@ def test_dense_ax_forward_backward_matches_spmm_path(r8, mode, graph, monkeypatc
     assert np.abs(la - lb).max() <= 1e-5 * scale, float(np.abs(la - lb).max())
     for k in ga:
         _grads_close(ga[k], gb[k], k)
+
+
+def test_dense_ax_misaligned_weight_falls_back_to_the_spmm_path(r8):
+    """gcnk_dense_gc1_f32 refuses W1 rows that are not 16-B aligned (GCNK_EUNSUP);
+    the module then takes the SpMM path (the record is skipped, ops.dense_gc1
+    returns None) instead of raising: a gc1 weight living 4 bytes
+    into its storage still gives the oracle's logits."""
+    Xn = _gensim_r8_x(r8)
+    Xs = datasets.dense_to_coo(Xn)
+    X, A = Xs.to(DEV), r8["adj"].to(DEV)
+    torch.manual_seed(123)
+    m = GCN(nfeat=Xn.shape[1], nhid=200, nclass=r8["nclass"], dropout=0.5).to(DEV).eval()
+    w = m.gc1.weight.detach()
+    buf = torch.empty(w.numel() + 1, device=DEV)
+    shifted = buf[1:].view_as(w)
+    shifted.copy_(w)
+    assert shifted.data_ptr() % 16 != 0
+    m.gc1.weight.data = shifted
+    with torch.no_grad():
+        lg = m(X, A)
+    ref = gcn_ref.RefGCN(nfeat=Xn.shape[1], nhid=200, nclass=r8["nclass"], dropout=0.5).eval()
+    ref.load_state_dict({k: v.cpu() for k, v in m.state_dict().items()})
+    with torch.no_grad():
+        want = ref(Xs, r8["adj"]).numpy()
+    assert np.abs(lg.cpu().numpy() - want).max() <= LOGIT_TOL
 
 
 # ------------------------------------------------------------------------------ whole-forward launch record

@@ -57,7 +57,8 @@ constexpr int kKC = 64;                 // condensed columns per tile chunk (16 
 // forward 0.5-1 us shorter, factored or not (profiles/r03_tile_nt.log)
 constexpr int kMaxNT = GCNK_TILE_MAXNT;
 constexpr int kMaxColTiles = 64;        // row-kernel column tiles per launch (arrival counters per heavy row)
-constexpr int kMaxSeg = 64;             // segments per heavy row (bounds the last arriver's combine)
+constexpr int kMaxSeg = 64;             // slots per heavy entry (bounds a last arriver's combine)
+constexpr int kMaxSegRow = kMaxSeg * kMaxSeg;  // segments per heavy row (two combine levels)
 // Schedule knobs of the whole-wavefront (F > 128) row kernel, overridable at
 // compile time for experiments (scripts/variants.sh times prebuilt variants).
 // Measured on R8 A-hat F = 200 / 20ng-shaped (profiles/r01_variants.log):
@@ -146,10 +147,12 @@ constexpr int kLightMax64 = 64 / kLightRPW;  // their nonzero limit (kLightRPW r
 //   8 ntile (chunks)  9 nred  10 nslabs  11 ntblk (tile blocks)  12 has_diag | segp << 1  13 nnz
 //   14 nslots (partial slots)  15 nsingle (chunk items of single-chunk blocks, listed first)
 // Body: items int2[nnz] {col, value bits} in CSR order | units int4[nunits]
-//   {row (-1: empty), nz begin, nz end, heavy row * 64 + segment or -1}: the
+//   {row (-1: empty), nz begin, nz end, heavy entry * 64 + slot or -1}: the
 //   heavy region first, then light rows, each laid out so that the units of
 //   workgroup b belong to XCD class b % 8 (below) | heavy int4[nheavy]
-//   {row, first partial slot, nseg, 0} | tile part (descriptors,
+//   {row, first partial slot, slots, parent entry * 64 + slot there or -1 (a
+//   row of more than kMaxSeg segments: one entry per group of <= kMaxSeg
+//   segments under one top entry whose slots are the groups' sums)} | tile part (descriptors,
 //   condensed columns, A fragments, reduce rows int4[64 * nred] {row (-1:
 //   none), first slab, slabs, diagonal value bits}, row lists, extracted
 //   diagonal float[64 * ntblk] in block order) | (segp > 0) the heavy units'
@@ -401,7 +404,7 @@ struct Proj {
 struct RowPlan {
   const int2* items;   // {col, value bits} per nonzero, CSR order
   const int4* units;   // {row (-1: empty), nz begin, nz end, heavy row * 64 + segment or -1}
-  const int4* heavy;   // {row, first partial slot, nseg, 0}
+  const int4* heavy;   // {row, first partial slot, slots, parent * 64 + group or -1}
   int32_t* cnt;        // per heavy row x column tile: arrival counters, in the caller's
                        // counter region (zero on entry, re-armed by each row's last arriver)
   int32_t nunits, nhunits;
@@ -761,66 +764,83 @@ spmm_row_kernel(RowPlan rp, int32_t nhb, const float* __restrict__ B, int64_t ld
     return;
   }
   // publish this segment's partial, then count in; the last arriver sums all of
-  // the row's partials in segment order
-  const int32_t hid = un.w >> 6;  // heavy row, segment un.w & 63
-  const int4 hv = rp.heavy[hid];
-  int32_t* ctr = rp.cnt + (int64_t)hid * kMaxColTiles + blockIdx.y;
-  int32_t last = 0;
-  // (the unit, hence the slot row, is wave-uniform; lane group 0 stores)
-  if constexpr (LPR == 64) {
-    if (q == 0 && colok) store_coherent_v(uniform_ptr(part + (int64_t)(hv.y + (un.w & 63)) * part_ld), colv, acc);
-  } else {
-    if (q == 0 && colok) store_coherent(part + (int64_t)(hv.y + (un.w & 63)) * part_ld + colv, acc);
-  }
-  if (!WG || w == 0) {  // the wavefront that stored counts in, after its stores completed
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    int32_t arrived = 0;
-    if (lane == 0) arrived = __hip_atomic_fetch_add(ctr, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    last = __builtin_amdgcn_readfirstlane(arrived) == hv.z - 1;
-  }
-  if constexpr (WG) {
-    if (tid == 0) s_last = last;
-    __syncthreads();
-    last = s_last;
-  }
-  stamp(epi, 3);
-  if (!last) return;
-  // group q sums slots q, q + GS, ... (U loads in flight), then the groups meet
-  if constexpr (LPR == 64) proj.template begin<BLOCK>(pa, F);  // in flight with the partial loads
-  T sum = V::zero();
-  if (colok) {
-    const float* p0 = uniform_ptr(part + (int64_t)hv.y * part_ld);
-    for (int32_t s0 = q; s0 < hv.z; s0 += GS * U) {
-      T pv[U];
-#pragma unroll
-      for (int j = 0; j < U; ++j) {
-        const int32_t sl = s0 + GS * j;
-        // base: the row's first slot (wave-uniform); byte offsets stay below
-        // kMaxSeg * part_ld * 4 < 2^31 (checked at launch)
-        if constexpr (LPR == 64)
-          pv[j] = sl < hv.z ? load_coherent_v<T>(p0, (int64_t)sl * part_ld + colv) : V::zero();
-        else
-          pv[j] = sl < hv.z ? load_coherent<T>(p0 + (int64_t)sl * part_ld + colv) : V::zero();
-      }
-#pragma unroll
-      for (int j = 0; j < U; ++j)
-        if (s0 + GS * j < hv.z) V::add(sum, pv[j]);
+  // the group's partials in segment order.  A row of more than kMaxSeg segments
+  // is cut into groups of at most kMaxSeg (heavy entry .w = parent * 64 + group,
+  // -1 at the top): a group's last arriver publishes the group's sum into its
+  // parent's slot and counts in there, so no combine reads more than kMaxSeg
+  // partials and segments stay ipc-sized on power-law rows (one level per loop
+  // turn; the parent's last arriver stores the row)
+  int32_t hid = un.w >> 6;  // heavy entry, slot un.w & 63
+  int32_t slot = un.w & 63;
+  int4 hv = rp.heavy[hid];
+  T val = acc;
+  for (;;) {
+    int32_t* ctr = rp.cnt + (int64_t)hid * kMaxColTiles + blockIdx.y;
+    int32_t last = 0;
+    // (the entry, hence the slot row, is wave-uniform; lane group 0 stores)
+    if constexpr (LPR == 64) {
+      if (q == 0 && colok) store_coherent_v(uniform_ptr(part + (int64_t)(hv.y + slot) * part_ld), colv, val);
+    } else {
+      if (q == 0 && colok) store_coherent(part + (int64_t)(hv.y + slot) * part_ld + colv, val);
     }
-  }
-  wave_group_sum<LPR>(sum);
-  if constexpr (WG) {
-    __syncthreads();  // s_red reuse
-    if (w > 0) s_red[w][lane] = sum;
-    __syncthreads();
+    if (!WG || w == 0) {  // the wavefront that stored counts in, after its stores completed
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      int32_t arrived = 0;
+      if (lane == 0) arrived = __hip_atomic_fetch_add(ctr, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      last = __builtin_amdgcn_readfirstlane(arrived) == hv.z - 1;
+    }
+    if constexpr (WG) {
+      if (tid == 0) s_last = last;
+      __syncthreads();
+      last = s_last;
+    }
+    stamp(epi, 3);
+    if (!last) return;
+    const bool top = hv.w < 0;  // (workgroup-uniform)
+    // group q sums slots q, q + GS, ... (U loads in flight), then the groups meet
+    if constexpr (LPR == 64)
+      if (top) proj.template begin<BLOCK>(pa, F);  // in flight with the partial loads
+    T sum = V::zero();
+    if (colok) {
+      const float* p0 = uniform_ptr(part + (int64_t)hv.y * part_ld);
+      for (int32_t s0 = q; s0 < hv.z; s0 += GS * U) {
+        T pv[U];
 #pragma unroll
-    for (int v = 1; v < WPB; ++v) V::add(sum, s_red[v][lane]);
+        for (int j = 0; j < U; ++j) {
+          const int32_t sl = s0 + GS * j;
+          // base: the entry's first slot (wave-uniform); byte offsets stay below
+          // kMaxSeg * part_ld * 4 < 2^31 (checked at launch)
+          if constexpr (LPR == 64)
+            pv[j] = sl < hv.z ? load_coherent_v<T>(p0, (int64_t)sl * part_ld + colv) : V::zero();
+          else
+            pv[j] = sl < hv.z ? load_coherent<T>(p0 + (int64_t)sl * part_ld + colv) : V::zero();
+        }
+#pragma unroll
+        for (int j = 0; j < U; ++j)
+          if (s0 + GS * j < hv.z) V::add(sum, pv[j]);
+      }
+    }
+    wave_group_sum<LPR>(sum);
+    if constexpr (WG) {
+      __syncthreads();  // s_red reuse
+      if (w > 0) s_red[w][lane] = sum;
+      __syncthreads();
+#pragma unroll
+      for (int v = 1; v < WPB; ++v) V::add(sum, s_red[v][lane]);
+    }
+    if (q == 0 && lane == 0) __hip_atomic_store(ctr, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);  // re-armed
+    if (!top) {  // a group of a long row: its sum goes up one level
+      hid = hv.w >> 6;
+      slot = hv.w & 63;
+      hv = rp.heavy[hid];
+      val = sum;
+      continue;
+    }
+    if constexpr (LPR == 64) proj.template finish_stage<BLOCK>(pa, F);  // the last arriver (workgroup-uniform)
+    if (q == 0) finish_row<LPR, VEC, NP>(sum, hv.x, colv, colok, bv, lg, C, ldc, epi, store_main, proj, pa);
+    stamp(epi, 3);
+    return;
   }
-  if constexpr (LPR == 64) proj.template finish_stage<BLOCK>(pa, F);  // the last arriver (workgroup-uniform)
-  if (q == 0) {
-    finish_row<LPR, VEC, NP>(sum, hv.x, colv, colok, bv, lg, C, ldc, epi, store_main, proj, pa);
-    if (lane == 0) __hip_atomic_store(ctr, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-  }
-  stamp(epi, 3);
 }
 
 // ---------------------------------------------------------------------------
@@ -1561,27 +1581,45 @@ int host_plan(const int32_t* rp, const int32_t* ci, const float* vv, int32_t M, 
     }
     rb.push_back(e);
     const int64_t nruns = (int64_t)rcl.size();
+    // segments of `seg` nonzeros (longer only past kMaxSegRow of them, ~200k
+    // nonzeros at R8's widths): a row of more than kMaxSeg segments gets two
+    // combine levels instead of longer segments, so a power-law hub is walked
+    // by many short segments, not by 64 long ones
     int64_t sr = seg, nseg = 0;
     for (;;) {
       nseg = 0;
       for (int64_t i = 0; i < nruns; ++i) nseg += (rb[(size_t)i + 1] - rb[(size_t)i] + sr - 1) / sr;
-      if (nseg <= kMaxSeg) break;
+      if (nseg <= kMaxSegRow) break;
       sr *= 2;
     }
     if (nseg == 1) {
       hq[(size_t)rcl[0]].insert(hq[(size_t)rcl[0]].end(), {r, (int32_t)b, (int32_t)e, -1});
       continue;
     }
-    const int32_t hid = nheavy++;
-    hp.heavy.insert(hp.heavy.end(), {r, (int32_t)nslots, (int32_t)nseg, 0});
-    int32_t sgi = 0;
+    // heavy entries: one (nseg <= kMaxSeg), or a top entry over ng groups of
+    // consecutive segments (group g: segments [g nseg / ng, (g + 1) nseg / ng))
+    const int64_t ng = nseg <= kMaxSeg ? 1 : (nseg + kMaxSeg - 1) / kMaxSeg;
+    int32_t top = -1;
+    if (ng > 1) {
+      top = nheavy++;
+      hp.heavy.insert(hp.heavy.end(), {r, (int32_t)nslots, (int32_t)ng, -1});
+      nslots += ng;
+    }
+    std::vector<int32_t> seg_w((size_t)nseg);
+    for (int64_t g = 0; g < ng; ++g) {
+      const int64_t s0 = g * nseg / ng, s1 = (g + 1) * nseg / ng;
+      const int32_t hid = nheavy++;
+      hp.heavy.insert(hp.heavy.end(), {r, (int32_t)nslots, (int32_t)(s1 - s0), ng > 1 ? (int32_t)((int64_t)top * 64 + g) : -1});
+      for (int64_t sgi = s0; sgi < s1; ++sgi) seg_w[(size_t)sgi] = (int32_t)((int64_t)hid * 64 + (sgi - s0));
+      nslots += s1 - s0;
+    }
+    int64_t sgi = 0;
     for (int64_t i = 0; i < nruns; ++i) {
       const int64_t pb = rb[(size_t)i], len = rb[(size_t)i + 1] - pb, np = (len + sr - 1) / sr;
       std::vector<int32_t>& q = hq[(size_t)rcl[(size_t)i]];
       for (int64_t s = 0; s < np; ++s, ++sgi)
-        q.insert(q.end(), {r, (int32_t)(pb + len * s / np), (int32_t)(pb + len * (s + 1) / np), hid * 64 + sgi});
+        q.insert(q.end(), {r, (int32_t)(pb + len * s / np), (int32_t)(pb + len * (s + 1) / np), seg_w[(size_t)sgi]});
     }
-    nslots += nseg;
   }
   // lay out rounds of NX workgroups, workgroup 8k + c taking `per` units of class c
   // (empty units pad short classes)

@@ -4,11 +4,14 @@ Mirrors, step by step, the host unit planning (spmm.hip host_plan, row part:
 light rows, heavy rows cut at XCD column-class boundaries and into segments,
 the class-by-workgroup layout with empty padding units) and the row kernel's
 control flow (light units per lane group, heavy segments shared by lane
-groups, partial slots and the last-arriver combine in segment order), so the
-control logic can be checked on CPU against a dense product."""
+groups, partial slots and the last-arriver combine in segment order; rows of
+more than K_MAX_SEG segments in groups whose last arrivers publish the group
+sums one level up), so the control logic can be checked on CPU against a
+dense product."""
 import numpy as np
 
 K_MAX_SEG = 64
+K_MAX_SEG_ROW = K_MAX_SEG * K_MAX_SEG
 NX = 8
 
 
@@ -28,7 +31,7 @@ def geometry(groups):
 
 
 def host_plan(rowptr, colind, K, ipc, groups):
-    """-> (units [(row, b, e, w)], heavy [(row, first slot, nseg)], nh, nslots)."""
+    """-> (units [(row, b, e, w)], heavy [(row, first slot, slots, parent * 64 + slot or -1)], nh, nslots)."""
     hpb, lpb, seg_groups, lpr = geometry(groups)
     seg = ipc * seg_groups
     light_max = min(2 * ipc, 32) if lpr == 64 else ipc
@@ -55,22 +58,33 @@ def host_plan(rowptr, colind, K, ipc, groups):
         sr = seg
         while True:
             nseg = sum((bounds[i + 1] - bounds[i] + sr - 1) // sr for i in range(len(runs)))
-            if nseg <= K_MAX_SEG:
+            if nseg <= K_MAX_SEG_ROW:
                 break
             sr *= 2
         if nseg == 1:
             hq[runs[0][1]].append((r, b, e, -1))
             continue
-        hid = len(heavy)
-        heavy.append((r, nslots, nseg))
+        ng = 1 if nseg <= K_MAX_SEG else (nseg + K_MAX_SEG - 1) // K_MAX_SEG
+        top = -1
+        if ng > 1:
+            top = len(heavy)
+            heavy.append((r, nslots, ng, -1))
+            nslots += ng
+        seg_w = [0] * nseg
+        for g in range(ng):
+            s0, s1 = g * nseg // ng, (g + 1) * nseg // ng
+            hid = len(heavy)
+            heavy.append((r, nslots, s1 - s0, top * 64 + g if ng > 1 else -1))
+            for sgi in range(s0, s1):
+                seg_w[sgi] = hid * 64 + sgi - s0
+            nslots += s1 - s0
         sgi = 0
         for i, (pb, c) in enumerate(runs):
             ln = bounds[i + 1] - pb
             npc = (ln + sr - 1) // sr
             for s in range(npc):
-                hq[c].append((r, pb + ln * s // npc, pb + ln * (s + 1) // npc, hid * 64 + sgi))
+                hq[c].append((r, pb + ln * s // npc, pb + ln * (s + 1) // npc, seg_w[sgi]))
                 sgi += 1
-        nslots += nseg
 
     def layout(qs, per):
         out = []
@@ -115,13 +129,20 @@ def spmm(rowptr, colind, val, B, ipc, groups):
             C[r] = acc
             written[r] += 1
             continue
-        hid, sgi = w >> 6, w & 63
-        hr, first, nseg = heavy[hid]
-        part[first + sgi] = acc
-        arrivals[hid] += 1
-        if arrivals[hid] == nseg:       # last arriver: slots in segment order
-            C[hr] = sum(part[first + s] for s in range(nseg))
-            written[hr] += 1
+        hid, slot, pv = w >> 6, w & 63, acc
+        while True:
+            hr, first, nsl, up = heavy[hid]
+            assert nsl <= K_MAX_SEG, "no combine reads more than K_MAX_SEG partials"
+            part[first + slot] = pv
+            arrivals[hid] += 1
+            if arrivals[hid] < nsl:
+                break
+            pv = sum(part[first + s] for s in range(nsl))    # last arriver: slots in order
+            if up < 0:
+                C[hr] = pv
+                written[hr] += 1
+                break
+            hid, slot = up >> 6, up & 63                      # a group's sum goes up one level
     for u in range(nh, len(units)):
         r, b, e, _ = units[u]
         if r < 0:

@@ -31,7 +31,7 @@ def test_r8_plan_shape(r8):
     units, heavy, nh, nslots = path_model.host_plan(rp, ci, r8["nodes"], 32, 1)
     light = [x for x in units[nh:] if x[0] >= 0]
     assert len(light) == 7674 and len(heavy) == 50
-    assert all(1 < h[2] <= path_model.K_MAX_SEG for h in heavy)
+    assert all(1 < h[2] <= path_model.K_MAX_SEG and h[3] == -1 for h in heavy)
     assert nslots == sum(h[2] for h in heavy)
     assert sum(1 for x in units if x[0] < 0) < 0.05 * len(units)
 
@@ -48,3 +48,26 @@ def test_model_on_skewed_random(seed):
     for groups, ipc in [(1, 4), (1, 32), (32, 8), (4, 3)]:
         C = path_model.spmm(rp, ci, v, B, ipc, groups)
         np.testing.assert_allclose(C, csr_ref.spmm_csr(rp, ci, v, B), atol=1e-10)
+
+
+def test_power_law_row_takes_two_combine_levels():
+    """A row of ~90 k nonzeros (a power-law hub) keeps base-length segments:
+    > 64 of them, in groups of <= 64 under one top entry, and the model's
+    two-level combine gives the float64 product."""
+    rng = np.random.default_rng(11)
+    M, K = 40, 5000
+    deg = np.array([90_000, 3000, 0, 7] + [20] * (M - 4))
+    rows = np.repeat(np.arange(M), deg)
+    cols = rng.integers(0, K, rows.size)
+    rp, ci, v = csr_ref.coo_to_csr(rows, cols, rng.standard_normal(rows.size), (M, K))
+    ipc, groups = 12, 1
+    units, heavy, nh, nslots = path_model.host_plan(rp, ci, K, ipc, groups)
+    seg = ipc * path_model.geometry(groups)[2]
+    hub = [u for u in units[:nh] if u[0] == 0]
+    assert len(hub) > path_model.K_MAX_SEG and max(u[2] - u[1] for u in hub) <= seg
+    tops = [h for h in heavy if h[0] == 0 and h[3] == -1]
+    assert len(tops) == 1 and 1 < tops[0][2] <= path_model.K_MAX_SEG
+    assert all(h[2] <= path_model.K_MAX_SEG for h in heavy)
+    B = rng.standard_normal((K, 2))
+    np.testing.assert_allclose(path_model.spmm(rp, ci, v, B, ipc, groups), csr_ref.spmm_csr(rp, ci, v, B), rtol=1e-9,
+                               atol=1e-9)

@@ -119,3 +119,39 @@ def test_plan_bytes_is_exactly_the_built_image(kind):
     assert buf[nbytes // 4 - 1] != -7, "plan_bytes reported more than the build wrote"
 
 
+
+
+def test_power_law_hub_keeps_short_segments_two_levels():
+    """on an R-MAT graph whose hub rows hold ~10^4
+    nonzeros the plan keeps every heavy segment at the base length (ipc x the
+    workgroup's lane groups; it used to double it past 64 segments) and gives
+    such a row a top heavy entry over groups of <= 64 segments; no heavy entry
+    has more than 64 slots, slots never overlap, and the units cover every
+    nonzero of the heavy rows exactly once."""
+    from graph_convolutional_networks_for_text_classification_amd import datasets
+    rp, ci, v = (t.numpy() for t in datasets.rmat_csr(16, 1_300_000, seed=2))
+    n = len(rp) - 1
+    ipc, groups = 12, 1                      # whole-wavefront groups (F > 128): 4-wave segments
+    plan = build_host_plan(rp, ci, v, (n, n), groups=groups, ipc=ipc, dense=2.0)
+    hdr = plan[:16]
+    nnz, nunits, nh, nheavy = hdr[13], hdr[5], hdr[6], hdr[7]
+    units = plan[16 + 2 * nnz:16 + 2 * nnz + 4 * nunits].reshape(-1, 4)
+    heavy = plan[16 + 2 * nnz + 4 * nunits:16 + 2 * nnz + 4 * nunits + 4 * nheavy].reshape(-1, 4)
+    seg = ipc * 4
+    deg = np.diff(rp)
+    hub = int(np.argmax(deg))
+    assert deg[hub] > 64 * seg
+    hu = units[:nh][units[:nh, 0] == hub]
+    assert len(hu) > 64 and (hu[:, 2] - hu[:, 1]).max() <= seg
+    assert (heavy[:, 2] <= 64).all() and (heavy[:, 2] >= 1).all()
+    tops = heavy[(heavy[:, 0] == hub) & (heavy[:, 3] == -1)]
+    assert len(tops) == 1 and tops[0, 2] > 1
+    groups_of_hub = heavy[(heavy[:, 0] == hub) & (heavy[:, 3] >= 0)]
+    assert len(groups_of_hub) == tops[0, 2] and (groups_of_hub[:, 3] & 63).tolist() == list(range(tops[0, 2]))
+    assert groups_of_hub[:, 2].sum() == len(hu)
+    slots = np.concatenate([np.arange(h[1], h[1] + h[2]) for h in heavy])
+    assert len(np.unique(slots)) == len(slots) == hdr[14]
+    for r in np.unique(units[:nh, 0][units[:nh, 0] >= 0])[:200]:
+        u = units[:nh][units[:nh, 0] == r]
+        got = np.sort(np.concatenate([np.arange(a, b) for a, b in u[:, 1:3]]))
+        assert np.array_equal(got, np.arange(rp[r], rp[r + 1]))

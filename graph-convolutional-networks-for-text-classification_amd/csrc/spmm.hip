@@ -144,25 +144,27 @@ constexpr int kLightMax64 = 64 / kLightRPW;  // their nonzero limit (kLightRPW r
 // Plan layout (int32 words).  Header (16 words, see gcnk.h):
 //   0 magic  1 M  2 K  3 lane groups per wavefront (64 / LPR)  4 ipc (light-row limit)
 //   5 nunits  6 nhunits (heavy region, padded)  7 nheavy (rows of > 1 segment)
-//   8 ntile (chunks)  9 nred  10 nslabs  11 ntblk (tile blocks)  12 has_diag | segp << 1  13 nnz
+//   8 ntile (chunks)  9 nred  10 nslabs  11 ntblk (tile blocks)  12 has_diag | segp << 1 | tops << 30  13 nnz
 //   14 nslots (partial slots)  15 nsingle (chunk items of single-chunk blocks, listed first)
 // Body: items int2[nnz] {col, value bits} in CSR order | units int4[nunits]
 //   {row (-1: empty), nz begin, nz end, heavy entry * 64 + slot or -1}: the
 //   heavy region first, then light rows, each laid out so that the units of
 //   workgroup b belong to XCD class b % 8 (below) | heavy int4[nheavy]
-//   {row, first partial slot, slots, parent entry * 64 + slot there or -1 (a
-//   row of more than kMaxSeg segments: one entry per group of <= kMaxSeg
-//   segments under one top entry whose slots are the groups' sums)} | tile part (descriptors,
+//   {row, first partial slot, slots, -1 (a row of <= kMaxSeg segments), or for
+//   a row of more (bit 30 of header word 12 set): one entry per group of <=
+//   kMaxSeg segments with .w = the top entry's slot for the group's sum, and
+//   the top entry, .w = -2} | tile part (descriptors,
 //   condensed columns, A fragments, reduce rows int4[64 * nred] {row (-1:
 //   none), first slab, slabs, diagonal value bits}, row lists, extracted
 //   diagonal float[64 * ntblk] in block order) | (segp > 0) the heavy units'
 //   items, padded: int2[nhunits][segp], col -1 past a unit's end.
 struct Layout {
-  int64_t M, nnz, nunits, nhunits, nheavy, nslots, ntile, nred, ntblk, has_diag, segp;
+  int64_t M, nnz, nunits, nhunits, nheavy, nslots, ntile, nred, ntblk, has_diag, segp, tops;
   int64_t items, units, heavy, tdesc, tcols, tfrag, red, trows, dval, hitems, total;
   __host__ __device__ explicit Layout(const int32_t* h) {
     M = h[1]; nunits = h[5]; nhunits = h[6]; nheavy = h[7]; ntile = h[8]; nred = h[9]; ntblk = h[11];
-    has_diag = h[12] & 1; segp = (uint32_t)h[12] >> 1; nnz = h[13]; nslots = h[14];
+    has_diag = h[12] & 1; segp = ((uint32_t)h[12] >> 1) & ((1u << 29) - 1); tops = ((uint32_t)h[12] >> 30) & 1;
+    nnz = h[13]; nslots = h[14];
     items = 16;
     units = (items + 2 * nnz + 3) & ~3LL;
     heavy = units + 4 * nunits;
@@ -764,83 +766,99 @@ spmm_row_kernel(RowPlan rp, int32_t nhb, const float* __restrict__ B, int64_t ld
     return;
   }
   // publish this segment's partial, then count in; the last arriver sums all of
-  // the group's partials in segment order.  A row of more than kMaxSeg segments
-  // is cut into groups of at most kMaxSeg (heavy entry .w = parent * 64 + group,
-  // -1 at the top): a group's last arriver publishes the group's sum into its
-  // parent's slot and counts in there, so no combine reads more than kMaxSeg
-  // partials and segments stay ipc-sized on power-law rows (one level per loop
-  // turn; the parent's last arriver stores the row)
-  int32_t hid = un.w >> 6;  // heavy entry, slot un.w & 63
-  int32_t slot = un.w & 63;
-  int4 hv = rp.heavy[hid];
-  T val = acc;
-  for (;;) {
-    int32_t* ctr = rp.cnt + (int64_t)hid * kMaxColTiles + blockIdx.y;
-    int32_t last = 0;
-    // (the entry, hence the slot row, is wave-uniform; lane group 0 stores)
-    if constexpr (LPR == 64) {
-      if (q == 0 && colok) store_coherent_v(uniform_ptr(part + (int64_t)(hv.y + slot) * part_ld), colv, val);
-    } else {
-      if (q == 0 && colok) store_coherent(part + (int64_t)(hv.y + slot) * part_ld + colv, val);
-    }
-    if (!WG || w == 0) {  // the wavefront that stored counts in, after its stores completed
-      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-      int32_t arrived = 0;
-      if (lane == 0) arrived = __hip_atomic_fetch_add(ctr, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-      last = __builtin_amdgcn_readfirstlane(arrived) == hv.z - 1;
-    }
-    if constexpr (WG) {
-      if (tid == 0) s_last = last;
-      __syncthreads();
-      last = s_last;
-    }
-    stamp(epi, 3);
-    if (!last) return;
-    const bool top = hv.w < 0;  // (workgroup-uniform)
-    // group q sums slots q, q + GS, ... (U loads in flight), then the groups meet
-    if constexpr (LPR == 64)
-      if (top) proj.template begin<BLOCK>(pa, F);  // in flight with the partial loads
-    T sum = V::zero();
-    if (colok) {
-      const float* p0 = uniform_ptr(part + (int64_t)hv.y * part_ld);
-      for (int32_t s0 = q; s0 < hv.z; s0 += GS * U) {
-        T pv[U];
-#pragma unroll
-        for (int j = 0; j < U; ++j) {
-          const int32_t sl = s0 + GS * j;
-          // base: the entry's first slot (wave-uniform); byte offsets stay below
-          // kMaxSeg * part_ld * 4 < 2^31 (checked at launch)
-          if constexpr (LPR == 64)
-            pv[j] = sl < hv.z ? load_coherent_v<T>(p0, (int64_t)sl * part_ld + colv) : V::zero();
-          else
-            pv[j] = sl < hv.z ? load_coherent<T>(p0 + (int64_t)sl * part_ld + colv) : V::zero();
-        }
-#pragma unroll
-        for (int j = 0; j < U; ++j)
-          if (s0 + GS * j < hv.z) V::add(sum, pv[j]);
-      }
-    }
-    wave_group_sum<LPR>(sum);
-    if constexpr (WG) {
-      __syncthreads();  // s_red reuse
-      if (w > 0) s_red[w][lane] = sum;
-      __syncthreads();
-#pragma unroll
-      for (int v = 1; v < WPB; ++v) V::add(sum, s_red[v][lane]);
-    }
-    if (q == 0 && lane == 0) __hip_atomic_store(ctr, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);  // re-armed
-    if (!top) {  // a group of a long row: its sum goes up one level
-      hid = hv.w >> 6;
-      slot = hv.w & 63;
-      hv = rp.heavy[hid];
-      val = sum;
-      continue;
-    }
-    if constexpr (LPR == 64) proj.template finish_stage<BLOCK>(pa, F);  // the last arriver (workgroup-uniform)
-    if (q == 0) finish_row<LPR, VEC, NP>(sum, hv.x, colv, colok, bv, lg, C, ldc, epi, store_main, proj, pa);
-    stamp(epi, 3);
-    return;
+  // the entry's partials in segment order.  A row of more than kMaxSeg segments
+  // has one entry per group of at most kMaxSeg of them (.w = the row's slot for
+  // the group's sum) and a top entry (.w = -2) whose slots spmm_heavy_top_kernel
+  // sums after this launch: segments stay ipc-sized on power-law rows and no
+  // combine reads more than kMaxSeg partials
+  const int32_t hid = un.w >> 6;  // heavy entry, segment un.w & 63
+  const int4 hv = rp.heavy[hid];
+  int32_t* ctr = rp.cnt + (int64_t)hid * kMaxColTiles + blockIdx.y;
+  int32_t last = 0;
+  // (the unit, hence the slot row, is wave-uniform; lane group 0 stores)
+  if constexpr (LPR == 64) {
+    if (q == 0 && colok) store_coherent_v(uniform_ptr(part + (int64_t)(hv.y + (un.w & 63)) * part_ld), colv, acc);
+  } else {
+    if (q == 0 && colok) store_coherent(part + (int64_t)(hv.y + (un.w & 63)) * part_ld + colv, acc);
   }
+  if (!WG || w == 0) {  // the wavefront that stored counts in, after its stores completed
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    int32_t arrived = 0;
+    if (lane == 0) arrived = __hip_atomic_fetch_add(ctr, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    last = __builtin_amdgcn_readfirstlane(arrived) == hv.z - 1;
+  }
+  if constexpr (WG) {
+    if (tid == 0) s_last = last;
+    __syncthreads();
+    last = s_last;
+  }
+  stamp(epi, 3);
+  if (!last) return;
+  // group q sums slots q, q + GS, ... (U loads in flight), then the groups meet
+  if constexpr (LPR == 64) proj.template begin<BLOCK>(pa, F);  // in flight with the partial loads
+  T sum = V::zero();
+  if (colok) {
+    const float* p0 = uniform_ptr(part + (int64_t)hv.y * part_ld);
+    for (int32_t s0 = q; s0 < hv.z; s0 += GS * U) {
+      T pv[U];
+#pragma unroll
+      for (int j = 0; j < U; ++j) {
+        const int32_t sl = s0 + GS * j;
+        // base: the row's first slot (wave-uniform); byte offsets stay below
+        // kMaxSeg * part_ld * 4 < 2^31 (checked at launch)
+        if constexpr (LPR == 64)
+          pv[j] = sl < hv.z ? load_coherent_v<T>(p0, (int64_t)sl * part_ld + colv) : V::zero();
+        else
+          pv[j] = sl < hv.z ? load_coherent<T>(p0 + (int64_t)sl * part_ld + colv) : V::zero();
+      }
+#pragma unroll
+      for (int j = 0; j < U; ++j)
+        if (s0 + GS * j < hv.z) V::add(sum, pv[j]);
+    }
+  }
+  wave_group_sum<LPR>(sum);
+  if constexpr (WG) {
+    __syncthreads();  // s_red reuse
+    if (w > 0) s_red[w][lane] = sum;
+    __syncthreads();
+#pragma unroll
+    for (int v = 1; v < WPB; ++v) V::add(sum, s_red[v][lane]);
+  }
+  if constexpr (LPR == 64) proj.template finish_stage<BLOCK>(pa, F);  // the last arriver (workgroup-uniform)
+  if (q == 0) {
+    if (hv.w >= 0) {  // a group of a row of > kMaxSeg segments: its sum into the row's slot hv.w
+      if constexpr (LPR == 64) {
+        if (colok) store_coherent_v(uniform_ptr(part + (int64_t)hv.w * part_ld), colv, sum);
+      } else {
+        if (colok) store_coherent(part + (int64_t)hv.w * part_ld + colv, sum);
+      }
+    } else {
+      finish_row<LPR, VEC, NP>(sum, hv.x, colv, colok, bv, lg, C, ldc, epi, store_main, proj, pa);
+    }
+    if (lane == 0) __hip_atomic_store(ctr, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  }
+  stamp(epi, 3);
+}
+
+// Rows of more than kMaxSeg segments, after the row kernel: each top heavy
+// entry's slots (its groups' sums, in group order) summed, the epilogue applied,
+// the row stored.  One workgroup per heavy entry (entries that are not tops
+// exit at once) x column tile of 256 VEC.
+template <int VEC>
+__global__ void __launch_bounds__(256) spmm_heavy_top_kernel(const int4* __restrict__ heavy, int32_t nheavy,
+                                                            const float* __restrict__ part, int64_t part_ld, int32_t F,
+                                                            float* __restrict__ C, int64_t ldc, Epi epi) {
+  resolve_rng(epi);
+  using V = Vec<VEC>;
+  using T = typename V::T;
+  const int4 hv = heavy[blockIdx.x];
+  if (hv.w != -2) return;   // (workgroup-uniform)
+  const int64_t colv = ((int64_t)blockIdx.y * 256 + threadIdx.x) * VEC;
+  if (colv >= F) return;
+  T acc = V::zero();
+  for (int32_t s = 0; s < hv.z; ++s) V::add(acc, load_coherent<T>(part + (int64_t)(hv.y + s) * part_ld + colv));
+  const T bv = epi.bias ? V::load(epi.bias + colv) : V::zero();
+  V::store(C + (int64_t)hv.x * ldc + colv, V::epi(epi, acc, bv, hv.x, colv));
 }
 
 // ---------------------------------------------------------------------------
@@ -1555,6 +1573,7 @@ int host_plan(const int32_t* rp, const int32_t* ci, const float* vv, int32_t M, 
   std::vector<std::vector<int32_t>> hq(NX), lq(NX);  // int4 units per class
   int32_t nheavy = 0;
   int64_t nslots = 0;
+  bool any_top = false;
   hp.units.clear();
   hp.heavy.clear();
   std::vector<int64_t> rb, rcl;  // runs of one column class: start, class
@@ -1599,17 +1618,19 @@ int host_plan(const int32_t* rp, const int32_t* ci, const float* vv, int32_t M, 
     // heavy entries: one (nseg <= kMaxSeg), or a top entry over ng groups of
     // consecutive segments (group g: segments [g nseg / ng, (g + 1) nseg / ng))
     const int64_t ng = nseg <= kMaxSeg ? 1 : (nseg + kMaxSeg - 1) / kMaxSeg;
-    int32_t top = -1;
+    int64_t top_slot = -1;
     if (ng > 1) {
-      top = nheavy++;
-      hp.heavy.insert(hp.heavy.end(), {r, (int32_t)nslots, (int32_t)ng, -1});
+      ++nheavy;
+      hp.heavy.insert(hp.heavy.end(), {r, (int32_t)nslots, (int32_t)ng, -2});
+      top_slot = nslots;
       nslots += ng;
+      any_top = true;
     }
     std::vector<int32_t> seg_w((size_t)nseg);
     for (int64_t g = 0; g < ng; ++g) {
       const int64_t s0 = g * nseg / ng, s1 = (g + 1) * nseg / ng;
       const int32_t hid = nheavy++;
-      hp.heavy.insert(hp.heavy.end(), {r, (int32_t)nslots, (int32_t)(s1 - s0), ng > 1 ? (int32_t)((int64_t)top * 64 + g) : -1});
+      hp.heavy.insert(hp.heavy.end(), {r, (int32_t)nslots, (int32_t)(s1 - s0), ng > 1 ? (int32_t)(top_slot + g) : -1});
       for (int64_t sgi = s0; sgi < s1; ++sgi) seg_w[(size_t)sgi] = (int32_t)((int64_t)hid * 64 + (sgi - s0));
       nslots += s1 - s0;
     }
@@ -1692,7 +1713,7 @@ int host_plan(const int32_t* rp, const int32_t* ci, const float* vv, int32_t M, 
       if (hp.units[(size_t)(4 * u)] >= 0)
         segp = std::max<int64_t>(segp, (int64_t)hp.units[(size_t)(4 * u + 2)] - hp.units[(size_t)(4 * u + 1)]);
   segp = (segp + 3) & ~3LL;
-  if (segp > (1 << 29) || 2 * nh * segp >= (int64_t)INT32_MAX) segp = 0;   // (never for real plans: keep the old path)
+  if (segp >= (1 << 28) || 2 * nh * segp >= (int64_t)INT32_MAX) segp = 0;   // (never for real plans: keep the old path)
   layout(lq, lpb);
   const int64_t nunits = (int64_t)hp.units.size() / 4;
   if (nunits >= (int64_t)INT32_MAX || nslots >= (int64_t)INT32_MAX || nheavy >= (1 << 25)) {
@@ -1701,7 +1722,7 @@ int host_plan(const int32_t* rp, const int32_t* ci, const float* vv, int32_t M, 
     return GCNK_EUNSUP;
   }
   const int32_t h[16] = {kMagic, M,     K,      groups, ipc,  (int32_t)nunits, (int32_t)nh, nheavy,
-                         ntile,  nred, nslabs, ntblk,  (any_diag ? 1 : 0) | (int32_t)(segp << 1), (int32_t)nnz,
+                         ntile,  nred, nslabs, ntblk,  (any_diag ? 1 : 0) | (int32_t)(segp << 1) | (any_top ? 1 << 30 : 0), (int32_t)nnz,
                          (int32_t)nslots, nsingle};
   std::copy(h, h + 16, hp.hdr);
   return GCNK_OK;
@@ -1911,6 +1932,8 @@ extern "C" int gcnk_spmm_plan_query(const void* plan, int32_t* out16, void* stre
 
 static int64_t tile_fpad(int32_t F) { return ((int64_t)F + 15) & ~15LL; }
 
+static bool L_tops(const int32_t* hdr) { return ((uint32_t)hdr[12] >> 30) & 1; }
+
 static bool plan_magic(const int32_t* hdr) {
   return hdr && hdr[0] == kMagic;
 }
@@ -1996,7 +2019,7 @@ static int spmm_impl(const void* plan, const int32_t* hdr, const float* B, int64
   hipStream_t s = (hipStream_t)stream;
   if (proj) {
     // the projection needs whole rows in one group: row-kernel rows only, float4, one column tile
-    if (hdr[8] > 0 || !vec4 || F > lpr * 4 || pa.P > 32 || lpr < 16) {
+    if (hdr[8] > 0 || !vec4 || F > lpr * 4 || pa.P > 32 || lpr < 16 || L_tops(hdr)) {
       set_error("gcnk_spmm_proj_f32: fused projection unsupported here (tile chunks=%d vec4=%d F=%d P=%d lanes=%d)",
                 hdr[8], (int)vec4, F, pa.P, lpr);
       return GCNK_EUNSUP;
@@ -2047,7 +2070,18 @@ static int spmm_impl(const void* plan, const int32_t* hdr, const float* B, int64
                L.segp > 0 ? reinterpret_cast<const int2*>(p + L.hitems) : nullptr, (int32_t)L.segp};
     RowLaunch a{rp, K, B, ldb, F, C, ldc, e, workspace, part_ld, pa, s};
     if (proj) return pa.P <= 8 ? dispatch_rows_proj<8>(lpr, a) : dispatch_rows_proj<32>(lpr, a);
-    return vec4 ? dispatch_rows<4>(lpr, a) : dispatch_rows<1>(lpr, a);
+    const int rc = vec4 ? dispatch_rows<4>(lpr, a) : dispatch_rows<1>(lpr, a);
+    if (rc || !L.tops) return rc;
+    // rows of more than kMaxSeg segments: their groups' sums, after the row kernel
+    const int vec = vec4 ? 4 : 1;
+    const dim3 grid((unsigned)L.nheavy, (unsigned)((F + 256 * vec - 1) / (256 * vec)));
+    if (vec4)
+      hipLaunchKernelGGL(spmm_heavy_top_kernel<4>, grid, dim3(256), 0, s, reinterpret_cast<const int4*>(p + L.heavy),
+                         (int32_t)L.nheavy, workspace, part_ld, F, C, ldc, e);
+    else
+      hipLaunchKernelGGL(spmm_heavy_top_kernel<1>, grid, dim3(256), 0, s, reinterpret_cast<const int4*>(p + L.heavy),
+                         (int32_t)L.nheavy, workspace, part_ld, F, C, ldc, e);
+    return launch_check("spmm_heavy_top_kernel");
   }
   return GCNK_OK;
 }

@@ -6,8 +6,8 @@ the class-by-workgroup layout with empty padding units) and the row kernel's
 control flow (light units per lane group, heavy segments shared by lane
 groups, partial slots and the last-arriver combine in segment order; rows of
 more than K_MAX_SEG segments in groups whose last arrivers publish the group
-sums one level up), so the control logic can be checked on CPU against a
-dense product."""
+sums into the row's top entry, summed by spmm_heavy_top_kernel after the
+launch), so the control logic can be checked on CPU against a dense product."""
 import numpy as np
 
 K_MAX_SEG = 64
@@ -31,7 +31,8 @@ def geometry(groups):
 
 
 def host_plan(rowptr, colind, K, ipc, groups):
-    """-> (units [(row, b, e, w)], heavy [(row, first slot, slots, parent * 64 + slot or -1)], nh, nslots)."""
+    """-> (units [(row, b, e, w)], heavy [(row, first slot, slots, w)], nh, nslots); heavy w: -1 one
+    level, -2 a top entry (slots = its groups' sums), >= 0 a group (w = the top's slot for its sum)."""
     hpb, lpb, seg_groups, lpr = geometry(groups)
     seg = ipc * seg_groups
     light_max = min(2 * ipc, 32) if lpr == 64 else ipc
@@ -65,16 +66,16 @@ def host_plan(rowptr, colind, K, ipc, groups):
             hq[runs[0][1]].append((r, b, e, -1))
             continue
         ng = 1 if nseg <= K_MAX_SEG else (nseg + K_MAX_SEG - 1) // K_MAX_SEG
-        top = -1
+        top_slot = -1
         if ng > 1:
-            top = len(heavy)
-            heavy.append((r, nslots, ng, -1))
+            heavy.append((r, nslots, ng, -2))
+            top_slot = nslots
             nslots += ng
         seg_w = [0] * nseg
         for g in range(ng):
             s0, s1 = g * nseg // ng, (g + 1) * nseg // ng
             hid = len(heavy)
-            heavy.append((r, nslots, s1 - s0, top * 64 + g if ng > 1 else -1))
+            heavy.append((r, nslots, s1 - s0, top_slot + g if ng > 1 else -1))
             for sgi in range(s0, s1):
                 seg_w[sgi] = hid * 64 + sgi - s0
             nslots += s1 - s0
@@ -129,20 +130,22 @@ def spmm(rowptr, colind, val, B, ipc, groups):
             C[r] = acc
             written[r] += 1
             continue
-        hid, slot, pv = w >> 6, w & 63, acc
-        while True:
-            hr, first, nsl, up = heavy[hid]
-            assert nsl <= K_MAX_SEG, "no combine reads more than K_MAX_SEG partials"
-            part[first + slot] = pv
-            arrivals[hid] += 1
-            if arrivals[hid] < nsl:
-                break
-            pv = sum(part[first + s] for s in range(nsl))    # last arriver: slots in order
-            if up < 0:
-                C[hr] = pv
+        hid, slot = w >> 6, w & 63
+        hr, first, nsl, up = heavy[hid]
+        assert nsl <= K_MAX_SEG, "no combine reads more than K_MAX_SEG partials"
+        part[first + slot] = acc
+        arrivals[hid] += 1
+        if arrivals[hid] == nsl:        # last arriver: slots in segment order
+            gsum = sum(part[first + s] for s in range(nsl))
+            if up >= 0:                 # a group of a long row: into the top entry's slot
+                part[up] = gsum
+            else:
+                C[hr] = gsum
                 written[hr] += 1
-                break
-            hid, slot = up >> 6, up & 63                      # a group's sum goes up one level
+    for hr, first, nsl, up in heavy:    # after the launch: spmm_heavy_top_kernel
+        if up == -2:
+            C[hr] = sum(part[first + s] for s in range(nsl))
+            written[hr] += 1
     for u in range(nh, len(units)):
         r, b, e, _ = units[u]
         if r < 0:

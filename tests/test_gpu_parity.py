@@ -121,6 +121,8 @@ def test_spmm_power_law_rows_and_linearity(rmat17, F):
     B1 = torch.from_numpy(rng.standard_normal((n, F)).astype(np.float32)).to(DEV)
     B2 = torch.from_numpy(rng.standard_normal((n, F)).astype(np.float32)).to(DEV)
     C1 = spmm(a, B1)
+    if F == 256:   # rows past 64 segments: groups + the top-entry launch (spmm_heavy_top_kernel)
+        assert any((p.header[12] >> 30) & 1 for p in a._plans.values())
     rows = np.unique(np.concatenate([np.argsort(deg)[-16:], rng.choice(n, 400, replace=False),
                                      np.flatnonzero(deg == 0)[:8]]))
     sub_rp = np.concatenate([[0], np.cumsum(deg[rows])])

@@ -65,7 +65,7 @@ def test_power_law_row_takes_two_combine_levels():
     seg = ipc * path_model.geometry(groups)[2]
     hub = [u for u in units[:nh] if u[0] == 0]
     assert len(hub) > path_model.K_MAX_SEG and max(u[2] - u[1] for u in hub) <= seg
-    tops = [h for h in heavy if h[0] == 0 and h[3] == -1]
+    tops = [h for h in heavy if h[0] == 0 and h[3] == -2]
     assert len(tops) == 1 and 1 < tops[0][2] <= path_model.K_MAX_SEG
     assert all(h[2] <= path_model.K_MAX_SEG for h in heavy)
     B = rng.standard_normal((K, 2))

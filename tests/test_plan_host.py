@@ -125,7 +125,8 @@ def test_power_law_hub_keeps_short_segments_two_levels():
     """on an R-MAT graph whose hub rows hold ~10^4
     nonzeros the plan keeps every heavy segment at the base length (ipc x the
     workgroup's lane groups; it used to double it past 64 segments) and gives
-    such a row a top heavy entry over groups of <= 64 segments; no heavy entry
+    such a row a top heavy entry (.w = -2) over groups of <= 64 segments, each
+    group's .w the top's slot for its sum; no heavy entry
     has more than 64 slots, slots never overlap, and the units cover every
     nonzero of the heavy rows exactly once."""
     from graph_convolutional_networks_for_text_classification_amd import datasets
@@ -144,10 +145,12 @@ def test_power_law_hub_keeps_short_segments_two_levels():
     hu = units[:nh][units[:nh, 0] == hub]
     assert len(hu) > 64 and (hu[:, 2] - hu[:, 1]).max() <= seg
     assert (heavy[:, 2] <= 64).all() and (heavy[:, 2] >= 1).all()
-    tops = heavy[(heavy[:, 0] == hub) & (heavy[:, 3] == -1)]
+    assert (hdr[12] >> 30) & 1, "the plan flags its two-level rows"
+    tops = heavy[(heavy[:, 0] == hub) & (heavy[:, 3] == -2)]
     assert len(tops) == 1 and tops[0, 2] > 1
     groups_of_hub = heavy[(heavy[:, 0] == hub) & (heavy[:, 3] >= 0)]
-    assert len(groups_of_hub) == tops[0, 2] and (groups_of_hub[:, 3] & 63).tolist() == list(range(tops[0, 2]))
+    assert len(groups_of_hub) == tops[0, 2]
+    assert groups_of_hub[:, 3].tolist() == list(range(tops[0, 1], tops[0, 1] + tops[0, 2]))
     assert groups_of_hub[:, 2].sum() == len(hu)
     slots = np.concatenate([np.arange(h[1], h[1] + h[2]) for h in heavy])
     assert len(np.unique(slots)) == len(slots) == hdr[14]

@@ -137,6 +137,14 @@ SIGNATURES = {
     "gcnk_gcn_fwd_layout": (_i32, [_vp, _i32]),
     "gcnk_factor_u_f32": (ctypes.c_int, [_vp, _vp, _vp, _i32, _vp, _vp, _vp, _i64, _i32, _vp, _i64, _i32, _vp]),
     "gcnk_factor_records": (ctypes.c_int, [_vp, _vp, _vp, _i32, _vp, _vp, _vp, _i32, _vp, _vp]),
+    "gcnk_factor_analyze_workspace_bytes": (_i64, [_i32, _i32]),
+    # rowptr, colind, M, hmin, x_rowptr, x_colind, x_val, x_dense, ldx, K, max_hubs, info, hubs, cnt (host),
+    # workspace, bytes, stream
+    "gcnk_factor_analyze": (ctypes.c_int, [_vp, _vp, _i32, _i32, _vp, _vp, _vp, _vp, _i64, _i32, _i32, _vp, _vp, _vp,
+                                           _vp, _i64, _vp]),
+    "gcnk_factor_xl_f32": (ctypes.c_int, [_vp, _vp, _vp, _i32, _vp, _i32, _i32, _vp, _i64, _i32, _vp]),
+    "gcnk_csr_gather_rows": (ctypes.c_int, [_vp, _vp, _vp, _vp, _i32, _vp, _vp, _vp, _vp]),
+    "gcnk_dense_gather_rows_f32": (ctypes.c_int, [_vp, _i64, _i32, _vp, _i32, _vp, _i64, _vp]),
     "gcnk_gcn_backward_f32": (ctypes.c_int, [_vp, _vp, _vp, _i64, _vp, _f32, _vp, _vp, _vp, _vp, _vp]),
     "gcnk_class_stats": (ctypes.c_int, [_vp, _i64, _vp, _vp, _i64, _i32, _vp, _vp]),
     "gcnk_edgelist_size": (ctypes.c_int, [ctypes.c_char_p, _vp, _vp]),

@@ -80,42 +80,45 @@ def _perm(hubs, M):
 
 def build(adj, xop):
     """HubFactor for (adj, X) on adj's device, or None when the operands lack
-    the structure.  The structure tests (hub rows, light rows touching only hub
-    columns and themselves, X's light-row column range) are device reductions
-    read back once each; U and the A_H records are csrc/factor_build.hip
-    (fixed-order float64 sums, bitwise the host restatement oracle/factor_host.py)."""
+    the structure.  The structure test (hub rows, light rows touching only hub
+    columns and themselves, X's light-row column range, per-row hub-item
+    counts) is one device pass read back once (gcnk_factor_analyze); X's light
+    rows (Xl), U, the A_H records and X's hub rows are library kernels
+    (csrc/factor_build.hip: fixed-order float64 sums, bitwise the host
+    restatement oracle/factor_host.py).  No torch kernel runs here: their
+    first-use module loads were ~120 ms of the first forward (round 5)."""
+    import ctypes
+
     from . import _lib
     M, K = adj.shape
     if M != K or xop.shape[0] != M:
         return None
     dev = adj.device
     lib = _lib.load()
-    rp, ci, v = adj.rowptr, adj.colind, adj.val
+    stream = ctypes.c_void_p(torch.cuda.current_stream(dev).cuda_stream)
     nnz = adj.nnz
-    deg = rp[1:] - rp[:-1]
     hmin = max(64, 8 * ((nnz + M - 1) // M))
-    hubs = torch.nonzero(deg >= hmin).flatten()
-    H = hubs.numel()
-    if H == 0 or H > MAX_HUBS or H >= M:
-        return None
-    is_hub = torch.zeros(M, dtype=torch.bool, device=dev)
-    is_hub[hubs] = True
-    ar = torch.arange(M, device=dev, dtype=torch.int32)
-    rows = torch.repeat_interleave(ar, deg, output_size=nnz)
-    cil = ci.long()
-    if bool((~is_hub[rows] & ~is_hub[cil] & (ci != rows)).any()):
-        return None
-    # X's light rows: column range [k0, k0 + Kc)
-    if xop.csr is not None:
-        x = xop.csr
-        xrows = torch.repeat_interleave(torch.arange(x.shape[0], device=dev, dtype=torch.int32),
-                                        x.rowptr[1:] - x.rowptr[:-1], output_size=x.nnz)
-        sel = ~is_hub[xrows.long()] & (x.val != 0)
-        cols = x.colind[sel]
+    x = xop.csr
+    info = np.zeros(8, np.int32)
+    found = np.zeros(MAX_HUBS + 1, np.int32)
+    cnt = np.zeros(M, np.int32)
+    wsb = int(lib.gcnk_factor_analyze_workspace_bytes(M, MAX_HUBS + 1))
+    ws = torch.empty(wsb, dtype=torch.uint8, device=dev)
+    if x is not None:
+        xa = (x.rowptr.data_ptr(), x.colind.data_ptr(), x.val.data_ptr(), None, 0, x.shape[1])
     else:
-        cols = torch.nonzero((xop.dense[~is_hub] != 0).any(0)).flatten()
-    if cols.numel():
-        k0, k1 = (int(t) for t in torch.stack([cols.min(), cols.max()]).cpu())
+        if xop.dense.stride(1) != 1:
+            raise RuntimeError("factor.build: dense features need unit column stride")
+        xa = (None, None, None, xop.dense.data_ptr(), xop.dense.stride(0), xop.shape[1])
+    with torch.cuda.device(dev):
+        _lib.check(lib.gcnk_factor_analyze(adj.rowptr.data_ptr(), adj.colind.data_ptr(), M, hmin, *xa, MAX_HUBS + 1,
+                                           info.ctypes.data, found.ctypes.data, cnt.ctypes.data, ws.data_ptr(), wsb,
+                                           stream), "gcnk_factor_analyze")
+    H, bad, k0, k1, xtot = (int(t) for t in info[:5])
+    if H == 0 or H > MAX_HUBS or H >= M or bad:
+        return None
+    hubs_h = np.sort(found[:H])
+    if k1 >= 0:
         k1 += 1
     else:
         k0, k1 = 0, 1
@@ -123,65 +126,64 @@ def build(adj, xop):
     if Kc > MAX_KC:
         return None
     Kcp = (Kc + 3) // 4 * 4
-    hubs_h = hubs.cpu().numpy()
     perm = _perm(hubs_h, M)
+    hub_index_h = np.full(M, -1, np.int32)
+    hub_index_h[hubs_h] = np.arange(H, dtype=np.int32)
+    # (host -> device copies only: no kernel launches)
     perm_d = torch.from_numpy(perm.astype(np.int32)).to(dev)
-    hub_index = torch.full((M,), -1, dtype=torch.int32, device=dev)
-    hub_index[hubs] = torch.arange(H, device=dev, dtype=torch.int32)
-    # X's light rows, columns [k0, k1), dense (hub rows never read)
-    if xop.csr is not None:
-        Xl = torch.zeros((M, Kcp), dtype=torch.float32, device=dev)
-        Xl[xrows[sel].long(), (cols - k0).long()] = x.val[sel]
-        ldxl = Kcp
-    else:
-        Xl = xop.dense[:, k0:]
-        ldxl = xop.dense.stride(0)
-        if xop.dense.stride(1) != 1:
-            raise RuntimeError("factor.build: dense features need unit column stride")
-    stream = torch.cuda.current_stream(dev).cuda_stream
-    U = torch.empty((M, Kcp), dtype=torch.float32, device=dev)
-    _lib.check(lib.gcnk_factor_u_f32(rp.data_ptr(), ci.data_ptr(), v.data_ptr(), M, hub_index.data_ptr(),
-                                     perm_d.data_ptr(), Xl.data_ptr(), ldxl, Kc, U.data_ptr(), Kcp, Kcp, stream),
-               "gcnk_factor_u_f32")
-    # A_H records: each block's hub items sized from per-row counts in block order
+    hub_index = torch.from_numpy(hub_index_h).to(dev)
+    hubs_d = torch.from_numpy(hubs_h.astype(np.int32)).to(dev)
     nblk = (M + ROWS_PER_BLOCK - 1) // ROWS_PER_BLOCK
-    hub_item = is_hub[cil].to(torch.int32)
-    cs = torch.zeros(nnz + 1, dtype=torch.int64, device=dev)
-    cs[1:] = torch.cumsum(hub_item, 0)
-    counts = cs[rp[1:].long()] - cs[rp[:-1].long()]
-    pc = torch.zeros(nblk * ROWS_PER_BLOCK, dtype=torch.int64, device=dev)
-    pc[:M] = counts[perm_d.long()]
-    rec_words = (REC_HEAD + 2 * int(pc.view(nblk, ROWS_PER_BLOCK).sum(1).max()) + 3) // 4 * 4
-    rec = torch.zeros((nblk, rec_words), dtype=torch.int32, device=dev)
-    overflow = torch.zeros(1, dtype=torch.int32, device=dev)
-    _lib.check(lib.gcnk_factor_records(rp.data_ptr(), ci.data_ptr(), v.data_ptr(), M, hub_index.data_ptr(),
-                                       perm_d.data_ptr(), rec.data_ptr(), rec_words, overflow.data_ptr(), stream),
-               "gcnk_factor_records")
-    f = HubFactor()
+    pc = np.zeros(nblk * ROWS_PER_BLOCK, np.int64)
+    pc[:M] = cnt[perm]
+    rec_words = (REC_HEAD + 2 * int(pc.reshape(nblk, ROWS_PER_BLOCK).sum(1).max()) + 3) // 4 * 4
+    U = torch.empty((M, Kcp), dtype=torch.float32, device=dev)
+    rec = torch.empty((nblk, rec_words), dtype=torch.int32, device=dev)
+    overflow = torch.empty(1, dtype=torch.int32, device=dev)
+    rp, ci, v = adj.rowptr, adj.colind, adj.val
+    with torch.cuda.device(dev):
+        # X's light rows, columns [k0, k1), dense (hub rows never read)
+        if x is not None:
+            Xl = torch.empty((M, Kcp), dtype=torch.float32, device=dev)
+            _lib.check(lib.gcnk_factor_xl_f32(x.rowptr.data_ptr(), x.colind.data_ptr(), x.val.data_ptr(), M,
+                                              hub_index.data_ptr(), k0, Kc, Xl.data_ptr(), Kcp, Kcp, stream),
+                       "gcnk_factor_xl_f32")
+            xl_ptr, ldxl = Xl.data_ptr(), Kcp
+        else:
+            xl_ptr, ldxl = xop.dense.data_ptr() + 4 * k0, xop.dense.stride(0)
+        _lib.check(lib.gcnk_factor_u_f32(rp.data_ptr(), ci.data_ptr(), v.data_ptr(), M, hub_index.data_ptr(),
+                                         perm_d.data_ptr(), xl_ptr, ldxl, Kc, U.data_ptr(), Kcp, Kcp, stream),
+                   "gcnk_factor_u_f32")
+        # A_H records: each block's hub items, sized from the per-row counts in block order
+        _lib.check(lib.gcnk_factor_records(rp.data_ptr(), ci.data_ptr(), v.data_ptr(), M, hub_index.data_ptr(),
+                                           perm_d.data_ptr(), rec.data_ptr(), rec_words, overflow.data_ptr(), stream),
+                   "gcnk_factor_records")
+        f = HubFactor()
+        if x is not None:
+            # X's hub rows as a CSR (rows in hub order)
+            hrp = torch.empty(H + 1, dtype=torch.int32, device=dev)
+            hci = torch.empty(max(xtot, 1), dtype=torch.int32, device=dev)
+            hv = torch.empty(max(xtot, 1), dtype=torch.float32, device=dev)
+            _lib.check(lib.gcnk_csr_gather_rows(x.rowptr.data_ptr(), x.colind.data_ptr(), x.val.data_ptr(),
+                                                hubs_d.data_ptr(), H, hrp.data_ptr(), hci.data_ptr(), hv.data_ptr(),
+                                                stream), "gcnk_csr_gather_rows")
+            f.x_hub = CSR(hrp, hci[:xtot], hv[:xtot], (H, x.shape[1]))
+            f.x_hub_dense = None
+        else:
+            f.x_hub = None
+            kx = xop.shape[1]
+            d = torch.empty((H, (kx + 3) // 4 * 4), dtype=torch.float32, device=dev)   # rows padded to 4 floats
+            _lib.check(lib.gcnk_dense_gather_rows_f32(xop.dense.data_ptr(), xop.dense.stride(0), kx,
+                                                      hubs_d.data_ptr(), H, d.data_ptr(), d.stride(0), stream),
+                       "gcnk_dense_gather_rows_f32")
+            f.x_hub_dense = d[:, :kx]
     f.nblk = nblk
     f.M, f.H, f.k0, f.Kc = M, H, k0, Kc
     f.K = xop.shape[1]
-    f.hubs = hubs.to(torch.int64)
-    f.perm = torch.from_numpy(perm.astype(np.int64))            # host: tests and tools
+    f.hubs = torch.from_numpy(hubs_h.astype(np.int64))            # host: tests and tools
+    f.perm = torch.from_numpy(perm.astype(np.int64))              # host: tests and tools
     f.U, f.rec, f.rec_words = U, rec, rec_words
-    if xop.csr is not None:
-        # X's hub rows as a CSR (rows in hub order)
-        xrp = x.rowptr.long()
-        lens = xrp[hubs + 1] - xrp[hubs]
-        hrp = torch.zeros(H + 1, dtype=torch.int64, device=dev)
-        hrp[1:] = torch.cumsum(lens, 0)
-        tot = int(hrp[-1])
-        idx = torch.repeat_interleave(xrp[hubs] - hrp[:-1], lens, output_size=tot) + \
-            torch.arange(tot, device=dev, dtype=torch.int64)
-        f.x_hub = CSR(hrp.to(torch.int32), x.colind[idx], x.val[idx], (H, x.shape[1]))
-        f.x_hub_dense = None
-    else:
-        f.x_hub = None
-        kx = xop.shape[1]
-        d = torch.zeros((H, (kx + 3) // 4 * 4), dtype=torch.float32, device=dev)   # rows padded to 4 floats
-        d[:, :kx] = xop.dense.index_select(0, f.hubs)
-        f.x_hub_dense = d[:, :kx]
-    if int(overflow.item()) != 0:
+    if int(overflow.item()) != 0:   # (a device -> host copy, no kernel)
         raise RuntimeError("factor.build: A_H records overflowed their sized length (internal error)")
     return f
 

@@ -298,15 +298,47 @@ int gcnk_aggregate_f32(const int32_t* rowptr, const int32_t* colind, const float
  *                        Kc <= c < Kcp <= 128.  Xl [M x >= Kc] (ldxl): X's
  *                        columns k0.. (hub rows never read).
  *   gcnk_factor_records: the per-32-row-block A_H records gcnk_hubfactor_gc1_f32
- *                        reads, into a zeroed rec [ceil(M/32) x rec_words];
- *                        *overflow (zeroed int) counts blocks whose items
- *                        did not fit. */
+ *                        reads, into rec [ceil(M/32) x rec_words] (zeroed by
+ *                        the call first); *overflow (zeroed by the call)
+ *                        counts blocks whose items did not fit.
+ *   gcnk_factor_analyze: the structure test in front of them, on the device
+ *                        with one host sync (ABI 12; replaces torch element-wise
+ *                        / nonzero / index kernels whose first-use loads cost
+ *                        the first forward ~120 ms): hub rows = rows of >= hmin
+ *                        nonzeros; host outputs info[8] = {H, bad (a light row
+ *                        with a column that is neither a hub nor its diagonal),
+ *                        k0, k1 (column range of X's nonzero entries in light
+ *                        rows, k1 = -1 if none), total length of X's hub rows
+ *                        (CSR X), 0, 0, 0}, hubs[max_hubs] (the first H found,
+ *                        unordered; H > max_hubs: some missing), cnt[M] (each
+ *                        row's hub-column items).  X: CSR (x_rowptr non-NULL, M
+ *                        rows) or dense [M x K] (x_dense, ldx).  Workspace:
+ *                        gcnk_factor_analyze_workspace_bytes(M, max_hubs).
+ *   gcnk_factor_xl_f32:  Xl [M x Kcp] (ldxl) = X[r, k0 .. k0 + Kc) for light
+ *                        rows (hub_index[r] < 0) of a CSR X, zero elsewhere.
+ *   gcnk_csr_gather_rows / gcnk_dense_gather_rows_f32: the rows `rows[0 ..
+ *                        nrows)` of a CSR (out_rowptr[nrows + 1] written; out
+ *                        arrays sized by the caller) or of a dense matrix (out
+ *                        [nrows x ldo], columns K .. ldo - 1 zero): X's hub rows. */
 int gcnk_factor_u_f32(const int32_t* rowptr, const int32_t* colind, const float* val, int32_t M,
                       const int32_t* hub_index, const int32_t* perm, const float* Xl, int64_t ldxl, int32_t Kc,
                       float* U, int64_t ldu, int32_t Kcp, void* stream);
 int gcnk_factor_records(const int32_t* rowptr, const int32_t* colind, const float* val, int32_t M,
                         const int32_t* hub_index, const int32_t* perm, int32_t* rec, int32_t rec_words,
                         int32_t* overflow, void* stream);
+int64_t gcnk_factor_analyze_workspace_bytes(int32_t M, int32_t max_hubs);
+int gcnk_factor_analyze(const int32_t* rowptr, const int32_t* colind, int32_t M, int32_t hmin,
+                        const int32_t* x_rowptr, const int32_t* x_colind, const float* x_val,
+                        const float* x_dense, int64_t ldx, int32_t K, int32_t max_hubs, int32_t* info /* host */,
+                        int32_t* hubs /* host */, int32_t* cnt /* host */, void* workspace, int64_t workspace_bytes,
+                        void* stream);
+int gcnk_factor_xl_f32(const int32_t* x_rowptr, const int32_t* x_colind, const float* x_val, int32_t M,
+                       const int32_t* hub_index, int32_t k0, int32_t Kc, float* Xl, int64_t ldxl, int32_t Kcp,
+                       void* stream);
+int gcnk_csr_gather_rows(const int32_t* rowptr, const int32_t* colind, const float* val, const int32_t* rows,
+                         int32_t nrows, int32_t* out_rowptr, int32_t* out_colind, float* out_val, void* stream);
+int gcnk_dense_gather_rows_f32(const float* X, int64_t ldx, int32_t K, const int32_t* rows, int32_t nrows,
+                               float* out, int64_t ldo, void* stream);
 
 /* ---------------------------------------------------------------------------
  * Whole-forward launch record (ABI 8): GCN.forward (layer.py:164-190) as the

@@ -945,8 +945,10 @@ def main():
             for _ in range(3):
                 forward()
         torch.cuda.current_stream().wait_stream(s)
-        per = max(1, args.graph_steps)
-        while args.steps % per or args.warmup % per:
+        # the largest forwards-per-graph <= --graph-steps that divides --steps
+        # (every replay is `per` complete forwards, so exactly --steps run timed)
+        per = max(1, min(args.graph_steps, args.steps))
+        while args.steps % per:
             per -= 1
         graph = torch.cuda.CUDAGraph()
         with torch.cuda.graph(graph):
@@ -954,8 +956,11 @@ def main():
                 out = forward()
         step = graph.replay
 
+    # exactly --warmup untimed forwards: whole replays, then single eager calls
     for _ in range(args.warmup // per):
         step()
+    for _ in range(args.warmup % per):
+        forward()
     torch.cuda.synchronize()
     if world > 1:
         dist.barrier(device_ids=[torch.cuda.current_device()])

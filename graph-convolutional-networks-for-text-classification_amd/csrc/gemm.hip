@@ -330,93 +330,89 @@ gemm_shortk_kernel(int32_t M, int32_t N, int32_t K, const float* __restrict__ A,
   }
 }
 
-// Small-M, long-K split-K GEMM (NN; M <= 64, N % 4 == 0, lda % 4 == 0,
-// ldb % 4 == 0, A and B 16-B aligned): the slabs of C = A B for the hub rows
-// of a graph whose hub feature rows are dense -- X[hubs] W1 of the factored
-// gc1 (R8: [50 x 7463] x [7463 x 200], 7.5 MB of operands).  The generic tile
-// kernel runs it as 64 x 64 tiles x 64 k-slabs (13.7 us with its reduce) and
-// the tile SpMM on the CSR of those rows 9.8 us.  Here workgroup (s, y) owns
-// k chunk s (16 * KCH deep) and columns [112 y, 112 y + 112): it stages its B
-// chunk in LDS once (every load in flight with the A loads), wave w multiplies
-// rows [16 w, 16 w + 16) by it (7 accumulators over 4 * KCH k steps, the k
-// order inside a 16-deep block permuted alike for A and B as in the skinny
-// kernel) and writes slab s of [S][M][N]; gemm_slab_reduce4_kernel sums the
-// slabs in a fixed order.  Columns of A past K (its row padding up to lda)
-// are zeroed, never multiplied.
-template <int KCH>
-__global__ void __launch_bounds__(256)
-gemm_smallm_splitk_kernel(int32_t M, int32_t N, int32_t K, const float* __restrict__ A, int64_t lda,
-                          const float* __restrict__ B, int64_t ldb, float* __restrict__ slab) {
-  constexpr int NT = 7, BN = 16 * NT, LW = BN + 4, KP = 16 * KCH, NQ = BN / 4;
-  constexpr int PT = (KP * NQ + 255) / 256;
-  __shared__ __attribute__((aligned(16))) float s_B[KP * LW];
+// Small-M, long-K GEMM with the K split INSIDE the workgroup (round 6; NN, M <=
+// 64, N % 4 == 0, lda % 4 == 0, A 16-B aligned): X[hubs] W1 of the factored
+// gc1 with dense hub rows, R8-shaped [50 x 7463] x [7463 x 200].  Round 4's
+// kernel here staged a 64-deep chunk of B in LDS per workgroup and left one
+// slab per chunk (117 slabs, 4.7 MB of partials; 7.7 + 4.7 us with its reduce,
+// profiles/r04_smallm_*).  Here workgroup (s, g) owns slab s (8 x 16 KBW k deep)
+// and 16 NTG columns: wave w takes k blocks [KBW w, KBW w + KBW) of the slab
+// for ALL four 16-row tiles (its B fragments feed four MFMA chains), the eight
+// waves' products meet in LDS in wave order and one slab partial [M x 16 NTG]
+// is written: 30 slabs (1.2 MB) at R8's shape, 1,680 waves carrying the MFMAs.
+// A's 16-deep k block is read as one float4 per lane (k = 16 c + 4 q + j for
+// quadrant q, step j) and B's rows in the same permuted order, so each MFMA
+// still pairs A[row][k] with B[k][col].  Fixed-order sums: reproducible.
+template <int KBW, int NTG>
+__global__ void __launch_bounds__(512)
+gemm_smallm_wk_kernel(int32_t M, int32_t N, int32_t K, const float* __restrict__ A, int64_t lda,
+                      const float* __restrict__ B, int64_t ldb, float* __restrict__ slab) {
+  constexpr int kW = 8, RT = 4;   // waves, 16-row tiles (M <= 64)
+  __shared__ __attribute__((aligned(16))) f32x4 s_acc[kW][RT * NTG][64];
   const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
   const int r = lane & 15, q = lane >> 4;
-  const int64_t k0 = (int64_t)blockIdx.x * KP;
-  const int64_t n0 = (int64_t)blockIdx.y * BN;
-  const int64_t row = 16 * w + r;
-  const bool rok = row < M;
-  float4 a[KCH];
+  const int64_t kb0 = ((int64_t)blockIdx.x * kW + w) * KBW;   // this wave's first 16-deep k block
+  const int64_t n0 = (int64_t)blockIdx.y * 16 * NTG;
+  float4 a[RT][KBW];
 #pragma unroll
-  for (int c = 0; c < KCH; ++c) {
-    const int64_t k = k0 + 16 * c + 4 * q;
-    const bool ok = rok && k < K;  // lda % 4 == 0 and lda >= K: the float4 is inside the row
-    a[c] = *reinterpret_cast<const float4*>(A + (ok ? row * lda + k : 0));
-    if (!ok) a[c] = make_float4(0.f, 0.f, 0.f, 0.f);
-  }
-  float4 v[PT];
+  for (int t = 0; t < RT; ++t)
 #pragma unroll
-  for (int p = 0; p < PT; ++p) {
-    const int e = tid + 256 * p;
-    const int64_t k = k0 + e / NQ;
-    const int64_t n = n0 + 4 * (e % NQ);
-    const bool ok = e < KP * NQ && k < K && n < N;  // N % 4 == 0
-    v[p] = *reinterpret_cast<const float4*>(B + (ok ? k * ldb + n : 0));
-    if (!ok) v[p] = make_float4(0.f, 0.f, 0.f, 0.f);
-  }
+    for (int c = 0; c < KBW; ++c) {
+      const int64_t row = 16 * t + r, k = 16 * (kb0 + c) + 4 * q;
+      const bool ok = row < M && k < K;  // lda % 4 == 0 and lda >= K rounded up to 4: the float4 lies in the row
+      const float4 v = *reinterpret_cast<const float4*>(A + (ok ? row * lda + k : 0));
+      // (A's row padding past K is never multiplied: B's rows there are zero, and
+      // 0 x a NaN pad would not be)
+      a[t][c] = ok ? make_float4(v.x, k + 1 < K ? v.y : 0.f, k + 2 < K ? v.z : 0.f, k + 3 < K ? v.w : 0.f)
+                   : make_float4(0.f, 0.f, 0.f, 0.f);
+    }
+  float b[KBW][4][NTG];
 #pragma unroll
-  for (int p = 0; p < PT; ++p) {
-    const int e = tid + 256 * p;
-    if (e < KP * NQ) *reinterpret_cast<float4*>(s_B + (e / NQ) * LW + 4 * (e % NQ)) = v[p];
-  }
+  for (int c = 0; c < KBW; ++c)
+#pragma unroll
+    for (int j = 0; j < 4; ++j)
+#pragma unroll
+      for (int u = 0; u < NTG; ++u) {
+        const int64_t k = 16 * (kb0 + c) + 4 * q + j, n = n0 + 16 * u + r;
+        const bool ok = k < K && n < N;
+        const float v = B[ok ? k * ldb + n : 0];
+        b[c][j][u] = ok ? v : 0.f;
+      }
+  f32x4 acc[RT][NTG];
+#pragma unroll
+  for (int t = 0; t < RT; ++t)
+#pragma unroll
+    for (int u = 0; u < NTG; ++u) acc[t][u] = f32x4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+  for (int c = 0; c < KBW; ++c)
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+#pragma unroll
+      for (int t = 0; t < RT; ++t) {
+        const float av = j == 0 ? a[t][c].x : j == 1 ? a[t][c].y : j == 2 ? a[t][c].z : a[t][c].w;
+#pragma unroll
+        for (int u = 0; u < NTG; ++u) acc[t][u] = __builtin_amdgcn_mfma_f32_16x16x4f32(av, b[c][j][u], acc[t][u], 0, 0, 0);
+      }
+    }
+#pragma unroll
+  for (int t = 0; t < RT; ++t)
+#pragma unroll
+    for (int u = 0; u < NTG; ++u) s_acc[w][t * NTG + u][lane] = acc[t][u];
   __syncthreads();
-  if (16 * w >= M) return;  // no barrier below
-  f32x4 acc[NT];
-#pragma unroll
-  for (int t = 0; t < NT; ++t) acc[t] = f32x4{0.f, 0.f, 0.f, 0.f};
-  // B fragments of block c + 1 are read from LDS while block c's MFMAs run
-  // (left to itself the compiler waited on each ds_read2 before its two MFMAs)
-  float bf[2][4][NT];
-  auto fetch = [&](int c, float (&b)[4][NT]) {
-#pragma unroll
-    for (int j = 0; j < 4; ++j)
-#pragma unroll
-      for (int t = 0; t < NT; ++t) b[j][t] = s_B[(16 * c + 4 * q + j) * LW + r + 16 * t];
-  };
-  fetch(0, bf[0]);
-#pragma unroll
-  for (int c = 0; c < KCH; ++c) {
-    if (c + 1 < KCH) fetch(c + 1, bf[(c + 1) & 1]);
-    __builtin_amdgcn_sched_barrier(0);
-    const int64_t k = k0 + 16 * c + 4 * q;
-    const float av[4] = {k + 0 < K ? a[c].x : 0.f, k + 1 < K ? a[c].y : 0.f, k + 2 < K ? a[c].z : 0.f,
-                         k + 3 < K ? a[c].w : 0.f};
-#pragma unroll
-    for (int j = 0; j < 4; ++j)
-#pragma unroll
-      for (int t = 0; t < NT; ++t)
-        acc[t] = __builtin_amdgcn_mfma_f32_16x16x4f32(av[j], bf[c & 1][j][t], acc[t], 0, 0, 0);
-    __builtin_amdgcn_sched_barrier(0);
-  }
-  // C/D map: reg jj -> row 4q + jj, column lane & 15
+  // the eight waves' tiles summed in wave order; thread e owns (tile e / 64, lane e % 64)
   float* out = slab + (int64_t)blockIdx.x * M * N;
+  for (int e = tid; e < RT * NTG * 64; e += 512) {
+    const int ti = e / 64, l = e % 64;
+    f32x4 v = s_acc[0][ti][l];
 #pragma unroll
-  for (int t = 0; t < NT; ++t) {
-    const int64_t n = n0 + 16 * t + r;
+    for (int ww = 1; ww < kW; ++ww) v += s_acc[ww][ti][l];
+    const int t = ti / NTG, u = ti % NTG;
+    const int64_t n = n0 + 16 * u + (l & 15);
+    // C/D map: reg jj -> row 4 (l >> 4) + jj of the tile, column l & 15
 #pragma unroll
     for (int jj = 0; jj < 4; ++jj) {
-      const int64_t gm = 16 * w + 4 * q + jj;
-      if (gm < M && n < N) out[gm * N + n] = acc[t][jj];
+      const int64_t m = 16 * t + 4 * (l >> 4) + jj;
+      if (m < M && n < N) out[m * N + n] = v[jj];
     }
   }
 }
@@ -662,30 +658,21 @@ extern "C" int gcnk_gemm_f32(int32_t transA, int32_t transB, int32_t M, int32_t 
 #undef GCNK_SHORTK
     return launch_check("gemm_shortk_kernel");
   }
-  // chunk = 16 KCH >= ceil(K / split_k): at most split_k slabs (the workspace);
-  // splits too few for 128-deep chunks take the generic kernel
-  const int64_t sm_want = (K + split_k - 1) / split_k;
-  const int sm_kch = sm_want <= 16 ? 1 : sm_want <= 32 ? 2 : sm_want <= 64 ? 4 : 8;
-  const int64_t sm_S = ((int64_t)K + 16 * sm_kch - 1) / (16 * sm_kch);
-  if (!ta && !tb && M <= 64 && K >= 512 && N % 4 == 0 && lda % 4 == 0 && ldb % 4 == 0 && aligned16(A) &&
-      aligned16(B) && split_k > 1 && sm_S <= split_k) {
-    const int kch = sm_kch;
-    const int32_t S = (int32_t)sm_S;
-    const dim3 grid((unsigned)S, (unsigned)((N + 111) / 112));
-#define GCNK_SMALLM(KCH_) \
-  hipLaunchKernelGGL((gemm_smallm_splitk_kernel<KCH_>), grid, dim3(256), 0, s, M, N, K, A, lda, B, ldb, workspace)
-    switch (kch) {
-      case 1: GCNK_SMALLM(1); break;
-      case 2: GCNK_SMALLM(2); break;
-      case 4: GCNK_SMALLM(4); break;
-      default: GCNK_SMALLM(8); break;
-    }
-#undef GCNK_SMALLM
-    int rc = launch_check("gemm_smallm_splitk_kernel");
+#ifndef GCNK_GEMM_SMALLM_WK
+#define GCNK_GEMM_SMALLM_WK 1
+#endif
+  // small M, long K: the in-workgroup K split (gemm_smallm_wk_kernel), slabs of
+  // 8 waves x 32 k, summed by gemm_slab_reduce4_kernel
+  const int64_t wk_S = ((int64_t)K + 8 * 32 - 1) / (8 * 32);
+  if (GCNK_GEMM_SMALLM_WK && !ta && !tb && M <= 64 && K >= 512 && N % 4 == 0 && lda % 4 == 0 && aligned16(A) &&
+      split_k > 1 && wk_S <= split_k && wk_S <= 65535) {
+    const dim3 grid((unsigned)wk_S, (unsigned)((N + 31) / 32));
+    hipLaunchKernelGGL((gemm_smallm_wk_kernel<2, 2>), grid, dim3(512), 0, s, M, N, K, A, lda, B, ldb, workspace);
+    int rc = launch_check("gemm_smallm_wk_kernel");
     if (rc) return rc;
     const int64_t total4 = (int64_t)M * N / 4;
     hipLaunchKernelGGL(gemm_slab_reduce4_kernel, dim3((unsigned)((total4 + kRedItems - 1) / kRedItems)),
-                       dim3(kRedItems * kRedGroups), 0, s, M, N, S, workspace, C, ldc, e);
+                       dim3(kRedItems * kRedGroups), 0, s, M, N, (int32_t)wk_S, workspace, C, ldc, e);
     return launch_check("gemm_slab_reduce4_kernel");
   }
   if (N <= 16) return launch_gemm<4, 1, 2, 1>(ta, tb, M, N, K, A, lda, B, ldb, C, ldc, e, split_k, workspace, s);

@@ -30,7 +30,11 @@ from .sparse import CSR
 MAX_HUBS = 128    # hub rows staged in LDS (S_T [hubs x F]; the kernel checks the LDS budget)
 # X[hubs] W1 (R8: 50 dense hub rows x 7463): the SpMM tile plan on their CSR
 # plus its slab reduce (9.8 us per call; 6.8 + 4.9 us in the forward's trace);
-# dense X's hub rows: the MFMA GEMM (gcnk_gemm_f32, small-M split-K).  Measured
+# dense X's hub rows: the MFMA GEMM (gcnk_gemm_f32, small-M split-K).  A dense
+# copy of R8's sparse hub rows through round 6's in-workgroup K-split GEMM
+# (30 slabs instead of 117) measured 7.16 + 4.86 us against the tile plan's
+# 6.79 + 4.89 in the same trace (profiles/r06_xhub_ab_*), so sparse hub rows
+# stay on the tile plan.  Measured
 # and removed (DESIGN.md keeps the numbers): a dense copy of the sparse hub rows
 # through the small-M split-K GEMM (10.4 us per call, profiles/r04_smallm_*), a
 # one-launch split-K kernel with two levels of last-arriver slab sums (12.1 us,

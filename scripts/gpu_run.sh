@@ -8,6 +8,7 @@
 #   test:<pytest -k expr>     GPU tests matching the expression (-m gpu)
 #   tests                     the whole GPU suite
 #   bench[:<args>]            python bench.py <args> (default --steps 200 --warmup 20) -> bench.json
+#   benchn:<name>:<args>      python bench.py <args> -> bench_<name>.json
 #   prof:<script>[:<args>]    rocprofv3 --kernel-trace --stats over python scripts/<script> -> <script>_stats/
 #   py:<script>[:<args>]      python scripts/<script> <args> -> <script>.log
 #   vpy:<variant>:<script>[:<args>]  the same on _variants/libgcnk_<variant>.so
@@ -48,6 +49,10 @@ for step in "$@"; do
       args="${rest:---steps 200 --warmup 20}"
       timeout -k 10 900 python -u bench.py $args --rocprof-dir "$out/bench_prof" > "$out/bench.json" 2> "$out/bench.err"
       rc=$?; tail -c 3000 "$out/bench.json"; [ $rc -eq 0 ] || { echo "rc=$rc"; tail -n 20 "$out/bench.err"; exit 1; } ;;
+    benchn)   # benchn:<name>:<args>: python bench.py <args> -> bench_<name>.json (several per call)
+      nm="${rest%%:*}"; args="${rest#*:}"
+      timeout -k 10 600 python -u bench.py $args > "$out/bench_$nm.json" 2> "$out/bench_$nm.err"
+      rc=$?; tail -c 600 "$out/bench_$nm.json"; echo; [ $rc -eq 0 ] || { echo "rc=$rc"; tail -n 20 "$out/bench_$nm.err"; exit 1; } ;;
     prof)
       s="${rest%%:*}"; args="${rest#*:}"; [ "$args" = "$rest" ] && args=""
       timeout -k 10 400 rocprofv3 --kernel-trace --stats --output-format csv -d "$out/${s%.py}_stats$n" -o kt -- \

@@ -258,41 +258,10 @@ __global__ void __launch_bounds__(kBwdBlock) gcn_bwd2_kernel(Bwd2Args a) {
   stamp(a.stamps, 3);
 }
 
-// out[e] = sum over workgroups of part[b][e], b in order: 16 entries x 16
-// workgroup lanes per block, each lane summing workgroups l, l + 16, ... (16
-// loads in flight), then the 16 lanes in order through LDS.
-__global__ void __launch_bounds__(256) gcn_bwd2_reduce_kernel(const float* __restrict__ part, int64_t part_ld,
-                                                              int32_t nblk, int32_t N, int32_t P, int32_t with_g,
-                                                              float* __restrict__ gW, float* __restrict__ gb1,
-                                                              float* __restrict__ gb2) {
+// gW2 / gb1 / gb2 from the per-workgroup partials (side_reduce_body, gcnk_common.h)
+__global__ void __launch_bounds__(256) gcn_bwd2_reduce_kernel(SideReduce r) {
   __shared__ float s[16][17];
-  const int el = threadIdx.x & 15, bl = threadIdx.x >> 4;
-  const int64_t E = (int64_t)N * P + N + (with_g ? P : 0);
-  const int64_t e = (int64_t)blockIdx.x * 16 + el;
-  float acc = 0.f;
-  if (e < E) {
-    for (int32_t b0 = bl; b0 < nblk; b0 += 16 * 16) {
-      float v[16];
-#pragma unroll
-      for (int j = 0; j < 16; ++j) v[j] = b0 + 16 * j < nblk ? part[(int64_t)(b0 + 16 * j) * part_ld + e] : 0.f;
-#pragma unroll
-      for (int j = 0; j < 16; ++j)
-        if (b0 + 16 * j < nblk) acc += v[j];
-    }
-  }
-  s[bl][el] = acc;
-  __syncthreads();
-  if (bl != 0 || e >= E) return;
-  float t = s[0][el];
-  for (int q = 1; q < 16; ++q) t += s[q][el];
-  const int64_t NP = (int64_t)N * P;
-  if (e < NP) {
-    if (gW) gW[e] = t;
-  } else if (e < NP + N) {
-    if (gb1) gb1[e - NP] = t;
-  } else if (gb2) {
-    gb2[e - NP - N] = t;
-  }
+  side_reduce_body(r, blockIdx.x, s);
 }
 
 struct Bwd2Geom {
@@ -323,10 +292,26 @@ extern "C" int64_t gcnk_gcn_bwd2_workspace_bytes(int32_t M, int32_t N, int32_t P
   return (int64_t)g.nblk * g.part_ld * 4;
 }
 
+int gcnk::side_reduce_launch(const SideReduce& side, void* stream) {
+  hipLaunchKernelGGL(gcn_bwd2_reduce_kernel, dim3((unsigned)side_reduce_blocks(side)), dim3(256), 0,
+                     (hipStream_t)stream, side);
+  return launch_check("gcn_bwd2_reduce_kernel");
+}
+
 extern "C" int gcnk_gcn_bwd2_f32(const float* H, int64_t ldh, const float* gS, int64_t ldgs, const float* W,
                                  int64_t ldw, const float* G, int64_t ldg, int32_t M, int32_t N, int32_t P,
                                  float scale, float* Z, int64_t ldz, float* gW, float* gb1, float* gb2,
                                  void* workspace, int64_t workspace_bytes, void* stream) {
+  SideReduce side;
+  const int rc = gcn_bwd2_main(H, ldh, gS, ldgs, W, ldw, G, ldg, M, N, P, scale, Z, ldz, gW, gb1, gb2, workspace,
+                               workspace_bytes, stream, &side);
+  return rc ? rc : side_reduce_launch(side, stream);
+}
+
+int gcnk::gcn_bwd2_main(const float* H, int64_t ldh, const float* gS, int64_t ldgs, const float* W, int64_t ldw,
+                        const float* G, int64_t ldg, int32_t M, int32_t N, int32_t P, float scale, float* Z,
+                        int64_t ldz, float* gW, float* gb1, float* gb2, void* workspace, int64_t workspace_bytes,
+                        void* stream, SideReduce* side) {
   if (M < 0 || N < 0 || P < 0) {
     set_error("gcnk_gcn_bwd2_f32: negative size (M=%d N=%d P=%d)", M, N, P);
     return GCNK_EARG;
@@ -370,10 +355,6 @@ extern "C" int gcnk_gcn_bwd2_f32(const float* H, int64_t ldh, const float* gS, i
     else GCNK_BWD2(1, 32);
   }
 #undef GCNK_BWD2
-  int rc = launch_check("gcn_bwd2_kernel");
-  if (rc) return rc;
-  const int64_t E = (int64_t)N * P + N + (G ? P : 0);
-  hipLaunchKernelGGL(gcn_bwd2_reduce_kernel, dim3((unsigned)((E + 15) / 16)), dim3(256), 0, s,
-                     (const float*)workspace, g.part_ld, g.nblk, N, P, G ? 1 : 0, gW, gb1, gb2);
-  return launch_check("gcn_bwd2_reduce_kernel");
+  *side = SideReduce{(const float*)workspace, g.part_ld, g.nblk, N, P, G ? 1 : 0, gW, gb1, gb2};
+  return launch_check("gcn_bwd2_kernel");
 }

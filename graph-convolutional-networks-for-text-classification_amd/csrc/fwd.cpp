@@ -126,21 +126,32 @@ extern "C" int gcnk_gcn_backward_f32(const gcnk_gcn_bwd* rec, const float* G, co
   if ((rc = spmm_ref(r.aTP, G, r.P, r.P, r.gS2, r.P, nullptr, GCNK_EPI_NONE, nullptr, 0, 1.f, 1.f, 0, 0, nullptr,
                      stream)) != GCNK_OK)
     return rc;
-  // gc2's weight/bias grads and gc1's ReLU + dropout backward (layer.py:102-110,182-188)
-  if ((rc = gcnk_gcn_bwd2_f32(H1, ldh, r.gS2, r.P, W2, r.P, gb2 ? G : nullptr, r.P, r.M, r.F, r.P, scale, r.gZ1, r.F,
-                              gW2, gb1, gb2, r.bwd2_ws, r.bwd2_ws_bytes, stream)) != GCNK_OK)
+  // gc2's weight/bias grads and gc1's ReLU + dropout backward (layer.py:102-110,182-188); the fixed-order
+  // sum of its gW2 / gb1 / gb2 partials has no consumer before Adam, so it rides in the backward's last
+  // launch (X^T gS1's tile reduce) when that launch exists, else it runs at the end as its own
+  SideReduce side;
+  if ((rc = gcn_bwd2_main(H1, ldh, r.gS2, r.P, W2, r.P, gb2 ? G : nullptr, r.P, r.M, r.F, r.P, scale, r.gZ1, r.F,
+                          gW2, gb1, gb2, r.bwd2_ws, r.bwd2_ws_bytes, stream, &side)) != GCNK_OK)
     return rc;
-  if (!gW1) return GCNK_OK;
-  if (ax)  // gW1 = (A-hat X)^T gZ1: the DENSE_AX forward's Z1 = (A-hat X) W1
-    return gcnk_gemm_f32(1, 0, r.x_cols, r.F, r.x_rows, r.x_dense, r.ldx, r.gZ1, r.F, gW1, r.F, nullptr,
-                         GCNK_GEMM_EPI_NONE, nullptr, 0, 1.f, r.x_split_k, r.gemm_ws, r.gemm_ws_bytes, stream);
+  if (!gW1) return side_reduce_launch(side, stream);
+  if (ax) {  // gW1 = (A-hat X)^T gZ1: the DENSE_AX forward's Z1 = (A-hat X) W1
+    if ((rc = gcnk_gemm_f32(1, 0, r.x_cols, r.F, r.x_rows, r.x_dense, r.ldx, r.gZ1, r.F, gW1, r.F, nullptr,
+                            GCNK_GEMM_EPI_NONE, nullptr, 0, 1.f, r.x_split_k, r.gemm_ws, r.gemm_ws_bytes, stream)) !=
+        GCNK_OK)
+      return rc;
+    return side_reduce_launch(side, stream);
+  }
   // gS1 = A-hat^T gZ1, gW1 = X^T gS1  (autograd of layer.py:106, :102 in gc1)
   if ((rc = spmm_ref(r.aTF, r.gZ1, r.F, r.F, r.gS1, r.F, nullptr, GCNK_EPI_NONE, nullptr, 0, 1.f, 1.f, 0, 0, nullptr,
                      stream)) != GCNK_OK)
     return rc;
+  int carried = 0;
   if (r.xT.plan)
-    return spmm_ref(r.xT, r.gS1, r.F, r.F, gW1, r.F, nullptr, GCNK_EPI_NONE, nullptr, 0, 1.f, 1.f, 0, 0, nullptr,
-                    stream);
-  return gcnk_gemm_f32(1, 0, r.x_cols, r.F, r.x_rows, r.x_dense, r.ldx, r.gS1, r.F, gW1, r.F, nullptr,
+    rc = spmm_csr_f32_side(r.xT.plan, r.xT.hdr, r.gS1, r.F, r.F, gW1, r.F, r.xT.workspace, r.xT.workspace_bytes,
+                           r.xT.counters, r.xT.counter_bytes, r.xT.lanes_hint, stream, side, &carried);
+  else
+    rc = gcnk_gemm_f32(1, 0, r.x_cols, r.F, r.x_rows, r.x_dense, r.ldx, r.gS1, r.F, gW1, r.F, nullptr,
                        GCNK_GEMM_EPI_NONE, nullptr, 0, 1.f, r.x_split_k, r.gemm_ws, r.gemm_ws_bytes, stream);
+  if (rc != GCNK_OK || carried) return rc;
+  return side_reduce_launch(side, stream);
 }

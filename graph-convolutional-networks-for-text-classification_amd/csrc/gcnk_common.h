@@ -180,4 +180,68 @@ __device__ __forceinline__ void lds_dma4(const void* gsrc, void* lds_wave) {
   __builtin_amdgcn_global_load_lds(const_cast<void*>(gsrc), (__attribute__((address_space(3))) void*)lds_wave, 4, 0, 0);
 }
 
+// ----------------------------------------------------------------------------
+// A pending fixed-order sum over per-workgroup partials -- gcn_bwd2's gW2 / gb1
+// / gb2 (csrc/bwd.hip) -- that another launch of the same backward carries as
+// extra workgroups (round 6: the backward record runs it inside X^T gS1's tile
+// reduce launch instead of a launch of its own).  out[e] = sum over b of
+// part[b * part_ld + e], b in order: 16 entries x 16 workgroup lanes per
+// workgroup of 256 threads, each lane summing workgroups l, l + 16, ... (16
+// loads in flight), then the 16 lanes in order through LDS.
+struct SideReduce {
+  const float* part;
+  int64_t part_ld;
+  int32_t nblk, N, P, with_g;
+  float *gW, *gb1, *gb2;
+};
+
+__host__ __device__ inline int64_t side_reduce_entries(const SideReduce& r) {
+  return (int64_t)r.N * r.P + r.N + (r.with_g ? r.P : 0);
+}
+__host__ __device__ inline int64_t side_reduce_blocks(const SideReduce& r) { return (side_reduce_entries(r) + 15) / 16; }
+
+// workgroup `blk` of the side reduce (256 threads; s: 16 x 17 floats of LDS)
+__device__ __forceinline__ void side_reduce_body(const SideReduce& r, int64_t blk, float (*s)[17]) {
+  const int el = threadIdx.x & 15, bl = threadIdx.x >> 4;
+  const int64_t E = side_reduce_entries(r);
+  const int64_t e = blk * 16 + el;
+  float acc = 0.f;
+  if (e < E) {
+    for (int32_t b0 = bl; b0 < r.nblk; b0 += 16 * 16) {
+      float v[16];
+#pragma unroll
+      for (int j = 0; j < 16; ++j) v[j] = b0 + 16 * j < r.nblk ? r.part[(int64_t)(b0 + 16 * j) * r.part_ld + e] : 0.f;
+#pragma unroll
+      for (int j = 0; j < 16; ++j)
+        if (b0 + 16 * j < r.nblk) acc += v[j];
+    }
+  }
+  s[bl][el] = acc;
+  __syncthreads();
+  if (bl != 0 || e >= E) return;
+  float t = s[0][el];
+  for (int q = 1; q < 16; ++q) t += s[q][el];
+  const int64_t NP = (int64_t)r.N * r.P;
+  if (e < NP) {
+    if (r.gW) r.gW[e] = t;
+  } else if (e < NP + r.N) {
+    if (r.gb1) r.gb1[e - NP] = t;
+  } else if (r.gb2) {
+    r.gb2[e - NP - r.N] = t;
+  }
+}
+
+// gcn_bwd2's main launch only, its reduce returned in *side (csrc/bwd.hip), and
+// that reduce as a launch of its own
+int gcn_bwd2_main(const float* H, int64_t ldh, const float* gS, int64_t ldgs, const float* W, int64_t ldw,
+                  const float* G, int64_t ldg, int32_t M, int32_t N, int32_t P, float scale, float* Z, int64_t ldz,
+                  float* gW, float* gb1, float* gb2, void* workspace, int64_t workspace_bytes, void* stream,
+                  SideReduce* side);
+int side_reduce_launch(const SideReduce& side, void* stream);
+// gcnk_spmm_csr_f32 carrying `side` in its tile reduce launch when it has one
+// (*carried = 1); otherwise the side reduce is left to the caller (*carried = 0)
+int spmm_csr_f32_side(const void* plan, const int32_t* hdr, const float* B, int64_t ldb, int32_t F, float* C,
+                      int64_t ldc, float* workspace, int64_t workspace_bytes, int32_t* counters,
+                      int64_t counter_bytes, int32_t lanes_hint, void* stream, const SideReduce& side, int* carried);
+
 }  // namespace gcnk

@@ -1201,7 +1201,14 @@ __device__ __forceinline__ void reduce_body(int32_t bx, int32_t by, int32_t bz, 
 
 __global__ void __launch_bounds__(256)
 spmm_tile_reduce_kernel(const int4* __restrict__ red, int32_t F, const float* __restrict__ slabs, int64_t slab_ld,
-                        const float* __restrict__ B, int64_t ldb, float* __restrict__ C, int64_t ldc, Epi epi) {
+                        const float* __restrict__ B, int64_t ldb, float* __restrict__ C, int64_t ldc, Epi epi,
+                        int32_t nred, SideReduce side) {
+  if ((int32_t)blockIdx.x >= nred) {   // extra columns of the grid: a carried side reduce (workgroup-uniform)
+    __shared__ float s_side[16][17];
+    const int64_t blk = ((int64_t)(blockIdx.x - nred) * gridDim.y + blockIdx.y) * gridDim.z + blockIdx.z;
+    if (blk < side_reduce_blocks(side)) side_reduce_body(side, blk, s_side);
+    return;
+  }
   resolve_rng(epi);
   reduce_body((int32_t)blockIdx.x, (int32_t)blockIdx.y, (int32_t)blockIdx.z, red, F, slabs, slab_ld, B, ldb, C, ldc,
               epi);
@@ -1955,7 +1962,9 @@ static int spmm_impl(const void* plan, const int32_t* hdr, const float* B, int64
                      int64_t ldc, const float* bias, int32_t epilogue, const uint8_t* drop_mask, int64_t ldm,
                      float drop_scale, float keep_prob, uint64_t seed, uint64_t offset, const uint64_t* rng_base,
                      float* workspace, int64_t workspace_bytes, int32_t* counters, int64_t counter_bytes, int32_t lanes_hint,
-                     const ProjArgs& pa, void* stream, int32_t part = 0) {
+                     const ProjArgs& pa, void* stream, int32_t part = 0, const SideReduce* side = nullptr,
+                     int* carried = nullptr) {
+  if (carried) *carried = 0;
   if (!plan || !plan_magic(hdr) || F < 0 || part < 0 || part > 2) {
     set_error("gcnk_spmm_csr_f32: bad argument (plan/header missing or not a gcnk plan, F=%d)", F);
     return GCNK_EARG;
@@ -2057,8 +2066,14 @@ static int spmm_impl(const void* plan, const int32_t* hdr, const float* B, int64
     const int rc = launch_tile(vec4, nt_need, (unsigned)(i1 - i0), ta, s);
     if (rc) return rc;
     if (L.nred > 0 && part != 1) {
-      hipLaunchKernelGGL(spmm_tile_reduce_kernel, dim3((unsigned)L.nred, kRB, (unsigned)((F + 63) / 64)), dim3(256),
-                         0, s, reinterpret_cast<const int4*>(p + L.red), F, slabs, slab_ld, B, ldb, C, ldc, e);
+      // a carried side reduce takes extra x columns of the grid (kRB x column tiles workgroups each)
+      const int64_t per_x = (int64_t)kRB * ((F + 63) / 64);
+      const int64_t side_x = side ? (side_reduce_blocks(*side) + per_x - 1) / per_x : 0;
+      const SideReduce none{nullptr, 0, 0, 0, 0, 0, nullptr, nullptr, nullptr};
+      hipLaunchKernelGGL(spmm_tile_reduce_kernel, dim3((unsigned)(L.nred + side_x), kRB, (unsigned)((F + 63) / 64)),
+                         dim3(256), 0, s, reinterpret_cast<const int4*>(p + L.red), F, slabs, slab_ld, B, ldb, C, ldc,
+                         e, (int32_t)L.nred, side ? *side : none);
+      if (side && carried) *carried = 1;
       int rc = launch_check("spmm_tile_reduce_kernel");
       if (rc) return rc;
     }
@@ -2094,6 +2109,15 @@ extern "C" int gcnk_spmm_csr_f32(const void* plan, const int32_t* hdr, const flo
   const ProjArgs none{nullptr, 0, 0, nullptr, 0, 1};
   return spmm_impl(plan, hdr, B, ldb, F, C, ldc, bias, epilogue, drop_mask, ldm, drop_scale, keep_prob, seed, offset,
                    rng_base, workspace, workspace_bytes, counters, counter_bytes, lanes_hint, none, stream);
+}
+
+int gcnk::spmm_csr_f32_side(const void* plan, const int32_t* hdr, const float* B, int64_t ldb, int32_t F, float* C,
+                            int64_t ldc, float* workspace, int64_t workspace_bytes, int32_t* counters,
+                            int64_t counter_bytes, int32_t lanes_hint, void* stream, const SideReduce& side,
+                            int* carried) {
+  const ProjArgs none{nullptr, 0, 0, nullptr, 0, 1};
+  return spmm_impl(plan, hdr, B, ldb, F, C, ldc, nullptr, GCNK_EPI_NONE, nullptr, 0, 1.f, 1.f, 0, 0, nullptr, workspace,
+                   workspace_bytes, counters, counter_bytes, lanes_hint, none, stream, 0, &side, carried);
 }
 
 extern "C" int gcnk_spmm_csr_f32_part(const void* plan, const int32_t* hdr, const float* B, int64_t ldb,

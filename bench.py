@@ -122,6 +122,21 @@ def launch_ranks(args):
     return subprocess.call(cmd, env=dict(os.environ, HSA_ENABLE_IPC_MODE_LEGACY="0"))
 
 
+def upload_graph(graph):
+    """hipGraphUpload of a captured graph's executable on torch's current
+    stream, so no replay (least of all a timed one) pays the lazy upload."""
+    import ctypes
+    import torch
+    try:
+        hip = ctypes.CDLL("libamdhip64.so")
+        hip.hipGraphUpload.argtypes = [ctypes.c_void_p, ctypes.c_void_p]
+        hip.hipGraphUpload(ctypes.c_void_p(graph.raw_cuda_graph_exec()),
+                           ctypes.c_void_p(torch.cuda.current_stream().cuda_stream))
+        torch.cuda.synchronize()
+    except (OSError, AttributeError, RuntimeError):
+        pass
+
+
 def graph_us(fns, reps_per_fn):
     """Average us per call of a hipGraph replaying fns round-robin (HIP events
     on torch's current stream, the stream every op is launched on)."""
@@ -945,22 +960,22 @@ def main():
             for _ in range(3):
                 forward()
         torch.cuda.current_stream().wait_stream(s)
-        # the largest forwards-per-graph <= --graph-steps that divides --steps
-        # (every replay is `per` complete forwards, so exactly --steps run timed)
+        # the largest forwards-per-graph <= --graph-steps that divides --steps and
+        # --warmup (every replay is `per` complete forwards, so exactly --steps run
+        # timed and exactly --warmup untimed, the latter including a replay of the
+        # same graph: its first launch pays one-time costs)
         per = max(1, min(args.graph_steps, args.steps))
-        while args.steps % per:
+        while args.steps % per or (args.warmup and args.warmup % per):
             per -= 1
         graph = torch.cuda.CUDAGraph()
         with torch.cuda.graph(graph):
             for _ in range(per):
                 out = forward()
+        upload_graph(graph)
         step = graph.replay
 
-    # exactly --warmup untimed forwards: whole replays, then single eager calls
     for _ in range(args.warmup // per):
         step()
-    for _ in range(args.warmup % per):
-        forward()
     torch.cuda.synchronize()
     if world > 1:
         dist.barrier(device_ids=[torch.cuda.current_device()])

@@ -661,13 +661,20 @@ extern "C" int gcnk_gemm_f32(int32_t transA, int32_t transB, int32_t M, int32_t 
 #ifndef GCNK_GEMM_SMALLM_WK
 #define GCNK_GEMM_SMALLM_WK 1
 #endif
+#ifndef GCNK_WK_KBW   // 16-deep k blocks per wave (a slab is 8 waves of them)
+#define GCNK_WK_KBW 2
+#endif
+#ifndef GCNK_WK_NTG   // 16-column n-tiles per workgroup
+#define GCNK_WK_NTG 2
+#endif
   // small M, long K: the in-workgroup K split (gemm_smallm_wk_kernel), slabs of
-  // 8 waves x 32 k, summed by gemm_slab_reduce4_kernel
-  const int64_t wk_S = ((int64_t)K + 8 * 32 - 1) / (8 * 32);
+  // 8 waves x 16 KBW k, summed by gemm_slab_reduce4_kernel
+  const int64_t wk_S = ((int64_t)K + 8 * 16 * GCNK_WK_KBW - 1) / (8 * 16 * GCNK_WK_KBW);
   if (GCNK_GEMM_SMALLM_WK && !ta && !tb && M <= 64 && K >= 512 && N % 4 == 0 && lda % 4 == 0 && aligned16(A) &&
       split_k > 1 && wk_S <= split_k && wk_S <= 65535) {
-    const dim3 grid((unsigned)wk_S, (unsigned)((N + 31) / 32));
-    hipLaunchKernelGGL((gemm_smallm_wk_kernel<2, 2>), grid, dim3(512), 0, s, M, N, K, A, lda, B, ldb, workspace);
+    const dim3 grid((unsigned)wk_S, (unsigned)((N + 16 * GCNK_WK_NTG - 1) / (16 * GCNK_WK_NTG)));
+    hipLaunchKernelGGL((gemm_smallm_wk_kernel<GCNK_WK_KBW, GCNK_WK_NTG>), grid, dim3(512), 0, s, M, N, K, A, lda, B,
+                       ldb, workspace);
     int rc = launch_check("gemm_smallm_wk_kernel");
     if (rc) return rc;
     const int64_t total4 = (int64_t)M * N / 4;

@@ -20,6 +20,7 @@ dropout + the gc2 projection H1 W2), and the hub rows' 600-term gather sums
 of the SpMM never run.  The association differs from A (X W1) only in fp32
 rounding (checked against the reference's goldens to 1e-4, tests/).
 """
+import os
 import threading
 
 import numpy as np
@@ -43,6 +44,10 @@ MAX_HUBS = 128    # hub rows staged in LDS (S_T [hubs x F]; the kernel checks th
 # kslab.hip, ABI 11) and a one-launch small-M GEMM whose tiles' last workgroups
 # sum the partials (12.2 us, ~4 of it the coherent hand-off,
 # profiles/r05_smallm_*; smallm.hip, ABI 11).
+# X's hub rows at least XHUB_DENSE_FILL full run X_hubs W1 as a dense small-M
+# GEMM; GCNK_XHUB_DENSE=0 keeps the tile SpMM on their CSR (A/B timing)
+XHUB_DENSE = os.environ.get("GCNK_XHUB_DENSE", "1") != "0"
+XHUB_DENSE_FILL = 0.5
 MAX_KC = 128      # X's light-row column range (U's width)
 ROWS_PER_BLOCK = 32   # csrc/factor.hip kRB
 # record words before the items: 33 row offsets | 3 pad | 32 row ids (-1 past
@@ -173,6 +178,15 @@ def build(adj, xop):
                                                 stream), "gcnk_csr_gather_rows")
             f.x_hub = CSR(hrp, hci[:xtot], hv[:xtot], (H, x.shape[1]))
             f.x_hub_dense = None
+            kx = x.shape[1]
+            if XHUB_DENSE and H <= 64 and xtot >= XHUB_DENSE_FILL * H * kx and H * kx * 4 <= 64 << 20:
+                # dense hub rows (R8's topic rows: all 7,463 columns): X_hubs W1 on the
+                # small-M GEMM (gcnk_gemm_f32's in-workgroup K split) instead of the
+                # tile plan + its slab reduce
+                d = torch.empty((H, (kx + 3) // 4 * 4), dtype=torch.float32, device=dev)
+                _lib.check(lib.gcnk_csr_to_dense(hrp.data_ptr(), hci.data_ptr(), hv.data_ptr(), H, kx, d.data_ptr(),
+                                                 d.stride(0), stream), "gcnk_csr_to_dense")
+                f.x_hub_dense = d[:, :kx]
         else:
             f.x_hub = None
             kx = xop.shape[1]

@@ -296,7 +296,7 @@ def _get(adj, xop, F, P, device, cls, tag):
     it, so two graphs of the same record must not replay concurrently."""
     stream = torch.cuda.current_stream(device).cuda_stream
     src = xop.csr if xop.csr is not None else xop.dense
-    key = (tag, id(src), F, P, stream, ops.FACTOR_GC1, ops.FUSE_PROJECTION, ops.DENSE_AX)
+    key = (tag, id(src), F, P, stream, ops.FACTOR_GC1, ops.FUSE_PROJECTION, ops.DENSE_AX, factor.XHUB_DENSE)
     recs = getattr(adj, "_records", None)
     if recs is None:
         with _lock:

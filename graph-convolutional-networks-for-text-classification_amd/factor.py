@@ -33,9 +33,12 @@ MAX_HUBS = 128    # hub rows staged in LDS (S_T [hubs x F]; the kernel checks th
 # plus its slab reduce (9.8 us per call; 6.8 + 4.9 us in the forward's trace);
 # dense X's hub rows: the MFMA GEMM (gcnk_gemm_f32, small-M split-K).  A dense
 # copy of R8's sparse hub rows through round 6's in-workgroup K-split GEMM
-# (30 slabs instead of 117) measured 7.16 + 4.86 us against the tile plan's
-# 6.79 + 4.89 in the same trace (profiles/r06_xhub_ab_*), so sparse hub rows
-# stay on the tile plan.  Measured
+# (30 slabs instead of 117): 7.16 + 4.86 us against the tile plan's 6.79 + 4.89
+# in one trace (profiles/r06_xhub_ab_*), yet the eval forward 25.20 / 25.26 us
+# against 25.56 / 25.48 interleaved (profiles/r06_xhub_forward_ab.json); in the
+# training step, where W1 arrives fresh from Adam, the tile plan is the faster
+# one (profiles/r06_xhub_train_ab.log), so training forwards keep it
+# (XHUB_TRAIN_TILE).  Measured
 # and removed (DESIGN.md keeps the numbers): a dense copy of the sparse hub rows
 # through the small-M split-K GEMM (10.4 us per call, profiles/r04_smallm_*), a
 # one-launch split-K kernel with two levels of last-arriver slab sums (12.1 us,
@@ -48,6 +51,7 @@ MAX_HUBS = 128    # hub rows staged in LDS (S_T [hubs x F]; the kernel checks th
 # GEMM; GCNK_XHUB_DENSE=0 keeps the tile SpMM on their CSR (A/B timing)
 XHUB_DENSE = os.environ.get("GCNK_XHUB_DENSE", "1") != "0"
 XHUB_DENSE_FILL = 0.5
+XHUB_TRAIN_TILE = os.environ.get("GCNK_XHUB_TRAIN_TILE", "1") != "0"
 MAX_KC = 128      # X's light-row column range (U's width)
 ROWS_PER_BLOCK = 32   # csrc/factor.hip kRB
 # record words before the items: 33 row offsets | 3 pad | 32 row ids (-1 past
@@ -67,10 +71,17 @@ class HubFactor:
     __slots__ = ("M", "H", "K", "hubs", "k0", "Kc", "U", "perm", "rec", "rec_words", "nblk", "x_hub",
                  "x_hub_dense", "_src")
 
-    def hub_times(self, W):
+    def hub_operand(self, train=False):
+        """'csr' or 'dense': which form of X[hubs] the product S_T = X[hubs] W1
+        takes (a training forward keeps the tile plan where both exist)."""
+        if self.x_hub_dense is None or (train and XHUB_TRAIN_TILE and self.x_hub is not None):
+            return "csr"
+        return "dense"
+
+    def hub_times(self, W, train=False):
         """S_T = X[hubs] @ W  (the hub rows of reference layer.py:102)."""
         from .ops import gemm, spmm
-        if self.x_hub_dense is None:
+        if self.hub_operand(train) == "csr":
             return spmm(self.x_hub, W)
         return gemm(self.x_hub_dense, W)
 

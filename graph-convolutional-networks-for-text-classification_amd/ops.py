@@ -229,7 +229,7 @@ def hubfactor_gc1(f, W1, b1, W2, epilogue=_lib.EPI_BIAS_RELU, mask=None, scale=1
     if int(lib.gcnk_hubfactor_lds_bytes(F, f.Kc, f.H, f.rec_words, P)) > 160 * 1024:
         return None
     if S is None:
-        S = f.hub_times(W1).contiguous()
+        S = f.hub_times(W1, train=store_h1).contiguous()
     H1 = torch.empty((M, F), dtype=torch.float32, device=W1.device) if store_h1 else None
     S2 = torch.empty((M, P), dtype=torch.float32, device=W1.device)
     if b1 is not None:
@@ -578,7 +578,7 @@ def record_forward(W1, b1, W2, b2, xop, adj, epi, mask, scale, keep, seed, offse
     if dev.index != torch.cuda.current_device():
         with torch.cuda.device(dev):
             return record_forward(W1, b1, W2, b2, xop, adj, epi, mask, scale, keep, seed, offset, keep_h1, rng_base)
-    rec, stream = record.get(adj, xop, F, P, dev)
+    rec, stream = record.get(adj, xop, F, P, dev, train=bool(keep_h1))
     if rec is None:
         return None
     if rec.kind == record.DENSE_AX and not all(t is None or t.data_ptr() % 16 == 0 for t in (W1, b1)):

@@ -90,7 +90,7 @@ class ForwardRecord:
 
     __slots__ = ("s", "keep", "kind", "M", "F", "P", "src", "pinned", "__weakref__")
 
-    def __init__(self, adj, xop, F, P, device):
+    def __init__(self, adj, xop, F, P, device, train=False):
         lib = _lib.load()
         M = adj.shape[0]
         s = GcnFwd()
@@ -120,7 +120,7 @@ class ForwardRecord:
             s.Kc, s.nhub, s.k0, s.rec_words = fac.Kc, fac.H, fac.k0, fac.rec_words
             s.U, s.ldu, s.rec = fac.U.data_ptr(), fac.U.stride(0), fac.rec.data_ptr()
             keep += [fac.U, fac.rec]
-            if fac.x_hub_dense is None:
+            if fac.hub_operand(train) == "csr":
                 x_csr, x_dense = fac.x_hub, None
             else:
                 x_csr, x_dense = None, fac.x_hub_dense
@@ -280,13 +280,14 @@ def get_backward(adj, xop, F, P, device):
     return _get(adj, xop, F, P, device, BackwardRecord, "bwd")
 
 
-def get(adj, xop, F, P, device):
+def get(adj, xop, F, P, device, train=False):
     """(record, stream): the ForwardRecord of (adj, X, F, P) for torch's current
-    stream, built on first use, and that stream."""
-    return _get(adj, xop, F, P, device, ForwardRecord, "fwd")
+    stream, built on first use, and that stream.  ``train``: a forward whose H1
+    the backward keeps (its X_hubs W1 may take another form, factor.hub_operand)."""
+    return _get(adj, xop, F, P, device, ForwardRecord, "fwd", train)
 
 
-def _get(adj, xop, F, P, device, cls, tag):
+def _get(adj, xop, F, P, device, cls, tag, train=False):
     """A record's launches bake in raw pointers to its scratch buffers, so a
     record is rebuilt when either operand's values change in place (the
     factored operands and plans are derived from them) and a record that was
@@ -296,7 +297,8 @@ def _get(adj, xop, F, P, device, cls, tag):
     it, so two graphs of the same record must not replay concurrently."""
     stream = torch.cuda.current_stream(device).cuda_stream
     src = xop.csr if xop.csr is not None else xop.dense
-    key = (tag, id(src), F, P, stream, ops.FACTOR_GC1, ops.FUSE_PROJECTION, ops.DENSE_AX, factor.XHUB_DENSE)
+    key = (tag, id(src), F, P, stream, ops.FACTOR_GC1, ops.FUSE_PROJECTION, ops.DENSE_AX, factor.XHUB_DENSE,
+           bool(train) and factor.XHUB_TRAIN_TILE)
     recs = getattr(adj, "_records", None)
     if recs is None:
         with _lock:
@@ -311,7 +313,7 @@ def _get(adj, xop, F, P, device, cls, tag):
             hit[2].pinned = True
         return hit[2], stream
     with _lock:
-        rec = cls(adj, xop, F, P, device)
+        rec = cls(adj, xop, F, P, device, train) if cls is ForwardRecord else cls(adj, xop, F, P, device)
         rec.pinned = capturing
         old = recs.get(key)
         if old is not None and old[2].pinned:

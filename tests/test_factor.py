@@ -146,3 +146,18 @@ def test_factor_refuses_unstructured_graph():
     A = sp.csr_matrix((np.ones(len(rows)), (rows, cols)), shape=(nd + nt, nd + nt)) + sp.eye(nd + nt)
     X = sp.csr_matrix(rng.random((nd + nt, 5)))
     assert factor.build(_csr(A), _XOp(csr=_csr(X))) is None
+
+
+def test_hub_operand_choice():
+    """Which form of X[hubs] the product S_T = X[hubs] W1 takes (factor.py):
+    the CSR when no dense copy exists; with both, the dense copy in eval and
+    the CSR in a training forward (XHUB_TRAIN_TILE, profiles/r06_xhub_train_ab.log)."""
+    from graph_convolutional_networks_for_text_classification_amd import factor
+    f = factor.HubFactor()
+    f.x_hub, f.x_hub_dense = object(), None
+    assert f.hub_operand(False) == "csr" and f.hub_operand(True) == "csr"
+    f.x_hub_dense = object()
+    assert f.hub_operand(False) == "dense"
+    assert f.hub_operand(True) == ("csr" if factor.XHUB_TRAIN_TILE else "dense")
+    f.x_hub = None   # a dense X: its hub rows exist only as the dense copy
+    assert f.hub_operand(True) == "dense"

@@ -1203,6 +1203,32 @@ def test_factored_gc1_matches_spmm_path(r8, mode):
         _grads_close(ga[k], gb[k], k)
 
 
+def test_xhub_product_per_mode(r8):
+    """S_T = X[hubs] W1 of the factored forward takes R8's dense hub rows
+    through the K-split GEMM in eval and their CSR through the tile plan in
+    training (factor.hub_operand; profiles/r06_xhub_train_ab.log): both within
+    fp32 reassociation error of float64, and the forward records follow the
+    same choice."""
+    from graph_convolutional_networks_for_text_classification_amd import factor, ops, record
+    from graph_convolutional_networks_for_text_classification_amd.sparse import as_csr
+    X, A = r8["features"].to(DEV), r8["adj"].to(DEV)
+    adj, xop = as_csr(A), ops.Operand(X)
+    f = factor.get(adj, xop)
+    assert f is not None and f.x_hub is not None and f.x_hub_dense is not None
+    assert f.hub_operand(False) == "dense"
+    assert f.hub_operand(True) == ("csr" if factor.XHUB_TRAIN_TILE else "dense")
+    W1 = torch.randn(r8["nfeat"], 200, generator=torch.Generator().manual_seed(5)).to(DEV) * 0.05
+    want = f.x_hub_dense.double().cpu().numpy() @ W1.double().cpu().numpy()
+    for train in (False, True):
+        got = f.hub_times(W1, train=train).cpu().double().numpy()
+        assert np.abs(got - want).max() <= 1e-5 * max(1.0, np.abs(want).max()), train
+    rec_e, _ = record.get(adj, xop, 200, r8["nclass"], DEV)
+    rec_t, _ = record.get(adj, xop, 200, r8["nclass"], DEV, train=True)
+    assert rec_e.kind == rec_t.kind == record.FACTORED
+    assert rec_e.s.x_dense and not rec_e.s.x.plan
+    assert bool(rec_t.s.x.plan) == (f.hub_operand(True) == "csr")
+
+
 @pytest.mark.parametrize("F,P,ndoc", [(52, 3, 2000), (200, 20, 2000), (36, 32, 2000), (200, 20, 12000)])
 def test_factored_gc1_kernel_against_float64(F, P, ndoc):
     """gcnk_hubfactor_gc1_f32 alone on a synthetic doc-topic graph with hub x

@@ -327,8 +327,22 @@ def _get(adj, xop, F, P, device, cls, tag, train=False):
         return rec, stream
 
 
-# records displaced from a cache while a captured graph still points into them
+# records displaced from a cache while a captured graph still points into them:
+# kept alive (a replay writes into their buffers through raw pointers, which
+# no reference count sees), so this list grows by one record each time the
+# operands of a captured forward change in place; release_pinned() drops them
+# once the caller's graphs are gone
 _PINNED = []
+
+
+def release_pinned():
+    """Drop the records kept alive for hipGraphs captured before their operands
+    changed (call after those graphs are destroyed; replaying one afterwards
+    writes into freed memory).  Returns how many were dropped."""
+    with _lock:
+        n = len(_PINNED)
+        _PINNED.clear()
+    return n
 
 
 def _version(src):

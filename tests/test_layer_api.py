@@ -61,3 +61,12 @@ def test_default_split_k_keeps_short_reductions_whole():
     assert ops.default_split_k(7724, 8, 200) == 1        # H1 W2: the skinny kernel's shape
     assert ops.default_split_k(7724, 200, 8) == 1        # g W2^T
     assert ops.default_split_k(200, 8, 7724) >= 16       # H1^T g: K = nodes
+
+
+def test_release_pinned_drops_displaced_records():
+    """record.release_pinned() empties the list of records kept alive for
+    captured graphs (the list otherwise only grows: ADVICE round 5)."""
+    from graph_convolutional_networks_for_text_classification_amd import record
+    record._PINNED.append(object())
+    assert record.release_pinned() >= 1
+    assert record._PINNED == []

@@ -137,6 +137,34 @@ def test_spmm_power_law_rows_and_linearity(rmat17, F):
     assert torch.equal(spmm(a, B1), C1)
 
 
+@pytest.mark.parametrize("F,ipc,lanes", [(64, 4, 64), (64, None, None), (8, 4, 0), (200, None, None)])
+def test_spmm_heavy_rows_at_the_combine_boundaries(F, ipc, lanes):
+    """Rows around the plan's combine boundaries (csrc/spmm.hip: 64 segments
+    per combine, groups of <= 64 under a top entry past that, segment length
+    doubled only past 4,096 segments): degrees one below / at / above 64 and
+    128 segments of the smallest segment (ipc 4 x 4 waves = 16), a row of
+    70,000 nonzeros (4,375 segments of 16: the doubling), empty and light
+    rows; against the float64 oracle, bitwise reproducible."""
+    rng = np.random.default_rng(F + (ipc or 0))
+    K = 80_000
+    degs = [1023, 1024, 1025, 2047, 2049, 70_000, 0, 5, 1, 300]
+    rows, cols = [], []
+    for r, d in enumerate(degs):
+        span = K // 8 if r < 5 else K   # (one column class: one run, exact segment counts)
+        c = np.sort(rng.choice(span, d, replace=False)) if d else np.zeros(0, np.int64)
+        rows.append(np.full(d, r))
+        cols.append(c)
+    rows, cols = np.concatenate(rows), np.concatenate(cols)
+    rp, ci, v = csr_ref.coo_to_csr(rows, cols, rng.standard_normal(rows.size), (len(degs), K))
+    a = from_arrays(rp, ci, v, (len(degs), K), DEV)
+    B = rng.standard_normal((K, F)).astype(np.float32)
+    Bt = torch.from_numpy(B).to(DEV)
+    kw = {} if ipc is None else {"ipc": ipc, "lanes": lanes}
+    got = spmm(a, Bt, **kw)
+    _close(got, csr_ref.spmm_csr(rp, ci, v, B), rtol=1e-5, atol=2e-5 * np.sqrt(70_000))
+    assert torch.equal(spmm(a, Bt, **kw), got)
+
+
 @pytest.mark.parametrize("ipc", [4, 8, 12, 16, 32, 64])
 @pytest.mark.parametrize("lanes", [0, 16, 32])
 def test_spmm_schedule_variants(ipc, lanes):

@@ -71,3 +71,39 @@ def test_power_law_row_takes_two_combine_levels():
     B = rng.standard_normal((K, 2))
     np.testing.assert_allclose(path_model.spmm(rp, ci, v, B, ipc, groups), csr_ref.spmm_csr(rp, ci, v, B), rtol=1e-9,
                                atol=1e-9)
+
+
+def test_combine_levels_at_the_boundaries():
+    """csrc/spmm.hip's heavy-row plan at its boundaries (segment length 16 at
+    ipc 4 with one lane group): 64 segments -> one combine; 65 -> a top entry
+    over 2 groups; 4,375 segments (> 4,096) -> the segment length doubles, then
+    groups of <= 64 under a top entry; the model's product is the float64 one."""
+    rng = np.random.default_rng(3)
+    K = 80_000
+    degs = [1024, 1025, 70_000, 3]
+    # rows 0 and 1 inside one column class (K / 8 columns): one run, so their
+    # segment counts are exactly ceil(deg / 16) = 64 and 65
+    span = [K // 8, K // 8, K, K]
+    rows = np.concatenate([np.full(d, r) for r, d in enumerate(degs)])
+    cols = np.concatenate([np.sort(rng.choice(sp, d, replace=False)) for d, sp in zip(degs, span)])
+    rp, ci, v = csr_ref.coo_to_csr(rows, cols, rng.standard_normal(rows.size), (len(degs), K))
+    ipc, groups = 4, 1
+    units, heavy, nh, nslots = path_model.host_plan(rp, ci, K, ipc, groups)
+    seg = ipc * path_model.geometry(groups)[2]
+    assert seg == 16
+
+    def entries(r):
+        return [h for h in heavy if h[0] == r]
+    e0 = entries(0)
+    assert len(e0) == 1 and e0[0][2] == 64 and e0[0][3] == -1
+    e1 = entries(1)
+    assert [h[3] for h in e1].count(-2) == 1 and len(e1) == 3
+    e2 = entries(2)
+    top = [h for h in e2 if h[3] == -2]
+    assert len(top) == 1 and top[0][2] == len(e2) - 1
+    assert all(h[2] <= path_model.K_MAX_SEG for h in e2)
+    seglens = [u[2] - u[1] for u in units[:nh] if u[0] == 2]
+    assert max(seglens) <= 2 * seg < 3 * seg and len(seglens) <= 4096
+    B = rng.standard_normal((K, 2))
+    np.testing.assert_allclose(path_model.spmm(rp, ci, v, B, ipc, groups), csr_ref.spmm_csr(rp, ci, v, B),
+                               rtol=1e-9, atol=1e-9)

@@ -30,6 +30,7 @@
 namespace gcnk {
 namespace {
 
+typedef float f32x4v __attribute__((ext_vector_type(4)));
 constexpr int kBwdBlock = 256;
 constexpr int kBwdCols = 256;      // columns per workgroup slice
 constexpr int kBwdRowsMax = 256;   // rows per workgroup (LDS staging of gS2 / G)
@@ -38,6 +39,10 @@ constexpr int kBwdBatch = 8;       // rows per lane whose H1 loads are in flight
 #define GCNK_BWD_TARGET 256
 #endif
 constexpr int kBwdTarget = GCNK_BWD_TARGET;    // workgroups per slice (256: one per CU)
+// 1 (default): the row lanes' gW2 / gb1 partials summed as float4 pieces where P == PM
+#ifndef GCNK_BWD2_VSUM
+#define GCNK_BWD2_VSUM 1
+#endif
 #ifndef GCNK_BWD2_STAMPV   // stamps-build timeline variant (2: around the lane sum)
 #define GCNK_BWD2_STAMPV 1
 #endif
@@ -206,6 +211,51 @@ __global__ void __launch_bounds__(kBwdBlock) gcn_bwd2_kernel(Bwd2Args a) {
 #else
   stamp(a.stamps, 2);
 #endif
+  float* prow = a.part + (int64_t)blockIdx.x * a.part_ld;
+#if GCNK_BWD2_VSUM
+  // P == PM with 16-B partial rows: the thread's VEC x PM gW2 terms then its VEC
+  // gb1 terms as float4 pieces in LDS, each output float4 (8 of gW2 + 1 of gb1
+  // per column unit) summed over the row lanes in lane order and stored as one
+  // 16-B piece -- the partial's layout in global memory is unchanged (gW2
+  // [N x P] row-major | gb1 [N] | gb2 [P]).  (The per-float form below spends
+  // ~7 dword iterations of index math, eight LDS reads and a 4-B store per
+  // element: the phase measured ~3.7 us at R8, profiles/r05_bwd2_stamps_v2.log.)
+  if (VEC == 4 && a.P == PM && (a.part_ld & 3) == 0 && (a.N * a.P) % 4 == 0) {
+    constexpr int KE4 = KE / 4;   // VEC (PM + 1) / 4 float4 per thread (PM % 4 == 0)
+    f32x4v* mine = reinterpret_cast<f32x4v*>(s_red) + tid * KE4;
+#pragma unroll
+    for (int v = 0; v < VEC; ++v)
+#pragma unroll
+      for (int p = 0; p < PM; p += 4) mine[(v * PM + p) / 4] = f32x4v{gw[v][p], gw[v][p + 1], gw[v][p + 2], gw[v][p + 3]};
+#pragma unroll
+    for (int v = 0; v < VEC; v += 4) {
+      f32x4v g4;
+#pragma unroll
+      for (int i = 0; i < 4; ++i) g4[i] = v + i < VEC ? gb[v + i] : 0.f;
+      mine[(VEC * PM + v) / 4] = g4;
+    }
+    __syncthreads();
+#if GCNK_BWD2_STAMPV == 2
+    stamp(a.stamps, 2);
+#endif
+    const f32x4v* red = reinterpret_cast<const f32x4v*>(s_red);
+    for (int e = tid; e < CT * KE4; e += kBwdBlock) {
+      const int u = e / KE4, k4 = e - u * KE4;
+      f32x4v sum = red[u * KE4 + k4];
+      for (int l = 1; l < RL; ++l) sum += red[(l * CT + u) * KE4 + k4];
+      const int64_t c0 = (int64_t)(cu0 + u) * VEC;
+      if (c0 >= a.N) continue;
+      if (k4 < VEC * PM / 4) {   // gW2 rows c0 .. c0 + VEC - 1: VEC PM contiguous floats
+        *reinterpret_cast<f32x4v*>(prow + c0 * a.P + 4 * k4) = sum;
+      } else {                   // gb1 [c0 .. c0 + VEC): VEC floats
+#pragma unroll
+        for (int i = 0; i < 4; ++i)
+          if (4 * (k4 - VEC * PM / 4) + i < VEC) prow[(int64_t)a.N * a.P + c0 + 4 * (k4 - VEC * PM / 4) + i] = sum[i];
+      }
+    }
+  } else
+#endif
+  {
   // row lanes -> one partial per column, summed in lane order
   {
     float* mine = s_red + tid * KE;
@@ -220,7 +270,6 @@ __global__ void __launch_bounds__(kBwdBlock) gcn_bwd2_kernel(Bwd2Args a) {
 #if GCNK_BWD2_STAMPV == 2
   stamp(a.stamps, 2);
 #endif
-  float* prow = a.part + (int64_t)blockIdx.x * a.part_ld;
   for (int e = tid; e < CT * KE; e += kBwdBlock) {
     const int u = e / KE, k = e % KE;
     const int v = k / (PM + 1), p = k % (PM + 1);
@@ -243,6 +292,7 @@ __global__ void __launch_bounds__(kBwdBlock) gcn_bwd2_kernel(Bwd2Args a) {
     } else {
       prow[(int64_t)a.N * a.P + col] = s;
     }
+  }
   }
   if (with_g && tid < a.P) {  // gb2: the G rows, in row order (eight LDS reads in flight)
     float s = 0.f;

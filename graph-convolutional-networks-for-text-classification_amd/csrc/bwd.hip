@@ -128,11 +128,24 @@ __global__ void __launch_bounds__(kBwdBlock) gcn_bwd2_kernel(Bwd2Args a) {
 #pragma unroll
       for (int v = 0; v < VEC; ++v) h[j][v] = 0.f;
   }
-  // gS2 (and G) rows of the workgroup -> LDS, padded to PM columns with zeros
-  for (int i = tid; i < nr * PM; i += kBwdBlock) {
-    const int rr = i / PM, p = i % PM;
-    s_g[i] = p < a.P ? a.gS[(int64_t)(r0 + rr) * a.ldgs + p] : 0.f;
-    if (with_g) s_gg[i] = p < a.P ? a.G[(int64_t)(r0 + rr) * a.ldg + p] : 0.f;
+  // gS2 (and G) rows of the workgroup -> LDS, padded to PM columns with zeros.
+  // Unpadded contiguous rows (P == PM == ld, R8): LDS-DMA, no register round
+  // trip before the barrier (a load -> LDS store pair waits on its load)
+  const bool g_dma = a.P == PM && a.ldgs == PM && (!with_g || a.ldg == PM);
+  if (g_dma) {
+    const int n = nr * PM, lane = tid & 63;
+    for (int e0 = tid & ~63; e0 < n; e0 += kBwdBlock) {   // (wave-uniform base)
+      if (e0 + lane < n) {
+        lds_dma4(a.gS + (int64_t)r0 * PM + e0 + lane, s_g + e0);
+        if (with_g) lds_dma4(a.G + (int64_t)r0 * PM + e0 + lane, s_gg + e0);
+      }
+    }
+  } else {
+    for (int i = tid; i < nr * PM; i += kBwdBlock) {
+      const int rr = i / PM, p = i % PM;
+      s_g[i] = p < a.P ? a.gS[(int64_t)(r0 + rr) * a.ldgs + p] : 0.f;
+      if (with_g) s_gg[i] = p < a.P ? a.G[(int64_t)(r0 + rr) * a.ldg + p] : 0.f;
+    }
   }
   // this lane's columns of W2 (rows of W2: W2[n, :]).  (Issued before the
   // staging above instead: staging 2.7 -> 4.2 us, profiles/r04_bwd2_stamps_v2.log.)
@@ -140,14 +153,20 @@ __global__ void __launch_bounds__(kBwdBlock) gcn_bwd2_kernel(Bwd2Args a) {
   // of VEC PM floats: 16-B loads instead of VEC PM 4-B loads 32 lanes apart)
   float w[VEC][PM];
   if (a.ldw == PM && a.P == PM && (reinterpret_cast<uintptr_t>(a.W) & 15) == 0) {
+    // (clamped row, value masked by bits: the guarded load compiled to a branch
+    // per load with its own vmcnt(0) -- eight serialised round trips)
 #pragma unroll
-    for (int v = 0; v < VEC; ++v)
+    for (int v = 0; v < VEC; ++v) {
+      const bool ok = act && c + v < a.N;
+      const int m = ok ? -1 : 0;
+      const float* wr = a.W + (ok ? c + v : 0) * a.ldw;
 #pragma unroll
       for (int p = 0; p < PM; p += 4) {
-        float4 q = make_float4(0.f, 0.f, 0.f, 0.f);
-        if (act && c + v < a.N) q = *reinterpret_cast<const float4*>(a.W + (c + v) * a.ldw + p);
-        w[v][p] = q.x; w[v][p + 1] = q.y; w[v][p + 2] = q.z; w[v][p + 3] = q.w;
+        const float4 q = *reinterpret_cast<const float4*>(wr + p);
+        w[v][p] = __int_as_float(__float_as_int(q.x) & m); w[v][p + 1] = __int_as_float(__float_as_int(q.y) & m);
+        w[v][p + 2] = __int_as_float(__float_as_int(q.z) & m); w[v][p + 3] = __int_as_float(__float_as_int(q.w) & m);
       }
+    }
   } else {
 #pragma unroll
     for (int v = 0; v < VEC; ++v)
@@ -162,6 +181,7 @@ __global__ void __launch_bounds__(kBwdBlock) gcn_bwd2_kernel(Bwd2Args a) {
 #pragma unroll
     for (int p = 0; p < PM; ++p) gw[v][p] = 0.f;
   }
+  if (g_dma) __builtin_amdgcn_s_waitcnt(0x0F70);  // vmcnt(0): this wave's DMA (and loads) landed
   __syncthreads();
 #if GCNK_BWD2_STAMPV != 2
   stamp(a.stamps, 1);

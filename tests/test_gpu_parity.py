@@ -1372,11 +1372,15 @@ def _gensim_r8_x(r8):
 
 
 @pytest.mark.parametrize("K,F,P,M", [(100, 200, 20, 18916), (100, 200, 8, 7724), (7, 8, 3, 1000),
-                                     (50, 52, 32, 777), (128, 256, 17, 2049), (64, 100, 16, 33), (13, 200, 1, 16)])
+                                     (50, 52, 32, 777), (128, 256, 17, 2049), (64, 100, 16, 33), (13, 200, 1, 16),
+                                     (30, 180, 18, 500), (100, 208, 20, 1000), (97, 196, 19, 300), (100, 240, 20, 600)])
 def test_dense_gc1_kernel_against_float64(K, F, P, M):
     """gcnk_dense_gc1_f32 alone: H1 = relu(AX W1 + b1) and S2 = H1 W2 against
     float64 for K of 1-32 k-steps (K not a multiple of 4 included), F not a
-    multiple of 16, P of one and two MFMA n-tiles, M ragged (a partial last
+    multiple of 16, both column layouts (three n-tiles a wave with the rotating
+    tail n-tile for F in 193..208 -- 196, 200, 208 -- and without it; four past
+    208), P of one and two MFMA n-tiles and of one tile + 1-4 VALU columns
+    (17-20), M ragged (a partial last
     16-row tile) and below / above the CU count in tiles; H1 stored or not
     (S2 bitwise the same); the dropout-mask epilogue against the same mask in
     float64; the launch bitwise reproducible."""

@@ -293,34 +293,44 @@ dense_gc1_kernel(DenseArgs a) {
     //      tile into wave-private LDS (local column NI c + t; the tail's 48 + c)
     const int64_t row0 = (int64_t)tile * 16;
     const bool plain = a.epi.code == GCNK_EPI_BIAS_RELU;
-    //      (columns past F: acc and b1 zero, h = 0 written)
-#pragma unroll
-    for (int r = 0; r < 4; ++r) {
+    //      (the plain / dropout choice is one uniform branch around all the
+    //      tile's elements: tested per element, it compiled into ~50
+    //      instructions and 5 branches per element on the plain path too)
+    auto emit = [&](int r, const float (&h)[NI], float ht) __attribute__((always_inline)) {
       const int64_t row = row0 + 4 * q + r;
-      float h[NI];
-#pragma unroll
-      for (int t = 0; t < NI; ++t) {
-        if (plain) h[t] = fmaxf(acc[t][r] + bv[t], 0.f);
-        else h[t] = (row < a.M && col0 + t < F) ? apply_epi(a.epi, acc[t][r], bv[t], row, col0 + t) : 0.f;
-      }
       if constexpr (NI == 4) {
         const f32x4 h4 = {h[0], h[1], h[2], h[3]};
         if (a.H && row < a.M && col0 < F) __builtin_nontemporal_store(h4, reinterpret_cast<f32x4*>(a.H + row * a.ldh + col0));
         *reinterpret_cast<f32x4*>(&hw[(4 * q + r) * kHP + 4 * c]) = h4;
       } else {
+        if (a.H) {
 #pragma unroll
-        for (int t = 0; t < NI; ++t) {
-          if (a.H && row < a.M && col0 + t < F) __builtin_nontemporal_store(h[t], a.H + row * a.ldh + col0 + t);
-          hw[(4 * q + r) * kHP + NI * c + t] = h[t];
+          for (int t = 0; t < NI; ++t)
+            if (row < a.M && col0 + t < F) __builtin_nontemporal_store(h[t], a.H + row * a.ldh + col0 + t);
+          if (mine && row < a.M && kTail0 + c < F) __builtin_nontemporal_store(ht, a.H + row * a.ldh + kTail0 + c);
         }
-        if (mine) {
-          const int ct = kTail0 + c;
-          float ht;
-          if (plain) ht = fmaxf(acct[r] + btl, 0.f);
-          else ht = (row < a.M && ct < F) ? apply_epi(a.epi, acct[r], btl, row, ct) : 0.f;
-          if (a.H && row < a.M && ct < F) __builtin_nontemporal_store(ht, a.H + row * a.ldh + ct);
-          hw[(4 * q + r) * kHP + 48 + c] = ht;
-        }
+#pragma unroll
+        for (int t = 0; t < NI; ++t) hw[(4 * q + r) * kHP + NI * c + t] = h[t];
+        if (mine) hw[(4 * q + r) * kHP + 48 + c] = ht;
+      }
+    };
+    if (plain) {
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        float h[NI];
+#pragma unroll
+        for (int t = 0; t < NI; ++t) h[t] = fmaxf(acc[t][r] + bv[t], 0.f);
+        emit(r, h, fmaxf(acct[r] + btl, 0.f));
+      }
+    } else {
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const int64_t row = row0 + 4 * q + r;
+        float h[NI];
+#pragma unroll
+        for (int t = 0; t < NI; ++t)
+          h[t] = (row < a.M && col0 + t < F) ? apply_epi(a.epi, acc[t][r], bv[t], row, col0 + t) : 0.f;
+        emit(r, h, (mine && row < a.M && kTail0 + c < F) ? apply_epi(a.epi, acct[r], btl, row, kTail0 + c) : 0.f);
       }
     }
     // the wave's own LDS writes before its reads (other lanes' elements)

@@ -236,24 +236,31 @@ hubfactor_gc1_kernel(FactorArgs a) {
       for (int u = 0; u < NTQ; ++u) Vec<4>::fma(z[u], v, sv[u]);
     }
     if (row >= 0) {
-      const bool plain = a.epi.code == GCNK_EPI_BIAS_RELU;  // eval / no-dropout: no per-element branches
+      auto put = [&](int q, const float4& h) __attribute__((always_inline)) {
+        if (a.H) {  // H1 for the backward: streaming store (no dirty L2 lines at the kernel's end)
+          typedef float f4a __attribute__((ext_vector_type(4), aligned(16)));
+          __builtin_nontemporal_store(f4a{h.x, h.y, h.z, h.w}, reinterpret_cast<f4a*>(a.H + row * a.ldh + 4 * q));
+        }
+        *reinterpret_cast<float4*>(s_Z + r * Fz + 4 * q) = h;
+      };
+      // eval / no-dropout: one uniform branch around all the elements (tested
+      // per element, the dropout path's code sat on the plain path: ~50
+      // instructions and several branches per float4)
+      if (a.epi.code == GCNK_EPI_BIAS_RELU) {
 #pragma unroll
-      for (int u = 0; u < NTQ; ++u) {
-        const int q = c16 + 16 * u;
-        if (q < Q) {
-          const float4 bv = *reinterpret_cast<const float4*>(s_bias + 4 * q);
-          float4 h;
-          if (plain) {
-            h.x = fmaxf(z[u].x + bv.x, 0.f); h.y = fmaxf(z[u].y + bv.y, 0.f);
-            h.z = fmaxf(z[u].z + bv.z, 0.f); h.w = fmaxf(z[u].w + bv.w, 0.f);
-          } else {
-            h = Vec<4>::epi(a.epi, z[u], bv, row, 4 * (int64_t)q);
+        for (int u = 0; u < NTQ; ++u) {
+          const int q = c16 + 16 * u;
+          if (q < Q) {
+            const float4 bv = *reinterpret_cast<const float4*>(s_bias + 4 * q);
+            put(q, make_float4(fmaxf(z[u].x + bv.x, 0.f), fmaxf(z[u].y + bv.y, 0.f), fmaxf(z[u].z + bv.z, 0.f),
+                               fmaxf(z[u].w + bv.w, 0.f)));
           }
-          if (a.H) {  // H1 for the backward: streaming store (no dirty L2 lines at the kernel's end)
-            typedef float f4a __attribute__((ext_vector_type(4), aligned(16)));
-            __builtin_nontemporal_store(f4a{h.x, h.y, h.z, h.w}, reinterpret_cast<f4a*>(a.H + row * a.ldh + 4 * q));
-          }
-          *reinterpret_cast<float4*>(s_Z + r * Fz + 4 * q) = h;
+        }
+      } else {
+#pragma unroll
+        for (int u = 0; u < NTQ; ++u) {
+          const int q = c16 + 16 * u;
+          if (q < Q) put(q, Vec<4>::epi(a.epi, z[u], *reinterpret_cast<const float4*>(s_bias + 4 * q), row, 4 * (int64_t)q));
         }
       }
     }

@@ -147,6 +147,17 @@ struct Vec<4> {
   }
   static __device__ __forceinline__ T epi(const Epi& e, const T& a, const T& b, int64_t row, int64_t col) {
     T r;
+    // the dropout-free codes tested once for the four elements (per element,
+    // each apply_epi carried its own chain of code tests and the dropout paths'
+    // blocks sat between them); the same arithmetic as apply_epi
+    if (e.code <= GCNK_EPI_BIAS_RELU) {
+      if (e.code == GCNK_EPI_NONE) return a;
+      r = make_float4(a.x + b.x, a.y + b.y, a.z + b.z, a.w + b.w);
+      if (e.code == GCNK_EPI_BIAS) return r;
+      r.x = r.x > 0.0f ? r.x : 0.0f; r.y = r.y > 0.0f ? r.y : 0.0f;
+      r.z = r.z > 0.0f ? r.z : 0.0f; r.w = r.w > 0.0f ? r.w : 0.0f;
+      return r;
+    }
     r.x = apply_epi(e, a.x, b.x, row, col + 0);
     r.y = apply_epi(e, a.y, b.y, row, col + 1);
     r.z = apply_epi(e, a.z, b.z, row, col + 2);

@@ -106,27 +106,24 @@ dense_gc1_kernel(DenseArgs a) {
   float* hw = s_h[w];
   // the A tile [16 x 4 KS] (zero past K and M): thread element e -> row e / (4 KS),
   // k e % (4 KS) -- consecutive threads, consecutive k: coalesced
-  auto load_a_raw = [&](int tile, float (&av)[kAPer]) {
+  // The A tile through a buffer resource over the tile's rows (rows past M,
+  // and every row of a tile past the last, read 0): thread element i has a
+  // fixed offset inside the tile, and an element past K or past the tile gets
+  // an offset past any tile's resource, so it reads 0 too -- one load
+  // instruction per element, no compares or selects in the tile loop.
+  int voff[kAPer];
 #pragma unroll
-    for (int i = 0; i < kAPer; ++i) {
-      const int e = tid + kThreads * i, r = e / (4 * KS), k = e % (4 * KS);
-      const int64_t row = (int64_t)tile * 16 + r;
-      // (the address clamped into A, the value selected after: no branch per load)
-      const int64_t rc = row < a.M ? row : a.M - 1;
-      av[i] = a.A[rc * a.lda + (k < K ? k : K - 1)];
-    }
-  };
-  auto mask_a = [&](int tile, float (&av)[kAPer]) {
-#pragma unroll
-    for (int i = 0; i < kAPer; ++i) {
-      const int e = tid + kThreads * i, r = e / (4 * KS), k = e % (4 * KS);
-      const int64_t row = (int64_t)tile * 16 + r;
-      av[i] = (e < 16 * 4 * KS && tile < a.ntiles && row < a.M && k < K) ? av[i] : 0.f;
-    }
-  };
+  for (int i = 0; i < kAPer; ++i) {
+    const int e = tid + kThreads * i, r = e / (4 * KS), k = e % (4 * KS);
+    voff[i] = (e < 16 * 4 * KS && k < K) ? (r * (int)a.lda + k) * 4 : 0x7ffffff0;
+  }
   auto load_a = [&](int tile, float (&av)[kAPer]) {
-    load_a_raw(tile, av);
-    mask_a(tile, av);
+    const int64_t row0 = (int64_t)tile * 16;
+    const int rows = row0 < a.M ? (int)min<int64_t>(16, a.M - row0) : 0;
+    const __amdgpu_buffer_rsrc_t ra = __builtin_amdgcn_make_buffer_rsrc(
+        const_cast<float*>(a.A + (rows ? row0 : 0) * a.lda), (short)0, rows * (int)a.lda * 4, 0x00020000);
+#pragma unroll
+    for (int i = 0; i < kAPer; ++i) av[i] = __uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(ra, voff[i], 0, 0));
   };
   auto put_a = [&](int buf, const float (&av)[kAPer]) {
 #pragma unroll
@@ -198,7 +195,7 @@ dense_gc1_kernel(DenseArgs a) {
   if constexpr (kTail)
     btl = __uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(rb1, (kTail0 + c < F ? kTail0 + c : F) * 4, 0, 0));
   float av0[kAPer];
-  load_a_raw(blockIdx.x, av0);
+  load_a(blockIdx.x, av0);
   float pv[PV ? PV : 1];
 #pragma unroll
   for (int i = 0; i < PV; ++i)   // W2[tid][16 NPM + i] (rows past F read 0)
@@ -244,7 +241,6 @@ dense_gc1_kernel(DenseArgs a) {
   }
 #pragma unroll
   for (int i = 0; i < PV; ++i) s_w2v[i][tid] = pv[i];
-  mask_a(blockIdx.x, av0);
   put_a(0, av0);
 #ifdef GCNK_STAMPS
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
@@ -521,7 +517,8 @@ extern "C" int gcnk_dense_gc1_f32(int32_t M, int32_t K, int32_t F, int32_t P, co
     return GCNK_EARG;
   }
   if (K > 128 || F > 256 || F % 4 || P > kMaxP || ldw1 % 4 || !aligned16(W1) ||
-      (int64_t)K * ldw1 * 4 >= INT32_MAX || (int64_t)F * ldw2 * 4 >= INT32_MAX ||   // (32-bit buffer offsets)
+      (int64_t)K * ldw1 * 4 >= INT32_MAX || (int64_t)F * ldw2 * 4 >= INT32_MAX ||   // (32-bit buffer offsets;
+      (int64_t)16 * ldax * 4 >= 0x7ff00000 ||                                        //  A's tile sentinel past them)
       (bias && !aligned16(bias)) || (H && (ldh % 4 || !aligned16(H)))) {
     set_error("gcnk_dense_gc1_f32: unsupported shape (K=%d <= 128, F=%d <= 256 and %% 4, P=%d <= 32, "
               "16-B aligned W1 / b1 / H1 rows)", K, F, P);

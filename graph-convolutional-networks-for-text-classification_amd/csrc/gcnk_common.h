@@ -158,6 +158,17 @@ struct Vec<4> {
       r.z = r.z > 0.0f ? r.z : 0.0f; r.w = r.w > 0.0f ? r.w : 0.0f;
       return r;
     }
+    if (e.code == GCNK_EPI_BIAS_RELU_HASH) {   // apply_epi's hash mask, the element index formed once
+      const uint64_t i0 = e.offset + (uint64_t)(row * e.ldm + col);
+      const float v[4] = {a.x + b.x, a.y + b.y, a.z + b.z, a.w + b.w};
+      float o[4];
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        const float h = v[j] > 0.0f ? v[j] : 0.0f;
+        o[j] = hash_uniform(e.seed_lo, e.seed_hi, i0 + (uint64_t)j) < e.keep_prob ? h * e.scale : 0.0f;
+      }
+      return make_float4(o[0], o[1], o[2], o[3]);
+    }
     r.x = apply_epi(e, a.x, b.x, row, col + 0);
     r.y = apply_epi(e, a.y, b.y, row, col + 1);
     r.z = apply_epi(e, a.z, b.z, row, col + 2);

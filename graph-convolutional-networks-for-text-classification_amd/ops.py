@@ -305,7 +305,9 @@ def dense_gc1(d, W1, b1, W2, epilogue=_lib.EPI_BIAS_RELU, mask=None, scale=1.0, 
     gcnk_dense_gc1_f32 -- H1 = drop(relu((A-hat X) W1 + b1)) (reference
     layer.py:102,106,110,182,185) and S2 = H1 W2 (layer.py:102, gc2).  None
     where the kernel refuses the operands (GCNK_EUNSUP: rows of W1 / b1 / H1
-    that are not 16-B aligned): the caller then takes the SpMM path."""
+    that are not 16-B aligned, or row strides that put W1, W2 or a 16-row tile
+    of A-hat X past its 32-bit buffer offsets -- not reachable with the
+    module's contiguous operands): the caller then takes the SpMM path."""
     W1 = _dense_f32(W1, "gc1 weight")
     W2 = _dense_f32(W2, "gc2 weight")
     _check_rng_base(rng_base, W1.device)

@@ -353,18 +353,26 @@ gemm_smallm_wk_kernel(int32_t M, int32_t N, int32_t K, const float* __restrict__
   const int r = lane & 15, q = lane >> 4;
   const int64_t kb0 = ((int64_t)blockIdx.x * kW + w) * KBW;   // this wave's first 16-deep k block
   const int64_t n0 = (int64_t)blockIdx.y * 16 * NTG;
+  // A and B through buffer resources sized to them (the dispatch keeps both
+  // under 2 GB): rows of A past M and rows of B past K read 0 with no compare
+  // or 64-bit address per load (that prologue was ~300 instructions a wave,
+  // issued at 4 cycles each before the last load left); a column of B past N
+  // only feeds an output column that is never stored.  A's components past K
+  // are still zeroed: its row padding is not ours, and 0 x a NaN pad is NaN.
+  const __amdgpu_buffer_rsrc_t ra =
+      __builtin_amdgcn_make_buffer_rsrc(const_cast<float*>(A), (short)0, M * (int)lda * 4, 0x00020000);
+  const __amdgpu_buffer_rsrc_t rb =
+      __builtin_amdgcn_make_buffer_rsrc(const_cast<float*>(B), (short)0, K * (int)ldb * 4, 0x00020000);
   float4 a[RT][KBW];
 #pragma unroll
   for (int t = 0; t < RT; ++t)
 #pragma unroll
     for (int c = 0; c < KBW; ++c) {
-      const int64_t row = 16 * t + r, k = 16 * (kb0 + c) + 4 * q;
-      const bool ok = row < M && k < K;  // lda % 4 == 0 and lda >= K rounded up to 4: the float4 lies in the row
-      const float4 v = *reinterpret_cast<const float4*>(A + (ok ? row * lda + k : 0));
-      // (A's row padding past K is never multiplied: B's rows there are zero, and
-      // 0 x a NaN pad would not be)
-      a[t][c] = ok ? make_float4(v.x, k + 1 < K ? v.y : 0.f, k + 2 < K ? v.z : 0.f, k + 3 < K ? v.w : 0.f)
-                   : make_float4(0.f, 0.f, 0.f, 0.f);
+      const int row = 16 * t + r, k = 16 * ((int)kb0 + c) + 4 * q;
+      const f32x4 v = __builtin_bit_cast(
+          f32x4, __builtin_amdgcn_raw_buffer_load_b128(ra, (row * (int)lda + (k < K ? k : 0)) * 4, 0, 0));
+      a[t][c] = k + 3 < K ? make_float4(v[0], v[1], v[2], v[3])
+                          : make_float4(k < K ? v[0] : 0.f, k + 1 < K ? v[1] : 0.f, k + 2 < K ? v[2] : 0.f, 0.f);
     }
   float b[KBW][4][NTG];
 #pragma unroll
@@ -373,10 +381,8 @@ gemm_smallm_wk_kernel(int32_t M, int32_t N, int32_t K, const float* __restrict__
     for (int j = 0; j < 4; ++j)
 #pragma unroll
       for (int u = 0; u < NTG; ++u) {
-        const int64_t k = 16 * (kb0 + c) + 4 * q + j, n = n0 + 16 * u + r;
-        const bool ok = k < K && n < N;
-        const float v = B[ok ? k * ldb + n : 0];
-        b[c][j][u] = ok ? v : 0.f;
+        const int k = 16 * ((int)kb0 + c) + 4 * q + j, n = (int)n0 + 16 * u + r;
+        b[c][j][u] = __uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(rb, (k * (int)ldb + n) * 4, 0, 0));
       }
   f32x4 acc[RT][NTG];
 #pragma unroll
@@ -671,7 +677,8 @@ extern "C" int gcnk_gemm_f32(int32_t transA, int32_t transB, int32_t M, int32_t 
   // 8 waves x 16 KBW k, summed by gemm_slab_reduce4_kernel
   const int64_t wk_S = ((int64_t)K + 8 * 16 * GCNK_WK_KBW - 1) / (8 * 16 * GCNK_WK_KBW);
   if (GCNK_GEMM_SMALLM_WK && !ta && !tb && M <= 64 && K >= 512 && N % 4 == 0 && lda % 4 == 0 && aligned16(A) &&
-      split_k > 1 && wk_S <= split_k && wk_S <= 65535) {
+      split_k > 1 && wk_S <= split_k && wk_S <= 65535 &&
+      (int64_t)M * lda * 4 < INT32_MAX && ((int64_t)K + 16) * ldb * 4 < INT32_MAX) {   // (its buffer offsets)
     const dim3 grid((unsigned)wk_S, (unsigned)((N + 16 * GCNK_WK_NTG - 1) / (16 * GCNK_WK_NTG)));
     hipLaunchKernelGGL((gemm_smallm_wk_kernel<GCNK_WK_KBW, GCNK_WK_NTG>), grid, dim3(512), 0, s, M, N, K, A, lda, B,
                        ldb, workspace);

@@ -363,16 +363,14 @@ gemm_smallm_wk_kernel(int32_t M, int32_t N, int32_t K, const float* __restrict__
       __builtin_amdgcn_make_buffer_rsrc(const_cast<float*>(A), (short)0, M * (int)lda * 4, 0x00020000);
   const __amdgpu_buffer_rsrc_t rb =
       __builtin_amdgcn_make_buffer_rsrc(const_cast<float*>(B), (short)0, K * (int)ldb * 4, 0x00020000);
-  float4 a[RT][KBW];
+  f32x4 a4[RT][KBW];
 #pragma unroll
   for (int t = 0; t < RT; ++t)
 #pragma unroll
     for (int c = 0; c < KBW; ++c) {
       const int row = 16 * t + r, k = 16 * ((int)kb0 + c) + 4 * q;
-      const f32x4 v = __builtin_bit_cast(
+      a4[t][c] = __builtin_bit_cast(
           f32x4, __builtin_amdgcn_raw_buffer_load_b128(ra, (row * (int)lda + (k < K ? k : 0)) * 4, 0, 0));
-      a[t][c] = k + 3 < K ? make_float4(v[0], v[1], v[2], v[3])
-                          : make_float4(k < K ? v[0] : 0.f, k + 1 < K ? v[1] : 0.f, k + 2 < K ? v[2] : 0.f, 0.f);
     }
   float b[KBW][4][NTG];
 #pragma unroll
@@ -384,6 +382,22 @@ gemm_smallm_wk_kernel(int32_t M, int32_t N, int32_t K, const float* __restrict__
         const int k = 16 * ((int)kb0 + c) + 4 * q + j, n = (int)n0 + 16 * u + r;
         b[c][j][u] = __uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(rb, (k * (int)ldb + n) * 4, 0, 0));
       }
+  // A's components past K zeroed by bit masks once every load is issued (as a
+  // select, each A load compiled into a branch with its own vmcnt(0): eight
+  // serial round trips; left to itself the scheduler also spread the loads
+  // over the MFMAs, each waited for right after it left)
+  __builtin_amdgcn_sched_barrier(0);
+  float4 a[RT][KBW];
+#pragma unroll
+  for (int t = 0; t < RT; ++t)
+#pragma unroll
+    for (int c = 0; c < KBW; ++c) {
+      const int k = 16 * ((int)kb0 + c) + 4 * q;
+      a[t][c] = make_float4(__int_as_float(__float_as_int(a4[t][c][0]) & (k < K ? -1 : 0)),
+                            __int_as_float(__float_as_int(a4[t][c][1]) & (k + 1 < K ? -1 : 0)),
+                            __int_as_float(__float_as_int(a4[t][c][2]) & (k + 2 < K ? -1 : 0)),
+                            __int_as_float(__float_as_int(a4[t][c][3]) & (k + 3 < K ? -1 : 0)));
+    }
   f32x4 acc[RT][NTG];
 #pragma unroll
   for (int t = 0; t < RT; ++t)

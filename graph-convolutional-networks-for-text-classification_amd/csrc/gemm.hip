@@ -74,7 +74,42 @@ gemm_f32_mfma_kernel(int32_t M, int32_t N, int32_t K, int32_t kchunk, const floa
   // flight while tile t is multiplied out of LDS
   constexpr int PA = (BM * BK + 255) / 256, PB = (BN * BK + 255) / 256;
   float ra[PA], rb[PB];
-  auto fetch = [&](int32_t k0) {
+  // A and B through buffer resources when both fit 32-bit offsets: an element
+  // outside the tile's rows or past this K chunk gets an offset past the
+  // resource and reads 0 -- no branch per load (guarded, each of the tile's
+  // loads compiled into a branch with its own vmcnt(0): the double buffer's
+  // next tile arrived one load at a time)
+  const int64_t a_bytes = (TA ? (int64_t)K : (int64_t)M) * lda * 4, b_bytes = (TB ? (int64_t)N : (int64_t)K) * ldb * 4;
+  const bool use_buf = a_bytes < 0x7ff00000 && b_bytes < 0x7ff00000;   // (uniform)
+  const __amdgpu_buffer_rsrc_t rsa =
+      __builtin_amdgcn_make_buffer_rsrc(const_cast<float*>(A), (short)0, use_buf ? (int)a_bytes : 0, 0x00020000);
+  const __amdgpu_buffer_rsrc_t rsb =
+      __builtin_amdgcn_make_buffer_rsrc(const_cast<float*>(B), (short)0, use_buf ? (int)b_bytes : 0, 0x00020000);
+  auto fetch_buf = [&](int32_t k0) {
+#pragma unroll
+    for (int p = 0; p < PA; ++p) {
+      const int e = tid + p * 256;
+      int m, k;
+      if (!TA) { m = e / BK; k = e % BK; }
+      else { k = e / BM; m = e % BM; }
+      const int gm = (int)m0 + m, gk = k0 + k;
+      const bool ok = e < BM * BK && gm < M && gk < ke;
+      ra[p] = __uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(
+          rsa, ok ? (TA ? (gk * (int)lda + gm) * 4 : (gm * (int)lda + gk) * 4) : 0x7ffffff0, 0, 0));
+    }
+#pragma unroll
+    for (int p = 0; p < PB; ++p) {
+      const int e = tid + p * 256;
+      int n, k;
+      if (!TB) { k = e / BN; n = e % BN; }
+      else { n = e / BK; k = e % BK; }
+      const int gn = (int)n0 + n, gk = k0 + k;
+      const bool ok = e < BN * BK && gn < N && gk < ke;
+      rb[p] = __uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(
+          rsb, ok ? (TB ? (gn * (int)ldb + gk) * 4 : (gk * (int)ldb + gn) * 4) : 0x7ffffff0, 0, 0));
+    }
+  };
+  auto fetch_ptr = [&](int32_t k0) {
 #pragma unroll
     for (int p = 0; p < PA; ++p) {
       const int e = tid + p * 256;
@@ -95,6 +130,10 @@ gemm_f32_mfma_kernel(int32_t M, int32_t N, int32_t K, int32_t kchunk, const floa
       const int32_t gk = k0 + k;
       rb[p] = (e < BN * BK && gn < N && gk < ke) ? (TB ? B[gn * ldb + gk] : B[(int64_t)gk * ldb + gn]) : 0.f;
     }
+  };
+  auto fetch = [&](int32_t k0) {
+    if (use_buf) fetch_buf(k0);
+    else fetch_ptr(k0);
   };
   if (kb < ke) fetch(kb);
   for (int32_t k0 = kb; k0 < ke; k0 += BK) {
